@@ -1,0 +1,380 @@
+"""Program acquisition: run the user's callable on proxies and record a trace (parity: reference
+``thunder/core/jit_ext.py`` — ``thunder_general_jit`` :2149-2272, ``unpack_inputs`` :1649-1972,
+``process_recorded_modifications`` :1973).
+
+The reference acquires programs with a CPython bytecode interpreter
+(``interpreter.py``).  This frontend acquires them by *execution*: module
+parameters, buffers and tensor attributes are swapped for proxies, tensor
+arguments become proxies, and every torch call is routed through a
+``TorchFunctionMode`` to the ``ltorch`` language (or auto-registered as an opaque
+op).  Python control flow runs natively and is specialised, exactly like the
+reference's "constant values" cache mode.  Provenance of every input is
+recorded, so the prologue re-fetches inputs and checks guards on each call,
+and attribute writes made during tracing are replayed by the epilogue.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from numbers import Number
+from typing import Any, Callable
+
+import torch
+from torch.overrides import TorchFunctionMode
+
+from . import prims
+from .codeutils import sanitize_name
+from .proxies import Proxy, TensorProxy, NumberProxy, AnyProxy, tensorproxy, ProxyTag
+from .pytree import tree_flatten, tree_unflatten, tree_map
+from .trace import TraceCtx, tracectx, get_tracectx, TraceProvenance
+from .symbol import BoundSymbol
+
+
+# -----------------------------------------------------------------------------------------
+# Torch function dispatch while tracing
+# -----------------------------------------------------------------------------------------
+class _AcquisitionState:
+    """Per-trace bookkeeping of external (captured) tensors."""
+
+    def __init__(self):
+        self.constants: dict[int, tuple[torch.Tensor, TensorProxy]] = {}
+        self.lookasides: dict[Callable, Callable] = {}
+
+    def proxify_constant(self, t: torch.Tensor) -> TensorProxy:
+        hit = self.constants.get(id(t))
+        if hit is not None and hit[0] is t:
+            return hit[1]
+        p = tensorproxy(t, prefix="tc")
+        p.requires_grad = False if not t.requires_grad else True
+        p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+        self.constants[id(t)] = (t, p)
+        return p
+
+
+_state_stack: list[_AcquisitionState] = []
+
+
+def _current_state() -> _AcquisitionState | None:
+    return _state_stack[-1] if _state_stack else None
+
+
+_RANDOM_OR_FACTORY = None
+
+
+def _random_or_factory_fns():
+    global _RANDOM_OR_FACTORY
+    if _RANDOM_OR_FACTORY is None:
+        names = [
+            "rand", "randn", "randint", "rand_like", "randn_like", "randint_like", "randperm", "normal", "bernoulli",
+            "multinomial", "empty", "empty_like", "zeros", "zeros_like", "ones", "ones_like", "full", "full_like",
+            "arange", "linspace", "tensor",
+        ]
+        s = set()
+        for n in names:
+            f = getattr(torch, n, None)
+            if f is not None:
+                s.add(f)
+        f = getattr(torch.nn.functional, "dropout", None)
+        if f is not None:
+            s.add(f)
+        _RANDOM_OR_FACTORY = s
+    return _RANDOM_OR_FACTORY
+
+
+_PASSTHROUGH_NAMES = {"__get__", "__set__", "__repr__", "__format__", "__str__", "__hash__", "__len__", "__bool__"}
+
+
+def dispatch_torch_function(func, args, kwargs):
+    """Routes a torch callable with (possibly) proxy arguments to the ltorch language."""
+    from .. import torch as ltorch
+    from ..torch.default_torch_ops import opaque_symbol
+
+    trc = get_tracectx()
+    flat, spec = tree_flatten((args, kwargs))
+    has_proxy = any(isinstance(x, Proxy) for x in flat)
+    state = _current_state()
+
+    if state is not None:
+        la = state.lookasides.get(func)
+        if la is not None:
+            return la(*args, **kwargs)
+
+    sym = ltorch._torch_to_thunder_function_map.get(func)
+    if trc is None or (not has_proxy and (sym is None or func not in _random_or_factory_fns())):
+        # Eager computation on real tensors (constant folding of trace-independent values)
+        with _disabled_mode():
+            return func(*args, **kwargs)
+
+    name = getattr(func, "__name__", "")
+    if name in _PASSTHROUGH_NAMES and not has_proxy:
+        return func(*args, **kwargs)
+
+    # Proxify captured real tensors that meet traced values
+    if state is not None:
+        changed = False
+        nflat = []
+        for x in flat:
+            if isinstance(x, torch.Tensor) and not isinstance(x, Proxy):
+                nflat.append(state.proxify_constant(x))
+                changed = True
+            else:
+                nflat.append(x)
+        if changed:
+            args, kwargs = tree_unflatten(nflat, spec)
+
+    if sym is not None:
+        from .symbol import CALLED_TORCH_FN
+
+        prev = CALLED_TORCH_FN[0]
+        CALLED_TORCH_FN[0] = func
+        try:
+            return sym(*args, **kwargs)
+        finally:
+            CALLED_TORCH_FN[0] = prev
+    return opaque_symbol(func)(*args, **kwargs)
+
+
+class ThunderTorchFunctionMode(TorchFunctionMode):
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        from .symbol import META_DEPTH
+
+        if META_DEPTH[0] > 0:
+            return func(*args, **(kwargs or {}))
+        return dispatch_torch_function(func, args, kwargs or {})
+
+
+@contextlib.contextmanager
+def user_code_tracing():
+    """Re-enables tracing of user code called from inside a symbol meta (e.g. activation checkpointing)."""
+    from .symbol import META_DEPTH
+
+    prev = META_DEPTH[0]
+    META_DEPTH[0] = 0
+    try:
+        yield
+    finally:
+        META_DEPTH[0] = prev
+
+
+@contextlib.contextmanager
+def _disabled_mode():
+    with torch._C.DisableTorchFunction():
+        yield
+
+
+# -----------------------------------------------------------------------------------------
+# Input provenance
+# -----------------------------------------------------------------------------------------
+class InputSpec:
+    """Where a computation input comes from at call time."""
+
+    __slots__ = ("kind", "path", "proxy", "value", "module_path", "attr")
+
+    def __init__(self, kind, path=None, proxy=None, value=None, module_path=None, attr=None):
+        self.kind = kind  # "arg" | "param" | "buffer" | "attr" | "const"
+        self.path = path
+        self.proxy = proxy
+        self.value = value
+        self.module_path = module_path
+        self.attr = attr
+
+
+def _named_tensor_attrs(module: torch.nn.Module):
+    """(module_path, submodule, attr_name, tensor) for plain tensor attributes (not params/buffers)."""
+    for mpath, m in module.named_modules(remove_duplicate=True):
+        for k, v in list(vars(m).items()):
+            if isinstance(v, torch.Tensor) and not isinstance(v, torch.nn.Parameter) and not k.startswith("__"):
+                yield mpath, m, k, v
+
+
+class AcquiredProgram:
+    def __init__(self):
+        self.prologue_trace: TraceCtx | None = None
+        self.computation_trace: TraceCtx | None = None
+        self.epilogue_trace: TraceCtx | None = None
+        self.input_specs: list[InputSpec] = []
+        self.arg_spec = None
+        self.param_accessors: list[tuple[torch.nn.Module, str, str]] = []  # (module, name, kind)
+        self.constants: list[torch.Tensor] = []
+        self.output_spec = None
+        self.epilogue_writes: list[tuple[torch.nn.Module, str]] = []
+
+
+def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
+            lookasides: dict | None = None, prune_param_checks: bool = True) -> AcquiredProgram:
+    """Traces ``fn(*args, **kwargs)`` and builds prologue / computation / epilogue traces."""
+    prog = AcquiredProgram()
+    comp = TraceCtx(fn if not isinstance(fn, torch.nn.Module) else type(fn).forward)
+    comp.fn_name = "computation"
+    from ..transforms.autocast import current_autocast_dtype
+
+    comp.autocast_dtype = current_autocast_dtype()
+    state = _AcquisitionState()
+    if lookasides:
+        state.lookasides.update(lookasides)
+
+    flat_args, arg_spec = tree_flatten((args, kwargs))
+    prog.arg_spec = arg_spec
+    swapped: list[tuple[dict, str, Any]] = []
+    attr_swaps: list[tuple[torch.nn.Module, str, Any]] = []
+
+    with tracectx(comp):
+        # 1. tensor arguments
+        proxied_flat = []
+        arg_proxies = []
+        for i, x in enumerate(flat_args):
+            if isinstance(x, torch.Tensor):
+                p = tensorproxy(x)
+                arg_proxies.append((i, p))
+                proxied_flat.append(p)
+                prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
+            else:
+                proxied_flat.append(x)
+        pargs, pkwargs = tree_unflatten(proxied_flat, arg_spec)
+
+        # 2. module state
+        if module is not None:
+            seen: dict[int, TensorProxy] = {}
+            for mpath, m in module.named_modules(remove_duplicate=False):
+                for pname, param in list(m._parameters.items()):
+                    if param is None:
+                        continue
+                    full = f"{mpath}.{pname}" if mpath else pname
+                    if id(param) in seen:
+                        p = seen[id(param)]
+                    else:
+                        p = tensorproxy(param, name=comp.make_unique_name("t_" + full))
+                        p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                        seen[id(param)] = p
+                        prog.input_specs.append(InputSpec("param", path=full, proxy=p, module_path=mpath, attr=pname))
+                        prog.param_accessors.append((m, pname, "param"))
+                    swapped.append((m._parameters, pname, param))
+                    m._parameters[pname] = p
+                for bname, buf in list(m._buffers.items()):
+                    if buf is None:
+                        continue
+                    full = f"{mpath}.{bname}" if mpath else bname
+                    if id(buf) in seen:
+                        p = seen[id(buf)]
+                    else:
+                        p = tensorproxy(buf, name=comp.make_unique_name("t_" + full))
+                        p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                        seen[id(buf)] = p
+                        prog.input_specs.append(InputSpec("buffer", path=full, proxy=p, module_path=mpath, attr=bname))
+                        prog.param_accessors.append((m, bname, "buffer"))
+                    swapped.append((m._buffers, bname, buf))
+                    m._buffers[bname] = p
+            for mpath, m, k, v in list(_named_tensor_attrs(module)):
+                full = f"{mpath}.{k}" if mpath else k
+                if id(v) in seen:
+                    p = seen[id(v)]
+                else:
+                    p = tensorproxy(v, name=comp.make_unique_name("t_" + full))
+                    p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                    seen[id(v)] = p
+                    prog.input_specs.append(InputSpec("attr", path=full, proxy=p, module_path=mpath, attr=k))
+                    prog.param_accessors.append((m, k, "attr"))
+                attr_swaps.append((m, k, v))
+                object.__setattr__(m, k, p)
+
+        # snapshot of module attribute identity to detect writes made during tracing
+        before = {}
+        if module is not None:
+            for mpath, m in module.named_modules(remove_duplicate=True):
+                before[id(m)] = dict(vars(m))
+
+        _state_stack.append(state)
+        try:
+            with ThunderTorchFunctionMode():
+                if module is not None:
+                    result = module(*pargs, **pkwargs)
+                else:
+                    result = fn(*pargs, **pkwargs)
+        finally:
+            _state_stack.pop()
+            # detect attribute writes (epilogue) before restoring
+            writes = []
+            if module is not None:
+                for mpath, m in module.named_modules(remove_duplicate=True):
+                    old = before.get(id(m), {})
+                    for k, v in vars(m).items():
+                        if isinstance(v, TensorProxy) and old.get(k) is not v:
+                            writes.append((m, k, v))
+            for d, k, v in swapped:
+                d[k] = v
+            for m, k, v in attr_swaps:
+                # if the attribute was overwritten during tracing keep the write for the epilogue
+                object.__setattr__(m, k, v)
+
+        # 3. captured constants become inputs
+        for t, p in state.constants.values():
+            prog.constants.append(t)
+            prog.input_specs.append(InputSpec("const", proxy=p, value=t))
+
+        # 4. epilogue writes are returned from the computation
+        prog.epilogue_writes = [(m, k) for m, k, v in writes]
+        epi_values = [v for m, k, v in writes]
+
+        # outputs: real tensors in the result are constants
+        def fix_out(x):
+            if isinstance(x, torch.Tensor) and not isinstance(x, Proxy):
+                return state.proxify_constant(x)
+            return x
+
+        result = tree_map(fix_out, result)
+        for t, p in state.constants.values():
+            if all(t is not c for c in prog.constants):
+                prog.constants.append(t)
+                prog.input_specs.append(InputSpec("const", proxy=p, value=t))
+        if epi_values:
+            prims.python_return((result, tuple(epi_values)))
+        else:
+            prims.python_return(result)
+
+    comp.args = [s.proxy for s in prog.input_specs]
+    comp.set_provenance(TraceProvenance("Acquisition (trace-by-execution frontend)"))
+    prog.computation_trace = comp
+    prog.output_spec = None
+    prog.prologue_trace = build_prologue(prog, flat_args, prune_param_checks=prune_param_checks)
+    if prog.epilogue_writes:
+        prog.epilogue_trace = None  # epilogue is applied by the runtime (see common.run_epilogue)
+    return prog
+
+
+def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks: bool) -> TraceCtx:
+    """Prologue: flattened args -> checks -> computation inputs (reference ``unpack_inputs`` :1649)."""
+    pro = TraceCtx(None)
+    pro.fn_name = "prologue"
+    with tracectx(pro):
+        fa = AnyProxy(None, name="flat_args")
+        st = AnyProxy(None, name="module_state")
+        cs = AnyProxy(None, name="constants")
+        pro.args = [fa, st, cs]
+        n = len(flat_args)
+        unpacked = prims.unpack_sequence(fa, n)
+        for i, (u, x) in enumerate(zip(unpacked, flat_args)):
+            if isinstance(x, torch.Tensor):
+                prims.check_tensor_shape_and_metadata(u, tuple(x.shape), str(x.device), x.dtype, x.requires_grad)
+            elif x is None:
+                prims.check_none(u)
+            elif isinstance(x, str):
+                prims.check_string_value(u, x)
+            elif isinstance(x, (bool, int, float, complex)):
+                prims.check_number_type_and_value(u, x)
+            elif isinstance(x, (torch.dtype, torch.device)):
+                prims.check_literal_like(u, x)
+        arg_outs = [unpacked[s.path] for s in prog.input_specs if s.kind == "arg"]
+        n_state = len(prog.param_accessors)
+        state_vals = prims.unpack_sequence(st, n_state) if n_state else []
+        if not prune_param_checks:
+            j = 0
+            for s in prog.input_specs:
+                if s.kind in ("param", "buffer", "attr"):
+                    p = s.proxy
+                    prims.check_tensor_shape_and_metadata(state_vals[j], tuple(p.shape), str(p.device), p.dtype, p.requires_grad)
+                    j += 1
+        n_const = len(prog.constants)
+        const_vals = prims.unpack_sequence(cs, n_const) if n_const else []
+        prims.python_return(list(arg_outs) + list(state_vals) + list(const_vals))
+    pro.set_provenance(TraceProvenance("Prologue construction"))
+    return pro

@@ -1,0 +1,76 @@
+"""Bridge from compiled forward/backward traces to ``torch.autograd`` (parity: reference
+``thunder/executors/torch_autograd.py:17-185``).
+
+``ThunderFunction`` runs the compiled augmented forward; its backward calls the
+compiled backward with a *list* of saved tensors + cotangents that the generated
+program clears immediately, so activations are freed as the backward proceeds.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd.function import once_differentiable
+
+
+class ThunderFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, entry, n_inputs, *flat_inputs):
+        out, saved_tensors, saved_other = entry.forward_fn(*flat_inputs)
+        from ..core.pytree import tree_flatten
+
+        flat_out, out_spec = tree_flatten(out)
+        ctx.entry = entry
+        ctx.saved = list(saved_tensors) + list(saved_other)
+        ctx.n_inputs = n_inputs
+        tensor_outs = []
+        nondiff = []
+        for o, diff in zip(flat_out, entry.diff_output_mask):
+            if isinstance(o, torch.Tensor):
+                tensor_outs.append(o)
+                if not diff:
+                    nondiff.append(o)
+        ctx.out_is_tensor = [isinstance(o, torch.Tensor) for o in flat_out]
+        entry._last_out_spec = out_spec
+        entry._last_flat_out = flat_out
+        if nondiff:
+            ctx.mark_non_differentiable(*nondiff)
+        ctx.set_materialize_grads(False)
+        return tuple(tensor_outs)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *grads):
+        entry = ctx.entry
+        args = ctx.saved
+        ctx.saved = None
+        # align tensor-output grads with the differentiable outputs
+        gi = iter(grads)
+        cts = []
+        k = 0
+        for is_t, diff in zip(ctx.out_is_tensor, entry.diff_output_mask):
+            g = next(gi) if is_t else None
+            if diff:
+                cts.append(g)
+        outs_meta = entry.diff_output_meta
+        for i, g in enumerate(cts):
+            if g is None:
+                shape, dtype, device = outs_meta[i]
+                cts[i] = torch.zeros(shape, dtype=dtype, device=device)
+        args.extend(cts)
+        in_grads = entry.backward_fn(args)
+        result = [None] * ctx.n_inputs
+        for idx, g in zip(entry.grad_input_indices, in_grads):
+            result[idx] = g
+        return (None, None, *result)
+
+
+def connect_to_autograd(entry, flat_inputs):
+    outs = ThunderFunction.apply(entry, len(flat_inputs), *flat_inputs)
+    from ..core.pytree import tree_unflatten
+
+    flat_out = list(entry._last_flat_out)
+    it = iter(outs)
+    for i, o in enumerate(flat_out):
+        if isinstance(o, torch.Tensor):
+            flat_out[i] = next(it)
+    entry._last_flat_out = None
+    return tree_unflatten(flat_out, entry._last_out_spec)
