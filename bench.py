@@ -1,0 +1,240 @@
+#!/usr/bin/env python
+"""Headline benchmark: LitGPT Llama-2-7B pretraining step (seq 4096, micro-batch 1, bf16, AdamW) on MI355X.
+
+Mirrors the reference's ``thunder/benchmarks/benchmark_litgpt.py`` headline run
+(``docs/source/intermediate/benchmarking.rst:36-54``: 10,690 tokens/s/GPU on 1×H100).
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+Synthetic token ids and random-init weights of the exact Llama-2-7B architecture
+(no network for datasets/checkpoints).  One JSON line is printed by rank 0;
+``value`` is the whole-job aggregate tokens/s (sum over ranks), timing is the max
+over ranks of K steps bracketed by barrier + device synchronize.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch
+
+BASELINE_TOKENS_PER_SEC_PER_GPU_1 = 10690.01  # 1x H100, Thunder default executors (benchmarking.rst:36-54)
+BASELINE_TOKENS_PER_SEC_PER_GPU_FSDP = 11750.0  # 8x H100 ZeRO-2 Thunder (chart, normalized_training_throughput_zero2.png)
+METRIC = "tokens/sec/GPU Llama-2-7B pretrain (LitGPT) + speedup vs eager at 1/2/4/8 MI355X"
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="Llama-2-7b-hf")
+    p.add_argument("--seq", type=int, default=4096)
+    p.add_argument("--mbs", type=int, default=1)
+    p.add_argument("--mode", default="thunder", choices=["thunder", "eager"])
+    p.add_argument("--parallel", default="auto", choices=["auto", "fsdp", "ddp", "none"])
+    p.add_argument("--executors", default=None, help="comma separated executor names (default: framework defaults)")
+    p.add_argument("--fp8", action="store_true")
+    p.add_argument("--hipgraph", action="store_true")
+    p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
+    p.add_argument("--eager-baseline", action="store_true", help="also time PyTorch eager (1 GPU) for speedup")
+    p.add_argument("--profile-dir", default=None)
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(args, device):
+    from lightning_thunder_amd.models.litgpt import GPT, Config, init_weights
+
+    kw = {}
+    if args.n_layer is not None:
+        kw["n_layer"] = args.n_layer
+    cfg = Config.from_name(args.model, **kw)
+    with torch.device("meta"):
+        model = GPT(cfg)
+    model = model.to_empty(device=device).to(torch.bfloat16)
+    torch.manual_seed(1234)
+    init_weights(model)
+    model.set_rope_cache(args.seq, device=device)
+    return model, cfg
+
+
+def make_optimizer(params):
+    try:
+        return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
+    except (RuntimeError, TypeError):
+        return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, foreach=True)
+
+
+def run(args, rank, world, device, mode):
+    import lightning_thunder_amd as thunder
+
+    model, cfg = build_model(args, device)
+    parallel = args.parallel
+    if parallel == "auto":
+        parallel = "fsdp" if world > 1 else "none"
+    V = cfg.padded_vocab_size
+    if mode == "thunder":
+        kwargs = {}
+        if args.executors:
+            kwargs["executors"] = args.executors.split(",")
+        transforms = []
+        if args.fp8:
+            from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+            transforms.append(FP8LinearTransform())
+
+        class TrainStep(torch.nn.Module):
+            """Model + loss in one compiled program so the fused cross-entropy kernel is used."""
+
+            def __init__(self, m):
+                super().__init__()
+                self.m = m
+
+            def forward(self, x, y):
+                logits = self.m(x)
+                return torch.nn.functional.cross_entropy(logits.reshape(-1, V), y.reshape(-1))
+
+        jm = thunder.jit(TrainStep(model), transforms=transforms, **kwargs)
+        if world > 1 and parallel == "fsdp":
+            from lightning_thunder_amd.distributed import fsdp
+
+            jm = fsdp(jm)
+        elif world > 1 and parallel == "ddp":
+            from lightning_thunder_amd.distributed import ddp
+
+            jm = ddp(jm)
+        if args.hipgraph:
+            from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
+            from lightning_thunder_amd.core.transforms import add_transform
+
+            jm = add_transform(jm, transform=HipGraphTransform())
+        fwd = jm
+        params = list(jm.parameters())
+    else:
+        fwd = model
+        if world > 1:
+            from torch.nn.parallel import DistributedDataParallel
+
+            fwd = DistributedDataParallel(model, device_ids=[device.index])
+        params = list(model.parameters())
+    opt = make_optimizer(params)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1000 + rank)
+
+    def batch():
+        x = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq + 1), device=device, generator=gen)
+        return x[:, :-1].contiguous(), x[:, 1:].contiguous()
+
+    def step(x, y):
+        if mode == "thunder":
+            loss = fwd(x, y)
+        else:
+            logits = fwd(x)
+            loss = torch.nn.functional.cross_entropy(logits.reshape(-1, V), y.reshape(-1))
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    data = [batch() for _ in range(4)]
+    t_first = time.perf_counter()
+    for i in range(args.warmup):
+        loss = step(*data[i % 4])
+        if i == 0:
+            torch.cuda.synchronize()
+            log(rank, f"[{mode}] first step (incl. compile) {time.perf_counter() - t_first:.1f}s loss={loss.item():.4f}")
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(*data[i % 4])
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    mem = torch.cuda.max_memory_allocated(device) / 1e9
+    log(rank, f"[{mode}] {args.steps} steps in {dt:.3f}s, loss={loss.item():.4f}, peak mem {mem:.1f} GB")
+    del model, opt, fwd, params
+    return dt, cfg, mem, parallel
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+        torch.distributed.init_process_group("nccl", device_id=device)
+
+    dt, cfg, mem, parallel = run(args, rank, world, device, args.mode)
+    tokens = args.steps * args.mbs * args.seq * world
+    value = tokens / dt
+    per_gpu = value / world
+    from lightning_thunder_amd.models.litgpt import flops_per_token
+
+    tflops = flops_per_token(cfg, args.seq) * per_gpu / 1e12
+    speedup = None
+    if args.eager_baseline and world == 1 and args.mode == "thunder":
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        dte, _, _, _ = run(args, rank, world, device, "eager")
+        speedup = dte / dt
+    base = BASELINE_TOKENS_PER_SEC_PER_GPU_1 if world == 1 else BASELINE_TOKENS_PER_SEC_PER_GPU_FSDP
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(per_gpu / base, 4),
+            "dtype": "fp8" if args.fp8 else "bf16",
+            "data": "synthetic token ids, random-init weights",
+            "config": {
+                "model": args.model + ("" if args.n_layer is None else f"-{args.n_layer}L(debug)"),
+                "global_batch": args.mbs * world,
+                "micro_batch": args.mbs,
+                "seq_len": args.seq,
+                "parallelism": f"{parallel}{world}" if world > 1 else "single",
+                "mode": args.mode,
+                "optimizer": "AdamW",
+            },
+            "tokens_per_sec_per_gpu": round(per_gpu, 2),
+            "model_tflops_per_gpu": round(tflops, 1),
+            "peak_mem_gb": round(mem, 2),
+            "speedup_vs_eager": None if speedup is None else round(speedup, 3),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -369,6 +369,100 @@ def _register_ltorch():
 _register_ltorch()
 
 
+# =========================================================================================
+# Fused attention through ATen (fallback when the HIP flash-attention kernel does not apply)
+# (parity: reference thunder/executors/sdpaex.py:34-568)
+# =========================================================================================
+def _sdpa_fwd_meta(q, k, v, is_causal, scale):
+    B, H, L, E = q.shape
+    out = TensorProxy(like=q, shape=(B, H, L, v.shape[-1]))
+    lse = TensorProxy(like=q, shape=(B, H, L), dtype=torch.float32, requires_grad=False)
+    return out, lse
+
+
+def _sdpa_fwd_impl(q, k, v, is_causal, scale):
+    r = torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, is_causal, False, scale=scale)
+    return r[0], r[1]
+
+
+def _sdpa_bwd_meta(g, q, k, v, out, lse, is_causal, scale):
+    return TensorProxy(like=q), TensorProxy(like=k), TensorProxy(like=v)
+
+
+def _sdpa_bwd_impl(g, q, k, v, out, lse, is_causal, scale):
+    L, S = q.shape[-2], k.shape[-2]
+    zero = torch.empty((), dtype=torch.int64, device="cpu")
+    r = torch.ops.aten._scaled_dot_product_flash_attention_backward(
+        g.contiguous(), q, k, v, out, lse, None, None, L, S, 0.0, is_causal, zero, zero, scale=scale
+    )
+    return r[0], r[1], r[2]
+
+
+aten_sdpa_fwd = ex.register_operator("aten_flash_sdpa_fwd", meta=_sdpa_fwd_meta, fn=_sdpa_fwd_impl)
+aten_sdpa_bwd = ex.register_operator("aten_flash_sdpa_bwd", meta=_sdpa_bwd_meta, fn=_sdpa_bwd_impl)
+
+
+def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    if attn_mask is not None or dropout_p != 0.0:
+        return False
+    if query.device.type != "cuda" or query.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    if query.ndim != 4 or key.dtype != query.dtype or value.dtype != query.dtype:
+        return False
+    return query.shape[-1] <= 256 and query.shape[-1] % 8 == 0
+
+
+def _expand_kv(query, key, value):
+    from .. import torch as ltorch
+
+    rep = query.shape[-3] // key.shape[-3]
+    if rep > 1:
+        key = ltorch.repeat_interleave(key, rep, -3)
+        value = ltorch.repeat_interleave(value, rep, -3)
+    return key, value
+
+
+def _sdpa_grad(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    from .. import torch as ltorch
+
+    if not _sdpa_checker(query, key, value, attn_mask, dropout_p, is_causal, scale=scale, enable_gqa=enable_gqa):
+        return None
+    sc = scale if scale is not None else 1.0 / math.sqrt(query.shape[-1])
+    k, v = _expand_kv(query, key, value)
+    out, lse = aten_sdpa_fwd(query, k, v, is_causal, sc)
+
+    def bwd(g):
+        dq, dk, dv = aten_sdpa_bwd(g, query, k, v, out, lse, is_causal, sc)
+        rep = query.shape[-3] // key.shape[-3]
+        if rep > 1:
+            shp = tuple(key.shape)
+            dk = ltorch.sum(ltorch.reshape(dk, shp[:-3] + (shp[-3], rep) + shp[-2:]), -3)
+            dv = ltorch.sum(ltorch.reshape(dv, shp[:-3] + (shp[-3], rep) + shp[-2:]), -3)
+        return dq, dk, dv
+
+    return out, bwd
+
+
+def _sdpa_exec(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    sc = scale if scale is not None else 1.0 / math.sqrt(query.shape[-1])
+    k, v = _expand_kv(query, key, value)
+    out, _ = aten_sdpa_fwd(query, k, v, is_causal, sc)
+    return out
+
+
+def _register_sdpa():
+    from .. import torch as ltorch
+
+    # keep the plain replay for forward-only use; add the fused grad transform
+    impl = ex.implmap.get(ltorch.scaled_dot_product_attention.id)
+    ex.register_implementation(ltorch.scaled_dot_product_attention, impl.symbol if impl else None,
+                               grad_transform=_sdpa_grad, checker=None)
+    ex._sdpa_grad_checker = _sdpa_checker
+
+
+_register_sdpa()
+
+
 def register_opaque(sym: Symbol, fn: Callable) -> None:
     op = ex.register_operator(f"torch_{sym.name}", like=sym, fn=fn)
     ex.register_implementation(sym, op)

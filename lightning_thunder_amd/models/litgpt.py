@@ -1,0 +1,285 @@
+"""LitGPT-architecture decoder models in plain PyTorch (parity: the LitGPT configs/model used by the
+reference's ``thunder/benchmarks/benchmark_litgpt.py:295,335`` and ``thunder/tests/litgpt_model.py:1-131``).
+
+LitGPT itself is not installed in this image, so the architecture is defined
+here with LitGPT's module names (``transformer.wte``, ``transformer.h[i].attn.attn``,
+``mlp.fc_1/fc_2/proj``, ``lm_head`` …) so checkpoints and traces line up.
+
+Hot spots live in small module-level helpers (``apply_rope``, ``qkv_split_rope``)
+written in plain torch; the HIP executor registers lookasides for them so a
+compiled model runs the fused CDNA4 kernels while eager PyTorch runs the same
+math unfused (that is the "speedup vs eager" baseline).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class Config:
+    name: str = ""
+    block_size: int = 4096
+    vocab_size: int = 32000
+    padded_vocab_size: Optional[int] = None
+    padding_multiple: int = 512
+    n_layer: int = 32
+    n_head: int = 32
+    n_embd: int = 4096
+    head_size: Optional[int] = None
+    n_query_groups: Optional[int] = None
+    rotary_percentage: float = 1.0
+    parallel_residual: bool = False
+    bias: bool = False
+    norm_class_name: str = "RMSNorm"
+    norm_eps: float = 1e-5
+    mlp_class_name: str = "LLaMAMLP"
+    intermediate_size: Optional[int] = None
+    rope_base: int = 10000
+    rope_condense_ratio: int = 1
+    shared_attention_norm: bool = False
+    gelu_approximate: str = "none"
+    tie_embeddings: bool = False
+
+    def __post_init__(self):
+        if self.head_size is None:
+            self.head_size = self.n_embd // self.n_head
+        if self.padded_vocab_size is None:
+            self.padded_vocab_size = ((self.vocab_size + self.padding_multiple - 1) // self.padding_multiple) * self.padding_multiple
+        if self.n_query_groups is None:
+            self.n_query_groups = self.n_head
+        if self.intermediate_size is None:
+            self.intermediate_size = 4 * self.n_embd
+        self.rope_n_elem = int(self.rotary_percentage * self.head_size)
+
+    @classmethod
+    def from_name(cls, name: str, **kwargs) -> "Config":
+        base = name_to_config[name]
+        return replace(base, **kwargs)
+
+    @property
+    def qkv_size(self) -> int:
+        return (self.n_head + 2 * self.n_query_groups) * self.head_size
+
+
+configs = [
+    # Meta Llama 2
+    Config(name="Llama-2-7b-hf", vocab_size=32000, padding_multiple=64, n_layer=32, n_head=32, n_embd=4096,
+           intermediate_size=11008, norm_eps=1e-5),
+    Config(name="Llama-2-13b-hf", vocab_size=32000, padding_multiple=64, n_layer=40, n_head=40, n_embd=5120,
+           intermediate_size=13824, norm_eps=1e-5),
+    Config(name="Llama-2-70b-hf", vocab_size=32000, padding_multiple=64, n_layer=80, n_head=64, n_embd=8192,
+           n_query_groups=8, intermediate_size=28672, norm_eps=1e-5),
+    # Meta Llama 3
+    Config(name="Llama-3-8B", block_size=8192, vocab_size=128000, padded_vocab_size=128256, n_layer=32, n_head=32,
+           n_embd=4096, n_query_groups=8, intermediate_size=14336, rope_base=500000),
+    Config(name="Llama-3-70B", block_size=8192, vocab_size=128000, padded_vocab_size=128256, n_layer=80, n_head=64,
+           n_embd=8192, n_query_groups=8, intermediate_size=28672, rope_base=500000),
+    Config(name="Llama-3.2-1B", block_size=8192, vocab_size=128000, padded_vocab_size=128256, n_layer=16, n_head=32,
+           n_embd=2048, n_query_groups=8, intermediate_size=8192, rope_base=500000, tie_embeddings=True),
+    # Mistral
+    Config(name="Mistral-7B-v0.1", block_size=4096, vocab_size=32000, padded_vocab_size=32000, n_layer=32, n_head=32,
+           n_embd=4096, n_query_groups=8, intermediate_size=14336),
+    # CodeLlama
+    Config(name="CodeLlama-34b-hf", block_size=16384, vocab_size=32000, padded_vocab_size=32000, n_layer=48, n_head=64,
+           n_embd=8192, n_query_groups=8, intermediate_size=22016, rope_base=1000000),
+    # Small test configs (reference thunder/tests/litgpt_model.py)
+    Config(name="llama2-like", vocab_size=320, padding_multiple=64, n_layer=2, n_head=4, n_embd=64, intermediate_size=86,
+           block_size=128),
+    Config(name="llama3-like", vocab_size=320, padded_vocab_size=320, n_layer=2, n_head=4, n_embd=64, n_query_groups=2,
+           intermediate_size=96, block_size=128, rope_base=500000),
+    Config(name="gpt-neox-like", vocab_size=320, padding_multiple=64, n_layer=2, n_head=4, n_embd=64, block_size=128,
+           norm_class_name="LayerNorm", mlp_class_name="GptNeoxMLP", bias=True, parallel_residual=True,
+           rotary_percentage=0.25),
+    Config(name="llama2-7b-shape-2l", vocab_size=32000, padding_multiple=64, n_layer=2, n_head=32, n_embd=4096,
+           intermediate_size=11008),
+]
+name_to_config = {c.name: c for c in configs}
+
+
+def build_rope_cache(seq_len: int, n_elem: int, device=None, base: int = 10000, condense_ratio: int = 1):
+    theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, device=device).float() / n_elem))
+    seq_idx = torch.arange(seq_len, device=device) / condense_ratio
+    idx_theta = torch.outer(seq_idx, theta).repeat(1, 2)
+    return torch.cos(idx_theta), torch.sin(idx_theta)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x: [B, H, T, hs]; cos/sin: [T, hs]  (LitGPT's rotate-half formulation)."""
+    head_size = x.size(-1)
+    x1 = x[..., : head_size // 2]
+    x2 = x[..., head_size // 2:]
+    rotated = torch.cat((-x2, x1), dim=-1)
+    roped = (x * cos) + (rotated * sin)
+    return roped.to(dtype=x.dtype)
+
+
+def qkv_split_rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_head: int, n_query_groups: int,
+                   head_size: int, rope_n_elem: int):
+    """Splits fused qkv [B, T, (nh+2*ng)*hs] into q [B, nh, T, hs], k/v [B, ng, T, hs] and applies RoPE to q, k."""
+    B, T, _ = qkv.shape
+    q_size = n_head * head_size
+    kv_size = n_query_groups * head_size
+    q, k, v = qkv.split((q_size, kv_size, kv_size), dim=-1)
+    q = q.view(B, T, n_head, head_size).transpose(1, 2)
+    k = k.view(B, T, n_query_groups, head_size).transpose(1, 2)
+    v = v.view(B, T, n_query_groups, head_size).transpose(1, 2)
+    if rope_n_elem == head_size:
+        q = apply_rope(q, cos, sin)
+        k = apply_rope(k, cos, sin)
+    else:
+        q = torch.cat((apply_rope(q[..., :rope_n_elem], cos, sin), q[..., rope_n_elem:]), dim=-1)
+        k = torch.cat((apply_rope(k[..., :rope_n_elem], cos, sin), k[..., rope_n_elem:]), dim=-1)
+    return q, k, v
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, size: int, dim: int = -1, eps: float = 1e-6):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(size))
+        self.eps = eps
+        self.dim = dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return F.rms_norm(x, (x.shape[-1],), self.weight, self.eps)
+
+    def reset_parameters(self) -> None:
+        nn.init.ones_(self.weight)
+
+
+def _norm(config: Config, size: int) -> nn.Module:
+    if config.norm_class_name == "RMSNorm":
+        return RMSNorm(size, eps=config.norm_eps)
+    return nn.LayerNorm(size, eps=config.norm_eps)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, config: Config):
+        super().__init__()
+        self.attn = nn.Linear(config.n_embd, config.qkv_size, bias=config.bias)
+        self.proj = nn.Linear(config.n_head * config.head_size, config.n_embd, bias=config.bias)
+        self.config = config
+
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+        B, T, C = x.shape
+        c = self.config
+        qkv = self.attn(x)
+        q, k, v = qkv_split_rope(qkv, cos, sin, c.n_head, c.n_query_groups, c.head_size, c.rope_n_elem)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.n_query_groups != c.n_head)
+        y = y.transpose(1, 2).reshape(B, T, c.n_head * c.head_size)
+        return self.proj(y)
+
+
+class LLaMAMLP(nn.Module):
+    def __init__(self, config: Config):
+        super().__init__()
+        self.fc_1 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.fc_2 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x_fc_1 = self.fc_1(x)
+        x_fc_2 = self.fc_2(x)
+        x = F.silu(x_fc_1) * x_fc_2
+        return self.proj(x)
+
+
+class GptNeoxMLP(nn.Module):
+    def __init__(self, config: Config):
+        super().__init__()
+        self.fc = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
+        self.config = config
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.fc(x)
+        x = F.gelu(x, approximate=self.config.gelu_approximate)
+        return self.proj(x)
+
+
+class Block(nn.Module):
+    def __init__(self, config: Config):
+        super().__init__()
+        self.norm_1 = _norm(config, config.n_embd)
+        self.attn = CausalSelfAttention(config)
+        self.norm_2 = None if config.shared_attention_norm else _norm(config, config.n_embd)
+        self.mlp = LLaMAMLP(config) if config.mlp_class_name == "LLaMAMLP" else GptNeoxMLP(config)
+        self.config = config
+
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+        x_normed = self.norm_1(x)
+        h = self.attn(x_normed, cos, sin)
+        if self.config.parallel_residual:
+            n2 = x_normed if self.norm_2 is None else self.norm_2(x)
+            return self.mlp(n2) + h + x
+        x = h + x
+        return self.mlp(self.norm_2(x)) + x
+
+
+class GPT(nn.Module):
+    def __init__(self, config: Config):
+        super().__init__()
+        self.config = config
+        self.lm_head = nn.Linear(config.n_embd, config.padded_vocab_size, bias=config.lm_head_bias if hasattr(config, "lm_head_bias") else False)
+        self.transformer = nn.ModuleDict(
+            dict(
+                wte=nn.Embedding(config.padded_vocab_size, config.n_embd),
+                h=nn.ModuleList(Block(config) for _ in range(config.n_layer)),
+                ln_f=_norm(config, config.n_embd),
+            )
+        )
+        if config.tie_embeddings:
+            self.lm_head.weight = self.transformer.wte.weight
+        self.max_seq_length = config.block_size
+        self.register_buffer("cos", torch.empty(0), persistent=False)
+        self.register_buffer("sin", torch.empty(0), persistent=False)
+        self._rope_seq = 0
+
+    def set_rope_cache(self, seq_len: int, device=None) -> None:
+        cos, sin = build_rope_cache(seq_len, self.config.rope_n_elem, device=device, base=self.config.rope_base,
+                                    condense_ratio=self.config.rope_condense_ratio)
+        self.cos = cos
+        self.sin = sin
+        self._rope_seq = seq_len
+
+    def forward(self, idx: torch.Tensor) -> torch.Tensor:
+        T = idx.size(1)
+        if self.cos.numel() == 0 or self.cos.shape[0] < T:
+            raise RuntimeError("call model.set_rope_cache(seq_len, device) before forward")
+        cos = self.cos[:T]
+        sin = self.sin[:T]
+        x = self.transformer.wte(idx)
+        for block in self.transformer.h:
+            x = block(x, cos, sin)
+        x = self.transformer.ln_f(x)
+        return self.lm_head(x)
+
+    @classmethod
+    def from_name(cls, name: str, **kwargs) -> "GPT":
+        return cls(Config.from_name(name, **kwargs))
+
+
+def init_weights(model: GPT, std: float = 0.02) -> None:
+    """Random init (synthetic benchmark weights; no checkpoints are available offline)."""
+    for m in model.modules():
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, mean=0.0, std=std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, mean=0.0, std=std)
+
+
+def flops_per_token(config: Config, seq_len: int, training: bool = True) -> float:
+    """Model FLOPs per token (matmuls + attention), as used for MFU/TFLOP/s reporting."""
+    c = config
+    n_params_linear = c.n_layer * (c.n_embd * c.qkv_size + c.n_head * c.head_size * c.n_embd
+                                   + 3 * c.n_embd * c.intermediate_size) + c.n_embd * c.padded_vocab_size
+    attn = c.n_layer * 2 * 2 * seq_len * c.n_head * c.head_size / 2  # causal: half of QK^T and PV
+    fwd = 2 * n_params_linear + attn
+    return fwd * (3 if training else 1)

@@ -1,0 +1,88 @@
+"""In-tree build of the native library ``_lta_kernels.so`` (HIP kernels for gfx950 + C++ runtime).
+
+``python -m lightning_thunder_amd.ops.build`` compiles every ``csrc/*.hip`` kernel
+translation unit and every ``csrc/runtime/*.cpp`` host unit with ``hipcc
+--offload-arch=gfx950`` and links them (plus hiprtc for the fusion JIT) into
+``ops/_lta_kernels.so``.  Incremental: objects are rebuilt only when a source or
+header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "_lta_kernels.so")
+ARCH = os.environ.get("LTA_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build lightning_thunder_amd kernels)")
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _sources():
+    hip = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    cpp = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    return hip, cpp
+
+
+def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:
+    cmd = [_hipcc(), "-c", src, "-o", obj, "-fPIC", "-O3", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
+    if is_device:
+        cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+    else:
+        cmd += ["-D__HIP_PLATFORM_AMD__"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compilation failed for {src}:\n{r.stderr[-8000:]}")
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hip, cpp = _sources()
+    hdr = _headers_mtime()
+    todo = []
+    objs = []
+    for src in hip + cpp:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
+            todo.append((src, obj, src.endswith(".hip")))
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 4) // 2))
+    if todo:
+        with cf.ThreadPoolExecutor(jobs) as pool:
+            futs = [pool.submit(_compile, s, o, d, verbose) for s, o, d in todo]
+            for f in futs:
+                f.result()
+    newest = max((os.path.getmtime(o) for o in objs), default=0.0)
+    if force or todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp", *objs, "-lhiprtc"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    path = build(force="--force" in sys.argv, verbose="-v" in sys.argv)
+    print(path)

@@ -1,0 +1,285 @@
+// K4: RMSNorm forward/backward for CDNA4 (gfx950).
+// y = x * rsqrt(mean(x^2) + eps) * w, fp32 accumulation (reference decomposition:
+// thunder/torch/__init__.py:4450-4477; apex fused RMSNorm / nvFuser in the reference).
+//
+// Memory-bound: one 256-thread workgroup (4 waves) per row in the forward, each lane
+// moving 16 B per access (8 bf16) and caching its slice of the row in registers so the
+// row is read from HBM once.  The backward processes several rows per workgroup and keeps
+// the per-column dW partial sums in registers, writing one fp32 partial row per workgroup;
+// a second kernel reduces the partials (no float atomics: deterministic).
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+
+template <typename T, int CHUNKS>
+__global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                               T* __restrict__ y, float* __restrict__ rstd_out,
+                                                               int64_t rows, int cols, float eps) {
+  constexpr int V = Vec16<T>::N;
+  __shared__ float smem[kWaves];
+  const int64_t row = blockIdx.x;
+  const T* xr = x + row * cols;
+  T* yr = y + row * cols;
+  Vec16<T> xv[CHUNKS];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int idx = (c * kThreads + threadIdx.x) * V;
+    if (idx < cols) {
+      xv[c] = load16(xr + idx);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float f = to_f32(xv[c].v[j]);
+        ss += f * f;
+      }
+    }
+  }
+  const float total = block_sum<kWaves>(ss, smem);
+  const float r = rsqrtf(total / (float)cols + eps);
+  if (threadIdx.x == 0 && rstd_out != nullptr) rstd_out[row] = r;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int idx = (c * kThreads + threadIdx.x) * V;
+    if (idx < cols) {
+      Vec16<T> o;
+      if (w != nullptr) {
+        const Vec16<T> wv = load16(w + idx);
+#pragma unroll
+        for (int j = 0; j < V; ++j) o.v[j] = from_f32<T>(to_f32(xv[c].v[j]) * r * to_f32(wv.v[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) o.v[j] = from_f32<T>(to_f32(xv[c].v[j]) * r);
+      }
+      store16(yr + idx, o);
+    }
+  }
+}
+
+// Generic (any cols) fallback: strided scalar loops, two passes over the row.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void rmsnorm_fwd_generic(const T* __restrict__ x, const T* __restrict__ w,
+                                                                T* __restrict__ y, float* __restrict__ rstd_out,
+                                                                int64_t rows, int cols, float eps) {
+  __shared__ float smem[kWaves];
+  const int64_t row = blockIdx.x;
+  const T* xr = x + row * cols;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < cols; i += kThreads) {
+    const float f = to_f32(xr[i]);
+    ss += f * f;
+  }
+  const float r = rsqrtf(block_sum<kWaves>(ss, smem) / (float)cols + eps);
+  if (threadIdx.x == 0 && rstd_out != nullptr) rstd_out[row] = r;
+  for (int i = threadIdx.x; i < cols; i += kThreads) {
+    const float wv = w ? to_f32(w[i]) : 1.f;
+    y[row * cols + i] = from_f32<T>(to_f32(xr[i]) * r * wv);
+  }
+}
+
+template <typename T, int CHUNKS>
+__global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const T* __restrict__ w, const float* __restrict__ rstd,
+                                                               T* __restrict__ dx, float* __restrict__ dw_partial,
+                                                               int64_t rows, int cols, int rows_per_block) {
+  constexpr int V = Vec16<T>::N;
+  __shared__ float smem[kWaves];
+  float dw_acc[CHUNKS][V];
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c)
+#pragma unroll
+    for (int j = 0; j < V; ++j) dw_acc[c][j] = 0.f;
+  Vec16<T> wv[CHUNKS];
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int idx = (c * kThreads + threadIdx.x) * V;
+    if (idx < cols) {
+      if (w != nullptr) {
+        wv[c] = load16(w + idx);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) wv[c].v[j] = from_f32<T>(1.f);
+      }
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  for (int64_t row = r0; row < r1; ++row) {
+    const float r = rstd[row];
+    Vec16<T> xv[CHUNKS], gv[CHUNKS];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+      const int idx = (c * kThreads + threadIdx.x) * V;
+      if (idx < cols) {
+        xv[c] = load16(x + row * cols + idx);
+        gv[c] = load16(dy + row * cols + idx);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float xh = to_f32(xv[c].v[j]) * r;
+          const float g = to_f32(gv[c].v[j]);
+          dot += g * to_f32(wv[c].v[j]) * xh;
+          dw_acc[c][j] += g * xh;
+        }
+      }
+    }
+    dot = block_sum<kWaves>(dot, smem) / (float)cols;
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+      const int idx = (c * kThreads + threadIdx.x) * V;
+      if (idx < cols) {
+        Vec16<T> o;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float xh = to_f32(xv[c].v[j]) * r;
+          const float gw = to_f32(gv[c].v[j]) * to_f32(wv[c].v[j]);
+          o.v[j] = from_f32<T>(r * (gw - xh * dot));
+        }
+        store16(dx + row * cols + idx, o);
+      }
+    }
+  }
+  if (dw_partial != nullptr) {
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+      const int idx = (c * kThreads + threadIdx.x) * V;
+      if (idx < cols) {
+        float* p = dw_partial + (int64_t)blockIdx.x * cols + idx;
+#pragma unroll
+        for (int j = 0; j < V; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(dw_acc[c][j], dw_acc[c][j + 1], dw_acc[c][j + 2], dw_acc[c][j + 3]);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void rmsnorm_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                const T* __restrict__ w, const float* __restrict__ rstd,
+                                                                T* __restrict__ dx, float* __restrict__ dw_partial,
+                                                                int64_t rows, int cols, int rows_per_block) {
+  __shared__ float smem[kWaves];
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  for (int i = threadIdx.x; i < cols; i += kThreads) {
+    if (dw_partial) dw_partial[(int64_t)blockIdx.x * cols + i] = 0.f;
+  }
+  for (int64_t row = r0; row < r1; ++row) {
+    const float r = rstd[row];
+    float dot = 0.f;
+    for (int i = threadIdx.x; i < cols; i += kThreads) {
+      const float wv = w ? to_f32(w[i]) : 1.f;
+      dot += to_f32(dy[row * cols + i]) * wv * to_f32(x[row * cols + i]) * r;
+    }
+    dot = block_sum<kWaves>(dot, smem) / (float)cols;
+    for (int i = threadIdx.x; i < cols; i += kThreads) {
+      const float wv = w ? to_f32(w[i]) : 1.f;
+      const float xh = to_f32(x[row * cols + i]) * r;
+      const float g = to_f32(dy[row * cols + i]);
+      dx[row * cols + i] = from_f32<T>(r * (g * wv - xh * dot));
+      if (dw_partial) dw_partial[(int64_t)blockIdx.x * cols + i] += g * xh;
+    }
+  }
+}
+
+// Column reduction of the fp32 partials: dw[c] = sum_b partial[b, c]
+template <typename T>
+__global__ __launch_bounds__(kThreads) void column_reduce_kernel(const float* __restrict__ partial, T* __restrict__ out,
+                                                                 int nblocks, int cols) {
+  // each 256-thread block handles 64 columns with 4 waves splitting the rows
+  __shared__ float sm[kWaves][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (col < cols) {
+    for (int b = wid; b < nblocks; b += kWaves) acc += partial[(int64_t)b * cols + col];
+  }
+  sm[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && col < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) t += sm[i][lane];
+    out[col] = from_f32<T>(t);
+  }
+}
+
+template <typename T>
+int launch_fwd(const void* x, const void* w, void* y, void* rstd, int64_t rows, int cols, float eps, hipStream_t s) {
+  constexpr int V = Vec16<T>::N;
+  const int per_pass = kThreads * V;
+  const int chunks = (cols + per_pass - 1) / per_pass;
+  const T* X = (const T*)x;
+  const T* W = (const T*)w;
+  T* Y = (T*)y;
+  float* R = (float*)rstd;
+  dim3 grid((unsigned)rows), block(kThreads);
+  if (cols % V != 0 || chunks > 8 || ((uintptr_t)x % 16) || ((uintptr_t)y % 16) || (w && ((uintptr_t)w % 16))) {
+    hipLaunchKernelGGL((rmsnorm_fwd_generic<T>), grid, block, 0, s, X, W, Y, R, rows, cols, eps);
+  } else {
+    switch (chunks) {
+#define LTA_CASE(C) \
+  case C: hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, C>), grid, block, 0, s, X, W, Y, R, rows, cols, eps); break;
+      LTA_CASE(1) LTA_CASE(2) LTA_CASE(3) LTA_CASE(4) LTA_CASE(5) LTA_CASE(6) LTA_CASE(7) LTA_CASE(8)
+#undef LTA_CASE
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_bwd(const void* dy, const void* x, const void* w, const void* rstd, void* dx, void* dw, void* workspace,
+               int64_t rows, int cols, int nblocks, hipStream_t s) {
+  constexpr int V = Vec16<T>::N;
+  const int per_pass = kThreads * V;
+  const int chunks = (cols + per_pass - 1) / per_pass;
+  const int rpb = (int)((rows + nblocks - 1) / nblocks);
+  float* P = (float*)workspace;
+  dim3 grid((unsigned)nblocks), block(kThreads);
+  const T* DY = (const T*)dy;
+  const T* X = (const T*)x;
+  const T* W = (const T*)w;
+  const float* R = (const float*)rstd;
+  T* DX = (T*)dx;
+  float* Pp = dw ? P : nullptr;
+  if (cols % V != 0 || chunks > 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) || ((uintptr_t)dx % 16) || (w && ((uintptr_t)w % 16))) {
+    hipLaunchKernelGGL((rmsnorm_bwd_generic<T>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb);
+  } else {
+    switch (chunks) {
+#define LTA_CASE(C) \
+  case C: hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, C>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb); break;
+      LTA_CASE(1) LTA_CASE(2) LTA_CASE(3) LTA_CASE(4)
+#undef LTA_CASE
+    }
+  }
+  if (dw) {
+    dim3 g2((unsigned)((cols + 63) / 64));
+    hipLaunchKernelGGL((column_reduce_kernel<T>), g2, block, 0, s, P, (T*)dw, nblocks, cols);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, void* rstd, int64_t rows, int64_t cols,
+                               float eps, hipStream_t stream) {
+  switch (dtype) {
+    case kBF16: return launch_fwd<__hip_bfloat16>(x, w, y, rstd, rows, (int)cols, eps, stream);
+    case kF16: return launch_fwd<__half>(x, w, y, rstd, rows, (int)cols, eps, stream);
+    case kF32: return launch_fwd<float>(x, w, y, rstd, rows, (int)cols, eps, stream);
+  }
+  return -1;
+}
+
+LTA_EXPORT int lta_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const void* rstd, void* dx,
+                               void* dw, void* workspace, int64_t rows, int64_t cols, int nblocks, hipStream_t stream) {
+  switch (dtype) {
+    case kBF16: return launch_bwd<__hip_bfloat16>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
+    case kF16: return launch_bwd<__half>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
+    case kF32: return launch_bwd<float>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
+  }
+  return -1;
+}

@@ -1,0 +1,45 @@
+"""K4 RMSNorm wrappers (kernels in ``csrc/rmsnorm.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import require, dcode, ptr, stream_ptr, check
+
+
+def _as_2d(x: torch.Tensor):
+    cols = x.shape[-1]
+    x2 = x.reshape(-1, cols)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    return x2, x2.shape[0], cols
+
+
+def rms_norm_fwd(x: torch.Tensor, weight: torch.Tensor | None, eps: float):
+    lib = require()
+    x2, rows, cols = _as_2d(x)
+    w = None if weight is None else weight.contiguous()
+    y = torch.empty_like(x2)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rc = lib.lta_rmsnorm_fwd(dcode(x2), ptr(x2), ptr(w), ptr(y), ptr(rstd), rows, cols, float(eps), stream_ptr(x.device))
+    check(rc, "lta_rmsnorm_fwd")
+    return y.view(x.shape), rstd
+
+
+def _bwd_blocks(rows: int) -> int:
+    # ~2 workgroups per CU on MI355X (256 CUs), at least one row each
+    return max(1, min(rows, 512))
+
+
+def rms_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor | None, rstd: torch.Tensor):
+    lib = require()
+    x2, rows, cols = _as_2d(x)
+    dy2, _, _ = _as_2d(dy)
+    w = None if weight is None else weight.contiguous()
+    dx = torch.empty_like(x2)
+    nblocks = _bwd_blocks(rows)
+    dw = None if weight is None else torch.empty_like(w)
+    ws = torch.empty((nblocks, cols), device=x.device, dtype=torch.float32) if weight is not None else None
+    rc = lib.lta_rmsnorm_bwd(dcode(x2), ptr(dy2), ptr(x2), ptr(w), ptr(rstd), ptr(dx), ptr(dw), ptr(ws), rows, cols,
+                             nblocks, stream_ptr(x.device))
+    check(rc, "lta_rmsnorm_bwd")
+    return dx.view(x.shape), dw

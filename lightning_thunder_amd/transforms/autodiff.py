@@ -118,12 +118,24 @@ def _zip_grads(args, grads, acc):
             _zip_grads(a, grads.get(k), acc)
 
 
-def _executor_grad_transform(bsym: BoundSymbol, executors):
-    for ex in executors or ():
+def _executor_grad_transforms(bsym: BoundSymbol, executors) -> list:
+    """Grad transforms of the executors (in priority order, always-executors last) able to run ``bsym``.
+
+    A grad transform may return ``None`` to decline (e.g. unsupported layout), in which case the
+    next candidate is tried.
+    """
+    from ..extend import get_always_executors
+
+    out = []
+    seen = set()
+    for ex in list(executors or ()) + list(get_always_executors()):
+        if ex.name in seen:
+            continue
+        seen.add(ex.name)
         gt = ex.get_grad_transform(bsym.sym)
         if gt is not None and ex.can_execute_directly(bsym):
-            return gt
-    return None
+            out.append(gt)
+    return out
 
 
 # ---- generic torch.autograd rule for opaque (auto-registered) ops -------------------------
@@ -237,32 +249,29 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
         if not _is_differentiable_bsym(b):
             fw.bound_symbols.append(b)
             return
-        rule = _executor_grad_transform(b, executors)
-        if rule is None:
-            rule = _vjp_rules.get(b.sym.id, "missing")
-            if rule is None:  # explicitly non-differentiable
-                fw.bound_symbols.append(b)
-                return
-            if rule == "missing":
-                rule = None
-        if rule is None and OpTags.AUTO_REGISTERED in b.sym.tags:
-            rule = _opaque_rule(b.sym)
-        if rule is None:
+        candidates = _executor_grad_transforms(b, executors)
+        registered = _vjp_rules.get(b.sym.id, "missing")
+        if registered is None and not candidates:  # explicitly non-differentiable
+            fw.bound_symbols.append(b)
+            return
+        if registered not in (None, "missing"):
+            candidates.append(registered)
+        if OpTags.AUTO_REGISTERED in b.sym.tags:
+            candidates.append(_opaque_rule(b.sym))
+        args, kwargs = _canonicalize_args(b.sym, b.args, b.kwargs)
+        n_before = len(fw.bound_symbols)
+        res = None
+        for rule in candidates:
+            res = rule(*args, **kwargs)
+            if res is not None:
+                break
+            del fw.bound_symbols[n_before:]  # the rule declined (unsupported options)
+        if res is None:  # differentiate the decomposition
             if b.subsymbols:
                 for s in b.subsymbols:
                     process(s, recompute)
                 return
             raise NotImplementedError(f"No VJP rule for {b.sym.name} ({b.sym.id}) and it has no decomposition")
-        args, kwargs = _canonicalize_args(b.sym, b.args, b.kwargs)
-        n_before = len(fw.bound_symbols)
-        res = rule(*args, **kwargs)
-        if res is None:  # the rule declined (e.g. unsupported options): differentiate the decomposition
-            del fw.bound_symbols[n_before:]
-            if b.subsymbols:
-                for s in b.subsymbols:
-                    process(s, recompute)
-                return
-            raise NotImplementedError(f"VJP rule for {b.sym.name} declined and it has no decomposition")
         out, bwd = res
         if recompute:
             for nb in fw.bound_symbols[n_before:]:
