@@ -154,13 +154,16 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
     tok = _compile_data_ctx.set(cd)
     try:
         lookasides = {}
+        python_lookasides = []
         for ex in cd.executors_list:
             lookasides.update(ex._lookasides)
+            python_lookasides.extend(getattr(ex, "_python_lookasides", ()))
         from .transforms.autocast import autocast_ctx
 
         with autocast_ctx(entry.autocast_key):
             prog = acquire(cd.fn if module is None else module, args, kwargs, module=module, lookasides=lookasides,
-                           prune_param_checks=cd.compile_options.get("prune_prologue_checks", True))
+                           prune_param_checks=cd.compile_options.get("prune_prologue_checks", True),
+                           python_lookasides=python_lookasides)
         cs.last_trace_tracing_stop = time.perf_counter_ns()
         pro, comp, epi = prog.prologue_trace, prog.computation_trace, prog.epilogue_trace
         computation_traces = [comp]

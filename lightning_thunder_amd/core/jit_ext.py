@@ -201,8 +201,25 @@ class AcquiredProgram:
 
 
 def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
-            lookasides: dict | None = None, prune_param_checks: bool = True) -> AcquiredProgram:
+            lookasides: dict | None = None, prune_param_checks: bool = True,
+            python_lookasides: list | None = None) -> AcquiredProgram:
     """Traces ``fn(*args, **kwargs)`` and builds prologue / computation / epilogue traces."""
+    patched = []
+    for owner, attr, repl in python_lookasides or ():
+        if hasattr(owner, attr):
+            orig = getattr(owner, attr)
+            repl.__wrapped_original__ = orig
+            patched.append((owner, attr, orig))
+            setattr(owner, attr, repl)
+    try:
+        return _acquire(fn, args, kwargs, module=module, lookasides=lookasides, prune_param_checks=prune_param_checks)
+    finally:
+        for owner, attr, orig in reversed(patched):
+            setattr(owner, attr, orig)
+
+
+def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
+             lookasides: dict | None = None, prune_param_checks: bool = True) -> AcquiredProgram:
     prog = AcquiredProgram()
     comp = TraceCtx(fn if not isinstance(fn, torch.nn.Module) else type(fn).forward)
     comp.fn_name = "computation"

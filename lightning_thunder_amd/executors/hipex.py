@@ -87,10 +87,160 @@ def _rms_grad(a, normalized_shape, weight=None, eps=None):
     return y, bwd
 
 
+# =========================================================================================
+# K6 fused qkv split + RoPE (lookaside for the LitGPT helper `qkv_split_rope`)
+# =========================================================================================
+def _qkv_rope_meta(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    B, T, _ = qkv.shape
+    q = TensorProxy(like=qkv, shape=(B, n_head, T, head_size))
+    k = TensorProxy(like=qkv, shape=(B, n_query_groups, T, head_size))
+    v = TensorProxy(like=qkv, shape=(B, n_query_groups, T, head_size))
+    return q, k, v
+
+
+def _qkv_rope_impl(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    from ..ops.fused import qkv_rope_fwd
+
+    return qkv_rope_fwd(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n)
+
+
+def _qkv_rope_bwd_meta(dq, dk, dv, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    B, _, T, _ = dq.shape
+    return TensorProxy(like=dq, shape=(B, T, (n_head + 2 * n_query_groups) * head_size))
+
+
+def _qkv_rope_bwd_impl(dq, dk, dv, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    from ..ops.fused import qkv_rope_bwd
+
+    return qkv_rope_bwd(dq, dk, dv, cos, sin, n_head, n_query_groups, head_size, rope_n)
+
+
+hip_qkv_rope = ex.register_operator("hip_qkv_rope", meta=_qkv_rope_meta, fn=_qkv_rope_impl)
+hip_qkv_rope_bwd = ex.register_operator("hip_qkv_rope_bwd", meta=_qkv_rope_bwd_meta, fn=_qkv_rope_bwd_impl)
+
+
+def _qkv_rope_vjp(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    q, k, v = hip_qkv_rope(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n)
+
+    def bwd(gq, gk, gv):
+        return (hip_qkv_rope_bwd(gq, gk, gv, cos, sin, n_head, n_query_groups, head_size, rope_n),)
+
+    return (q, k, v), bwd
+
+
+def qkv_split_rope_lookaside(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n_elem):
+    ok = (
+        _gpu(qkv, cos, sin)
+        and qkv.dtype in _FLOAT16ISH
+        and qkv.ndim == 3
+        and head_size % 8 == 0
+        and rope_n_elem % 16 == 0
+        and rope_n_elem <= head_size
+        and cos.ndim == 2
+        and cos.shape[0] >= qkv.shape[1]
+        and cos.shape[1] == rope_n_elem
+        and cos.dtype in (torch.float32, qkv.dtype)
+    )
+    if not ok:
+        return qkv_split_rope_lookaside.__wrapped_original__(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n_elem)
+    return hip_qkv_rope(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n_elem)
+
+
+# =========================================================================================
+# SwiGLU (lookaside for the LitGPT helper `swiglu`)
+# =========================================================================================
+hip_swiglu = ex.register_operator("hip_swiglu", meta=lambda a, b: TensorProxy(like=a),
+                                  fn=lambda a, b: __import__("lightning_thunder_amd.ops.fused", fromlist=["x"]).swiglu_fwd(a, b))
+hip_swiglu_bwd = ex.register_operator(
+    "hip_swiglu_bwd", meta=lambda g, a, b: (TensorProxy(like=a), TensorProxy(like=b)),
+    fn=lambda g, a, b: __import__("lightning_thunder_amd.ops.fused", fromlist=["x"]).swiglu_bwd(g, a, b),
+)
+
+
+def _swiglu_vjp(a, b):
+    y = hip_swiglu(a, b)
+
+    def bwd(g):
+        da, db = hip_swiglu_bwd(g, a, b)
+        return da, db
+
+    return y, bwd
+
+
+def swiglu_lookaside(a, b):
+    if _gpu(a, b) and a.dtype in _FLOAT16ISH and a.dtype == b.dtype and tuple(a.shape) == tuple(b.shape):
+        return hip_swiglu(a, b)
+    return swiglu_lookaside.__wrapped_original__(a, b)
+
+
+# =========================================================================================
+# K7 softmax cross-entropy
+# =========================================================================================
+def _ce_fwd_meta(logits, target, ignore_index, reduction, label_smoothing):
+    rows = logits.shape[0]
+    loss = TensorProxy(like=logits, shape=(rows,) if reduction == "none" else ())
+    lse = TensorProxy(like=logits, shape=(rows,), dtype=torch.float32, requires_grad=False)
+    stats = TensorProxy(like=logits, shape=(2,), dtype=torch.float32, requires_grad=False)
+    return loss, lse, stats
+
+
+def _ce_fwd_impl(logits, target, ignore_index, reduction, label_smoothing):
+    from ..ops.fused import cross_entropy_fwd
+
+    return cross_entropy_fwd(logits, target, ignore_index, reduction, label_smoothing)
+
+
+def _ce_bwd_impl(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing):
+    from ..ops.fused import cross_entropy_bwd
+
+    return cross_entropy_bwd(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing)
+
+
+hip_cross_entropy_fwd = ex.register_operator("hip_cross_entropy_fwd", meta=_ce_fwd_meta, fn=_ce_fwd_impl)
+hip_cross_entropy_bwd = ex.register_operator(
+    "hip_cross_entropy_bwd", meta=lambda g, logits, *a: TensorProxy(like=logits), fn=_ce_bwd_impl
+)
+
+
+def _ce_checker(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
+    return (
+        _gpu(a, target)
+        and a.ndim == 2
+        and target.ndim == 1
+        and weight is None
+        and size_average is None
+        and reduce is None
+        and reduction in ("mean", "sum", "none")
+        and a.dtype in _FLOAT16ISH
+        and target.dtype in (torch.int64, torch.int32)
+    )
+
+
+def _ce_exec(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
+    loss, _, _ = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing)
+    return loss
+
+
+def _ce_grad(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
+    loss, lse, stats = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing)
+
+    def bwd(g):
+        return (hip_cross_entropy_bwd(g, a, target, lse, stats, ignore_index, reduction, label_smoothing),)
+
+    return loss, bwd
+
+
 def _register_all():
     from .. import torch as ltorch
+    from ..core.transforms import register_vjp
+    from ..models import litgpt
 
     ex.register_implementation(ltorch.rms_norm, checker=_rms_checker, execution_transform=_rms_exec, grad_transform=_rms_grad)
+    ex.register_implementation(ltorch.cross_entropy, checker=_ce_checker, execution_transform=_ce_exec, grad_transform=_ce_grad)
+    register_vjp(hip_qkv_rope)(_qkv_rope_vjp)
+    register_vjp(hip_swiglu)(_swiglu_vjp)
+    ex.register_python_lookaside(litgpt, "qkv_split_rope", qkv_split_rope_lookaside)
+    ex.register_python_lookaside(litgpt, "swiglu", swiglu_lookaside)
 
 
 _register_all()

@@ -152,6 +152,13 @@ class Executor:
     def register_lookaside(self, fn: Callable, replacement: Callable) -> None:
         self._lookasides[fn] = replacement
 
+    def register_python_lookaside(self, owner: Any, attr: str, replacement: Callable) -> None:
+        """While a program is acquired, ``owner.attr`` (a python function, e.g. a model helper) is
+        replaced by ``replacement``; the replacement may emit this executor's fused operators."""
+        if not hasattr(self, "_python_lookasides"):
+            self._python_lookasides = []
+        self._python_lookasides.append((owner, attr, replacement))
+
     def bind_call_ctx(self, bsym: BoundSymbol, original: BoundSymbol | None = None) -> BoundSymbol:
         # Replay the exact torch callable the user invoked (keeps the user's call signature valid)
         if original is not None and getattr(bsym.sym, "replay_torch", False):

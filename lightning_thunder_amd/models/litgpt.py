@@ -138,6 +138,11 @@ def qkv_split_rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_he
     return q, k, v
 
 
+def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """LLaMA MLP gate: silu(a) * b."""
+    return F.silu(a) * b
+
+
 class RMSNorm(nn.Module):
     def __init__(self, size: int, dim: int = -1, eps: float = 1e-6):
         super().__init__()
@@ -185,8 +190,7 @@ class LLaMAMLP(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x_fc_1 = self.fc_1(x)
         x_fc_2 = self.fc_2(x)
-        x = F.silu(x_fc_1) * x_fc_2
-        return self.proj(x)
+        return self.proj(swiglu(x_fc_1, x_fc_2))
 
 
 class GptNeoxMLP(nn.Module):

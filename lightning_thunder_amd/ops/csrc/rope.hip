@@ -1,0 +1,172 @@
+// K6: fused qkv split + RoPE (forward and backward) for CDNA4.
+//
+// Forward: qkv [B, T, (nh + 2*ng) * hs] (output of the fused QKV projection) ->
+//   q [B, nh, T, hs], k [B, ng, T, hs] with LitGPT's rotate-half RoPE on the first `rope_n`
+//   elements of every head, v [B, ng, T, hs] (pure layout change).
+// Backward: (dq, dk, dv) -> dqkv with the inverse rotation.
+// Replaces the reference's torch.compile(Inductor) "torchcompile_cat" RoPE fusion
+// (thunder/executors/torch_compile.py:205-234; benchmark LlamaQKVSplitRopeBenchmark).
+//
+// Each work item moves one 16-byte chunk (8 elements) of a head row and, for rotated chunks,
+// also its partner chunk half a rope width away, so every HBM access is a 16-B vector.
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+template <typename T, typename C>
+__global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__ qkv, const C* __restrict__ cos_,
+                                                           const C* __restrict__ sin_, T* __restrict__ q,
+                                                           T* __restrict__ k, T* __restrict__ v, int B, int Tn, int nh,
+                                                           int ng, int hs, int rope_n) {
+  const int chunks = hs / 8;
+  const int heads = nh + 2 * ng;
+  const int64_t total = (int64_t)B * Tn * heads * chunks;
+  const int half = rope_n / 2;
+  for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(it % chunks);
+    int64_t rest = it / chunks;
+    const int h = (int)(rest % heads);
+    rest /= heads;
+    const int t = (int)(rest % Tn);
+    const int b = (int)(rest / Tn);
+    const int d0 = c * 8;
+    const T* src = qkv + (((int64_t)b * Tn + t) * heads + h) * hs;
+    T* dst;
+    bool rotate;
+    if (h < nh) {
+      dst = q + (((int64_t)b * nh + h) * Tn + t) * hs;
+      rotate = true;
+    } else if (h < nh + ng) {
+      dst = k + (((int64_t)b * ng + (h - nh)) * Tn + t) * hs;
+      rotate = true;
+    } else {
+      dst = v + (((int64_t)b * ng + (h - nh - ng)) * Tn + t) * hs;
+      rotate = false;
+    }
+    if (!rotate || d0 >= rope_n) {
+      store16(dst + d0, load16(src + d0));
+      continue;
+    }
+    if (d0 >= half) continue;  // handled together with its partner chunk
+    const Vec16<T> x1 = load16(src + d0);
+    const Vec16<T> x2 = load16(src + d0 + half);
+    const C* cr = cos_ + (int64_t)t * rope_n;
+    const C* sr = sin_ + (int64_t)t * rope_n;
+    Vec16<T> o1, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = to_f32(x1.v[j]), bb = to_f32(x2.v[j]);
+      const float c1 = to_f32(cr[d0 + j]), s1 = to_f32(sr[d0 + j]);
+      const float c2 = to_f32(cr[d0 + half + j]), s2 = to_f32(sr[d0 + half + j]);
+      o1.v[j] = from_f32<T>(a * c1 - bb * s1);
+      o2.v[j] = from_f32<T>(bb * c2 + a * s2);
+    }
+    store16(dst + d0, o1);
+    store16(dst + d0 + half, o2);
+  }
+}
+
+template <typename T, typename C>
+__global__ __launch_bounds__(256) void qkv_rope_bwd_kernel(const T* __restrict__ dq, const T* __restrict__ dk,
+                                                           const T* __restrict__ dv, const C* __restrict__ cos_,
+                                                           const C* __restrict__ sin_, T* __restrict__ dqkv, int B,
+                                                           int Tn, int nh, int ng, int hs, int rope_n) {
+  const int chunks = hs / 8;
+  const int heads = nh + 2 * ng;
+  const int64_t total = (int64_t)B * Tn * heads * chunks;
+  const int half = rope_n / 2;
+  for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(it % chunks);
+    int64_t rest = it / chunks;
+    const int h = (int)(rest % heads);
+    rest /= heads;
+    const int t = (int)(rest % Tn);
+    const int b = (int)(rest / Tn);
+    const int d0 = c * 8;
+    T* dst = dqkv + (((int64_t)b * Tn + t) * heads + h) * hs;
+    const T* src;
+    bool rotate;
+    if (h < nh) {
+      src = dq + (((int64_t)b * nh + h) * Tn + t) * hs;
+      rotate = true;
+    } else if (h < nh + ng) {
+      src = dk + (((int64_t)b * ng + (h - nh)) * Tn + t) * hs;
+      rotate = true;
+    } else {
+      src = dv + (((int64_t)b * ng + (h - nh - ng)) * Tn + t) * hs;
+      rotate = false;
+    }
+    if (!rotate || d0 >= rope_n) {
+      store16(dst + d0, load16(src + d0));
+      continue;
+    }
+    if (d0 >= half) continue;
+    const Vec16<T> g1 = load16(src + d0);
+    const Vec16<T> g2 = load16(src + d0 + half);
+    const C* cr = cos_ + (int64_t)t * rope_n;
+    const C* sr = sin_ + (int64_t)t * rope_n;
+    Vec16<T> o1, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = to_f32(g1.v[j]), bb = to_f32(g2.v[j]);
+      const float c1 = to_f32(cr[d0 + j]), s1 = to_f32(sr[d0 + j]);
+      const float c2 = to_f32(cr[d0 + half + j]), s2 = to_f32(sr[d0 + half + j]);
+      // y1 = x1*c1 - x2*s1 ; y2 = x2*c2 + x1*s2
+      o1.v[j] = from_f32<T>(a * c1 + bb * s2);
+      o2.v[j] = from_f32<T>(bb * c2 - a * s1);
+    }
+    store16(dst + d0, o1);
+    store16(dst + d0 + half, o2);
+  }
+}
+
+int grid_for(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+#define LTA_DISPATCH_TC(dtype, cdtype, ...)                       \
+  do {                                                           \
+    if (dtype == kBF16 && cdtype == kF32) {                      \
+      using T = __hip_bfloat16; using C = float; __VA_ARGS__;     \
+    } else if (dtype == kBF16 && cdtype == kBF16) {              \
+      using T = __hip_bfloat16; using C = __hip_bfloat16; __VA_ARGS__; \
+    } else if (dtype == kF16 && cdtype == kF32) {                \
+      using T = __half; using C = float; __VA_ARGS__;             \
+    } else if (dtype == kF16 && cdtype == kF16) {                \
+      using T = __half; using C = __half; __VA_ARGS__;            \
+    } else if (dtype == kF32 && cdtype == kF32) {                \
+      using T = float; using C = float; __VA_ARGS__;              \
+    } else {                                                     \
+      return -1;                                                 \
+    }                                                            \
+  } while (0)
+
+LTA_EXPORT int lta_qkv_rope_fwd(int dtype, int cdtype, const void* qkv, const void* cos_, const void* sin_, void* q,
+                                void* k, void* v, int B, int Tn, int nh, int ng, int hs, int rope_n,
+                                hipStream_t stream) {
+  if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
+  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / 8);
+  LTA_DISPATCH_TC(dtype, cdtype,
+                  hipLaunchKernelGGL((qkv_rope_fwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
+                                     (const T*)qkv, (const C*)cos_, (const C*)sin_, (T*)q, (T*)k, (T*)v, B, Tn, nh, ng,
+                                     hs, rope_n));
+  return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_qkv_rope_bwd(int dtype, int cdtype, const void* dq, const void* dk, const void* dv, const void* cos_,
+                                const void* sin_, void* dqkv, int B, int Tn, int nh, int ng, int hs, int rope_n,
+                                hipStream_t stream) {
+  if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
+  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / 8);
+  LTA_DISPATCH_TC(dtype, cdtype,
+                  hipLaunchKernelGGL((qkv_rope_bwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
+                                     (const T*)dq, (const T*)dk, (const T*)dv, (const C*)cos_, (const C*)sin_, (T*)dqkv,
+                                     B, Tn, nh, ng, hs, rope_n));
+  return (int)hipGetLastError();
+}

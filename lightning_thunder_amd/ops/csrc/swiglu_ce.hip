@@ -1,0 +1,248 @@
+// SwiGLU (silu(a) * b) forward/backward and K7 softmax cross-entropy forward/backward for CDNA4.
+//
+// SwiGLU is the LLaMA MLP gate ([tokens, 11008] x 2 for Llama-2-7B); forward reads a, b and
+// writes y; backward reads g, a, b and writes da, db — one pass each, 16-B vectors.
+//
+// Cross entropy replaces the reference's in-repo Triton kernels
+// (thunder/executors/triton_crossentropy_impl.py:49-540): forward is one online
+// max/sum-exp pass per row (logits read once), saving the row's log-sum-exp; backward
+// writes (softmax - onehot) * dloss / n_valid in one pass.  Rows are [tokens, vocab]
+// with vocab = 32000 for Llama-2 (64 KB of bf16 per row).
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                         T* __restrict__ y, int64_t n) {
+  constexpr int V = Vec16<T>::N;
+  const int64_t nv = n / V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const Vec16<T> av = load16(a + i * V), bv = load16(b + i * V);
+    Vec16<T> o;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float x = to_f32(av.v[j]);
+      o.v[j] = from_f32<T>(x * sigmoidf_(x) * to_f32(bv.v[j]));
+    }
+    store16(y + i * V, o);
+  }
+  // tail
+  for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float x = to_f32(a[i]);
+    y[i] = from_f32<T>(x * sigmoidf_(x) * to_f32(b[i]));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ g, const T* __restrict__ a,
+                                                         const T* __restrict__ b, T* __restrict__ da,
+                                                         T* __restrict__ db, int64_t n) {
+  constexpr int V = Vec16<T>::N;
+  const int64_t nv = n / V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const Vec16<T> gv = load16(g + i * V), av = load16(a + i * V), bv = load16(b + i * V);
+    Vec16<T> oa, ob;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float x = to_f32(av.v[j]), gg = to_f32(gv.v[j]), bb = to_f32(bv.v[j]);
+      const float s = sigmoidf_(x);
+      const float silu = x * s;
+      oa.v[j] = from_f32<T>(gg * bb * (s * (1.f + x * (1.f - s))));
+      ob.v[j] = from_f32<T>(gg * silu);
+    }
+    store16(da + i * V, oa);
+    store16(db + i * V, ob);
+  }
+  for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float x = to_f32(a[i]), gg = to_f32(g[i]), bb = to_f32(b[i]);
+    const float s = sigmoidf_(x);
+    da[i] = from_f32<T>(gg * bb * (s * (1.f + x * (1.f - s))));
+    db[i] = from_f32<T>(gg * x * s);
+  }
+}
+
+int ew_grid(int64_t n_items) {
+  int64_t g = (n_items + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  return (int)(g < 1 ? 1 : g);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross entropy.  One 256-thread workgroup per row.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCeThreads = 256;
+constexpr int kCeWaves = kCeThreads / 64;
+
+template <typename T>
+__global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                            float* __restrict__ loss, float* __restrict__ lse_out,
+                                                            int64_t rows, int V, int64_t ignore_index,
+                                                            float label_smoothing) {
+  constexpr int VEC = Vec16<T>::N;
+  __shared__ float sm[kCeWaves];
+  const int64_t row = blockIdx.x;
+  const T* x = logits + row * (int64_t)V;
+  float m = -INFINITY, s = 0.f, sum_x = 0.f;
+  const bool vec = (V % VEC == 0) && (((uintptr_t)logits) % 16 == 0);
+  if (vec) {
+    for (int i = threadIdx.x * VEC; i < V; i += kCeThreads * VEC) {
+      const Vec16<T> xv = load16(x + i);
+      float lm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) lm = fmaxf(lm, to_f32(xv.v[j]));
+      const float nm = fmaxf(m, lm);
+      float acc = s * __expf(m - nm);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float f = to_f32(xv.v[j]);
+        acc += __expf(f - nm);
+        sum_x += f;
+      }
+      s = acc;
+      m = nm;
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += kCeThreads) {
+      const float f = to_f32(x[i]);
+      const float nm = fmaxf(m, f);
+      s = s * __expf(m - nm) + __expf(f - nm);
+      m = nm;
+      sum_x += f;
+    }
+  }
+  // combine (m, s) across the block
+  const float gm = block_max<kCeWaves>(m, sm);
+  const float scaled = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  __syncthreads();
+  const float gs = block_sum<kCeWaves>(scaled, sm);
+  __syncthreads();
+  const float gsum_x = (label_smoothing != 0.f) ? block_sum<kCeWaves>(sum_x, sm) : 0.f;
+  if (threadIdx.x == 0) {
+    const float lse = gm + __logf(gs);
+    lse_out[row] = lse;
+    const int64_t t = target[row];
+    if (t == ignore_index) {
+      loss[row] = 0.f;
+    } else {
+      const float xt = to_f32(x[t]);
+      float l = lse - xt;
+      if (label_smoothing != 0.f) l = (1.f - label_smoothing) * l + label_smoothing * (lse - gsum_x / (float)V);
+      loss[row] = l;
+    }
+  }
+}
+
+// reduction: out[0] = sum(loss)/max(count,1) (mean) or sum; out[1] = count of valid rows
+__global__ __launch_bounds__(256) void ce_reduce_kernel(const float* __restrict__ loss, const int64_t* __restrict__ target,
+                                                        float* __restrict__ out, int64_t rows, int64_t ignore_index,
+                                                        int mean) {
+  __shared__ float sm[4];
+  float s = 0.f, c = 0.f;
+  for (int64_t i = threadIdx.x; i < rows; i += 256) {
+    s += loss[i];
+    c += (target[i] != ignore_index) ? 1.f : 0.f;
+  }
+  const float ts = block_sum<4>(s, sm);
+  __syncthreads();
+  const float tc = block_sum<4>(c, sm);
+  if (threadIdx.x == 0) {
+    out[0] = mean ? ts / fmaxf(tc, 1.f) : ts;
+    out[1] = tc;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kCeThreads) void ce_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                            const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                            const float* __restrict__ stats, T* __restrict__ dlogits,
+                                                            int64_t rows, int V, int64_t ignore_index, int mean,
+                                                            int per_row_grad, float label_smoothing) {
+  constexpr int VEC = Vec16<T>::N;
+  const int64_t row = blockIdx.x;
+  const int64_t t = target[row];
+  const T* x = logits + row * (int64_t)V;
+  T* dx = dlogits + row * (int64_t)V;
+  float g;
+  if (per_row_grad) {
+    g = gscale[row];
+  } else {
+    g = gscale[0];
+    if (mean) g = g / fmaxf(stats[1], 1.f);
+  }
+  if (t == ignore_index) g = 0.f;
+  const float l = lse[row];
+  const float smooth = label_smoothing / (float)V;
+  const float on = 1.f - label_smoothing;
+  const bool vec = (V % VEC == 0) && (((uintptr_t)logits) % 16 == 0) && (((uintptr_t)dlogits) % 16 == 0);
+  if (vec) {
+    for (int i = threadIdx.x * VEC; i < V; i += kCeThreads * VEC) {
+      const Vec16<T> xv = load16(x + i);
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float p = __expf(to_f32(xv.v[j]) - l);
+        const float oh = (i + j == t) ? on : 0.f;
+        o.v[j] = from_f32<T>(g * (p - oh - smooth));
+      }
+      store16(dx + i, o);
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += kCeThreads) {
+      const float p = __expf(to_f32(x[i]) - l);
+      const float oh = (i == t) ? on : 0.f;
+      dx[i] = from_f32<T>(g * (p - oh - smooth));
+    }
+  }
+}
+
+}  // namespace
+
+#define LTA_DISPATCH_T(dtype, ...)                                     \
+  do {                                                                \
+    if (dtype == kBF16) { using T = __hip_bfloat16; __VA_ARGS__; }      \
+    else if (dtype == kF16) { using T = __half; __VA_ARGS__; }          \
+    else if (dtype == kF32) { using T = float; __VA_ARGS__; }           \
+    else { return -1; }                                               \
+  } while (0)
+
+LTA_EXPORT int lta_swiglu_fwd(int dtype, const void* a, const void* b, void* y, int64_t n, hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((swiglu_fwd_kernel<T>), dim3(ew_grid(n / Vec16<T>::N + 1)), dim3(256), 0,
+                                           stream, (const T*)a, (const T*)b, (T*)y, n));
+  return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_swiglu_bwd(int dtype, const void* g, const void* a, const void* b, void* da, void* db, int64_t n,
+                              hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((swiglu_bwd_kernel<T>), dim3(ew_grid(n / Vec16<T>::N + 1)), dim3(256), 0,
+                                           stream, (const T*)g, (const T*)a, (const T*)b, (T*)da, (T*)db, n));
+  return (int)hipGetLastError();
+}
+
+// reduction: 0 = none (per-row losses returned), 1 = mean, 2 = sum
+LTA_EXPORT int lta_ce_fwd(int dtype, const void* logits, const int64_t* target, void* loss_rows, void* lse, void* out,
+                          int64_t rows, int64_t V, int64_t ignore_index, int reduction, float label_smoothing,
+                          hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
+                                           (const T*)logits, target, (float*)loss_rows, (float*)lse, rows, (int)V,
+                                           ignore_index, label_smoothing));
+  if (reduction != 0) {
+    hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, stream, (const float*)loss_rows, target, (float*)out,
+                       rows, ignore_index, reduction == 1 ? 1 : 0);
+  }
+  return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_ce_bwd(int dtype, const void* logits, const int64_t* target, const void* lse, const void* gscale,
+                          const void* stats, void* dlogits, int64_t rows, int64_t V, int64_t ignore_index,
+                          int reduction, float label_smoothing, hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
+                                           (const T*)logits, target, (const float*)lse, (const float*)gscale,
+                                           (const float*)stats, (T*)dlogits, rows, (int)V, ignore_index,
+                                           reduction == 1 ? 1 : 0, reduction == 0 ? 1 : 0, label_smoothing));
+  return (int)hipGetLastError();
+}

@@ -32,4 +32,37 @@ def test_litgpt_fwd_bwd_gpu(name, dtype):
         torch.testing.assert_close(got[n], p.grad.float(), atol=tol * 10, rtol=tol * 10, msg=n)
     src = str(thunder.last_traces(tm)[-1])
     if name != "gpt-neox-like":
-        assert "hip_rms_norm_fwd" in src
+        assert "hip_rms_norm_fwd" in src and "hip_qkv_rope" in src and "hip_swiglu" in src
+
+
+def test_train_step_with_fused_loss_gpu():
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = GPT.from_name("llama2-like").to(device=dev, dtype=torch.bfloat16)
+    init_weights(m)
+    m.set_rope_cache(64, device=dev)
+    V = m.config.padded_vocab_size
+
+    class TS(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, x, y):
+            return torch.nn.functional.cross_entropy(self.m(x).reshape(-1, V), y.reshape(-1))
+
+    ts = TS(m)
+    tm = thunder.jit(ts)
+    x = torch.randint(0, 320, (2, 64), device=dev)
+    y = torch.randint(0, 320, (2, 64), device=dev)
+    loss = tm(x, y)
+    loss.backward()
+    got = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    for p in m.parameters():
+        p.grad = None
+    ref = ts(x, y)
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    for n, p in m.named_parameters():
+        torch.testing.assert_close(got[n], p.grad.float(), atol=5e-2, rtol=5e-2, msg=n)
+    assert "hip_cross_entropy_fwd" in str(thunder.last_traces(tm)[-1])
