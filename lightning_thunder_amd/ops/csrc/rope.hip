@@ -20,7 +20,8 @@ __global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__
                                                            const C* __restrict__ sin_, T* __restrict__ q,
                                                            T* __restrict__ k, T* __restrict__ v, int B, int Tn, int nh,
                                                            int ng, int hs, int rope_n) {
-  const int chunks = hs / 8;
+  constexpr int VW = Vec16<T>::N;
+  const int chunks = hs / VW;
   const int heads = nh + 2 * ng;
   const int64_t total = (int64_t)B * Tn * heads * chunks;
   const int half = rope_n / 2;
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__
     rest /= heads;
     const int t = (int)(rest % Tn);
     const int b = (int)(rest / Tn);
-    const int d0 = c * 8;
+    const int d0 = c * VW;
     const T* src = qkv + (((int64_t)b * Tn + t) * heads + h) * hs;
     T* dst;
     bool rotate;
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__
     const C* sr = sin_ + (int64_t)t * rope_n;
     Vec16<T> o1, o2;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < VW; ++j) {
       const float a = to_f32(x1.v[j]), bb = to_f32(x2.v[j]);
       const float c1 = to_f32(cr[d0 + j]), s1 = to_f32(sr[d0 + j]);
       const float c2 = to_f32(cr[d0 + half + j]), s2 = to_f32(sr[d0 + half + j]);
@@ -73,7 +74,8 @@ __global__ __launch_bounds__(256) void qkv_rope_bwd_kernel(const T* __restrict__
                                                            const T* __restrict__ dv, const C* __restrict__ cos_,
                                                            const C* __restrict__ sin_, T* __restrict__ dqkv, int B,
                                                            int Tn, int nh, int ng, int hs, int rope_n) {
-  const int chunks = hs / 8;
+  constexpr int VW = Vec16<T>::N;
+  const int chunks = hs / VW;
   const int heads = nh + 2 * ng;
   const int64_t total = (int64_t)B * Tn * heads * chunks;
   const int half = rope_n / 2;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) void qkv_rope_bwd_kernel(const T* __restrict__
     rest /= heads;
     const int t = (int)(rest % Tn);
     const int b = (int)(rest / Tn);
-    const int d0 = c * 8;
+    const int d0 = c * VW;
     T* dst = dqkv + (((int64_t)b * Tn + t) * heads + h) * hs;
     const T* src;
     bool rotate;
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void qkv_rope_bwd_kernel(const T* __restrict__
     const C* sr = sin_ + (int64_t)t * rope_n;
     Vec16<T> o1, o2;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < VW; ++j) {
       const float a = to_f32(g1.v[j]), bb = to_f32(g2.v[j]);
       const float c1 = to_f32(cr[d0 + j]), s1 = to_f32(sr[d0 + j]);
       const float c2 = to_f32(cr[d0 + half + j]), s2 = to_f32(sr[d0 + half + j]);
@@ -151,7 +153,7 @@ LTA_EXPORT int lta_qkv_rope_fwd(int dtype, int cdtype, const void* qkv, const vo
                                 void* k, void* v, int B, int Tn, int nh, int ng, int hs, int rope_n,
                                 hipStream_t stream) {
   if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
-  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / 8);
+  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / (dtype == kF32 ? 4 : 8));
   LTA_DISPATCH_TC(dtype, cdtype,
                   hipLaunchKernelGGL((qkv_rope_fwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
                                      (const T*)qkv, (const C*)cos_, (const C*)sin_, (T*)q, (T*)k, (T*)v, B, Tn, nh, ng,
@@ -163,7 +165,7 @@ LTA_EXPORT int lta_qkv_rope_bwd(int dtype, int cdtype, const void* dq, const voi
                                 const void* sin_, void* dqkv, int B, int Tn, int nh, int ng, int hs, int rope_n,
                                 hipStream_t stream) {
   if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
-  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / 8);
+  const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / (dtype == kF32 ? 4 : 8));
   LTA_DISPATCH_TC(dtype, cdtype,
                   hipLaunchKernelGGL((qkv_rope_bwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
                                      (const T*)dq, (const T*)dk, (const T*)dv, (const C*)cos_, (const C*)sin_, (T*)dqkv,
