@@ -230,6 +230,71 @@ def _ce_grad(a, target, weight=None, size_average=None, ignore_index=-100, reduc
     return loss, bwd
 
 
+# =========================================================================================
+# K3 flash attention (claims ltorch.scaled_dot_product_attention; saves O and LSE for backward)
+# =========================================================================================
+def _attn_fwd_meta(q, k, v, causal, scale):
+    B, H, L, E = q.shape
+    return TensorProxy(like=q), TensorProxy(like=q, shape=(B, H, L), dtype=torch.float32, requires_grad=False)
+
+
+def _attn_fwd_impl(q, k, v, causal, scale):
+    from ..ops.attention import attn_fwd
+
+    return attn_fwd(q, k, v, causal, scale)
+
+
+def _attn_bwd_impl(g, q, k, v, o, lse, causal, scale):
+    from ..ops.attention import attn_bwd
+
+    return attn_bwd(g, q, k, v, o, lse, causal, scale)
+
+
+hip_attn_fwd = ex.register_operator("hip_flash_attn_fwd", meta=_attn_fwd_meta, fn=_attn_fwd_impl)
+hip_attn_bwd = ex.register_operator(
+    "hip_flash_attn_bwd",
+    meta=lambda g, q, k, v, o, lse, causal, scale: (TensorProxy(like=q), TensorProxy(like=k), TensorProxy(like=v)),
+    fn=_attn_bwd_impl,
+)
+
+
+def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    if attn_mask is not None or dropout_p != 0.0 or not _gpu(query, key, value):
+        return False
+    if query.ndim != 4 or key.ndim != 4 or value.ndim != 4:
+        return False
+    if query.dtype not in (torch.bfloat16, torch.float16) or key.dtype != query.dtype or value.dtype != query.dtype:
+        return False
+    D = query.shape[-1]
+    if D not in (64, 128) or key.shape[-1] != D or value.shape[-1] != D:
+        return False
+    if key.shape[1] != value.shape[1] or query.shape[1] % key.shape[1] != 0:
+        return False
+    if key.shape[1] != query.shape[1] and not enable_gqa:
+        return False
+    return query.shape[0] == key.shape[0] == value.shape[0] and key.shape[2] == value.shape[2]
+
+
+def _sc(q, scale):
+    return scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+
+
+def _sdpa_exec(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    out, _ = hip_attn_fwd(query, key, value, bool(is_causal), _sc(query, scale))
+    return out
+
+
+def _sdpa_grad(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    sc = _sc(query, scale)
+    out, lse = hip_attn_fwd(query, key, value, bool(is_causal), sc)
+
+    def bwd(g):
+        dq, dk, dv = hip_attn_bwd(g, query, key, value, out, lse, bool(is_causal), sc)
+        return dq, dk, dv
+
+    return out, bwd
+
+
 def _register_all():
     from .. import torch as ltorch
     from ..core.transforms import register_vjp
@@ -237,6 +302,8 @@ def _register_all():
 
     ex.register_implementation(ltorch.rms_norm, checker=_rms_checker, execution_transform=_rms_exec, grad_transform=_rms_grad)
     ex.register_implementation(ltorch.cross_entropy, checker=_ce_checker, execution_transform=_ce_exec, grad_transform=_ce_grad)
+    ex.register_implementation(ltorch.scaled_dot_product_attention, checker=_sdpa_checker, execution_transform=_sdpa_exec,
+                               grad_transform=_sdpa_grad)
     register_vjp(hip_qkv_rope)(_qkv_rope_vjp)
     register_vjp(hip_swiglu)(_swiglu_vjp)
     ex.register_python_lookaside(litgpt, "qkv_split_rope", qkv_split_rope_lookaside)

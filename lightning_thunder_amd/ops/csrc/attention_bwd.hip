@@ -1,0 +1,392 @@
+// K3 flash-attention backward for CDNA4 (gfx950): recompute P from Q, K and the forward LSE.
+//
+// Three launches (FA2-style split; no float atomics, bitwise reproducible):
+//  1. preprocess: delta[q] = rowsum(dO[q] * O[q])                                  (fp32)
+//  2. dK/dV: one workgroup per 128-key block (32 keys per wave, K and V rows held in registers
+//     as MFMA B operands), sweeping 32-query tiles of every query head of the kv group:
+//        S = Q K^T (key on the lane), P = exp2(S*c - lse*log2e), dP = dO V^T,
+//        dS = P (dP - delta),  dV^T += dO^T P,  dK^T += Q^T dS
+//     The S/dP accumulators feed dV^T/dK^T directly as B operands (attention.h), dO^T and Q^T
+//     come from transposed LDS reads.
+//  3. dQ: one workgroup per 128-query block (as the forward), sweeping 64-key tiles:
+//        S^T = K Q^T, P^T, dP^T = V dO^T, dS^T,  dQ^T += K^T dS^T
+// Both main kernels skip fully masked tiles under causal masking.
+#include "attention.h"
+
+using namespace lta;
+using namespace lta::attn;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+template <int D> struct BCfg {
+  static constexpr int RSTR = D + 8;    // row-read image stride (ds_read_b128 conflict-free)
+  static constexpr int TSTR = D + 32;   // transposed-read image stride (ds_read_b64_tr_b16 conflict-free)
+  static constexpr int CH = D / 8;
+  static constexpr int KS = D / 16;
+  static constexpr int DT = D / 32;
+};
+
+// ---------------------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__ dO, const T* __restrict__ O,
+                                                           float* __restrict__ delta, int64_t rows) {
+  // 8 lanes per row (16 B each per step)
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 8;
+  const int sub = threadIdx.x & 7;
+  float acc = 0.f;
+  if (row < rows) {
+    const T* a = dO + row * D;
+    const T* b = O + row * D;
+#pragma unroll
+    for (int c = sub * 8; c < D; c += 64) {
+      const Vec16<T> x = load16(a + c), y = load16(b + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += to_f32(x.v[j]) * to_f32(y.v[j]);
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < rows && sub == 0) delta[row] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK / dV
+// ---------------------------------------------------------------------------------------------
+constexpr int kKB = 128;  // keys per workgroup
+constexpr int kQT = 32;   // queries per inner tile
+
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                    const T* __restrict__ V, const T* __restrict__ dO,
+                                                                    const float* __restrict__ LSE,
+                                                                    const float* __restrict__ DELTA, T* __restrict__ dK,
+                                                                    T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
+                                                                    float scale, float scale_log2) {
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  __shared__ __attribute__((aligned(16))) short smem[2 * kQT * C::RSTR + 2 * kQT * C::TSTR];
+  __shared__ float s_lse[kQT], s_delta[kQT];
+  short* Qr = smem;                          // [32][RSTR]
+  short* dOr = Qr + kQT * C::RSTR;           // [32][RSTR]
+  short* Qt = dOr + kQT * C::RSTR;           // [32][TSTR]
+  short* dOt = Qt + kQT * C::TSTR;           // [32][TSTR]
+  const __attribute__((address_space(3))) short* Qt3 = (const __attribute__((address_space(3))) short*)Qt;
+  const __attribute__((address_space(3))) short* dOt3 = (const __attribute__((address_space(3))) short*)dOt;
+
+  const int n_kb = (Sk + kKB - 1) / kKB;
+  const int kb = (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int group = Hq / Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  const int kw = kb * kKB + wave * 32;  // this wave's first key
+  const int key = kw + r;               // this lane's key
+  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+
+  F kf[C::KS], vf[C::KS];
+  {
+    const int krow = min(key, Sk - 1);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      kf[s] = load_frag<F>(Kb + (int64_t)krow * D + 16 * s + 8 * h);
+      vf[s] = load_frag<F>(Vb + (int64_t)krow * D + 16 * s + 8 * h);
+    }
+  }
+  f32x16 dkacc[C::DT], dvacc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dkacc[dt][i] = 0.f;
+      dvacc[dt][i] = 0.f;
+    }
+
+  const int n_qt = (Tq + kQT - 1) / kQT;
+  const int qt_begin = CAUSAL ? (kb * kKB) / kQT : 0;
+  constexpr int LOADS = kQT * C::CH / kThreads;  // 16-B chunks per thread per tile
+
+  for (int hg = 0; hg < group; ++hg) {
+    const int hq = hk * group + hg;
+    const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* dOb = dO + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const float* Lb = LSE + ((int64_t)b * Hq + hq) * Tq;
+    const float* Db = DELTA + ((int64_t)b * Hq + hq) * Tq;
+    for (int qt = qt_begin; qt < n_qt; ++qt) {
+      const int qbase = qt * kQT;
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < LOADS; ++c) {
+        const int id = c * kThreads + tid;
+        const int row = id / C::CH, ch = id % C::CH;
+        const int qq = qbase + row;
+        uint4 xq = make_uint4(0, 0, 0, 0), xo = make_uint4(0, 0, 0, 0);
+        if (qq < Tq) {
+          xq = *reinterpret_cast<const uint4*>(Qb + (int64_t)qq * D + ch * 8);
+          xo = *reinterpret_cast<const uint4*>(dOb + (int64_t)qq * D + ch * 8);
+        }
+        *reinterpret_cast<uint4*>(Qr + row * C::RSTR + ch * 8) = xq;
+        *reinterpret_cast<uint4*>(dOr + row * C::RSTR + ch * 8) = xo;
+        *reinterpret_cast<uint4*>(Qt + row * C::TSTR + ch * 8) = xq;
+        *reinterpret_cast<uint4*>(dOt + row * C::TSTR + ch * 8) = xo;
+      }
+      if (tid < kQT) {
+        const int qq = qbase + tid;
+        s_lse[tid] = (qq < Tq) ? Lb[qq] * 1.44269504088896340736f : INFINITY;
+        s_delta[tid] = (qq < Tq) ? Db[qq] : 0.f;
+      }
+      __syncthreads();
+
+      // S = Q K^T  (rows: queries of this tile, cols: this wave's keys)
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        sacc[i] = 0.f;
+        pacc[i] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const F qa = load_frag<F>(Qr + r * C::RSTR + 16 * s + 8 * h);
+        const F oa = load_frag<F>(dOr + r * C::RSTR + 16 * s + 8 * h);
+        sacc = mfma(qa, kf[s], sacc);
+        pacc = mfma(oa, vf[s], pacc);  // dP = dO V^T
+      }
+      // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = acc_row(i, h);
+        const int qq = qbase + qr;
+        float p = exp2f(sacc[i] * scale_log2 - s_lse[qr]);
+        if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) p = 0.f;
+        sacc[i] = p;                                  // P
+        pacc[i] = p * (pacc[i] - s_delta[qr]);        // dS
+      }
+      F pf0, pf1, df0, df1;
+      pack_frag(pf0, sacc, 0);
+      pack_frag(pf1, sacc, 1);
+      pack_frag(df0, pacc, 0);
+      pack_frag(df1, pacc, 1);
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const int col0 = dt * 32 + 16 * (g & 1);
+        const F oa0 = tr_frag<F>(dOt3, 4 * h, col0, C::TSTR, l16);
+        const F oa1 = tr_frag<F>(dOt3, 16 + 4 * h, col0, C::TSTR, l16);
+        dvacc[dt] = mfma(oa0, pf0, dvacc[dt]);
+        dvacc[dt] = mfma(oa1, pf1, dvacc[dt]);
+        const F qa0 = tr_frag<F>(Qt3, 4 * h, col0, C::TSTR, l16);
+        const F qa1 = tr_frag<F>(Qt3, 16 + 4 * h, col0, C::TSTR, l16);
+        dkacc[dt] = mfma(qa0, df0, dkacc[dt]);
+        dkacc[dt] = mfma(qa1, df1, dkacc[dt]);
+      }
+    }
+  }
+
+  // dK^T / dV^T: element i of tile dt is d = dt*32 + acc_row(i,h), key = this lane's key
+  if (key < Sk) {
+    T* dkrow = dK + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+    T* dvrow = dV + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        union {
+          T v[4];
+          uint2 u;
+        } pk, pv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pk.v[e] = from_f32<T>(dkacc[dt][4 * a + e] * scale);
+          pv.v[e] = from_f32<T>(dvacc[dt][4 * a + e]);
+        }
+        *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
+        *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dQ
+// ---------------------------------------------------------------------------------------------
+constexpr int kBM = 128;
+constexpr int kBN = 64;
+
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                  const T* __restrict__ V, const T* __restrict__ dO,
+                                                                  const float* __restrict__ LSE,
+                                                                  const float* __restrict__ DELTA, T* __restrict__ dQ,
+                                                                  int Hq, int Hkv, int Tq, int Sk, float scale,
+                                                                  float scale_log2) {
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  __shared__ __attribute__((aligned(16))) short smem[2 * kBN * C::RSTR + kBN * C::TSTR];
+  short* Kr = smem;                    // [64][RSTR]  K rows (A operand of S^T)
+  short* Vr = Kr + kBN * C::RSTR;      // [64][RSTR]  V rows (A operand of dP^T)
+  short* Kt = Vr + kBN * C::RSTR;      // [64][TSTR]  K image for transposed reads (A of dQ^T)
+  const __attribute__((address_space(3))) short* Kt3 = (const __attribute__((address_space(3))) short*)Kt;
+
+  const int n_qt = (Tq + kBM - 1) / kBM;
+  const int qt = n_qt - 1 - (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hk = hq / (Hq / Hkv);
+  const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* dOb = dO + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  const int q0 = qt * kBM + wave * 32;
+  const int qi = q0 + r;
+  const int qrow = min(qi, Tq - 1);
+
+  F qf[C::KS], of[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+    of[s] = load_frag<F>(dOb + (int64_t)qrow * D + 16 * s + 8 * h);
+  }
+  const float lse2 = LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
+  const float dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
+
+  f32x16 dqacc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
+
+  int n_tiles = (Sk + kBN - 1) / kBN;
+  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
+  constexpr int LOADS = kBN * C::CH / kThreads;
+
+  for (int t = 0; t < n_tiles; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      const int kk = t * kBN + row;
+      uint4 xk = make_uint4(0, 0, 0, 0), xv = make_uint4(0, 0, 0, 0);
+      if (kk < Sk) {
+        xk = *reinterpret_cast<const uint4*>(Kb + (int64_t)kk * D + ch * 8);
+        xv = *reinterpret_cast<const uint4*>(Vb + (int64_t)kk * D + ch * 8);
+      }
+      *reinterpret_cast<uint4*>(Kr + row * C::RSTR + ch * 8) = xk;
+      *reinterpret_cast<uint4*>(Vr + row * C::RSTR + ch * 8) = xv;
+      *reinterpret_cast<uint4*>(Kt + row * C::TSTR + ch * 8) = xk;
+    }
+    __syncthreads();
+
+    f32x16 sacc[2], pacc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        sacc[kt][i] = 0.f;
+        pacc[kt][i] = 0.f;
+      }
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const F ka = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h);
+        const F va = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h);
+        sacc[kt] = mfma(ka, qf[s], sacc[kt]);  // S^T = K Q^T
+        pacc[kt] = mfma(va, of[s], pacc[kt]);  // dP^T = V dO^T
+      }
+    }
+    const int kbase = t * kBN;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = kbase + kt * 32 + acc_row(i, h);
+        float p = exp2f(sacc[kt][i] * scale_log2 - lse2);
+        if (kk >= Sk || (CAUSAL && kk > qi)) p = 0.f;
+        pacc[kt][i] = p * (pacc[kt][i] - dlt);  // dS^T
+      }
+    }
+    F df[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      pack_frag(df[kt][0], pacc[kt], 0);
+      pack_frag(df[kt][1], pacc[kt], 1);
+    }
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int col0 = dt * 32 + 16 * (g & 1);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const F ka = tr_frag<F>(Kt3, kt * 32 + 16 * s + 4 * h, col0, C::TSTR, l16);
+          dqacc[dt] = mfma(ka, df[kt][s], dqacc[dt]);  // dQ^T += K^T dS^T
+        }
+      }
+    }
+  }
+
+  if (qi < Tq) {
+    T* drow = dQ + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        union {
+          T v[4];
+          uint2 u;
+        } pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(dqacc[dt][4 * a + e] * scale);
+        *reinterpret_cast<uint2*>(drow + d) = pk.u;
+      }
+    }
+  }
+}
+
+template <typename T, int D>
+int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
+               void* dQ, void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, int causal,
+               hipStream_t s) {
+  const float sl2 = scale * 1.44269504088896340736f;
+  const int64_t rows = (int64_t)B * Hq * Tq;
+  hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                     (const T*)dO, (const T*)O, (float*)DELTA, rows);
+  dim3 g1((Sk + kKB - 1) / kKB, B * Hkv), g2((Tq + kBM - 1) / kBM, B * Hq), blk(kThreads);
+  if (causal) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                            const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, void* workspace, int B, int Hq,
+                            int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
+  if (Hq % Hkv != 0) return -2;
+  if (dtype == kBF16) {
+    if (D == 128) return launch_bwd<__hip_bfloat16, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 64) return launch_bwd<__hip_bfloat16, 64>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+  } else if (dtype == kF16) {
+    if (D == 128) return launch_bwd<__half, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 64) return launch_bwd<__half, 64>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+  }
+  return -1;
+}

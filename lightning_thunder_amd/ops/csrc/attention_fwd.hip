@@ -1,0 +1,243 @@
+// K3 flash-attention forward for CDNA4 (gfx950), bf16/fp16, head dim 64 or 128, causal or full,
+// grouped-query heads.  Replaces the reference's cuDNN/aten-flash/FA3 SDPA executors
+// (thunder/executors/{cudnn_sdpa,sdpaex,fa3ex}.py).
+//
+// Structure (see attention.h for the MFMA operand maps):
+//  * workgroup = 4 waves = 128 query rows (32 per wave), grid = (query tiles, batch*heads),
+//    heaviest causal tiles first;
+//  * per 64-key tile: K and V are staged global -> registers -> LDS (padded rows: K rows read
+//    with ds_read_b128 are conflict-free at stride 68 dwords, V rows read with
+//    ds_read_b64_tr_b16 are conflict-free at stride 80 dwords) with the next tile's global
+//    loads issued before the current tile's math (async-STAGE split, T14);
+//  * "swapped" S^T = K * Q^T: each lane owns one query, so the online-softmax row max/sum is
+//    16 register ops + one lane^32 exchange, and O^T = V^T * P^T keeps the rescale lane-local;
+//  * P^T goes from the S accumulator straight into the PV MFMA as the B operand (no LDS
+//    round trip), V^T comes from transposed LDS reads.
+// Outputs O [B,H,T,D] and LSE [B,H,T] (natural-log log-sum-exp of the scaled scores).
+#include "attention.h"
+
+using namespace lta;
+using namespace lta::attn;
+
+namespace {
+
+constexpr int kBM = 128;  // queries per workgroup
+constexpr int kBN = 64;   // keys per tile
+constexpr int kThreads = 256;
+
+template <int D> struct Cfg {
+  static constexpr int KSTR = D + 8;               // K tile row stride (elements)
+  static constexpr int VSTR = D + (D == 128 ? 32 : 32);  // V tile row stride
+  static constexpr int CH = D / 8;                 // 16-byte chunks per row
+  static constexpr int LOADS = kBN * CH / kThreads;  // chunks per thread per tile
+  static constexpr int KS = D / 16;                // MFMA k-steps over D
+  static constexpr int DT = D / 32;                // 32-wide d tiles
+};
+
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                               const T* __restrict__ V, T* __restrict__ O,
+                                                               float* __restrict__ LSE, int Hq, int Hkv, int Tq,
+                                                               int Sk, float scale_log2) {
+  using C = Cfg<D>;
+  using F = typename Frag<T>::type;
+  __shared__ __attribute__((aligned(16))) short smem[kBN * C::KSTR + kBN * C::VSTR];
+  short* Ks = smem;
+  short* Vs = smem + kBN * C::KSTR;
+  const __attribute__((address_space(3))) short* Vs3 = (const __attribute__((address_space(3))) short*)Vs;
+
+  const int n_qt = (Tq + kBM - 1) / kBM;
+  const int qt = n_qt - 1 - (int)blockIdx.x;  // heaviest (causal) tiles first
+  const int bh = blockIdx.y;
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hk = hq / (Hq / Hkv);
+  const T* Qb = Q + ((int64_t)b * Hq + hq) * Tq * D;
+  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  const int q0 = qt * kBM + wave * 32;
+  const int qi = q0 + r;  // this lane's query
+
+  // Q fragments (B operand of S^T = K Q^T): Q[qi][16s + 8h .. +7]
+  F qf[C::KS];
+  {
+    const int qrow = min(qi, Tq - 1);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+  }
+
+  f32x16 oacc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  int n_tiles = (Sk + kBN - 1) / kBN;
+  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
+
+  // register staging of one K/V tile
+  uint4 kreg[C::LOADS], vreg[C::LOADS];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < C::LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      const int key = t * kBN + row;
+      if (key < Sk) {
+        kreg[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)key * D + ch * 8);
+        vreg[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)key * D + ch * 8);
+      } else {
+        kreg[c] = make_uint4(0, 0, 0, 0);
+        vreg[c] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int c = 0; c < C::LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      *reinterpret_cast<uint4*>(Ks + row * C::KSTR + ch * 8) = kreg[c];
+      *reinterpret_cast<uint4*>(Vs + row * C::VSTR + ch * 8) = vreg[c];
+    }
+  };
+
+  if (n_tiles > 0) gload(0);
+  for (int t = 0; t < n_tiles; ++t) {
+    __syncthreads();  // previous tile fully consumed
+    lstore();
+    __syncthreads();
+    if (t + 1 < n_tiles) gload(t + 1);  // next tile's HBM traffic overlaps this tile's math
+
+    // ---- S^T = K Q^T : two 32-key sub-tiles -------------------------------------------------
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const F ka = load_frag<F>(Ks + (kt * 32 + r) * C::KSTR + 16 * s + 8 * h);
+        sacc[kt] = mfma(ka, qf[s], sacc[kt]);
+      }
+    }
+
+    // ---- scale, mask, online softmax (lane-local row = query qi) --------------------------------
+    const int kbase = t * kBN;
+    const bool need_mask = (kbase + kBN > Sk) || (CAUSAL && kbase + kBN - 1 > q0);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float v = sacc[kt][i] * scale_log2;
+        if (need_mask) {
+          const int key = kbase + kt * 32 + acc_row(i, h);
+          if (key >= Sk || (CAUSAL && key > qi)) v = -INFINITY;
+        }
+        sacc[kt][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m - m_use);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(sacc[kt][i] - m_use);
+        sacc[kt][i] = p;
+        rs += p;
+      }
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = m_new;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+
+    // ---- O^T += V^T P^T ----------------------------------------------------------------------
+    F pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      pack_frag(pf[kt][0], sacc[kt], 0);
+      pack_frag(pf[kt][1], sacc[kt], 1);
+    }
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int col0 = dt * 32 + 16 * (g & 1);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const F va = tr_frag<F>(Vs3, kt * 32 + 16 * s + 4 * h, col0, C::VSTR, l16);
+          oacc[dt] = mfma(va, pf[kt][s], oacc[dt]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: O = O^T / l ; LSE --------------------------------------------------------------
+  if (qi < Tq) {
+    const float inv = (l > 0.f) ? 1.f / l : 0.f;
+    T* orow = O + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        union {
+          T v[4];
+          uint2 u;
+        } pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(oacc[dt][4 * a + e] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = pk.u;
+      }
+    }
+    if (h == 0 && LSE != nullptr) {
+      // natural-log LSE of the scaled scores: (m + log2 l) * ln 2
+      LSE[((int64_t)b * Hq + hq) * Tq + qi] = (l > 0.f) ? (m + log2f(l)) * 0.69314718055994530942f : -INFINITY;
+    }
+  }
+}
+
+template <typename T, int D>
+int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
+           float scale, int causal, hipStream_t s) {
+  const float sl2 = scale * 1.44269504088896340736f;
+  dim3 grid((Tq + kBM - 1) / kBM, B * Hq), block(kThreads);
+  if (causal)
+    hipLaunchKernelGGL((attn_fwd_kernel<T, D, true>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
+                       (float*)lse, Hq, Hkv, Tq, Sk, sl2);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<T, D, false>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
+                       (float*)lse, Hq, Hkv, Tq, Sk, sl2);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                            int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
+  if (Hq % Hkv != 0) return -2;
+  if (dtype == kBF16) {
+    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+  } else if (dtype == kF16) {
+    if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+  }
+  return -1;
+}

@@ -8,28 +8,42 @@ from lightning_thunder_amd.models.litgpt import GPT, init_weights
 pytestmark = pytest.mark.gpu
 
 
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
 @pytest.mark.parametrize("name", ["llama2-like", "llama3-like", "gpt-neox-like"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_litgpt_fwd_bwd_gpu(name, dtype):
+    """Compiled model vs an fp32 eager reference (bf16 runs must be as accurate as bf16 eager, up to 3x)."""
     torch.manual_seed(0)
     dev = torch.device("cuda")
-    m = GPT.from_name(name).to(device=dev, dtype=dtype)
-    init_weights(m)
+    m32 = GPT.from_name(name).to(device=dev)
+    init_weights(m32)
+    m32.set_rope_cache(64, device=dev)
+    m = GPT.from_name(name).to(device=dev)
+    m.load_state_dict(m32.state_dict())
+    m = m.to(dtype)
     m.set_rope_cache(64, device=dev)
     idx = torch.randint(0, 320, (2, 64), device=dev)
     tm = thunder.jit(m)
     out = tm(idx)
-    ref = m(idx)
-    tol = 1e-4 if dtype == torch.float32 else 5e-2
-    torch.testing.assert_close(out.float(), ref.float(), atol=tol, rtol=tol)
-    g = torch.randn_like(out)
-    out.backward(g)
-    got = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    ref32 = m32(idx)
+    eager = m(idx)
+    g = torch.randn_like(ref32)
+    base_fwd = max(_rel(eager, ref32), 1e-6)
+    assert _rel(out, ref32) <= 3 * base_fwd + 1e-5, (_rel(out, ref32), base_fwd)
+    out.backward(g.to(dtype))
+    got = {n: p.grad.clone() for n, p in m.named_parameters()}
     for p in m.parameters():
         p.grad = None
-    ref.backward(g)
-    for n, p in m.named_parameters():
-        torch.testing.assert_close(got[n], p.grad.float(), atol=tol * 10, rtol=tol * 10, msg=n)
+    eager.backward(g.to(dtype))
+    eg = {n: p.grad.clone() for n, p in m.named_parameters()}
+    ref32.backward(g)
+    for n, p in m32.named_parameters():
+        base = max(_rel(eg[n], p.grad), 1e-6)
+        err = _rel(got[n], p.grad)
+        assert err <= 3 * base + 1e-5, (n, err, base)
     src = str(thunder.last_traces(tm)[-1])
     if name != "gpt-neox-like":
         assert "hip_rms_norm_fwd" in src and "hip_qkv_rope" in src and "hip_swiglu" in src
