@@ -261,7 +261,14 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                         p = seen[id(param)]
                     else:
                         p = tensorproxy(param, name=comp.make_unique_name("t_" + full))
+                        full_shape = getattr(param, "_lc_full_shape", None)
+                        if full_shape is not None:
+                            # sharded (FSDP) parameter: the model code sees the full shape; the
+                            # FSDP transform re-types the input as the local shard + all-gather.
+                            p._shape = tuple(full_shape)
+                            p.tags.add("sharded")
                         p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                        p.tags.add("parameter")
                         seen[id(param)] = p
                         prog.input_specs.append(InputSpec("param", path=full, proxy=p, module_path=mpath, attr=pname))
                         prog.param_accessors.append((m, pname, "param"))

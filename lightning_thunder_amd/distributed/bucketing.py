@@ -1,0 +1,107 @@
+"""Gradient bucketing for data parallelism (parity: reference ``thunder/distributed/bucketing.py:28-197``
+and ``thunder/distributed/transforms/ddp.py:137-320``).
+
+Runs on backward traces before claiming.  Each ``grad_sync`` marker (emitted by the VJP
+of ``synchronize``) is grouped, in production order, into buckets keyed by (process
+group, parallel type, dtype, device).  When a bucket is full it is packed into one flat
+buffer and its collective is issued *asynchronously* right there — RCCL then runs
+concurrently with the rest of the backward — and all waits + unpacks are placed just
+before the return:
+
+* REPLICATED (DDP): ``pack`` → ``all_reduce(AVG)``
+* FULLY_SHARDED (FSDP): ``pack_for_fsdp`` (interleaved: rank r's chunk holds its shard of
+  every gradient) → ``reduce_scatter(AVG)`` → ``unpack_for_fsdp``
+
+Bucket sizes default to 256 MiB: large messages saturate all 7 xGMI links per MI355X
+and 288 GB of HBM makes the staging buffers free.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+from ..core.prims import PrimIDs
+from ..core.proxies import TensorProxy, DistParallelType, Proxy
+from ..core.symbol import BoundSymbol
+from ..core.trace import TraceCtx, from_trace, tracectx, TraceProvenance
+from ..core.dtypes import itemsize
+from . import prims as dist_prims
+
+DEFAULT_BUCKET_SIZE_MB = 256.0
+
+
+def _key(b: BoundSymbol):
+    g, group, dpt, world = b.args
+    return (id(group), dpt, g.dtype, str(g.device))
+
+
+def has_grad_syncs(trace: TraceCtx) -> bool:
+    return any(b.sym is dist_prims.grad_sync for b in trace.bound_symbols)
+
+
+def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> TraceCtx:
+    if not has_grad_syncs(trace):
+        return trace
+    if bucket_size_mb is None:
+        bucket_size_mb = DEFAULT_BUCKET_SIZE_MB
+    limit = bucket_size_mb * 1024 * 1024
+    new = from_trace(trace)
+    new.bound_symbols = []
+    new.scopes = [new.bound_symbols]
+    swap: dict[str, Proxy] = {}
+    open_buckets: "OrderedDict[tuple, list]" = OrderedDict()
+    pending: list = []  # (future, bucket entries, kind)
+
+    def issue(key):
+        entries = open_buckets.pop(key)
+        grads = [b.args[0] for b in entries]
+        _, group, dpt, world = entries[0].args
+        if dpt is DistParallelType.FULLY_SHARDED:
+            if len(grads) == 1:
+                fut = dist_prims.reduce_scatter(grads[0], dist_prims.DistributedReduceOps.AVG, group, True, 0)
+                pending.append((fut, entries, "rs1"))
+            else:
+                buf = dist_prims.pack_for_fsdp(grads, world, "scatter")
+                fut = dist_prims.reduce_scatter(buf, dist_prims.DistributedReduceOps.AVG, group, True, 0)
+                pending.append((fut, entries, "rs"))
+        else:
+            if len(grads) == 1:
+                fut = dist_prims.all_reduce(grads[0], dist_prims.DistributedReduceOps.AVG, group, True, True)
+                pending.append((fut, entries, "ar1"))
+            else:
+                buf = dist_prims.pack(grads, str(key))
+                fut = dist_prims.all_reduce(buf, dist_prims.DistributedReduceOps.AVG, group, True, True)
+                pending.append((fut, entries, "ar"))
+
+    def finish():
+        for key in list(open_buckets.keys()):
+            issue(key)
+        for fut, entries, kind in pending:
+            res = dist_prims.wait(fut)
+            grads = [b.args[0] for b in entries]
+            world = entries[0].args[3]
+            if kind in ("rs1", "ar1"):
+                outs = [res]
+            elif kind == "rs":
+                outs = dist_prims.unpack_for_fsdp(res, grads, world, "scatter")
+            else:
+                outs = dist_prims.unpack(res, grads, "bucket")
+            for b, o in zip(entries, outs):
+                swap[b.output.name] = o
+
+    with tracectx(new):
+        for bsym in trace.bound_symbols:
+            if bsym.sym is dist_prims.grad_sync:
+                b = bsym.swap_proxies(swap, skip_output=True)
+                key = _key(b)
+                entries = open_buckets.setdefault(key, [])
+                entries.append(b)
+                size = sum(math.prod(e.args[0].shape) * itemsize(e.args[0].dtype) for e in entries)
+                if limit <= 0 or size >= limit:
+                    issue(key)
+                continue
+            if bsym.sym.id == PrimIDs.RETURN:
+                finish()
+            new.bound_symbols.append(bsym.swap_proxies(swap))
+    new.set_provenance(TraceProvenance(f"Gradient bucketing ({bucket_size_mb} MiB buckets)"))
+    return new

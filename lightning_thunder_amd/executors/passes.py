@@ -83,6 +83,13 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
     for ex in get_always_executors():
         if ex not in executors:
             executors.append(ex)
+    from ..distributed.bucketing import has_grad_syncs, bucket_grad_syncs
+
+    if has_grad_syncs(trace):
+        from ..common import get_compile_option
+
+        trace = bucket_grad_syncs(trace, get_compile_option("lta_bucket_size_mb", "DDP/FSDP gradient bucket size (MiB)"))
+        traces.append(trace)
     trace = dce(trace)
     traces.append(trace)
     trace = _transform_for_operator_executor_execution(trace, executors)

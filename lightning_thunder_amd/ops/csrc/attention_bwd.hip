@@ -81,7 +81,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   const int bh = blockIdx.y;
   const int b = bh / Hkv, hk = bh % Hkv;
   const int group = Hq / Hkv;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int kw = kb * kKB + wave * 32;  // this wave's first key
   const int key = kw + r;               // this lane's key
@@ -124,10 +125,12 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
         const int id = c * kThreads + tid;
         const int row = id / C::CH, ch = id % C::CH;
         const int qq = qbase + row;
-        uint4 xq = make_uint4(0, 0, 0, 0), xo = make_uint4(0, 0, 0, 0);
-        if (qq < Tq) {
-          xq = *reinterpret_cast<const uint4*>(Qb + (int64_t)qq * D + ch * 8);
-          xo = *reinterpret_cast<const uint4*>(dOb + (int64_t)qq * D + ch * 8);
+        const int qc = min(qq, Tq - 1);
+        uint4 xq = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
+        uint4 xo = *reinterpret_cast<const uint4*>(dOb + (int64_t)qc * D + ch * 8);
+        if (qq >= Tq) {
+          xq = make_uint4(0, 0, 0, 0);
+          xo = make_uint4(0, 0, 0, 0);
         }
         *reinterpret_cast<uint4*>(Qr + row * C::RSTR + ch * 8) = xq;
         *reinterpret_cast<uint4*>(dOr + row * C::RSTR + ch * 8) = xo;
@@ -160,8 +163,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       for (int i = 0; i < 16; ++i) {
         const int qr = acc_row(i, h);
         const int qq = qbase + qr;
-        float p = exp2f(sacc[i] * scale_log2 - s_lse[qr]);
-        if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) p = 0.f;
+        float p = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - s_lse[qr]);
+        p = (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) ? 0.f : p;
         sacc[i] = p;                                  // P
         pacc[i] = p * (pacc[i] - s_delta[qr]);        // dS
       }
@@ -241,7 +244,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
   const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int q0 = qt * kBM + wave * 32;
   const int qi = q0 + r;
@@ -273,10 +277,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
       const int kk = t * kBN + row;
-      uint4 xk = make_uint4(0, 0, 0, 0), xv = make_uint4(0, 0, 0, 0);
-      if (kk < Sk) {
-        xk = *reinterpret_cast<const uint4*>(Kb + (int64_t)kk * D + ch * 8);
-        xv = *reinterpret_cast<const uint4*>(Vb + (int64_t)kk * D + ch * 8);
+      const int kc = min(kk, Sk - 1);
+      uint4 xk = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
+      uint4 xv = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+      if (kk >= Sk) {
+        xk = make_uint4(0, 0, 0, 0);
+        xv = make_uint4(0, 0, 0, 0);
       }
       *reinterpret_cast<uint4*>(Kr + row * C::RSTR + ch * 8) = xk;
       *reinterpret_cast<uint4*>(Vr + row * C::RSTR + ch * 8) = xv;
@@ -308,8 +314,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kbase + kt * 32 + acc_row(i, h);
-        float p = exp2f(sacc[kt][i] * scale_log2 - lse2);
-        if (kk >= Sk || (CAUSAL && kk > qi)) p = 0.f;
+        float p = __builtin_amdgcn_exp2f(sacc[kt][i] * scale_log2 - lse2);
+        p = (kk >= Sk || (CAUSAL && kk > qi)) ? 0.f : p;
         pacc[kt][i] = p * (pacc[kt][i] - dlt);  // dS^T
       }
     }

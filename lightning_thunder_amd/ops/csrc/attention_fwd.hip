@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int q0 = qt * kBM + wave * 32;
   const int qi = q0 + r;  // this lane's query
@@ -87,13 +88,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
       const int key = t * kBN + row;
-      if (key < Sk) {
-        kreg[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)key * D + ch * 8);
-        vreg[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)key * D + ch * 8);
-      } else {
-        kreg[c] = make_uint4(0, 0, 0, 0);
-        vreg[c] = make_uint4(0, 0, 0, 0);
-      }
+      const int kc = min(key, Sk - 1);  // branch-free: clamp the address, zero the data
+      uint4 kx = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
+      uint4 vx = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+      const bool ok = key < Sk;
+      kreg[c] = ok ? kx : make_uint4(0, 0, 0, 0);
+      vreg[c] = ok ? vx : make_uint4(0, 0, 0, 0);
     }
   };
   auto lstore = [&]() {
@@ -137,9 +137,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float v = sacc[kt][i] * scale_log2;
-        if (need_mask) {
+        if (need_mask) {  // wave-uniform branch; per-element select
           const int key = kbase + kt * 32 + acc_row(i, h);
-          if (key >= Sk || (CAUSAL && key > qi)) v = -INFINITY;
+          v = (key >= Sk || (CAUSAL && key > qi)) ? -INFINITY : v;
         }
         sacc[kt][i] = v;
         mx = fmaxf(mx, v);
@@ -148,13 +148,13 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m, mx);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m - m_use);
+    const float alpha = __builtin_amdgcn_exp2f(m - m_use);
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(sacc[kt][i] - m_use);
+        const float p = __builtin_amdgcn_exp2f(sacc[kt][i] - m_use);
         sacc[kt][i] = p;
         rs += p;
       }

@@ -241,12 +241,16 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
         if b.sym.id == PrimIDs.RETURN:
             ret_bsym = b
             return
-        if bsym.sym.id == "torch.checkpoint" or BoundSymbolTag.RECOMPUTE_IN_BACKWARD in bsym.tags:
+        if bsym.sym.id == "torch.checkpoint":
             for s in bsym.subsymbols:
                 s2 = s.from_bsym(tags=set(s.tags) | {BoundSymbolTag.RECOMPUTE_IN_BACKWARD})
                 process(s2, recompute=True)
             return
+        if BoundSymbolTag.RECOMPUTE_IN_BACKWARD in bsym.tags:
+            recompute = True
         if not _is_differentiable_bsym(b):
+            if recompute:
+                b.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
             fw.bound_symbols.append(b)
             return
         candidates = _executor_grad_transforms(b, executors)

@@ -1,0 +1,78 @@
+"""Micro-benchmarks of the hand-written HIP kernels vs PyTorch-ROCm at Llama-2-7B shapes.
+
+Interleaved timing in one process (cdna_hip_programming.md §5.4 rule 24), random data.
+"""
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def timeit(fn, iters=20, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def bench_attention(results, B=1, H=32, T=4096, D=128, causal=True):
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+    q = torch.randn(B, H, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn_like(q)
+    v = torch.randn_like(q)
+    do = torch.randn_like(q)
+    flops_fwd = 4 * B * H * T * T * D / (2 if causal else 1)
+    o, lse = attn_fwd(q, k, v, causal)
+    t_fwd = timeit(lambda: attn_fwd(q, k, v, causal))
+    t_bwd = timeit(lambda: attn_bwd(do, q, k, v, o, lse, causal))
+    r = torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, causal, False)
+    t_tfwd = timeit(lambda: torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, causal, False))
+    zero = torch.empty((), dtype=torch.int64)
+    t_tbwd = timeit(lambda: torch.ops.aten._scaled_dot_product_flash_attention_backward(
+        do, q, k, v, r[0], r[1], None, None, T, T, 0.0, causal, zero, zero))
+    results["attention"] = {
+        "shape": [B, H, T, D], "causal": causal,
+        "hip_fwd_ms": t_fwd, "hip_fwd_tflops": flops_fwd / t_fwd / 1e9,
+        "hip_bwd_ms": t_bwd, "hip_bwd_tflops": 2.5 * flops_fwd / t_bwd / 1e9,
+        "torch_fwd_ms": t_tfwd, "torch_bwd_ms": t_tbwd,
+    }
+
+
+def bench_gemm(results):
+    out = {}
+    for (M, N, K) in [(4096, 12288, 4096), (4096, 4096, 4096), (4096, 11008, 4096), (4096, 4096, 11008), (4096, 32000, 4096)]:
+        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: torch.nn.functional.linear(a, w))
+        out[f"{M}x{N}x{K}"] = {"torch_ms": t, "tflops": 2 * M * N * K / t / 1e9}
+    results["gemm_hipblaslt"] = out
+
+
+def main():
+    torch.manual_seed(0)
+    results = {}
+    which = sys.argv[1:] or ["attention", "gemm"]
+    if "attention" in which:
+        bench_attention(results)
+    if "gemm" in which:
+        bench_gemm(results)
+    print(json.dumps(results, indent=1))
+
+
+if __name__ == "__main__":
+    main()
