@@ -70,7 +70,11 @@ def build_model(args, device):
     return model, cfg
 
 
-def make_optimizer(params):
+def make_optimizer(params, mode="eager"):
+    if mode == "thunder" and os.environ.get("LTA_TORCH_ADAMW") != "1":
+        from lightning_thunder_amd.optim import AdamW
+
+        return AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)  # fused multi-tensor HIP kernel
     try:
         return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
     except (RuntimeError, TypeError):
@@ -129,7 +133,7 @@ def run(args, rank, world, device, mode):
 
             fwd = DistributedDataParallel(model, device_ids=[device.index])
         params = list(model.parameters())
-    opt = make_optimizer(params)
+    opt = make_optimizer(params, mode)
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
 
@@ -183,11 +187,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # Rehearsal knobs (never used for reported numbers): several ranks on one GPU over gloo.
+    dev_index = 0 if os.environ.get("LTA_BENCH_SAME_DEVICE") == "1" else local_rank
+    backend = os.environ.get("LTA_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
-        torch.distributed.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=device)
+        else:
+            torch.distributed.init_process_group(backend)
 
     dt, cfg, mem, parallel = run(args, rank, world, device, args.mode)
     tokens = args.steps * args.mbs * args.seq * world

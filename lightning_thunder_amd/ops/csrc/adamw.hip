@@ -1,0 +1,95 @@
+// K15: multi-tensor fused AdamW for CDNA4 (one launch for every parameter of the model).
+// (reference: the benchmark's torch.optim.AdamW(fused=True), thunder/benchmarks/benchmark_litgpt.py:275-283)
+//
+// Pure HBM streaming: per element read p, g, m, v and write p, m, v (14 B/elem for bf16
+// params with bf16 state; fp32 state is supported too).  Work is cut into fixed-size chunks
+// described by a device table {tensor index, element offset}; every lane moves 16-byte
+// vectors.  Math in fp32.
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+struct TensorMeta {
+  void* p;
+  const void* g;
+  void* m;
+  void* v;
+  int64_t n;
+};
+
+constexpr int kChunk = 16384;  // elements per workgroup-chunk
+
+template <typename TP, typename TS>
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float lr, float b1, float b2,
+                                           float eps, float wd, float bc1, float bc2_sqrt) {
+  p = p * (1.f - lr * wd);
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  p = p - (lr / bc1) * (m / denom);
+}
+
+template <typename TP, typename TS>
+__global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
+                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                    float bc2_sqrt, float grad_scale) {
+  const int2 ck = chunks[blockIdx.x];
+  const TensorMeta mt = metas[ck.x];
+  const int64_t start = (int64_t)ck.y * kChunk;
+  const int64_t end = min(mt.n, start + kChunk);
+  TP* P = (TP*)mt.p;
+  const TP* G = (const TP*)mt.g;
+  TS* M = (TS*)mt.m;
+  TS* V = (TS*)mt.v;
+  constexpr int VP = Vec16<TP>::N;
+  const bool vec = ((end - start) % VP == 0) && ((uintptr_t)(P + start) % 16 == 0) && ((uintptr_t)(G + start) % 16 == 0) &&
+                   (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0);
+  if (vec) {
+    for (int64_t i = start + (int64_t)threadIdx.x * VP; i < end; i += 256 * VP) {
+      Vec16<TP> pv = load16(P + i), gv = load16(G + i);
+      Vec16<TS> mv = load16(M + i), vv = load16(V + i);
+#pragma unroll
+      for (int j = 0; j < VP; ++j) {
+        float p = to_f32(pv.v[j]), m = to_f32(mv.v[j]), v = to_f32(vv.v[j]);
+        adamw_elem<TP, TS>(p, to_f32(gv.v[j]) * grad_scale, m, v, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+        pv.v[j] = from_f32<TP>(p);
+        mv.v[j] = from_f32<TS>(m);
+        vv.v[j] = from_f32<TS>(v);
+      }
+      store16(P + i, pv);
+      store16(M + i, mv);
+      store16(V + i, vv);
+    }
+  } else {
+    for (int64_t i = start + threadIdx.x; i < end; i += 256) {
+      float p = to_f32(P[i]), m = to_f32(M[i]), v = to_f32(V[i]);
+      adamw_elem<TP, TS>(p, to_f32(G[i]) * grad_scale, m, v, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+      P[i] = from_f32<TP>(p);
+      M[i] = from_f32<TS>(m);
+      V[i] = from_f32<TS>(v);
+    }
+  }
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_adamw_chunk_size() { return kChunk; }
+
+// metas: device array of TensorMeta; chunks: device int2 array {tensor, chunk index}
+LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr, float b1,
+                         float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, hipStream_t stream) {
+  dim3 grid(n_chunks), block(256);
+#define LTA_L(TPt, TSt)                                                                                           \
+  hipLaunchKernelGGL((adamw_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas, (const int2*)chunks, \
+                     lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale)
+  if (pdtype == kBF16 && sdtype == kBF16) LTA_L(__hip_bfloat16, __hip_bfloat16);
+  else if (pdtype == kBF16 && sdtype == kF32) LTA_L(__hip_bfloat16, float);
+  else if (pdtype == kF16 && sdtype == kF16) LTA_L(__half, __half);
+  else if (pdtype == kF16 && sdtype == kF32) LTA_L(__half, float);
+  else if (pdtype == kF32 && sdtype == kF32) LTA_L(float, float);
+  else return -1;
+#undef LTA_L
+  return (int)hipGetLastError();
+}

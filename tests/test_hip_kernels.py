@@ -139,3 +139,25 @@ def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
     for got, want, name in ((dq, qf.grad, "dq"), (dk, kf.grad, "dk"), (dv, vf.grad, "dv")):
         err = ((got.float() - want).norm() / want.norm()).item()
         assert err < (2e-2 if dtype == torch.bfloat16 else 5e-3), (name, err)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_fused_adamw_matches_torch(dtype):
+    from lightning_thunder_amd.optim import AdamW
+
+    torch.manual_seed(0)
+    shapes = [(33,), (128, 64), (7, 5, 3), (4096,)]
+    ps = [torch.randn(s, device="cuda", dtype=dtype, requires_grad=True) for s in shapes]
+    qs = [p.detach().clone().float().requires_grad_(True) for p in ps]
+    o1 = AdamW(ps, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, state_dtype=torch.float32)
+    o2 = torch.optim.AdamW(qs, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+    for _ in range(3):
+        for p, q in zip(ps, qs):
+            g = torch.randn_like(q)
+            p.grad = g.to(dtype)
+            q.grad = g.to(dtype).float()
+        o1.step()
+        o2.step()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    for p, q in zip(ps, qs):
+        torch.testing.assert_close(p.float(), q, atol=tol, rtol=tol)
