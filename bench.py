@@ -94,6 +94,10 @@ def run(args, rank, world, device, mode):
         if args.executors:
             kwargs["executors"] = args.executors.split(",")
         transforms = []
+        if args.hipgraph:
+            from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
+
+            transforms.append(HipGraphTransform())
         if args.fp8:
             from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
 
@@ -119,11 +123,6 @@ def run(args, rank, world, device, mode):
             from lightning_thunder_amd.distributed import ddp
 
             jm = ddp(jm)
-        if args.hipgraph:
-            from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
-            from lightning_thunder_amd.core.transforms import add_transform
-
-            jm = add_transform(jm, transform=HipGraphTransform())
         fwd = jm
         params = list(jm.parameters())
     else:

@@ -1,0 +1,1048 @@
+"""hipfuse code generator: fusion region (a list of prims) -> one gfx950 HIP kernel (K1).
+
+This replaces what nvFuser does for the reference (``thunder/executors/nvfuserex_impl.py``:
+translate a region's prims into a FusionDefinition, ``:301-412``; JIT and launch, ``:526-577``).
+The design is CDNA4-first rather than a translation:
+
+* Every value of a region is described by a *map* from its dims to the dims of the
+  region's iteration **domain** (the largest elementwise shape).  Broadcasts, unit-dim
+  reshapes/squeezes and keepdim reductions are therefore free: they only change maps.
+  External tensors are read through per-domain-dim strides that are baked into the
+  source as constants (shapes are static in a trace; strides are specialised per call
+  signature), so every index computation is a multiply-shift, never a runtime divide.
+* **Pointwise mode** (no reduction): a grid-stride loop in which every lane owns ``VEC``
+  consecutive elements of the innermost dim -> 16-byte global loads/stores (8 x bf16),
+  broadcast operands along the innermost dim are loaded once as scalars.
+* **Row mode** (reductions over the trailing dims, e.g. softmax / layer_norm / rms_norm
+  decompositions): ``T`` in {64,128,256} lanes per row, ``256/T`` rows per workgroup.
+  Each dependent reduction level is one pass over the row (recomputing its cone from
+  global memory, which stays L2-resident for a row), combined with 64-lane
+  ``__shfl_xor`` butterflies and (for T>64) a 4-slot LDS exchange; values that do not
+  vary along the reduced dims are hoisted to row scope and computed once.
+* Low-precision values live in fp32 registers and are rounded to bf16/fp16 exactly where
+  the trace produces a bf16/fp16 tensor, so results are bit-identical to op-by-op
+  execution up to fp32 reassociation in reductions.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from ..core.prims import PrimIDs
+from ..core.proxies import TensorProxy, NumberProxy, Proxy, pyval
+
+# -----------------------------------------------------------------------------------------
+# dtype tables
+# -----------------------------------------------------------------------------------------
+_CTYPE = {
+    torch.float32: "float",
+    torch.bfloat16: "float",
+    torch.float16: "float",
+    torch.float64: "double",
+    torch.bool: "bool",
+    torch.int8: "int",
+    torch.int16: "int",
+    torch.int32: "int",
+    torch.uint8: "int",
+    torch.int64: "long long",
+}
+_STYPE = {
+    torch.float32: "float",
+    torch.bfloat16: "unsigned short",
+    torch.float16: "_Float16",
+    torch.float64: "double",
+    torch.bool: "unsigned char",
+    torch.int8: "signed char",
+    torch.int16: "short",
+    torch.int32: "int",
+    torch.uint8: "unsigned char",
+    torch.int64: "long long",
+}
+_FLOATS = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
+_INTS = (torch.int8, torch.int16, torch.int32, torch.uint8, torch.int64)
+
+
+def supported_dtype(dt) -> bool:
+    return dt in _CTYPE
+
+
+class NotFusible(Exception):
+    pass
+
+
+# -----------------------------------------------------------------------------------------
+# Op tables: prim id -> expression builder (operands are C expressions of the compute type)
+# -----------------------------------------------------------------------------------------
+def _f(name, ct):
+    return name + "f" if ct == "float" else name
+
+
+_UNARY_FLOAT = {
+    PrimIDs.EXP: "exp", PrimIDs.EXP2: "exp2", PrimIDs.EXPM1: "expm1", PrimIDs.LOG: "log", PrimIDs.LOG1P: "log1p",
+    PrimIDs.LOG2: "log2", PrimIDs.LOG10: "log10", PrimIDs.SQRT: "sqrt", PrimIDs.RSQRT: "rsqrt", PrimIDs.SIN: "sin",
+    PrimIDs.COS: "cos", PrimIDs.TAN: "tan", PrimIDs.SINH: "sinh", PrimIDs.COSH: "cosh", PrimIDs.TANH: "tanh",
+    PrimIDs.ASIN: "asin", PrimIDs.ACOS: "acos", PrimIDs.ATAN: "atan", PrimIDs.ASINH: "asinh", PrimIDs.ACOSH: "acosh",
+    PrimIDs.ATANH: "atanh", PrimIDs.ERF: "erf", PrimIDs.ERFC: "erfc", PrimIDs.ERFINV: "erfinv", PrimIDs.LGAMMA: "lgamma",
+    PrimIDs.FLOOR: "floor", PrimIDs.CEIL: "ceil", PrimIDs.TRUNC: "trunc", PrimIDs.ROUND: "rint",
+}
+_UNARY_ANY = {PrimIDs.NEG, PrimIDs.ABS, PrimIDs.RECIPROCAL, PrimIDs.SIGN, PrimIDs.BITWISE_NOT, PrimIDs.ISFINITE,
+              PrimIDs.SIGNBIT}
+_BINARY = {PrimIDs.ADD: "+", PrimIDs.SUB: "-", PrimIDs.MUL: "*", PrimIDs.EQ: "==", PrimIDs.NE: "!=", PrimIDs.LT: "<",
+           PrimIDs.LE: "<=", PrimIDs.GT: ">", PrimIDs.GE: ">=", PrimIDs.BITWISE_AND: "&", PrimIDs.BITWISE_OR: "|",
+           PrimIDs.BITWISE_XOR: "^", PrimIDs.BITWISE_LEFT_SHIFT: "<<", PrimIDs.BITWISE_RIGHT_SHIFT: ">>"}
+_BINARY_FLOAT_ONLY = {PrimIDs.DIV, PrimIDs.POW, PrimIDs.FMOD, PrimIDs.REMAINDER, PrimIDs.ATAN2, PrimIDs.COPYSIGN}
+_BINARY_SPECIAL = {PrimIDs.MAXIMUM, PrimIDs.MINIMUM}
+REDUCTIONS = {PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD, PrimIDs.VAR_MEAN}
+ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY | _BINARY_SPECIAL | {
+    PrimIDs.WHERE, PrimIDs.CONVERT_ELEMENT_TYPE}
+VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE}
+SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL}
+
+
+def is_compute(bsym) -> bool:
+    return bsym.sym.id in ELEMENTWISE or bsym.sym.id in REDUCTIONS
+
+
+def _sq(shape):
+    return tuple(s for s in shape if s != 1)
+
+
+# -----------------------------------------------------------------------------------------
+# Planning: incremental admission of prims into a region
+# -----------------------------------------------------------------------------------------
+@dataclass
+class Plan:
+    domain: tuple | None = None
+    red: int = 0  # number of trailing reduced domain dims
+    has_reduction: bool = False
+    nodes: list = field(default_factory=list)
+    maps: dict = field(default_factory=dict)  # internal value name -> map tuple
+    arg_maps: list = field(default_factory=list)  # per node: {arg position: map} for tensor args
+
+    def copy(self) -> "Plan":
+        return Plan(self.domain, self.red, self.has_reduction, list(self.nodes), dict(self.maps),
+                    [dict(m) for m in self.arg_maps])
+
+    # --- maps ----------------------------------------------------------------------------
+    def _identity(self, shape):
+        return tuple(i if s != 1 else None for i, s in enumerate(shape))
+
+    def _row_map(self, shape):
+        """Map a row-shaped value (its non-unit dims == the non-unit row dims, in order)."""
+        if self.domain is None or self.red == 0:
+            return None
+        nrow = len(self.domain) - self.red
+        rdims = [d for d in range(nrow) if self.domain[d] != 1]
+        nz = [i for i, s in enumerate(shape) if s != 1]
+        if len(nz) != len(rdims):
+            return None
+        m = [None] * len(shape)
+        for i, d in zip(nz, rdims):
+            if shape[i] != self.domain[d]:
+                return None
+            m[i] = d
+        return tuple(m)
+
+    def _map_for_shape(self, shape):
+        """Map for a value of ``shape`` with no other information (an all-external op)."""
+        shape = tuple(shape)
+        if self.domain is None:
+            return "new"
+        if shape == self.domain:
+            return self._identity(shape)
+        return self._row_map(shape)
+
+    def _internal(self, a):
+        return isinstance(a, TensorProxy) and a.name in self.maps
+
+    def _check_dtype(self, *ts):
+        for t in ts:
+            if isinstance(t, TensorProxy) and not supported_dtype(t.dtype):
+                raise NotFusible(f"dtype {t.dtype}")
+
+    def _set_domain(self, shape):
+        self.domain = tuple(int(s) for s in shape)
+
+    # --- admission -----------------------------------------------------------------------
+    def try_add(self, bsym) -> bool:
+        snapshot = self.copy()
+        try:
+            self._add(bsym)
+            return True
+        except NotFusible:
+            self.__dict__.update(snapshot.__dict__)
+            return False
+
+    def _add(self, bsym):
+        sid = bsym.sym.id
+        if sid not in SUPPORTED:
+            raise NotFusible(str(sid))
+        outs = [o for o in bsym.flat_outs]
+        if not outs or not all(isinstance(o, TensorProxy) for o in outs):
+            raise NotFusible("non-tensor output")
+        self._check_dtype(*outs, *[a for a in bsym.flat_args if isinstance(a, TensorProxy)])
+        for o in outs:
+            if any(not isinstance(s, int) for s in o.shape):
+                raise NotFusible("symbolic shape")
+        am: dict[int, tuple] = {}
+        if sid in ELEMENTWISE:
+            self._add_elementwise(bsym, am)
+        elif sid == PrimIDs.BROADCAST_IN_DIM:
+            self._add_broadcast(bsym, am)
+        elif sid in (PrimIDs.RESHAPE, PrimIDs.SQUEEZE):
+            self._add_unit_reshape(bsym, am)
+        elif sid in REDUCTIONS:
+            self._add_reduction(bsym, am)
+        elif sid == PrimIDs.FULL:
+            out = bsym.output
+            m = self._map_for_shape(out.shape)
+            if m == "new":
+                self._set_domain(out.shape)
+                m = self._identity(out.shape)
+            if m is None:
+                raise NotFusible("full shape")
+            self.maps[out.name] = m
+        self.nodes.append(bsym)
+        self.arg_maps.append(am)
+
+    def _add_elementwise(self, bsym, am):
+        out = bsym.output
+        targs = [(i, a) for i, a in enumerate(bsym.args) if isinstance(a, TensorProxy)]
+        if bsym.sym.id in _BINARY_FLOAT_ONLY and out.dtype not in _FLOATS:
+            raise NotFusible("integer division/pow")
+        if bsym.sym.id in _UNARY_FLOAT and out.dtype not in _FLOATS:
+            raise NotFusible("float op on ints")
+        internal = [a for _, a in targs if self._internal(a)]
+        if internal:
+            m = self.maps[internal[0].name]
+            for a in internal[1:]:
+                if self.maps[a.name] != m:
+                    raise NotFusible("operands with different maps")
+        else:
+            m = self._map_for_shape(out.shape)
+            if m == "new":
+                self._set_domain(out.shape)
+                m = self._identity(out.shape)
+            if m is None:
+                raise NotFusible("shape not in domain")
+        for i, _ in targs:
+            am[i] = m
+        self.maps[out.name] = m
+
+    def _add_broadcast(self, bsym, am):
+        a, shape, bdims = bsym.args[0], tuple(bsym.args[1]), tuple(bsym.args[2])
+        out = bsym.output
+        if self._internal(a):
+            amap = self.maps[a.name]
+            if self.domain is not None and shape != self.domain and tuple(a.shape) == self.domain and not self.has_reduction \
+                    and len(shape) >= len(self.domain):
+                # domain upgrade: the whole (pointwise) region so far is re-indexed into the larger shape
+                for d, s in enumerate(self.domain):
+                    if s != 1 and shape[bdims[d]] != s:
+                        raise NotFusible("bad upgrade")
+                def remap(mp):
+                    return tuple(None if x is None else bdims[x] for x in mp)
+                self.maps = {k: remap(v) for k, v in self.maps.items()}
+                self.arg_maps = [{k: remap(v) for k, v in d.items()} for d in self.arg_maps]
+                self._set_domain(shape)
+                self.maps[out.name] = self._identity(shape)
+                return
+            om = self._map_for_shape(shape)
+            if om is None or om == "new":
+                raise NotFusible("broadcast of internal to non-domain shape")
+            # consistency: each non-broadcast dim of a keeps its domain dim
+            for i, j in enumerate(bdims):
+                if a.shape[i] != 1 and amap[i] != om[j]:
+                    raise NotFusible("inconsistent broadcast map")
+            self.maps[out.name] = om
+            return
+        om = self._map_for_shape(shape)
+        if om == "new":
+            self._set_domain(shape)
+            om = self._identity(shape)
+        if om is None:
+            raise NotFusible("broadcast of external to non-domain shape")
+        am[0] = tuple(om[bdims[i]] if a.shape[i] != 1 else None for i in range(len(a.shape)))
+        self.maps[out.name] = om
+
+    def _add_unit_reshape(self, bsym, am):
+        a, out = bsym.args[0], bsym.output
+        if _sq(a.shape) != _sq(out.shape):
+            raise NotFusible("non-unit reshape")
+        if self._internal(a):
+            amap = [x for x, s in zip(self.maps[a.name], a.shape) if s != 1]
+            om, k = [], 0
+            for s in out.shape:
+                if s != 1:
+                    om.append(amap[k])
+                    k += 1
+                else:
+                    om.append(None)
+            self.maps[out.name] = tuple(om)
+            return
+        om = self._map_for_shape(out.shape)
+        if om == "new":
+            self._set_domain(out.shape)
+            om = self._identity(out.shape)
+        if om is None:
+            raise NotFusible("reshape of external to non-domain shape")
+        onz = [x for x, s in zip(om, out.shape) if s != 1]
+        amap, k = [], 0
+        for s in a.shape:
+            if s != 1:
+                amap.append(onz[k])
+                k += 1
+            else:
+                amap.append(None)
+        am[0] = tuple(amap)
+        self.maps[out.name] = om
+
+    def _add_reduction(self, bsym, am):
+        a = bsym.args[0]
+        dims = tuple(sorted(bsym.args[1]))
+        if not isinstance(a, TensorProxy) or a.ndim == 0 or not dims:
+            raise NotFusible("reduction arg")
+        if self._internal(a):
+            if tuple(a.shape) != self.domain or self.maps[a.name] != self._identity(a.shape):
+                raise NotFusible("reduction of non-domain value")
+        else:
+            if self.domain is None:
+                self._set_domain(a.shape)
+            elif tuple(a.shape) != self.domain:
+                raise NotFusible("reduction of non-domain external")
+            am[0] = self._identity(a.shape)
+        nd, k = len(self.domain), len(dims)
+        if dims != tuple(range(nd - k, nd)):
+            raise NotFusible("non-trailing reduction")
+        if self.red and self.red != k:
+            raise NotFusible("different reduction dims")
+        rows = math.prod(self.domain[: nd - k])
+        R = math.prod(self.domain[nd - k:])
+        if rows < 128 and R > 8192:
+            raise NotFusible("too few rows for a row kernel")
+        if bsym.sym.id == PrimIDs.SUM and bsym.kwargs.get("output_dtype") not in (None, bsym.output.dtype):
+            raise NotFusible("sum output dtype")
+        if bsym.sym.id == PrimIDs.PROD and a.dtype not in _FLOATS:
+            raise NotFusible("int prod")
+        if bsym.sym.id == PrimIDs.VAR_MEAN and a.dtype not in _FLOATS:
+            raise NotFusible("int var")
+        self.red = k
+        self.has_reduction = True
+        for o in bsym.flat_outs:
+            m = self._row_map(o.shape)
+            if m is None:
+                raise NotFusible("reduction output shape")
+            self.maps[o.name] = m
+
+
+# -----------------------------------------------------------------------------------------
+# Source generation
+# -----------------------------------------------------------------------------------------
+_PREAMBLE = r"""
+__device__ __forceinline__ float bf2f(unsigned short x) { return __builtin_bit_cast(float, ((unsigned)x) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned u = __builtin_bit_cast(unsigned, f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ float hfr(float f) { return (float)(_Float16)f; }
+template <class T> __device__ __forceinline__ T nmax(T a, T b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+template <class T> __device__ __forceinline__ T nmin(T a, T b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
+__device__ __forceinline__ float pymod(float a, float b) { float r = fmodf(a, b); return (r != 0.f && ((r < 0.f) != (b < 0.f))) ? r + b : r; }
+__device__ __forceinline__ double pymod(double a, double b) { double r = fmod(a, b); return (r != 0.0 && ((r < 0.0) != (b < 0.0))) ? r + b : r; }
+template <class T> __device__ __forceinline__ T sgn(T a) { return (a != a) ? a : (T)((a > (T)0) - (a < (T)0)); }
+"""
+
+
+def _lit(v, ct: str) -> str:
+    if ct == "bool":
+        return "true" if v else "false"
+    if ct in ("int", "long long"):
+        return f"({ct})({int(v)}LL)"
+    v = float(v)
+    if math.isnan(v):
+        return "__builtin_nanf(\"\")" if ct == "float" else "__builtin_nan(\"\")"
+    if math.isinf(v):
+        s = "__builtin_inff()" if ct == "float" else "__builtin_inf()"
+        return s if v > 0 else "(-" + s + ")"
+    r = repr(v)
+    if "e" not in r and "." not in r and "inf" not in r:
+        r += ".0"
+    return r + ("f" if ct == "float" else "")
+
+
+def _rnd(dt, expr: str) -> str:
+    if dt == torch.bfloat16:
+        return f"bfr({expr})"
+    if dt == torch.float16:
+        return f"hfr({expr})"
+    if dt == torch.int8:
+        return f"(int)(signed char)({expr})"
+    if dt == torch.uint8:
+        return f"(int)(unsigned char)({expr})"
+    if dt == torch.int16:
+        return f"(int)(short)({expr})"
+    return expr
+
+
+def _load_conv(dt, x: str) -> str:
+    if dt == torch.bfloat16:
+        return f"bf2f({x})"
+    if dt == torch.bool:
+        return f"({x} != 0)"
+    return f"({_CTYPE[dt]})({x})"
+
+
+def _store_conv(dt, v: str) -> str:
+    if dt == torch.bfloat16:
+        return f"f2bf({v})"
+    return f"({_STYPE[dt]})({v})"
+
+
+@dataclass
+class TensorArg:
+    """Runtime description of one external tensor input (part of the specialisation key)."""
+    shape: tuple
+    strides: tuple
+    dtype: torch.dtype
+    align16: bool
+
+
+class KernelSource:
+    def __init__(self, name, src, grid, block, vec, mode):
+        self.name, self.src, self.grid, self.block, self.vec, self.mode = name, src, grid, block, vec, mode
+
+
+def _contig_strides(shape):
+    st, acc = [], 1
+    for s in reversed(shape):
+        st.append(acc)
+        acc *= s
+    return tuple(reversed(st))
+
+
+def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix: str = "lta_fused") -> KernelSource:
+    """``inputs``: region inputs (TensorProxy/NumberProxy), ``outputs``: TensorProxies,
+    ``targs``: input name -> TensorArg for the tensor inputs at this call signature."""
+    g = _Gen(plan, inputs, outputs, targs)
+    body, grid, block, vec, mode = g.build()
+    src = _PREAMBLE + body
+    h = hashlib.sha1(src.encode()).hexdigest()[:16]
+    name = f"{kernel_prefix}_{h}"
+    src = src.replace("__KERNEL_NAME__", name)
+    return KernelSource(name, src, grid, block, vec, mode)
+
+
+class _Gen:
+    def __init__(self, plan: Plan, inputs, outputs, targs):
+        self.p = plan
+        self.inputs = inputs
+        self.outputs = outputs
+        self.targs = targs
+        self.D = plan.domain if plan.domain is not None else ()
+        self.nd = len(self.D)
+        self.red = plan.red
+        self.tensor_inputs = [a for a in inputs if isinstance(a, TensorProxy)]
+        self.number_inputs = [a for a in inputs if not isinstance(a, TensorProxy)]
+        self.in_index = {a.name: i for i, a in enumerate(self.tensor_inputs)}
+        self.num_index = {a.name: i for i, a in enumerate(self.number_inputs)}
+        self.out_index = {o.name: i for i, o in enumerate(outputs)}
+        self.producer = {}
+        for k, b in enumerate(plan.nodes):
+            for o in b.flat_outs:
+                self.producer[o.name] = k
+        self.lines: list[str] = []
+        self.typedefs: dict[str, str] = {}
+
+    # --- analysis ---------------------------------------------------------------------------
+    def _reduced_dims(self):
+        return set(range(self.nd - self.red, self.nd)) if self.red else set()
+
+    def _analyse(self):
+        """dep[name]: value varies along the loop dims; level[name]: pass after which it exists."""
+        red = self._reduced_dims()
+        self.dep: dict[str, bool] = {}
+        self.level: dict[str, int] = {}
+        self.load_dep: dict[tuple, bool] = {}
+        for k, b in enumerate(self.p.nodes):
+            am = self.p.arg_maps[k]
+            dep, lvl = False, 0
+            for i, a in enumerate(b.args):
+                if not isinstance(a, TensorProxy):
+                    continue
+                if a.name in self.dep:
+                    dep |= self.dep[a.name]
+                    lvl = max(lvl, self.level[a.name])
+                else:
+                    m = am.get(i)
+                    d = self.red == 0 or any(x in red for x in m if x is not None)
+                    dep |= d
+            if b.sym.id in REDUCTIONS:
+                if b.sym.id == PrimIDs.VAR_MEAN:
+                    v, mu = b.output
+                    self.dep[mu.name], self.level[mu.name] = False, lvl + 1
+                    self.dep[v.name], self.level[v.name] = False, lvl + 2
+                else:
+                    self.dep[b.output.name], self.level[b.output.name] = False, lvl + 1
+                continue
+            if b.sym.id == PrimIDs.FULL:
+                dep = self.red == 0
+            for o in b.flat_outs:
+                self.dep[o.name] = dep if self.red else True
+                self.level[o.name] = lvl
+
+    # --- emission helpers ---------------------------------------------------------------------
+    def _vtype(self, stype: str, vec: int) -> str:
+        nm = "v%d_%s" % (vec, stype.replace(" ", "_"))
+        if nm not in self.typedefs:
+            size = {"float": 4, "double": 8, "unsigned short": 2, "_Float16": 2, "unsigned char": 1, "signed char": 1,
+                    "short": 2, "int": 4, "long long": 8}[stype]
+            al = min(16, size * vec)
+            self.typedefs[nm] = f"typedef {stype} {nm} __attribute__((ext_vector_type({vec}), aligned({al})));"
+        return nm
+
+    def _dstrides(self, arg: TensorArg, amap) -> list:
+        """Per-domain-dim element strides of an external tensor read through ``amap``."""
+        st = [0] * self.nd
+        for i, d in enumerate(amap):
+            if d is not None and arg.shape[i] != 1:
+                st[d] += arg.strides[i]
+        return st
+
+    def build(self):
+        self._analyse()
+        D, nd = self.D, self.nd
+        numel = math.prod(D) if D else 1
+        # choose VEC along the innermost domain dim
+        inner = D[-1] if nd else 1
+        max_item = max([t.dtype.itemsize for t in self.tensor_inputs] + [o.dtype.itemsize for o in self.outputs] + [1])
+        vec = 1
+        for v in ((8, 4, 2) if max_item <= 4 else (4, 2)):
+            if inner % v == 0:
+                vec = v
+                break
+        # every vector-loaded operand must keep 16B-compatible alignment; otherwise it gathers
+        self.vec = vec
+        big = numel >= 2**31 or any(
+            sum((s - 1) * st for s, st in zip(t.shape, t.strides)) >= 2**31 for t in self.targs.values())
+        self.IT = "unsigned long long" if big else "unsigned"
+        if self.red:
+            return self._build_row(numel)
+        return self._build_pointwise(numel)
+
+    def _decl_args(self):
+        nin, nout, ns = len(self.tensor_inputs), len(self.outputs), len(self.number_inputs)
+        fields = []
+        if nin:
+            fields.append(f"const void* in[{nin}];")
+        fields.append(f"void* out[{max(nout, 1)}];")
+        if ns:
+            fields.append(f"double s[{ns}];")
+        return "struct Args { " + " ".join(fields) + " };"
+
+    def _ptr(self, t: TensorProxy, is_out: bool) -> str:
+        if is_out:
+            i = self.out_index[t.name]
+            return f"(({_STYPE[t.dtype]}*)A.out[{i}])"
+        i = self.in_index[t.name]
+        return f"((const {_STYPE[t.dtype]}*)A.in[{i}])"
+
+    def _scalar_ref(self, a, ct: str) -> str:
+        if isinstance(a, Proxy) and not isinstance(a, TensorProxy):
+            if a.name in self.num_index:
+                return f"(({ct})A.s[{self.num_index[a.name]}])"
+            v = pyval(a)
+        else:
+            v = a
+        if ct in ("float", "double") or isinstance(v, bool):
+            return _lit(v, ct if ct != "bool" or isinstance(v, bool) else "bool")
+        if isinstance(v, float):
+            return _lit(v, "double")
+        return _lit(v, ct)
+
+    # expression for node k at vector lane "j" ("" in row scope); refs resolved via self.ref
+    def _expr(self, b, k, lane: str) -> list[tuple[str, str]]:
+        """Returns [(output name, expression)] for node ``b``."""
+        sid = b.sym.id
+        out = b.flat_outs[0]
+        ct = _CTYPE[out.dtype]
+
+        def R(i, want_ct=None):
+            a = b.args[i]
+            if isinstance(a, TensorProxy):
+                return self.ref(a, k, i, lane)
+            return self._scalar_ref(a, want_ct or ct)
+
+        if sid == PrimIDs.CONVERT_ELEMENT_TYPE:
+            a = b.args[0]
+            if not isinstance(a, TensorProxy):
+                return [(out.name, _lit(pyval(a), ct))]
+            x = R(0)
+            if out.dtype == torch.bool:
+                return [(out.name, f"({x} != 0)")]
+            return [(out.name, _rnd(out.dtype, f"({ct})({x})"))]
+        if sid == PrimIDs.WHERE:
+            cond = R(0, "bool")
+            return [(out.name, f"({cond} ? {R(1)} : {R(2)})")]
+        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE):
+            return [(out.name, R(0))]
+        if sid == PrimIDs.FULL:
+            return [(out.name, self._scalar_ref(b.args[1], ct))]
+        # operand compute type: that of the first tensor operand (prims enforce equal dtypes)
+        tin = [a for a in b.args if isinstance(a, TensorProxy)]
+        ict = _CTYPE[tin[0].dtype] if tin else ct
+        if sid in _UNARY_FLOAT:
+            return [(out.name, _rnd(out.dtype, f"{_f(_UNARY_FLOAT[sid], ict)}({R(0)})"))]
+        if sid in _UNARY_ANY:
+            x = R(0, ict)
+            if sid == PrimIDs.NEG:
+                e = f"(-{x})"
+            elif sid == PrimIDs.ABS:
+                e = f"{_f('fabs', ict)}({x})" if ict in ("float", "double") else f"({x} < 0 ? -{x} : {x})"
+            elif sid == PrimIDs.RECIPROCAL:
+                e = f"(({ict})1 / {x})"
+            elif sid == PrimIDs.SIGN:
+                e = f"sgn<{ict}>({x})"
+            elif sid == PrimIDs.BITWISE_NOT:
+                e = f"(!{x})" if ict == "bool" else f"(~{x})"
+            elif sid == PrimIDs.ISFINITE:
+                return [(out.name, f"isfinite({x})" if ict in ("float", "double") else "true")]
+            else:  # SIGNBIT
+                return [(out.name, f"signbit({x})" if ict in ("float", "double") else f"({x} < 0)")]
+            return [(out.name, _rnd(out.dtype, e))]
+        if sid in _BINARY:
+            op = _BINARY[sid]
+            x, y = R(0, ict), R(1, ict)
+            e = f"({x} {op} {y})"
+            if out.dtype == torch.bool:
+                return [(out.name, e)]
+            return [(out.name, _rnd(out.dtype, e))]
+        if sid in _BINARY_SPECIAL:
+            x, y = R(0, ict), R(1, ict)
+            fn = "nmax" if sid == PrimIDs.MAXIMUM else "nmin"
+            return [(out.name, _rnd(out.dtype, f"{fn}<{ict}>({x}, {y})"))]
+        if sid in _BINARY_FLOAT_ONLY:
+            x, y = R(0, ict), R(1, ict)
+            if sid == PrimIDs.DIV:
+                e = f"({x} / {y})"
+            elif sid == PrimIDs.POW:
+                e = f"{_f('pow', ict)}({x}, {y})"
+            elif sid == PrimIDs.FMOD:
+                e = f"{_f('fmod', ict)}({x}, {y})"
+            elif sid == PrimIDs.REMAINDER:
+                e = f"pymod({x}, {y})"
+            elif sid == PrimIDs.ATAN2:
+                e = f"{_f('atan2', ict)}({x}, {y})"
+            else:
+                e = f"{_f('copysign', ict)}({x}, {y})"
+            return [(out.name, _rnd(out.dtype, e))]
+        raise NotFusible(f"codegen: {b.sym.name}")
+
+    # --- references -------------------------------------------------------------------------
+    def ref(self, a: TensorProxy, k: int, argpos: int, lane: str) -> str:
+        if a.name in self.producer:
+            if lane and self.dep.get(a.name, True):
+                return f"v_{a.name}[{lane}]"
+            return f"r_{a.name}"
+        # external load through the node's arg map
+        amap = self.p.arg_maps[k][argpos]
+        key = (a.name, amap)
+        nm = self.load_names.get(key)
+        if nm is None:
+            nm = f"L{len(self.load_names)}"
+            self.load_names[key] = nm
+        red = self._reduced_dims()
+        dep = self.red == 0 or any(x in red for x in amap if x is not None)
+        if lane and dep:
+            return f"{nm}[{lane}]"
+        return nm
+
+    # --- pointwise kernel -------------------------------------------------------------------
+    def _emit_nodes(self, needed: set, scope: str, emitted: set, out: list, indent: str):
+        """Emit nodes whose outputs are in ``needed`` (and their cones) for ``scope`` ('vec' or 'row')."""
+        order = []
+
+        def want(name):
+            if name in emitted or name not in self.producer:
+                return
+            k = self.producer[name]
+            b = self.p.nodes[k]
+            for a in b.args:
+                if isinstance(a, TensorProxy):
+                    if a.name in self.producer:
+                        if scope == "row" or self.dep.get(a.name, True):
+                            want(a.name)
+                    # external loads are materialised when referenced
+            if k not in order:
+                order.append(k)
+            for o in b.flat_outs:
+                emitted.add(o.name)
+
+        for n in needed:
+            want(n)
+        for k in sorted(order):
+            b = self.p.nodes[k]
+            if b.sym.id in REDUCTIONS:
+                continue
+            vec_scope = scope == "vec" and self.dep.get(b.flat_outs[0].name, True)
+            self._materialize_loads(b, k, vec_scope, out, indent)
+            exprs = self._expr(b, k, "j" if vec_scope else "")
+            for name, e in exprs:
+                ct = _CTYPE[[o for o in b.flat_outs if o.name == name][0].dtype]
+                if vec_scope:
+                    out.append(f"{indent}{ct} v_{name}[{self.vec}];")
+                    out.append(f"{indent}#pragma unroll")
+                    out.append(f"{indent}for (int j = 0; j < {self.vec}; ++j) v_{name}[j] = {e};")
+                else:
+                    out.append(f"{indent}const {ct} r_{name} = {e};")
+
+    def _load_dep(self, amap) -> bool:
+        red = self._reduced_dims()
+        return self.red == 0 or any(x in red for x in amap if x is not None)
+
+    def _materialize_loads(self, b, k, vec_scope, out, indent):
+        """Emit the external loads node ``k`` references, once per scope."""
+        for i, a in enumerate(b.args):
+            if not isinstance(a, TensorProxy) or a.name in self.producer:
+                continue
+            amap = self.p.arg_maps[k][i]
+            nm = self.load_names[(a.name, amap)]
+            if self._load_dep(amap):
+                assert vec_scope, "loop-varying load referenced at row scope"
+                key = (nm, self._scope_id)
+                if key not in self.loaded:
+                    self.loaded.add(key)
+                    self._emit_load(a, amap, nm, True, out, indent)
+                continue
+            if (nm, "row") in self.loaded:
+                continue
+            if vec_scope:
+                key = (nm, self._scope_id)
+                if key not in self.loaded:
+                    self.loaded.add(key)
+                    self._emit_load(a, amap, nm, False, out, indent)
+            else:
+                self.loaded.add((nm, "row"))
+                self._emit_load(a, amap, nm, False, out, indent)
+
+    def _emit_load(self, a, amap, nm, vec_scope, out, indent):
+        ta = self.targs[a.name]
+        st = self._dstrides(ta, amap)
+        ct, sty = _CTYPE[a.dtype], _STYPE[a.dtype]
+        ptr = self._ptr(a, False)
+        for d in range(self.nd):
+            if st[d] and f"i{d}" not in self.idx_avail:
+                raise NotFusible(f"codegen: index i{d} not available for load of {a.name}")
+        off = " + ".join(f"(({self.IT})i{d} * {st[d]}u)" for d in range(self.nd) if st[d]) or "0"
+        if not vec_scope:
+            out.append(f"{indent}const {ct} {nm} = {_load_conv(a.dtype, f'{ptr}[{off}]')};")
+            return
+        V = self.vec
+        last = self.nd - 1
+        sl = st[last] if self.nd else 0
+        if sl == 0:
+            out.append(f"{indent}const {ct} {nm}_s = {_load_conv(a.dtype, f'{ptr}[{off}]')};")
+            out.append(f"{indent}{ct} {nm}[{V}];")
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {nm}_s;")
+            return
+        vec_ok = V > 1 and sl == 1 and ta.align16 and all(st[d] % V == 0 for d in range(last)) and \
+            (a.dtype.itemsize * V <= 16 or ta.align16)
+        out.append(f"{indent}{ct} {nm}[{V}];")
+        if vec_ok:
+            vt = self._vtype(sty, V)
+            out.append(f"{indent}{{ const {vt} t = *(const {vt}*)({ptr} + ({off}));")
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, 't[j]')}; }}")
+        else:
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, f'{ptr}[({off}) + ({self.IT})j * {sl}u]')};")
+
+    def _out_strides(self, o):
+        """Per-domain-dim strides of a (contiguous) output plus its guard dims."""
+        m = self.p.maps[o.name]
+        cst = _contig_strides(tuple(o.shape))
+        st = [0] * self.nd
+        for i, d in enumerate(m):
+            if d is not None and o.shape[i] != 1:
+                st[d] = cst[i]
+        guard = [d for d in range(self.nd) if self.D[d] != 1 and st[d] == 0]
+        return st, guard
+
+    def _emit_store(self, o, vec_scope, out, indent):
+        st, guard = self._out_strides(o)
+        ptr = self._ptr(o, True)
+        val = f"v_{o.name}" if (vec_scope and self.dep.get(o.name, True)) else f"r_{o.name}"
+        off = " + ".join(f"(({self.IT})i{d} * {st[d]}u)" for d in range(self.nd) if st[d]) or "0"
+        last = self.nd - 1
+        if vec_scope:
+            g = [f"i{d} == 0" for d in guard if d != last]
+        else:
+            g = [f"i{d} == 0" for d in guard if d < self.nd - self.red]
+        cond = " && ".join(g + (["rvalid"] if self.red else []))
+        if not vec_scope:
+            if self.red:
+                cond = " && ".join(["lane == 0"] + ([cond] if cond else []))
+            pre = f"if ({cond}) " if cond else ""
+            out.append(f"{indent}{pre}{ptr}[{off}] = {_store_conv(o.dtype, val)};")
+            return
+        V = self.vec
+        pre = f"if ({cond}) " if cond else ""
+        sl = st[last] if self.nd else 0
+        if self.nd and last in guard:
+            # value is constant along the innermost dim: lane 0 of the vector writes it
+            c2 = " && ".join(([cond] if cond else []) + [f"i{last} == 0"])
+            out.append(f"{indent}if ({c2}) {ptr}[{off}] = {_store_conv(o.dtype, val + '[0]' if val.startswith('v_') else val)};")
+            return
+        vec_ok = V > 1 and sl == 1
+        if vec_ok:
+            vt = self._vtype(_STYPE[o.dtype], V)
+            out.append(f"{indent}{pre}{{ {vt} t;")
+            out.append(f"{indent}#pragma unroll")
+            src = f"{val}[j]" if val.startswith("v_") else val
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) t[j] = {_store_conv(o.dtype, src)};")
+            out.append(f"{indent}*({vt}*)({ptr} + ({off})) = t; }}")
+        else:
+            src = f"{val}[j]" if val.startswith("v_") else val
+            out.append(f"{indent}{pre}{{")
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {ptr}[({off}) + ({self.IT})j * {sl}u] = {_store_conv(o.dtype, src)}; }}")
+
+    def _decompose(self, var: str, dims: list, out: list, indent: str):
+        """i{d} = index of domain dim d from the flat index ``var`` over ``dims`` (row-major)."""
+        rem = 1
+        for d in reversed(dims):
+            s = self.D[d]
+            if s == 1:
+                out.append(f"{indent}const {self.IT} i{d} = 0;")
+            elif rem == 1:
+                out.append(f"{indent}const {self.IT} i{d} = {var} % {s}u;")
+            else:
+                out.append(f"{indent}const {self.IT} i{d} = ({var} / {rem}u) % {s}u;")
+            rem *= s
+            self.idx_avail.add(f"i{d}")
+
+    def _build_pointwise(self, numel):
+        V, IT = self.vec, self.IT
+        self.load_names, self.loaded, self._scope_id = {}, set(), "vec"
+        self.idx_avail = set()
+        body: list[str] = []
+        nvec = numel // V
+        block = 256
+        grid = max(1, min((nvec + block - 1) // block, 4096 * 2))
+        ind = "    "
+        body.append(f"  for ({IT} v = ({IT})blockIdx.x * {block}u + threadIdx.x; v < {nvec}u; v += ({IT})gridDim.x * {block}u) {{")
+        body.append(f"{ind}const {IT} e = v * {V}u;")
+        self._decompose("e", list(range(self.nd)), body, ind)
+        emitted: set = set()
+        # referencing builds the load-name table lazily; pre-populate by a dry run over all nodes
+        for k, b in enumerate(self.p.nodes):
+            for i, a in enumerate(b.args):
+                if isinstance(a, TensorProxy) and a.name not in self.producer:
+                    self.ref(a, k, i, "j")
+        self._emit_nodes({o.name for o in self.outputs}, "vec", emitted, body, ind)
+        for o in self.outputs:
+            self._emit_store(o, True, body, ind)
+        body.append("  }")
+        return self._wrap(body, block), (grid, 1, 1), (block, 1, 1), V, "pointwise"
+
+    # --- row kernel ---------------------------------------------------------------------------
+    def _build_row(self, numel):
+        V, IT = self.vec, self.IT
+        nd, red = self.nd, self.red
+        rows = math.prod(self.D[: nd - red])
+        R = math.prod(self.D[nd - red:])
+        nv = (R + V - 1) // V
+        # lanes per row: enough to give each lane ~1-4 vectors; several rows share a wave when rows are short
+        T = 1
+        while T < 256 and T * 4 < nv:
+            T *= 2
+        if nv > T and T < 256:
+            T *= 2
+        T = min(T, 256)
+        RPB = 256 // T
+        W = max(1, T // 64)
+        block = 256
+        grid = (rows + RPB - 1) // RPB
+        self.load_names, self.loaded = {}, set()
+        self.idx_avail = set()
+        for k, b in enumerate(self.p.nodes):
+            for i, a in enumerate(b.args):
+                if isinstance(a, TensorProxy) and a.name not in self.producer:
+                    self.ref(a, k, i, "j")
+        body: list[str] = []
+        body.append(f"  const unsigned lane = threadIdx.x % {T}u;")
+        body.append(f"  const {IT} row = ({IT})blockIdx.x * {RPB}u + threadIdx.x / {T}u;")
+        body.append(f"  const bool rvalid = row < {rows}u;")
+        body.append(f"  const {IT} rowc = rvalid ? row : 0u;")
+        if W > 1:
+            body.append("  const unsigned wv = threadIdx.x / 64u;")
+        self._decompose("rowc", list(range(nd - red)), body, "  ")
+        row_emitted: set = set()
+        # group reductions by pass
+        passes: dict[int, list] = {}
+        for k, b in enumerate(self.p.nodes):
+            if b.sym.id in REDUCTIONS:
+                lvl = max([self.level[a.name] for a in b.args if isinstance(a, TensorProxy) and a.name in self.level] + [0])
+                passes.setdefault(lvl, []).append(k)
+                if b.sym.id == PrimIDs.VAR_MEAN:
+                    passes.setdefault(lvl + 1, []).append(("var", k))
+        final_outs = [o for o in self.outputs if self.dep.get(o.name, False)]
+        row_outs = [o for o in self.outputs if not self.dep.get(o.name, False)]
+        max_pass = max(passes) if passes else -1
+        racc = 0
+        for p in range(max_pass + 1):
+            items = passes.get(p, [])
+            if not items:
+                continue
+            self._scope_id = f"pass{p}"
+            accs = []
+            # row-scope prerequisites for this pass
+            for it in items:
+                k = it[1] if isinstance(it, tuple) else it
+                b = self.p.nodes[k]
+                a = b.args[0]
+                need = set()
+                if isinstance(a, TensorProxy) and a.name in self.producer:
+                    need |= self._row_deps(a.name)
+                if isinstance(it, tuple):
+                    need.add(b.output[1].name)
+                self._emit_row_values(need, row_emitted, body)
+            for it in items:
+                is_var = isinstance(it, tuple)
+                k = it[1] if is_var else it
+                b = self.p.nodes[k]
+                a = b.args[0]
+                act = "double" if a.dtype == torch.float64 else ("long long" if a.dtype in _INTS + (torch.bool,) else "float")
+                sid = b.sym.id
+                if sid in (PrimIDs.AMAX, PrimIDs.AMIN):
+                    act = _CTYPE[a.dtype] if a.dtype != torch.bool else "int"
+                    init = _lit(float("-inf") if sid == PrimIDs.AMAX else float("inf"), act) if act in ("float", "double") else (
+                        "(-9223372036854775807LL - 1)" if sid == PrimIDs.AMAX and act == "long long" else
+                        "9223372036854775807LL" if act == "long long" else ("(-2147483647 - 1)" if sid == PrimIDs.AMAX else "2147483647"))
+                    comb = "nmax" if sid == PrimIDs.AMAX else "nmin"
+                elif sid == PrimIDs.PROD:
+                    init, comb = _lit(1.0, act), "*"
+                else:
+                    init, comb = ("0" if act == "long long" else _lit(0.0, act)), "+"
+                accs.append((f"acc{racc}", act, init, comb, b, is_var))
+                racc += 1
+            for nm, act, init, _, _, _ in accs:
+                body.append(f"  {act} {nm} = {init};")
+            body.append(f"  for ({IT} c = ({IT})lane * {V}u; c < (rvalid ? {R}u : 0u); c += {T * V}u) {{")
+            ind = "    "
+            self.idx_avail = {x for x in self.idx_avail if int(x[1:]) < nd - red}
+            self._decompose("c", list(range(nd - red, nd)), body, ind)
+            emitted = set(row_emitted)
+            need = set()
+            for nm, act, init, comb, b, is_var in accs:
+                a = b.args[0]
+                if isinstance(a, TensorProxy) and a.name in self.producer:
+                    need.add(a.name)
+            self._emit_nodes(need, "vec", emitted, body, ind)
+            for nm, act, init, comb, b, is_var in accs:
+                a = b.args[0]
+                k = self.p.nodes.index(b)
+                x = self.ref(a, k, 0, "j")
+                self._materialize_loads(b, k, True, body, ind)
+                if is_var:
+                    mu = f"r_{b.output[1].name}"
+                    x = f"(({act})({x}) - {mu}) * (({act})({x}) - {mu})"
+                else:
+                    x = f"({act})({x})"
+                body.append(f"{ind}#pragma unroll")
+                if comb in ("+", "*"):
+                    body.append(f"{ind}for (int j = 0; j < {V}; ++j) {nm} {comb}= {x};")
+                else:
+                    body.append(f"{ind}for (int j = 0; j < {V}; ++j) {nm} = {comb}<{act}>({nm}, {x});")
+            body.append("  }")
+            # cross-lane combine
+            for nm, act, init, comb, b, is_var in accs:
+                cf = (lambda u, v: f"{u} {comb} {v}") if comb in ("+", "*") else (lambda u, v, c=comb, t=act: f"{c}<{t}>({u}, {v})")
+                for off in (32, 16, 8, 4, 2, 1):
+                    if off >= T:
+                        continue
+                    body.append(f"  {nm} = {cf(nm, f'__shfl_xor({nm}, {off}, 64)')};")
+                if W > 1:
+                    body.append(f"  {{ __shared__ {act} sm_{nm}[4]; if ((threadIdx.x & 63u) == 0u) sm_{nm}[wv] = {nm}; __syncthreads();")
+                    base = f"(threadIdx.x / {T}u) * {W}u"
+                    expr = f"sm_{nm}[{base}]"
+                    for w in range(1, W):
+                        expr = cf(expr, f"sm_{nm}[{base} + {w}u]")
+                    body.append(f"    {nm} = {expr}; __syncthreads(); }}")
+                # finalise the reduction output(s) at row scope
+                out_ct = _CTYPE[b.flat_outs[0].dtype]
+                if b.sym.id == PrimIDs.VAR_MEAN:
+                    corr = b.kwargs.get("correction", 1)
+                    if not is_var:
+                        mu = b.output[1]
+                        body.append(f"  const {_CTYPE[mu.dtype]} r_{mu.name} = {_rnd(mu.dtype, f'({nm} / ({act}){R})')};")
+                        row_emitted.add(mu.name)
+                    else:
+                        v = b.output[0]
+                        body.append(f"  const {_CTYPE[v.dtype]} r_{v.name} = {_rnd(v.dtype, f'({nm} / ({act}){max(R - pyval(corr), 0)})')};")
+                        row_emitted.add(v.name)
+                else:
+                    o = b.output
+                    body.append(f"  const {out_ct} r_{o.name} = {_rnd(o.dtype, f'({out_ct})({nm})')};")
+                    row_emitted.add(o.name)
+        # row-scope outputs
+        self._scope_id = "final_row"
+        need = {o.name for o in row_outs}
+        self._emit_row_values(need, row_emitted, body)
+        for o in row_outs:
+            self._emit_store(o, False, body, "  ")
+        if final_outs:
+            self._scope_id = "final"
+            need = set()
+            for o in final_outs:
+                need |= self._row_deps(o.name)
+            self._emit_row_values(need, row_emitted, body)
+            body.append(f"  for ({IT} c = ({IT})lane * {V}u; c < (rvalid ? {R}u : 0u); c += {T * V}u) {{")
+            ind = "    "
+            self.idx_avail = {x for x in self.idx_avail if int(x[1:]) < nd - red}
+            self._decompose("c", list(range(nd - red, nd)), body, ind)
+            emitted = set(row_emitted)
+            self._emit_nodes({o.name for o in final_outs}, "vec", emitted, body, ind)
+            for o in final_outs:
+                self._emit_store(o, True, body, ind)
+            body.append("  }")
+        return self._wrap(body, block), (grid, 1, 1), (block, 1, 1), V, f"row(T={T})"
+
+    def _row_deps(self, name) -> set:
+        """Row-scope (loop-invariant) internal values in the cone of ``name``."""
+        res, seen = set(), set()
+
+        def walk(n):
+            if n in seen or n not in self.producer:
+                return
+            seen.add(n)
+            if not self.dep.get(n, True):
+                res.add(n)
+                return
+            b = self.p.nodes[self.producer[n]]
+            for a in b.args:
+                if isinstance(a, TensorProxy):
+                    walk(a.name)
+
+        walk(name)
+        return res
+
+    def _emit_row_values(self, need: set, row_emitted: set, body: list):
+        prev = self._scope_id
+        self._scope_id = "row"
+        need = {n for n in need if n not in row_emitted}
+        if need:
+            # the row cone can contain reductions that are already finalised (in row_emitted)
+            self._emit_nodes(need, "row", row_emitted, body, "  ")
+        self._scope_id = prev
+
+    def _wrap(self, body, block):
+        head = [self._decl_args(), *self.typedefs.values(),
+                f'extern "C" __global__ void __launch_bounds__({block}) __KERNEL_NAME__(Args A) {{']
+        return "\n".join(head + body + ["}"]) + "\n"
