@@ -67,18 +67,18 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
                                                                     float scale, float scale_log2) {
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
-  __shared__ __attribute__((aligned(16))) short smem[2 * kQT * C::RSTR + 2 * kQT * C::TSTR];
-  __shared__ float s_lse[kQT], s_delta[kQT];
-  short* Qr = smem;                          // [32][RSTR]
-  short* dOr = Qr + kQT * C::RSTR;           // [32][RSTR]
-  short* Qt = dOr + kQT * C::RSTR;           // [32][TSTR]
-  short* dOt = Qt + kQT * C::TSTR;           // [32][TSTR]
-  const __attribute__((address_space(3))) short* Qt3 = (const __attribute__((address_space(3))) short*)Qt;
-  const __attribute__((address_space(3))) short* dOt3 = (const __attribute__((address_space(3))) short*)dOt;
+  // Double-buffered Q / dO tiles: the global loads of tile i+1 are issued before the MFMAs of
+  // tile i and land in the other buffer afterwards, so HBM/L2 latency hides behind compute and
+  // one barrier per tile suffices.
+  constexpr int BUF = 2 * kQT * C::RSTR + 2 * kQT * C::TSTR;
+  __shared__ __attribute__((aligned(16))) short smem[2 * BUF];
+  __shared__ float s_lse[2][kQT], s_delta[2][kQT];
 
   const int n_kb = (Sk + kKB - 1) / kKB;
-  const int kb = (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  (void)n_kb;
+  // grid = (B*Hkv, key blocks): heaviest (causal) key blocks of every head first, balanced over XCDs
+  const int kb = (int)blockIdx.y;
+  const int bh = blockIdx.x;
   const int b = bh / Hkv, hk = bh % Hkv;
   const int group = Hq / Hkv;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -108,84 +108,120 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
     }
 
   const int n_qt = (Tq + kQT - 1) / kQT;
-  const int qt_begin = CAUSAL ? (kb * kKB) / kQT : 0;
+  const int qt_begin = CAUSAL ? min((kb * kKB) / kQT, n_qt) : 0;
+  const int nq = n_qt - qt_begin;
+  const int total = group * nq;
   constexpr int LOADS = kQT * C::CH / kThreads;  // 16-B chunks per thread per tile
 
-  for (int hg = 0; hg < group; ++hg) {
-    const int hq = hk * group + hg;
+  uint4 pq[LOADS], po[LOADS];
+  float plse = 0.f, pdel = 0.f;
+  auto issue = [&](int it) {
+    const int hq = hk * group + it / nq;
+    const int qbase = (qt_begin + it % nq) * kQT;
     const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
     const T* dOb = dO + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
-    const float* Lb = LSE + ((int64_t)b * Hq + hq) * Tq;
-    const float* Db = DELTA + ((int64_t)b * Hq + hq) * Tq;
-    for (int qt = qt_begin; qt < n_qt; ++qt) {
-      const int qbase = qt * kQT;
-      __syncthreads();
 #pragma unroll
-      for (int c = 0; c < LOADS; ++c) {
-        const int id = c * kThreads + tid;
-        const int row = id / C::CH, ch = id % C::CH;
-        const int qq = qbase + row;
-        const int qc = min(qq, Tq - 1);
-        uint4 xq = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
-        uint4 xo = *reinterpret_cast<const uint4*>(dOb + (int64_t)qc * D + ch * 8);
-        if (qq >= Tq) {
-          xq = make_uint4(0, 0, 0, 0);
-          xo = make_uint4(0, 0, 0, 0);
-        }
-        *reinterpret_cast<uint4*>(Qr + row * C::RSTR + ch * 8) = xq;
-        *reinterpret_cast<uint4*>(dOr + row * C::RSTR + ch * 8) = xo;
-        *reinterpret_cast<uint4*>(Qt + row * C::TSTR + ch * 8) = xq;
-        *reinterpret_cast<uint4*>(dOt + row * C::TSTR + ch * 8) = xo;
-      }
-      if (tid < kQT) {
-        const int qq = qbase + tid;
-        s_lse[tid] = (qq < Tq) ? Lb[qq] * 1.44269504088896340736f : INFINITY;
-        s_delta[tid] = (qq < Tq) ? Db[qq] : 0.f;
-      }
-      __syncthreads();
-
-      // S = Q K^T  (rows: queries of this tile, cols: this wave's keys)
-      f32x16 sacc, pacc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        sacc[i] = 0.f;
-        pacc[i] = 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F qa = load_frag<F>(Qr + r * C::RSTR + 16 * s + 8 * h);
-        const F oa = load_frag<F>(dOr + r * C::RSTR + 16 * s + 8 * h);
-        sacc = mfma(qa, kf[s], sacc);
-        pacc = mfma(oa, vf[s], pacc);  // dP = dO V^T
-      }
-      // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = acc_row(i, h);
-        const int qq = qbase + qr;
-        float p = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - s_lse[qr]);
-        p = (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) ? 0.f : p;
-        sacc[i] = p;                                  // P
-        pacc[i] = p * (pacc[i] - s_delta[qr]);        // dS
-      }
-      F pf0, pf1, df0, df1;
-      pack_frag(pf0, sacc, 0);
-      pack_frag(pf1, sacc, 1);
-      pack_frag(df0, pacc, 0);
-      pack_frag(df1, pacc, 1);
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        const int col0 = dt * 32 + 16 * (g & 1);
-        const F oa0 = tr_frag<F>(dOt3, 4 * h, col0, C::TSTR, l16);
-        const F oa1 = tr_frag<F>(dOt3, 16 + 4 * h, col0, C::TSTR, l16);
-        dvacc[dt] = mfma(oa0, pf0, dvacc[dt]);
-        dvacc[dt] = mfma(oa1, pf1, dvacc[dt]);
-        const F qa0 = tr_frag<F>(Qt3, 4 * h, col0, C::TSTR, l16);
-        const F qa1 = tr_frag<F>(Qt3, 16 + 4 * h, col0, C::TSTR, l16);
-        dkacc[dt] = mfma(qa0, df0, dkacc[dt]);
-        dkacc[dt] = mfma(qa1, df1, dkacc[dt]);
-      }
+    for (int c = 0; c < LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      const int qc = min(qbase + row, Tq - 1);
+      pq[c] = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
+      po[c] = *reinterpret_cast<const uint4*>(dOb + (int64_t)qc * D + ch * 8);
     }
+    if (tid < kQT) {
+      const int qc = min(qbase + tid, Tq - 1);
+      plse = LSE[((int64_t)b * Hq + hq) * Tq + qc];
+      pdel = DELTA[((int64_t)b * Hq + hq) * Tq + qc];
+    }
+  };
+  auto stash = [&](int it, int buf) {
+    const int qbase = (qt_begin + it % nq) * kQT;
+    short* Qr = smem + buf * BUF;
+    short* dOr = Qr + kQT * C::RSTR;
+    short* Qt = dOr + kQT * C::RSTR;
+    short* dOt = Qt + kQT * C::TSTR;
+#pragma unroll
+    for (int c = 0; c < LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      uint4 xq = pq[c], xo = po[c];
+      if (qbase + row >= Tq) {
+        xq = make_uint4(0, 0, 0, 0);
+        xo = make_uint4(0, 0, 0, 0);
+      }
+      *reinterpret_cast<uint4*>(Qr + row * C::RSTR + ch * 8) = xq;
+      *reinterpret_cast<uint4*>(dOr + row * C::RSTR + ch * 8) = xo;
+      *reinterpret_cast<uint4*>(Qt + row * C::TSTR + ch * 8) = xq;
+      *reinterpret_cast<uint4*>(dOt + row * C::TSTR + ch * 8) = xo;
+    }
+    if (tid < kQT) {
+      const bool ok = qbase + tid < Tq;
+      s_lse[buf][tid] = ok ? plse * 1.44269504088896340736f : INFINITY;
+      s_delta[buf][tid] = ok ? pdel : 0.f;
+    }
+  };
+
+  if (total > 0) {
+    issue(0);
+    stash(0, 0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const bool more = it + 1 < total;
+    if (more) issue(it + 1);
+    const int qbase = (qt_begin + it % nq) * kQT;
+    const short* Qr = smem + buf * BUF;
+    const short* dOr = Qr + kQT * C::RSTR;
+    const __attribute__((address_space(3))) short* Qt3 =
+        (const __attribute__((address_space(3))) short*)(dOr + kQT * C::RSTR);
+    const __attribute__((address_space(3))) short* dOt3 = Qt3 + kQT * C::TSTR;
+    const float* sl = s_lse[buf];
+    const float* sd = s_delta[buf];
+
+    // S = Q K^T  (rows: queries of this tile, cols: this wave's keys)
+    f32x16 sacc, pacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sacc[i] = 0.f;
+      pacc[i] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F qa = load_frag<F>(Qr + r * C::RSTR + 16 * s + 8 * h);
+      const F oa = load_frag<F>(dOr + r * C::RSTR + 16 * s + 8 * h);
+      sacc = mfma(qa, kf[s], sacc);
+      pacc = mfma(oa, vf[s], pacc);  // dP = dO V^T
+    }
+    // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qr = acc_row(i, h);
+      const int qq = qbase + qr;
+      float p = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - sl[qr]);
+      p = (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) ? 0.f : p;
+      sacc[i] = p;                           // P
+      pacc[i] = p * (pacc[i] - sd[qr]);      // dS
+    }
+    F pf0, pf1, df0, df1;
+    pack_frag(pf0, sacc, 0);
+    pack_frag(pf1, sacc, 1);
+    pack_frag(df0, pacc, 0);
+    pack_frag(df1, pacc, 1);
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int col0 = dt * 32 + 16 * (g & 1);
+      const F oa0 = tr_frag<F>(dOt3, 4 * h, col0, C::TSTR, l16);
+      const F oa1 = tr_frag<F>(dOt3, 16 + 4 * h, col0, C::TSTR, l16);
+      dvacc[dt] = mfma(oa0, pf0, dvacc[dt]);
+      dvacc[dt] = mfma(oa1, pf1, dvacc[dt]);
+      const F qa0 = tr_frag<F>(Qt3, 4 * h, col0, C::TSTR, l16);
+      const F qa1 = tr_frag<F>(Qt3, 16 + 4 * h, col0, C::TSTR, l16);
+      dkacc[dt] = mfma(qa0, df0, dkacc[dt]);
+      dkacc[dt] = mfma(qa1, df1, dkacc[dt]);
+    }
+    if (more) stash(it + 1, buf ^ 1);
+    __syncthreads();
   }
 
   // dK^T / dV^T: element i of tile dt is d = dt*32 + acc_row(i,h), key = this lane's key
@@ -235,8 +271,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   const __attribute__((address_space(3))) short* Kt3 = (const __attribute__((address_space(3))) short*)Kt;
 
   const int n_qt = (Tq + kBM - 1) / kBM;
-  const int qt = n_qt - 1 - (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int qt = n_qt - 1 - (int)blockIdx.y;
+  const int bh = blockIdx.x;
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
   const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
@@ -270,17 +306,27 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
   constexpr int LOADS = kBN * C::CH / kThreads;
 
+  // K/V tiles are prefetched into registers one tile ahead (latency hides behind the MFMAs).
+  uint4 pk[LOADS], pv[LOADS];
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < LOADS; ++c) {
+      const int id = c * kThreads + tid;
+      const int row = id / C::CH, ch = id % C::CH;
+      const int kc = min(t * kBN + row, Sk - 1);
+      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
+      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+    }
+  };
+  if (n_tiles > 0) issue(0);
   for (int t = 0; t < n_tiles; ++t) {
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < LOADS; ++c) {
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
-      const int kk = t * kBN + row;
-      const int kc = min(kk, Sk - 1);
-      uint4 xk = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
-      uint4 xv = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
-      if (kk >= Sk) {
+      uint4 xk = pk[c], xv = pv[c];
+      if (t * kBN + row >= Sk) {
         xk = make_uint4(0, 0, 0, 0);
         xv = make_uint4(0, 0, 0, 0);
       }
@@ -289,6 +335,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
       *reinterpret_cast<uint4*>(Kt + row * C::TSTR + ch * 8) = xk;
     }
     __syncthreads();
+    if (t + 1 < n_tiles) issue(t + 1);
 
     f32x16 sacc[2], pacc[2];
 #pragma unroll
@@ -366,7 +413,7 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   const int64_t rows = (int64_t)B * Hq * Tq;
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows);
-  dim3 g1((Sk + kKB - 1) / kKB, B * Hkv), g2((Tq + kBM - 1) / kBM, B * Hq), blk(kThreads);
+  dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
   if (causal) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2);

@@ -47,8 +47,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   const __attribute__((address_space(3))) short* Vs3 = (const __attribute__((address_space(3))) short*)Vs;
 
   const int n_qt = (Tq + kBM - 1) / kBM;
-  const int qt = n_qt - 1 - (int)blockIdx.x;  // heaviest (causal) tiles first
-  const int bh = blockIdx.y;
+  // grid = (B*H, tiles): dispatch is x-fastest and round-robins workgroups over the 8 XCDs, so
+  // every XCD receives the same mix of causal tile weights and the heaviest tiles start first.
+  const int qt = n_qt - 1 - (int)blockIdx.y;
+  const int bh = blockIdx.x;
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
   const T* Qb = Q + ((int64_t)b * Hq + hq) * Tq * D;
@@ -217,7 +219,7 @@ template <typename T, int D>
 int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
            float scale, int causal, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
-  dim3 grid((Tq + kBM - 1) / kBM, B * Hq), block(kThreads);
+  dim3 grid(B * Hq, (Tq + kBM - 1) / kBM), block(kThreads);
   if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<T, D, true>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
                        (float*)lse, Hq, Hkv, Tq, Sk, sl2);

@@ -61,6 +61,23 @@ def bench_gemm(results):
         t = timeit(lambda: torch.nn.functional.linear(a, w))
         out[f"{M}x{N}x{K}"] = {"torch_ms": t, "tflops": 2 * M * N * K / t / 1e9}
     results["gemm_hipblaslt"] = out
+    # backward layouts: dgrad dY @ W, wgrad dY^T @ X; and the fused fc_1||fc_2 forward
+    out = {}
+    for (M, N, K) in [(4096, 4096, 11008), (4096, 4096, 12288), (4096, 4096, 4096), (4096, 11008, 4096)]:
+        dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: torch.matmul(dy, w))
+        out[f"dgrad {M}x{N}x{K}"] = {"torch_ms": t, "tflops": 2 * M * N * K / t / 1e9}
+    for (N, K, M) in [(11008, 4096, 4096), (12288, 4096, 4096), (4096, 11008, 4096), (4096, 4096, 4096)]:
+        dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: torch.matmul(dy.t(), x))
+        out[f"wgrad {N}x{K}x{M}"] = {"torch_ms": t, "tflops": 2 * M * N * K / t / 1e9}
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(22016, 4096, device="cuda", dtype=torch.bfloat16)
+    t = timeit(lambda: torch.nn.functional.linear(a, w))
+    out["fwd fused fc 4096x22016x4096"] = {"torch_ms": t, "tflops": 2 * 4096 * 22016 * 4096 / t / 1e9}
+    results["gemm_layouts"] = out
 
 
 def main():
