@@ -1,1 +1,2 @@
-"""Developer utilities: trace checking, profiling transforms, debug transforms."""
+"""Developer utilities: trace checking, debug/profile transforms, roctx ranges, benchmarking
+(reference ``thunder/dev_utils``)."""

@@ -115,7 +115,7 @@ wait = _make("wait", _wait_meta)
 
 
 # ---- data-parallel synchronize ------------------------------------------------------------------
-def _synchronize_meta(a, group, distparallel_type=None):
+def _synchronize_meta(a, group, distparallel_type=None, replicate_group=None):
     dpt = distparallel_type or a.distparallel_type
     if dpt is DistParallelType.FULLY_SHARDED:
         w = _world(group)
@@ -291,7 +291,7 @@ def _wait_impl(fut):
     return fut.wait()
 
 
-def _synchronize_impl(a, group, distparallel_type=None):
+def _synchronize_impl(a, group, distparallel_type=None, replicate_group=None):
     dpt = distparallel_type or getattr(a, "distparallel_type", DistParallelType.NONE)
     if dpt is DistParallelType.FULLY_SHARDED:
         return _all_gather_impl(a, group)
@@ -384,7 +384,7 @@ def _register_vjps():
     from . import get_skip_data_parallel_grad_sync
 
     @register_vjp(synchronize)
-    def _sync_vjp(a, group, distparallel_type=None):
+    def _sync_vjp(a, group, distparallel_type=None, replicate_group=None):
         dpt = distparallel_type or a.distparallel_type
         w = _world(group)
         if dpt is DistParallelType.FULLY_SHARDED:
@@ -395,7 +395,11 @@ def _register_vjps():
         def bwd(g):
             if dpt is DistParallelType.REPLICATED and get_skip_data_parallel_grad_sync():
                 return (g,)
-            return (grad_sync(g, group, dpt, w),)
+            r = grad_sync(g, group, dpt, w)
+            if replicate_group is not None and dpt is DistParallelType.FULLY_SHARDED:
+                # hybrid sharding (2-D mesh): shards are replicated over `replicate_group`
+                r = wait(all_reduce(r, DistributedReduceOps.AVG, replicate_group, True, True))
+            return (r,)
 
         return out, bwd
 

@@ -124,8 +124,10 @@ class FSDPTransform(Transform):
     """
 
     def __init__(self, process_group=None, sharding_strategy=FSDPType.ZERO2, bucketing_strategy=FSDPBucketingStrategy.NONE,
-                 bucket_size_in_mb: float = 256.0, broadcast_from: int | None = None, device=None):
+                 bucket_size_in_mb: float = 256.0, broadcast_from: int | None = None, device=None,
+                 replicate_process_group=None):
         self.process_group = process_group
+        self.replicate_process_group = replicate_process_group  # hybrid (ddp x fsdp) mesh
         self.sharding_strategy = sharding_strategy
         self.bucketing_strategy = bucketing_strategy
         self.bucket_size_in_mb = bucket_size_in_mb
@@ -158,6 +160,8 @@ class FSDPTransform(Transform):
                     if id(p) in done:
                         m._parameters[pname] = done[id(p)]
                         continue
+                    if getattr(p, "_lc_full_shape", None) is not None:
+                        continue  # already sharded (transform_module re-run by add_transform)
                     self.original_shapes[full] = p.shape
                     shard, pad = shard_tensor(p.data, rank, world)
                     newp = torch.nn.Parameter(shard, requires_grad=p.requires_grad)
@@ -185,7 +189,7 @@ class FSDPTransform(Transform):
             shard = TensorProxy(like=p, shape=shard_shape, name=computation_trace.make_unique_name(p.name + "_shard"))
             shard.tags = set(p.tags)
             new_args[p.name] = shard
-            full = dist_prims.synchronize(shard, group, DistParallelType.FULLY_SHARDED)
+            full = dist_prims.synchronize(shard, group, DistParallelType.FULLY_SHARDED, self.replicate_process_group)
             if pad:
                 full = ltorch.narrow(full, 0, 0, n)
             return full

@@ -638,7 +638,7 @@ def arange(start, end=None, step=1, *, dtype=None, device=None, layout=None, req
     if end is None:
         start, end = 0, start
     if dtype is None:
-        dtype = torch.int64 if all(isinstance(x, builtins.int) for x in (start, end, step)) else torch.get_default_dtype()
+        dtype = torch.int64 if builtins.all(isinstance(x, builtins.int) for x in (start, end, step)) else torch.get_default_dtype()
     length = builtins.max(0, math.ceil((end - start) / step))
     return prims.iota(length, start=start, step=step, device=_infer_device(device), dtype=dtype)
 

@@ -1,0 +1,113 @@
+"""Transforms, recipes/plugins and dev utilities on CPU (reference: thunder/tests/test_transforms.py,
+test_recipes.py, test_check_trace.py)."""
+import pytest
+import torch
+
+import lightning_thunder_amd as thunder
+from lightning_thunder_amd.common import DebugOptions
+
+
+def _mlp():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.ReLU(), torch.nn.Linear(8, 2))
+
+
+def test_constant_folding():
+    from lightning_thunder_amd.transforms.constant_folding import ConstantFolding
+
+    def f(x):
+        mask = torch.ones(4, 4).tril() * 2 + 1
+        return x * mask + torch.arange(4).float()
+
+    x = torch.randn(4, 4)
+    jf = thunder.jit(f, transforms=[ConstantFolding()])
+    torch.testing.assert_close(jf(x), f(x))
+    names = [b.sym.name for b in thunder.last_traces(jf)[-1].bound_symbols]
+    assert sum(n.startswith("folded_constant") for n in names) == 2
+    assert not any(n in ("torch.ones", "torch_ones", "tril", "arange") for n in names)
+
+
+def test_prune_prologue_checks():
+    from lightning_thunder_amd.transforms.prune_prologue_checks import PrunePrologueChecks, ExtractionOnlyPrologueTransform
+
+    m = _mlp()
+    jm = thunder.jit(m, transforms=[ExtractionOnlyPrologueTransform()], prune_prologue_checks=False)
+    x = torch.randn(3, 4)
+    torch.testing.assert_close(jm(x), m(x))
+    pro = thunder.last_prologue_traces(jm)[-1]
+    assert not any(b.sym.name.startswith("check_") for b in pro.bound_symbols)
+    jm2 = thunder.jit(m, transforms=[PrunePrologueChecks()], prune_prologue_checks=False)
+    jm2(x)
+    pro2 = thunder.last_prologue_traces(jm2)[-1]
+    checks = [b for b in pro2.bound_symbols if b.sym.name.startswith("check_tensor")]
+    assert len(checks) == 1  # only the user input remains guarded
+
+
+def test_check_traces_and_debug_transform():
+    from lightning_thunder_amd.dev_utils.debug_transform import DebugTransform
+    from lightning_thunder_amd.dev_utils.profile_transform import RoctxProfileTransform, ProfileTransform
+
+    seen = []
+    m = _mlp()
+    jm = thunder.jit(m, transforms=[DebugTransform(pre_callback=lambda b, *a: seen.append(b.sym.name)),
+                                    RoctxProfileTransform(), ProfileTransform(warmup_runs=0)],
+                     debug_options=DebugOptions(check_traces=True))
+    x = torch.randn(3, 4)
+    y = jm(x)
+    y.sum().backward()
+    torch.testing.assert_close(y, m(x))
+    assert "torch_linear" in seen or "linear" in " ".join(seen)
+
+
+def test_check_trace_detects_use_before_def():
+    from lightning_thunder_amd.dev_utils.check_trace import check_trace, TraceCheckError
+
+    jf = thunder.jit(lambda a: a * 2 + 1)
+    jf(torch.randn(2))
+    tr = thunder.last_traces(jf)[-1]
+    check_trace(tr)
+    bad = thunder.core.trace.from_trace(tr)
+    bad.bound_symbols = list(reversed(tr.bound_symbols[:-1])) + [tr.bound_symbols[-1]]
+    with pytest.raises(TraceCheckError):
+        check_trace(bad)
+
+
+def test_compile_with_recipe_and_plugins():
+    from lightning_thunder_amd.core.recipe import Recipe, Plugin, PluginPolicy
+    from lightning_thunder_amd.recipes import BaseRecipe, get_recipes
+    from lightning_thunder_amd.plugins import get_plugin_names, ReduceOverhead
+
+    assert "base" in get_recipes() and "reduce-overhead" in get_plugin_names()
+    m = _mlp()
+    tm = thunder.compile(m, recipe=BaseRecipe(fuser=None))
+    x = torch.randn(3, 4)
+    torch.testing.assert_close(tm(x), m(x))
+    assert isinstance(Recipe.get_for_model(m), BaseRecipe)
+
+    class Marker(Plugin):
+        policy = PluginPolicy.POST
+
+        def setup_transforms(self):
+            from lightning_thunder_amd.transforms.constant_folding import ConstantFolding
+
+            return [ConstantFolding()]
+
+    tm2 = thunder.compile(m, plugins=[Marker()])
+    torch.testing.assert_close(tm2(x), m(x))
+    assert type(ReduceOverhead().setup_transforms()[0]).__name__ == "HipGraphTransform"
+
+
+def test_materialization_from_module_init():
+    from lightning_thunder_amd.transforms.materialization import MaterializationTransform
+
+    torch.manual_seed(0)
+    ref = _mlp()
+    with torch.device("meta"):
+        m = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.ReLU(), torch.nn.Linear(8, 2))
+    torch.manual_seed(0)
+    tm = thunder.jit(m, transforms=[MaterializationTransform(device="cpu")])
+    assert not any(p.is_meta for p in tm.parameters())
+    for p, q in zip(tm.parameters(), ref.parameters()):
+        torch.testing.assert_close(p, q)
+    x = torch.randn(3, 4)
+    torch.testing.assert_close(tm(x), ref(x))
