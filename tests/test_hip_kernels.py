@@ -161,3 +161,19 @@ def test_fused_adamw_matches_torch(dtype):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     for p, q in zip(ps, qs):
         torch.testing.assert_close(p.float(), q, atol=tol, rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_nf4_dequant_kernel(dtype):
+    from lightning_thunder_amd.transforms.quantization import quantize_nf4, dequantize_nf4, nf4_linear, NF4_CODE
+
+    torch.manual_seed(0)
+    w = torch.randn(256, 512, device="cuda")
+    q, a = quantize_nf4(w)
+    got = dequantize_nf4(q, a, w.shape, dtype)
+    ref = dequantize_nf4(q.cpu(), a.cpu(), w.shape, torch.float32)
+    torch.testing.assert_close(got.float().cpu(), ref.to(dtype).float(), rtol=0, atol=0)
+    x = torch.randn(8, 512, device="cuda", dtype=dtype)
+    y = nf4_linear(x, q, a, NF4_CODE.cuda(), 256, 512, 64, None)
+    torch.testing.assert_close(y.float(), (x.float() @ ref.cuda().t()), rtol=2e-2, atol=2e-1)

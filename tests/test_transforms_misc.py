@@ -111,3 +111,79 @@ def test_materialization_from_module_init():
         torch.testing.assert_close(p, q)
     x = torch.randn(3, 4)
     torch.testing.assert_close(tm(x), ref(x))
+
+
+def test_lora_transform_trains_only_adapters():
+    from lightning_thunder_amd.transforms.qlora import LORATransform
+
+    torch.manual_seed(0)
+    m = _mlp()
+    ref = _mlp()
+    t = LORATransform(r=2, lora_alpha=4)
+    jm = thunder.jit(m, transforms=[t])
+    x = torch.randn(3, 4)
+    # lora_b starts at zero: identical to the base model
+    torch.testing.assert_close(jm(x), ref(x))
+    with torch.no_grad():
+        m[0].lora_b.normal_()
+    y = jm(x)
+    expect = ref(x) * 0
+    h = torch.nn.functional.linear(x, ref[0].weight, ref[0].bias) + (x @ m[0].lora_a.t() @ m[0].lora_b.t()) * 2.0
+    expect = torch.nn.functional.linear(torch.relu(h), ref[2].weight, ref[2].bias) + \
+        (torch.relu(h) @ m[2].lora_a.t() @ m[2].lora_b.t()) * 2.0
+    torch.testing.assert_close(y, expect)
+    y.sum().backward()
+    assert m[0].weight.grad is None and m[0].lora_a.grad is not None and m[2].lora_b.grad is not None
+    assert {"0", "2"} == t.lora_linear_names
+
+
+def test_nf4_quantization_cpu():
+    from lightning_thunder_amd.transforms.quantization import NF4LinearQuant4bit, quantize_nf4, dequantize_nf4
+
+    torch.manual_seed(0)
+    w = torch.randn(64, 128)
+    q, a = quantize_nf4(w)
+    assert q.dtype == torch.uint8 and q.numel() == w.numel() // 2 and a.numel() == w.numel() // 64
+    wd = dequantize_nf4(q, a, w.shape, torch.float32)
+    assert (wd - w).abs().max() / w.abs().max() < 0.2
+    m = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.ReLU(), torch.nn.Linear(64, 32))
+    ref = [torch.nn.functional.linear, ]
+    x = torch.randn(4, 128, requires_grad=True)
+    ref_out = m(x)
+    jm = thunder.jit(m, transforms=[NF4LinearQuant4bit(skip=())])
+    out = jm(x)
+    assert (out - ref_out).abs().max() / ref_out.abs().max() < 0.2
+    out.sum().backward()
+    assert x.grad is not None
+    assert any("nf4" in b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols)
+
+
+def test_custom_op_traced_with_autograd():
+    @torch.library.custom_op("lta_test::scaled_sin", mutates_args=())
+    def scaled_sin(x: torch.Tensor, k: float) -> torch.Tensor:
+        return torch.sin(x) * k
+
+    @scaled_sin.register_fake
+    def _(x, k):
+        return torch.empty_like(x)
+
+    def setup(ctx, inputs, output):
+        ctx.save_for_backward(inputs[0])
+        ctx.k = inputs[1]
+
+    def bwd(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * torch.cos(x) * ctx.k, None
+
+    scaled_sin.register_autograd(bwd, setup_context=setup)
+
+    def f(x):
+        return scaled_sin(x * 2, 3.0).sum()
+
+    x = torch.randn(5, requires_grad=True)
+    jf = thunder.jit(f)
+    jf(x).backward()
+    g = x.grad.clone()
+    x.grad = None
+    f(x).backward()
+    torch.testing.assert_close(g, x.grad)
