@@ -1,0 +1,201 @@
+"""ThunderFX: a ``torch.compile`` backend that hands FX graphs to the lightning_thunder_amd compiler.
+
+Reference parity: ``thunder/dynamo/{compiler,splitter,utils,report}.py`` (``ThunderCompiler``,
+``thunderfx``, ``_splitter``, ``SubgraphInfo``, ``SplitReason``).
+
+* Dynamo captures the program (handling graph breaks, guards and Python control flow); the
+  backend receives each FX ``GraphModule``.
+* ``_split`` marks every node as supported or not by *executing it symbolically*: the node's
+  target is called under this framework's tracing mode on proxies built from the node's fake
+  example values (``node.meta["example_value"]``).  Maximal runs of supported nodes become
+  submodules compiled with :func:`lightning_thunder_amd.jit` (the HIP executors run there);
+  unsupported nodes stay in the outer graph and run eagerly on PyTorch-ROCm (there is no
+  Triton/Inductor fallback on this stack by design).
+* ``thunderfx(fn)`` is the convenience wrapper; ``ThunderCompiler.subgraph_infos`` records the
+  splits and their reasons for reports (``split_report``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import enum
+import operator
+from typing import Any, Callable
+
+import torch
+from torch.fx.passes.split_module import split_module
+
+__all__ = ["ThunderCompiler", "thunderfx", "SubgraphInfo", "SplitReason", "SplitReasonType", "split_report"]
+
+
+class SplitReasonType(enum.Enum):
+    UNSUPPORTED_NODE = enum.auto()
+    EXCEPTION_PROXY_THUNDER_OP = enum.auto()
+    EXCEPTION_META_THUNDER_OP = enum.auto()
+
+
+@dataclasses.dataclass
+class SplitReason:
+    reason_type: SplitReasonType
+    info: str
+    exception: str | None = None
+
+
+@dataclasses.dataclass
+class SubgraphInfo:
+    original_graph_module: torch.fx.GraphModule
+    split_graph_module: torch.fx.GraphModule | None
+    thunder_compiled_fns: list
+    submodule_to_compiled_functions: dict
+    split_reasons: list
+
+
+_ALWAYS_EAGER = {
+    "_local_scalar_dense", "item", "tolist", "nonzero", "unique", "masked_select", "manual_seed", "set_grad_enabled",
+    "_enter_autocast", "_exit_autocast", "print",
+}
+
+
+def _target_name(node) -> str:
+    t = node.target
+    return t if isinstance(t, str) else getattr(t, "__name__", str(t))
+
+
+def _proxy_of(v, trc):
+    from ..core.proxies import tensorproxy, TensorProxy
+
+    if isinstance(v, torch.Tensor):
+        return tensorproxy(v, name=trc.make_unique_name("fx"))
+    return v
+
+
+def is_node_supported(node: torch.fx.Node) -> tuple[bool, SplitReason | None]:
+    """Symbolically runs ``node`` through the framework's torch-function dispatch on proxies."""
+    if node.op in ("placeholder", "output", "get_attr"):
+        return True, None
+    name = _target_name(node)
+    if name in _ALWAYS_EAGER:
+        return False, SplitReason(SplitReasonType.UNSUPPORTED_NODE, f"{name} needs host values / side effects")
+    if node.op == "call_module":
+        return True, None  # submodules are traced through (their own nodes were checked by dynamo's inlining)
+    from ..core.trace import TraceCtx, tracectx
+    from ..core.jit_ext import ThunderTorchFunctionMode
+
+    def example(n):
+        if isinstance(n, torch.fx.Node):
+            ev = n.meta.get("example_value", n.meta.get("val"))
+            return ev
+        return n
+
+    args = torch.fx.node.map_arg(node.args, example)
+    kwargs = torch.fx.node.map_arg(node.kwargs, example)
+    flat = torch.utils._pytree.tree_leaves((args, kwargs))
+    if any(isinstance(a, torch.SymInt) for a in flat):
+        return False, SplitReason(SplitReasonType.UNSUPPORTED_NODE, f"{name}: symbolic shapes are not supported")
+    trc = TraceCtx()
+    try:
+        with tracectx(trc):
+            pargs = torch.utils._pytree.tree_map(lambda v: _proxy_of(v, trc), args)
+            pkwargs = torch.utils._pytree.tree_map(lambda v: _proxy_of(v, trc), kwargs)
+            with ThunderTorchFunctionMode():
+                if node.op == "call_method":
+                    getattr(pargs[0], node.target)(*pargs[1:], **pkwargs)
+                else:
+                    node.target(*pargs, **pkwargs)
+    except Exception as e:  # noqa: BLE001 - any failure means "run this node eagerly"
+        return False, SplitReason(SplitReasonType.EXCEPTION_META_THUNDER_OP, f"{name} failed to trace",
+                                  exception=f"{type(e).__name__}: {e}")
+    return True, None
+
+
+def _split(gm: torch.fx.GraphModule):
+    """Partition id per node: supported runs get even ids, unsupported nodes odd ids."""
+    reasons = []
+    part = {}
+    cur = 0
+    prev_supported = None
+    for node in gm.graph.nodes:
+        if node.op in ("placeholder", "output"):
+            continue
+        ok, why = is_node_supported(node)
+        if why is not None:
+            reasons.append(why)
+        if prev_supported is None or ok != prev_supported:
+            cur += 1
+        part[node] = (cur, ok)
+        prev_supported = ok
+    return part, reasons
+
+
+class ThunderCompiler:
+    """``torch.compile(model, backend=ThunderCompiler(**jit_options))``."""
+
+    def __init__(self, **thunder_options):
+        self.thunder_options = thunder_options
+        self.subgraph_infos: list[SubgraphInfo] = []
+
+    def __call__(self, gm: torch.fx.GraphModule, sample_args):
+        from .. import jit
+
+        part, reasons = _split(gm)
+        if not part:
+            return gm
+        compiled = []
+        mapping = {}
+        if all(ok for _, ok in part.values()):
+            fn = jit(gm, **self.thunder_options)
+            compiled.append(fn)
+            self.subgraph_infos.append(SubgraphInfo(gm, None, compiled, {"whole": fn}, reasons))
+            return fn
+        split_gm = split_module(gm, None, lambda n: part[n][0], keep_original_order=True)
+        for n in split_gm.graph.nodes:
+            if n.op != "call_module":
+                continue
+            idx = int(n.target.split("_")[-1])
+            sub = getattr(split_gm, n.target)
+            supported = any(ok for (i, ok) in part.values() if i == idx)
+            if supported:
+                fn = jit(sub, **self.thunder_options)
+                setattr(split_gm, n.target, fn)
+                compiled.append(fn)
+                mapping[n.target] = fn
+        split_gm.recompile()
+        self.subgraph_infos.append(SubgraphInfo(gm, split_gm, compiled, mapping, reasons))
+        return split_gm
+
+
+class ThunderFXCompiledObject:
+    def __init__(self, fn, backend: ThunderCompiler, **compile_kwargs):
+        self._backend = backend
+        self._fn = torch.compile(fn, backend=backend, **compile_kwargs)
+
+    def __call__(self, *args, **kwargs):
+        return self._fn(*args, **kwargs)
+
+    @property
+    def subgraph_infos(self):
+        return self._backend.subgraph_infos
+
+    @property
+    def last_traces(self):
+        from .. import last_traces
+
+        return [last_traces(f) for info in self._backend.subgraph_infos for f in info.thunder_compiled_fns]
+
+
+def thunderfx(fn: Callable, /, **kwargs) -> ThunderFXCompiledObject:
+    """``torch.compile(fn, backend=ThunderCompiler(**kwargs))`` with access to the split info."""
+    torch_kw = {k: kwargs.pop(k) for k in ("dynamic", "fullgraph", "mode") if k in kwargs}
+    torch_kw.setdefault("dynamic", False)
+    return ThunderFXCompiledObject(fn, ThunderCompiler(**kwargs), **torch_kw)
+
+
+def split_report(compiled) -> str:
+    """Human-readable summary of the graph splits (reference ``thunder/dynamo/report.py``)."""
+    infos = compiled.subgraph_infos if hasattr(compiled, "subgraph_infos") else compiled
+    lines = []
+    for i, info in enumerate(infos):
+        n_nodes = sum(1 for n in info.original_graph_module.graph.nodes if n.op not in ("placeholder", "output"))
+        lines.append(f"graph {i}: {n_nodes} nodes, {len(info.thunder_compiled_fns)} thunder submodule(s)")
+        for r in info.split_reasons:
+            lines.append(f"  split: {r.reason_type.name}: {r.info}" + (f" ({r.exception})" if r.exception else ""))
+    return "\n".join(lines)
