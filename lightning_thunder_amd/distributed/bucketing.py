@@ -31,8 +31,9 @@ DEFAULT_BUCKET_SIZE_MB = 256.0
 
 
 def _key(b: BoundSymbol):
-    g, group, dpt, world = b.args
-    return (id(group), dpt, g.dtype, str(g.device))
+    g, group, dpt, world = b.args[:4]
+    rg = b.args[4] if len(b.args) > 4 else None
+    return (id(group), dpt, g.dtype, str(g.device), id(rg))
 
 
 def has_grad_syncs(trace: TraceCtx) -> bool:
@@ -55,7 +56,7 @@ def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> T
     def issue(key):
         entries = open_buckets.pop(key)
         grads = [b.args[0] for b in entries]
-        _, group, dpt, world = entries[0].args
+        _, group, dpt, world = entries[0].args[:4]
         if dpt is DistParallelType.FULLY_SHARDED:
             if len(grads) == 1:
                 fut = dist_prims.reduce_scatter(grads[0], dist_prims.DistributedReduceOps.AVG, group, True, 0)
@@ -80,6 +81,10 @@ def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> T
             res = dist_prims.wait(fut)
             grads = [b.args[0] for b in entries]
             world = entries[0].args[3]
+            rg = entries[0].args[4] if len(entries[0].args) > 4 else None
+            if rg is not None:
+                # hybrid mesh: average the reduce-scattered shards over the replica group
+                res = dist_prims.wait(dist_prims.all_reduce(res, dist_prims.DistributedReduceOps.AVG, rg, True, True))
             if kind in ("rs1", "ar1"):
                 outs = [res]
             elif kind == "rs":

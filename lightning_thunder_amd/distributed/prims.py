@@ -129,7 +129,7 @@ synchronize = _make("synchronize", _synchronize_meta)
 
 
 # ---- grad sync marker (consumed by the bucketing pass) ----------------------------------------------
-def _grad_sync_meta(g, group, distparallel_type, world_size):
+def _grad_sync_meta(g, group, distparallel_type, world_size, replicate_group=None):
     if distparallel_type is DistParallelType.FULLY_SHARDED:
         shape = list(g.shape)
         shape[0] //= world_size
@@ -395,11 +395,10 @@ def _register_vjps():
         def bwd(g):
             if dpt is DistParallelType.REPLICATED and get_skip_data_parallel_grad_sync():
                 return (g,)
-            r = grad_sync(g, group, dpt, w)
             if replicate_group is not None and dpt is DistParallelType.FULLY_SHARDED:
-                # hybrid sharding (2-D mesh): shards are replicated over `replicate_group`
-                r = wait(all_reduce(r, DistributedReduceOps.AVG, replicate_group, True, True))
-            return (r,)
+                # hybrid sharding (2-D mesh): the bucketing pass adds an all-reduce over the replicas
+                return (grad_sync(g, group, dpt, w, replicate_group),)
+            return (grad_sync(g, group, dpt, w),)
 
         return out, bwd
 

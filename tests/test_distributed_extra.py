@@ -1,0 +1,97 @@
+"""FSDP distributed checkpoint (DCP) and hybrid (ddp x fsdp) mesh tests on CPU/gloo."""
+import os
+import socket
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(8, 15), torch.nn.GELU(), torch.nn.Linear(15, 3)).double()
+
+
+def _ckpt_worker(rank, world, port, d):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import fsdp
+    from lightning_thunder_amd.distributed import checkpoint as ck
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        jm = fsdp(thunder.jit(_model()))
+        with torch.no_grad():
+            for p in jm.parameters():
+                p.mul_(1.5)
+        sd = ck.get_model_state_dict(jm, ck.StateDictOptions(full_state_dict=False))
+        ck.save(sd, os.path.join(d, "ckpt"))
+        full = ck.get_model_state_dict(jm, ck.StateDictOptions(full_state_dict=True, rank0_only=True))
+        # a fresh sharded model, loaded from the sharded checkpoint
+        jm2 = fsdp(thunder.jit(_model()))
+        sd2 = ck.get_model_state_dict(jm2, ck.StateDictOptions(full_state_dict=False))
+        ck.load(sd2, os.path.join(d, "ckpt"))
+        ck.load_model_state_dict(sd2, jm2, ck.StateDictOptions(full_state_dict=False))
+        diff = max((a - b).abs().max().item() for a, b in zip(jm.parameters(), jm2.parameters()))
+        torch.save({"diff": diff, "full_keys": sorted(full), "full_shapes": {k: tuple(v.shape) for k, v in full.items()}},
+                   os.path.join(d, f"r{rank}.pt"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_fsdp_dcp_roundtrip():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ckpt_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=False)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=False)
+    assert r0["diff"] == 0.0 and r1["diff"] == 0.0
+    assert r0["full_shapes"]["0.weight"] == (15, 8) and r1["full_keys"] == []
+
+
+def _hybrid_worker(rank, world, port, d):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.plugins import FSDP
+    from torch.distributed.device_mesh import init_device_mesh
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mesh = init_device_mesh("cpu", (2, 2), mesh_dim_names=("ddp", "fsdp"))
+        m = _model()
+        tm = thunder.compile(m, plugins=[FSDP(process_group=mesh)])
+        g = torch.Generator().manual_seed(10 + rank)
+        x = torch.randn(4, 8, generator=g, dtype=torch.float64)
+        tm(x).pow(2).mean().backward()
+        grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+        torch.save({"grads": grads}, os.path.join(d, f"r{rank}.pt"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_hybrid_mesh_fsdp_plugin():
+    from lightning_thunder_amd.distributed.transforms import shard_tensor
+
+    world = 4
+    ref = _model()
+    loss = 0
+    for r in range(world):
+        g = torch.Generator().manual_seed(10 + r)
+        loss = loss + ref(torch.randn(4, 8, generator=g, dtype=torch.float64)).pow(2).mean() / world
+    loss.backward()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_hybrid_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+    for rank, r in enumerate(res):
+        fsdp_rank = rank % 2
+        for n, p in ref.named_parameters():
+            expected, _ = shard_tensor(p.grad, fsdp_rank, 2)
+            torch.testing.assert_close(r["grads"][n], expected)

@@ -187,3 +187,40 @@ def test_custom_op_traced_with_autograd():
     x.grad = None
     f(x).backward()
     torch.testing.assert_close(g, x.grad)
+
+
+def test_examine_patterns_and_memory(capsys):
+    from lightning_thunder_amd.examine import examine, make_trace_dot, get_alloc_memory
+    from lightning_thunder_amd.core.patterns import Pattern
+
+    def f(x):
+        return torch.nn.functional.gelu(torch.special.erfcx(x) + x.sum())
+
+    assert examine(f, torch.randn(4)) is not None
+    assert "opaque" in capsys.readouterr().out
+    jf = thunder.jit(lambda x, w, b: torch.relu(torch.nn.functional.linear(x, w) + b))
+    jf(torch.randn(2, 3), torch.randn(4, 3), torch.randn(4))
+    tr = thunder.last_traces(jf)[-1]
+    p = Pattern().match(lambda b: "linear" in b.sym.name).match(lambda b: "add" in b.sym.name).match(
+        lambda b: "relu" in b.sym.name)
+    m = p(tr)
+    assert len(m) == 1 and len(m[0]) == 3
+    peak, _ = get_alloc_memory(tr)
+    assert peak > 0
+    assert make_trace_dot(tr).startswith("digraph")
+
+
+def test_numpy_language_and_langctx():
+    from lightning_thunder_amd.core.langctxs import langctx, Languages, resolve_method
+    from lightning_thunder_amd import numpy as lnp
+    from lightning_thunder_amd.core.trace import TraceCtx, tracectx
+    from lightning_thunder_amd.core.proxies import TensorProxy
+
+    with tracectx(TraceCtx()):
+        t = TensorProxy(shape=(3, 4), device="cpu", dtype=torch.float32)
+        assert lnp.size(t) == 12 and lnp.compute_len(t) == 3
+        s = lnp.add(t, 1.0)
+        assert tuple(s.shape) == (3, 4)
+    with langctx(Languages.NUMPY):
+        assert resolve_method("size") is lnp.size
+    assert resolve_method("sum") is not None
