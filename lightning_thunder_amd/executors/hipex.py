@@ -29,6 +29,98 @@ _FLOAT16ISH = (torch.bfloat16, torch.float16, torch.float32)
 
 
 # =========================================================================================
+# K2 GEMM: linear forward (+ fused epilogues) on the hand-written MFMA kernel
+# =========================================================================================
+def _linear_meta(x, w, bias=None, residual=None, act=None):
+    return TensorProxy(like=x, shape=tuple(x.shape[:-1]) + (w.shape[0],))
+
+
+def _linear_impl(x, w, bias=None, residual=None, act=None):
+    from ..ops.gemm import linear
+
+    return linear(x, w, bias, residual, act)
+
+
+hip_linear = ex.register_operator("hip_linear", meta=_linear_meta, fn=_linear_impl)
+
+
+def _linear_checker(a, w, bias=None):
+    if not _gpu(a, w, bias) or a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.ndim != 2:
+        return False
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.ndim != 1):
+        return False
+    if a.ndim < 2:
+        return False
+    M = 1
+    for s in a.shape[:-1]:
+        M *= s
+    N, K = w.shape
+    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and a.shape[-1] == K
+
+
+def _linear_exec(a, w, bias=None):
+    return hip_linear(a, w, bias)
+
+
+def _register_linear():
+    from .. import torch as ltorch
+
+    ex.register_implementation(ltorch.linear, checker=_linear_checker, execution_transform=_linear_exec)
+
+
+_register_linear()
+
+
+def _fuse_linear_epilogues(trace):
+    """``y = hip_linear(x, w, b); z = y + r`` (y used nowhere else) -> ``z = hip_linear(x, w, b, r)``:
+    the residual add runs in the GEMM's epilogue (one HBM round trip of y saved)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = trace.bound_symbols
+    uses: dict[str, int] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            uses[a.name] = uses.get(a.name, 0) + 1
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym.name not in ("torch_add", "add") or b.kwargs.get("alpha") not in (None, 1):
+            continue
+        if len(b.args) < 2 or not all(isinstance(a, TensorProxy) for a in b.args[:2]):
+            continue
+        for pos in (0, 1):
+            y, r = b.args[pos], b.args[1 - pos]
+            j = producer.get(y.name)
+            if j is None or j in drop or bsyms[j].sym is not hip_linear or uses.get(y.name, 0) != 1:
+                continue
+            lb = bsyms[j]
+            if len(lb.args) > 3 and lb.args[3] is not None:
+                continue
+            if tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype or tuple(b.output.shape) != tuple(y.shape):
+                continue
+            bias = lb.args[2] if len(lb.args) > 2 else lb.kwargs.get("bias")
+            nb = hip_linear.bind(lb.args[0], lb.args[1], bias, r, output=b.output)
+            nb = ex.bind_call_ctx(nb)
+            replace[i] = nb
+            drop.add(j)
+            break
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} residual add(s) fused into GEMM epilogues"))
+    return new
+
+
+ex.post_claim_pass = _fuse_linear_epilogues
+
+
+# =========================================================================================
 # K4 RMSNorm
 # =========================================================================================
 def _rms_fwd_meta(x, weight, eps):

@@ -103,6 +103,15 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
     trace = _transform_for_operator_executor_execution(trace, [e for e in executors if not isinstance(e, FusionExecutor)])
     trace = dce(trace)
     traces.append(trace)
+    # executor-specific rewrites of the claimed program (e.g. hipex folds elementwise epilogues
+    # into its GEMM)
+    for ex in executors:
+        hook = getattr(ex, "post_claim_pass", None)
+        if hook is not None:
+            new = hook(trace)
+            if new is not trace:
+                trace = new
+                traces.append(trace)
     return traces
 
 

@@ -1,0 +1,220 @@
+// K2: bf16 GEMM with fused epilogues on CDNA4 MFMA, C[M,N] = act(alpha * A[M,K] . B[N,K]^T + bias) (+ R).
+// (reference: cuBLAS(Lt) behind ATen linear, thunder/executors/torchex.py; nvFuser matmul epilogues)
+//
+// "NT" layout = nn.Linear forward: activations A [M,K] and weights B [N,K] both K-contiguous.
+// Geometry (cdna_hip_programming.md §5, 256² template):
+//   * 256x256 output tile per workgroup, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N);
+//     each wave owns 128x64 = 8x4 tiles of v_mfma_f32_16x16x32_bf16 (128 fp32 accumulators/lane).
+//   * A and B tiles are staged global -> LDS with global_load_lds_dwordx4 (16 B per lane, no VGPR
+//     round trip) into two LDS buffers (2 x 64 KiB): the loads of tile t+1 are in flight while
+//     tile t is multiplied.
+//   * LDS image: 128-B rows (64 bf16 of K); the 16-B chunk c of row r is stored at chunk c ^ (r & 7).
+//     glds writes LDS lane-linearly, so the swizzle is applied to each lane's *global* source
+//     address; fragment reads (ds_read_b128, 16 rows x 16 B per lane group) then hit 16 distinct
+//     16-B slots of the 256-B bank row: conflict-free.
+//   * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous range of tiles), then
+//     groups of 8 tile-rows so the 32 CUs of an XCD share A rows and B columns in their L2.
+//   * Epilogue: alpha, bias[col], activation in fp32 registers -> bf16 into a swizzled LDS image
+//     -> 16-B row-contiguous global stores, with the residual added there (same rounding points
+//     as ATen's linear followed by add).
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int TILE_BYTES = BM * BK * 2;      // 32 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // A + B
+
+enum Act : int { kNone = 0, kGeluTanh = 1, kGeluErf = 2, kSilu = 3, kRelu = 4 };
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+  if constexpr (ACT == kGeluTanh) {
+    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  } else if constexpr (ACT == kGeluErf) {
+    return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+  } else if constexpr (ACT == kSilu) {
+    return x / (1.f + __expf(-x));
+  } else if constexpr (ACT == kRelu) {
+    return x > 0.f ? x : 0.f;
+  } else {
+    return x;
+  }
+}
+
+__device__ __forceinline__ int xcd_tile(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// stage one BMxBK (A) and one BNxBK (B) tile into LDS buffer `sbase`
+__device__ __forceinline__ void stage_tile(const __hip_bfloat16* __restrict__ A, const __hip_bfloat16* __restrict__ B,
+                                           int lda, int ldb, int m0, int n0, int k0, char* sbase, int wave, int lane) {
+  const int r = lane >> 3, p = lane & 7;
+  const int c = p ^ r;  // swizzled source chunk (row & 7 == r: chunks start at multiples of 8 rows)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 8 + wave;  // 8 rows per wave-instruction
+    const int row = chunk * 8 + r;
+    const __hip_bfloat16* ga = A + (int64_t)(m0 + row) * lda + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)ga, (lds_void*)(sbase + chunk * 1024), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 8 + wave;
+    const int row = chunk * 8 + r;
+    const __hip_bfloat16* gb = B + (int64_t)(n0 + row) * ldb + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)gb, (lds_void*)(sbase + TILE_BYTES + chunk * 1024), 16, 0, 0);
+  }
+}
+
+template <int ACT, bool BIAS, bool RES>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_kernel(const __hip_bfloat16* __restrict__ A,
+                                                              const __hip_bfloat16* __restrict__ B,
+                                                              __hip_bfloat16* __restrict__ C,
+                                                              const __hip_bfloat16* __restrict__ bias,
+                                                              const __hip_bfloat16* __restrict__ R, int M, int N, int K,
+                                                              int lda, int ldb, int ldc, int ldr, float alpha) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // tile assignment
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) stage_tile(A, B, lda, ldb, m0, n0, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int row = wm * 128 + m * 16 + fr;
+        af[m] = *reinterpret_cast<const bf16x8*>(cur + row * 128 + ((c ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row = wn * 64 + n * 16 + fr;
+        bfr[n] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + row * 128 + ((c ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: registers -> swizzled bf16 LDS image (per wave 128 x 64) -> 16-B stores ----
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;  // column within the wave tile
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 64 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        float v = acc[m][n][j] * alpha + bv;
+        v = act_fn<ACT>(v);
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) = __float2bfloat16(v);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS image is complete
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+    const int64_t grow = m0 + wm * 128 + row;
+    const int gcol = n0 + wn * 64 + ch * 8;
+    if constexpr (RES) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
+      v = o.u;
+    }
+    *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = v;
+  }
+}
+
+template <int ACT>
+int launch_act(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
+               int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_GEMM(BI, RE)                                                                                              \
+  hipLaunchKernelGGL((gemm_nt_bf16_kernel<ACT, BI, RE>), grid, block, 0, s, (const __hip_bfloat16*)A,                 \
+                     (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                       \
+                     (const __hip_bfloat16*)R, M, N, K, lda, ldb, ldc, ldr, alpha)
+  if (bias && R) LTA_GEMM(true, true);
+  else if (bias) LTA_GEMM(true, false);
+  else if (R) LTA_GEMM(false, true);
+  else LTA_GEMM(false, false);
+#undef LTA_GEMM
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_gemm_tile_m() { return BM; }
+LTA_EXPORT int lta_gemm_tile_n() { return BN; }
+LTA_EXPORT int lta_gemm_tile_k() { return BK; }
+
+// C = act(alpha * A @ B^T + bias) + R ; A [M,K] (lda), B [N,K] (ldb), C/R [M,N] (ldc/ldr), all bf16.
+// Requires M % 256 == 0, N % 256 == 0, K % 64 == 0 and 16-B aligned rows (checked by the caller).
+LTA_EXPORT int lta_gemm_nt_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                                int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, hipStream_t stream) {
+  if (M % BM || N % BN || K % BK) return -2;
+  switch (act) {
+    case kNone: return launch_act<kNone>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+    case kGeluTanh: return launch_act<kGeluTanh>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+    case kGeluErf: return launch_act<kGeluErf>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+    case kSilu: return launch_act<kSilu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+    case kRelu: return launch_act<kRelu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+  }
+  return -1;
+}

@@ -1,0 +1,120 @@
+"""Python bindings of the hand-written CDNA4 GEMMs (``csrc/gemm.hip``, K2)."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import require, stream_ptr, check, register_signature, c_int, c_void_p, c_float
+
+ACT = {None: 0, "none": 0, "gelu_tanh": 1, "gelu": 2, "gelu_erf": 2, "silu": 3, "relu": 4}
+TILE_M, TILE_N, TILE_K = 256, 256, 64
+
+register_signature("lta_gemm_nt_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_float, c_int, c_void_p])
+
+
+def _rowmajor_2d(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+def gemm_nt_supported(a: torch.Tensor, b: torch.Tensor, bias=None, residual=None) -> bool:
+    """a [M,K] and b [N,K] bf16 on the GPU with tile-divisible shapes."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda:
+        return False
+    if not (_rowmajor_2d(a) and _rowmajor_2d(b)):
+        return False
+    M, K = a.shape
+    N = b.shape[0]
+    if M % TILE_M or N % TILE_N or K % TILE_K or b.shape[1] != K:
+        return False
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()):
+        return False
+    if residual is not None and (residual.dtype != torch.bfloat16 or tuple(residual.shape) != (M, N)
+                                 or not _rowmajor_2d(residual)):
+        return False
+    return True
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=None, alpha: float = 1.0,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(alpha * a @ b.T + bias) + residual`` with the hand-written MFMA kernel."""
+    lib = require()
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    rc = lib.lta_gemm_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                              None if bias is None else bias.data_ptr(),
+                              None if residual is None else residual.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                              out.stride(0), 0 if residual is None else residual.stride(0), alpha, ACT[act],
+                              stream_ptr(a.device))
+    check(rc, "lta_gemm_nt_bf16")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# linear with per-shape kernel selection
+# ---------------------------------------------------------------------------------------------
+import os as _os
+
+_choice: dict = {}
+
+
+def _timeit(fn, iters: int = 5) -> float:
+    for _ in range(2):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def _torch_linear(x2, w, bias, residual, act):
+    y = torch.nn.functional.linear(x2, w, bias)
+    if act == "gelu_tanh":
+        y = torch.nn.functional.gelu(y, approximate="tanh")
+    elif act in ("gelu", "gelu_erf"):
+        y = torch.nn.functional.gelu(y)
+    elif act == "silu":
+        y = torch.nn.functional.silu(y)
+    elif act == "relu":
+        y = torch.relu(y)
+    if residual is not None:
+        y = y + residual
+    return y
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual`` choosing, once per shape, the faster of the hand-written
+    MFMA kernel (epilogue fused) and hipBLASLt + separate epilogue (``LTA_GEMM=hip|torch|auto``)."""
+    K = x.shape[-1]
+    N = w.shape[0]
+    x2 = x.reshape(-1, K)
+    r2 = None if residual is None else residual.reshape(-1, N)
+    ok = gemm_nt_supported(x2, w, bias, r2)
+    mode = _os.environ.get("LTA_GEMM", "auto")
+    if not ok or mode == "torch":
+        return _torch_linear(x2, w, bias, r2, act).reshape(*x.shape[:-1], N)
+    key = (x2.shape[0], N, K, bias is not None, residual is not None, act)
+    use = True if mode == "hip" else _choice.get(key)
+    if use is None:
+        if torch.cuda.is_current_stream_capturing():
+            use = True
+        else:
+            t_h = _timeit(lambda: gemm_nt(x2, w, bias=bias, residual=r2, act=act))
+            t_t = _timeit(lambda: _torch_linear(x2, w, bias, r2, act))
+            use = t_h <= t_t
+        _choice[key] = use
+    if use:
+        y = gemm_nt(x2, w, bias=bias, residual=r2, act=act)
+    else:
+        y = _torch_linear(x2, w, bias, r2, act)
+    return y.reshape(*x.shape[:-1], N)
+
+
+def selection_table() -> dict:
+    """(M, N, K, bias, residual, act) -> True if the HIP kernel was selected."""
+    return dict(_choice)

@@ -78,6 +78,32 @@ def bench_gemm(results):
     t = timeit(lambda: torch.nn.functional.linear(a, w))
     out["fwd fused fc 4096x22016x4096"] = {"torch_ms": t, "tflops": 2 * 4096 * 22016 * 4096 / t / 1e9}
     results["gemm_layouts"] = out
+    from lightning_thunder_amd.ops.gemm import gemm_nt
+
+    out = {}
+    for (M, N, K) in [(4096, 12288, 4096), (4096, 4096, 4096), (4096, 11008, 4096), (4096, 4096, 11008),
+                      (4096, 32000, 4096), (4096, 22016, 4096), (8192, 8192, 8192)]:
+        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+        t_h = timeit(lambda: gemm_nt(a, w))
+        t_t = timeit(lambda: torch.nn.functional.linear(a, w))
+        out[f"{M}x{N}x{K}"] = {"hip_ms": t_h, "hip_tflops": 2 * M * N * K / t_h / 1e9, "hipblaslt_ms": t_t,
+                               "hipblaslt_tflops": 2 * M * N * K / t_t / 1e9}
+    results["gemm_hip_vs_hipblaslt"] = out
+
+
+def bench_hipgemm(results):
+    from lightning_thunder_amd.ops.gemm import gemm_nt
+
+    out = {}
+    for (M, N, K) in [(4096, 12288, 4096), (4096, 4096, 4096), (4096, 11008, 4096), (4096, 4096, 11008),
+                      (4096, 32000, 4096), (4096, 22016, 4096), (8192, 8192, 8192)]:
+        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+        t_h = timeit(lambda: gemm_nt(a, w))
+        t_t = timeit(lambda: torch.nn.functional.linear(a, w))
+        out[f"{M}x{N}x{K}"] = {"hip_tflops": round(2 * M * N * K / t_h / 1e9), "hipblaslt_tflops": round(2 * M * N * K / t_t / 1e9)}
+    results["gemm_hip_vs_hipblaslt"] = out
 
 
 def main():
@@ -88,6 +114,8 @@ def main():
         bench_attention(results)
     if "gemm" in which:
         bench_gemm(results)
+    if "hipgemm" in which:
+        bench_hipgemm(results)
     print(json.dumps(results, indent=1))
 
 

@@ -80,3 +80,35 @@ def test_train_step_with_fused_loss_gpu():
     for n, p in m.named_parameters():
         torch.testing.assert_close(got[n], p.grad.float(), atol=5e-2, rtol=5e-2, msg=n)
     assert "hip_cross_entropy_fwd" in str(thunder.last_traces(tm)[-1])
+
+
+@pytest.mark.gpu
+def test_hip_linear_residual_epilogue_fusion():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.executors.hipex import hip_linear
+
+    torch.manual_seed(0)
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(512, 1024, bias=False)
+            self.proj = torch.nn.Linear(1024, 512, bias=True)
+
+        def forward(self, x):
+            return self.proj(torch.nn.functional.gelu(self.fc(x))) + x
+
+    m = M().cuda().bfloat16()
+    x = torch.randn(2, 128, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    jm = thunder.jit(m)
+    out = jm(x)
+    ref = m(x)
+    torch.testing.assert_close(out, ref, rtol=2e-2, atol=2e-2)
+    tr = thunder.last_traces(jm)[-1]
+    lin = [b for b in tr.bound_symbols if b.sym is hip_linear]
+    assert len(lin) == 2
+    assert any(len(b.args) > 3 and b.args[3] is not None for b in lin), "residual add not fused into the GEMM"
+    g = torch.randn_like(out)
+    (gx,) = torch.autograd.grad(out, (x,), g)
+    (rx,) = torch.autograd.grad(ref, (x,), g)
+    torch.testing.assert_close(gx, rx, rtol=2e-2, atol=2e-2)

@@ -177,3 +177,39 @@ def test_nf4_dequant_kernel(dtype):
     x = torch.randn(8, 512, device="cuda", dtype=dtype)
     y = nf4_linear(x, q, a, NF4_CODE.cuda(), 256, 512, 64, None)
     torch.testing.assert_close(y.float(), (x.float() @ ref.cuda().t()), rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 2048, 1024)])
+@pytest.mark.parametrize("epi", ["plain", "bias_gelu", "residual", "bias_silu_residual"])
+def test_gemm_nt_bf16(shape, epi):
+    from lightning_thunder_amd.ops.gemm import gemm_nt, gemm_nt_supported
+
+    torch.manual_seed(0)
+    M, N, K = shape
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16) if "bias" in epi else None
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if "residual" in epi else None
+    act = "gelu_tanh" if "gelu" in epi else ("silu" if "silu" in epi else None)
+    assert gemm_nt_supported(a, b, bias, res)
+    out = gemm_nt(a, b, bias=bias, residual=res, act=act)
+    ref = a.float() @ b.float().t()
+    if bias is not None:
+        ref = ref + bias.float()
+    if act == "gelu_tanh":
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif act == "silu":
+        ref = torch.nn.functional.silu(ref)
+    if res is not None:
+        ref = ref.bfloat16().float() + res.float()
+    err = (out.float() - ref).abs().max().item()
+    eager = torch.nn.functional.linear(a, b, bias)
+    if act == "gelu_tanh":
+        eager = torch.nn.functional.gelu(eager, approximate="tanh")
+    elif act == "silu":
+        eager = torch.nn.functional.silu(eager)
+    if res is not None:
+        eager = eager + res
+    err_e = (eager.float() - ref).abs().max().item()
+    assert err <= 2 * err_e + 1e-2, (err, err_e)
