@@ -35,6 +35,17 @@ from . import hipfuse_codegen as cg
 
 ex = FusionExecutor("hipfuse")
 register_executor(ex)
+
+
+def _add_after_hipex():
+    # default order: hipex (whole-op HIP kernels) claims first, then hipfuse fuses what is left
+    from ..extend import _default_executors
+
+    if ex not in _default_executors:
+        _default_executors.append(ex)
+
+
+_add_after_hipex()
 ex.allow_cpu = False  # tests flip this to exercise partitioning/codegen on CPU tensors
 
 _counter = itertools.count()
@@ -269,8 +280,24 @@ def _external_view(names: set, b: BoundSymbol) -> bool:
     return b.sym.id in cg.VIEWS and not any(a.name in names for a in b.flat_proxy_args)
 
 
-def _schedule_segment(seg: list) -> list:
-    """Dataflow partition of a side-effect-free segment -> list of bsyms and groups (lists)."""
+_LAZY: set = set()  # names of lazily re-materialised casts of the trace being partitioned
+
+
+def _is_widening_convert(b: BoundSymbol) -> bool:
+    if b.sym.id != PrimIDs.CONVERT_ELEMENT_TYPE or not isinstance(b.args[0], TensorProxy):
+        return False
+    return b.output.dtype.itemsize > b.args[0].dtype.itemsize
+
+
+def _schedule_segment(seg: list, used_outside: set | None = None) -> list:
+    """Dataflow partition of a side-effect-free segment -> list of bsyms and groups (lists).
+
+    Widening casts (bf16 -> fp32, ...) are *lazy*: they are never scheduled on their own but
+    re-materialised inside every region that consumes them (or once, standalone, before a
+    non-fusible consumer), so a region never writes an upcast copy of a tensor to HBM just
+    because a later region reads it in fp32.
+    """
+    used_outside = used_outside or set()
     n = len(seg)
     prod: dict[str, int] = {}
     for i, b in enumerate(seg):
@@ -284,56 +311,98 @@ def _schedule_segment(seg: list) -> list:
             if j is not None and j != i and j not in deps[i]:
                 deps[i].add(j)
                 users[j].append(i)
+    fusible = [_fusible_leaf(b) for b in seg]
+    lazy = [False] * n
+    for i, b in enumerate(seg):
+        if fusible[i] and _is_widening_convert(b) and not any(o.name in used_outside for o in b.flat_proxy_outs):
+            lazy[i] = True
+    for i in range(n):
+        if lazy[i] and any(lazy[d] for d in deps[i]):
+            lazy[i] = False
+    lazy_deps = [{d for d in deps[i] if lazy[d]} for i in range(n)]
+    materialized: set[int] = set()  # lazy nodes already emitted standalone
+    for i in range(n):
+        if lazy[i]:
+            _LAZY.update(o.name for o in seg[i].flat_proxy_outs)
     indeg = [len(d) for d in deps]
-    ready = [i for i in range(n) if indeg[i] == 0]
-    heapq.heapify(ready)
+    ready: list = []
     items: list = []
     plan = None
     group: list = []
+    in_group: set[int] = set()
     names: set = set()
     ins: set = set()
-    fusible = [_fusible_leaf(b) for b in seg]
 
     def done(i):
         for u in users[i]:
             indeg[u] -= 1
             if indeg[u] == 0:
-                heapq.heappush(ready, u)
+                if lazy[u]:
+                    done(u)  # available on demand: its consumers may become ready
+                else:
+                    heapq.heappush(ready, u)
+
+    for i in [i for i in range(n) if indeg[i] == 0]:
+        if lazy[i]:
+            done(i)
+        else:
+            heapq.heappush(ready, i)
 
     def close():
-        nonlocal plan, group, names, ins
+        nonlocal plan, group, names, ins, in_group
         if group:
             items.append((plan, group))
-        plan, group, names, ins = None, [], set(), set()
+        plan, group, names, ins, in_group = None, [], set(), set(), set()
+
+    def add_to_group(idxs):
+        nonlocal names, ins
+        for j in idxs:
+            group.append(seg[j])
+            in_group.add(j)
+            names |= {o.name for o in seg[j].flat_proxy_outs}
+            ins |= {a.name for a in seg[j].flat_proxy_args if isinstance(a, TensorProxy)}
+
+    def try_admit(i) -> bool:
+        extra = [d for d in sorted(lazy_deps[i]) if d not in in_group and d not in materialized]
+        trial = plan.copy()
+        for j in extra + [i]:
+            if not trial.try_add(seg[j]):
+                return False
+        if trial.has_pending():
+            return False
+        plan.__dict__.update(trial.__dict__)
+        add_to_group(extra + [i])
+        return True
 
     while ready:
         pick = None
         if plan is not None:
             for i in sorted(ready):
-                if fusible[i] and (_connected(names, ins, seg[i]) or _external_view(names, seg[i])) and plan.try_add(seg[i]):
+                if fusible[i] and (_connected(names, ins, seg[i]) or _external_view(names, seg[i]) or
+                                   any(d in in_group or _connected(names, ins, seg[d]) for d in lazy_deps[i])) \
+                        and try_admit(i):
                     pick = i
                     break
         if pick is not None:
             ready.remove(pick)
             heapq.heapify(ready)
-            group.append(seg[pick])
-            names |= {o.name for o in seg[pick].flat_proxy_outs}
-            ins |= {a.name for a in seg[pick].flat_proxy_args if isinstance(a, TensorProxy)}
             done(pick)
             continue
         close()
         i = heapq.heappop(ready)
         b = seg[i]
+        started = False
         if fusible[i]:
             plan = cg.Plan()
-            if plan.try_add(b):
-                group = [b]
-                names = {o.name for o in b.flat_proxy_outs}
-                ins = {a.name for a in b.flat_proxy_args if isinstance(a, TensorProxy)}
+            if try_admit(i):
+                started = True
             else:
                 plan = None
-                items.append(b)
-        else:
+        if not started:
+            for d in sorted(lazy_deps[i]):
+                if d not in materialized:
+                    materialized.add(d)
+                    items.append(seg[d])
             items.append(b)
         done(i)
     close()
@@ -344,19 +413,36 @@ def _fusion_pass(trace):
     flat: list[BoundSymbol] = []
     for b in trace.bound_symbols:
         flat.extend(_flatten(b))
-    items: list = []
+    # segment boundaries and the names each segment must export to the rest of the trace
+    segments: list = []
     seg: list = []
     for b in flat:
         if _is_barrier(b) or not (b.flat_proxy_outs or b.flat_proxy_args):
             if seg:
-                items.extend(_schedule_segment(seg))
+                segments.append(seg)
                 seg = []
-            items.append(b)
+            segments.append(b)
         else:
             seg.append(b)
     if seg:
-        items.extend(_schedule_segment(seg))
+        segments.append(seg)
+    _LAZY.clear()
+    uses_by_seg: list[set] = []
+    for s_ in segments:
+        bs = s_ if isinstance(s_, list) else [s_]
+        uses_by_seg.append({a.name for b in bs for a in b.flat_proxy_args})
+    items: list = []
+    for k, s_ in enumerate(segments):
+        if not isinstance(s_, list):
+            items.append(s_)
+            continue
+        outside = set()
+        for j, u in enumerate(uses_by_seg):
+            if j != k:
+                outside |= u
+        items.extend(_schedule_segment(s_, outside))
 
+    lazy_names = set(_LAZY)
     # consumers outside each group decide region outputs
     use_count: dict[str, list] = {}
     for idx, it in enumerate(items):
@@ -403,9 +489,12 @@ def _fusion_pass(trace):
         pset = set()
         for b in group:
             for o in b.flat_proxy_outs:
+                if o.name in pset:
+                    continue
                 produced.append(o)
                 pset.add(o.name)
-        outputs = [o for o in produced if o.name not in pre_names and any(u != idx for u in use_count.get(o.name, []))]
+        outputs = [o for o in produced if o.name not in pre_names and o.name not in lazy_names
+                   and any(u != idx for u in use_count.get(o.name, []))]
         seen = set()
         inputs = []
         for b in group:

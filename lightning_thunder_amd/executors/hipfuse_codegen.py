@@ -158,6 +158,23 @@ class Plan:
     def _internal(self, a):
         return isinstance(a, TensorProxy) and a.name in self.maps
 
+    def has_pending(self) -> bool:
+        """True while some value's index map is still unknown (see ``_add_elementwise``)."""
+        return any(m is None for m in self.maps.values())
+
+    def _resolve(self, name: str, m) -> None:
+        """Assign map ``m`` to pending value ``name`` and, transitively, to its pending producers."""
+        if self.maps.get(name, 0) is not None:
+            return
+        self.maps[name] = m
+        for k, b in enumerate(self.nodes):
+            if any(o.name == name for o in b.flat_outs):
+                for pos, a in enumerate(b.args):
+                    if isinstance(a, TensorProxy):
+                        self.arg_maps[k][pos] = m
+                        if a.name in self.maps:
+                            self._resolve(a.name, m)
+
     def _check_dtype(self, *ts):
         for t in ts:
             if isinstance(t, TensorProxy) and not supported_dtype(t.dtype):
@@ -216,18 +233,26 @@ class Plan:
         if bsym.sym.id in _UNARY_FLOAT and out.dtype not in _FLOATS:
             raise NotFusible("float op on ints")
         internal = [a for _, a in targs if self._internal(a)]
-        if internal:
-            m = self.maps[internal[0].name]
-            for a in internal[1:]:
+        known = [a for a in internal if self.maps[a.name] is not None]
+        if known:
+            m = self.maps[known[0].name]
+            for a in known[1:]:
                 if self.maps[a.name] != m:
                     raise NotFusible("operands with different maps")
+            for a in internal:
+                if self.maps[a.name] is None:
+                    self._resolve(a.name, m)
         else:
             m = self._map_for_shape(out.shape)
             if m == "new":
                 self._set_domain(out.shape)
                 m = self._identity(out.shape)
             if m is None:
-                raise NotFusible("shape not in domain")
+                # e.g. a cast of a weight vector that a later broadcast maps into the domain:
+                # keep it pending until a consumer fixes its map
+                if any(self.maps.get(a.name, 0) is not None for a in internal):
+                    raise NotFusible("shape not in domain")
+                m = None
         for i, _ in targs:
             am[i] = m
         self.maps[out.name] = m
@@ -235,6 +260,13 @@ class Plan:
     def _add_broadcast(self, bsym, am):
         a, shape, bdims = bsym.args[0], tuple(bsym.args[1]), tuple(bsym.args[2])
         out = bsym.output
+        if self._internal(a) and self.maps[a.name] is None:
+            om = self._map_for_shape(shape)
+            if om is None or om == "new":
+                raise NotFusible("broadcast of pending value to non-domain shape")
+            self._resolve(a.name, tuple(om[bdims[i]] if a.shape[i] != 1 else None for i in range(len(a.shape))))
+            self.maps[out.name] = om
+            return
         if self._internal(a):
             amap = self.maps[a.name]
             if self.domain is not None and shape != self.domain and tuple(a.shape) == self.domain and not self.has_reduction \

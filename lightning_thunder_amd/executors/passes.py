@@ -95,6 +95,15 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
     trace = _transform_for_operator_executor_execution(trace, executors)
     traces.append(trace)
     trace = dce(trace)
+    # executor-specific rewrites of the claimed program before fusion (e.g. hipex folds residual
+    # adds into its GEMM epilogue, which beats fusing them into a separate elementwise kernel)
+    for ex in executors:
+        hook = getattr(ex, "post_claim_pass", None)
+        if hook is not None:
+            new = hook(trace)
+            if new is not trace:
+                trace = new
+                traces.append(trace)
     for ex in executors:
         if isinstance(ex, FusionExecutor):
             trace = ex.fusion_pass(trace)
@@ -103,15 +112,6 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
     trace = _transform_for_operator_executor_execution(trace, [e for e in executors if not isinstance(e, FusionExecutor)])
     trace = dce(trace)
     traces.append(trace)
-    # executor-specific rewrites of the claimed program (e.g. hipex folds elementwise epilogues
-    # into its GEMM)
-    for ex in executors:
-        hook = getattr(ex, "post_claim_pass", None)
-        if hook is not None:
-            new = hook(trace)
-            if new is not trace:
-                trace = new
-                traces.append(trace)
     return traces
 
 
