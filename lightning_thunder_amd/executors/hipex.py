@@ -71,6 +71,79 @@ def _register_linear():
 _register_linear()
 
 
+# =========================================================================================
+# K8 FP8 linear (fwd/bwd on the block-scaled MFMA GEMM)
+# =========================================================================================
+def _fp8_quant_meta(t, e5m2):
+    C = t.shape[-1]
+    R = 1
+    for d in t.shape[:-1]:
+        R *= d
+    u8 = torch.uint8
+    return (TensorProxy(like=t, shape=(R, C), dtype=u8, requires_grad=False),
+            TensorProxy(like=t, shape=(C, R), dtype=u8, requires_grad=False),
+            TensorProxy(like=t, shape=(), dtype=torch.float32, requires_grad=False))
+
+
+def _fp8_quant_impl(t, e5m2):
+    from ..ops.fp8 import quantize
+
+    return quantize(t, e5m2)
+
+
+def _fp8_gemm_meta(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape):
+    return TensorProxy(like=qa, shape=tuple(out_shape), dtype=torch.bfloat16)
+
+
+def _fp8_gemm_impl(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape):
+    from ..ops.fp8 import gemm
+
+    return gemm(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape)
+
+
+# quantize = amax + cast(+transpose) (pure: CSE shares one quantisation of x between the sibling
+# fc_1 / fc_2 linears); gemm = the block-scaled-MFMA NT kernel
+hip_fp8_quantize = ex.register_operator("hip_fp8_quantize", meta=_fp8_quant_meta, fn=_fp8_quant_impl)
+hip_fp8_gemm = ex.register_operator("hip_fp8_gemm", meta=_fp8_gemm_meta, fn=_fp8_gemm_impl)
+
+
+def _fp8_vjp(x, w, bias=None):
+    from .. import torch as ltorch
+
+    qx, qxT, sx = hip_fp8_quantize(x, False)
+    qw, qwT, sw = hip_fp8_quantize(w, False)
+    out_shape = tuple(x.shape[:-1]) + (w.shape[0],)
+    y = hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, out_shape)
+
+    def bwd(g):
+        qg, qgT, sg = hip_fp8_quantize(g, True)
+        dx = hip_fp8_gemm(qg, qwT, sg, sw, 1, 0, None, tuple(x.shape))
+        dw = hip_fp8_gemm(qgT, qxT, sg, sx, 1, 0, None, tuple(w.shape))
+        if bias is None:
+            return dx, dw
+        db = ltorch.sum(g, tuple(range(g.ndim - 1)))
+        return dx, dw, db
+
+    return y, bwd
+
+
+def _fp8_exec(x, w, bias=None):
+    qx, _, sx = hip_fp8_quantize(x, False)
+    qw, _, sw = hip_fp8_quantize(w, False)
+    return hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
+
+
+def _register_fp8():
+    from ..transforms.fp8 import fp8_linear, eligible
+    from ..core.transforms import register_vjp
+
+    ex.register_implementation(fp8_linear, checker=eligible, execution_transform=_fp8_exec)
+    register_vjp(fp8_linear)(_fp8_vjp)
+
+
+_register_fp8()
+
+
 def _fuse_linear_epilogues(trace):
     """``y = hip_linear(x, w, b); z = y + r`` (y used nowhere else) -> ``z = hip_linear(x, w, b, r)``:
     the residual add runs in the GEMM's epilogue (one HBM round trip of y saved)."""

@@ -463,25 +463,33 @@ def _fusion_pass(trace):
             if not (b.sym.id in cg.VIEWS and not any(a.name in internal_names for a in b.flat_proxy_args)):
                 internal_names |= {o.name for o in b.flat_proxy_outs}
         used_inside = {a.name for b in group for a in b.flat_proxy_args}
-        keep = []
+        original = list(group)
+
+        def is_ext_view(b):
+            return b.sym.id in cg.VIEWS and not any(a.name in internal_names for a in b.flat_proxy_args)
+
+        # ext views needed outside the region are emitted standalone before it, together with the
+        # ext views they are built from (closed under ancestry, kept in group order)
+        need: set[str] = set()
         for b in group:
-            ext_view = b.sym.id in cg.VIEWS and not any(a.name in internal_names for a in b.flat_proxy_args)
-            if ext_view:
+            if is_ext_view(b):
                 o = b.flat_proxy_outs[0].name
                 if any(u != idx for u in use_count.get(o, [])):
-                    pre.append(b)
-                if o not in used_inside:
-                    continue
-            keep.append(b)
+                    need.add(o)
+        for b in reversed(group):
+            if is_ext_view(b) and b.flat_proxy_outs[0].name in need:
+                need |= {a.name for a in b.flat_proxy_args}
+        pre = [b for b in group if is_ext_view(b) and b.flat_proxy_outs[0].name in need]
+        keep = [b for b in group if not (is_ext_view(b) and b.flat_proxy_outs[0].name not in used_inside)]
         if len(keep) != len(group):
             plan = _replan(keep)
             if plan is None:
-                new_bsyms.extend(group)
+                new_bsyms.extend(original)
                 continue
             group = keep
         ncompute = sum(1 for b in group if cg.is_compute(b))
         if ncompute < 2 or not ex.get_fuel():
-            new_bsyms.extend(pre + [b for b in group if b not in pre])
+            new_bsyms.extend(original)
             continue
         new_bsyms.extend(pre)
         pre_names = {o.name for b in pre for o in b.flat_proxy_outs}

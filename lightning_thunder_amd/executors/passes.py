@@ -13,7 +13,7 @@ from ..core.proxies import Proxy, TensorProxy
 from ..core.pytree import tree_flatten
 from ..core.symbol import BoundSymbol
 from ..core.trace import TraceCtx, from_trace, tracectx, TraceProvenance
-from ..core.transform_common import dce
+from ..core.transform_common import dce, cse
 from ..extend import Executor, FusionExecutor, get_always_executors
 
 
@@ -94,7 +94,7 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
     traces.append(trace)
     trace = _transform_for_operator_executor_execution(trace, executors)
     traces.append(trace)
-    trace = dce(trace)
+    trace = dce(cse(trace))
     # executor-specific rewrites of the claimed program before fusion (e.g. hipex folds residual
     # adds into its GEMM epilogue, which beats fusing them into a separate elementwise kernel)
     for ex in executors:

@@ -182,6 +182,129 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_kernel(const __hip_bfloa
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// FP8 (OCP e4m3fn / e5m2) NT GEMM on the block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4,
+// 2x the bf16 rate).  Same geometry and LDS image as the bf16 kernel: BK = 128 fp8 = 128-B rows,
+// so staging (glds) and the XOR swizzle are byte-identical.  Per-tensor scaling: the operands
+// hold x * s_x; the MFMA block scales are 1.0 and alpha = 1 / (s_a * s_b) is applied in the
+// epilogue.  Lane l holds A[row l&15][k = 32 (l>>4) .. +32] (two 16-B LDS reads).
+// ---------------------------------------------------------------------------------------------
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void stage_tile_bytes(const char* __restrict__ A, const char* __restrict__ B, int lda,
+                                                 int ldb, int m0, int n0, int k0, char* sbase, int wave, int lane) {
+  const int r = lane >> 3, p = lane & 7;
+  const int c = p ^ r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 8 + wave;
+    const int row = chunk * 8 + r;
+    __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)(m0 + row) * lda + k0 + c * 16),
+                                     (lds_void*)(sbase + chunk * 1024), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 8 + wave;
+    const int row = chunk * 8 + r;
+    __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(n0 + row) * ldb + k0 + c * 16),
+                                     (lds_void*)(sbase + TILE_BYTES + chunk * 1024), 16, 0, 0);
+  }
+}
+
+template <int FA, int FB>
+__device__ __forceinline__ f32x4 mfma_fp8(const v8i& a, const v8i& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
+
+template <int FA, int FB, bool BIAS>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                             __hip_bfloat16* __restrict__ C,
+                                                             const __hip_bfloat16* __restrict__ bias, int M, int N,
+                                                             int K, int lda, int ldb, int ldc,
+                                                             const float* __restrict__ sa,
+                                                             const float* __restrict__ sb) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  constexpr int BKB = 128;  // fp8 elements (= bytes) per K-step
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BKB;
+  stage_tile_bytes(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) stage_tile_bytes(A, B, lda, ldb, m0, n0, (t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+    v8i af[8], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = wm * 128 + m * 16 + fr;
+      const uint4 lo = *reinterpret_cast<const uint4*>(cur + row * 128 + (((2 * fq) ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(cur + row * 128 + (((2 * fq + 1) ^ (row & 7)) << 4));
+      af[m] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int row = wn * 64 + n * 16 + fr;
+      const char* base = cur + TILE_BYTES + row * 128;
+      const uint4 lo = *reinterpret_cast<const uint4*>(base + (((2 * fq) ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(base + (((2 * fq + 1) ^ (row & 7)) << 4));
+      bfr[n] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = mfma_fp8<FA, FB>(af[m], bfr[n], acc[m][n]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const float alpha = 1.f / (*sa * *sb);
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 64 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) =
+            __float2bfloat16(acc[m][n][j] * alpha + bv);
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+    *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * ldc + n0 + wn * 64 + ch * 8) = v;
+  }
+}
+
 template <int ACT>
 int launch_act(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
                int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
@@ -199,6 +322,26 @@ int launch_act(const void* A, const void* B, void* C, const void* bias, const vo
 }
 
 }  // namespace
+
+// C[M,N] (bf16) = (A . B^T) / (*sa * *sb) (+ bias); A [M,K], B [N,K] fp8 (fmt 0 = e4m3fn, 1 = e5m2),
+// K % 128 == 0; sa / sb are device scalars (the per-tensor scales the operands were cast with).
+LTA_EXPORT int lta_gemm_nt_fp8(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                               int ldb, int ldc, int fmt_a, int fmt_b, const void* sa, const void* sb,
+                               hipStream_t stream) {
+  if (M % BM || N % BN || K % 128) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_F8(FA, FB, BI)                                                                                       \
+  hipLaunchKernelGGL((gemm_nt_fp8_kernel<FA, FB, BI>), grid, block, 0, stream, (const char*)A, (const char*)B,    \
+                     (__hip_bfloat16*)C, (const __hip_bfloat16*)bias, M, N, K, lda, ldb, ldc, (const float*)sa,          \
+                     (const float*)sb)
+  const bool bi = bias != nullptr;
+  if (fmt_a == 0 && fmt_b == 0) { if (bi) LTA_F8(0, 0, true); else LTA_F8(0, 0, false); }
+  else if (fmt_a == 1 && fmt_b == 0) { if (bi) LTA_F8(1, 0, true); else LTA_F8(1, 0, false); }
+  else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_F8(0, 1, true); else LTA_F8(0, 1, false); }
+  else return -1;
+#undef LTA_F8
+  return (int)hipGetLastError();
+}
 
 LTA_EXPORT int lta_gemm_tile_m() { return BM; }
 LTA_EXPORT int lta_gemm_tile_n() { return BN; }

@@ -1,0 +1,118 @@
+"""FP8 (OCP e4m3fn / e5m2) kernels for the FP8 linear path (K8): casts, cast+transpose and the
+hand-written block-scaled-MFMA GEMM (``csrc/fp8.hip``, ``csrc/gemm.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import require, stream_ptr, check, register_signature, c_int, c_int64, c_void_p, c_float, DTYPE_CODE
+
+E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
+
+register_signature("lta_amax", [c_int, c_void_p, c_int64, c_void_p, c_void_p])
+register_signature("lta_fp8_cast", [c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_void_p, c_void_p,
+                                    c_void_p])
+register_signature("lta_fp8_cast_transpose", [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                              c_float, c_void_p, c_void_p, c_void_p])
+register_signature("lta_gemm_nt_fp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, c_int, c_void_p, c_void_p, c_void_p])
+
+
+def amax_into(x: torch.Tensor, out: torch.Tensor) -> None:
+    """out (fp32 device scalar, zero-initialised) = max(out, max |x|) — one read of x, no temporaries."""
+    check(require().lta_amax(DTYPE_CODE[x.dtype], x.data_ptr(), x.numel(), out.data_ptr(), stream_ptr(x.device)),
+          "lta_amax")
+
+
+def scale_for(t: torch.Tensor, fmax: float, margin: float = 0.0) -> torch.Tensor:
+    """Per-tensor scale as a device scalar (reference helper; the kernels derive it on device)."""
+    amax = torch.zeros((), dtype=torch.float32, device=t.device)
+    amax_into(t, amax)
+    return (fmax / amax.clamp_min(1e-12)) * (2.0 ** -margin)
+
+
+def cast(x: torch.Tensor, amax: torch.Tensor, fmax: float, scale_out: torch.Tensor | None = None,
+         e5m2: bool = False, amax_out: torch.Tensor | None = None):
+    """fp8(x * fmax / amax) as uint8 storage; the scale used is written to ``scale_out``."""
+    lib = require()
+    y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    check(lib.lta_fp8_cast(DTYPE_CODE[x.dtype], int(e5m2), x.data_ptr(), y.data_ptr(), x.numel(), amax.data_ptr(), fmax,
+                           None if scale_out is None else scale_out.data_ptr(),
+                           None if amax_out is None else amax_out.data_ptr(), stream_ptr(x.device)), "lta_fp8_cast")
+    return y
+
+
+def cast_transpose(x2d: torch.Tensor, amax: torch.Tensor, fmax: float, scale_out: torch.Tensor | None = None,
+                   e5m2: bool = False, rowmajor: bool = True, amax_out: torch.Tensor | None = None):
+    """x [R, C] -> (fp8 [R, C] or None, fp8 [C, R]) as uint8 storage."""
+    lib = require()
+    R, C = x2d.shape
+    y = torch.empty((R, C), dtype=torch.uint8, device=x2d.device) if rowmajor else None
+    yt = torch.empty((C, R), dtype=torch.uint8, device=x2d.device)
+    check(lib.lta_fp8_cast_transpose(DTYPE_CODE[x2d.dtype], int(e5m2), x2d.data_ptr(),
+                                     None if y is None else y.data_ptr(), yt.data_ptr(), R, C, amax.data_ptr(), fmax,
+                                     None if scale_out is None else scale_out.data_ptr(),
+                                     None if amax_out is None else amax_out.data_ptr(), stream_ptr(x2d.device)),
+          "lta_fp8_cast_transpose")
+    return y, yt
+
+
+def gemm_nt_fp8(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int = 0, fmt_b: int = 0,
+                bias: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 [M, N] = (a [M,K] . b[N,K]^T) / (sa * sb) (+ bias); a/b fp8 as uint8, sa/sb device scalars."""
+    lib = require()
+    M, K = a.shape
+    N = b.shape[0]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    check(lib.lta_gemm_nt_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), None if bias is None else bias.data_ptr(), M,
+                              N, K, a.stride(0), b.stride(0), out.stride(0), fmt_a, fmt_b, sa.data_ptr(), sb.data_ptr(),
+                              stream_ptr(a.device)), "lta_gemm_nt_fp8")
+    return out
+
+
+def fp8_linear_supported(M: int, N: int, K: int) -> bool:
+    return M % 256 == 0 and N % 256 == 0 and K % 256 == 0
+
+
+def fp8_linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None):
+    """y = x @ w^T + b with e4m3 operands.  Returns (y, x^T fp8, w^T fp8, scales[sx, sw]) —
+    the transposed copies are what the backward's dgrad/wgrad GEMMs read.  Per call: one amax
+    pass and one cast(+transpose) pass per operand; the scales never leave the device."""
+    K = x.shape[-1]
+    N = w.shape[0]
+    x2 = x.reshape(-1, K)
+    st = torch.zeros(4, dtype=torch.float32, device=x.device)  # amax_x, amax_w, s_x, s_w
+    amax_into(x2, st[0])
+    amax_into(w, st[1])
+    qx, qxT = cast_transpose(x2, st[0], E4M3_MAX, st[2])
+    qw, qwT = cast_transpose(w, st[1], E4M3_MAX, st[3])
+    scales = st[2:4]
+    y = gemm_nt_fp8(qx, qw, st[2], st[3], 0, 0, bias)
+    return y.reshape(*x.shape[:-1], N), qxT, qwT, scales
+
+
+def fp8_linear_bwd(dy: torch.Tensor, qxT: torch.Tensor, qwT: torch.Tensor, scales: torch.Tensor, has_bias: bool,
+                   x_shape):
+    N = dy.shape[-1]
+    dy2 = dy.reshape(-1, N)
+    st = torch.zeros(4, dtype=torch.float32, device=dy.device)  # amax_dy, s_dy, (s_dy, s_w) / (s_dy, s_x) below
+    amax_into(dy2, st[0])
+    qdy, qdyT = cast_transpose(dy2, st[0], E5M2_MAX, st[1], e5m2=True)
+    dx = gemm_nt_fp8(qdy, qwT, st[1], scales[1], 1, 0)   # [M, K]
+    dw = gemm_nt_fp8(qdyT, qxT, st[1], scales[0], 1, 0)  # [N, K]
+    db = dy2.sum(0) if has_bias else None
+    return dx.reshape(x_shape), dw, db
+
+
+def quantize(t: torch.Tensor, e5m2: bool = False):
+    """t (any shape, last dim C) -> (q [R, C], q^T [C, R], scale) with per-tensor current scaling."""
+    t2 = t.reshape(-1, t.shape[-1])
+    st = torch.zeros(2, dtype=torch.float32, device=t.device)  # amax, scale
+    amax_into(t2, st[0])
+    q, qT = cast_transpose(t2, st[0], E5M2_MAX if e5m2 else E4M3_MAX, st[1], e5m2=e5m2)
+    return q, qT, st[1]
+
+
+def gemm(qa: torch.Tensor, qb: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int, fmt_b: int,
+         bias: torch.Tensor | None, out_shape) -> torch.Tensor:
+    return gemm_nt_fp8(qa, qb, sa, sb, fmt_a, fmt_b, bias).reshape(out_shape)

@@ -102,7 +102,14 @@ def bench_hipgemm(results):
         w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
         t_h = timeit(lambda: gemm_nt(a, w))
         t_t = timeit(lambda: torch.nn.functional.linear(a, w))
-        out[f"{M}x{N}x{K}"] = {"hip_tflops": round(2 * M * N * K / t_h / 1e9), "hipblaslt_tflops": round(2 * M * N * K / t_t / 1e9)}
+        from lightning_thunder_amd.ops.fp8 import gemm_nt_fp8
+
+        a8 = a.to(torch.float8_e4m3fn).view(torch.uint8)
+        w8 = w.to(torch.float8_e4m3fn).view(torch.uint8)
+        sc = torch.ones((), device="cuda")
+        t_8 = timeit(lambda: gemm_nt_fp8(a8, w8, sc, sc)) if K % 128 == 0 else float("nan")
+        out[f"{M}x{N}x{K}"] = {"hip_tflops": round(2 * M * N * K / t_h / 1e9), "hipblaslt_tflops": round(2 * M * N * K / t_t / 1e9),
+                               "hip_fp8_tflops": round(2 * M * N * K / t_8 / 1e9)}
     results["gemm_hip_vs_hipblaslt"] = out
 
 

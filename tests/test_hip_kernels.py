@@ -213,3 +213,66 @@ def test_gemm_nt_bf16(shape, epi):
         eager = eager + res
     err_e = (eager.float() - ref).abs().max().item()
     assert err <= 2 * err_e + 1e-2, (err, err_e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e5m2", [False, True])
+def test_fp8_cast_and_transpose(e5m2):
+    from lightning_thunder_amd.ops.fp8 import cast, cast_transpose, amax_into, E4M3_MAX, E5M2_MAX
+
+    torch.manual_seed(0)
+    x = torch.randn(128, 192, device="cuda", dtype=torch.bfloat16) * 3
+    fmax = E5M2_MAX if e5m2 else E4M3_MAX
+    amax = torch.zeros((), device="cuda")
+    amax_into(x, amax)
+    torch.testing.assert_close(amax, x.float().abs().amax())
+    scale = torch.zeros((), device="cuda")
+    y = cast(x, amax, fmax, scale, e5m2)
+    s = fmax / x.float().abs().amax()
+    torch.testing.assert_close(scale, s)
+    dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
+    ref = (x.float() * scale).clamp(-fmax, fmax).to(dt).view(torch.uint8)
+    assert (y != ref).sum().item() <= 2  # fp32 rounding of x*s at a tie at most
+    y2, yt = cast_transpose(x, amax, fmax, None, e5m2)
+    assert torch.equal(y2, y) and torch.equal(yt, y.t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmts", [(0, 0), (1, 0)])
+def test_gemm_nt_fp8(fmts):
+    from lightning_thunder_amd.ops.fp8 import gemm_nt_fp8
+
+    torch.manual_seed(0)
+    M, N, K = 512, 768, 1024
+    da = torch.float8_e5m2 if fmts[0] else torch.float8_e4m3fn
+    a8 = torch.randn(M, K, device="cuda").to(da)
+    b8 = torch.randn(N, K, device="cuda").to(torch.float8_e4m3fn)
+    sa, sb = torch.tensor(2.0, device="cuda"), torch.tensor(4.0, device="cuda")
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    out = gemm_nt_fp8(a8.view(torch.uint8), b8.view(torch.uint8), sa, sb, fmts[0], fmts[1], bias)
+    ref = (a8.float() @ b8.float().t()) / 8.0 + bias.float()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=5e-2)
+
+
+@pytest.mark.gpu
+def test_fp8_linear_training_close_to_bf16():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 1024), torch.nn.GELU(), torch.nn.Linear(1024, 512)).cuda().bfloat16()
+    t = FP8LinearTransform()
+    jm = thunder.jit(m, transforms=[t])
+    x = torch.randn(4, 64, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    out = jm(x)
+    assert t.n_converted == 2
+    assert any("fp8" in b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols)
+    ref = m(x)
+    rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
+    assert rel < 0.08, rel
+    g = torch.randn_like(out)
+    gx, gw = torch.autograd.grad(out, (x, m[0].weight), g)
+    rx, rw = torch.autograd.grad(ref, (x, m[0].weight), g)
+    for a, b in ((gx, rx), (gw, rw)):
+        cos = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+        assert cos > 0.99, cos

@@ -159,3 +159,27 @@ def test_fused_noncontiguous_and_backward_gpu():
     torch.testing.assert_close(ga, ra)
     torch.testing.assert_close(gb, rb)
     assert hipfuse.fusions(thunder.last_backward_traces(jf)[-1])
+
+
+@pytest.mark.parametrize("name", ["llama2-like", "llama3-like", "gpt-neox-like"])
+def test_litgpt_partition_cpu(name, cpu_fusion):
+    """Whole-model fwd+bwd through the fusion partitioner (reference path on CPU): catches
+    scheduling / region-output bugs without a GPU."""
+    from lightning_thunder_amd.models.litgpt import GPT, Config
+
+    torch.manual_seed(0)
+    cfg = Config.from_name(name, n_layer=2)
+    m = GPT(cfg)
+    m.set_rope_cache(32)
+    x = torch.randint(0, cfg.vocab_size, (2, 32))
+    jm = thunder.jit(m)
+    out = jm(x)
+    ref = m(x)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(out)
+    gj = torch.autograd.grad(out, list(m.parameters()), g, allow_unused=True)
+    gr = torch.autograd.grad(ref, list(m.parameters()), g, allow_unused=True)
+    for a, b in zip(gj, gr):
+        if b is not None:
+            torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+    assert hipfuse.fusions(thunder.last_backward_traces(jm)[-1])
