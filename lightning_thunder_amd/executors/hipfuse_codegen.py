@@ -924,8 +924,14 @@ class _Gen:
                 passes.setdefault(lvl, []).append(k)
                 if b.sym.id == PrimIDs.VAR_MEAN:
                     passes.setdefault(lvl + 1, []).append(("var", k))
-        final_outs = [o for o in self.outputs if self.dep.get(o.name, False)]
-        row_outs = [o for o in self.outputs if not self.dep.get(o.name, False)]
+        redset = self._reduced_dims()
+
+        def spans_reduced(o):  # stored over reduced dims even if its value is row-constant
+            return any(d in redset for d in self.p.maps[o.name] if d is not None)
+
+        final_outs = [o for o in self.outputs if self.dep.get(o.name, False) or spans_reduced(o)]
+        final_names = {o.name for o in final_outs}
+        row_outs = [o for o in self.outputs if o.name not in final_names]
         max_pass = max(passes) if passes else -1
         racc = 0
         for p in range(max_pass + 1):

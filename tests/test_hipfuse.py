@@ -182,4 +182,12 @@ def test_litgpt_partition_cpu(name, cpu_fusion):
     for a, b in zip(gj, gr):
         if b is not None:
             torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
-    assert hipfuse.fusions(thunder.last_backward_traces(jm)[-1])
+    bw = thunder.last_backward_traces(jm)[-1]
+    assert hipfuse.fusions(bw)
+    if os.path.exists(LIB):  # every generated kernel must compile for gfx950
+        for tr in (thunder.last_traces(jm)[-1], bw):
+            for fb in hipfuse.fusions(tr):
+                f = fb._call_ctx[fb.sym.name]
+                targs = {p.name: cg.TensorArg(tuple(p.shape), tuple(torch.empty(tuple(p.shape)).stride()), p.dtype, True)
+                         for p in f.inputs if isinstance(p, TensorProxy)}
+                hipfuse.compile_source(cg.generate(f.plan, f.inputs, f.outputs, targs))
