@@ -52,6 +52,7 @@ class PrimIDs(Enum):
     IOTA = auto()
     UNIFORM = auto()
     UNIFORM_PHILOX = auto()
+    GET_RNG_SEED_OFFSET = auto()
     RANDN = auto()
     EMPTY = auto()
     TENSOR_FROM_SEQUENCE = auto()
@@ -539,6 +540,15 @@ def _uniform_philox_meta(shape, minval, maxval, *, device, dtype, seed, offset):
 
 
 uniform_philox = make_prim(PrimIDs.UNIFORM_PHILOX, "uniform_philox", meta=_uniform_philox_meta)
+
+
+def _get_rng_seed_offset_meta(numel):
+    return _proxies.IntegerProxy(None), _proxies.IntegerProxy(None)
+
+
+# advances the framework's Philox counter (a side effect: never CSE'd or DCE'd, a fusion barrier)
+get_rng_seed_offset = make_prim(PrimIDs.GET_RNG_SEED_OFFSET, "get_rng_seed_offset", meta=_get_rng_seed_offset_meta,
+                                tags=(OpTags.DONT_DCE, OpTags.RANDOM_OP))
 
 
 def _randn_meta(shape, *, device, dtype):

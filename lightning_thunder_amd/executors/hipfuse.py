@@ -52,6 +52,9 @@ _counter = itertools.count()
 
 
 def _checker(*args, **kwargs):
+    dev = kwargs.get("device")
+    if dev is not None and getattr(dev, "type", None) not in (None, "cuda") and not ex.allow_cpu:
+        return False
     for a in tree_flatten((args, kwargs))[0]:
         if isinstance(a, TensorProxy):
             if not cg.supported_dtype(a.dtype):

@@ -99,11 +99,11 @@ REDUCTIONS = {PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD, PrimIDs.VAR
 ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY | _BINARY_SPECIAL | {
     PrimIDs.WHERE, PrimIDs.CONVERT_ELEMENT_TYPE}
 VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE}
-SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL}
+SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
 
 
 def is_compute(bsym) -> bool:
-    return bsym.sym.id in ELEMENTWISE or bsym.sym.id in REDUCTIONS
+    return bsym.sym.id in ELEMENTWISE or bsym.sym.id in REDUCTIONS or bsym.sym.id == PrimIDs.UNIFORM_PHILOX
 
 
 def _sq(shape):
@@ -213,6 +213,14 @@ class Plan:
             self._add_unit_reshape(bsym, am)
         elif sid in REDUCTIONS:
             self._add_reduction(bsym, am)
+        elif sid == PrimIDs.UNIFORM_PHILOX:
+            # per-element counter-based RNG: indexed by the flat position in the domain
+            out = bsym.output
+            if self.domain is None:
+                self._set_domain(out.shape)
+            if tuple(out.shape) != self.domain:
+                raise NotFusible("uniform_philox must span the iteration domain")
+            self.maps[out.name] = self._identity(out.shape)
         elif sid == PrimIDs.FULL:
             out = bsym.output
             m = self._map_for_shape(out.shape)
@@ -463,7 +471,9 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
     ``targs``: input name -> TensorArg for the tensor inputs at this call signature."""
     g = _Gen(plan, inputs, outputs, targs)
     body, grid, block, vec, mode = g.build()
-    src = _PREAMBLE + body
+    from ..core.rng import PHILOX_HIP
+
+    src = _PREAMBLE + (PHILOX_HIP if "philox_uniform(" in body else "") + body
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
     name = f"{kernel_prefix}_{h}"
     src = src.replace("__KERNEL_NAME__", name)
@@ -524,6 +534,8 @@ class _Gen:
                 continue
             if b.sym.id == PrimIDs.FULL:
                 dep = self.red == 0
+            if b.sym.id == PrimIDs.UNIFORM_PHILOX:
+                dep = True
             for o in b.flat_outs:
                 self.dep[o.name] = dep if self.red else True
                 self.level[o.name] = lvl
@@ -625,6 +637,14 @@ class _Gen:
             return [(out.name, R(0))]
         if sid == PrimIDs.FULL:
             return [(out.name, self._scalar_ref(b.args[1], ct))]
+        if sid == PrimIDs.UNIFORM_PHILOX:
+            seed = self._scalar_ref(b.kwargs["seed"], "double")
+            off = self._scalar_ref(b.kwargs["offset"], "double")
+            lo, hi = float(pyval(b.args[1])), float(pyval(b.args[2]))
+            u = f"philox_uniform((unsigned)(unsigned long long)({seed}), (unsigned long long)({off}), {self.flat_index})"
+            if lo != 0.0 or hi != 1.0:
+                u = f"({u} * {_lit(hi - lo, 'float')} + {_lit(lo, 'float')})"
+            return [(out.name, _rnd(out.dtype, f"({ct})({u})"))]
         # operand compute type: that of the first tensor operand (prims enforce equal dtypes)
         tin = [a for a in b.args if isinstance(a, TensorProxy)]
         ict = _CTYPE[tin[0].dtype] if tin else ct
@@ -870,6 +890,7 @@ class _Gen:
         ind = "    "
         body.append(f"  for ({IT} v = ({IT})blockIdx.x * {block}u + threadIdx.x; v < {nvec}u; v += ({IT})gridDim.x * {block}u) {{")
         body.append(f"{ind}const {IT} e = v * {V}u;")
+        self.flat_index = "((unsigned long long)e + (unsigned long long)j)"
         self._decompose("e", list(range(self.nd)), body, ind)
         emitted: set = set()
         # referencing builds the load-name table lazily; pre-populate by a dry run over all nodes
@@ -903,6 +924,7 @@ class _Gen:
         grid = (rows + RPB - 1) // RPB
         self.load_names, self.loaded = {}, set()
         self.idx_avail = set()
+        self.flat_index = f"((unsigned long long)rowc * {R}ull + (unsigned long long)c + (unsigned long long)j)"
         for k, b in enumerate(self.p.nodes):
             for i, a in enumerate(b.args):
                 if isinstance(a, TensorProxy) and a.name not in self.producer:

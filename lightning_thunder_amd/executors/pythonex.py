@@ -82,3 +82,13 @@ for prim, fn, name in (
 # Return, del, comment and unpack_trivial print themselves as python statements.
 for prim in (prims.python_return, prims.python_del, prims.comment, prims.unpack_trivial):
     ex.register_implementation(prim, prim)
+
+
+def _get_rng_seed_offset(numel):
+    from ..core.rng import next_seed_offset
+
+    return next_seed_offset(int(numel))
+
+
+_rng_op = ex.register_operator("get_rng_seed_offset", like=prims.get_rng_seed_offset, fn=_get_rng_seed_offset)
+ex.register_implementation(prims.get_rng_seed_offset, _rng_op)

@@ -79,13 +79,13 @@ _register_prim(prims.uniform, _uniform, name="uniform")
 
 
 def _uniform_philox(shape, minval, maxval, *, device, dtype, seed, offset):
-    # Deterministic, recomputable RNG: seeded generator per (seed, offset)
-    gen = torch.Generator(device=device)
-    s = int(seed.item()) if isinstance(seed, torch.Tensor) else int(seed)
-    o = int(offset.item()) if isinstance(offset, torch.Tensor) else int(offset)
-    gen.manual_seed(s * 1000003 + o)
-    t = torch.empty(shape, device=device, dtype=dtype)
-    return t.uniform_(minval, maxval, generator=gen)
+    # the framework's Philox (core/rng.py): bit-identical to hipfuse's inline generator
+    from ..core.rng import philox_uniform_torch
+
+    u = philox_uniform_torch(tuple(shape), int(seed), int(offset), device)
+    if minval != 0.0 or maxval != 1.0:
+        u = u * (maxval - minval) + minval
+    return u.to(dtype)
 
 
 _register_prim(prims.uniform_philox, _uniform_philox, name="uniform_philox")

@@ -1501,12 +1501,25 @@ def dropout(a, p: float = 0.5, training: bool = True, inplace: bool = False):
     if p == 1.0:
         return clang.full_like(a, 0)
     scale = 1.0 / (1.0 - p)
-    r = prims.uniform(a.shape, 0.0, 1.0, device=a.device, dtype=torch.float32)
-    keep = clang.lt(r, 1.0 - p)
+    keep = philox_keep_mask(a, p, *prims.get_rng_seed_offset(_numel(a)))
     compute = clang.compute_dtype(a.dtype)
     x = clang.maybe_convert_to_dtype(a, compute)
     y = prims.mul(prims.mul(x, clang.maybe_convert_to_dtype(keep, compute)), scale)
     return clang.maybe_convert_to_dtype(y, a.dtype)
+
+
+def _numel(a):
+    n = 1
+    for d in a.shape:
+        n *= d
+    return n
+
+
+def philox_keep_mask(a, p, seed, offset):
+    """Dropout keep-mask from the counter-based RNG: a pure function of (seed, offset), so the
+    backward recomputes it (fused into its kernel) instead of saving it."""
+    r = prims.uniform_philox(tuple(a.shape), 0.0, 1.0, device=a.device, dtype=torch.float32, seed=seed, offset=offset)
+    return clang.lt(r, 1.0 - p)
 
 
 @torchsymbol(*_tfn("nn.functional.scaled_dot_product_attention"))

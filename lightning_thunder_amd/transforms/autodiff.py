@@ -505,6 +505,35 @@ def _install_ltorch_rules():
 
         return out, bwd
 
+    @register_vjp(ltorch.dropout)
+    def _dropout(a, p=0.5, training=True, inplace=False):
+        """The mask is recomputed from (seed, offset) in the backward (K13): nothing but two
+        integers is saved, and hipfuse fuses the regenerated mask into the gradient kernel."""
+        from ..core import prims as _prims
+        from .. import clang as _clang
+
+        pv = pyval(p)
+        if not training or pv == 0.0:
+            return a, lambda g: (g,)
+        if pv == 1.0:
+            out = ltorch.mul(a, 0.0)
+            return out, lambda g: (ltorch.mul(g, 0.0),)
+        scale = 1.0 / (1.0 - pv)
+        n = 1
+        for d in a.shape:
+            n *= d
+        seed, offset = _prims.get_rng_seed_offset(n)
+
+        def apply(t):
+            keep = ltorch.philox_keep_mask(t, pv, seed, offset)
+            compute = _clang.compute_dtype(t.dtype)
+            x = _clang.maybe_convert_to_dtype(t, compute)
+            y = _prims.mul(_prims.mul(x, _clang.maybe_convert_to_dtype(keep, compute)), scale)
+            return _clang.maybe_convert_to_dtype(y, t.dtype)
+
+        out = apply(a)
+        return out, lambda g: (apply(g),)
+
     @register_vjp(ltorch.true_divide)
     def _div(a, b):
         out = ltorch.true_divide(a, b)

@@ -191,3 +191,61 @@ def test_litgpt_partition_cpu(name, cpu_fusion):
                 targs = {p.name: cg.TensorArg(tuple(p.shape), tuple(torch.empty(tuple(p.shape)).stride()), p.dtype, True)
                          for p in f.inputs if isinstance(p, TensorProxy)}
                 hipfuse.compile_source(cg.generate(f.plan, f.inputs, f.outputs, targs))
+
+
+def test_philox_dropout_mask_recomputed(cpu_fusion):
+    """Dropout masks come from the counter-based RNG and are regenerated in the backward."""
+    torch.manual_seed(0)
+
+    def f(x):
+        return torch.nn.functional.dropout(x * 2.0, p=0.3, training=True)
+
+    x = torch.randn(64, 128, requires_grad=True)
+    jf = thunder.jit(f)
+    y = jf(x)
+    keep = y != 0
+    frac = keep.float().mean().item()
+    assert 0.65 < frac < 0.75
+    torch.testing.assert_close(y[keep], (x * 2.0 / 0.7)[keep])
+    g = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, (x,), g)
+    torch.testing.assert_close(gx, torch.where(keep, g * 2.0 / 0.7, torch.zeros_like(g)))
+    bw = thunder.last_backward_traces(jf)[-1]
+    # nothing tensor-valued is saved for the mask: the backward regenerates it
+    assert "uniform_philox" in str(bw)
+    # a second call draws a fresh mask
+    y2 = jf(x)
+    assert not torch.equal(y2 != 0, keep)
+
+
+def test_philox_torch_matches_reference_vectors():
+    from lightning_thunder_amd.core.rng import philox_uniform_torch
+
+    u = philox_uniform_torch((8,), 1234, 0, "cpu")
+    assert ((u >= 0) & (u < 1)).all()
+    v = philox_uniform_torch((8,), 1234, 0, "cpu")
+    assert torch.equal(u, v)
+    w = philox_uniform_torch((8,), 1234, 8, "cpu")
+    assert not torch.equal(u, w)
+
+
+@pytest.mark.gpu
+def test_philox_dropout_gpu_matches_torch_philox():
+    from lightning_thunder_amd.core import rng
+    from lightning_thunder_amd.core.rng import philox_uniform_torch
+
+    def f(x):
+        return torch.nn.functional.dropout(torch.tanh(x), p=0.25, training=True)
+
+    x = torch.randn(256, 384, device="cuda", requires_grad=True)
+    jf = thunder.jit(f)
+    torch.manual_seed(123)
+    rng._state["seed"] = None  # restart the counter for this seed
+    y = jf(x)
+    assert any("uniform_philox" in str(b.subsymbols) for b in hipfuse.fusions(thunder.last_traces(jf)[-1]))
+    keep_ref = philox_uniform_torch(x.shape, 123, 0, "cuda") < 0.75
+    assert torch.equal(y != 0, keep_ref)
+    g = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, (x,), g)
+    ref = torch.where(keep_ref, g / 0.75 * (1 - torch.tanh(x) ** 2), torch.zeros_like(g))
+    torch.testing.assert_close(gx, ref, rtol=1e-4, atol=1e-5)
