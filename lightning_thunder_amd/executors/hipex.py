@@ -253,6 +253,64 @@ def _rms_grad(a, normalized_shape, weight=None, eps=None):
 
 
 # =========================================================================================
+# K5 LayerNorm
+# =========================================================================================
+def _ln_fwd_meta(x, weight, bias, eps):
+    rows = 1
+    for d in x.shape[:-1]:
+        rows *= d
+    st = TensorProxy(like=x, shape=(rows,), dtype=torch.float32, requires_grad=False)
+    return TensorProxy(like=x), st, TensorProxy(like=st)
+
+
+def _ln_fwd_impl(x, weight, bias, eps):
+    from ..ops.rmsnorm import layer_norm_fwd
+
+    return layer_norm_fwd(x, weight, bias, eps)
+
+
+def _ln_bwd_meta(dy, x, weight, mean, rstd, has_bias):
+    return (TensorProxy(like=x), None if weight is None else TensorProxy(like=weight),
+            TensorProxy(like=x, shape=(x.shape[-1],)) if has_bias else None)
+
+
+def _ln_bwd_impl(dy, x, weight, mean, rstd, has_bias):
+    from ..ops.rmsnorm import layer_norm_bwd
+
+    return layer_norm_bwd(dy, x, weight, mean, rstd, has_bias)
+
+
+hip_layer_norm_fwd = ex.register_operator("hip_layer_norm_fwd", meta=_ln_fwd_meta, fn=_ln_fwd_impl)
+hip_layer_norm_bwd = ex.register_operator("hip_layer_norm_bwd", meta=_ln_bwd_meta, fn=_ln_bwd_impl)
+
+
+def _ln_checker(a, normalized_shape, weight=None, bias=None, eps=1e-5):
+    if not _gpu(a, weight, bias) or a.dtype not in _FLOAT16ISH:
+        return False
+    if len(normalized_shape) != 1 or normalized_shape[0] != a.shape[-1]:
+        return False
+    for t in (weight, bias):
+        if t is not None and (t.dtype != a.dtype or tuple(t.shape) != (a.shape[-1],)):
+            return False
+    return True
+
+
+def _ln_exec(a, normalized_shape, weight=None, bias=None, eps=1e-5):
+    y, _, _ = hip_layer_norm_fwd(a, weight, bias, eps)
+    return y
+
+
+def _ln_grad(a, normalized_shape, weight=None, bias=None, eps=1e-5):
+    y, mean, rstd = hip_layer_norm_fwd(a, weight, bias, eps)
+
+    def bwd(g):
+        dx, dw, db = hip_layer_norm_bwd(g, a, weight, mean, rstd, bias is not None)
+        return dx, None, dw, db
+
+    return y, bwd
+
+
+# =========================================================================================
 # K6 fused qkv split + RoPE (lookaside for the LitGPT helper `qkv_split_rope`)
 # =========================================================================================
 def _qkv_rope_meta(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n):
@@ -466,6 +524,7 @@ def _register_all():
     from ..models import litgpt
 
     ex.register_implementation(ltorch.rms_norm, checker=_rms_checker, execution_transform=_rms_exec, grad_transform=_rms_grad)
+    ex.register_implementation(ltorch.layer_norm, checker=_ln_checker, execution_transform=_ln_exec, grad_transform=_ln_grad)
     ex.register_implementation(ltorch.cross_entropy, checker=_ce_checker, execution_transform=_ce_exec, grad_transform=_ce_grad)
     ex.register_implementation(ltorch.scaled_dot_product_attention, checker=_sdpa_checker, execution_transform=_sdpa_exec,
                                grad_transform=_sdpa_grad)

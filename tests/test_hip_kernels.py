@@ -276,3 +276,33 @@ def test_fp8_linear_training_close_to_bf16():
     for a, b in ((gx, rx), (gw, rw)):
         cos = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
         assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [768, 2560, 1000])
+def test_layer_norm_kernel(dtype, cols):
+    import lightning_thunder_amd as thunder
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 33, cols, device="cuda", dtype=dtype, requires_grad=True)
+    w = torch.randn(cols, device="cuda", dtype=dtype, requires_grad=True)
+    b = torch.randn(cols, device="cuda", dtype=dtype, requires_grad=True)
+
+    def f(x, w, b):
+        return torch.nn.functional.layer_norm(x, (cols,), w, b, 1e-5)
+
+    jf = thunder.jit(f)
+    y = jf(x, w, b)
+    assert any("hip_layer_norm" in bb.sym.name for bb in thunder.last_traces(jf)[-1].bound_symbols)
+    g = torch.randn_like(y)
+    grads = torch.autograd.grad(y, (x, w, b), g)
+    xr, wr, br = (t.detach().double().requires_grad_() for t in (x, w, b))
+    yr = f(xr, wr, br)
+    gr = torch.autograd.grad(yr, (xr, wr, br), g.double())
+    ye = f(x, w, b)
+    ge = torch.autograd.grad(ye, (x, w, b), g)
+    for o, r, e in zip((y,) + grads, (yr,) + gr, (ye,) + ge):
+        err = (o.double() - r).abs().max().item()
+        err_e = (e.double() - r).abs().max().item()
+        assert err <= 3 * err_e + 1e-4, (err, err_e)
