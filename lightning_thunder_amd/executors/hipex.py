@@ -253,6 +253,31 @@ def _rms_grad(a, normalized_shape, weight=None, eps=None):
 
 
 # =========================================================================================
+# K10 grouped GEMM (MoE experts)
+# =========================================================================================
+def _gmm_meta(a, b, offs):
+    return TensorProxy(like=a, shape=(a.shape[0], b.shape[2]))
+
+
+def _gmm_impl(a, b, offs):
+    from ..ops.gemm import grouped_mm
+
+    return grouped_mm(a, b, offs)
+
+
+hip_grouped_mm = ex.register_operator("hip_grouped_mm", meta=_gmm_meta, fn=_gmm_impl)
+
+
+def _gmm_checker(a, b, offs=None, bias=None, out_dtype=None):
+    return (_gpu(a, b, offs) and offs is not None and bias is None and out_dtype is None and a.ndim == 2 and b.ndim == 3
+            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16)
+
+
+def _gmm_exec(a, b, offs=None, bias=None, out_dtype=None):
+    return hip_grouped_mm(a, b, offs)
+
+
+# =========================================================================================
 # K5 LayerNorm
 # =========================================================================================
 def _ln_fwd_meta(x, weight, bias, eps):
@@ -525,6 +550,7 @@ def _register_all():
 
     ex.register_implementation(ltorch.rms_norm, checker=_rms_checker, execution_transform=_rms_exec, grad_transform=_rms_grad)
     ex.register_implementation(ltorch.layer_norm, checker=_ln_checker, execution_transform=_ln_exec, grad_transform=_ln_grad)
+    ex.register_implementation(ltorch._grouped_mm, checker=_gmm_checker, execution_transform=_gmm_exec)
     ex.register_implementation(ltorch.cross_entropy, checker=_ce_checker, execution_transform=_ce_exec, grad_transform=_ce_grad)
     ex.register_implementation(ltorch.scaled_dot_product_attention, checker=_sdpa_checker, execution_transform=_sdpa_exec,
                                grad_transform=_sdpa_grad)

@@ -245,8 +245,23 @@ _register_prim(prims.cumsum, lambda a, dim, *, dtype=None: torch.cumsum(a, dim, 
 # linear algebra / nn
 _register_prim(prims.matmul, torch.matmul, name="matmul")
 _register_prim(prims.linear, torch.nn.functional.linear, name="linear")
-if hasattr(torch, "_grouped_mm"):
-    _register_prim(prims._grouped_mm, lambda a, b, offsets: torch._grouped_mm(a, b, offsets), name="grouped_mm")
+def _grouped_mm_impl(a, b, offsets):
+    if a.is_cuda and hasattr(torch, "_grouped_mm") and a.dtype == torch.bfloat16:
+        return torch._grouped_mm(a, b, offsets)
+    # reference loop (CPU): group g owns rows/K-slices [offsets[g-1], offsets[g])
+    ends = offsets.tolist()
+    starts = [0] + ends[:-1]
+    if a.dim() == 2 and b.dim() == 3:
+        out = a.new_zeros((a.shape[0], b.shape[2]))
+        for g, (s, e) in enumerate(zip(starts, ends)):
+            out[s:e] = a[s:e] @ b[g]
+        return out
+    if a.dim() == 2 and b.dim() == 2:  # shared dim grouped: [G, M, N]
+        return torch.stack([a[:, s:e] @ b[s:e] for s, e in zip(starts, ends)])
+    raise NotImplementedError("grouped_mm layout")
+
+
+_register_prim(prims._grouped_mm, _grouped_mm_impl, name="grouped_mm")
 
 
 def _embedding(a, weight, *, padding_idx=-1, max_norm=None, norm_type=2.0, scale_grad_by_freq=False, sparse=False):

@@ -45,6 +45,8 @@ class Config:
     shared_attention_norm: bool = False
     gelu_approximate: str = "none"
     tie_embeddings: bool = False
+    n_expert: int = 0
+    n_expert_per_token: int = 0
 
     def __post_init__(self):
         if self.head_size is None:
@@ -96,6 +98,12 @@ configs = [
     Config(name="gpt-neox-like", vocab_size=320, padding_multiple=64, n_layer=2, n_head=4, n_embd=64, block_size=128,
            norm_class_name="LayerNorm", mlp_class_name="GptNeoxMLP", bias=True, parallel_residual=True,
            rotary_percentage=0.25),
+    # Mixtral-style sparse MoE (litgpt "LLaMAMoE"): 8 experts, top-2 routing
+    Config(name="Mixtral-8x7B-v0.1", vocab_size=32000, padding_multiple=512, n_layer=32, n_head=32, n_embd=4096,
+           n_query_groups=8, intermediate_size=14336, mlp_class_name="LLaMAMoE", n_expert=8, n_expert_per_token=2,
+           rope_base=1000000, norm_eps=1e-5),
+    Config(name="mixtral-like", vocab_size=320, padding_multiple=64, n_layer=2, n_head=4, n_embd=256, n_query_groups=2,
+           intermediate_size=512, mlp_class_name="LLaMAMoE", n_expert=4, n_expert_per_token=2),
     Config(name="llama2-7b-shape-2l", vocab_size=32000, padding_multiple=64, n_layer=2, n_head=32, n_embd=4096,
            intermediate_size=11008),
 ]
@@ -206,13 +214,56 @@ class GptNeoxMLP(nn.Module):
         return self.proj(x)
 
 
+class LLaMAMoE(nn.Module):
+    """Sparse MoE MLP (litgpt ``LLaMAMoE``): softmax top-k router, tokens sorted by expert and run
+    through *grouped* GEMMs (``torch._grouped_mm`` -> the K10 HIP kernel on MI355X), combined with
+    the routing weights.  Expert weights are stored [E, out, in] like ``nn.Linear``."""
+
+    def __init__(self, config: Config):
+        super().__init__()
+        E, D, I = config.n_expert, config.n_embd, config.intermediate_size
+        self.gate = nn.Linear(D, E, bias=False)
+        self.fc_1 = nn.Parameter(torch.empty(E, I, D))
+        self.fc_2 = nn.Parameter(torch.empty(E, I, D))
+        self.proj = nn.Parameter(torch.empty(E, D, I))
+        for w in (self.fc_1, self.fc_2, self.proj):
+            nn.init.normal_(w, std=0.02)
+        self.config = config
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, T, D = x.shape
+        E, k = self.config.n_expert, self.config.n_expert_per_token
+        xf = x.reshape(-1, D)
+        probs = torch.softmax(self.gate(xf).float(), dim=-1)
+        weights, experts = torch.topk(probs, k, dim=-1)                       # [N, k]
+        weights = (weights / weights.sum(-1, keepdim=True)).to(x.dtype)
+        flat_e = experts.reshape(-1)                                          # [N*k]
+        order = torch.argsort(flat_e, stable=True)
+        token = torch.div(order, k, rounding_mode="floor")
+        counts = torch.nn.functional.one_hot(flat_e, E).sum(0)
+        offs = torch.cumsum(counts, 0).to(torch.int32)
+        xs = xf[token]                                                        # [N*k, D] sorted by expert
+        a = torch._grouped_mm(xs, self.fc_1.transpose(1, 2), offs)
+        b = torch._grouped_mm(xs, self.fc_2.transpose(1, 2), offs)
+        h = swiglu(a, b)
+        ys = torch._grouped_mm(h, self.proj.transpose(1, 2), offs)            # [N*k, D]
+        ys = ys * weights.reshape(-1)[order].unsqueeze(-1)
+        out = torch.zeros_like(xf).index_add(0, token, ys)
+        return out.reshape(B, T, D)
+
+
 class Block(nn.Module):
     def __init__(self, config: Config):
         super().__init__()
         self.norm_1 = _norm(config, config.n_embd)
         self.attn = CausalSelfAttention(config)
         self.norm_2 = None if config.shared_attention_norm else _norm(config, config.n_embd)
-        self.mlp = LLaMAMLP(config) if config.mlp_class_name == "LLaMAMLP" else GptNeoxMLP(config)
+        if config.mlp_class_name == "LLaMAMLP":
+            self.mlp = LLaMAMLP(config)
+        elif config.mlp_class_name == "LLaMAMoE":
+            self.mlp = LLaMAMoE(config)
+        else:
+            self.mlp = GptNeoxMLP(config)
         self.config = config
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:

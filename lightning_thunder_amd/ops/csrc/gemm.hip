@@ -305,6 +305,122 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K10: grouped NT GEMM for mixture-of-experts: rows [off[g-1], off[g]) of A are multiplied by
+// expert g's weight W[g] ([N, K], K-contiguous like nn.Linear), out[M, N] bf16.  The grid is
+// sized for the worst case (ceil(M/256) + G row tiles per column tile); each workgroup finds
+// its (expert, row tile) by scanning the device offsets, so no host synchronisation is needed.
+// Rows past a group's end are clamped on load and masked on store.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHR, 1) void gemm_grouped_nt_bf16_kernel(const __hip_bfloat16* __restrict__ A,
+                                                                       const __hip_bfloat16* __restrict__ W,
+                                                                       __hip_bfloat16* __restrict__ C,
+                                                                       const int* __restrict__ offs, int G, int M,
+                                                                       int N, int K, int64_t wstride) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  // locate (expert, row tile)
+  int slot = blockIdx.x, g = 0, start = 0, end = 0;
+  bool found = false;
+  for (; g < G; ++g) {
+    end = offs[g];
+    const int tiles = (end - start + BM - 1) / BM;
+    if (slot < tiles) {
+      found = true;
+      break;
+    }
+    slot -= tiles;
+    start = end;
+  }
+  if (!found) return;  // uniform across the workgroup: no barrier skipped by part of it
+  const int m0 = start + slot * BM, n0 = blockIdx.y * BN;
+  const __hip_bfloat16* B = W + (int64_t)g * wstride;
+  const int last = end - 1;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int k0, char* sbase) {
+    const int r = lane >> 3, p = lane & 7;
+    const int c = p ^ r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;
+      const int row = min(m0 + chunk * 8 + r, last);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * K + k0 + c * 8),
+                                       (lds_void*)(sbase + chunk * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;
+      const int row = n0 + chunk * 8 + r;
+      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)row * K + k0 + c * 8),
+                                       (lds_void*)(sbase + TILE_BYTES + chunk * 1024), 16, 0, 0);
+    }
+  };
+  const int nk = K / BK;
+  stage(0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) stage((t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int row = wm * 128 + m * 16 + fr;
+        af[m] = *reinterpret_cast<const bf16x8*>(cur + row * 128 + ((c ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row = wn * 64 + n * 16 + fr;
+        bfr[n] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + row * 128 + ((c ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) =
+            __float2bfloat16(acc[m][n][j]);
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    const int grow = m0 + wm * 128 + row;
+    if (grow < end) {
+      const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+      *reinterpret_cast<uint4*>(C + (int64_t)grow * N + n0 + wn * 64 + ch * 8) = v;
+    }
+  }
+}
+
 template <int ACT>
 int launch_act(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
                int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
@@ -340,6 +456,16 @@ LTA_EXPORT int lta_gemm_nt_fp8(const void* A, const void* B, void* C, const void
   else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_F8(0, 1, true); else LTA_F8(0, 1, false); }
   else return -1;
 #undef LTA_F8
+  return (int)hipGetLastError();
+}
+
+// out[M, N] = A[rows of g] @ W[g]^T for g in 0..G-1; offs = int32 end offsets (device), W [G, N, K].
+LTA_EXPORT int lta_gemm_grouped_nt_bf16(const void* A, const void* W, void* C, const void* offs, int G, int M, int N,
+                                        int K, int64_t wstride, hipStream_t stream) {
+  if (N % BN || K % BK) return -2;
+  dim3 grid((M + BM - 1) / BM + G, N / BN), block(NTHR);
+  hipLaunchKernelGGL(gemm_grouped_nt_bf16_kernel, grid, block, 0, stream, (const __hip_bfloat16*)A,
+                     (const __hip_bfloat16*)W, (__hip_bfloat16*)C, (const int*)offs, G, M, N, K, wstride);
   return (int)hipGetLastError();
 }
 

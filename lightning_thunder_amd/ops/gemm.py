@@ -118,3 +118,35 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
 def selection_table() -> dict:
     """(M, N, K, bias, residual, act) -> True if the HIP kernel was selected."""
     return dict(_choice)
+
+
+# ---------------------------------------------------------------------------------------------
+# K10 grouped GEMM (mixture of experts)
+# ---------------------------------------------------------------------------------------------
+from ._lib import c_int64  # noqa: E402
+
+register_signature("lta_gemm_grouped_nt_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                                c_int64, c_void_p])
+
+
+def grouped_nt_supported(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> bool:
+    """a [M, K]; b [G, K, N] given as the transpose of a K-contiguous [G, N, K] weight."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 3):
+        return False
+    G, K, N = b.shape
+    if a.shape[1] != K or N % TILE_N or K % TILE_K or offs.dtype != torch.int32 or offs.numel() != G:
+        return False
+    return a.is_contiguous() and b.stride(1) == 1 and b.stride(2) == K and a.data_ptr() % 16 == 0
+
+
+def grouped_mm(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """out[M, N] = a[rows of group g] @ b[g] (offs: int32 cumulative row ends)."""
+    if not grouped_nt_supported(a, b, offs):
+        return torch._grouped_mm(a, b, offs)
+    lib = require()
+    G, K, N = b.shape
+    M = a.shape[0]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    check(lib.lta_gemm_grouped_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
+                                       b.stride(0), stream_ptr(a.device)), "lta_gemm_grouped_nt_bf16")
+    return out

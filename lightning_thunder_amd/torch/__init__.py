@@ -1066,8 +1066,8 @@ def _getitem_sym(a, key):
         return _advanced_getitem(a, key)
     # expand ellipsis
     n_specified = builtins.sum(1 for k in key if k is not None and k is not Ellipsis)
-    if Ellipsis in key:
-        i = key.index(Ellipsis)
+    if builtins.any(k is Ellipsis for k in key):
+        i = next(j for j, k in enumerate(key) if k is Ellipsis)
         key = key[:i] + (slice(None),) * (a.ndim - n_specified) + key[i + 1:]
     else:
         key = key + (slice(None),) * (a.ndim - n_specified)
@@ -1117,7 +1117,7 @@ def _getitem_sym(a, key):
 def _advanced_getitem(a, key):
     # Supports a single tensor index in one position (possibly with basic slices elsewhere).
     positions = [i for i, k in enumerate(key) if isinstance(k, TensorProxy)]
-    if len(positions) == 1 and Ellipsis not in key and None not in key:
+    if len(positions) == 1 and not builtins.any(k is Ellipsis or k is None for k in key):
         p = positions[0]
         idx = key[p]
         if idx.dtype == torch.bool:

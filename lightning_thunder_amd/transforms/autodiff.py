@@ -237,7 +237,7 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
 
     def process(bsym: BoundSymbol, recompute: bool = False):
         nonlocal ret_bsym
-        b = bsym.swap_proxies(swap, skip_output=True, skip_subsymbols=True)
+        b = bsym.swap_proxies(swap, skip_output=True)
         if b.sym.id == PrimIDs.RETURN:
             ret_bsym = b
             return
@@ -607,6 +607,18 @@ def _install_ltorch_rules():
     def _linear(a, w, bias=None):
         out = ltorch.linear(a, w, bias)
         return out, lambda g: linear_backward(a, w, bias, g)
+
+    @register_vjp(ltorch._grouped_mm)
+    def _grouped_mm_vjp(a, b, offs=None, bias=None, out_dtype=None):
+        """MoE expert GEMM: out[rows of g] = a[rows of g] @ b[g] (2-D x 3-D form)."""
+        out = ltorch._grouped_mm(a, b, offs)
+
+        def bwd(g):
+            ga = ltorch._grouped_mm(g, ltorch.transpose(b, -1, -2), offs) if rg(a) else None
+            gb = ltorch._grouped_mm(ltorch.transpose(a, 0, 1), g, offs) if rg(b) else None
+            return ga, gb
+
+        return out, bwd
 
     @register_vjp(ltorch.matmul)
     def _matmul(a, b):

@@ -112,3 +112,55 @@ def test_hip_linear_residual_epilogue_fusion():
     (gx,) = torch.autograd.grad(out, (x,), g)
     (rx,) = torch.autograd.grad(ref, (x,), g)
     torch.testing.assert_close(gx, rx, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_grouped_mm_kernel():
+    from lightning_thunder_amd.ops.gemm import grouped_mm, grouped_nt_supported
+
+    torch.manual_seed(0)
+    G, M, K, N = 5, 900, 256, 512
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(G, N, K, device="cuda", dtype=torch.bfloat16) / 16
+    ends = torch.tensor([0, 37, 300, 300, 900], device="cuda", dtype=torch.int32)  # an empty group too
+    b = w.transpose(1, 2)
+    assert grouped_nt_supported(a, b, ends)
+    out = grouped_mm(a, b, ends)
+    starts = [0] + ends.tolist()[:-1]
+    ref = torch.zeros(M, N, device="cuda")
+    for g, (s, e) in enumerate(zip(starts, ends.tolist())):
+        ref[s:e] = a[s:e].float() @ w[g].float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.gpu
+def test_moe_model_fp32_matches_eager():
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = GPT.from_name("mixtral-like").to(device=dev)
+    m.set_rope_cache(64, device=dev)
+    idx = torch.randint(0, 320, (2, 64), device=dev)
+    tm = thunder.jit(m)
+    out = tm(idx)
+    ref = m(idx)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(out)
+    gj = torch.autograd.grad(out, list(m.parameters()), g)
+    gr = torch.autograd.grad(ref, list(m.parameters()), g)
+    for a, b in zip(gj, gr):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_moe_model_bf16_uses_grouped_kernel():
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = GPT.from_name("mixtral-like").to(device=dev, dtype=torch.bfloat16)
+    m.set_rope_cache(64, device=dev)
+    idx = torch.randint(0, 320, (2, 64), device=dev)
+    tm = thunder.jit(m)
+    out = tm(idx)
+    assert torch.isfinite(out).all()
+    out.float().sum().backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+    assert "hip_grouped_mm" in str(thunder.last_traces(tm)[-1])
