@@ -90,6 +90,7 @@ class CacheEntry:
         self.grad_enabled = False
         self.uses_autograd = False
         self.no_grad_sync = False
+        self.alias_pattern = None
         self.grad_input_indices = []
         self.diff_output_mask = []
         self.diff_output_meta = []
@@ -137,6 +138,9 @@ def _check_traces(traces, cd):
             check_trace(t)
 
 
+from .core.functionalization import storage_alias_pattern  # noqa: E402
+
+
 def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) -> CacheEntry:
     from .core.jit_ext import acquire
     from .executors.passes import transform_for_execution, del_last_used
@@ -175,6 +179,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         computation_traces.append(comp)
 
         entry.param_accessors = prog.param_accessors
+        entry.alias_pattern = prog.alias_pattern
         entry.constants = prog.constants
         entry.epilogue_writes = prog.epilogue_writes
         entry.has_epilogue = bool(prog.epilogue_writes)
@@ -307,6 +312,8 @@ def jit(
         if cd.cache_option is not CACHE_OPTIONS.NO_CACHING:
             for entry in reversed(cs.interpreter_cache):
                 if entry.grad_enabled != grad_enabled or entry.autocast_key != ac or entry.no_grad_sync != nosync:
+                    continue
+                if entry.alias_pattern is not None and storage_alias_pattern(flat_args) != entry.alias_pattern:
                     continue
                 if cd.cache_option is CACHE_OPTIONS.SAME_INPUT:
                     inps = _same_input(entry, flat_args)

@@ -28,6 +28,7 @@ from .proxies import Proxy, TensorProxy, NumberProxy, AnyProxy, tensorproxy, Pro
 from .pytree import tree_flatten, tree_unflatten, tree_map
 from .trace import TraceCtx, tracectx, get_tracectx, TraceProvenance
 from .symbol import BoundSymbol
+from .functionalization import AliasTracker, storage_alias_pattern
 
 
 # -----------------------------------------------------------------------------------------
@@ -48,6 +49,9 @@ class _AcquisitionState:
         p.requires_grad = False if not t.requires_grad else True
         p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
         self.constants[id(t)] = (t, p)
+        trc = get_tracectx()
+        if trc is not None and trc.alias_tracker is not None:
+            trc.alias_tracker.register_input(p)
         return p
 
 
@@ -198,6 +202,7 @@ class AcquiredProgram:
         self.constants: list[torch.Tensor] = []
         self.output_spec = None
         self.epilogue_writes: list[tuple[torch.nn.Module, str]] = []
+        self.alias_pattern = None
 
 
 def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
@@ -234,17 +239,34 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
     prog.arg_spec = arg_spec
     swapped: list[tuple[dict, str, Any]] = []
     attr_swaps: list[tuple[torch.nn.Module, str, Any]] = []
+    tracker = AliasTracker(comp)
+    tracker.input_specs = prog.input_specs
+    comp.alias_tracker = tracker
 
     with tracectx(comp):
-        # 1. tensor arguments
+        # 1. tensor arguments (a tensor passed twice is an identity view of its first occurrence;
+        #    partially overlapping arguments may not be mutated)
         proxied_flat = []
         arg_proxies = []
+        by_view: dict = {}
+        by_storage: dict = {}
         for i, x in enumerate(flat_args):
             if isinstance(x, torch.Tensor):
                 p = tensorproxy(x)
                 arg_proxies.append((i, p))
                 proxied_flat.append(p)
                 prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
+                tracker.register_input(p)
+                if x.device.type != "meta":
+                    sp = x.untyped_storage().data_ptr()
+                    key = (sp, x.storage_offset(), tuple(x.shape), tuple(x.stride()), x.dtype)
+                    if key in by_view:
+                        tracker.register_identity_alias(p, by_view[key])
+                    else:
+                        by_view[key] = p
+                        if sp in by_storage:
+                            tracker.partial_alias.update((id(p), id(by_storage[sp])))
+                        by_storage.setdefault(sp, p)
             else:
                 proxied_flat.append(x)
         pargs, pkwargs = tree_unflatten(proxied_flat, arg_spec)
@@ -271,6 +293,7 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                         p.tags.add("parameter")
                         seen[id(param)] = p
                         prog.input_specs.append(InputSpec("param", path=full, proxy=p, module_path=mpath, attr=pname))
+                        tracker.register_input(p)
                         prog.param_accessors.append((m, pname, "param"))
                     swapped.append((m._parameters, pname, param))
                     m._parameters[pname] = p
@@ -285,6 +308,7 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                         p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
                         seen[id(buf)] = p
                         prog.input_specs.append(InputSpec("buffer", path=full, proxy=p, module_path=mpath, attr=bname))
+                        tracker.register_input(p)
                         prog.param_accessors.append((m, bname, "buffer"))
                     swapped.append((m._buffers, bname, buf))
                     m._buffers[bname] = p
@@ -297,6 +321,7 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                     p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
                     seen[id(v)] = p
                     prog.input_specs.append(InputSpec("attr", path=full, proxy=p, module_path=mpath, attr=k))
+                    tracker.register_input(p)
                     prog.param_accessors.append((m, k, "attr"))
                 attr_swaps.append((m, k, v))
                 object.__setattr__(m, k, p)
@@ -333,7 +358,7 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
         # 3. captured constants become inputs
         for t, p in state.constants.values():
             prog.constants.append(t)
-            prog.input_specs.append(InputSpec("const", proxy=p, value=t))
+            prog.input_specs.append(InputSpec("const", proxy=tracker.original(p), value=t))
 
         # 4. epilogue writes are returned from the computation
         prog.epilogue_writes = [(m, k) for m, k, v in writes]
@@ -346,10 +371,14 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             return x
 
         result = tree_map(fix_out, result)
+        epi_values = [tracker.refresh(v) or v for v in epi_values]
+        result = tracker.finish(result)
+        comp.alias_tracker = None
+        prog.alias_pattern = storage_alias_pattern(flat_args) if tracker.any_mutation else None
         for t, p in state.constants.values():
             if all(t is not c for c in prog.constants):
                 prog.constants.append(t)
-                prog.input_specs.append(InputSpec("const", proxy=p, value=t))
+                prog.input_specs.append(InputSpec("const", proxy=tracker.original(p), value=t))
         if epi_values:
             prims.python_return((result, tuple(epi_values)))
         else:

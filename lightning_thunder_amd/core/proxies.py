@@ -440,6 +440,8 @@ class TensorProxy(Proxy):
         ltorch = _ltorch()
         method = ltorch.get_method(attr)
         if method is None:
+            method = ltorch.resolve_fallback_method(attr)
+        if method is None:
             raise AttributeError(f"TensorProxy has no attribute or method '{attr}' in the torch language context")
 
         tmethod = getattr(torch.Tensor, attr, None)

@@ -131,6 +131,9 @@ class Symbol:
 
         called_fn = CALLED_TORCH_FN[0]
         CALLED_TORCH_FN[0] = None
+        tracker = trace.alias_tracker if len(trace.scopes) == 1 else None
+        if tracker is not None:
+            tracker.before_call(args, kwargs)
         # While a meta runs, torch calls made by the compiler itself (e.g. meta-tensor shape
         # inference) must execute eagerly instead of being traced by the acquisition mode.
         META_DEPTH[0] += 1
@@ -158,6 +161,8 @@ class Symbol:
         if called_fn is not None:
             bsym.torch_fn = called_fn
         trace.add_bound_symbol(bsym)
+        if tracker is not None:
+            result = tracker.after_call(bsym, result)
         return result
 
 

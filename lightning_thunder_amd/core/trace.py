@@ -97,6 +97,8 @@ class TraceCtx:
         self.autocast_dtype = None
         self.ignored_names: set[str] = set()
         self.unpack_list_arg = False
+        # set by the acquisition frontend (core/functionalization.AliasTracker)
+        self.alias_tracker = None
 
     # --- names ------------------------------------------------------------------------
     def add_name(self, name: str) -> None:

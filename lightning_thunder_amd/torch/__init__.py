@@ -62,6 +62,29 @@ def get_method(name: str):
     return _methods.get(name)
 
 
+def resolve_fallback_method(name: str):
+    """Tensor methods without a hand-written symbol: ``foo_`` becomes the out-of-place ``foo``
+    plus ``copy_`` (functionalized by the frontend), anything else an auto-registered opaque op."""
+    tm = getattr(torch.Tensor, name, None)
+    if tm is None or not callable(tm):
+        return None
+    if name.endswith("_") and not name.endswith("__"):
+        base = _methods.get(name[:-1])
+        if base is None and callable(getattr(torch.Tensor, name[:-1], None)):
+            from .default_torch_ops import opaque_symbol
+
+            base = opaque_symbol(getattr(torch.Tensor, name[:-1]))
+        if base is None:
+            return None
+        sym = _inplace(name, base)
+    else:
+        from .default_torch_ops import opaque_symbol
+
+        sym = opaque_symbol(tm)
+    _methods[name] = sym
+    return sym
+
+
 def _tfn(*names):
     """Resolves torch callables by dotted name, skipping ones missing in this torch build."""
     out = []

@@ -388,6 +388,7 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
 
     saved_tensors = [p for p in free.values() if isinstance(p, TensorProxy)]
     saved_other = [p for p in free.values() if not isinstance(p, TensorProxy)]
+    saved_tensors = _protect_saved_from_writeback(fw, bw, saved_tensors)
     bw.args = saved_tensors + saved_other + cotangent_args
     bw.set_provenance(TraceProvenance(f"Backward pass (took {(time.perf_counter_ns() - start) // 1000000} milliseconds)"))
 
@@ -398,6 +399,39 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
     fw.set_provenance(TraceProvenance(f"Augmented forward pass (took {(time.perf_counter_ns() - start) // 1000000} milliseconds)"))
     return ForwardBackward(fw, bw, saved_tensors, saved_other, grad_input_indices, diff_output_mask)
 
+
+def _protect_saved_from_writeback(fw: TraceCtx, bw: TraceCtx, saved: list) -> list:
+    """Inputs mutated by the forward (functionalized in-place ops end in one ``copy_`` write-back,
+    see ``core/functionalization.py``) keep their pre-mutation value for the backward: the saved
+    tensor becomes a clone taken just before the write-back."""
+    names = {p.name for p in saved}
+    swap: dict[str, Proxy] = {}
+    i = 0
+    while i < len(fw.bound_symbols):
+        b = fw.bound_symbols[i]
+        if b.sym.id == PrimIDs.COPY_ and isinstance(b.args[1], TensorProxy) and b.args[1].name in names:
+            dst = b.args[1]
+            if dst.name not in swap:
+                from .. import torch as ltorch
+
+                base = f"{dst.name}_saved"
+                name, k = base, 0
+                while name in fw.names or name in bw.names:
+                    k += 1
+                    name = f"{base}{k}"
+                with tracectx(fw):
+                    c = TensorProxy(name, like=dst)
+                bw.names.add(name)
+                sub = prims.shallow_copy.bind(dst, output=c)
+                fw.bound_symbols.insert(i, ltorch.clone.bind(dst, output=c, subsymbols=[sub]))
+                i += 1
+                swap[dst.name] = c
+        i += 1
+    if not swap:
+        return saved
+    bw.bound_symbols = [b.swap_proxies(swap) for b in bw.bound_symbols]
+    bw.scopes = [bw.bound_symbols]
+    return [swap.get(p.name, p) for p in saved]
 
 def _insert_recomputation(fw, bw, free, recompute_names, cotangent_args):
     """Moves RECOMPUTE_IN_BACKWARD producers needed by the backward into the backward (reference :363-432)."""

@@ -1,0 +1,163 @@
+"""In-place ops and aliasing (parity: reference ``thunder/tests/test_inplace_functionalization.py``,
+``test_update_aliases.py``).  CPU, torch executor; compared against eager PyTorch."""
+import pytest
+import torch
+
+import lightning_thunder_amd as thunder
+
+
+def _check(f, *args):
+    a1 = [t.clone() if isinstance(t, torch.Tensor) else t for t in args]
+    a2 = [t.clone() if isinstance(t, torch.Tensor) else t for t in args]
+    expected = f(*a1)
+    jf = thunder.jit(f)
+    got = jf(*a2)
+    torch.testing.assert_close(got, expected)
+    for p, q in zip(a1, a2):
+        if isinstance(p, torch.Tensor):
+            torch.testing.assert_close(q, p)
+    return jf
+
+
+def test_inplace_on_intermediate_is_functionalized():
+    def f(x):
+        y = x * 2
+        y.add_(1)
+        y.mul_(y)
+        return y * 3
+
+    jf = _check(f, torch.randn(4, 5))
+    src = str(thunder.last_traces(jf)[-1])
+    assert "copy_" not in src  # nothing to write back
+
+
+def test_inplace_through_view_updates_input():
+    def f(x):
+        v = x.view(-1)
+        v.mul_(2)
+        return x + 1
+
+    _check(f, torch.randn(2, 3))
+
+
+def test_setitem_and_views_of_intermediate():
+    def f(x):
+        y = x.clone()
+        z = y[0]
+        w = y[:, 1]
+        z.fill_(0)
+        return y + w.sum()
+
+    _check(f, torch.randn(3, 4))
+
+
+def test_input_mutation_and_alias_args():
+    def f(a, b):
+        a.add_(1)
+        return b * 2
+
+    jf = thunder.jit(f)
+    t = torch.zeros(3)
+    torch.testing.assert_close(jf(t, t), torch.full((3,), 2.0))
+    torch.testing.assert_close(t, torch.ones(3))
+    t1, t2 = torch.zeros(3), torch.zeros(3)
+    torch.testing.assert_close(jf(t1, t2), torch.zeros(3))
+    torch.testing.assert_close(t1, torch.ones(3))
+    assert thunder.cache_misses(jf) == 2  # different storage-aliasing pattern -> new entry
+
+
+def test_generic_inplace_method_fallback():
+    def f(x, idx, src):
+        y = x.clone()
+        y.index_copy_(0, idx, src)
+        y.clamp_(min=-0.5)
+        return y
+
+    _check(f, torch.randn(5, 3), torch.tensor([1, 3]), torch.randn(2, 3))
+
+
+def test_inplace_grad_matches_eager():
+    def g(x, w):
+        y = x * w
+        y[0].mul_(3)
+        z = y.view(-1)
+        z.add_(1)
+        return (y * y).sum()
+
+    x = torch.randn(3, 4)
+    w1 = torch.randn(3, 4, requires_grad=True)
+    w2 = w1.detach().clone().requires_grad_()
+    e = g(x, w1)
+    e.backward()
+    r = thunder.jit(g)(x, w2)
+    r.backward()
+    torch.testing.assert_close(r, e)
+    torch.testing.assert_close(w2.grad, w1.grad)
+
+
+class _M(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(4, 4)
+        self.register_buffer("cnt", torch.zeros(4))
+        self.register_buffer("cache", torch.zeros(8, 4))
+
+    def forward(self, x, pos):
+        h = torch.nn.functional.relu(self.lin(x), inplace=True)
+        self.cnt.add_(h.detach().sum(0))
+        self.cache[pos] = h[0].detach()
+        return (h * self.cnt).sum()
+
+
+def test_module_buffers_updated_in_place():
+    m1 = _M()
+    m2 = _M()
+    m2.load_state_dict(m1.state_dict())
+    jm = thunder.jit(m2)
+    for _ in range(3):
+        x = torch.randn(2, 4)
+        e = m1(x, 2)
+        e.backward()
+        r = jm(x, 2)
+        r.backward()
+        torch.testing.assert_close(r, e)
+        torch.testing.assert_close(m2.cnt, m1.cnt)
+        torch.testing.assert_close(m2.cache, m1.cache)
+        torch.testing.assert_close(m2.lin.weight.grad, m1.lin.weight.grad)
+    assert thunder.cache_misses(jm) == 1
+
+
+def test_saved_input_keeps_pre_mutation_value():
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.randn(4))
+            self.register_buffer("b", torch.randn(4))
+
+        def forward(self, x):
+            y = (self.w * self.b * x).sum()
+            self.b.mul_(0.5)
+            return y
+
+    m = M()
+    b0 = m.b.clone()
+    x = torch.randn(4)
+    jm = thunder.jit(m)
+    jm(x).backward()
+    torch.testing.assert_close(m.b, b0 * 0.5)
+    torch.testing.assert_close(m.w.grad, b0 * x)
+
+
+def test_leaf_parameter_inplace_raises():
+    with pytest.raises(RuntimeError, match="leaf Variable"):
+        thunder.jit(_Mut(torch.nn.Linear(3, 3)))(torch.randn(2, 3))
+
+
+class _Mut(torch.nn.Module):
+    def __init__(self, lin):
+        super().__init__()
+        self.lin = lin
+
+    def forward(self, x):
+        self.lin.weight.add_(1)
+        return self.lin(x)
