@@ -198,6 +198,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         executors = cd.executors_list
         if requires_grad:
             fb = forward_and_backward_from_trace(comp, executors=executors)
+            if cd.compile_options.get("rematerialize", True):
+                from .transforms.rematerialization import rematerialize_forward_and_backward
+
+                fb = rematerialize_forward_and_backward(fb)
             fw_traces = [fb.forward_trace] + transform_for_execution(fb.forward_trace, executors)
             bw_traces = [fb.backward_trace] + transform_for_execution(fb.backward_trace, executors)
             fw = fw_traces[-1]
