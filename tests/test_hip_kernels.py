@@ -306,3 +306,21 @@ def test_layer_norm_kernel(dtype, cols):
         err = (o.double() - r).abs().max().item()
         err_e = (e.double() - r).abs().max().item()
         assert err <= 3 * err_e + 1e-4, (err, err_e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 7, 256, 600])
+def test_fp8_inference_linear_gpu(M):
+    from lightning_thunder_amd.transforms.fp8_inference import fp8_linear_inference, quantize_weight_e4m3, dequantize_e4m3
+
+    torch.manual_seed(0)
+    N, K = 512, 1024
+    w = torch.randn(N, K, device="cuda") / K ** 0.5
+    q, s = quantize_weight_e4m3(w)
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(2, M, K, device="cuda", dtype=torch.bfloat16)
+    y = fp8_linear_inference(x, q, s, bias)
+    ref = x.float() @ dequantize_e4m3(q, s, torch.float32).t() + bias.float()
+    assert y.shape == (2, M, N) and y.dtype == torch.bfloat16
+    err = (y.float() - ref).abs().max() / ref.abs().max()
+    assert err < 0.06, err

@@ -224,3 +224,22 @@ def test_numpy_language_and_langctx():
     with langctx(Languages.NUMPY):
         assert resolve_method("size") is lnp.size
     assert resolve_method("sum") is not None
+
+
+def test_fp8_inference_transform_cpu():
+    from lightning_thunder_amd.transforms.fp8_inference import FP8InferenceTransform, quantize_weight_e4m3, dequantize_e4m3
+
+    torch.manual_seed(0)
+    w = torch.randn(64, 128)
+    q, s = quantize_weight_e4m3(w)
+    assert q.dtype == torch.uint8 and s.shape == ()
+    assert (dequantize_e4m3(q, s, torch.float32) - w).abs().max() / w.abs().max() < 0.07
+    m = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.GELU(), torch.nn.Linear(64, 32))
+    x = torch.randn(4, 128, requires_grad=True)
+    ref = m(x)
+    jm = thunder.jit(m, transforms=[FP8InferenceTransform(skip=())])
+    out = jm(x)
+    assert (out - ref).abs().max() / ref.abs().max() < 0.1
+    out.sum().backward()
+    assert x.grad is not None
+    assert any("fp8_linear_inference" in b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols)
