@@ -162,6 +162,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         for ex in cd.executors_list:
             lookasides.update(ex._lookasides)
             python_lookasides.extend(getattr(ex, "_python_lookasides", ()))
+        if _torch.distributed.is_available():
+            from .distributed.dtensor import python_lookasides as _dt_lookasides
+
+            python_lookasides.extend(_dt_lookasides())
         from .transforms.autocast import autocast_ctx
 
         with autocast_ctx(entry.autocast_key):

@@ -24,7 +24,7 @@ from torch.overrides import TorchFunctionMode
 
 from . import prims
 from .codeutils import sanitize_name
-from .proxies import Proxy, TensorProxy, NumberProxy, AnyProxy, tensorproxy, ProxyTag
+from .proxies import Proxy, TensorProxy, DTensorProxy, NumberProxy, AnyProxy, tensorproxy, ProxyTag
 from .pytree import tree_flatten, tree_unflatten, tree_map
 from .trace import TraceCtx, tracectx, get_tracectx, TraceProvenance
 from .symbol import BoundSymbol
@@ -126,6 +126,11 @@ def dispatch_torch_function(func, args, kwargs):
         if changed:
             args, kwargs = tree_unflatten(nflat, spec)
 
+    if has_proxy and any(isinstance(x, DTensorProxy) for x in flat):
+        from ..distributed.dtensor import dtensor_symbol
+
+        return dtensor_symbol(func)(*args, **kwargs)
+
     if sym is not None:
         from .symbol import CALLED_TORCH_FN
 
@@ -223,6 +228,15 @@ def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module 
             setattr(owner, attr, orig)
 
 
+def _storage_ptr(x: torch.Tensor):
+    if x.device.type == "meta" or type(x) is not torch.Tensor and not isinstance(x, torch.nn.Parameter):
+        return None
+    try:
+        return x.untyped_storage().data_ptr()
+    except (RuntimeError, NotImplementedError):
+        return None
+
+
 def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
              lookasides: dict | None = None, prune_param_checks: bool = True) -> AcquiredProgram:
     prog = AcquiredProgram()
@@ -257,8 +271,8 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                 proxied_flat.append(p)
                 prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
                 tracker.register_input(p)
-                if x.device.type != "meta":
-                    sp = x.untyped_storage().data_ptr()
+                sp = _storage_ptr(x)
+                if sp is not None:
                     key = (sp, x.storage_offset(), tuple(x.shape), tuple(x.stride()), x.dtype)
                     if key in by_view:
                         tracker.register_identity_alias(p, by_view[key])

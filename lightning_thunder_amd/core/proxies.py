@@ -526,7 +526,105 @@ def is_proxyable(x) -> bool:
     return isinstance(x, (torch.Tensor, Number)) and not isinstance(x, Proxy)
 
 
+class DTensorProxy(TensorProxy):
+    """Proxy of a ``torch.distributed.tensor.DTensor`` (parity: reference
+    ``thunder/torch/experimental/dtensor_proxy.py``).  ``shape`` is the global shape; the device
+    mesh, placements and local shape ride along.  Every torch operation on it is routed to a
+    DTensor-aware opaque symbol (``distributed/dtensor.py``) whose meta runs DTensor's own sharding
+    propagation on meta-device local tensors and whose execution is the torch op on the real
+    DTensors (which issues the RCCL/gloo collectives a redistribution needs)."""
+
+    prefix = "dt"
+
+    def __init__(self, name=None, *, mesh=None, placements=None, local_shape=None, stride=None, like=None, **kw):
+        super().__init__(name, like=like, **kw)
+        if like is not None and isinstance(like, DTensorProxy):
+            mesh = like.mesh if mesh is None else mesh
+            placements = like.placements if placements is None else placements
+            local_shape = like.local_shape if local_shape is None else local_shape
+            stride = like.stride_ if stride is None else stride
+        self.mesh = mesh
+        self.placements = tuple(placements) if placements is not None else ()
+        self.local_shape = tuple(local_shape) if local_shape is not None else tuple(self._shape)
+        self.stride_ = tuple(stride) if stride is not None else None
+
+    def replace(self, **changes):
+        kw = dict(
+            like=self,
+            shape=changes.get("shape", self._shape),
+            device=changes.get("device", self._device),
+            dtype=changes.get("dtype", self._dtype),
+            requires_grad=changes.get("requires_grad", self.requires_grad),
+            tags=changes.get("tags", self.tags),
+        )
+        return DTensorProxy(changes.get("name"), **kw)
+
+    def type_string(self) -> str:
+        pl = ",".join(str(p) for p in self.placements)
+        return f"{super().type_string()} DTensor[{pl}] local{list(self.local_shape)}"
+
+    def _dispatch(self, name, *args, **kwargs):
+        from .jit_ext import dispatch_torch_function
+
+        return dispatch_torch_function(getattr(torch.Tensor, name), (self,) + args, kwargs)
+
+    def __getattr__(self, attr: str):
+        if attr.startswith("_"):
+            raise AttributeError(attr)
+        tm = getattr(torch.Tensor, attr, None)
+        if tm is None:
+            from torch.distributed.tensor import DTensor
+
+            tm = getattr(DTensor, attr, None)
+            if tm is None or not callable(tm):
+                raise AttributeError(f"DTensorProxy has no attribute '{attr}'")
+
+            def dt_bound(*args, **kwargs):
+                from ..distributed.dtensor import dtensor_symbol
+
+                return dtensor_symbol(tm, f"DTensor.{attr}")(self, *args, **kwargs)
+
+            return dt_bound
+        if not callable(tm):
+            raise AttributeError(f"DTensorProxy has no attribute '{attr}'")
+
+        def bound(*args, **kwargs):
+            return self._dispatch(attr, *args, **kwargs)
+
+        return bound
+
+
+def _dt_op(name):
+    def fn(self, *args):
+        return self._dispatch(name, *args)
+
+    fn.__name__ = name
+    return fn
+
+
+for _n in ("__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__", "__truediv__", "__rtruediv__",
+           "__matmul__", "__rmatmul__", "__pow__", "__neg__", "__getitem__", "__eq__", "__ne__", "__lt__", "__le__",
+           "__gt__", "__ge__"):
+    setattr(DTensorProxy, _n, _dt_op(_n))
+DTensorProxy.__hash__ = object.__hash__
+DTensorProxy.T = property(lambda self: self._dispatch("permute", *reversed(range(self.ndim))))
+DTensorProxy.mT = property(lambda self: self._dispatch("transpose", -2, -1))
+
+
 def tensorproxy(t: torch.Tensor, name: str | None = None, **kw) -> TensorProxy:
+    if _is_dtensor(t):
+        return DTensorProxy(
+            name,
+            shape=tuple(t.shape),
+            device=t.device,
+            dtype=t.dtype,
+            requires_grad=t.requires_grad,
+            mesh=t.device_mesh,
+            placements=t.placements,
+            local_shape=tuple(t.to_local().shape),
+            stride=tuple(t.stride()),
+            **kw,
+        )
     return TensorProxy(
         name,
         shape=tuple(t.shape),
@@ -537,6 +635,11 @@ def tensorproxy(t: torch.Tensor, name: str | None = None, **kw) -> TensorProxy:
         thunder_fsdp_padding_size=getattr(t, "thunder_fsdp_padding_size", None),
         **kw,
     )
+
+
+def _is_dtensor(t) -> bool:
+    cls = type(t)
+    return cls.__name__ == "DTensor" and cls.__module__.startswith("torch.distributed")
 
 
 def proxy(x: Any, *, name: str | None = None):

@@ -29,7 +29,7 @@ import torch
 
 from ..core import dtypes, prims
 from ..core.prims import PrimIDs, OpTags
-from ..core.proxies import Proxy, TensorProxy, NumberProxy, pyval
+from ..core.proxies import Proxy, TensorProxy, DTensorProxy, NumberProxy, pyval
 from ..core.pytree import tree_flatten, tree_unflatten, tree_map
 from ..core.symbol import BoundSymbol, BoundSymbolTag, Symbol, NON_DIFFERENTIABLE_TAG, register_symbol
 from ..core.trace import TraceCtx, tracectx, from_trace, TraceProvenance, get_tracectx
@@ -163,7 +163,8 @@ def _torch_vjp_impl(fn, args, kwargs, cotangents):
 
 def _torch_vjp_meta(fn, args, kwargs, cotangents):
     flat, _ = tree_flatten((args, kwargs))
-    return tuple(TensorProxy(like=x, requires_grad=False) for x in flat if isinstance(x, TensorProxy) and dtypes.is_inexact_dtype(x.dtype))
+    return tuple(x.replace(requires_grad=False) if isinstance(x, DTensorProxy) else TensorProxy(like=x, requires_grad=False)
+                 for x in flat if isinstance(x, TensorProxy) and dtypes.is_inexact_dtype(x.dtype))
 
 
 torch_vjp = Symbol("torch_autograd_vjp", _torch_vjp_meta, id="autodiff.torch_autograd_vjp", is_prim=True)
