@@ -101,6 +101,9 @@ class CacheEntry:
         self._last_flat_out = None
         self.has_epilogue = False
         self.autocast_key = None
+        self.guard_roots = []
+        self.interpreter_log = None
+        self.sharp_edges = []
 
     def module_state(self):
         out = []
@@ -169,9 +172,18 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         from .transforms.autocast import autocast_ctx
 
         with autocast_ctx(entry.autocast_key):
+            dbg = cd.debug_options
+            record = cd.get_compile_option("record_interpreter_history", "Record the interpreter log", None)
+            if record is None:
+                record = dbg.record_interpreter_history
             prog = acquire(cd.fn if module is None else module, args, kwargs, module=module, lookasides=lookasides,
                            prune_param_checks=cd.compile_options.get("prune_prologue_checks", True),
-                           python_lookasides=python_lookasides)
+                           python_lookasides=python_lookasides,
+                           interpretation=cd.get_compile_option(
+                               "interpretation", "'python interpreter' (bytecode interpreter, default) or "
+                               "'torch function mode'", "python interpreter"),
+                           record_history=record, sharp_edges=cd.sharp_edges.value,
+                           show_progress=dbg.show_interpreter_progress)
         cs.last_trace_tracing_stop = time.perf_counter_ns()
         pro, comp, epi = prog.prologue_trace, prog.computation_trace, prog.epilogue_trace
         computation_traces = [comp]
@@ -182,6 +194,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         comp = dce(comp)
         computation_traces.append(comp)
 
+        entry.guard_roots = prog.guard_roots
+        entry.interpreter_log = prog.interpreter_log
+        entry.sharp_edges = prog.sharp_edges
+        cs.last_interpreter_log = prog.interpreter_log
         entry.param_accessors = prog.param_accessors
         entry.alias_pattern = prog.alias_pattern
         entry.constants = prog.constants
@@ -329,7 +345,7 @@ def jit(
                     cs.last_trace_cache_stop = time.perf_counter_ns()
                     return entry, inps
                 try:
-                    inps = entry.prologue_fn(flat_args, entry.module_state(), entry.constants)
+                    inps = entry.prologue_fn(flat_args, entry.module_state(), entry.constants, entry.guard_roots)
                 except ThunderCacheMiss:
                     continue
                 cs.cache_hits += 1
@@ -342,7 +358,7 @@ def jit(
         cs.last_traces = entry.computation_traces
         cs.last_backward_traces = entry.backward_traces
         cs.last_prologue_traces = entry.prologue_traces
-        inps = entry.prologue_fn(flat_args, entry.module_state(), entry.constants)
+        inps = entry.prologue_fn(flat_args, entry.module_state(), entry.constants, entry.guard_roots)
         return entry, inps
 
     def fn_(*args, **kwargs):
@@ -352,6 +368,7 @@ def jit(
         cs.last_traces = entry.computation_traces
         cs.last_backward_traces = entry.backward_traces
         cs.last_prologue_traces = entry.prologue_traces
+        cs.last_interpreter_log = entry.interpreter_log
         cs.last_executed = entry
         cs.last_trace_host_execution_start = time.perf_counter_ns()
         out = _run_entry(entry, inps)
@@ -459,10 +476,20 @@ def last_interpreter_log(fn):
     return _cs(fn).last_interpreter_log
 
 
-def print_last_interpreter_log(fn, **kwargs):
+def print_last_interpreter_log(fn, *, max_lines: int | None = None, **kwargs):
+    """Prints the interpreter log of the last compilation (``record_interpreter_history=True``)."""
     log = last_interpreter_log(fn)
-    for item in log or []:
+    if log is None:
+        print("no interpreter log recorded: pass record_interpreter_history=True (or DebugOptions)")
+        return
+    for item in log[:max_lines]:
         print(item)
+
+
+def last_sharp_edges(fn) -> list[str]:
+    """Sharp edges (global reads/writes, non-deterministic calls) seen by the last compilation."""
+    e = _cs(fn).last_executed
+    return [] if e is None else list(e.sharp_edges)
 
 
 def grad(fn):
@@ -478,11 +505,12 @@ def grad(fn):
     return wrapper
 
 
-def trace(fn, *args, **kwargs) -> TraceCtx:
+def trace(fn, *args, interpretation: str = "python interpreter", **kwargs) -> TraceCtx:
     """Acquires the computation trace of ``fn(*args, **kwargs)`` without executing it."""
     from .core.jit_ext import acquire
 
-    prog = acquire(fn, args, kwargs, module=fn if isinstance(fn, _torch.nn.Module) else None)
+    prog = acquire(fn, args, kwargs, module=fn if isinstance(fn, _torch.nn.Module) else None,
+                   interpretation=interpretation)
     return prog.computation_trace
 
 
@@ -492,7 +520,8 @@ from .transforms import *  # noqa: E402,F401,F403
 __all__ = [
     "jit", "compile", "trace", "last_traces", "last_backward_traces", "last_prologue_traces", "compile_data",
     "compile_stats", "cache_option", "cache_hits", "cache_misses", "list_transforms", "last_compile_options",
-    "get_auto_registered_torch_op_names", "DebugOptions", "set_execution_callback_file", "Transform",
+    "get_auto_registered_torch_op_names", "DebugOptions", "last_interpreter_log", "print_last_interpreter_log",
+    "last_sharp_edges", "set_execution_callback_file", "Transform",
     "ThunderModule", "resolve_executors", "add_executor_lists", "get_executor", "get_all_executors",
     "get_default_executors", "get_always_executors", "grad", "Proxy", "TensorProxy", "NumberProxy",
 ]

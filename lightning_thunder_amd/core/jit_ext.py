@@ -208,12 +208,25 @@ class AcquiredProgram:
         self.output_spec = None
         self.epilogue_writes: list[tuple[torch.nn.Module, str]] = []
         self.alias_pattern = None
+        self.guards: list = []  # (Prov, value) read by the program through module/global/closure state
+        self.guard_roots: list = []
+        self.interpreter_log = None
+        self.sharp_edges: list[str] = []
+        self.n_instructions = 0
 
 
 def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
             lookasides: dict | None = None, prune_param_checks: bool = True,
-            python_lookasides: list | None = None) -> AcquiredProgram:
-    """Traces ``fn(*args, **kwargs)`` and builds prologue / computation / epilogue traces."""
+            python_lookasides: list | None = None, interpretation: str = "python interpreter",
+            record_history: bool | str = False, sharp_edges: str = "allow", show_progress: bool = False) -> AcquiredProgram:
+    """Traces ``fn(*args, **kwargs)`` and builds prologue / computation / epilogue traces.
+
+    ``interpretation``: ``"python interpreter"`` (default) runs the user's Python on the bytecode
+    interpreter (:mod:`.interpreter`: provenance guards, lookasides on any callable, sharp
+    edges, interpreter log); ``"torch function mode"`` runs it natively.  Torch operations are
+    captured by the ``TorchFunctionMode`` in both cases."""
+    if interpretation not in ("python interpreter", "torch function mode"):
+        raise ValueError(f"unknown interpretation {interpretation!r}")
     patched = []
     for owner, attr, repl in python_lookasides or ():
         if hasattr(owner, attr):
@@ -222,7 +235,9 @@ def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module 
             patched.append((owner, attr, orig))
             setattr(owner, attr, repl)
     try:
-        return _acquire(fn, args, kwargs, module=module, lookasides=lookasides, prune_param_checks=prune_param_checks)
+        return _acquire(fn, args, kwargs, module=module, lookasides=lookasides, prune_param_checks=prune_param_checks,
+                        interp_options=None if interpretation != "python interpreter" else dict(
+                            record_history=record_history, sharp_edges=sharp_edges, show_progress=show_progress))
     finally:
         for owner, attr, orig in reversed(patched):
             setattr(owner, attr, orig)
@@ -238,7 +253,8 @@ def _storage_ptr(x: torch.Tensor):
 
 
 def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
-             lookasides: dict | None = None, prune_param_checks: bool = True) -> AcquiredProgram:
+             lookasides: dict | None = None, prune_param_checks: bool = True,
+             interp_options: dict | None = None) -> AcquiredProgram:
     prog = AcquiredProgram()
     comp = TraceCtx(fn if not isinstance(fn, torch.nn.Module) else type(fn).forward)
     comp.fn_name = "computation"
@@ -346,13 +362,24 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             for mpath, m in module.named_modules(remove_duplicate=True):
                 before[id(m)] = dict(vars(m))
 
+        interp = None
+        if interp_options is not None:
+            from .interpreter import Interpreter
+
+            def _capture(t):
+                from .proxies import Proxy as _P
+
+                return t if isinstance(t, _P) else state.proxify_constant(t)
+
+            interp = Interpreter(lookasides=lookasides, module=module, tensor_hook=_capture, **interp_options)
         _state_stack.append(state)
         try:
             with ThunderTorchFunctionMode():
-                if module is not None:
-                    result = module(*pargs, **pkwargs)
+                target = module if module is not None else fn
+                if interp is not None:
+                    result = interp.call(target, pargs, pkwargs)
                 else:
-                    result = fn(*pargs, **pkwargs)
+                    result = target(*pargs, **pkwargs)
         finally:
             _state_stack.pop()
             # detect attribute writes (epilogue) before restoring
@@ -398,17 +425,102 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
         else:
             prims.python_return(result)
 
+    if interp is not None:
+        prog.guards = list(interp.guards.values())
+        prog.interpreter_log = interp.history
+        prog.sharp_edges = interp.sharp_edges_seen
+        prog.n_instructions = interp.n_instructions
     comp.args = [s.proxy for s in prog.input_specs]
-    comp.set_provenance(TraceProvenance("Acquisition (trace-by-execution frontend)"))
+    comp.set_provenance(TraceProvenance(
+        "Acquisition (bytecode interpreter)" if interp is not None else "Acquisition (torch function mode)"))
     prog.computation_trace = comp
     prog.output_spec = None
-    prog.prologue_trace = build_prologue(prog, flat_args, prune_param_checks=prune_param_checks)
+    prog.prologue_trace = build_prologue(prog, flat_args, prune_param_checks=prune_param_checks, module_root=module)
     if prog.epilogue_writes:
         prog.epilogue_trace = None  # epilogue is applied by the runtime (see common.run_epilogue)
     return prog
 
 
-def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks: bool) -> TraceCtx:
+def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> None:
+    """Prologue checks for Python values the program read through module/global/closure state.
+
+    Each guard re-fetches its value along its provenance chain (``unpack_attr``/``unpack_key``
+    from a guard root: the compiled module, a globals dict or a closure cell) and checks it
+    (reference: provenance-driven ``unpack_inputs``, ``thunder/core/jit_ext.py:1649-1972``)."""
+    roots: list = []
+    root_ids: dict[int, int] = {}
+
+    def root_index(obj):
+        i = root_ids.get(id(obj))
+        if i is None:
+            i = len(roots)
+            root_ids[id(obj)] = i
+            roots.append(obj)
+        return i
+
+    chains = []
+    for prov, value in prog.guards:
+        r = prov.root()
+        if r.kind == "module":
+            if module_root is None:
+                continue
+            root_index(module_root)
+        elif r.kind == "global":
+            root_index(r.parent)
+        elif r.kind == "cell":
+            root_index(r.parent)
+        chains.append((prov, value))
+    if not chains:
+        return
+    root_vals = prims.unpack_sequence(roots_proxy, len(roots))
+    memo: dict = {}
+
+    def key_of(p):
+        if p.kind == "module":
+            return ("module", p.key)
+        if p.kind in ("global", "cell"):
+            return (p.kind, id(p.parent), p.key)
+        return (key_of(p.parent), p.kind, p.key)
+
+    def emit(p):
+        k = key_of(p)
+        hit = memo.get(k)
+        if hit is not None:
+            return hit
+        if p.kind == "module":
+            out = root_vals[root_ids[id(module_root)]]
+            path = ""
+            for part in (p.key.split(".") if p.key else ()):
+                path = f"{path}.{part}" if path else part
+                sub = memo.get(("module", path))
+                out = sub if sub is not None else prims.unpack_attr(out, part)
+                memo[("module", path)] = out
+        elif p.kind == "global":
+            out = prims.unpack_key(root_vals[root_ids[id(p.parent)]], p.key)
+        elif p.kind == "cell":
+            out = prims.unpack_attr(root_vals[root_ids[id(p.parent)]], "cell_contents")
+        elif p.kind == "attr":
+            out = prims.unpack_attr(emit(p.parent), p.key)
+        else:
+            out = prims.unpack_key(emit(p.parent), p.key)
+        memo[k] = out
+        return out
+
+    for prov, value in chains:
+        v = emit(prov)
+        if value is None:
+            prims.check_none(v)
+        elif isinstance(value, str):
+            prims.check_string_value(v, value)
+        elif isinstance(value, (bool, int, float)):
+            prims.check_number_type_and_value(v, value)
+        else:
+            prims.check_literal_like(v, value)
+    prog.guard_roots = roots
+
+
+def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks: bool,
+                   module_root: torch.nn.Module | None = None) -> TraceCtx:
     """Prologue: flattened args -> checks -> computation inputs (reference ``unpack_inputs`` :1649)."""
     pro = TraceCtx(None)
     pro.fn_name = "prologue"
@@ -416,7 +528,8 @@ def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks
         fa = AnyProxy(None, name="flat_args")
         st = AnyProxy(None, name="module_state")
         cs = AnyProxy(None, name="constants")
-        pro.args = [fa, st, cs]
+        gr = AnyProxy(None, name="guard_roots")
+        pro.args = [fa, st, cs, gr]
         n = len(flat_args)
         unpacked = prims.unpack_sequence(fa, n)
         for i, (u, x) in enumerate(zip(unpacked, flat_args)):
@@ -440,6 +553,8 @@ def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks
                     p = s.proxy
                     prims.check_tensor_shape_and_metadata(state_vals[j], tuple(p.shape), str(p.device), p.dtype, p.requires_grad)
                     j += 1
+        if prog.guards:
+            _emit_provenance_guards(prog, gr, module_root)
         n_const = len(prog.constants)
         const_vals = prims.unpack_sequence(cs, n_const) if n_const else []
         prims.python_return(list(arg_outs) + list(state_vals) + list(const_vals))

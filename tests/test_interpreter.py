@@ -1,0 +1,460 @@
+"""Bytecode interpreter tests (reference model: ``thunder/tests/test_interpreter.py``).
+
+Every program is run natively and on :class:`Interpreter`; results (or raised exception types)
+must agree.  The jit-level tests check provenance guards, sharp edges and the interpreter log.
+"""
+import asyncio
+import dataclasses
+import math
+import warnings
+
+import pytest
+import torch
+
+import lightning_thunder_amd as thunder
+from lightning_thunder_amd.core.interpreter import (
+    Interpreter, InterpretedGenerator, ThunderSharpEdgeError, ThunderSharpEdgeWarning, interpret,
+)
+
+
+def run_both(fn, *args, **kwargs):
+    try:
+        expected = fn(*args, **kwargs)
+        exc = None
+    except Exception as e:  # noqa: BLE001
+        expected, exc = None, e
+    interp = Interpreter(record_history=True)
+    if exc is not None:
+        with pytest.raises(type(exc)):
+            interp.call(fn, args, kwargs)
+        return None
+    got = interp.call(fn, args, kwargs)
+    assert got == expected, (got, expected)
+    assert any(line.strip().startswith("call:") for line in interp.history)
+    return got
+
+
+def test_arith_and_control_flow():
+    def f(a, b, *, c=3):
+        x = a + b * c - (a // 2) % 3
+        y = [i * i for i in range(a) if i % 2]
+        z = {k: v for k, v in zip("abc", (1, 2, 3))}
+        s = {i for i in y}
+        t = tuple(reversed(y))
+        w = 0
+        while w < 10:
+            w += 3
+            if w == 6:
+                continue
+        for i in range(5):
+            if i == 3:
+                break
+        else:
+            w = -1
+        u = a if a > b else b
+        return x, y, z, s, t, w, u, not a, -b, ~a, a ** 2, a / 4, a << 2, a >> 1, a & b, a | b, a ^ b, 3 in y
+
+    run_both(f, 7, 2)
+    run_both(f, 7, 2, c=5)
+
+
+def test_arg_binding_and_errors():
+    def g(a, b=2, /, c=3, *args, d, e=5, **kw):
+        return a, b, c, args, d, e, kw
+
+    run_both(g, 1, d=4)
+    run_both(g, 1, 2, 3, 4, 5, d=6, z=7)
+    run_both(g, 1)  # missing keyword-only -> TypeError
+    run_both(g, d=1)  # missing positional -> TypeError
+
+    def h(a):
+        return a
+
+    run_both(h, 1, 2)  # too many positional -> TypeError
+    run_both(h, b=1)  # unexpected keyword -> TypeError
+    run_both(lambda *a, **k: (a, k), *[1, 2], **{"x": 3})
+
+
+def test_closures_nonlocal_and_cells():
+    def outer(n):
+        acc = []
+
+        def inner(k):
+            nonlocal n
+            n += k
+            acc.append(n)
+            return n
+
+        for i in range(3):
+            inner(i)
+
+        def arg_cell(q):
+            return lambda: q * 2
+
+        return acc, n, arg_cell(21)()
+
+    run_both(outer, 10)
+
+
+def test_exceptions_finally_and_with():
+    class CM:
+        def __init__(self):
+            self.log = []
+
+        def __enter__(self):
+            self.log.append("enter")
+            return self
+
+        def __exit__(self, t, v, tb):
+            self.log.append(("exit", t.__name__ if t else None))
+            return t is KeyError
+
+    def f(x):
+        out = []
+        try:
+            out.append(1)
+            if x:
+                raise ValueError("boom")
+        except ValueError as e:
+            out.append(str(e))
+        except (TypeError, KeyError):
+            out.append("never")
+        else:
+            out.append("else")
+        finally:
+            out.append("finally")
+        cm = CM()
+        with cm as c:
+            raise KeyError("swallowed")
+        out.append(cm.log)
+        try:
+            try:
+                1 / 0
+            finally:
+                out.append("inner finally")
+        except ZeroDivisionError:
+            out.append("zde")
+        try:
+            raise RuntimeError("a") from KeyError("b")
+        except RuntimeError as e:
+            out.append(type(e.__cause__).__name__)
+        return out
+
+    run_both(f, True)
+    run_both(f, False)
+
+    def reraise():
+        try:
+            raise IndexError("x")
+        except IndexError:
+            raise
+
+    run_both(reraise)
+
+    def assertion(x):
+        assert x > 0, "neg"
+        return x
+
+    run_both(assertion, 1)
+    run_both(assertion, -1)
+
+
+def test_exception_context_and_sys_exc_info():
+    import sys
+
+    def f():
+        try:
+            raise KeyError("k")
+        except KeyError:
+            info = sys.exc_info()
+            try:
+                raise ValueError("v")
+            except ValueError as e:
+                return info[0].__name__, type(e.__context__).__name__
+
+    run_both(f)
+
+
+def test_generators_send_throw_close_and_yield_from():
+    def gen(n):
+        total = 0
+        for i in range(n):
+            got = yield i
+            if got:
+                total += got
+        return total
+
+    def deleg(n):
+        r = yield from gen(n)
+        yield ("ret", r)
+
+    def drive():
+        g = deleg(4)
+        out = [next(g), g.send(10), g.send(5), next(g), next(g)]
+        g2 = gen(3)
+        next(g2)
+        try:
+            g2.throw(KeyError("t"))
+        except KeyError:
+            out.append("thrown")
+        g3 = gen(3)
+        next(g3)
+        g3.close()
+        out.append(list(x * 2 for x in range(4)))
+        out.append(sum(gen(5)))
+        return out
+
+    run_both(drive)
+    interp = Interpreter()
+    g = interp.call(gen, (3,))
+    assert isinstance(g, InterpretedGenerator)
+    assert list(g) == [0, 1, 2]
+
+
+def test_stop_iteration_semantics():
+    def f():
+        it = iter([])
+        try:
+            next(it)
+        except StopIteration:
+            return "caught"
+
+    run_both(f)
+
+    def raises_si():
+        raise StopIteration
+
+    def caller():
+        try:
+            raises_si()
+        except StopIteration:
+            return "ok"
+
+    run_both(caller)
+
+
+def test_super_classes_dataclass_and_match():
+    class A:
+        def val(self):
+            return 1
+
+    class B(A):
+        def val(self):
+            return super().val() + 10
+
+    @dataclasses.dataclass
+    class P:
+        x: int
+        y: int
+
+    def f(obj, p):
+        match p:
+            case P(x=0, y=y):
+                m = ("y-axis", y)
+            case P(x, 0):
+                m = ("x-axis", x)
+            case _:
+                m = "other"
+        match [1, 2, 3]:
+            case [1, *rest]:
+                m2 = rest
+        match {"k": 1, "j": 2}:
+            case {"k": v, **others}:
+                m3 = (v, others)
+        return obj.val(), m, m2, m3, f"{p.x:>3}|{p!r}"
+
+    run_both(f, B(), P(0, 5))
+    run_both(f, B(), P(4, 0))
+
+
+def test_coroutines():
+    async def inner(x):
+        await asyncio.sleep(0)
+        return x * 2
+
+    async def outer(x):
+        return await inner(x) + 1
+
+    def f(x):
+        coro = outer(x)
+        try:
+            coro.send(None)
+            coro.send(None)
+        except StopIteration as e:
+            return e.value
+
+    interp = Interpreter()
+    assert interp.call(f, (5,)) == f(5) == 11
+
+
+def test_imports_globals_and_builtins():
+    def f(x):
+        import math as m
+        from os import path
+
+        return m.sqrt(x), path.join("a", "b"), len([1, 2]), isinstance(x, int), math.pi
+
+    run_both(f, 16)
+
+
+def test_locals_globals_eval_exec():
+    def f(a):
+        b = a + 1
+        loc = locals()
+        return sorted(loc), eval("a + b"), "test_interpreter" in globals()["__name__"]
+
+    run_both(f, 2)
+
+
+def test_lookaside_any_callable():
+    def helper(x):
+        return x + 1
+
+    def f(x):
+        return helper(x) * 2
+
+    interp = Interpreter(lookasides={helper: lambda x: x + 100})
+    assert interp.call(f, (1,)) == 202
+
+
+def test_interpret_wrapper_and_torch_ops():
+    def f(a, b):
+        return torch.nn.functional.relu(a @ b).sum(dim=-1)
+
+    a, b = torch.randn(3, 4), torch.randn(4, 5)
+    fi = interpret(f, record_history=True)
+    torch.testing.assert_close(fi(a, b), f(a, b))
+    assert fi.last_interpreter.history
+
+
+# ---------------------------------------------------------------------------------------
+# jit integration: provenance guards, sharp edges, log
+# ---------------------------------------------------------------------------------------
+SCALE = 2.0
+
+
+def scaled(x):
+    return x * SCALE
+
+
+def test_global_scalar_guard_triggers_recompile():
+    global SCALE
+    jf = thunder.jit(scaled)
+    x = torch.ones(3)
+    torch.testing.assert_close(jf(x), x * 2.0)
+    pro = str(thunder.last_prologue_traces(jf)[0])
+    assert "'SCALE'" in pro and "check_number_type_and_value" in pro
+    SCALE = 3.0
+    try:
+        torch.testing.assert_close(jf(x), x * 3.0)
+        assert thunder.cache_misses(jf) == 2
+    finally:
+        SCALE = 2.0
+    torch.testing.assert_close(jf(x), x * 2.0)
+    assert thunder.cache_misses(jf) == 2 and thunder.cache_hits(jf) == 1
+
+
+class _Drop(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(4, 4)
+        self.scale = 0.5
+
+    def forward(self, x):
+        y = self.lin(x)
+        if self.training:
+            y = y * self.scale
+        return y
+
+
+def test_module_training_flag_guard():
+    m = _Drop()
+    jm = thunder.jit(m)
+    x = torch.randn(2, 4)
+    torch.testing.assert_close(jm(x), m(x))
+    m.eval()
+    torch.testing.assert_close(jm(x), m(x))
+    assert thunder.cache_misses(jm) == 2
+    m.train()
+    m.scale = 0.25
+    torch.testing.assert_close(jm(x), m(x))
+    assert thunder.cache_misses(jm) == 3
+
+
+def test_closure_guard():
+    def make(k):
+        def f(x):
+            return x + k
+
+        return f
+
+    f = make(1.0)
+    jf = thunder.jit(f)
+    x = torch.zeros(2)
+    torch.testing.assert_close(jf(x), x + 1.0)
+    f.__closure__[0].cell_contents = 5.0
+    torch.testing.assert_close(jf(x), x + 5.0)
+    assert thunder.cache_misses(jf) == 2
+
+
+G_TENSOR = torch.ones(2)
+COUNTER = 0
+
+
+def reads_global_tensor(x):
+    return x + G_TENSOR
+
+
+def writes_global(x):
+    global COUNTER
+    COUNTER = COUNTER + 1
+    return x * 2
+
+
+def calls_random(x):
+    import random
+
+    return x * random.random()
+
+
+def test_sharp_edges():
+    x = torch.ones(2)
+    with pytest.raises(ThunderSharpEdgeError, match="global tensor"):
+        thunder.jit(reads_global_tensor, sharp_edges="error")(x)
+    with pytest.raises(ThunderSharpEdgeError, match="assigns the global"):
+        thunder.jit(writes_global, sharp_edges="error")(x)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        jf = thunder.jit(calls_random, sharp_edges="warn")
+        jf(x)
+    assert any(issubclass(i.category, ThunderSharpEdgeWarning) for i in w)
+    assert thunder.last_sharp_edges(jf)
+    torch.testing.assert_close(thunder.jit(reads_global_tensor)(x), x + 1)  # allowed by default
+
+
+def test_interpreter_log_and_fallback_mode():
+    m = _Drop()
+    jm = thunder.jit(m, record_interpreter_history=True)
+    x = torch.randn(2, 4)
+    jm(x)
+    log = thunder.last_interpreter_log(jm)
+    assert any("_Drop.forward" in line for line in log)
+    jm2 = thunder.jit(m, interpretation="torch function mode")
+    torch.testing.assert_close(jm2(x), m(x))
+    assert thunder.last_interpreter_log(jm2) is None
+
+
+def test_litgpt_through_interpreter_matches_eager():
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights
+
+    torch.manual_seed(0)
+    m = GPT.from_name("llama2-like")
+    init_weights(m)
+    m.set_rope_cache(16)
+    jm = thunder.jit(m, record_interpreter_history=True)
+    x = torch.randint(0, 100, (1, 16))
+    torch.testing.assert_close(jm(x), m(x))
+    log = thunder.last_interpreter_log(jm)
+    assert any("Block.forward" in line for line in log)
+    pro = str(thunder.last_prologue_traces(jm)[0])
+    assert "n_head" in pro  # config reads became guards
