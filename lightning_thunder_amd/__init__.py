@@ -102,6 +102,7 @@ class CacheEntry:
         self.has_epilogue = False
         self.autocast_key = None
         self.guard_roots = []
+        self.output_spec = None
         self.interpreter_log = None
         self.sharp_edges = []
 
@@ -194,6 +195,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         comp = dce(comp)
         computation_traces.append(comp)
 
+        entry.output_spec = prog.output_spec
         entry.guard_roots = prog.guard_roots
         entry.interpreter_log = prog.interpreter_log
         entry.sharp_edges = prog.sharp_edges
@@ -204,6 +206,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         entry.epilogue_writes = prog.epilogue_writes
         entry.has_epilogue = bool(prog.epilogue_writes)
         entry._same_input_positions = [s.path for s in prog.input_specs if s.kind == "arg"]
+        entry.has_prov_inputs = any(s.kind == "prov" for s in prog.input_specs)
         from .executors.pythonex import ex as pyex
 
         pro_exec = transform_for_execution(pro, [pyex])[-1]
@@ -272,13 +275,14 @@ def _run_entry(entry: CacheEntry, inps):
     else:
         out = entry.computation_fn(*inps)
     if entry.has_epilogue:
-        result, epi_vals = out
+        out, epi_vals = out
         for (m, k), v in zip(entry.epilogue_writes, epi_vals):
             if k in m._buffers:
                 m._buffers[k] = v
             else:
                 object.__setattr__(m, k, v)
-        return result
+    if entry.output_spec is not None:  # rebuild ModelOutput / dataclass / namedtuple results
+        out = tree_unflatten(tree_flatten(out)[0], entry.output_spec)
     return out
 
 
@@ -339,7 +343,7 @@ def jit(
                     continue
                 if entry.alias_pattern is not None and storage_alias_pattern(flat_args) != entry.alias_pattern:
                     continue
-                if cd.cache_option is CACHE_OPTIONS.SAME_INPUT:
+                if cd.cache_option is CACHE_OPTIONS.SAME_INPUT and not entry.has_prov_inputs:
                     inps = _same_input(entry, flat_args)
                     cs.cache_hits += 1
                     cs.last_trace_cache_stop = time.perf_counter_ns()

@@ -454,6 +454,30 @@ def _nondeterministic_fns():
 _NONDET = None
 
 
+def _library_lookasides() -> dict:
+    """Lookasides for third-party model libraries that are already imported.
+
+    ``transformers``: ``is_tracing(t)`` is how HF code asks "is ``t`` symbolic?" before
+    data-dependent checks (packed-sequence detection, causal-mask skipping); it answers True
+    exactly for proxies.  ``warn_if_padding_and_no_attention_mask`` inspects token values and
+    only warns: skipped."""
+    out = {}
+    tf = sys.modules.get("transformers")
+    if tf is not None:
+        from .proxies import Proxy
+
+        iu = sys.modules.get("transformers.utils.import_utils")
+        fn = getattr(iu, "is_tracing", None) if iu is not None else None
+        if fn is not None:
+            out[fn] = lambda tensor=None: isinstance(tensor, Proxy)
+        mu = sys.modules.get("transformers.modeling_utils")
+        pm = getattr(mu, "PreTrainedModel", None) if mu is not None else None
+        w = getattr(pm, "warn_if_padding_and_no_attention_mask", None) if pm is not None else None
+        if w is not None:
+            out[w] = lambda *a, **k: None
+    return out
+
+
 # =========================================================================================
 # The interpreter
 # =========================================================================================
@@ -490,10 +514,15 @@ class Interpreter:
         self.created_functions: set[int] = set()
         self._keepalive: list = []
         self.cell_prov: dict[int, Prov] = {}
+        self.container_prov: dict[int, dict] = {}
         self.n_instructions = 0
+        self.error_stack: list[str] = []  # interpreted frames an escaping exception unwound (innermost first)
+        self._error_id = None
         if module is not None:
             for path, m in module.named_modules(remove_duplicate=True):
                 self.module_paths[id(m)] = path
+        for fn, repl in _library_lookasides().items():
+            self.lookasides.setdefault(fn, repl)
 
     # ---------------------------------------------------------------------------------------
     def log(self, kind: str, what: str):
@@ -511,12 +540,12 @@ class Interpreter:
         if self.sharp_edges == "warn":
             warnings.warn(full, ThunderSharpEdgeWarning, stacklevel=2)
 
-    def captured(self, t):
+    def captured(self, t, p=None):
         """A real tensor read from Python state (global, closure, object attribute) while tracing:
         ``tensor_hook`` turns it into a trace input (the acquisition proxifies it as a constant)."""
         if self.tensor_hook is None:
             return t
-        return self.tensor_hook(t)
+        return self.tensor_hook(t, p)
 
     def mprov(self, v, p):
         """Provenance for ``v``: ``p`` or, for submodules of the compiled module, its path."""
@@ -532,7 +561,7 @@ class Interpreter:
         if isinstance(owner, types.ModuleType):
             return
         r = p.root()
-        if r.kind not in ("module", "global", "cell"):
+        if r.kind not in ("module", "global", "cell", "input"):
             return
         k = (id(owner), key)
         if k not in self.guards:
@@ -543,11 +572,27 @@ class Interpreter:
     def __call__(self, fn, *args, **kwargs):
         return self.call(fn, args, kwargs)
 
-    def call(self, fn, args=(), kwargs=None, arg_provs=None):
-        v, _ = self._call(fn, tuple(args), dict(kwargs or {}), None, arg_provs)
+    def call(self, fn, args=(), kwargs=None, arg_provs=None, kw_provs=None):
+        v, _ = self._call(fn, tuple(args), dict(kwargs or {}), None, arg_provs, kw_provs)
         return v
 
-    def _call(self, fn, args: tuple, kwargs: dict, fn_prov=None, arg_provs=None):
+    # container element provenance (dicts: key -> Prov, tuples/lists: index -> Prov) -------------
+    def set_cprov(self, obj, mapping):
+        if mapping and any(v is not None for v in mapping.values()):
+            self.container_prov[id(obj)] = mapping
+            self._keepalive.append(obj)
+
+    def elem_provs(self, obj, p):
+        """Per-element provenance of a container: recorded element provenance, else derived from ``p``."""
+        m = self.container_prov.get(id(obj))
+        if m is not None:
+            return m
+        if p is not None and type(obj) in (dict, tuple, list):
+            keys = obj.keys() if type(obj) is dict else range(len(obj))
+            return {k: Prov("item", p, k) for k in keys if type(k) in (int, str)}
+        return None
+
+    def _call(self, fn, args: tuple, kwargs: dict, fn_prov=None, arg_provs=None, kw_provs=None):
         """Call dispatch: lookasides, bound methods, partials, modules, interpreted or opaque."""
         la = self.lookasides.get(fn) if _hashable(fn) else None
         if la is not None:
@@ -557,6 +602,8 @@ class Interpreter:
         if gla is not None:
             return gla(self, *args, **kwargs), None
         if fn is getattr and len(args) >= 2 and isinstance(args[1], str) and not kwargs:
+            if len(args) == 3 and not hasattr(args[0], args[1]):
+                return args[2], None  # the default: no provenance (nothing to re-fetch)
             v = getattr(*args)
             p0 = arg_provs[0] if arg_provs else None
             p0 = self.mprov(args[0], p0)
@@ -568,19 +615,28 @@ class Interpreter:
         if t is types.MethodType:
             self_prov = fn_prov.parent if (fn_prov is not None and fn_prov.kind == "attr") else None
             provs = [self_prov] + list(arg_provs or [None] * len(args))
-            return self._call(fn.__func__, (fn.__self__,) + args, kwargs, None, provs)
+            return self._call(fn.__func__, (fn.__self__,) + args, kwargs, None, provs, kw_provs)
         if t is functools.partial:
             return self._call(fn.func, fn.args + args, {**fn.keywords, **kwargs}, None, None)
         if t is types.FunctionType:
             if not self.opaque(fn):
-                return self._interpret_function(fn, args, kwargs, arg_provs), None
+                return self._interpret_function(fn, args, kwargs, arg_provs, kw_provs), None
             return self._opaque(fn, args, kwargs), None
         if isinstance(fn, torch.nn.Module):
-            return self._call_module(fn, args, kwargs, fn_prov, arg_provs)
+            return self._call_module(fn, args, kwargs, fn_prov, arg_provs, kw_provs)
+        if t is types.BuiltinMethodType and type(getattr(fn, "__self__", None)) is dict and args \
+                and fn.__name__ in ("get", "pop", "setdefault", "__getitem__") and not kwargs:
+            d = fn.__self__
+            m = self.container_prov.get(id(d))
+            v = fn(*args)
+            if m is not None and _hashable(args[0]):
+                return v, m.get(args[0])
+            return v, None
         if not isinstance(fn, type):
             call = getattr(t, "__call__", None)
             if type(call) is types.FunctionType and not self.opaque(call):
-                return self._interpret_function(call, (fn,) + args, kwargs, [fn_prov] + list(arg_provs or [None] * len(args))), None
+                return self._interpret_function(call, (fn,) + args, kwargs,
+                                                [fn_prov] + list(arg_provs or [None] * len(args)), kw_provs), None
         return self._opaque(fn, args, kwargs), None
 
     def _opaque(self, fn, args, kwargs):
@@ -594,7 +650,7 @@ class Interpreter:
             self.log("opaque", _name(fn))
         return fn(*args, **kwargs)
 
-    def _call_module(self, m, args, kwargs, fn_prov, arg_provs):
+    def _call_module(self, m, args, kwargs, fn_prov, arg_provs, kw_provs=None):
         from torch.nn.modules import module as _tm
 
         hooks = (m._forward_hooks or m._forward_pre_hooks or m._backward_hooks or getattr(m, "_backward_pre_hooks", None)
@@ -605,9 +661,9 @@ class Interpreter:
         mp = self.mprov(m, fn_prov)
         fwd = m.__dict__.get("forward")
         if fwd is not None:
-            return self._call(fwd, args, kwargs, None, arg_provs)
+            return self._call(fwd, args, kwargs, None, arg_provs, kw_provs)
         fwd = type(m).forward
-        return self._call(fwd, (m,) + args, kwargs, None, [mp] + list(arg_provs or [None] * len(args)))
+        return self._call(fwd, (m,) + args, kwargs, None, [mp] + list(arg_provs or [None] * len(args)), kw_provs)
 
     # ---------------------------------------------------------------------------------------
     def _bind(self, fn, args, kwargs):
@@ -670,9 +726,12 @@ class Interpreter:
                             + ", ".join(repr(x) for x in missing))
         return fast
 
-    def _make_frame(self, fn, args, kwargs, arg_provs=None) -> Frame:
+    def _make_frame(self, fn, args, kwargs, arg_provs=None, kw_provs=None) -> Frame:
         co = fn.__code__
         fast = self._bind(fn, args, kwargs)
+        total = co.co_argcount + co.co_kwonlyargcount
+        varargs_obj = fast[total] if co.co_flags & CO_VARARGS else None
+        kwd = fast[total + (1 if co.co_flags & CO_VARARGS else 0)] if co.co_flags & CO_VARKEYWORDS else None
         cells = []
         names = co.co_varnames
         for name in co.co_cellvars:
@@ -691,17 +750,31 @@ class Interpreter:
                 self.cell_prov[id(c)] = Prov("cell", parent=c)
                 self._keepalive.append(c)
         f = Frame(co, fn, fn.__globals__, fast, cells)
+        argcount = co.co_argcount
         if arg_provs:
-            for i, p in enumerate(arg_provs[: co.co_argcount]):
+            for i, p in enumerate(arg_provs[:argcount]):
                 if p is not None and i < len(f.fprov):
                     f.fprov[i] = p
+            if varargs_obj is not None and len(arg_provs) > argcount:
+                self.set_cprov(varargs_obj, {i: p for i, p in enumerate(arg_provs[argcount:])})
+        if kw_provs:
+            rest = {}
+            for k, p in kw_provs.items():
+                if p is None:
+                    continue
+                if k in names[co.co_posonlyargcount:total]:
+                    f.fprov[names.index(k)] = p
+                elif kwd is not None and k in kwd:
+                    rest[k] = p
+            if rest:
+                self.set_cprov(kwd, rest)
         return f
 
-    def _interpret_function(self, fn, args, kwargs, arg_provs=None):
+    def _interpret_function(self, fn, args, kwargs, arg_provs=None, kw_provs=None):
         if len(self.frames) >= self.MAX_DEPTH:
             raise RecursionError(f"interpreter: maximum call depth {self.MAX_DEPTH} exceeded at {fn.__qualname__}")
         self.log("call", f"{fn.__qualname__} ({fn.__code__.co_filename}:{fn.__code__.co_firstlineno})")
-        f = self._make_frame(fn, args, kwargs, arg_provs)
+        f = self._make_frame(fn, args, kwargs, arg_provs, kw_provs)
         flags = fn.__code__.co_flags
         if flags & (CO_COROUTINE | CO_ITERABLE_COROUTINE):
             return InterpretedCoroutine(self, f)
@@ -829,6 +902,10 @@ class Interpreter:
                     raise
                 except BaseException as e:
                     if not self._unwind(f, e):
+                        if self._error_id != id(e):
+                            self._error_id = id(e)
+                            self.error_stack = []
+                        self.error_stack.append(f.location())
                         if isinstance(e, StopIteration) and not f.is_generator:
                             raise _StopIterationCarrier(e) from None
                         raise
@@ -969,6 +1046,12 @@ def _binary_subscr(interp, f, arg, argval, target):
     if pc is not None and type(k) in (int, str):
         p = Prov("item", pc, k)
         interp.maybe_guard(c, ("item", k), v, p)
+    elif pc is None and _hashable(k):
+        m = interp.container_prov.get(id(c))
+        if m is not None:
+            p = m.get(k)
+    if isinstance(v, torch.Tensor):
+        v = interp.captured(v, p)
     f.push(v, interp.mprov(v, p))
 
 
@@ -1083,7 +1166,7 @@ def _load_global(interp, f, arg, argval, target):
         if isinstance(v, torch.Tensor):
             if interp.sharp_edges != "allow" and not isinstance(v, torch.nn.Parameter):
                 interp.sharp_edge(f"reads the global tensor '{argval}' (pass it as an input instead)")
-            v = interp.captured(v)
+            v = interp.captured(v, p)
         interp.maybe_guard(g, argval, v, p)
         f.push(v, interp.mprov(v, p))
         return
@@ -1161,7 +1244,7 @@ def _load_deref(interp, f, arg, argval, target):
     if p is not None and p.kind == "cell":
         interp.maybe_guard(c, "cell_contents", v, p)
     if isinstance(v, torch.Tensor):
-        v = interp.captured(v)
+        v = interp.captured(v, p)
     f.push(v, interp.mprov(v, p))
 
 
@@ -1205,13 +1288,13 @@ def _delete_deref(interp, f, arg, argval, target):
 def _load_attr(interp, f, arg, argval, target):
     o, po = f.popp()
     v = getattr(o, argval)
-    if isinstance(v, torch.Tensor):
-        v = interp.captured(v)
     po = interp.mprov(o, po)
     p = None
     if po is not None:
         p = Prov("attr", po, argval)
         interp.maybe_guard(o, argval, v, p)
+    if isinstance(v, torch.Tensor):
+        v = interp.captured(v, p)
     f.push(v, interp.mprov(v, p))
 
 
@@ -1269,20 +1352,23 @@ def _call_function_kw(interp, f, arg, argval, target):
     nk = len(names)
     npos = arg - nk
     kwargs = dict(zip(names, vals[npos:]))
-    v, p = interp._call(fn, tuple(vals[:npos]), kwargs, pfn, provs[:npos])
+    v, p = interp._call(fn, tuple(vals[:npos]), kwargs, pfn, provs[:npos], dict(zip(names, provs[npos:])))
     f.push(v, interp.mprov(v, p))
 
 
 @handler("CALL_FUNCTION_EX")
 def _call_function_ex(interp, f, arg, argval, target):
-    kwargs = f.pop() if arg & 1 else {}
-    args = f.pop()
+    kwargs, pk = f.popp() if arg & 1 else ({}, None)
+    args, pa = f.popp()
     fn, pfn = f.popp()
+    aprov = interp.elem_provs(args, pa) if type(args) in (tuple, list) else None
+    kprov = interp.elem_provs(kwargs, pk) if type(kwargs) is dict else None
     if not isinstance(args, tuple):
         args = tuple(args)
     if not isinstance(kwargs, dict):
         kwargs = dict(kwargs)
-    v, p = interp._call(fn, args, kwargs, pfn, None)
+    arg_provs = [aprov.get(i) for i in range(len(args))] if aprov else None
+    v, p = interp._call(fn, args, kwargs, pfn, arg_provs, kprov or None)
     f.push(v, interp.mprov(v, p))
 
 
@@ -1310,12 +1396,17 @@ def _make_function(interp, f, arg, argval, target):
 # --- builders ------------------------------------------------------------------------------
 @handler("BUILD_TUPLE")
 def _build_tuple(interp, f, arg, argval, target):
-    f.push(tuple(f.popn(arg)))
+    vs, ps = f.popnp(arg)
+    t = tuple(vs)
+    interp.set_cprov(t, dict(enumerate(ps)))
+    f.push(t)
 
 
 @handler("BUILD_LIST")
 def _build_list(interp, f, arg, argval, target):
-    f.push(list(f.popn(arg)))
+    vs, ps = f.popnp(arg)
+    interp.set_cprov(vs, dict(enumerate(ps)))
+    f.push(vs)
 
 
 @handler("BUILD_SET")
@@ -1325,15 +1416,19 @@ def _build_set(interp, f, arg, argval, target):
 
 @handler("BUILD_MAP")
 def _build_map(interp, f, arg, argval, target):
-    vs = f.popn(2 * arg)
-    f.push({vs[i]: vs[i + 1] for i in range(0, 2 * arg, 2)})
+    vs, ps = f.popnp(2 * arg)
+    d = {vs[i]: vs[i + 1] for i in range(0, 2 * arg, 2)}
+    interp.set_cprov(d, {vs[i]: ps[i + 1] for i in range(0, 2 * arg, 2) if _hashable(vs[i])})
+    f.push(d)
 
 
 @handler("BUILD_CONST_KEY_MAP")
 def _build_const_key_map(interp, f, arg, argval, target):
     keys = f.pop()
-    vals = f.popn(arg)
-    f.push(dict(zip(keys, vals)))
+    vals, ps = f.popnp(arg)
+    d = dict(zip(keys, vals))
+    interp.set_cprov(d, dict(zip(keys, ps)))
+    f.push(d)
 
 
 @handler("BUILD_STRING")
@@ -1367,8 +1462,16 @@ def _map_add(interp, f, arg, argval, target):
 
 @handler("LIST_EXTEND")
 def _list_extend(interp, f, arg, argval, target):
-    v = f.pop()
-    f.stack[-arg].extend(v)
+    v, pv = f.popp()
+    lst = f.stack[-arg]
+    src = interp.elem_provs(v, pv) if type(v) in (tuple, list) else None
+    if src:
+        dst = dict(interp.container_prov.get(id(lst), {}))
+        off = len(lst)
+        for i, p in src.items():
+            dst[off + i] = p
+        interp.set_cprov(lst, dst)
+    lst.extend(v)
 
 
 @handler("SET_UPDATE")
@@ -1377,9 +1480,18 @@ def _set_update(interp, f, arg, argval, target):
     f.stack[-arg].update(v)
 
 
+def _merge_dict_prov(interp, d, v, pv):
+    src = interp.elem_provs(v, pv) if type(v) is dict else None
+    if src:
+        dst = dict(interp.container_prov.get(id(d), {}))
+        dst.update(src)
+        interp.set_cprov(d, dst)
+
+
 @handler("DICT_UPDATE")
 def _dict_update(interp, f, arg, argval, target):
-    v = f.pop()
+    v, pv = f.popp()
+    _merge_dict_prov(interp, f.stack[-arg], v, pv)
     try:
         f.stack[-arg].update(v)
     except (TypeError, AttributeError):
@@ -1388,8 +1500,9 @@ def _dict_update(interp, f, arg, argval, target):
 
 @handler("DICT_MERGE")
 def _dict_merge(interp, f, arg, argval, target):
-    v = f.pop()
+    v, pv = f.popp()
     d = f.stack[-arg]
+    _merge_dict_prov(interp, d, v, pv)
     fn = f.stack[-arg - 2] if len(f.stack) >= arg + 2 else None
     for k in v.keys():
         if k in d:
@@ -1399,7 +1512,12 @@ def _dict_merge(interp, f, arg, argval, target):
 
 @handler("LIST_TO_TUPLE")
 def _list_to_tuple(interp, f, arg, argval, target):
-    f.push(tuple(f.pop()))
+    lst = f.pop()
+    t = tuple(lst)
+    m = interp.container_prov.get(id(lst))
+    if m:
+        interp.set_cprov(t, m)
+    f.push(t)
 
 
 @handler("UNPACK_SEQUENCE")

@@ -243,6 +243,48 @@ def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module 
             setattr(owner, attr, orig)
 
 
+def _needs_restructure(spec) -> bool:
+    """True if the output contains containers the printed trace cannot rebuild (dict subclasses,
+    dataclasses, namedtuples such as HF ``ModelOutput``)."""
+    if spec.kind == "dict" and spec.ctx[0] is not dict:
+        return True
+    if spec.kind in ("dataclass", "namedtuple", "structseq"):
+        return True
+    return any(_needs_restructure(c) for c in spec.children)
+
+
+def _argument_provenance(args, kwargs):
+    """``Prov("input", key=flat_index)`` for every top-level argument that is a pytree leaf."""
+    from .interpreter import Prov
+    from .pytree import LEAF
+
+    off = 0
+    aprov = []
+    for a in args:
+        leaves, spec = tree_flatten(a)
+        aprov.append(Prov("input", key=off) if spec is LEAF and not isinstance(a, (torch.Tensor, Proxy)) else None)
+        off += len(leaves)
+    kprov = {}
+    for k, v in kwargs.items():
+        leaves, spec = tree_flatten(v)
+        if spec is LEAF and not isinstance(v, (torch.Tensor, Proxy)):
+            kprov[k] = Prov("input", key=off)
+        off += len(leaves)
+    return aprov, kprov
+
+
+def _annotate_with_interpreted_stack(e: Exception, stack: list[str]) -> None:
+    """Appends the interpreted (user-code) call stack to an exception raised while tracing."""
+    if not stack or getattr(e, "_lta_annotated", False):
+        return
+    try:
+        e._lta_annotated = True
+        if e.args and isinstance(e.args[0], str):
+            e.args = (e.args[0] + "\n\nwhile tracing (innermost last):\n  " + "\n  ".join(reversed(stack)),) + e.args[1:]
+    except Exception:  # exceptions with read-only args
+        pass
+
+
 def _storage_ptr(x: torch.Tensor):
     if x.device.type == "meta" or type(x) is not torch.Tensor and not isinstance(x, torch.nn.Parameter):
         return None
@@ -366,18 +408,42 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
         if interp_options is not None:
             from .interpreter import Interpreter
 
-            def _capture(t):
-                from .proxies import Proxy as _P
+            prov_inputs: dict[int, tuple] = {}
 
-                return t if isinstance(t, _P) else state.proxify_constant(t)
+            def _capture(t, prov):
+                """A real tensor read through Python state becomes a computation input: re-fetched
+                along its provenance by the prologue when the chain starts at an argument, a global,
+                a closure cell or the module; otherwise captured as a constant."""
+                if isinstance(t, Proxy):
+                    return t
+                hit = prov_inputs.get(id(t))
+                if hit is not None and hit[0] is t:
+                    return hit[1]
+                root = prov.root().kind if prov is not None else None
+                if root in ("input", "global", "cell") or (root == "module" and module is not None):
+                    c = state.constants.get(id(t))
+                    if c is not None and c[0] is t:
+                        return c[1]
+                    p = tensorproxy(t, name=comp.make_unique_name("tp"))
+                    p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                    tracker.register_input(p)
+                    prov_inputs[id(t)] = (t, p, prov)
+                    return p
+                return state.proxify_constant(t)
 
             interp = Interpreter(lookasides=lookasides, module=module, tensor_hook=_capture, **interp_options)
+            # provenance of top-level (leaf) arguments: their index in the flattened inputs
+            arg_provs, kw_provs = _argument_provenance(args, kwargs)
         _state_stack.append(state)
         try:
             with ThunderTorchFunctionMode():
                 target = module if module is not None else fn
                 if interp is not None:
-                    result = interp.call(target, pargs, pkwargs)
+                    try:
+                        result = interp.call(target, pargs, pkwargs, arg_provs=arg_provs, kw_provs=kw_provs)
+                    except Exception as e:
+                        _annotate_with_interpreted_stack(e, interp.error_stack)
+                        raise
                 else:
                     result = target(*pargs, **pkwargs)
         finally:
@@ -412,6 +478,7 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             return x
 
         result = tree_map(fix_out, result)
+        out_spec = tree_flatten(result)[1]
         epi_values = [tracker.refresh(v) or v for v in epi_values]
         result = tracker.finish(result)
         comp.alias_tracker = None
@@ -426,6 +493,8 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             prims.python_return(result)
 
     if interp is not None:
+        for t, p, prov in prov_inputs.values():
+            prog.input_specs.append(InputSpec("prov", proxy=tracker.original(p), value=prov))
         prog.guards = list(interp.guards.values())
         prog.interpreter_log = interp.history
         prog.sharp_edges = interp.sharp_edges_seen
@@ -434,14 +503,14 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
     comp.set_provenance(TraceProvenance(
         "Acquisition (bytecode interpreter)" if interp is not None else "Acquisition (torch function mode)"))
     prog.computation_trace = comp
-    prog.output_spec = None
+    prog.output_spec = out_spec if _needs_restructure(out_spec) else None
     prog.prologue_trace = build_prologue(prog, flat_args, prune_param_checks=prune_param_checks, module_root=module)
     if prog.epilogue_writes:
         prog.epilogue_trace = None  # epilogue is applied by the runtime (see common.run_epilogue)
     return prog
 
 
-def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> None:
+def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root, unpacked_args) -> list:
     """Prologue checks for Python values the program read through module/global/closure state.
 
     Each guard re-fetches its value along its provenance chain (``unpack_attr``/``unpack_key``
@@ -458,8 +527,9 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> 
             roots.append(obj)
         return i
 
+    prov_specs = [s for s in prog.input_specs if s.kind == "prov"]
     chains = []
-    for prov, value in prog.guards:
+    for prov, value in list(prog.guards) + [(s.value, s) for s in prov_specs]:
         r = prov.root()
         if r.kind == "module":
             if module_root is None:
@@ -471,8 +541,8 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> 
             root_index(r.parent)
         chains.append((prov, value))
     if not chains:
-        return
-    root_vals = prims.unpack_sequence(roots_proxy, len(roots))
+        return []
+    root_vals = prims.unpack_sequence(roots_proxy, len(roots)) if roots else []
     memo: dict = {}
 
     def key_of(p):
@@ -495,6 +565,8 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> 
                 sub = memo.get(("module", path))
                 out = sub if sub is not None else prims.unpack_attr(out, part)
                 memo[("module", path)] = out
+        elif p.kind == "input":
+            out = unpacked_args[p.key]
         elif p.kind == "global":
             out = prims.unpack_key(root_vals[root_ids[id(p.parent)]], p.key)
         elif p.kind == "cell":
@@ -506,8 +578,14 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> 
         memo[k] = out
         return out
 
+    fetched = []
     for prov, value in chains:
         v = emit(prov)
+        if isinstance(value, InputSpec):  # a tensor input re-fetched along its provenance
+            t = value.proxy
+            prims.check_tensor_shape_and_metadata(v, tuple(t.shape), str(t.device), t.dtype, t.requires_grad)
+            fetched.append(v)
+            continue
         if value is None:
             prims.check_none(v)
         elif isinstance(value, str):
@@ -517,6 +595,7 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root) -> 
         else:
             prims.check_literal_like(v, value)
     prog.guard_roots = roots
+    return fetched
 
 
 def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks: bool,
@@ -553,10 +632,11 @@ def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks
                     p = s.proxy
                     prims.check_tensor_shape_and_metadata(state_vals[j], tuple(p.shape), str(p.device), p.dtype, p.requires_grad)
                     j += 1
-        if prog.guards:
-            _emit_provenance_guards(prog, gr, module_root)
+        fetched = []
+        if prog.guards or any(s.kind == "prov" for s in prog.input_specs):
+            fetched = _emit_provenance_guards(prog, gr, module_root, unpacked)
         n_const = len(prog.constants)
         const_vals = prims.unpack_sequence(cs, n_const) if n_const else []
-        prims.python_return(list(arg_outs) + list(state_vals) + list(const_vals))
+        prims.python_return(list(arg_outs) + list(state_vals) + list(const_vals) + list(fetched))
     pro.set_provenance(TraceProvenance("Prologue construction"))
     return pro

@@ -101,6 +101,11 @@ def tree_unflatten(leaves, spec: TreeSpec):
             typ, keys = s.ctx
             d = OrderedDict(zip(keys, vals)) if typ is OrderedDict else dict(zip(keys, vals))
             if typ not in (dict, OrderedDict):
+                if dataclasses.is_dataclass(typ):  # e.g. transformers ModelOutput (OrderedDict + dataclass)
+                    try:
+                        return typ(**d)
+                    except Exception:
+                        pass
                 try:
                     nd = typ.__new__(typ)
                     dict.__init__(nd)

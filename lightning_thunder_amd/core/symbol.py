@@ -160,10 +160,26 @@ class Symbol:
         bsym = self.bind(*args, output=result, subsymbols=subsymbols, _call_ctx=call_ctx, **kwargs)
         if called_fn is not None:
             bsym.torch_fn = called_fn
-        trace.add_bound_symbol(bsym)
+        if self.is_prim or subsymbols or self.name in _LAYOUT_IDENTITIES or not _is_identity(bsym):
+            # an op that decomposed to nothing and returns its own input (dropout in eval, a
+            # same-dtype .to, cat of one tensor) is not recorded: a line "t1 = op(t1)" would
+            # re-bind a name that dead-code elimination treats as produced twice
+            trace.add_bound_symbol(bsym)
         if tracker is not None:
             result = tracker.after_call(bsym, result)
         return result
+
+
+# identity at the proxy level but not at run time (memory layout)
+_LAYOUT_IDENTITIES = {"contiguous"}
+
+
+def _is_identity(bsym) -> bool:
+    outs = bsym.flat_proxy_outs
+    if not outs:
+        return False
+    ins = {id(a) for a in bsym.flat_proxy_args}
+    return all(id(o) in ins for o in outs)
 
 
 _symbol_registry: dict[Any, Symbol] = {}

@@ -29,6 +29,20 @@ def _unpack_sequence(x, n):
     return x
 
 
+def _unpack_attr(o, n):
+    try:
+        return getattr(o, n)
+    except AttributeError as e:  # a guarded attribute disappeared: not this cache entry
+        raise ThunderCacheMiss(str(e)) from None
+
+
+def _unpack_key(d, k):
+    try:
+        return d[k]
+    except (KeyError, IndexError, TypeError) as e:
+        raise ThunderCacheMiss(f"key {k!r}: {e}") from None
+
+
 def _check_tensor(t, shape, device, dtype, requires_grad):
     if not isinstance(t, torch.Tensor):
         raise ThunderCacheMiss(f"expected a tensor, got {type(t)}")
@@ -70,8 +84,8 @@ for prim, fn, name in (
     (prims.check_none, _check_none, "check_none"),
     (prims.check_string_value, _check_string, "check_string_value"),
     (prims.check_literal_like, _check_literal_like, "check_literal_like"),
-    (prims.unpack_key, lambda d, k: d[k], "unpack_key"),
-    (prims.unpack_attr, lambda o, n: getattr(o, n), "unpack_attr"),
+    (prims.unpack_key, _unpack_key, "unpack_key"),
+    (prims.unpack_attr, _unpack_attr, "unpack_attr"),
     (prims.unpack_parameter, lambda o, n: o._parameters[n], "unpack_parameter"),
     (prims.unpack_buffer, lambda o, n: o._buffers[n], "unpack_buffer"),
     (prims.unpack_sequence, _unpack_sequence, "unpack_sequence"),

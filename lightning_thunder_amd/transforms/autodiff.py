@@ -31,7 +31,7 @@ from ..core import dtypes, prims
 from ..core.prims import PrimIDs, OpTags
 from ..core.proxies import Proxy, TensorProxy, DTensorProxy, NumberProxy, pyval
 from ..core.pytree import tree_flatten, tree_unflatten, tree_map
-from ..core.symbol import BoundSymbol, BoundSymbolTag, Symbol, NON_DIFFERENTIABLE_TAG, register_symbol
+from ..core.symbol import BoundSymbol, BoundSymbolTag, Symbol, NON_DIFFERENTIABLE_TAG, register_symbol, _LAYOUT_IDENTITIES
 from ..core.trace import TraceCtx, tracectx, from_trace, TraceProvenance, get_tracectx
 from ..core.transforms import get_vjp_rule, register_vjp, _vjp_rules, grad_like, sum_to_shape, linear_backward, _requires
 from ..core.transform_common import dce
@@ -253,6 +253,13 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
             if recompute:
                 b.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
             fw.bound_symbols.append(b)
+            return
+        in_names = {a.name for a in bsym.flat_proxy_args}
+        if (not bsym.subsymbols and bsym.sym.name not in _LAYOUT_IDENTITIES
+                and all(o.name in in_names for o in bsym.flat_proxy_outs)):
+            # identity (e.g. cat with an empty operand): the output *is* an input, whose name the
+            # swap table already maps; the gradient flows through the shared name.  (contiguous is
+            # kept: it has a rule producing a fresh proxy, needed for the run-time memory layout)
             return
         candidates = _executor_grad_transforms(b, executors)
         registered = _vjp_rules.get(b.sym.id, "missing")
