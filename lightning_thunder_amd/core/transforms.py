@@ -139,6 +139,28 @@ register_vjp(PrimIDs.ERFC)(
     _unary_rule(P.erfc, lambda a, o, g: P.mul(g, P.mul(P.exp(P.neg(P.mul(a, a))), -2.0 / math.sqrt(math.pi))))
 )
 register_vjp(PrimIDs.ABS)(_unary_rule(P.abs, lambda a, o, g: P.mul(g, P.sign(a))))
+register_vjp(PrimIDs.ERFINV)(
+    _unary_rule(P.erfinv, lambda a, o, g: P.mul(g, P.mul(P.exp(P.mul(o, o)), math.sqrt(math.pi) / 2.0)))
+)
+
+
+def _trigamma(x):
+    """psi_1(x) = sum_{k<6} 1/(x+k)^2 + asymptotic series at x+6 (accurate to ~1e-10 for x > 0)."""
+    acc = None
+    for k in range(6):
+        xk = P.add(x, float(k)) if k else x
+        t = P.reciprocal(P.mul(xk, xk))
+        acc = t if acc is None else P.add(acc, t)
+    z = P.add(x, 6.0)
+    iz = P.reciprocal(z)
+    iz2 = P.mul(iz, iz)
+    # 1/z + 1/(2z^2) + 1/(6z^3) - 1/(30z^5) + 1/(42z^7) - 1/(30z^9)
+    poly = P.add(1.0 / 6.0, P.mul(iz2, P.add(-1.0 / 30.0, P.mul(iz2, P.add(1.0 / 42.0, P.mul(iz2, -1.0 / 30.0))))))
+    series = P.add(P.add(iz, P.mul(iz2, 0.5)), P.mul(P.mul(iz2, iz), poly))
+    return P.add(acc, series)
+
+
+register_vjp(PrimIDs.DIGAMMA)(_unary_rule(P.digamma, lambda a, o, g: P.mul(g, _trigamma(a))))
 register_vjp(PrimIDs.LGAMMA)(_unary_rule(P.lgamma, lambda a, o, g: P.mul(g, P.digamma(a))))
 
 for _zero_grad_prim in (P.sign, P.floor, P.ceil, P.round, P.trunc):
@@ -207,6 +229,17 @@ def _maxmin_rule(fwd, cmp):
 
 register_vjp(PrimIDs.MAXIMUM)(_maxmin_rule(P.maximum, P.gt))
 register_vjp(PrimIDs.MINIMUM)(_maxmin_rule(P.minimum, P.lt))
+
+
+@register_vjp(PrimIDs.COPYSIGN)
+def _copysign_rule(a, b):
+    out = P.copysign(a, b)
+
+    def bwd(g):
+        # d/da |a|*sign(b) = sign(a)*sign(out); b only contributes its sign (zero gradient)
+        return P.mul(g, P.mul(P.sign(a), P.sign(out))), None
+
+    return out, bwd
 
 
 @register_vjp(PrimIDs.ATAN2)

@@ -1632,9 +1632,12 @@ def cross_entropy(a, target, weight=None, size_average=None, ignore_index: int =
 
 
 @torchsymbol(torch.nn.functional.mse_loss)
-def mse_loss(a, target, size_average=None, reduce=None, reduction: str = "mean"):
+def mse_loss(a, target, size_average=None, reduce=None, reduction: str = "mean", weight=None):
     d = sub(a, target)
-    return _reduce_loss(mul(d, d), reduction)
+    sq = mul(d, d)
+    if weight is not None:
+        sq = mul(sq, weight)
+    return _reduce_loss(sq, reduction)
 
 
 @torchsymbol(torch.nn.functional.l1_loss)

@@ -1,0 +1,457 @@
+"""OpInfo table: sample inputs + torch reference for the ltorch operator library.
+
+Parity: reference ``thunder/tests/opinfos.py`` (``OpInfo`` :138, sample generators, dtypes,
+``DecorateInfo`` skips).  Each :class:`OpInfo` gives a callable to compile (``op``), a sample
+generator ``samples(device, dtype, requires_grad)`` yielding ``SampleInput``s, the dtypes it
+supports and whether it is differentiable.  The torch reference is the op itself run eagerly
+(float64 for gradient checks).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class SampleInput:
+    args: tuple
+    kwargs: dict = field(default_factory=dict)
+
+    def __repr__(self):
+        def r(x):
+            if isinstance(x, torch.Tensor):
+                return f"T{tuple(x.shape)}:{str(x.dtype).split('.')[-1]}"
+            return repr(x)
+
+        return "(" + ", ".join([r(a) for a in self.args] + [f"{k}={r(v)}" for k, v in self.kwargs.items()]) + ")"
+
+
+FLOATS = (torch.float32, torch.bfloat16, torch.float16)
+FLOAT32 = (torch.float32,)
+INTS = (torch.int64, torch.int32)
+
+
+@dataclass
+class OpInfo:
+    name: str
+    op: Callable
+    samples: Callable
+    dtypes: tuple = FLOATS
+    differentiable: bool = True
+    atol: float | None = None
+    rtol: float | None = None
+    skip_gpu: bool = False
+    grad_atol: float = 1e-6
+
+    def __repr__(self):
+        return self.name
+
+
+def _t(shape, device, dtype, requires_grad=False, low=-2.0, high=2.0):
+    if dtype.is_floating_point:
+        x = torch.empty(shape, device=device, dtype=torch.float32).uniform_(low, high).to(dtype)
+    elif dtype == torch.bool:
+        x = torch.rand(shape, device=device) > 0.5
+    else:
+        x = torch.randint(int(low) if low > -100 else -5, int(high) + 1 if high < 100 else 6, shape, device=device, dtype=dtype)
+    if requires_grad and dtype.is_floating_point:
+        x.requires_grad_(True)
+    return x
+
+
+SHAPES = [(5,), (3, 4), (2, 3, 5)]
+
+
+def unary_samples(low=-2.0, high=2.0, shapes=SHAPES):
+    def gen(device, dtype, requires_grad):
+        for s in shapes:
+            yield SampleInput((_t(s, device, dtype, requires_grad, low, high),))
+
+    return gen
+
+
+def binary_samples(low=-2.0, high=2.0, rhs_low=None, rhs_high=None, scalar=True):
+    rl = low if rhs_low is None else rhs_low
+    rh = high if rhs_high is None else rhs_high
+
+    def gen(device, dtype, requires_grad):
+        yield SampleInput((_t((3, 4), device, dtype, requires_grad, low, high), _t((3, 4), device, dtype, requires_grad, rl, rh)))
+        yield SampleInput((_t((2, 3, 4), device, dtype, requires_grad, low, high), _t((3, 1), device, dtype, requires_grad, rl, rh)))
+        if scalar:
+            yield SampleInput((_t((4,), device, dtype, requires_grad, low, high), (rl + rh) / 2 + 0.75))
+
+    return gen
+
+
+def reduction_samples(dims=(None, 0, -1, (0, 1)), keepdim=(False, True), extra=None):
+    def gen(device, dtype, requires_grad):
+        x = _t((3, 4, 5), device, dtype, requires_grad)
+        for d in dims:
+            for k in keepdim:
+                kw = {} if d is None else {"dim": d, "keepdim": k}
+                if d is None and k:
+                    continue
+                kw.update(extra or {})
+                yield SampleInput((x,), kw)
+
+    return gen
+
+
+def _pos(shapes=SHAPES):
+    return unary_samples(0.1, 3.0, shapes)
+
+
+def elementwise_unary(name, fn, low=-2.0, high=2.0, dtypes=FLOATS, differentiable=True, **kw):
+    return OpInfo(name, fn, unary_samples(low, high), dtypes=dtypes, differentiable=differentiable, **kw)
+
+
+def elementwise_binary(name, fn, dtypes=FLOATS, differentiable=True, **kw):
+    s = kw.pop("samples", None) or binary_samples(**kw.pop("sample_kw", {}))
+    return OpInfo(name, fn, s, dtypes=dtypes, differentiable=differentiable, **kw)
+
+
+def _shape_samples(fn_args):
+    def gen(device, dtype, requires_grad):
+        for shape, args, kwargs in fn_args:
+            yield SampleInput((_t(shape, device, dtype, requires_grad),) + tuple(args), dict(kwargs))
+
+    return gen
+
+
+def _matmul_samples(device, dtype, requires_grad):
+    yield SampleInput((_t((3, 4), device, dtype, requires_grad), _t((4, 5), device, dtype, requires_grad)))
+    yield SampleInput((_t((2, 3, 4), device, dtype, requires_grad), _t((4, 5), device, dtype, requires_grad)))
+    yield SampleInput((_t((2, 3, 4), device, dtype, requires_grad), _t((2, 4, 5), device, dtype, requires_grad)))
+    yield SampleInput((_t((4,), device, dtype, requires_grad), _t((4, 3), device, dtype, requires_grad)))
+
+
+def _linear_samples(device, dtype, requires_grad):
+    yield SampleInput((_t((3, 4), device, dtype, requires_grad), _t((5, 4), device, dtype, requires_grad)))
+    yield SampleInput((_t((2, 3, 4), device, dtype, requires_grad), _t((5, 4), device, dtype, requires_grad),
+                       _t((5,), device, dtype, requires_grad)))
+
+
+def _norm_samples(kind):
+    def gen(device, dtype, requires_grad):
+        x = _t((2, 3, 8), device, dtype, requires_grad)
+        w = _t((8,), device, dtype, requires_grad, 0.5, 1.5)
+        b = _t((8,), device, dtype, requires_grad)
+        if kind == "layer_norm":
+            yield SampleInput((x, (8,)), {})
+            yield SampleInput((x, (8,), w, b), {"eps": 1e-5})
+        else:
+            yield SampleInput((x, (8,)), {"eps": 1e-6})
+            yield SampleInput((x, (8,), w), {"eps": 1e-6})
+
+    return gen
+
+
+def _softmax_samples(device, dtype, requires_grad):
+    x = _t((3, 4, 5), device, dtype, requires_grad)
+    for d in (0, -1, 1):
+        yield SampleInput((x,), {"dim": d})
+
+
+def _ce_samples(device, dtype, requires_grad):
+    logits = _t((6, 10), device, dtype, requires_grad)
+    tgt = torch.randint(0, 10, (6,), device=device)
+    yield SampleInput((logits, tgt))
+    tgt2 = tgt.clone()
+    tgt2[1] = -100
+    yield SampleInput((logits, tgt2), {"ignore_index": -100})
+    yield SampleInput((logits, tgt), {"label_smoothing": 0.1})
+    yield SampleInput((logits, tgt), {"reduction": "sum"})
+
+
+def _sdpa_samples(device, dtype, requires_grad):
+    q = _t((1, 2, 8, 16), device, dtype, requires_grad)
+    k = _t((1, 2, 8, 16), device, dtype, requires_grad)
+    v = _t((1, 2, 8, 16), device, dtype, requires_grad)
+    yield SampleInput((q, k, v), {"is_causal": True})
+    yield SampleInput((q, k, v), {})
+
+
+def _embedding_samples(device, dtype, requires_grad):
+    idx = torch.randint(0, 10, (3, 4), device=device)
+    w = _t((10, 6), device, dtype, requires_grad)
+    yield SampleInput((idx, w))
+
+
+def _where_samples(device, dtype, requires_grad):
+    c = torch.rand(3, 4, device=device) > 0.5
+    yield SampleInput((c, _t((3, 4), device, dtype, requires_grad), _t((3, 4), device, dtype, requires_grad)))
+    yield SampleInput((c, _t((3, 4), device, dtype, requires_grad), 0.5))
+
+
+def _cat_samples(device, dtype, requires_grad):
+    a, b = _t((2, 3), device, dtype, requires_grad), _t((4, 3), device, dtype, requires_grad)
+    yield SampleInput(([a, b],), {"dim": 0})
+    c = _t((2, 5), device, dtype, requires_grad)
+    yield SampleInput(([a, c],), {"dim": 1})
+
+
+def _stack_samples(device, dtype, requires_grad):
+    a, b = _t((2, 3), device, dtype, requires_grad), _t((2, 3), device, dtype, requires_grad)
+    yield SampleInput(([a, b],), {"dim": 0})
+    yield SampleInput(([a, b],), {"dim": -1})
+
+
+def _getitem_samples(device, dtype, requires_grad):
+    x = _t((4, 5, 6), device, dtype, requires_grad)
+    for key in (1, (slice(1, 3), 2), (Ellipsis, 0), (slice(None), None, slice(0, 4, 2)), -1):
+        yield SampleInput((x, key))
+
+
+def _gather_samples(device, dtype, requires_grad):
+    x = _t((3, 5), device, dtype, requires_grad)
+    idx = torch.randint(0, 5, (3, 2), device=device)
+    yield SampleInput((x, 1, idx))
+
+
+def _index_select_samples(device, dtype, requires_grad):
+    x = _t((4, 5), device, dtype, requires_grad)
+    yield SampleInput((x, 0, torch.tensor([0, 2, 3], device=device)))
+    yield SampleInput((x, 1, torch.tensor([4, 1], device=device)))
+
+
+def _masked_fill_samples(device, dtype, requires_grad):
+    x = _t((3, 4), device, dtype, requires_grad)
+    m = torch.rand(3, 4, device=device) > 0.5
+    yield SampleInput((x, m, -1.5))
+
+
+def _clamp_samples(device, dtype, requires_grad):
+    x = _t((3, 4), device, dtype, requires_grad)
+    yield SampleInput((x,), {"min": -0.5, "max": 0.5})
+    yield SampleInput((x,), {"min": -0.3})
+
+
+def _pad_samples(device, dtype, requires_grad):
+    x = _t((2, 3, 4), device, dtype, requires_grad)
+    yield SampleInput((x, (1, 2)))
+    yield SampleInput((x, (1, 0, 0, 2)), {"value": 0.5})
+
+
+def _topk_samples(device, dtype, requires_grad):
+    x = _t((3, 6), device, dtype, requires_grad)
+    yield SampleInput((x, 2))
+    yield SampleInput((x, 3), {"dim": 0})
+
+
+def _cumsum_samples(device, dtype, requires_grad):
+    x = _t((3, 4), device, dtype, requires_grad)
+    yield SampleInput((x, 0))
+    yield SampleInput((x, -1))
+
+
+def _einsum_samples(device, dtype, requires_grad):
+    a, b = _t((2, 3), device, dtype, requires_grad), _t((3, 4), device, dtype, requires_grad)
+    yield SampleInput(("ij,jk->ik", a, b))
+    c = _t((2, 3, 4), device, dtype, requires_grad)
+    yield SampleInput(("bij->bji", c))
+
+
+def _mse_samples(device, dtype, requires_grad):
+    yield SampleInput((_t((3, 4), device, dtype, requires_grad), _t((3, 4), device, dtype, requires_grad)))
+
+
+def _group_norm_samples(device, dtype, requires_grad):
+    x = _t((2, 4, 3, 3), device, dtype, requires_grad)
+    yield SampleInput((x, 2), {"weight": _t((4,), device, dtype, requires_grad), "bias": _t((4,), device, dtype, requires_grad)})
+
+
+def _split_samples(device, dtype, requires_grad):
+    x = _t((6, 4), device, dtype, requires_grad)
+    yield SampleInput((x, 2))
+    yield SampleInput((x, [1, 5]))
+    yield SampleInput((x, 2), {"dim": 1})
+
+
+def _bce_samples(device, dtype, requires_grad):
+    yield SampleInput((_t((3, 4), device, dtype, requires_grad), torch.rand(3, 4, device=device, dtype=dtype)))
+
+
+def _scatter_add_samples(device, dtype, requires_grad):
+    x = _t((3, 5), device, dtype, requires_grad)
+    idx = torch.randint(0, 5, (3, 2), device=device)
+    src = _t((3, 2), device, dtype, requires_grad)
+    yield SampleInput((x, 1, idx, src))
+
+
+def _index_add_samples(device, dtype, requires_grad):
+    x = _t((5, 3), device, dtype, requires_grad)
+    idx = torch.tensor([0, 2, 2], device=device)
+    src = _t((3, 3), device, dtype, requires_grad)
+    yield SampleInput((x, 0, idx, src))
+
+
+OPS: list[OpInfo] = [
+    # ---- unary elementwise ----
+    elementwise_unary("abs", torch.abs),
+    elementwise_unary("neg", torch.neg),
+    elementwise_unary("exp", torch.exp),
+    elementwise_unary("exp2", torch.exp2),
+    elementwise_unary("expm1", torch.expm1),
+    elementwise_unary("log", torch.log, 0.1, 3.0),
+    elementwise_unary("log2", torch.log2, 0.1, 3.0),
+    elementwise_unary("log10", torch.log10, 0.1, 3.0),
+    elementwise_unary("log1p", torch.log1p, -0.5, 3.0),
+    elementwise_unary("sqrt", torch.sqrt, 0.1, 3.0),
+    elementwise_unary("rsqrt", torch.rsqrt, 0.1, 3.0),
+    elementwise_unary("reciprocal", torch.reciprocal, 0.5, 3.0),
+    elementwise_unary("sin", torch.sin),
+    elementwise_unary("cos", torch.cos),
+    elementwise_unary("tan", torch.tan, -1.0, 1.0),
+    elementwise_unary("asin", torch.asin, -0.9, 0.9),
+    elementwise_unary("acos", torch.acos, -0.9, 0.9),
+    elementwise_unary("atan", torch.atan),
+    elementwise_unary("sinh", torch.sinh),
+    elementwise_unary("cosh", torch.cosh),
+    elementwise_unary("tanh", torch.tanh),
+    elementwise_unary("asinh", torch.asinh),
+    elementwise_unary("acosh", torch.acosh, 1.1, 3.0),
+    elementwise_unary("atanh", torch.atanh, -0.9, 0.9),
+    elementwise_unary("sigmoid", torch.sigmoid),
+    elementwise_unary("erf", torch.erf),
+    elementwise_unary("erfc", torch.erfc),
+    elementwise_unary("erfinv", torch.erfinv, -0.9, 0.9),
+    elementwise_unary("lgamma", torch.lgamma, 0.5, 3.0),
+    elementwise_unary("digamma", torch.digamma, 0.5, 3.0),
+    elementwise_unary("square", torch.square),
+    elementwise_unary("sign", torch.sign, differentiable=False),
+    elementwise_unary("floor", torch.floor, differentiable=False),
+    elementwise_unary("ceil", torch.ceil, differentiable=False),
+    elementwise_unary("round", torch.round, differentiable=False),
+    elementwise_unary("trunc", torch.trunc, differentiable=False),
+    elementwise_unary("isnan", torch.isnan, differentiable=False),
+    elementwise_unary("isfinite", torch.isfinite, differentiable=False),
+    elementwise_unary("relu", F.relu),
+    elementwise_unary("relu6", F.relu6, -7.0, 7.0),
+    elementwise_unary("gelu", F.gelu),
+    elementwise_unary("gelu_tanh", lambda x: F.gelu(x, approximate="tanh")),
+    elementwise_unary("silu", F.silu),
+    elementwise_unary("mish", F.mish),
+    elementwise_unary("elu", F.elu),
+    elementwise_unary("leaky_relu", lambda x: F.leaky_relu(x, 0.2)),
+    elementwise_unary("softplus", F.softplus),
+    elementwise_unary("hardswish", F.hardswish),
+    elementwise_unary("hardtanh", F.hardtanh),
+    elementwise_unary("logsigmoid", F.logsigmoid),
+    elementwise_unary("nan_to_num", torch.nan_to_num),
+    elementwise_unary("bitwise_not", torch.bitwise_not, dtypes=INTS, differentiable=False),
+    OpInfo("clamp", torch.clamp, _clamp_samples),
+    OpInfo("pow_scalar", lambda x: torch.pow(x, 3), unary_samples()),
+    OpInfo("pow_frac", lambda x: x ** 0.5, unary_samples(0.1, 3.0)),
+    # ---- binary elementwise ----
+    elementwise_binary("add", torch.add),
+    elementwise_binary("add_alpha", lambda a, b: torch.add(a, b, alpha=2), samples=binary_samples(scalar=False)),
+    elementwise_binary("sub", torch.sub),
+    elementwise_binary("mul", torch.mul),
+    elementwise_binary("div", torch.div, sample_kw=dict(rhs_low=0.5, rhs_high=2.0)),
+    elementwise_binary("div_floor", lambda a, b: torch.div(a, b, rounding_mode="floor"), differentiable=False,
+                       sample_kw=dict(rhs_low=0.5, rhs_high=2.0)),
+    elementwise_binary("remainder", torch.remainder, differentiable=False, sample_kw=dict(rhs_low=0.5, rhs_high=2.0)),
+    elementwise_binary("fmod", torch.fmod, differentiable=False, sample_kw=dict(rhs_low=0.5, rhs_high=2.0)),
+    elementwise_binary("pow", torch.pow, sample_kw=dict(low=0.5, high=2.0, rhs_low=-1.0, rhs_high=2.0)),
+    elementwise_binary("maximum", torch.maximum, samples=binary_samples(scalar=False)),
+    elementwise_binary("minimum", torch.minimum, samples=binary_samples(scalar=False)),
+    elementwise_binary("atan2", torch.atan2, samples=binary_samples(scalar=False)),
+    elementwise_binary("copysign", torch.copysign, samples=binary_samples(scalar=False)),
+    elementwise_binary("eq", torch.eq, differentiable=False),
+    elementwise_binary("ne", torch.ne, differentiable=False),
+    elementwise_binary("lt", torch.lt, differentiable=False),
+    elementwise_binary("le", torch.le, differentiable=False),
+    elementwise_binary("gt", torch.gt, differentiable=False),
+    elementwise_binary("ge", torch.ge, differentiable=False),
+    elementwise_binary("bitwise_and", torch.bitwise_and, dtypes=INTS, differentiable=False,
+                       samples=binary_samples(scalar=False)),
+    elementwise_binary("bitwise_xor", torch.bitwise_xor, dtypes=INTS, differentiable=False,
+                       samples=binary_samples(scalar=False)),
+    elementwise_binary("int_add", torch.add, dtypes=INTS, differentiable=False, samples=binary_samples(scalar=False)),
+    OpInfo("lerp", torch.lerp, lambda d, t, r: iter([SampleInput((_t((3, 4), d, t, r), _t((3, 4), d, t, r), 0.3))])),
+    OpInfo("addcmul", lambda a, b, c: torch.addcmul(a, b, c, value=0.5),
+           lambda d, t, r: iter([SampleInput((_t((3, 4), d, t, r), _t((3, 4), d, t, r), _t((3, 4), d, t, r)))])),
+    OpInfo("addcdiv", lambda a, b, c: torch.addcdiv(a, b, c, value=0.5),
+           lambda d, t, r: iter([SampleInput((_t((3, 4), d, t, r), _t((3, 4), d, t, r), _t((3, 4), d, t, r, 0.5, 2.0)))])),
+    OpInfo("where", torch.where, _where_samples),
+    OpInfo("masked_fill", torch.masked_fill, _masked_fill_samples),
+    # ---- reductions ----
+    OpInfo("sum", torch.sum, reduction_samples()),
+    OpInfo("mean", torch.mean, reduction_samples()),
+    OpInfo("prod", lambda x, **k: torch.prod(x, **k) if k else torch.prod(x), reduction_samples(dims=(None, 1))),
+    OpInfo("amax", torch.amax, reduction_samples(dims=(0, -1, (0, 1)))),
+    OpInfo("amin", torch.amin, reduction_samples(dims=(0, -1))),
+    OpInfo("var", torch.var, reduction_samples(dims=(None, 0, -1))),
+    OpInfo("var_unbiased0", lambda x, **k: torch.var(x, correction=0, **k), reduction_samples(dims=(None, 1))),
+    OpInfo("std", torch.std, reduction_samples(dims=(None, 1))),
+    OpInfo("logsumexp", lambda x, dim=-1, keepdim=False: torch.logsumexp(x, dim, keepdim), reduction_samples(dims=(0, -1))),
+    OpInfo("argmax", torch.argmax, reduction_samples(dims=(0, -1)), differentiable=False),
+    OpInfo("argmin", torch.argmin, reduction_samples(dims=(0, -1)), differentiable=False),
+    OpInfo("any", lambda x: torch.any(x > 0), unary_samples(), differentiable=False),
+    OpInfo("all", lambda x: torch.all(x > -10), unary_samples(), differentiable=False),
+    OpInfo("cumsum", torch.cumsum, _cumsum_samples),
+    OpInfo("topk_values", lambda x, k, **kw: torch.topk(x, k, **kw).values, _topk_samples),
+    OpInfo("sort_values", lambda x: torch.sort(x, -1).values, unary_samples(shapes=[(3, 6)])),
+    # ---- shape ops ----
+    OpInfo("reshape", torch.reshape, _shape_samples([((3, 4), ((12,),), {}), ((2, 3, 4), ((6, -1),), {})])),
+    OpInfo("view", lambda x, s: x.view(s), _shape_samples([((3, 4), ((4, 3),), {})])),
+    OpInfo("transpose", torch.transpose, _shape_samples([((3, 4), (0, 1), {}), ((2, 3, 4), (-1, 0), {})])),
+    OpInfo("permute", torch.permute, _shape_samples([((2, 3, 4), ((2, 0, 1),), {})])),
+    OpInfo("unsqueeze", torch.unsqueeze, _shape_samples([((3, 4), (1,), {}), ((3,), (-1,), {})])),
+    OpInfo("squeeze", torch.squeeze, _shape_samples([((3, 1, 4), (1,), {}), ((1, 3, 1), (), {})])),
+    OpInfo("flatten", torch.flatten, _shape_samples([((2, 3, 4), (1,), {}), ((2, 3, 4), (), {})])),
+    OpInfo("expand", lambda x, *s: x.expand(*s), _shape_samples([((3, 1), (3, 4), {}), ((4,), (2, 4), {})])),
+    OpInfo("repeat", lambda x, *s: x.repeat(*s), _shape_samples([((2, 3), (2, 1), {})])),
+    OpInfo("flip", torch.flip, _shape_samples([((3, 4), ((0,),), {}), ((3, 4), ((0, 1),), {})])),
+    OpInfo("roll", torch.roll, _shape_samples([((3, 4), (1, 1), {})])),
+    OpInfo("narrow", torch.narrow, _shape_samples([((4, 5), (1, 1, 3), {})])),
+    OpInfo("movedim", torch.movedim, _shape_samples([((2, 3, 4), (0, 2), {})])),
+    OpInfo("tril", torch.tril, unary_samples(shapes=[(4, 4), (3, 5)])),
+    OpInfo("triu", lambda x: torch.triu(x, 1), unary_samples(shapes=[(4, 4)])),
+    OpInfo("cat", torch.cat, _cat_samples),
+    OpInfo("stack", torch.stack, _stack_samples),
+    OpInfo("split", lambda x, s, **k: torch.split(x, s, **k), _split_samples),
+    OpInfo("chunk", lambda x: torch.chunk(x, 3, 0), unary_samples(shapes=[(6, 2)])),
+    OpInfo("unbind", lambda x: torch.unbind(x, 1), unary_samples(shapes=[(2, 3)])),
+    OpInfo("getitem", lambda x, k: x[k], _getitem_samples),
+    OpInfo("pad", F.pad, _pad_samples),
+    OpInfo("contiguous_T", lambda x: x.t().contiguous().view(-1), unary_samples(shapes=[(3, 4)])),
+    OpInfo("to_dtype", lambda x: x.to(torch.float64).sum(-1), unary_samples()),
+    # ---- indexing ----
+    OpInfo("gather", torch.gather, _gather_samples),
+    OpInfo("index_select", torch.index_select, _index_select_samples),
+    OpInfo("take_along_dim", lambda x, i: torch.take_along_dim(x, i, 1),
+           lambda d, t, r: iter([SampleInput((_t((3, 5), d, t, r), torch.randint(0, 5, (3, 2), device=d)))])),
+    OpInfo("scatter_add", torch.scatter_add, _scatter_add_samples),
+    OpInfo("index_add", torch.index_add, _index_add_samples),
+    OpInfo("embedding", F.embedding, _embedding_samples),
+    OpInfo("one_hot", lambda i: F.one_hot(i, 7), lambda d, t, r: iter([SampleInput((torch.randint(0, 7, (3, 4), device=d),))]),
+           dtypes=(torch.int64,), differentiable=False),
+    # ---- linear algebra ----
+    OpInfo("matmul", torch.matmul, _matmul_samples, atol=1e-2, rtol=1e-2),
+    OpInfo("linear", F.linear, _linear_samples, atol=1e-2, rtol=1e-2),
+    OpInfo("bmm", torch.bmm, lambda d, t, r: iter([SampleInput((_t((2, 3, 4), d, t, r), _t((2, 4, 5), d, t, r)))]),
+           atol=1e-2, rtol=1e-2),
+    OpInfo("addmm", torch.addmm, lambda d, t, r: iter([SampleInput((_t((3, 5), d, t, r), _t((3, 4), d, t, r), _t((4, 5), d, t, r)))]),
+           atol=1e-2, rtol=1e-2),
+    OpInfo("outer", torch.outer, lambda d, t, r: iter([SampleInput((_t((3,), d, t, r), _t((4,), d, t, r)))])),
+    OpInfo("einsum", torch.einsum, _einsum_samples, atol=1e-2, rtol=1e-2),
+    # ---- nn ----
+    OpInfo("softmax", F.softmax, _softmax_samples),
+    OpInfo("log_softmax", F.log_softmax, _softmax_samples),
+    OpInfo("layer_norm", F.layer_norm, _norm_samples("layer_norm"), atol=2e-2, rtol=2e-2),
+    OpInfo("rms_norm", F.rms_norm, _norm_samples("rms_norm"), atol=2e-2, rtol=2e-2),
+    OpInfo("group_norm", F.group_norm, _group_norm_samples, atol=2e-2, rtol=2e-2),
+    OpInfo("cross_entropy", F.cross_entropy, _ce_samples, atol=2e-2, rtol=2e-2),
+    OpInfo("mse_loss", F.mse_loss, _mse_samples),
+    OpInfo("l1_loss", F.l1_loss, _mse_samples),
+    OpInfo("bce_with_logits", F.binary_cross_entropy_with_logits, _bce_samples),
+    OpInfo("sdpa", F.scaled_dot_product_attention, _sdpa_samples, atol=2e-2, rtol=2e-2),
+    OpInfo("normalize", F.normalize, unary_samples(shapes=[(3, 4)])),
+]
+
+OPS_BY_NAME = {o.name: o for o in OPS}
