@@ -313,6 +313,8 @@ class Plan:
         if _sq(a.shape) != _sq(out.shape):
             raise NotFusible("non-unit reshape")
         if self._internal(a):
+            if self.maps[a.name] is None:
+                raise NotFusible("unit reshape of a value whose index map is not known yet")
             amap = [x for x, s in zip(self.maps[a.name], a.shape) if s != 1]
             om, k = [], 0
             for s in out.shape:

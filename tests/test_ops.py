@@ -125,3 +125,27 @@ def test_vjp_correctness(opinfo):
     for sample in opinfo.samples("cpu", torch.float64, False):
         checked += _check_vjp(opinfo, sample)
     assert checked > 0
+
+
+@pytest.fixture
+def hipfuse_on_cpu():
+    from lightning_thunder_amd.executors import hipfuse
+
+    old = hipfuse.ex.allow_cpu
+    hipfuse.ex.allow_cpu = True
+    yield
+    hipfuse.ex.allow_cpu = old
+
+
+@pytest.mark.parametrize("opinfo,dtype", [pytest.param(o, dt, id=f"{o.name}-{str(dt).split('.')[-1]}")
+                                          for o in OPS for dt in (torch.float32, torch.bfloat16) if dt in o.dtypes])
+def test_hipfuse_partition_consistency(opinfo, dtype, hipfuse_on_cpu):
+    """The hipfuse fusion pass (partitioning, index maps) on every op; regions run through the
+    torch reference path on the CPU, so partition bugs surface without a GPU."""
+    torch.manual_seed(1234)
+    jfn = thunder.jit(opinfo.op, executors=["hipfuse", "torch"])
+    for requires_grad in ((False, True) if opinfo.differentiable else (False,)):
+        for sample in opinfo.samples("cpu", dtype, requires_grad):
+            expected = opinfo.op(*sample.args, **sample.kwargs)
+            got = jfn(*sample.args, **sample.kwargs)
+            _compare(got, expected, opinfo, dtype)
