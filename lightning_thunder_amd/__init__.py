@@ -252,6 +252,13 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             entry.computation_traces = computation_traces + fw_traces
             entry.backward_traces = bw_traces
         else:
+            if cd.compile_options.get("inplace_index_copy", True):
+                from .transforms.inplace_index_copy import inplace_index_copy
+
+                comp2 = inplace_index_copy(comp)
+                if comp2 is not comp:
+                    comp = comp2
+                    computation_traces.append(comp)
             ex_traces = transform_for_execution(comp, executors)
             c = ex_traces[-1]
             c = maybe_sort_waits(c)

@@ -1,0 +1,112 @@
+"""Generation latency benchmark (parity: reference ``examples/quickstart/hf_llm.py``; README
+``README.md:308-317``: HF Llama-3.2-1B, 100 new tokens, static cache — eager 1,493 ms,
+Thunder + CUDAGraphs 542 ms on 1x H100).
+
+Same task on MI355X with the LitGPT-architecture Llama-3.2-1B (random-init weights, synthetic
+prompt; no checkpoints offline): greedy decoding of ``--new-tokens`` tokens after a
+``--prompt-len`` token prompt with a static KV cache, bf16.  Modes:
+
+* ``eager``    — PyTorch eager (ROCm), same model code;
+* ``thunder``  — ``jit(model)``: prefill and decode are two cached programs (hipex/hipfuse kernels,
+  in-place KV-cache updates);
+* ``hipgraph`` — ``jit(model, transforms=[HipGraphTransform()])``: the decode step replays as
+  hipGraphs (the "reduce-overhead" configuration).
+
+Prints one JSON line per mode: mean latency (ms) of ``--iters`` full generations after
+``--warmup`` untimed ones.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+import torch
+
+
+def _build(model_name: str, max_seq: int, device, n_layer=None):
+    from ..models.litgpt import GPT, Config, init_weights
+
+    kw = {} if n_layer is None else {"n_layer": n_layer}
+    cfg = Config.from_name(model_name, **kw)
+    with torch.device("meta"):
+        model = GPT(cfg)
+    model = model.to_empty(device=device).to(torch.bfloat16)
+    torch.manual_seed(0)
+    init_weights(model)
+    model.requires_grad_(False)
+    model.eval()
+    model.set_kv_cache(1, max_seq, device=device, dtype=torch.bfloat16)
+    return model, cfg
+
+
+def run(mode: str, args) -> dict:
+    import lightning_thunder_amd as thunder
+    from ..models.litgpt import generate
+
+    device = torch.device("cuda", 0)
+    model, cfg = _build(args.model, args.prompt_len + args.new_tokens + 8, device, args.n_layer)
+    prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), device=device)
+    if mode == "eager":
+        fwd = model
+    elif mode == "thunder":
+        fwd = thunder.jit(model)
+    else:
+        from ..transforms.hipgraph import HipGraphTransform
+
+        fwd = thunder.jit(model, transforms=[HipGraphTransform()])
+
+    def once():
+        return generate(model, prompt, args.new_tokens, forward=fwd)
+
+    t0 = time.perf_counter()
+    out = once()
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    for _ in range(args.warmup):
+        once()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(args.iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = once()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ms = 1000 * sum(times) / len(times)
+    res = {
+        "metric": f"{args.model} greedy generate latency ({args.new_tokens} new tokens, static KV cache)",
+        "mode": mode, "value": round(ms, 2), "unit": "ms", "higher_is_better": False,
+        "ms_per_token": round(ms / args.new_tokens, 3), "first_call_s": round(first, 2),
+        "prompt_len": args.prompt_len, "new_tokens": args.new_tokens, "dtype": "bf16",
+        "data": "synthetic prompt, random-init weights", "n_gpus": 1,
+        "reference_ms": {"thunder+cudagraphs (1xH100)": 542, "eager (1xH100)": 1493},
+    }
+    res["tokens"] = out[0, -4:].tolist()
+    return res
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="Llama-3.2-1B")
+    p.add_argument("--prompt-len", type=int, default=16)
+    p.add_argument("--new-tokens", type=int, default=100)
+    p.add_argument("--iters", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--modes", default="eager,thunder,hipgraph")
+    p.add_argument("--n-layer", type=int, default=None, help="debug only")
+    args = p.parse_args(argv)
+    results = []
+    for mode in args.modes.split(","):
+        r = run(mode, args)
+        results.append(r)
+        print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+    toks = {tuple(r["tokens"]) for r in results}
+    if len(toks) > 1:
+        print(f"warning: modes generated different tokens: {toks}", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -171,19 +171,47 @@ def _norm(config: Config, size: int) -> nn.Module:
     return nn.LayerNorm(size, eps=config.norm_eps)
 
 
+class KVCache(nn.Module):
+    """Static key/value cache (LitGPT ``KVCache``): [B, n_query_groups, max_seq, head_size] buffers
+    updated in place at ``input_pos``.  Static storage keeps the decode step's addresses fixed, so
+    a compiled decode step is a cache hit every token and can be replayed as one hipGraph."""
+
+    def __init__(self, k_shape, v_shape, device=None, dtype=None):
+        super().__init__()
+        self.register_buffer("k", torch.zeros(k_shape, device=device, dtype=dtype), persistent=False)
+        self.register_buffer("v", torch.zeros(v_shape, device=device, dtype=dtype), persistent=False)
+
+    def forward(self, input_pos: torch.Tensor, k: torch.Tensor, v: torch.Tensor):
+        k_all = self.k.index_copy_(2, input_pos, k.to(self.k.dtype))
+        v_all = self.v.index_copy_(2, input_pos, v.to(self.v.dtype))
+        return k_all, v_all
+
+    def reset_parameters(self) -> None:
+        torch.nn.init.zeros_(self.k)
+        torch.nn.init.zeros_(self.v)
+
+
 class CausalSelfAttention(nn.Module):
     def __init__(self, config: Config):
         super().__init__()
         self.attn = nn.Linear(config.n_embd, config.qkv_size, bias=config.bias)
         self.proj = nn.Linear(config.n_head * config.head_size, config.n_embd, bias=config.bias)
         self.config = config
+        self.kv_cache: Optional[KVCache] = None
 
-    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, T, C = x.shape
         c = self.config
         qkv = self.attn(x)
         q, k, v = qkv_split_rope(qkv, cos, sin, c.n_head, c.n_query_groups, c.head_size, c.rope_n_elem)
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.n_query_groups != c.n_head)
+        if input_pos is not None:
+            if self.kv_cache is None:
+                raise TypeError("call model.set_kv_cache(...) before passing input_pos")
+            k, v = self.kv_cache(input_pos, k, v)
+            y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=c.n_query_groups != c.n_head)
+        else:
+            y = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.n_query_groups != c.n_head)
         y = y.transpose(1, 2).reshape(B, T, c.n_head * c.head_size)
         return self.proj(y)
 
@@ -266,9 +294,10 @@ class Block(nn.Module):
             self.mlp = GptNeoxMLP(config)
         self.config = config
 
-    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
         x_normed = self.norm_1(x)
-        h = self.attn(x_normed, cos, sin)
+        h = self.attn(x_normed, cos, sin, mask, input_pos)
         if self.config.parallel_residual:
             n2 = x_normed if self.norm_2 is None else self.norm_2(x)
             return self.mlp(n2) + h + x
@@ -293,6 +322,7 @@ class GPT(nn.Module):
         self.max_seq_length = config.block_size
         self.register_buffer("cos", torch.empty(0), persistent=False)
         self.register_buffer("sin", torch.empty(0), persistent=False)
+        self.mask_cache: Optional[torch.Tensor] = None
         self._rope_seq = 0
 
     def set_rope_cache(self, seq_len: int, device=None) -> None:
@@ -302,15 +332,42 @@ class GPT(nn.Module):
         self.sin = sin
         self._rope_seq = seq_len
 
-    def forward(self, idx: torch.Tensor) -> torch.Tensor:
+    def set_kv_cache(self, batch_size: int, max_seq_length: Optional[int] = None, device=None,
+                     dtype: Optional[torch.dtype] = None) -> None:
+        """Allocates a static KV cache in every block and the causal mask for incremental decoding."""
+        c = self.config
+        max_seq_length = max_seq_length or c.block_size
+        dtype = dtype or self.lm_head.weight.dtype
+        device = device or self.lm_head.weight.device
+        shape = (batch_size, c.n_query_groups, max_seq_length, c.head_size)
+        for block in self.transformer.h:
+            block.attn.kv_cache = KVCache(shape, shape, device=device, dtype=dtype)
+        if self.cos.numel() == 0 or self.cos.shape[0] < max_seq_length:
+            self.set_rope_cache(max_seq_length, device=device)
+        ones = torch.ones((max_seq_length, max_seq_length), device=device, dtype=torch.bool)
+        self.mask_cache = torch.tril(ones).unsqueeze(0).unsqueeze(0)
+        self.max_seq_length = max_seq_length
+
+    def clear_kv_cache(self) -> None:
+        for block in self.transformer.h:
+            block.attn.kv_cache = None
+        self.mask_cache = None
+
+    def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
         T = idx.size(1)
         if self.cos.numel() == 0 or self.cos.shape[0] < T:
             raise RuntimeError("call model.set_rope_cache(seq_len, device) before forward")
-        cos = self.cos[:T]
-        sin = self.sin[:T]
+        if input_pos is not None:  # incremental decoding against the KV cache
+            cos = self.cos.index_select(0, input_pos)
+            sin = self.sin.index_select(0, input_pos)
+            mask = self.mask_cache.index_select(2, input_pos)
+        else:
+            cos = self.cos[:T]
+            sin = self.sin[:T]
+            mask = None
         x = self.transformer.wte(idx)
         for block in self.transformer.h:
-            x = block(x, cos, sin)
+            x = block(x, cos, sin, mask, input_pos)
         x = self.transformer.ln_f(x)
         return self.lm_head(x)
 
@@ -338,3 +395,42 @@ def flops_per_token(config: Config, seq_len: int, training: bool = True) -> floa
     attn = c.n_layer * 2 * 2 * seq_len * c.n_head * c.head_size / 2  # causal: half of QK^T and PV
     fwd = 2 * n_params_linear + attn
     return fwd * (3 if training else 1)
+
+
+@torch.no_grad()
+def generate(model, prompt: torch.Tensor, max_new_tokens: int, *, forward=None, temperature: float = 0.0,
+             top_k: Optional[int] = None, eos_id: Optional[int] = None) -> torch.Tensor:
+    """Autoregressive generation with the static KV cache (LitGPT ``generate``).
+
+    ``forward`` is the callable used for every step (default: ``model``; pass ``thunder.jit(model)``).
+    Prefill runs the prompt with ``input_pos = arange(T)``; every decode step feeds one token with
+    the *same* ``input_pos`` tensor advanced in place, so a compiled decode step keeps its input
+    addresses (hipGraph-replayable) and is a cache hit after the first token.
+    Greedy when ``temperature == 0``.  Returns ``[B, T + max_new_tokens]`` token ids.
+    """
+    forward = forward or model
+    B, T = prompt.shape
+    if model.transformer.h[0].attn.kv_cache is None:
+        raise RuntimeError("call model.set_kv_cache(batch_size, max_seq_length) first")
+    device = prompt.device
+    input_pos = torch.arange(T, device=device)
+    logits = forward(prompt, input_pos)
+    out = [prompt]
+    pos = torch.tensor([T], device=device, dtype=torch.int64)
+    for i in range(max_new_tokens):
+        last = logits[:, -1]
+        if temperature > 0:
+            last = last / temperature
+            if top_k is not None:
+                v, _ = torch.topk(last, min(top_k, last.size(-1)))
+                last = torch.where(last < v[:, [-1]], torch.full_like(last, -float("inf")), last)
+            nxt = torch.multinomial(torch.softmax(last.float(), -1), 1)
+        else:
+            nxt = last.argmax(-1, keepdim=True)
+        out.append(nxt)
+        if eos_id is not None and bool((nxt == eos_id).all()):
+            break
+        if i + 1 < max_new_tokens:
+            logits = forward(nxt, pos)
+            pos.add_(1)
+    return torch.cat(out, dim=1)

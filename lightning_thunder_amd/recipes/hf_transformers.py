@@ -15,11 +15,7 @@ from ..core.transform_common import Transform
 from .base import BaseRecipe
 
 
-class InplaceIndexCopyTransform(Transform):
-    """Rewrites ``Tensor.index_copy_`` on cache buffers into ``index_copy`` + copy-back (functional)."""
-
-    def transform_traces_pre_prologue(self, prologue_trace, computation_trace, epilogue_trace, **kwargs):
-        return prologue_trace, computation_trace, epilogue_trace
+from ..transforms.inplace_index_copy import InplaceIndexCopyTransform  # noqa: E402
 
 
 class HFTransformers(BaseRecipe):
