@@ -58,6 +58,7 @@ def test_generate_gpu_bf16(graphs):
     out = generate(m, p, 16, forward=jm)
     out2 = generate(m, p, 16, forward=jm)  # replays
     torch.cuda.synchronize()
-    # bf16 kernels differ from eager's in rounding: greedy tokens agree on the first steps
-    assert torch.equal(out[:, :10], ref[:, :10])
-    assert torch.equal(out, out2)
+    # bf16 kernels differ from eager's in rounding, so near-ties in the random-init logits can
+    # flip a later greedy token: the prompt and the first generated tokens must agree
+    assert torch.equal(out[:, :12], ref[:, :12])
+    assert torch.equal(out, out2)  # replays are deterministic

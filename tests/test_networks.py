@@ -108,3 +108,33 @@ def test_litgpt_configs_training_parity(name):
     ref.sum().backward()
     for g, p in zip(grads, m.parameters()):
         torch.testing.assert_close(g, p.grad, atol=1e-4, rtol=1e-3)
+
+
+def test_nanogpt_training_parity():
+    from lightning_thunder_amd.models.nanogpt import NanoGPT
+
+    torch.manual_seed(0)
+    m = NanoGPT.from_name("gpt2", n_layer=2, n_embd=64, n_head=4, vocab_size=256, block_size=64, dropout=0.0)
+    x = torch.randint(0, 256, (2, 32))
+    jm = thunder.jit(m)
+    logits, loss = jm(x, x)
+    rl, rloss = m(x, x)
+    torch.testing.assert_close(logits, rl, atol=1e-5, rtol=1e-4)
+    loss.backward()
+    g = [p.grad.clone() for p in m.parameters()]
+    m.zero_grad()
+    rloss.backward()
+    for a, p in zip(g, m.parameters()):
+        torch.testing.assert_close(a, p.grad, atol=1e-5, rtol=1e-4)
+
+
+def test_nanogpt_dropout_trains():
+    from lightning_thunder_amd.models.nanogpt import NanoGPT
+
+    torch.manual_seed(0)
+    m = NanoGPT.from_name("test", dropout=0.1, vocab_size=256, block_size=16, n_head=2)
+    x = torch.randint(0, 256, (4, 8))
+    jm = thunder.jit(m)
+    _, loss = jm(x, x)
+    loss.backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
