@@ -506,8 +506,42 @@ hip_attn_bwd = ex.register_operator(
 )
 
 
+def _decode_attn_meta(q, k, v, mask, causal, scale):
+    return TensorProxy(like=q)
+
+
+def _decode_attn_impl(q, k, v, mask, causal, scale):
+    from ..ops.attention import decode_attn
+
+    return decode_attn(q, k, v, mask, causal, scale)
+
+
+hip_decode_attn = ex.register_operator("hip_decode_attn", meta=_decode_attn_meta, fn=_decode_attn_impl)
+
+
+def _broadcastable(shape, target) -> bool:
+    if len(shape) > len(target):
+        return False
+    for a, b in zip(reversed(shape), reversed(target)):
+        if a != 1 and a != b:
+            return False
+    return True
+
+
+def _is_decode(query, key, attn_mask) -> bool:
+    """Few query rows against a KV cache with a boolean mask: the K3d decode kernel."""
+    from ..ops.attention import DECODE_MAX_QUERIES
+
+    if attn_mask is None or not isinstance(attn_mask, TensorProxy) or attn_mask.dtype != torch.bool:
+        return False
+    B, Hq, T, _ = query.shape
+    return T <= DECODE_MAX_QUERIES and _broadcastable(tuple(attn_mask.shape), (B, Hq, T, key.shape[2]))
+
+
 def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
-    if attn_mask is not None or dropout_p != 0.0 or not _gpu(query, key, value):
+    if dropout_p != 0.0 or not _gpu(query, key, value):
+        return False
+    if attn_mask is not None and not (query.ndim == 4 and _is_decode(query, key, attn_mask)):
         return False
     if query.ndim != 4 or key.ndim != 4 or value.ndim != 4:
         return False
@@ -528,11 +562,15 @@ def _sc(q, scale):
 
 
 def _sdpa_exec(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    if attn_mask is not None:
+        return hip_decode_attn(query, key, value, attn_mask, bool(is_causal), _sc(query, scale))
     out, _ = hip_attn_fwd(query, key, value, bool(is_causal), _sc(query, scale))
     return out
 
 
 def _sdpa_grad(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
+    if attn_mask is not None:
+        return None  # decline: the generic rule differentiates; the forward still runs on K3d
     sc = _sc(query, scale)
     out, lse = hip_attn_fwd(query, key, value, bool(is_causal), sc)
 

@@ -64,3 +64,55 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None):
                           ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal), stream_ptr(q.device))
     check(rc, "lta_attn_bwd")
     return dq, dk, dv
+
+
+# ------------------------------------------------------------------------------------------------
+# K3d decode attention (csrc/decode_attention.hip): T <= 16 query rows against a long KV cache
+# ------------------------------------------------------------------------------------------------
+import ctypes  # noqa: E402
+
+from ._lib import c_int64  # noqa: E402
+
+register_signature("lta_decode_attn", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float,
+                                       c_void_p])
+
+DECODE_MAX_QUERIES = 16
+
+
+def _aligned_rows(t: torch.Tensor) -> torch.Tensor:
+    """Head dim contiguous and every row start 16-byte aligned (the kernel uses 16-byte loads)."""
+    ok = t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
+    return t if ok else t.contiguous()
+
+
+def decode_attn(q, k, v, mask=None, causal: bool = False, scale: float | None = None):
+    """q [B, Hq, T, D] (T <= 16), k/v [B, Hkv, S, D], mask bool broadcastable to [B, Hq, T, S] -> [B, Hq, T, D]."""
+    lib = require()
+    q, k, v = _aligned_rows(q), _aligned_rows(k), _aligned_rows(v)
+    B, Hq, T, D = q.shape
+    Hkv, S = k.shape[1], k.shape[2]
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    if mask is not None:
+        mask = torch.broadcast_to(mask, (B, Hq, T, S))
+        ms = mask.stride()
+    else:
+        ms = (0, 0, 0, 0)
+    rows = B * Hq * T
+    blocks = (rows + 3) // 4
+    # split the cache so that a decode step still launches >= ~256 workgroups (flash-decoding)
+    nsplit = max(1, min((256 + blocks - 1) // blocks, (S + 127) // 128))
+    chunk = ((S + nsplit - 1) // nsplit + 63) // 64 * 64
+    nsplit = (S + chunk - 1) // chunk
+    o = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)
+    ws_acc = ws_ml = None
+    if nsplit > 1:
+        ws_acc = torch.empty((nsplit, rows, D), device=q.device, dtype=torch.float32)
+        ws_ml = torch.empty((nsplit, rows, 2), device=q.device, dtype=torch.float32)
+    st = (ctypes.c_int64 * 13)(q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                               v.stride(0), v.stride(1), v.stride(2), *ms)
+    mptr = None if mask is None else mask.data_ptr()
+    rc = lib.lta_decode_attn(dcode(q), ptr(q), ptr(k), ptr(v), mptr, ptr(o), ptr(ws_acc), ptr(ws_ml), B, Hq, Hkv, T, S, D,
+                             ctypes.cast(st, ctypes.c_void_p), chunk, nsplit, int(causal), float(sc), stream_ptr(q.device))
+    check(rc, "lta_decode_attn")
+    return o

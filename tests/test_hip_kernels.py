@@ -324,3 +324,58 @@ def test_fp8_inference_linear_gpu(M):
     assert y.shape == (2, M, N) and y.dtype == torch.bfloat16
     err = (y.float() - ref).abs().max() / ref.abs().max()
     assert err < 0.06, err
+
+
+def _sdpa_ref(q, k, v, mask, causal, scale):
+    qf, kf, vf = q.float(), k.float(), v.float()
+    rep = q.shape[1] // k.shape[1]
+    kf, vf = kf.repeat_interleave(rep, 1), vf.repeat_interleave(rep, 1)
+    s = qf @ kf.transpose(-2, -1) * scale
+    if causal:
+        s = s.masked_fill(~torch.ones(q.shape[2], k.shape[2], device=q.device, dtype=torch.bool).tril(), float("-inf"))
+    if mask is not None:
+        s = s.masked_fill(~mask, float("-inf"))
+    return torch.softmax(s, -1) @ vf
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,Hq,Hkv,T,S,D", [
+    (1, 32, 8, 1, 124, 64),     # Llama-3.2-1B decode, short cache (single split)
+    (1, 32, 8, 1, 4096, 128),   # long cache: split-K + combine
+    (2, 8, 8, 3, 700, 64),      # MHA, a few query rows, ragged tail block
+    (1, 4, 2, 16, 257, 128),    # prefill-chunk sized T
+])
+@pytest.mark.parametrize("mask_kind", ["cache_mask", "none", "causal"])
+def test_decode_attention(dtype, B, Hq, Hkv, T, S, D, mask_kind):
+    import math
+
+    from lightning_thunder_amd.ops.attention import decode_attn
+
+    torch.manual_seed(0)
+    q = torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
+    k = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype)
+    v = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype)
+    scale = 1.0 / math.sqrt(D)
+    mask, causal = None, False
+    if mask_kind == "cache_mask":  # LitGPT/HF: rows of a causal mask cache picked at input_pos
+        pos = torch.arange(S - T, S, device="cuda") - S // 3
+        mask = torch.ones(S, S, device="cuda", dtype=torch.bool).tril()[None, None].index_select(2, pos)
+    elif mask_kind == "causal":
+        causal = True
+    out = decode_attn(q, k, v, mask, causal, scale)
+    ref = _sdpa_ref(q, k, v, mask, causal, scale)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_decode_attention_claimed_in_generate():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights, generate
+
+    torch.manual_seed(0)
+    m = GPT.from_name("llama3-like", n_layer=2, n_embd=256, n_head=4, intermediate_size=512).to(device="cuda", dtype=torch.bfloat16)
+    init_weights(m, std=0.2)
+    m.requires_grad_(False)
+    m.set_kv_cache(1, 64)
+    jm = thunder.jit(m)
+    generate(m, torch.randint(0, 300, (1, 8), device="cuda"), 4, forward=jm)
+    assert "hip_decode_attn" in str(thunder.last_traces(jm)[-1])
