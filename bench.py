@@ -39,7 +39,9 @@ def parse_args():
     p.add_argument("--seq", type=int, default=4096)
     p.add_argument("--mbs", type=int, default=1)
     p.add_argument("--mode", default="thunder", choices=["thunder", "eager"])
-    p.add_argument("--parallel", default="auto", choices=["auto", "fsdp", "ddp", "none"])
+    p.add_argument("--parallel", default="auto", choices=["auto", "fsdp", "ddp", "tp", "none"],
+                   help="auto: fsdp for N>1; tp: Megatron tensor parallel over all ranks (BASELINE config 4, "
+                        "e.g. --model Llama-3-8B --parallel tp; strong scaling)")
     p.add_argument("--executors", default=None, help="comma separated executor names (default: framework defaults)")
     p.add_argument("--fp8", action="store_true")
     p.add_argument("--hipgraph", action="store_true")
@@ -123,6 +125,13 @@ def run(args, rank, world, device, mode):
             from lightning_thunder_amd.distributed import ddp
 
             jm = ddp(jm)
+        elif world > 1 and parallel == "tp":
+            from lightning_thunder_amd.distributed import column_parallel, row_parallel
+
+            n = cfg.n_layer
+            cols = [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.attn", "mlp.fc_1", "mlp.fc_2")]
+            rows = [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.proj", "mlp.proj")]
+            jm = row_parallel(column_parallel(jm, cols), rows)
         fwd = jm
         params = list(jm.parameters())
     else:
@@ -135,6 +144,9 @@ def run(args, rank, world, device, mode):
     opt = make_optimizer(params, mode)
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
+
+    if parallel == "tp":
+        gen.manual_seed(1000)  # tensor parallel: every rank sees the same tokens
 
     def batch():
         x = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq + 1), device=device, generator=gen)
@@ -199,7 +211,8 @@ def main():
             torch.distributed.init_process_group(backend)
 
     dt, cfg, mem, parallel = run(args, rank, world, device, args.mode)
-    tokens = args.steps * args.mbs * args.seq * world
+    data_parallel = parallel != "tp"
+    tokens = args.steps * args.mbs * args.seq * (world if data_parallel else 1)
     value = tokens / dt
     per_gpu = value / world
     from lightning_thunder_amd.models.litgpt import flops_per_token
@@ -222,13 +235,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1000, 3),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(per_gpu / base, 4),
+            "scaling": "weak" if data_parallel else "strong",
+            "vs_baseline": round(per_gpu / base, 4) if data_parallel else None,  # no published TP number
             "dtype": "fp8" if args.fp8 else "bf16",
             "data": "synthetic token ids, random-init weights",
             "config": {
                 "model": args.model + ("" if args.n_layer is None else f"-{args.n_layer}L(debug)"),
-                "global_batch": args.mbs * world,
+                "global_batch": args.mbs * (world if data_parallel else 1),
                 "micro_batch": args.mbs,
                 "seq_len": args.seq,
                 "parallelism": f"{parallel}{world}" if world > 1 else "single",

@@ -145,6 +145,16 @@ def _check_traces(traces, cd):
 from .core.functionalization import storage_alias_pattern  # noqa: E402
 
 
+def _post_transforms(cd: CompileData) -> list:
+    """User transforms, plus the kernel-sync debug transform when requested."""
+    ts = list(cd.transforms)
+    if cd.debug_options.sync_after_each_kernel:
+        from .dev_utils.numerics_check import SyncAfterEachKernelTransform
+
+        ts.append(SyncAfterEachKernelTransform())
+    return ts
+
+
 def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) -> CacheEntry:
     from .core.jit_ext import acquire
     from .executors.passes import transform_for_execution, del_last_used
@@ -234,7 +244,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             fw = del_last_used(fw)
             bw = del_last_used(bw)
             bw.unpack_list_arg = True
-            for t in cd.transforms:
+            for t in _post_transforms(cd):
                 fw = t.transform_trace_post_optimization(fw, compile_data=cd)
                 bw = t.transform_trace_post_optimization(bw, compile_data=cd)
             fw_traces.append(fw)
@@ -263,7 +273,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             c = ex_traces[-1]
             c = maybe_sort_waits(c)
             c = del_last_used(c)
-            for t in cd.transforms:
+            for t in _post_transforms(cd):
                 c = t.transform_trace_post_optimization(c, compile_data=cd)
             ex_traces.append(c)
             _check_traces(ex_traces, cd)

@@ -372,7 +372,7 @@ def test_decode_attention_claimed_in_generate():
     from lightning_thunder_amd.models.litgpt import GPT, init_weights, generate
 
     torch.manual_seed(0)
-    m = GPT.from_name("llama3-like", n_layer=2, n_embd=256, n_head=4, intermediate_size=512).to(device="cuda", dtype=torch.bfloat16)
+    m = GPT.from_name("llama3-like", n_layer=2, n_embd=256, n_head=4, head_size=64, intermediate_size=512).to(device="cuda", dtype=torch.bfloat16)
     init_weights(m, std=0.2)
     m.requires_grad_(False)
     m.set_kv_cache(1, 64)

@@ -243,3 +243,21 @@ def test_fp8_inference_transform_cpu():
     out.sum().backward()
     assert x.grad is not None
     assert any("fp8_linear_inference" in b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols)
+
+
+def test_numerics_check_transform_cpu():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.dev_utils.numerics_check import NumericsCheckTransform
+
+    def f(x, y):
+        return torch.log(x) * y + torch.exp(y).sum(-1, keepdim=True)
+
+    t = NumericsCheckTransform(sync=False)
+    jf = thunder.jit(f, transforms=[t])
+    x, y = torch.rand(4, 8) + 0.1, torch.randn(4, 8)
+    torch.testing.assert_close(jf(x, y), f(x, y))
+    assert t.checked > 0 and not t.findings
+    jf(-x, y)  # log of negatives -> nan from finite inputs: reported
+    assert any("non-finite" in m for m in t.findings)
+    jd = thunder.jit(f, debug_options=thunder.DebugOptions(sync_after_each_kernel=True))
+    torch.testing.assert_close(jd(x, y), f(x, y))
