@@ -9,11 +9,14 @@ MI355X design:
 * ``torch.cuda.CUDAGraph`` is a hipGraph on ROCm; every launch inside a region — hipBLASLt
   GEMMs, the hand-written HIP kernels (ctypes launches on the current stream) and
   hipfuse's ``hipModuleLaunchKernel`` launches — is captured.
-* Inputs are *not* copied into separate static buffers up front: the first captured
-  call's tensors become the graph's static inputs, and on replay an input is copied only
-  if it lives at a different address.  Parameters never move and the backward consumes
-  the forward graph's outputs (which live in the graph pool at fixed addresses), so in a
-  training step only the token batch and the incoming loss gradient are copied.
+* Framework-owned inputs are not copied into separate static buffers: the captured call's
+  tensors become the graph's static inputs and on replay an input is copied only if it lives
+  at a different address.  Parameters/buffers never move and the backward consumes the
+  forward graph's outputs (graph pool, fixed addresses), so a training step copies only the
+  token batch and the incoming loss gradient.  Tensors the *caller* passed in (arguments of
+  a forward/computation trace that are not parameters/buffers) are cloned into private
+  static buffers at capture: the caller may keep using its tensor (e.g. ``generate`` keeps
+  every sampled token), and later replays must not write into it.
 * One private memory pool is shared by every graph of the transform (fw and bw graphs
   replay in capture order), so graphed memory ~= eager peak.
 * First call per signature runs eagerly (warm-up: lazy library init, hiprtc compiles of
@@ -62,8 +65,10 @@ def default_capturable(bsym: BoundSymbol, *, capture_collectives: bool = False) 
 class HipGraphRunner:
     """Graph cache for one region (reference ``CUDAGraphRunner``)."""
 
-    def __init__(self, fn, name: str, pool_owner: "HipGraphTransform", copy_outputs: bool = False):
+    def __init__(self, fn, name: str, pool_owner: "HipGraphTransform", copy_outputs: bool = False,
+                 private_inputs: tuple = ()):
         self.fn = fn
+        self.private_inputs = private_inputs
         self.name = name
         self.owner = pool_owner
         self.copy_outputs = copy_outputs
@@ -102,7 +107,9 @@ class HipGraphRunner:
         return outs
 
     def _capture(self, key, args):
-        ins = tuple(args)
+        priv = self.private_inputs
+        ins = tuple(a.clone() if (i < len(priv) and priv[i] and isinstance(a, torch.Tensor)) else a
+                    for i, a in enumerate(args))
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         with torch.cuda.graph(g, pool=self.owner.pool()):
@@ -163,6 +170,12 @@ class HipGraphTransform(Transform):
             for b in bs:
                 s |= {a.name for a in b.flat_proxy_args}
             later_uses[i] = s
+        from ..core.proxies import ProxyTag
+
+        caller_owned = set()
+        if not trace.unpack_list_arg:  # forward / inference program: its tensor args come from the caller
+            caller_owned = {a.name for a in trace.args
+                            if isinstance(a, TensorProxy) and ProxyTag.STATIC_MEMORY_LOCATION not in a.tags}
         new_bsyms = []
         for i, r in enumerate(regions):
             if not isinstance(r, list):
@@ -196,7 +209,8 @@ class HipGraphTransform(Transform):
             sub.bound_symbols = list(r) + [prims.python_return.bind(tuple(outputs), output=None)]
             sub = del_last_used(sub)
             fn = sub.python_callable()
-            runner = HipGraphRunner(fn, name, self, copy_outputs=self.copy_outputs)
+            private = tuple(isinstance(p, TensorProxy) and p.name in caller_owned for p in inputs)
+            runner = HipGraphRunner(fn, name, self, copy_outputs=self.copy_outputs, private_inputs=private)
             self.runners.append(runner)
             sym = Symbol(name, meta=None, is_prim=True, is_fusion=True)
             nb = BoundSymbol(sym, args=tuple(inputs), kwargs={}, output=tuple(outputs), subsymbols=list(r),
