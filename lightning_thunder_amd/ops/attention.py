@@ -101,7 +101,7 @@ def decode_attn(q, k, v, mask=None, causal: bool = False, scale: float | None = 
     rows = B * Hq * T
     blocks = (rows + 3) // 4
     # split the cache so that a decode step still launches >= ~256 workgroups (flash-decoding)
-    nsplit = max(1, min((256 + blocks - 1) // blocks, (S + 127) // 128))
+    nsplit = max(1, min((256 + blocks - 1) // blocks, S // 256))  # a split is worth a combine launch from ~256 keys
     chunk = ((S + nsplit - 1) // nsplit + 63) // 64 * 64
     nsplit = (S + chunk - 1) // chunk
     o = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)

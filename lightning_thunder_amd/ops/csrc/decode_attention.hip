@@ -6,11 +6,14 @@
 // reading K/V once.  Layout of the work (wave64, CDNA4):
 //   * one wave owns one query row (b, hq, t); a 256-thread block holds 4 rows with consecutive
 //     hq, i.e. heads of the same KV group (GQA) -> the 4 waves stream the same K/V rows (L1/L2 hits);
-//   * QK^T: lane l scores key j0+l (its K row read with 16-byte loads, q held in VGPRs as fp32);
-//     a 64-key block whose mask is all-false is skipped before any K/V byte is read;
+//   * lane l owns key j0+l of each 64-key block for both products: QK^T reads its K row with
+//     16-byte loads against q broadcast from LDS, PV accumulates p * V-row into a per-lane
+//     acc[D] (no serial per-key loop); a block whose mask is all-false is skipped before any
+//     K/V byte is read;
 //   * online softmax with wave max/sum butterflies once per 64 keys;
-//   * PV: lane l owns head dims {l} (D=64) or {2l, 2l+1} (D=128) -> every V row is one coalesced
-//     128/256-byte wave load; p is broadcast from wave-private LDS;
+//   * the per-lane partial outputs are combined once per row by a recursive-halving
+//     reduce-scatter of shuffles (D/2 + D/4 + ... + D/64 of them), leaving each lane D/64
+//     contiguous output dims;
 //   * split-K over the cache (grid.y) when the cache is long: partial (m, l, acc) go to an fp32
 //     workspace and a combine kernel merges them (flash-decoding).
 #include "common.h"
@@ -26,8 +29,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     T* __restrict__ o, float* __restrict__ ws_acc, float* __restrict__ ws_ml, int B, int Hq, int Hkv, int Tq, int S,
     int64_t qsb, int64_t qsh, int64_t qst, int64_t ksb, int64_t ksh, int64_t kss, int64_t vsb, int64_t vsh,
     int64_t vss, int64_t msb, int64_t msh, int64_t mst, int64_t mss, int chunk, int causal, float scale) {
-  constexpr int DPL = D / 64;  // output dims per lane
-  __shared__ float p_lds[kRowsPerBlock][64];
+  constexpr int DPL = D / 64;          // output dims per lane after the final reduce-scatter
+  constexpr int NV = Vec16<T>::N;      // elements per 16-byte load
+  __shared__ float q_lds[kRowsPerBlock][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rows = B * Tq * Hq;
   const int row = blockIdx.x * kRowsPerBlock + w;
@@ -41,66 +45,68 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   int j_end = min(S, j_begin + chunk);
   if (causal) j_end = min(j_end, t + 1);
 
-  // q row in fp32 registers (same address for all lanes: broadcast loads)
-  float qf[D];
+  // scaled q row -> wave-private LDS (read back as broadcasts)
   const T* qrow = q + b * qsb + hq * qsh + t * qst;
-#pragma unroll
-  for (int d = 0; d < D; d += Vec16<T>::N) {
-    Vec16<T> x = load16(qrow + d);
-#pragma unroll
-    for (int e = 0; e < Vec16<T>::N; ++e) qf[d + e] = to_f32(x.v[e]) * scale;
-  }
+  for (int d = lane; d < D; d += 64) q_lds[w][d] = to_f32(qrow[d]) * scale;
+  __builtin_amdgcn_wave_barrier();
   const T* kbase = k + b * ksb + hk * ksh;
   const T* vbase = v + b * vsb + hk * vsh;
   const uint8_t* mrow = mask ? mask + b * msb + hq * msh + t * mst : nullptr;
 
+  // every lane owns one key per 64-key block: QK and PV are both lane-parallel; the per-lane
+  // partial outputs acc[D] are reduce-scattered across the wave once at the end.
   float m = -INFINITY, l = 0.f;
-  float acc[DPL];
+  float acc[D];
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+  for (int i = 0; i < D; ++i) acc[i] = 0.f;
 
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const int j = j0 + lane;
     bool valid = j < j_end;
     if (valid && mrow) valid = mrow[(int64_t)j * mss] != 0;
-    if (!__any(valid)) continue;
+    if (!__any(valid)) continue;  // fully masked block: no K/V traffic
     float s = -INFINITY;
     if (valid) {
       const T* krow = kbase + (int64_t)j * kss;
       float dot = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; d += Vec16<T>::N) {
+      for (int d = 0; d < D; d += NV) {
         Vec16<T> x = load16(krow + d);
 #pragma unroll
-        for (int e = 0; e < Vec16<T>::N; ++e) dot = fmaf(qf[d + e], to_f32(x.v[e]), dot);
+        for (int e = 0; e < NV; ++e) dot = fmaf(q_lds[w][d + e], to_f32(x.v[e]), dot);
       }
       s = dot;
     }
-    const float bm = wave_max(s);
-    const float m_new = fmaxf(m, bm);
+    const float m_new = fmaxf(m, wave_max(s));
     const float p = valid ? __expf(s - m_new) : 0.f;
     const float corr = __expf(m - m_new);  // m = -inf on the first block -> 0
     l = l * corr + wave_sum(p);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) acc[i] *= corr;
     m = m_new;
-    p_lds[w][lane] = p;
-    __builtin_amdgcn_wave_barrier();
-    const int nk = min(64, j_end - j0);
-    for (int kk = 0; kk < nk; ++kk) {
-      const float pk = p_lds[w][kk];
-      if (pk == 0.f) continue;  // masked key (uniform across the wave)
-      const T* vrow = vbase + (int64_t)(j0 + kk) * vss + lane * DPL;
-      if (DPL == 2) {
-        const uint32_t raw = *reinterpret_cast<const uint32_t*>(vrow);
-        const T* pair = reinterpret_cast<const T*>(&raw);
-        acc[0] = fmaf(pk, to_f32(pair[0]), acc[0]);
-        acc[DPL - 1] = fmaf(pk, to_f32(pair[1]), acc[DPL - 1]);
-      } else {
-        acc[0] = fmaf(pk, to_f32(vrow[0]), acc[0]);
+    if (valid) {
+      const T* vrow = vbase + (int64_t)j * vss;
+#pragma unroll
+      for (int d = 0; d < D; d += NV) {
+        Vec16<T> x = load16(vrow + d);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) acc[d + e] = fmaf(p, to_f32(x.v[e]), acc[d + e] * corr);
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc[i] *= corr;
     }
-    __builtin_amdgcn_wave_barrier();
+  }
+
+  // recursive-halving reduce-scatter over the 64 lanes: lane ends with dims [lane*DPL, lane*DPL+DPL)
+#pragma unroll
+  for (int off = 32, n = D; off >= 1; off >>= 1, n >>= 1) {
+    const bool upper = (lane & off) != 0;
+    const int half = n >> 1;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float give = upper ? acc[i] : acc[half + i];
+      const float keep = upper ? acc[half + i] : acc[i];
+      acc[i] = keep + __shfl_xor(give, off, 64);
+    }
   }
 
   if (gridDim.y == 1) {

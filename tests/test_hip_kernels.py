@@ -326,7 +326,7 @@ def test_fp8_inference_linear_gpu(M):
     assert err < 0.06, err
 
 
-def _sdpa_ref(q, k, v, mask, causal, scale):
+def _decode_sdpa_ref(q, k, v, mask, causal, scale):
     qf, kf, vf = q.float(), k.float(), v.float()
     rep = q.shape[1] // k.shape[1]
     kf, vf = kf.repeat_interleave(rep, 1), vf.repeat_interleave(rep, 1)
@@ -363,7 +363,7 @@ def test_decode_attention(dtype, B, Hq, Hkv, T, S, D, mask_kind):
     elif mask_kind == "causal":
         causal = True
     out = decode_attn(q, k, v, mask, causal, scale)
-    ref = _sdpa_ref(q, k, v, mask, causal, scale)
+    ref = _decode_sdpa_ref(q, k, v, mask, causal, scale)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 

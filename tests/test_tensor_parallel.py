@@ -100,3 +100,62 @@ def test_megatron_mlp_has_single_allreduce_per_row_layer():
     # emb all-reduce, one identity sync for the shared fc input, proj all-reduce, head all-gather;
     # the fc_1/fc_2 all-gathers and the proj slice are removed through the silu(.)*(.) chain
     assert res["n_sync"] == 4, res
+
+
+def _litgpt_worker(rank, port, out_dir):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import column_parallel, row_parallel
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        class TrainStep(torch.nn.Module):  # the wrapper bench.py compiles
+            def __init__(self, m):
+                super().__init__()
+                self.m = m
+
+            def forward(self, x, y):
+                logits = self.m(x)
+                return torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
+
+        torch.manual_seed(0)
+        ref = GPT.from_name("llama3-like").double()
+        init_weights(ref)
+        ref.set_rope_cache(16)
+        m = GPT.from_name("llama3-like").double()
+        m.load_state_dict(ref.state_dict())
+        m.set_rope_cache(16)
+        n = m.config.n_layer
+        tm = thunder.jit(TrainStep(m))
+        tm = column_parallel(tm, [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.attn", "mlp.fc_1", "mlp.fc_2")])
+        tm = row_parallel(tm, [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.proj", "mlp.proj")])
+        x = torch.randint(0, 300, (2, 16))
+        y = torch.randint(0, 300, (2, 16))
+        loss = tm(x, y)
+        rl = TrainStep(ref)(x, y)
+        loss.backward()
+        rl.backward()
+        res = {"loss": abs(loss.item() - rl.item())}
+        gref = dict(ref.named_parameters())
+        gmax = 0.0
+        for name, p in m.named_parameters():
+            full = gref[name].grad
+            if p.shape != full.shape:
+                dim = 0 if p.shape[0] != full.shape[0] else 1
+                k = p.shape[dim]
+                full = full.narrow(dim, rank * k, k)
+            gmax = max(gmax, (p.grad - full).abs().max().item())
+        res["grad"] = gmax
+        torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_litgpt_tensor_parallel_train_step_like_bench():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_litgpt_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        for r in range(WORLD):
+            res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
+            assert res["loss"] < 1e-10 and res["grad"] < 1e-8, res
