@@ -452,6 +452,7 @@ def _nondeterministic_fns():
 
 
 _NONDET = None
+_FUNCTION_APPLY = torch.autograd.Function.apply.__func__
 
 
 def _library_lookasides() -> dict:
@@ -612,6 +613,12 @@ class Interpreter:
             self.maybe_guard(args[0], args[1], v, p)
             return v, p
         t = type(fn)
+        if t is types.MethodType and isinstance(fn.__self__, type) and issubclass(fn.__self__, torch.autograd.Function) \
+                and fn.__func__ is _FUNCTION_APPLY:
+            from ..torch import autograd_function
+
+            self.log("lookaside", f"{fn.__self__.__qualname__}.apply (autograd.Function)")
+            return autograd_function.apply(fn.__self__, *args, **kwargs), None
         if t is types.MethodType:
             self_prov = fn_prov.parent if (fn_prov is not None and fn_prov.kind == "attr") else None
             provs = [self_prov] + list(arg_provs or [None] * len(args))

@@ -458,3 +458,49 @@ def test_litgpt_through_interpreter_matches_eager():
     assert any("Block.forward" in line for line in log)
     pro = str(thunder.last_prologue_traces(jm)[0])
     assert "n_head" in pro  # config reads became guards
+
+
+class _ScaledExp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        y = torch.exp(x) * k
+        ctx.save_for_backward(y)
+        ctx.k = k
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        return g * y * 3.0, None  # deliberately not the true gradient: proves the user backward is used
+
+
+class _NewStyleSin(torch.autograd.Function):
+    @staticmethod
+    def forward(x):
+        return torch.sin(x)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        (x,) = inputs
+        ctx.save_for_backward(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * torch.cos(x)
+
+
+def test_autograd_function_uses_user_backward():
+    def f(x):
+        return _ScaledExp.apply(x, 2.0).sum() + _NewStyleSin.apply(x).sum()
+
+    x = torch.randn(5, requires_grad=True)
+    jf = thunder.jit(f)
+    out = jf(x)
+    torch.testing.assert_close(out, f(x))
+    out.backward()
+    g = x.grad.clone()
+    x.grad = None
+    f(x).backward()
+    torch.testing.assert_close(g, x.grad)
+    assert any("autograd_function__ScaledExp" in str(t) for t in thunder.last_traces(jf))
