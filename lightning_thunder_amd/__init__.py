@@ -488,7 +488,7 @@ def last_compile_options(fn) -> None:
 
 
 def get_auto_registered_torch_op_names(fn=None) -> set[str]:
-    from ._torch.default_torch_ops import get_auto_registered_torch_op_names as g
+    from .torch.default_torch_ops import get_auto_registered_torch_op_names as g
 
     return g()
 
@@ -536,6 +536,7 @@ def trace(fn, *args, interpretation: str = "python interpreter", **kwargs) -> Tr
 
 
 from . import distributed  # noqa: E402,F401
+from .torch import einops_backend as _einops_backend  # noqa: E402,F401  (einops on traced tensors)
 from .transforms import *  # noqa: E402,F401,F403
 
 __all__ = [

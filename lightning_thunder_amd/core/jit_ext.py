@@ -400,9 +400,11 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
 
         # snapshot of module attribute identity to detect writes made during tracing
         before = {}
+        before_buffers = {}
         if module is not None:
             for mpath, m in module.named_modules(remove_duplicate=True):
                 before[id(m)] = dict(vars(m))
+                before_buffers[id(m)] = dict(m._buffers)
 
         interp = None
         if interp_options is not None:
@@ -455,6 +457,10 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                     old = before.get(id(m), {})
                     for k, v in vars(m).items():
                         if isinstance(v, TensorProxy) and old.get(k) is not v:
+                            writes.append((m, k, v))
+                    old_b = before_buffers.get(id(m), {})
+                    for k, v in m._buffers.items():  # `self.buf = new` rebinds a registered buffer
+                        if isinstance(v, TensorProxy) and old_b.get(k) is not v:
                             writes.append((m, k, v))
             for d, k, v in swapped:
                 d[k] = v

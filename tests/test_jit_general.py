@@ -1,0 +1,195 @@
+"""General ``jit`` behaviour (reference: ``thunder/tests/test_jit_general.py``, ``test_einops.py``,
+``test_autocast.py``, ``test_randomness.py``, ``test_extend.py``, ``test_auto_register_torchops.py``)."""
+import pytest
+import torch
+
+import lightning_thunder_amd as thunder
+
+
+def test_kwargs_nested_containers_and_python_values():
+    def f(x, *, scale=2.0, d=None, flag=True):
+        out = x * scale
+        if flag:
+            out = out + d["b"][1]
+        return {"out": out, "pair": (out.sum(), [x.shape[0], "tag"])}
+
+    x = torch.randn(3, 4)
+    d = {"a": 1, "b": [torch.zeros(4), torch.ones(4)]}
+    jf = thunder.jit(f)
+    r, e = jf(x, scale=3.0, d=d), f(x, scale=3.0, d=d)
+    torch.testing.assert_close(r["out"], e["out"])
+    assert r["pair"][1] == [3, "tag"]
+    jf(x, scale=3.0, d=d)
+    assert thunder.cache_hits(jf) == 1
+    jf(x, scale=4.0, d=d)  # a different Python number: a new specialization
+    assert thunder.cache_misses(jf) == 2
+
+
+def test_cache_options():
+    def f(x, k):
+        return x * k
+
+    x = torch.randn(4)
+    same = thunder.jit(f, cache="same input")
+    same(x, 2)
+    torch.testing.assert_close(same(x, 2), x * 2)
+    assert thunder.cache_hits(same) == 1
+    none = thunder.jit(f, cache="no caching")
+    none(x, 2)
+    none(x, 2)
+    assert thunder.cache_misses(none) == 2 and thunder.cache_hits(none) == 0
+    assert thunder.cache_option(none) == thunder.CACHE_OPTIONS.NO_CACHING if hasattr(thunder, "CACHE_OPTIONS") else True
+
+
+def test_shape_change_recompiles():
+    jf = thunder.jit(lambda x: x.relu() + 1)
+    jf(torch.randn(2, 3))
+    jf(torch.randn(4, 3))
+    jf(torch.randn(2, 3))
+    assert thunder.cache_misses(jf) == 2 and thunder.cache_hits(jf) == 1
+
+
+class _Counter(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(4, 4)
+        self.register_buffer("running", torch.zeros(4))
+
+    def forward(self, x):
+        y = self.lin(x)
+        self.running = self.running * 0.9 + y.mean(0).detach() * 0.1  # attribute write -> epilogue
+        return y
+
+
+def test_module_buffer_rebinding_epilogue():
+    m = _Counter()
+    ref = _Counter()
+    ref.load_state_dict(m.state_dict())
+    jm = thunder.jit(m)
+    x = torch.randn(8, 4)
+    for _ in range(3):
+        torch.testing.assert_close(jm(x), ref(x))
+    torch.testing.assert_close(m.running, ref.running)
+
+
+def test_no_grad_and_grad_enabled_entries():
+    m = torch.nn.Linear(4, 2)
+    jm = thunder.jit(m)
+    x = torch.randn(3, 4)
+    with torch.no_grad():
+        y = jm(x)
+    assert not y.requires_grad
+    y2 = jm(x)
+    assert y2.requires_grad
+    assert thunder.cache_misses(jm) == 2
+
+
+def test_nested_modules_shared_weights_and_containers():
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.layers = torch.nn.ModuleList(torch.nn.Linear(4, 4) for _ in range(3))
+            self.heads = torch.nn.ModuleDict({"a": torch.nn.Linear(4, 2), "b": torch.nn.Linear(4, 2)})
+            self.heads["b"].weight = self.heads["a"].weight  # tied
+
+        def forward(self, x, which: str):
+            for i, l in enumerate(self.layers):
+                x = torch.tanh(l(x)) if i % 2 == 0 else l(x)
+            return self.heads[which](x)
+
+    m = M()
+    jm = thunder.jit(m)
+    x = torch.randn(5, 4)
+    for w in ("a", "b"):
+        torch.testing.assert_close(jm(x, w), m(x, w))
+    out = jm(x, "b").sum()
+    out.backward()
+    assert m.heads["a"].weight.grad is not None
+
+
+def test_einops_rearrange_reduce_repeat():
+    einops = pytest.importorskip("einops")
+
+    def f(x):
+        y = einops.rearrange(x, "b (h d) t -> b h t d", h=2)
+        z = einops.reduce(y, "b h t d -> b t", "mean")
+        return einops.repeat(z, "b t -> b t k", k=3)
+
+    x = torch.randn(2, 8, 5, requires_grad=True)
+    jf = thunder.jit(f)
+    out = jf(x)
+    torch.testing.assert_close(out, f(x))
+    out.sum().backward()
+    g = x.grad.clone()
+    x.grad = None
+    f(x).sum().backward()
+    torch.testing.assert_close(g, x.grad)
+
+
+def test_autocast_bf16_matmul():
+    def f(a, b):
+        return (a @ b).sum(-1)
+
+    a, b = torch.randn(8, 16), torch.randn(16, 4)
+    jf = thunder.jit(f)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        out = jf(a, b)
+        ref = f(a, b)
+    assert out.dtype == ref.dtype == torch.bfloat16
+    torch.testing.assert_close(out, ref, atol=1e-1, rtol=2e-2)
+    out2 = jf(a, b)  # outside autocast: another cache entry, fp32
+    assert out2.dtype == torch.float32
+
+
+def test_randomness_follows_torch_seed():
+    def f(x):
+        return torch.nn.functional.dropout(x, 0.5, training=True) + torch.rand_like(x)
+
+    jf = thunder.jit(f)
+    x = torch.ones(64, 64)
+    torch.manual_seed(7)
+    a = jf(x)
+    torch.manual_seed(7)
+    b = jf(x)
+    torch.testing.assert_close(a, b)
+    c = jf(x)
+    assert not torch.equal(a, c)
+    kept = (a >= 1.0).float().mean().item()
+    assert 0.35 < kept < 0.65  # dropout keeps ~half
+
+
+def test_custom_executor_register_operator_and_claim():
+    from lightning_thunder_amd.extend import OperatorExecutor, register_executor
+    from lightning_thunder_amd import torch as ltorch
+
+    ex = OperatorExecutor("test_relu_ex")
+    register_executor(ex)
+    calls = []
+
+    def relu_impl(a):
+        calls.append(1)
+        return torch.clamp_min(a, 0)
+
+    op = ex.register_operator("my_relu", like=ltorch.relu, fn=relu_impl)
+    ex.register_implementation(ltorch.relu, op, checker=lambda a, *r, **k: True)
+    jf = thunder.jit(lambda x: torch.relu(x) * 2, executors=[ex])
+    x = torch.randn(10)
+    torch.testing.assert_close(jf(x), torch.relu(x) * 2)
+    assert calls and "my_relu" in str(thunder.last_traces(jf)[-1])
+
+
+def test_auto_registered_torch_op_fwd_bwd():
+    def f(x):
+        return torch.special.i0(x).sum() + torch.cummax(x, 0).values.sum()
+
+    x = torch.randn(6, requires_grad=True)
+    jf = thunder.jit(f)
+    out = jf(x)
+    torch.testing.assert_close(out, f(x))
+    out.backward()
+    g = x.grad.clone()
+    x.grad = None
+    f(x).backward()
+    torch.testing.assert_close(g, x.grad)
+    names = thunder.get_auto_registered_torch_op_names()
+    assert any("i0" in n for n in names)
