@@ -455,7 +455,7 @@ _NONDET = None
 _FUNCTION_APPLY = torch.autograd.Function.apply.__func__
 
 
-def _library_lookasides() -> dict:
+def _library_lookasides(interp=None) -> dict:
     """Lookasides for third-party model libraries that are already imported.
 
     ``transformers``: ``is_tracing(t)`` is how HF code asks "is ``t`` symbolic?" before
@@ -476,7 +476,37 @@ def _library_lookasides() -> dict:
         w = getattr(pm, "warn_if_padding_and_no_attention_mask", None) if pm is not None else None
         if w is not None:
             out[w] = lambda *a, **k: None
+        # static KV caches allocate their storage lazily on the first ``update`` (inside the traced
+        # forward): allocate it eagerly as real tensors, so the cache object never holds proxies and
+        # later calls reach the storage as provenance-tracked inputs updated in place
+        cu = sys.modules.get("transformers.cache_utils")
+        for name in dir(cu) if cu is not None else ():
+            c = getattr(cu, name)
+            init = c.__dict__.get("lazy_initialization") if isinstance(c, type) and "Static" in name else None
+            if init is not None:
+                out[init] = _eager_cache_init(init, interp)
     return out
+
+
+def _eager_cache_init(orig, interp):
+    def lookaside(layer, *args, **kwargs):
+        from .jit_ext import _disabled_mode
+        from .proxies import TensorProxy
+
+        def real(t):
+            if isinstance(t, TensorProxy):
+                return torch.empty(tuple(t.shape), dtype=t.dtype, device=torch.device(str(t.device)))
+            return t
+
+        with _disabled_mode():
+            out = orig(layer, *[real(a) for a in args], **{k: real(v) for k, v in kwargs.items()})
+        if interp is not None:  # the guard read `not self.is_initialized` before this call: the
+            for (oid, key), (p, _) in list(interp.guards.items()):  # entry is valid for the new state
+                if oid == id(layer) and hasattr(layer, key):
+                    interp.guards[(oid, key)] = (p, getattr(layer, key))
+        return out
+
+    return lookaside
 
 
 # =========================================================================================
@@ -522,7 +552,7 @@ class Interpreter:
         if module is not None:
             for path, m in module.named_modules(remove_duplicate=True):
                 self.module_paths[id(m)] = path
-        for fn, repl in _library_lookasides().items():
+        for fn, repl in _library_lookasides(self).items():
             self.lookasides.setdefault(fn, repl)
 
     # ---------------------------------------------------------------------------------------
@@ -612,6 +642,14 @@ class Interpreter:
             p = self.mprov(v, p)
             self.maybe_guard(args[0], args[1], v, p)
             return v, p
+        if _hashable(fn) and (getattr(fn, "__module__", None) or "").startswith("torch.distributed"):
+            # c10d collectives have no __torch_function__ hook: route them to their ltorch symbols
+            from .. import torch as ltorch
+            from .jit_ext import dispatch_torch_function
+
+            if fn in ltorch._torch_to_thunder_function_map:
+                self.log("lookaside", _name(fn))
+                return dispatch_torch_function(fn, args, kwargs), None
         t = type(fn)
         if t is types.MethodType and isinstance(fn.__self__, type) and issubclass(fn.__self__, torch.autograd.Function) \
                 and fn.__func__ is _FUNCTION_APPLY:

@@ -554,6 +554,8 @@ def _emit_provenance_guards(prog: AcquiredProgram, roots_proxy, module_root, unp
     def key_of(p):
         if p.kind == "module":
             return ("module", p.key)
+        if p.kind == "input":
+            return ("input", p.key)
         if p.kind in ("global", "cell"):
             return (p.kind, id(p.parent), p.key)
         return (key_of(p.parent), p.kind, p.key)

@@ -97,3 +97,4 @@ def __getattr__(name):
 
 
 from . import prims  # noqa: E402,F401  (registers collectives with the torch executor)
+from . import torch_ops  # noqa: E402,F401  (user-visible collectives: ltorch.all_reduce, torch.distributed.*)

@@ -55,7 +55,11 @@ def _linear_checker(a, w, bias=None):
     for s in a.shape[:-1]:
         M *= s
     N, K = w.shape
-    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and a.shape[-1] == K
+    if a.shape[-1] != K:
+        return False
+    if M <= 8:  # decode: the weight-streaming GEMV (csrc/gemv.hip)
+        return K % 8 == 0
+    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0
 
 
 def _linear_exec(a, w, bias=None):

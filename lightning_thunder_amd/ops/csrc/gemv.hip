@@ -1,0 +1,155 @@
+// Skinny GEMM for decode (K2b): y[M, N] = act(x[M, K] @ w[N, K]^T + bias) + residual for M <= 8
+// activation rows (batch-1..8 incremental decoding, LM head on the last position).
+//
+// Why not the MFMA GEMM / hipBLASLt: at M = 1 the problem is a weight stream (Llama-3.2-1B:
+// 8-67 MB per projection) and a library tile of 16 x 16 leaves most of the chip idle or
+// serialises K.  Layout (cdna_hip_programming.md §5 "GEMV / M <= 16": straight to VGPRs, deep
+// unroll, late vmcnt):
+//   * a 256-thread block owns kRows = 8 consecutive output columns (rows of w); its 4 waves split
+//     K, lane l reading the 16-byte piece [k0 + 8 l, k0 + 8 l + 8) of all 8 weight rows at once
+//     (8 x 1 KiB fully coalesced row segments per wave step, two steps unrolled -> 16 loads in
+//     flight per lane);
+//   * x (<= 8 rows, L2-resident, shared by every block) is read with the same 16-byte pieces;
+//   * the M x 8 per-lane partial dots are combined by a recursive-halving reduce-scatter of
+//     shuffles (V/2 + V/4 + ... shuffles for V values instead of 6 V for V butterflies), then
+//     across the 4 waves through 1 KiB of LDS; bias / activation / residual are applied by the
+//     V threads that write the outputs.
+// Grid = ceil(N / 8) blocks: >= 256 for every projection of a 1B+ model (N >= 2048).
+#include "common.h"
+
+namespace lta {
+namespace {
+
+constexpr int kRows = 8;
+constexpr int kWaves = 4;
+constexpr int kStep = 64 * 8;  // K elements per wave step (8 x 16-bit per lane)
+
+__device__ __forceinline__ float gemv_act(float v, int act) {
+  switch (act) {
+    case 1: {  // gelu (tanh approximation)
+      const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
+      return 0.5f * v * (1.f + tanhf(u));
+    }
+    case 2:
+      return 0.5f * v * (1.f + erff(v * 0.7071067811865476f));
+    case 3:
+      return v / (1.f + __expf(-v));
+    case 4:
+      return fmaxf(v, 0.f);
+    default:
+      return v;
+  }
+}
+
+template <int V>
+struct Log2 {
+  static constexpr int value = 1 + Log2<V / 2>::value;
+};
+template <>
+struct Log2<1> {
+  static constexpr int value = 0;
+};
+
+template <typename T, int MM>
+__global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                   const T* __restrict__ bias, const T* __restrict__ res,
+                                                   T* __restrict__ y, int M, int N, int K, int64_t ldx, int64_t ldw,
+                                                   int64_t ldy, int64_t ldr, int act) {
+  constexpr int V = MM * kRows;  // partial sums per lane (power of two, <= 64)
+  constexpr int LOGV = Log2<V>::value;
+  constexpr int NV = Vec16<T>::N;
+  static_assert(V <= 64 && (V & (V - 1)) == 0, "V must be a power of two <= 64");
+  __shared__ float part[kWaves][V];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * kRows;
+
+  const T* wrow[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) wrow[r] = w + (int64_t)min(n0 + r, N - 1) * ldw;  // clamp: read valid, never write
+
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+
+#pragma unroll 2
+  for (int k = wv * kStep + lane * NV; k < K; k += kWaves * kStep) {
+    Vec16<T> wr[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) wr[r] = load16(wrow[r] + k);
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      if (m < M) {
+        const Vec16<T> xv = load16(x + (int64_t)m * ldx + k);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          const float xf = to_f32(xv.v[e]);
+#pragma unroll
+          for (int r = 0; r < kRows; ++r) acc[m * kRows + r] = fmaf(xf, to_f32(wr[r].v[e]), acc[m * kRows + r]);
+        }
+      }
+    }
+  }
+
+  // reduce-scatter: after LOGV halvings the lane holds element (lane >> (6 - LOGV)) summed over the
+  // lanes that share those top bits; a butterfly over the remaining low bits completes the sum.
+#pragma unroll
+  for (int step = 0; step < LOGV; ++step) {
+    const int off = 32 >> step;
+    const int half = V >> (step + 1);  // compile-time after unrolling: acc stays in VGPRs
+    const bool upper = (lane & off) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float give = upper ? acc[i] : acc[half + i];
+      const float keep = upper ? acc[half + i] : acc[i];
+      acc[i] = keep + __shfl_xor(give, off, 64);
+    }
+  }
+  float s = acc[0];
+#pragma unroll
+  for (int off = 32 >> LOGV; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((lane & ((64 >> LOGV) - 1)) == 0) part[wv][lane >> (6 - LOGV)] = s;
+  __syncthreads();
+
+  if (threadIdx.x < V) {
+    const int e = threadIdx.x;
+    const int m = e / kRows, r = e % kRows, nn = n0 + r;
+    if (m < M && nn < N) {
+      float v = part[0][e] + part[1][e] + part[2][e] + part[3][e];
+      if (bias) v += to_f32(bias[nn]);
+      v = gemv_act(v, act);
+      if (res) v += to_f32(res[(int64_t)m * ldr + nn]);
+      y[(int64_t)m * ldy + nn] = from_f32<T>(v);
+    }
+  }
+}
+
+template <typename T>
+int launch(const void* x, const void* w, const void* bias, const void* res, void* y, int M, int N, int K, int64_t ldx,
+           int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
+  dim3 grid((N + kRows - 1) / kRows), block(256);
+  const T *xp = (const T*)x, *wp = (const T*)w, *bp = (const T*)bias, *rp = (const T*)res;
+  T* yp = (T*)y;
+  if (M == 1)
+    hipLaunchKernelGGL((gemv_kernel<T, 1>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+  else if (M == 2)
+    hipLaunchKernelGGL((gemv_kernel<T, 2>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+  else if (M <= 4)
+    hipLaunchKernelGGL((gemv_kernel<T, 4>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+  else
+    hipLaunchKernelGGL((gemv_kernel<T, 8>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+}  // namespace lta
+
+// x [M, K] (row stride ldx), w [N, K] (row stride ldw), y [M, N]; K % 8 == 0, 16-byte aligned rows.
+LTA_EXPORT int lta_gemv_nt(int dtype, const void* x, const void* w, const void* bias, const void* res, void* y, int M,
+                           int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, void* stream) {
+  using namespace lta;
+  if (M < 1 || M > 8 || N < 1 || K < 8 || K % 8 || ldx % 8 || ldw % 8) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == kBF16) return launch<__hip_bfloat16>(x, w, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  if (dtype == kF16) return launch<__half>(x, w, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  return (int)hipErrorInvalidValue;
+}

@@ -3,7 +3,9 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import require, stream_ptr, check, register_signature, c_int, c_void_p, c_float
+import ctypes
+
+from ._lib import require, stream_ptr, check, register_signature, dcode, c_int, c_void_p, c_float
 
 ACT = {None: 0, "none": 0, "gelu_tanh": 1, "gelu": 2, "gelu_erf": 2, "silu": 3, "relu": 4}
 TILE_M, TILE_N, TILE_K = 256, 256, 64
@@ -87,15 +89,55 @@ def _torch_linear(x2, w, bias, residual, act):
     return y
 
 
+register_signature("lta_gemv_nt", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                    ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_int, c_void_p])
+GEMV_MAX_M = 8
+
+
+def gemv_supported(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None) -> bool:
+    """Decode-shaped linear: x [M <= 8, K] and w [N, K] (bf16/fp16, K % 8 == 0, 16-byte aligned rows)."""
+    if x.dtype not in (torch.bfloat16, torch.float16) or w.dtype != x.dtype or not x.is_cuda:
+        return False
+    if x.dim() != 2 or w.dim() != 2 or not 1 <= x.shape[0] <= GEMV_MAX_M or w.shape[1] != x.shape[1]:
+        return False
+    if x.shape[1] % 8 or x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or w.stride(0) % 8:
+        return False
+    if x.data_ptr() % 16 or w.data_ptr() % 16:
+        return False
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != w.shape[0] or not bias.is_contiguous()):
+        return False
+    if residual is not None and (residual.dtype != x.dtype or tuple(residual.shape) != (x.shape[0], w.shape[0])
+                                 or residual.stride(1) != 1):
+        return False
+    return True
+
+
+def gemv_nt(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, act=None) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual`` for M <= 8 rows with the weight-streaming kernel (``csrc/gemv.hip``)."""
+    lib = require()
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    rc = lib.lta_gemv_nt(dcode(x), x.data_ptr(), w.data_ptr(), None if bias is None else bias.data_ptr(),
+                         None if residual is None else residual.data_ptr(), out.data_ptr(), M, N, K, x.stride(0),
+                         w.stride(0), out.stride(0), 0 if residual is None else residual.stride(0), ACT[act],
+                         stream_ptr(x.device))
+    check(rc, "lta_gemv_nt")
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` choosing, once per shape, the faster of the hand-written
-    MFMA kernel (epilogue fused) and hipBLASLt + separate epilogue (``LTA_GEMM=hip|torch|auto``)."""
+    kernel (MFMA GEMM, or the weight-streaming GEMV for M <= 8; epilogue fused) and hipBLASLt +
+    separate epilogue (``LTA_GEMM=hip|torch|auto``)."""
     K = x.shape[-1]
     N = w.shape[0]
     x2 = x.reshape(-1, K)
     r2 = None if residual is None else residual.reshape(-1, N)
-    ok = gemm_nt_supported(x2, w, bias, r2)
     mode = _os.environ.get("LTA_GEMM", "auto")
+    if mode != "torch" and gemv_supported(x2, w, bias, r2):
+        return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
+    ok = gemm_nt_supported(x2, w, bias, r2)
     if not ok or mode == "torch":
         return _torch_linear(x2, w, bias, r2, act).reshape(*x.shape[:-1], N)
     key = (x2.shape[0], N, K, bias is not None, residual is not None, act)

@@ -7,6 +7,7 @@ functional form, and (3) when the model's mask is a plain causal mask, lets SDPA
 """
 from __future__ import annotations
 
+import types
 import warnings
 
 import torch
@@ -39,6 +40,35 @@ class HFTransformers(BaseRecipe):
 
     def setup_transforms(self):
         return super().setup_transforms() + [InplaceIndexCopyTransform()]
+
+    def apply(self, model):
+        """Compiles ``model`` and makes HF generation run on the compiled forward.
+
+        ``GenerationMixin.generate`` looks decoding methods up on ``type(self)`` and calls
+        ``self(**model_inputs)``; the returned module is an instance of a per-model subclass of
+        :class:`ThunderModule` carrying the model class's generation methods, so ``generate``
+        (greedy/sampling, static or dynamic caches) drives the compiled program while every other
+        attribute resolves on the wrapped model."""
+        tm = super().apply(model)
+        from ..core.module import ThunderModule
+
+        cls = type(model)
+        skip = set(dir(ThunderModule))
+        members = {}
+        for name in dir(cls):
+            if name in skip or name.startswith("__"):
+                continue
+            owner = next((k for k in cls.__mro__ if name in k.__dict__), None)
+            if owner is None or owner is object:
+                continue
+            raw = owner.__dict__[name]
+            # methods and class-level data (``_auto_class``, ``_supports_*``); properties keep
+            # resolving on the wrapped model through ThunderModule.__getattr__
+            if not isinstance(raw, property):
+                members[name] = raw
+        sub = type(f"Thunder{cls.__name__}", (type(tm),), members)
+        tm.__class__ = sub
+        return tm
 
 
 BaseRecipe.register("transformers")(HFTransformers)

@@ -379,3 +379,41 @@ def test_decode_attention_claimed_in_generate():
     jm = thunder.jit(m)
     generate(m, torch.randint(0, 300, (1, 8), device="cuda"), 4, forward=jm)
     assert "hip_decode_attn" in str(thunder.last_traces(jm)[-1])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 2048), (1, 3072, 2048), (2, 2050, 8192), (3, 1000, 520), (8, 512, 4096),
+                                   (5, 128256 // 16, 2048)])
+@pytest.mark.parametrize("epi", ["plain", "bias_silu_residual"])
+def test_gemv_decode_linear(dtype, M, N, K, epi):
+    from lightning_thunder_amd.ops.gemm import gemv_nt, gemv_supported
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=dtype) if "bias" in epi else None
+    res = torch.randn(M, N, device="cuda", dtype=dtype) if "residual" in epi else None
+    act = "silu" if "silu" in epi else None
+    assert gemv_supported(x, w, bias, res)
+    out = gemv_nt(x, w, bias=bias, residual=res, act=act)
+    ref = x.float() @ w.float().t()
+    if bias is not None:
+        ref = ref + bias.float()
+    if act == "silu":
+        ref = torch.nn.functional.silu(ref)
+    if res is not None:
+        ref = ref + res.float()
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_gemv_claimed_for_decode_linear():
+    import lightning_thunder_amd as thunder
+
+    lin = torch.nn.Linear(256, 512, device="cuda", dtype=torch.bfloat16)
+    jl = thunder.jit(lin)
+    x = torch.randn(1, 1, 256, device="cuda", dtype=torch.bfloat16)
+    with torch.no_grad():
+        out = jl(x)
+        ref = lin(x)
+    torch.testing.assert_close(out, ref, atol=2e-2, rtol=2e-2)
+    assert "hip_linear" in str(thunder.last_traces(jl)[-1])

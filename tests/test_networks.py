@@ -138,3 +138,18 @@ def test_nanogpt_dropout_trains():
     _, loss = jm(x, x)
     loss.backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+def test_hf_generate_static_cache_through_recipe():
+    cfg = tf.LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
+    torch.manual_seed(0)
+    m = tf.LlamaForCausalLM(cfg).eval()
+    m.requires_grad_(False)
+    x = torch.randint(1, 128, (1, 8))
+    kw = dict(do_sample=False, max_new_tokens=10, cache_implementation="static", pad_token_id=0)
+    ref = m.generate(x, **kw)
+    tm = thunder.compile(m, recipe="hf-transformers")
+    out = tm.generate(x, **kw)
+    assert torch.equal(out, ref), (out, ref)
+    assert thunder.cache_hits(tm) >= 5
