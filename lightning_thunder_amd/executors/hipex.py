@@ -12,6 +12,7 @@ import math
 import torch
 
 from ..core.proxies import TensorProxy
+from ..core.pytree import tree_flatten
 from ..extend import OperatorExecutor, register_executor, add_default_executor
 
 ex = OperatorExecutor("hipex", version="0.1")
@@ -194,7 +195,160 @@ def _fuse_linear_epilogues(trace):
     return new
 
 
-ex.post_claim_pass = _fuse_linear_epilogues
+# =========================================================================================
+# K2b decode GEMV with fused prologues (rmsnorm) / gated epilogues (SwiGLU up-projection pair)
+# =========================================================================================
+def _decode_linear_meta(x, w, bias=None, residual=None, act=None, gate_weight=None, norm=False, norm_weight=None,
+                        eps=1e-5):
+    return TensorProxy(like=x, shape=tuple(x.shape[:-1]) + (w.shape[0],))
+
+
+def _decode_linear_impl(x, w, bias=None, residual=None, act=None, gate_weight=None, norm=False, norm_weight=None,
+                        eps=1e-5):
+    from ..ops.gemm import gemv_nt, gemv_supported, _torch_linear
+
+    K, N = x.shape[-1], w.shape[0]
+    x2 = x.reshape(-1, K)
+    r2 = None if residual is None else residual.reshape(-1, N)
+    ok = gemv_supported(x2, w, bias, r2) and (gate_weight is None or gate_weight.stride() == w.stride())
+    if ok and norm_weight is not None:
+        ok = norm_weight.is_contiguous() and norm_weight.dtype == x.dtype
+    if ok:
+        y = gemv_nt(x2, w, bias=bias, residual=r2, act=act, gate_weight=gate_weight, norm=norm,
+                    norm_weight=norm_weight, eps=eps)
+        return y.reshape(*x.shape[:-1], N)
+    if norm:  # unaligned operands: the same math on the library path
+        from ..ops.rmsnorm import rms_norm_fwd
+
+        x2, _ = rms_norm_fwd(x2, norm_weight, eps)
+    if gate_weight is not None:
+        y = _torch_linear(x2, w, None, None, act) * torch.nn.functional.linear(x2, gate_weight)
+    else:
+        y = _torch_linear(x2, w, bias, r2, act)
+    return y.reshape(*x.shape[:-1], N)
+
+
+hip_decode_linear = ex.register_operator("hip_decode_linear", meta=_decode_linear_meta, fn=_decode_linear_impl)
+_GEMV_MAX_ROWS = 8
+
+
+def _rows(t) -> int:
+    r = 1
+    for d in t.shape[:-1]:
+        r *= d
+    return r
+
+
+def _linear_parts(b):
+    names = ("x", "w", "bias", "residual", "act")
+    d = dict(zip(names, b.args))
+    d.update({k: v for k, v in b.kwargs.items() if k in names})
+    return d
+
+
+def _fuse_decode_gemv(trace):
+    """Decode-shaped (<= 8 rows) chains around the weight-streaming GEMV, one launch each:
+
+    * ``a = hip_linear(x, w1); b = hip_linear(x, w2); y = hip_swiglu(a, b)`` ->
+      ``y = hip_decode_linear(x, w1, act="silu", gate_weight=w2)`` (LLaMA MLP up-projections + gate);
+    * ``y, rstd = hip_rms_norm_fwd(x, g, eps)`` whose ``y`` only feeds decode linears (and ``rstd``
+      nothing) -> the norm runs in those GEMVs' prologue (``norm=True``).
+    Every launch removed is ~5 us of a ~1 ms decode step on MI355X (kernel floor + boundary)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+
+    def count_uses(skip):
+        u: dict[str, int] = {}
+        for k, b in enumerate(bsyms):
+            if k not in skip:
+                for a in b.flat_proxy_args:
+                    u[a.name] = u.get(a.name, 0) + 1
+        for o in tree_flatten(trace.output)[0] if trace.output is not None else ():
+            if isinstance(o, TensorProxy):
+                u[o.name] = u.get(o.name, 0) + 1
+        return u
+
+    uses = count_uses(())
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    n_gated = n_norm = 0
+
+    def bind(i, *args, output, **kwargs):
+        bsyms[i] = ex.bind_call_ctx(hip_decode_linear.bind(*args, output=output, **kwargs))
+
+    # SwiGLU up-projection pairs
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_swiglu or len(b.args) != 2:
+            continue
+        a, g = b.args
+        ja, jg = producer.get(a.name), producer.get(g.name)
+        if ja is None or jg is None or ja in drop or jg in drop or ja == jg:
+            continue
+        la, lg = bsyms[ja], bsyms[jg]
+        if la.sym is not hip_linear or lg.sym is not hip_linear or uses.get(a.name) != 1 or uses.get(g.name) != 1:
+            continue
+        pa, pg = _linear_parts(la), _linear_parts(lg)
+        if pa["x"].name != pg["x"].name or any(p.get(k) is not None for p in (pa, pg) for k in ("bias", "residual", "act")):
+            continue
+        if _rows(pa["x"]) > _GEMV_MAX_ROWS or tuple(pa["w"].shape) != tuple(pg["w"].shape):
+            continue
+        bind(i, pa["x"], pa["w"], None, None, "silu", pg["w"], False, None, 1e-5, output=b.output)
+        drop.update((ja, jg))
+        n_gated += 1
+
+    # RMSNorm prologues
+    uses = count_uses(drop)
+    for i, b in enumerate(bsyms):
+        if i in drop or b.sym is not hip_rms_norm_fwd:
+            continue
+        y, rstd = b.output
+        x, g, eps = b.args[0], b.args[1], b.args[2]
+        if uses.get(rstd.name, 0) or _rows(x) > _GEMV_MAX_ROWS or not isinstance(eps, (int, float)):
+            continue
+        consumers = [j for j, c in enumerate(bsyms) if j not in drop and any(a.name == y.name for a in c.flat_proxy_args)]
+        ok = bool(consumers)
+        for j in consumers:
+            c = bsyms[j]
+            if c.sym is hip_linear:
+                p = _linear_parts(c)
+                ok = ok and p["x"] is not None and p["x"].name == y.name and p["w"].name != y.name
+            elif c.sym is hip_decode_linear:
+                ok = ok and c.args[0].name == y.name and not c.args[6] and all(
+                    getattr(a, "name", None) != y.name for a in c.args[1:])
+            else:
+                ok = False
+        if not ok or sum(1 for j in consumers) != uses.get(y.name, 0):
+            continue
+        for j in consumers:
+            c = bsyms[j]
+            if c.sym is hip_linear:
+                p = _linear_parts(c)
+                bind(j, x, p["w"], p.get("bias"), p.get("residual"), p.get("act"), None, True, g, float(eps),
+                     output=c.output)
+            else:
+                a = list(c.args)
+                bind(j, x, a[1], a[2], a[3], a[4], a[5], True, g, float(eps), output=c.output)
+        drop.add(i)
+        n_norm += 1
+
+    if not drop:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [b for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: decode GEMV fusion ({n_gated} gated pair(s), {n_norm} norm prologue(s))"))
+    return new
+
+
+def _post_claim(trace):
+    return _fuse_decode_gemv(_fuse_linear_epilogues(trace))
+
+
+ex.post_claim_pass = _post_claim
 
 
 # =========================================================================================

@@ -7,14 +7,14 @@
 // unroll, late vmcnt):
 //   * a 256-thread block owns kRows = 8 consecutive output columns (rows of w); its 4 waves split
 //     K, lane l reading the 16-byte piece [k0 + 8 l, k0 + 8 l + 8) of all 8 weight rows at once
-//     (8 x 1 KiB fully coalesced row segments per wave step, two steps unrolled -> 16 loads in
-//     flight per lane);
+//     (8 x 1 KiB fully coalesced row segments per wave step; the next step's rows are requested
+//     before the current step's FMAs -> up to 16 loads in flight per lane);
 //   * x (<= 8 rows, L2-resident, shared by every block) is read with the same 16-byte pieces;
 //   * the M x 8 per-lane partial dots are combined by a recursive-halving reduce-scatter of
 //     shuffles (V/2 + V/4 + ... shuffles for V values instead of 6 V for V butterflies), then
 //     across the 4 waves through 1 KiB of LDS; bias / activation / residual are applied by the
 //     V threads that write the outputs.
-// Grid = ceil(N / 8) blocks: >= 256 for every projection of a 1B+ model (N >= 2048).
+// Grid = ceil(N / 8) blocks (N / 4 gated): >= 256 for every projection of a 1B+ model (N >= 2048).
 #include "common.h"
 
 namespace lta {
@@ -50,43 +50,97 @@ struct Log2<1> {
   static constexpr int value = 0;
 };
 
-template <typename T, int MM>
+// NORM: x is replaced by rmsnorm(x) * g (the row's rstd computed per wave from the L2-resident x
+//   rows, so no block barrier sits in front of the weight loads); normalized values are rounded to
+//   T exactly as the stand-alone rmsnorm kernel would store them.
+// GATED: the block streams 4 rows of w and the same 4 rows of w2 and writes act(x w^T) * (x w2^T)
+//   (SwiGLU / GeGLU: the two up-projections and the gate in one launch); both products are
+//   rounded to T first, as the unfused linear -> swiglu chain stores them.
+template <typename T, int MM, bool NORM, bool GATED>
 __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                   const T* __restrict__ w2, const T* __restrict__ g, float eps,
                                                    const T* __restrict__ bias, const T* __restrict__ res,
                                                    T* __restrict__ y, int M, int N, int K, int64_t ldx, int64_t ldw,
                                                    int64_t ldy, int64_t ldr, int act) {
   constexpr int V = MM * kRows;  // partial sums per lane (power of two, <= 64)
   constexpr int LOGV = Log2<V>::value;
   constexpr int NV = Vec16<T>::N;
+  constexpr int COLS = GATED ? kRows / 2 : kRows;  // output columns per block
   static_assert(V <= 64 && (V & (V - 1)) == 0, "V must be a power of two <= 64");
   __shared__ float part[kWaves][V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * kRows;
+  const int n0 = blockIdx.x * COLS;
 
   const T* wrow[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = w + (int64_t)min(n0 + r, N - 1) * ldw;  // clamp: read valid, never write
+  for (int r = 0; r < kRows; ++r) {
+    const int c = GATED ? (r % COLS) : r;
+    const T* base = (GATED && r >= COLS) ? w2 : w;
+    wrow[r] = base + (int64_t)min(n0 + c, N - 1) * ldw;  // clamp: read valid rows, never write them
+  }
+
+  // software pipeline: the first step's weight rows are requested before anything else (including
+  // the NORM prologue's row statistics), and every step requests the next step's rows before its FMAs
+  constexpr int kStride = kWaves * kStep;
+  int k = wv * kStep + lane * NV;
+  Vec16<T> wr[kRows];
+  if (k < K) {
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) wr[r] = load16(wrow[r] + k);
+  }
+
+  float rstd[MM];
+#pragma unroll
+  for (int m = 0; m < MM; ++m) rstd[m] = 1.f;
+  if constexpr (NORM) {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      float ss = 0.f;
+      if (m < M) {
+        for (int kk = lane * NV; kk < K; kk += 64 * NV) {
+          const Vec16<T> xv = load16(x + (int64_t)m * ldx + kk);
+#pragma unroll
+          for (int e = 0; e < NV; ++e) {
+            const float f = to_f32(xv.v[e]);
+            ss = fmaf(f, f, ss);
+          }
+        }
+      }
+      rstd[m] = rsqrtf(wave_sum(ss) / (float)K + eps);
+    }
+  }
 
   float acc[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.f;
 
-#pragma unroll 2
-  for (int k = wv * kStep + lane * NV; k < K; k += kWaves * kStep) {
-    Vec16<T> wr[kRows];
+  for (; k < K; k += kStride) {
+    Vec16<T> wn[kRows];
+    const bool more = k + kStride < K;
+    if (more) {
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) wr[r] = load16(wrow[r] + k);
+      for (int r = 0; r < kRows; ++r) wn[r] = load16(wrow[r] + k + kStride);
+    }
+    Vec16<T> gv;
+    if constexpr (NORM) {
+      if (g) gv = load16(g + k);
+    }
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
       if (m < M) {
         const Vec16<T> xv = load16(x + (int64_t)m * ldx + k);
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
-          const float xf = to_f32(xv.v[e]);
+          float xf = to_f32(xv.v[e]);
+          if constexpr (NORM) xf = to_f32(from_f32<T>(xf * rstd[m] * (g ? to_f32(gv.v[e]) : 1.f)));
 #pragma unroll
           for (int r = 0; r < kRows; ++r) acc[m * kRows + r] = fmaf(xf, to_f32(wr[r].v[e]), acc[m * kRows + r]);
         }
       }
+    }
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) wr[r] = wn[r];
     }
   }
 
@@ -112,44 +166,77 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
 
   if (threadIdx.x < V) {
     const int e = threadIdx.x;
-    const int m = e / kRows, r = e % kRows, nn = n0 + r;
-    if (m < M && nn < N) {
-      float v = part[0][e] + part[1][e] + part[2][e] + part[3][e];
-      if (bias) v += to_f32(bias[nn]);
-      v = gemv_act(v, act);
-      if (res) v += to_f32(res[(int64_t)m * ldr + nn]);
-      y[(int64_t)m * ldy + nn] = from_f32<T>(v);
+    const int m = e / kRows, r = e % kRows;
+    if (GATED) {
+      const int nn = n0 + r;
+      if (r < COLS && m < M && nn < N) {
+        const float a = to_f32(from_f32<T>(part[0][e] + part[1][e] + part[2][e] + part[3][e]));
+        const int e2 = e + COLS;
+        const float b = to_f32(from_f32<T>(part[0][e2] + part[1][e2] + part[2][e2] + part[3][e2]));
+        y[(int64_t)m * ldy + nn] = from_f32<T>(gemv_act(a, act) * b);
+      }
+    } else {
+      const int nn = n0 + r;
+      if (m < M && nn < N) {
+        float v = part[0][e] + part[1][e] + part[2][e] + part[3][e];
+        if (bias) v += to_f32(bias[nn]);
+        v = gemv_act(v, act);
+        if (res) v += to_f32(res[(int64_t)m * ldr + nn]);
+        y[(int64_t)m * ldy + nn] = from_f32<T>(v);
+      }
     }
   }
 }
 
-template <typename T>
-int launch(const void* x, const void* w, const void* bias, const void* res, void* y, int M, int N, int K, int64_t ldx,
-           int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
-  dim3 grid((N + kRows - 1) / kRows), block(256);
-  const T *xp = (const T*)x, *wp = (const T*)w, *bp = (const T*)bias, *rp = (const T*)res;
-  T* yp = (T*)y;
+template <typename T, int MM, bool NORM, bool GATED>
+void launch_mm(const T* x, const T* w, const T* w2, const T* g, float eps, const T* bias, const T* res, T* y, int M,
+               int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
+  constexpr int COLS = GATED ? kRows / 2 : kRows;
+  dim3 grid((N + COLS - 1) / COLS), block(256);
+  hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED>), grid, block, 0, s, x, w, w2, g, eps, bias, res, y, M, N, K,
+                     ldx, ldw, ldy, ldr, act);
+}
+
+template <typename T, bool NORM, bool GATED>
+void launch_m(const T* x, const T* w, const T* w2, const T* g, float eps, const T* bias, const T* res, T* y, int M,
+              int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
   if (M == 1)
-    hipLaunchKernelGGL((gemv_kernel<T, 1>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+    launch_mm<T, 1, NORM, GATED>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
   else if (M == 2)
-    hipLaunchKernelGGL((gemv_kernel<T, 2>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+    launch_mm<T, 2, NORM, GATED>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
   else if (M <= 4)
-    hipLaunchKernelGGL((gemv_kernel<T, 4>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+    launch_mm<T, 4, NORM, GATED>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
   else
-    hipLaunchKernelGGL((gemv_kernel<T, 8>), grid, block, 0, s, xp, wp, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act);
+    launch_mm<T, 8, NORM, GATED>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
+}
+
+template <typename T>
+int launch(const void* x, const void* w, const void* w2, const void* g, int norm, float eps, const void* bias,
+           const void* res, void* y, int M, int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act,
+           hipStream_t s) {
+  const T *xp = (const T*)x, *wp = (const T*)w, *w2p = (const T*)w2, *gp = (const T*)g, *bp = (const T*)bias,
+          *rp = (const T*)res;
+  T* yp = (T*)y;
+  if (norm && w2p) launch_m<T, true, true>(xp, wp, w2p, gp, eps, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  else if (norm) launch_m<T, true, false>(xp, wp, w2p, gp, eps, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  else if (w2p) launch_m<T, false, true>(xp, wp, w2p, gp, eps, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  else launch_m<T, false, false>(xp, wp, w2p, gp, eps, bp, rp, yp, M, N, K, ldx, ldw, ldy, ldr, act, s);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 }  // namespace lta
 
-// x [M, K] (row stride ldx), w [N, K] (row stride ldw), y [M, N]; K % 8 == 0, 16-byte aligned rows.
-LTA_EXPORT int lta_gemv_nt(int dtype, const void* x, const void* w, const void* bias, const void* res, void* y, int M,
-                           int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, void* stream) {
+// x [M, K] (row stride ldx), w (and w2) [N, K] (row stride ldw), y [M, N]; K % 8 == 0, 16-byte aligned
+// rows.  norm != 0: x -> rmsnorm(x, g, eps) first; w2 != null: y = act(x w^T) * (x w2^T) (no bias/residual).
+LTA_EXPORT int lta_gemv_nt(int dtype, const void* x, const void* w, const void* w2, const void* g, int norm, float eps,
+                           const void* bias, const void* res, void* y, int M, int N, int K, int64_t ldx, int64_t ldw,
+                           int64_t ldy, int64_t ldr, int act, void* stream) {
   using namespace lta;
   if (M < 1 || M > 8 || N < 1 || K < 8 || K % 8 || ldx % 8 || ldw % 8) return (int)hipErrorInvalidValue;
+  if (w2 && (bias || res)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == kBF16) return launch<__hip_bfloat16>(x, w, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
-  if (dtype == kF16) return launch<__half>(x, w, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  if (dtype == kBF16) return launch<__hip_bfloat16>(x, w, w2, g, norm, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
+  if (dtype == kF16) return launch<__half>(x, w, w2, g, norm, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
   return (int)hipErrorInvalidValue;
 }

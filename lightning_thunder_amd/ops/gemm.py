@@ -89,8 +89,9 @@ def _torch_linear(x2, w, bias, residual, act):
     return y
 
 
-register_signature("lta_gemv_nt", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                                    ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_int, c_void_p])
+register_signature("lta_gemv_nt", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64, c_int, c_void_p])
 GEMV_MAX_M = 8
 
 
@@ -112,16 +113,25 @@ def gemv_supported(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None) -
     return True
 
 
-def gemv_nt(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, act=None) -> torch.Tensor:
-    """``act(x @ w.T + bias) + residual`` for M <= 8 rows with the weight-streaming kernel (``csrc/gemv.hip``)."""
+def gemv_nt(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, act=None, gate_weight=None,
+            norm: bool = False, norm_weight=None, eps: float = 1e-5) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual`` for M <= 8 rows with the weight-streaming kernel (``csrc/gemv.hip``).
+
+    ``norm=True`` first replaces x by ``rmsnorm(x) * norm_weight``; ``gate_weight`` (same shape as w)
+    makes the result ``act(x @ w.T) * (x @ gate_weight.T)`` (SwiGLU/GeGLU up-projection pair)."""
     lib = require()
     M, K = x.shape
     N = w.shape[0]
+    if gate_weight is not None:
+        assert gate_weight.shape == w.shape and gate_weight.stride() == w.stride() and bias is None and residual is None
+    if norm_weight is not None:
+        assert norm_weight.numel() == K and norm_weight.is_contiguous() and norm_weight.dtype == x.dtype
     out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    rc = lib.lta_gemv_nt(dcode(x), x.data_ptr(), w.data_ptr(), None if bias is None else bias.data_ptr(),
-                         None if residual is None else residual.data_ptr(), out.data_ptr(), M, N, K, x.stride(0),
-                         w.stride(0), out.stride(0), 0 if residual is None else residual.stride(0), ACT[act],
-                         stream_ptr(x.device))
+    rc = lib.lta_gemv_nt(dcode(x), x.data_ptr(), w.data_ptr(), None if gate_weight is None else gate_weight.data_ptr(),
+                         None if norm_weight is None else norm_weight.data_ptr(), int(norm), float(eps),
+                         None if bias is None else bias.data_ptr(), None if residual is None else residual.data_ptr(),
+                         out.data_ptr(), M, N, K, x.stride(0), w.stride(0), out.stride(0),
+                         0 if residual is None else residual.stride(0), ACT[act], stream_ptr(x.device))
     check(rc, "lta_gemv_nt")
     return out
 

@@ -417,3 +417,51 @@ def test_gemv_claimed_for_decode_linear():
         ref = lin(x)
     torch.testing.assert_close(out, ref, atol=2e-2, rtol=2e-2)
     assert "hip_linear" in str(thunder.last_traces(jl)[-1])
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("mode", ["norm", "gated", "norm_gated"])
+def test_gemv_fused_norm_and_gate(M, mode):
+    from lightning_thunder_amd.ops.gemm import gemv_nt
+    from lightning_thunder_amd.ops.rmsnorm import rms_norm_fwd
+
+    torch.manual_seed(0)
+    N, K = 1536, 2048
+    dt = torch.bfloat16
+    x = torch.randn(M, K, device="cuda", dtype=dt) * 3
+    w = torch.randn(N, K, device="cuda", dtype=dt) / K ** 0.5
+    w2 = torch.randn(N, K, device="cuda", dtype=dt) / K ** 0.5
+    g = torch.rand(K, device="cuda", dtype=dt) + 0.5
+    norm = "norm" in mode
+    gate = w2 if "gated" in mode else None
+    out = gemv_nt(x, w, act="silu" if gate is not None else None, gate_weight=gate, norm=norm, norm_weight=g, eps=1e-5)
+    xn = rms_norm_fwd(x, g, 1e-5)[0] if norm else x
+    ref = xn.float() @ w.float().t()
+    if gate is not None:
+        ref = torch.nn.functional.silu(ref.bfloat16().float()) * (xn.float() @ w2.float().t()).bfloat16().float()
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_decode_gemv_fusion_in_litgpt_decode():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights
+
+    torch.manual_seed(0)
+    m = GPT.from_name("llama3-like", n_layer=2, n_embd=256, n_head=4, head_size=64, intermediate_size=512).to(
+        device="cuda", dtype=torch.bfloat16)
+    init_weights(m, std=0.05)
+    m.requires_grad_(False)
+    idx = torch.randint(0, 300, (1, 8), device="cuda")
+    pos = torch.arange(8, device="cuda")
+    tok = torch.randint(0, 300, (1, 1), device="cuda")
+    p1 = torch.tensor([8], device="cuda")
+    m.set_kv_cache(1, 64)
+    m(idx, pos)
+    ref = m(tok, p1)
+    m.set_kv_cache(1, 64)
+    jm = thunder.jit(m)
+    jm(idx, pos)
+    out = jm(tok, p1)
+    trace = str(thunder.last_traces(jm)[-1])
+    assert "hip_decode_linear" in trace and "hip_swiglu(" not in trace and "hip_rms_norm_fwd" not in trace, trace
+    torch.testing.assert_close(out.float(), ref.float(), atol=5e-2, rtol=5e-2)
