@@ -11,6 +11,7 @@ import math
 
 import torch
 
+from ..core.prims import OpTags
 from ..core.proxies import TensorProxy
 from ..core.pytree import tree_flatten
 from ..extend import OperatorExecutor, register_executor, add_default_executor
@@ -344,8 +345,68 @@ def _fuse_decode_gemv(trace):
     return new
 
 
+def _qkv_rope_cache_meta(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n, kc, vc, pos):
+    B, T, _ = qkv.shape
+    return TensorProxy(like=qkv, shape=(B, n_head, T, head_size)), TensorProxy(like=kc), TensorProxy(like=vc)
+
+
+def _qkv_rope_cache_impl(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n, kc, vc, pos):
+    from ..ops.fused import qkv_rope_cache_fwd, qkv_rope_cache_supported, qkv_rope_fwd
+
+    if qkv_rope_cache_supported(qkv, kc, vc, pos, n_query_groups, head_size):
+        return qkv_rope_cache_fwd(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n, kc, vc, pos)
+    q, k, v = qkv_rope_fwd(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n)
+    return q, kc.index_copy_(2, pos, k), vc.index_copy_(2, pos, v)
+
+
+hip_qkv_rope_cache = ex.register_operator("hip_qkv_rope_cache", meta=_qkv_rope_cache_meta, fn=_qkv_rope_cache_impl,
+                                          tags=(OpTags.DONT_DCE, OpTags.IN_PLACE))
+
+
+def _fuse_kv_cache_writes(trace):
+    """``q, k, v = hip_qkv_rope(...); kc = index_copy_inplace(cache_k, 2, pos, k);
+    vc = index_copy_inplace(cache_v, 2, pos, v)`` (k, v used nowhere else) ->
+    ``q, kc, vc = hip_qkv_rope_cache(..., cache_k, cache_v, pos)``: the rotated keys and the values
+    are stored straight into the static caches by the RoPE kernel (two launches fewer per layer)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+    uses: dict[str, list[int]] = {}
+    for i, b in enumerate(bsyms):
+        for a in b.flat_proxy_args:
+            uses.setdefault(a.name, []).append(i)
+    out_names = {o.name for o in tree_flatten(trace.output)[0] if isinstance(o, TensorProxy)} \
+        if trace.output is not None else set()
+    replace, drop = {}, set()
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_qkv_rope:
+            continue
+        q, k, v = b.output
+        uk, uv = uses.get(k.name, []), uses.get(v.name, [])
+        if len(uk) != 1 or len(uv) != 1 or k.name in out_names or v.name in out_names:
+            continue
+        ck, cv = bsyms[uk[0]], bsyms[uv[0]]
+        if ck.sym.name != "index_copy_inplace" or cv.sym.name != "index_copy_inplace":
+            continue
+        (bk, dk, pk, sk), (bv, dv, pv, sv) = ck.args[:4], cv.args[:4]
+        if dk != 2 or dv != 2 or sk is not k or sv is not v or getattr(pk, "name", None) != getattr(pv, "name", 1):
+            continue
+        if pk.dtype != torch.int64 or bk.dtype != k.dtype or bv.dtype != v.dtype:
+            continue
+        nb = hip_qkv_rope_cache.bind(*b.args, bk, bv, pk, output=(q, ck.output, cv.output))
+        replace[i] = ex.bind_call_ctx(nb)
+        drop.update((uk[0], uv[0]))
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} KV-cache write pair(s) fused into RoPE"))
+    return new
+
+
 def _post_claim(trace):
-    return _fuse_decode_gemv(_fuse_linear_epilogues(trace))
+    return _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_linear_epilogues(trace)))
 
 
 ex.post_claim_pass = _post_claim

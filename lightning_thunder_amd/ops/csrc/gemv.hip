@@ -7,8 +7,8 @@
 // unroll, late vmcnt):
 //   * a 256-thread block owns kRows = 8 consecutive output columns (rows of w); its 4 waves split
 //     K, lane l reading the 16-byte piece [k0 + 8 l, k0 + 8 l + 8) of all 8 weight rows at once
-//     (8 x 1 KiB fully coalesced row segments per wave step; the next step's rows are requested
-//     before the current step's FMAs -> up to 16 loads in flight per lane);
+//     (8 x 1 KiB fully coalesced row segments per wave step; up to 4 steps' rows requested before
+//     the first FMA -> up to 32 loads in flight per lane);
 //   * x (<= 8 rows, L2-resident, shared by every block) is read with the same 16-byte pieces;
 //   * the M x 8 per-lane partial dots are combined by a recursive-halving reduce-scatter of
 //     shuffles (V/2 + V/4 + ... shuffles for V values instead of 6 V for V butterflies), then
@@ -56,7 +56,7 @@ struct Log2<1> {
 // GATED: the block streams 4 rows of w and the same 4 rows of w2 and writes act(x w^T) * (x w2^T)
 //   (SwiGLU / GeGLU: the two up-projections and the gate in one launch); both products are
 //   rounded to T first, as the unfused linear -> swiglu chain stores them.
-template <typename T, int MM, bool NORM, bool GATED>
+template <typename T, int MM, bool NORM, bool GATED, int U>
 __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                    const T* __restrict__ w2, const T* __restrict__ g, float eps,
                                                    const T* __restrict__ bias, const T* __restrict__ res,
@@ -79,20 +79,20 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
     wrow[r] = base + (int64_t)min(n0 + c, N - 1) * ldw;  // clamp: read valid rows, never write them
   }
 
-  // software pipeline: the first step's weight rows are requested before anything else (including
-  // the NORM prologue's row statistics), and every step requests the next step's rows before its FMAs
+  // Loads are issued a group of U wave-steps at a time, x pieces first and then every weight row
+  // piece of the group (vmcnt retires in order: waiting for x never waits for the weights), so up
+  // to U * kRows 16-byte weight loads per lane are in flight before the first FMA.  U is chosen
+  // per launch from K (a group covers the whole row when it can) within the VGPR budget.
   constexpr int kStride = kWaves * kStep;
-  int k = wv * kStep + lane * NV;
-  Vec16<T> wr[kRows];
-  if (k < K) {
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) wr[r] = load16(wrow[r] + k);
-  }
+  const int kbase = wv * kStep + lane * NV;
+  const int steps = (K + kStride - 1) / kStride;
+  __shared__ float ss_part[kWaves][MM];
 
   float rstd[MM];
 #pragma unroll
   for (int m = 0; m < MM; ++m) rstd[m] = 1.f;
-  if constexpr (NORM) {
+  // NORM with more steps than one group holds: row statistics up front (K > U * 2048 only)
+  if (NORM && steps > U) {
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
       float ss = 0.f;
@@ -114,33 +114,72 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.f;
 
-  for (; k < K; k += kStride) {
-    Vec16<T> wn[kRows];
-    const bool more = k + kStride < K;
-    if (more) {
+  for (int s0 = 0; s0 < steps; s0 += U) {
+    Vec16<T> xv[U][MM];
+    Vec16<T> wr[U][kRows];
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) wn[r] = load16(wrow[r] + k + kStride);
-    }
-    Vec16<T> gv;
-    if constexpr (NORM) {
-      if (g) gv = load16(g + k);
-    }
+    for (int u = 0; u < U; ++u) {
+      const int k = kbase + (s0 + u) * kStride;
+      if (k < K) {
 #pragma unroll
-    for (int m = 0; m < MM; ++m) {
-      if (m < M) {
-        const Vec16<T> xv = load16(x + (int64_t)m * ldx + k);
-#pragma unroll
-        for (int e = 0; e < NV; ++e) {
-          float xf = to_f32(xv.v[e]);
-          if constexpr (NORM) xf = to_f32(from_f32<T>(xf * rstd[m] * (g ? to_f32(gv.v[e]) : 1.f)));
-#pragma unroll
-          for (int r = 0; r < kRows; ++r) acc[m * kRows + r] = fmaf(xf, to_f32(wr[r].v[e]), acc[m * kRows + r]);
-        }
+        for (int m = 0; m < MM; ++m)
+          if (m < M) xv[u][m] = load16(x + (int64_t)m * ldx + k);
       }
     }
-    if (more) {
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) wr[r] = wn[r];
+    for (int u = 0; u < U; ++u) {
+      const int k = kbase + (s0 + u) * kStride;
+      if (k < K) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) wr[u][r] = load16(wrow[r] + k);
+      }
+    }
+    if (NORM && steps <= U) {
+      // this wave's x pieces cover its share of every row: block-reduce the sums of squares
+      // (plain global loads stay in flight across the barrier)
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (m < M && kbase + (s0 + u) * kStride < K) {
+#pragma unroll
+            for (int e = 0; e < NV; ++e) {
+              const float f = to_f32(xv[u][m].v[e]);
+              ss = fmaf(f, f, ss);
+            }
+          }
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) ss_part[wv][m] = ss;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+        rstd[m] = rsqrtf((ss_part[0][m] + ss_part[1][m] + ss_part[2][m] + ss_part[3][m]) / (float)K + eps);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kbase + (s0 + u) * kStride;
+      if (k < K) {
+        Vec16<T> gv;
+        if constexpr (NORM) {
+          if (g) gv = load16(g + k);
+        }
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+          if (m < M) {
+#pragma unroll
+            for (int e = 0; e < NV; ++e) {
+              float xf = to_f32(xv[u][m].v[e]);
+              if constexpr (NORM) xf = to_f32(from_f32<T>(xf * rstd[m] * (g ? to_f32(gv.v[e]) : 1.f)));
+#pragma unroll
+              for (int r = 0; r < kRows; ++r)
+                acc[m * kRows + r] = fmaf(xf, to_f32(wr[u][r].v[e]), acc[m * kRows + r]);
+            }
+          }
+        }
+      }
     }
   }
 
@@ -193,8 +232,17 @@ void launch_mm(const T* x, const T* w, const T* w2, const T* g, float eps, const
                int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
   constexpr int COLS = GATED ? kRows / 2 : kRows;
   dim3 grid((N + COLS - 1) / COLS), block(256);
-  hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED>), grid, block, 0, s, x, w, w2, g, eps, bias, res, y, M, N, K,
-                     ldx, ldw, ldy, ldr, act);
+  const int steps = (K + kWaves * kStep - 1) / (kWaves * kStep);
+  // weight registers: U * kRows * 4 VGPRs; MM <= 2 affords U = 4, MM = 4 U = 2, MM = 8 U = 1
+  if (MM <= 2 && steps >= 3)
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 2 ? 4 : 1)>), grid, block, 0, s, x, w, w2, g, eps, bias,
+                       res, y, M, N, K, ldx, ldw, ldy, ldr, act);
+  else if (MM <= 4 && steps >= 2)
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 4 ? 2 : 1)>), grid, block, 0, s, x, w, w2, g, eps, bias,
+                       res, y, M, N, K, ldx, ldw, ldy, ldr, act);
+  else
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, 1>), grid, block, 0, s, x, w, w2, g, eps, bias, res, y, M, N,
+                       K, ldx, ldw, ldy, ldr, act);
 }
 
 template <typename T, bool NORM, bool GATED>

@@ -15,11 +15,18 @@ using namespace lta;
 
 namespace {
 
+// k / v rows go to k + b*ks[0] + g*ks[1] + s*ks[2] with s = pos ? pos[t] : t: with `pos` they are
+// written straight into a static KV cache at the decode positions (no separate index_copy launch).
+struct KVDst {
+  int64_t ksb, ksg, kss, vsb, vsg, vss;
+};
+
 template <typename T, typename C>
 __global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__ qkv, const C* __restrict__ cos_,
                                                            const C* __restrict__ sin_, T* __restrict__ q,
-                                                           T* __restrict__ k, T* __restrict__ v, int B, int Tn, int nh,
-                                                           int ng, int hs, int rope_n) {
+                                                           T* __restrict__ k, T* __restrict__ v,
+                                                           const int64_t* __restrict__ pos, KVDst st, int B, int Tn,
+                                                           int nh, int ng, int hs, int rope_n) {
   constexpr int VW = Vec16<T>::N;
   const int chunks = hs / VW;
   const int heads = nh + 2 * ng;
@@ -40,10 +47,12 @@ __global__ __launch_bounds__(256) void qkv_rope_fwd_kernel(const T* __restrict__
       dst = q + (((int64_t)b * nh + h) * Tn + t) * hs;
       rotate = true;
     } else if (h < nh + ng) {
-      dst = k + (((int64_t)b * ng + (h - nh)) * Tn + t) * hs;
+      const int64_t s = pos ? pos[t] : t;
+      dst = k + b * st.ksb + (h - nh) * st.ksg + s * st.kss;
       rotate = true;
     } else {
-      dst = v + (((int64_t)b * ng + (h - nh - ng)) * Tn + t) * hs;
+      const int64_t s = pos ? pos[t] : t;
+      dst = v + b * st.vsb + (h - nh - ng) * st.vsg + s * st.vss;
       rotate = false;
     }
     if (!rotate || d0 >= rope_n) {
@@ -149,16 +158,35 @@ int grid_for(int64_t total) {
     }                                                            \
   } while (0)
 
-LTA_EXPORT int lta_qkv_rope_fwd(int dtype, int cdtype, const void* qkv, const void* cos_, const void* sin_, void* q,
-                                void* k, void* v, int B, int Tn, int nh, int ng, int hs, int rope_n,
-                                hipStream_t stream) {
+static int qkv_rope_fwd_launch(int dtype, int cdtype, const void* qkv, const void* cos_, const void* sin_, void* q,
+                               void* k, void* v, const int64_t* pos, KVDst st, int B, int Tn, int nh, int ng, int hs,
+                               int rope_n, hipStream_t stream) {
   if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
   const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / (dtype == kF32 ? 4 : 8));
   LTA_DISPATCH_TC(dtype, cdtype,
                   hipLaunchKernelGGL((qkv_rope_fwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
-                                     (const T*)qkv, (const C*)cos_, (const C*)sin_, (T*)q, (T*)k, (T*)v, B, Tn, nh, ng,
-                                     hs, rope_n));
+                                     (const T*)qkv, (const C*)cos_, (const C*)sin_, (T*)q, (T*)k, (T*)v, pos, st, B, Tn,
+                                     nh, ng, hs, rope_n));
   return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_qkv_rope_fwd(int dtype, int cdtype, const void* qkv, const void* cos_, const void* sin_, void* q,
+                                void* k, void* v, int B, int Tn, int nh, int ng, int hs, int rope_n,
+                                hipStream_t stream) {
+  const int64_t sg = (int64_t)Tn * hs, sb = ng * sg;
+  return qkv_rope_fwd_launch(dtype, cdtype, qkv, cos_, sin_, q, k, v, nullptr, KVDst{sb, sg, hs, sb, sg, hs}, B, Tn,
+                             nh, ng, hs, rope_n, stream);
+}
+
+// k/v written in place into caches kc/vc [B, ng, S, hs] (strides in elements, head dim contiguous and
+// 16-byte aligned) at rows pos[0..Tn) (int64, one per query position).
+LTA_EXPORT int lta_qkv_rope_cache_fwd(int dtype, int cdtype, const void* qkv, const void* cos_, const void* sin_,
+                                      void* q, void* kc, void* vc, const void* pos, const int64_t* strides, int B,
+                                      int Tn, int nh, int ng, int hs, int rope_n, hipStream_t stream) {
+  if ((strides[0] | strides[1] | strides[2] | strides[3] | strides[4] | strides[5]) % 8) return -2;
+  const KVDst st{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5]};
+  return qkv_rope_fwd_launch(dtype, cdtype, qkv, cos_, sin_, q, kc, vc, (const int64_t*)pos, st, B, Tn, nh, ng, hs,
+                             rope_n, stream);
 }
 
 LTA_EXPORT int lta_qkv_rope_bwd(int dtype, int cdtype, const void* dq, const void* dk, const void* dv, const void* cos_,

@@ -1,12 +1,16 @@
 """Wrappers for K6 (qkv split + RoPE), SwiGLU and K7 (cross entropy) kernels."""
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from ._lib import require, dcode, ptr, stream_ptr, check, register_signature, c_int, c_int64, c_void_p, c_float
 
 register_signature("lta_qkv_rope_fwd", [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+register_signature("lta_qkv_rope_cache_fwd", [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
 register_signature("lta_qkv_rope_bwd", [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
 register_signature("lta_swiglu_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p])
@@ -38,6 +42,38 @@ def qkv_rope_fwd(qkv, cos, sin, n_head: int, n_query_groups: int, head_size: int
                               n_head, n_query_groups, head_size, rope_n, stream_ptr(qkv.device))
     check(rc, "lta_qkv_rope_fwd")
     return q, k, v
+
+
+def qkv_rope_cache_supported(qkv, kc, vc, pos, n_query_groups: int, head_size: int) -> bool:
+    """Static caches [B, ng, S, hs] (head dim contiguous, 16-byte aligned rows) and int64 positions."""
+    B, T, _ = qkv.shape
+    for c in (kc, vc):
+        if c.dtype != qkv.dtype or c.dim() != 4 or tuple(c.shape[:2]) != (B, n_query_groups) or c.shape[3] != head_size:
+            return False
+        if c.stride(3) != 1 or any(st % 8 for st in c.stride()[:3]) or c.data_ptr() % 16:
+            return False
+    return pos.dtype == torch.int64 and pos.dim() == 1 and pos.numel() == T and pos.is_contiguous()
+
+
+def qkv_rope_cache_fwd(qkv, cos, sin, n_head: int, n_query_groups: int, head_size: int, rope_n: int, kc, vc, pos):
+    """qkv split + RoPE with k / v written in place into the static caches ``kc`` / ``vc`` at rows
+    ``pos`` (the decode step's ``index_copy_`` fused into the same launch).  Returns (q, kc, vc)."""
+    lib = require()
+    qkv = _c(qkv)
+    B, T, _ = qkv.shape
+    cos = _c(cos[:T])
+    sin = _c(sin[:T])
+    if cos.dtype != sin.dtype:
+        sin = sin.to(cos.dtype)
+    if cos.dtype not in (torch.float32, qkv.dtype):
+        cos, sin = cos.float(), sin.float()
+    q = torch.empty((B, n_head, T, head_size), device=qkv.device, dtype=qkv.dtype)
+    st = (ctypes.c_int64 * 6)(*kc.stride()[:3], *vc.stride()[:3])
+    rc = lib.lta_qkv_rope_cache_fwd(dcode(qkv), dcode(cos), ptr(qkv), ptr(cos), ptr(sin), ptr(q), ptr(kc), ptr(vc),
+                                    ptr(pos), st, B, T, n_head, n_query_groups, head_size, rope_n,
+                                    stream_ptr(qkv.device))
+    check(rc, "lta_qkv_rope_cache_fwd")
+    return q, kc, vc
 
 
 def qkv_rope_bwd(dq, dk, dv, cos, sin, n_head: int, n_query_groups: int, head_size: int, rope_n: int):

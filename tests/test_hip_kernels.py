@@ -464,4 +464,9 @@ def test_decode_gemv_fusion_in_litgpt_decode():
     out = jm(tok, p1)
     trace = str(thunder.last_traces(jm)[-1])
     assert "hip_decode_linear" in trace and "hip_swiglu(" not in trace and "hip_rms_norm_fwd" not in trace, trace
+    assert "hip_qkv_rope_cache" in trace and "index_copy" not in trace, trace
     torch.testing.assert_close(out.float(), ref.float(), atol=5e-2, rtol=5e-2)
+    # the caches were updated in place at position 8 by the fused RoPE kernel
+    jm(tok, torch.tensor([9], device="cuda"))
+    k0 = m.transformer.h[0].attn.kv_cache.k
+    assert k0[:, :, 8].abs().sum() > 0 and k0[:, :, 9].abs().sum() > 0 and k0[:, :, 10:].abs().sum() == 0
