@@ -408,6 +408,8 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, *, forward=None, 
     addresses (hipGraph-replayable) and is a cache hit after the first token.
     Greedy when ``temperature == 0``.  Returns ``[B, T + max_new_tokens]`` token ids.
     """
+    from ..ops.sampling import argmax_last
+
     forward = forward or model
     B, T = prompt.shape
     if model.transformer.h[0].attn.kv_cache is None:
@@ -426,7 +428,7 @@ def generate(model, prompt: torch.Tensor, max_new_tokens: int, *, forward=None, 
                 last = torch.where(last < v[:, [-1]], torch.full_like(last, -float("inf")), last)
             nxt = torch.multinomial(torch.softmax(last.float(), -1), 1)
         else:
-            nxt = last.argmax(-1, keepdim=True)
+            nxt = argmax_last(last, keepdim=True)
         out.append(nxt)
         if eos_id is not None and bool((nxt == eos_id).all()):
             break

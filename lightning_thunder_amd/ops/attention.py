@@ -75,7 +75,7 @@ from ._lib import c_int64  # noqa: E402
 
 register_signature("lta_decode_attn", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float,
-                                       c_void_p])
+                                       c_int, c_void_p])
 
 DECODE_MAX_QUERIES = 16
 
@@ -99,7 +99,9 @@ def decode_attn(q, k, v, mask=None, causal: bool = False, scale: float | None = 
     else:
         ms = (0, 0, 0, 0)
     rows = B * Hq * T
-    blocks = (rows + 3) // 4
+    # few rows (batch-1 decode): one row per workgroup with its 4 waves splitting the keys
+    wsplit = rows < 256
+    blocks = rows if wsplit else (rows + 3) // 4
     # split the cache so that a decode step still launches >= ~256 workgroups (flash-decoding)
     nsplit = max(1, min((256 + blocks - 1) // blocks, S // 256))  # a split is worth a combine launch from ~256 keys
     chunk = ((S + nsplit - 1) // nsplit + 63) // 64 * 64
@@ -113,6 +115,7 @@ def decode_attn(q, k, v, mask=None, causal: bool = False, scale: float | None = 
                                v.stride(0), v.stride(1), v.stride(2), *ms)
     mptr = None if mask is None else mask.data_ptr()
     rc = lib.lta_decode_attn(dcode(q), ptr(q), ptr(k), ptr(v), mptr, ptr(o), ptr(ws_acc), ptr(ws_ml), B, Hq, Hkv, T, S, D,
-                             ctypes.cast(st, ctypes.c_void_p), chunk, nsplit, int(causal), float(sc), stream_ptr(q.device))
+                             ctypes.cast(st, ctypes.c_void_p), chunk, nsplit, int(causal), float(sc), int(wsplit),
+                             stream_ptr(q.device))
     check(rc, "lta_decode_attn")
     return o

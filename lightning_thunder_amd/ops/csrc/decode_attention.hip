@@ -23,7 +23,10 @@ namespace {
 
 constexpr int kRowsPerBlock = 4;
 
-template <typename T, int D>
+// WSPLIT (few rows, e.g. batch-1 decode: 32 rows would occupy 8 CUs): one row per block, the 4
+// waves take interleaved 64-key blocks of the row's range and merge their (m, l, acc) through LDS,
+// so a row's serial key loop is 4x shorter without a second launch.
+template <typename T, int D, bool WSPLIT>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint8_t* __restrict__ mask,
     T* __restrict__ o, float* __restrict__ ws_acc, float* __restrict__ ws_ml, int B, int Hq, int Hkv, int Tq, int S,
@@ -34,8 +37,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   __shared__ float q_lds[kRowsPerBlock][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rows = B * Tq * Hq;
-  const int row = blockIdx.x * kRowsPerBlock + w;
-  if (row >= rows) return;  // whole wave exits together (no block-level sync below)
+  const int row = WSPLIT ? blockIdx.x : blockIdx.x * kRowsPerBlock + w;
+  if (!WSPLIT && row >= rows) return;  // whole wave exits together (no block-level sync below)
   const int hq = row % Hq;
   const int t = (row / Hq) % Tq;
   const int b = row / (Hq * Tq);
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
   for (int i = 0; i < D; ++i) acc[i] = 0.f;
 
-  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
+  for (int j0 = j_begin + (WSPLIT ? w * 64 : 0); j0 < j_end; j0 += (WSPLIT ? kRowsPerBlock * 64 : 64)) {
     const int j = j0 + lane;
     bool valid = j < j_end;
     if (valid && mrow) valid = mrow[(int64_t)j * mss] != 0;
@@ -109,6 +112,34 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
   }
 
+  if constexpr (WSPLIT) {
+    __shared__ float c_acc[kRowsPerBlock][D];
+    __shared__ float c_ml[kRowsPerBlock][2];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) c_acc[w][lane * DPL + i] = acc[i];
+    if (lane == 0) {
+      c_ml[w][0] = m;
+      c_ml[w][1] = l;
+    }
+    __syncthreads();
+    if (w != 0) return;
+    float M = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < kRowsPerBlock; ++u) M = fmaxf(M, c_ml[u][0]);
+    float L = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kRowsPerBlock; ++u) {
+      const float c = c_ml[u][0] == -INFINITY ? 0.f : __expf(c_ml[u][0] - M);
+      L = fmaf(c, c_ml[u][1], L);
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) acc[i] = fmaf(c, c_acc[u][lane * DPL + i], acc[i]);
+    }
+    m = M;
+    l = L;
+  }
+
   if (gridDim.y == 1) {
     const float inv = 1.f / l;  // fully masked row -> 0 * inf = nan, like PyTorch SDPA
     T* orow = o + (((int64_t)b * Hq + hq) * Tq + t) * D + lane * DPL;  // o is [B, Hq, Tq, D]
@@ -155,13 +186,20 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
 template <typename T, int D>
 int launch(const void* q, const void* k, const void* v, const void* mask, void* o, void* ws_acc, void* ws_ml, int B,
            int Hq, int Hkv, int Tq, int S, const int64_t* st, int chunk, int nsplit, int causal, float scale,
-           hipStream_t stream) {
+           int wsplit, hipStream_t stream) {
   const int rows = B * Tq * Hq;
-  dim3 grid((rows + kRowsPerBlock - 1) / kRowsPerBlock, nsplit);
-  hipLaunchKernelGGL((decode_attn_kernel<T, D>), grid, dim3(256), 0, stream, (const T*)q, (const T*)k, (const T*)v,
-                     (const uint8_t*)mask, (T*)o, (float*)ws_acc, (float*)ws_ml, B, Hq, Hkv, Tq, S, st[0], st[1],
-                     st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], chunk, causal,
-                     scale);
+  if (wsplit) {
+    hipLaunchKernelGGL((decode_attn_kernel<T, D, true>), dim3(rows, nsplit), dim3(256), 0, stream, (const T*)q,
+                       (const T*)k, (const T*)v, (const uint8_t*)mask, (T*)o, (float*)ws_acc, (float*)ws_ml, B, Hq, Hkv,
+                       Tq, S, st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11],
+                       st[12], chunk, causal, scale);
+  } else {
+    dim3 grid((rows + kRowsPerBlock - 1) / kRowsPerBlock, nsplit);
+    hipLaunchKernelGGL((decode_attn_kernel<T, D, false>), grid, dim3(256), 0, stream, (const T*)q, (const T*)k,
+                       (const T*)v, (const uint8_t*)mask, (T*)o, (float*)ws_acc, (float*)ws_ml, B, Hq, Hkv, Tq, S,
+                       st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12],
+                       chunk, causal, scale);
+  }
   if (nsplit > 1)
     hipLaunchKernelGGL((decode_attn_combine_kernel<T, D>), dim3(rows), dim3(64), 0, stream, (const float*)ws_acc,
                        (const float*)ws_ml, (T*)o, rows, nsplit, Hq, Tq);
@@ -174,16 +212,17 @@ int launch(const void* q, const void* k, const void* v, const void* mask, void* 
 // strides (elements): q b,h,t | k b,h,s | v b,h,s | mask b,h,t,s (0 for broadcast dims); head dim contiguous.
 LTA_EXPORT int lta_decode_attn(int dtype, const void* q, const void* k, const void* v, const void* mask, void* o,
                                void* ws_acc, void* ws_ml, int B, int Hq, int Hkv, int Tq, int S, int D,
-                               const int64_t* strides, int chunk, int nsplit, int causal, float scale, void* stream) {
+                               const int64_t* strides, int chunk, int nsplit, int causal, float scale, int wsplit,
+                               void* stream) {
   using namespace lta;
   hipStream_t s = (hipStream_t)stream;
   if (Hkv <= 0 || Hq % Hkv != 0 || chunk <= 0 || nsplit <= 0) return (int)hipErrorInvalidValue;
   if (dtype == kBF16) {
-    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, s);
-    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, s);
+    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, wsplit, s);
+    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, wsplit, s);
   } else if (dtype == kF16) {
-    if (D == 64) return launch<__half, 64>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, s);
-    if (D == 128) return launch<__half, 128>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, s);
+    if (D == 64) return launch<__half, 64>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, wsplit, s);
+    if (D == 128) return launch<__half, 128>(q, k, v, mask, o, ws_acc, ws_ml, B, Hq, Hkv, Tq, S, strides, chunk, nsplit, causal, scale, wsplit, s);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -470,3 +470,17 @@ def test_decode_gemv_fusion_in_litgpt_decode():
     jm(tok, torch.tensor([9], device="cuda"))
     k0 = m.transformer.h[0].attn.kv_cache.k
     assert k0[:, :, 8].abs().sum() > 0 and k0[:, :, 9].abs().sum() > 0 and k0[:, :, 10:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("R,V", [(1, 128256), (3, 32003), (2, 7)])
+def test_argmax_rows_kernel(dtype, R, V):
+    from lightning_thunder_amd.ops.sampling import argmax_last
+
+    torch.manual_seed(0)
+    x = torch.randn(R, V, device="cuda", dtype=dtype)
+    x[0, V // 3] = 100.0
+    x[0, V // 2] = 100.0  # tie: the smaller index wins
+    assert torch.equal(argmax_last(x), x.argmax(-1))
+    logits = torch.randn(2, 5, V + 1, device="cuda", dtype=dtype)[..., :V]  # strided rows fall back or run aligned
+    assert torch.equal(argmax_last(logits[:, -1], keepdim=True), logits[:, -1].argmax(-1, keepdim=True))
