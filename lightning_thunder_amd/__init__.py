@@ -103,6 +103,7 @@ class CacheEntry:
         self.autocast_key = None
         self.guard_roots = []
         self.output_spec = None
+        self.output_arg_refs = []
         self.interpreter_log = None
         self.sharp_edges = []
 
@@ -206,6 +207,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         computation_traces.append(comp)
 
         entry.output_spec = prog.output_spec
+        entry.output_arg_refs = prog.output_arg_refs
         entry.guard_roots = prog.guard_roots
         entry.interpreter_log = prog.interpreter_log
         entry.sharp_edges = prog.sharp_edges
@@ -284,7 +286,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
     return entry
 
 
-def _run_entry(entry: CacheEntry, inps):
+def _run_entry(entry: CacheEntry, inps, flat_args=None):
     if entry.uses_autograd:
         from .executors.torch_autograd import connect_to_autograd
 
@@ -298,6 +300,11 @@ def _run_entry(entry: CacheEntry, inps):
                 m._buffers[k] = v
             else:
                 object.__setattr__(m, k, v)
+    if entry.output_arg_refs and flat_args is not None:  # input objects handed back: this call's
+        leaves, spec = tree_flatten(out)
+        for i, j in entry.output_arg_refs:
+            leaves[i] = flat_args[j]
+        out = tree_unflatten(leaves, spec)
     if entry.output_spec is not None:  # rebuild ModelOutput / dataclass / namedtuple results
         out = tree_unflatten(tree_flatten(out)[0], entry.output_spec)
     return out
@@ -392,7 +399,7 @@ def jit(
         cs.last_interpreter_log = entry.interpreter_log
         cs.last_executed = entry
         cs.last_trace_host_execution_start = time.perf_counter_ns()
-        out = _run_entry(entry, inps)
+        out = _run_entry(entry, inps, tree_flatten((args, kwargs))[0] if entry.output_arg_refs else None)
         cs.last_trace_host_execution_stop = time.perf_counter_ns()
         cs.last_trace_host_stop = cs.last_trace_host_execution_stop
         return out

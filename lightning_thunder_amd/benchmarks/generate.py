@@ -10,7 +10,11 @@ prompt; no checkpoints offline): greedy decoding of ``--new-tokens`` tokens afte
 * ``thunder``  — ``jit(model)``: prefill and decode are two cached programs (hipex/hipfuse kernels,
   in-place KV-cache updates);
 * ``hipgraph`` — ``jit(model, transforms=[HipGraphTransform()])``: the decode step replays as
-  hipGraphs (the "reduce-overhead" configuration).
+  hipGraphs (the "reduce-overhead" configuration);
+* ``hf_eager`` / ``hf_thunder`` / ``hf_hipgraph`` — the reference's exact setup: a
+  ``transformers.LlamaForCausalLM`` (Llama-3.2-1B architecture, random init) driven by HF
+  ``model.generate(cache_implementation="static")``, eager or through
+  ``compile(recipe="hf-transformers"[, plugins="reduce-overhead"])``.
 
 Prints one JSON line per mode: mean latency (ms) of ``--iters`` full generations after
 ``--warmup`` untimed ones.
@@ -41,24 +45,56 @@ def _build(model_name: str, max_seq: int, device, n_layer=None):
     return model, cfg
 
 
+def _build_hf(device, n_layer=None):
+    """Hugging Face ``LlamaForCausalLM`` with the Llama-3.2-1B architecture (random init)."""
+    import transformers as tf
+
+    cfg = tf.LlamaConfig(vocab_size=128256, hidden_size=2048, intermediate_size=8192,
+                         num_hidden_layers=n_layer or 16, num_attention_heads=32, num_key_value_heads=8,
+                         max_position_embeddings=131072, rope_theta=500000.0, rms_norm_eps=1e-5,
+                         tie_word_embeddings=True,
+                         rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                                       "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    with torch.device(device):
+        model = tf.LlamaForCausalLM(cfg).to(torch.bfloat16)
+    model.requires_grad_(False)
+    model.eval()
+    return model, cfg
+
+
 def run(mode: str, args) -> dict:
     import lightning_thunder_amd as thunder
     from ..models.litgpt import generate
 
     device = torch.device("cuda", 0)
-    model, cfg = _build(args.model, args.prompt_len + args.new_tokens + 8, device, args.n_layer)
-    prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), device=device)
-    if mode == "eager":
-        fwd = model
-    elif mode == "thunder":
-        fwd = thunder.jit(model)
+    if mode.startswith("hf_"):
+        # the reference's benchmark: HF transformers model.generate with a static cache
+        model, cfg = _build_hf(device, args.n_layer)
+        if mode == "hf_eager":
+            gm = model
+        else:
+            gm = thunder.compile(model, recipe="hf-transformers",
+                                 plugins="reduce-overhead" if mode == "hf_hipgraph" else None)
+        prompt = torch.randint(1, cfg.vocab_size, (1, args.prompt_len), device=device)
+        kw = dict(max_new_tokens=args.new_tokens, min_new_tokens=args.new_tokens, do_sample=False,
+                  cache_implementation="static", pad_token_id=0, disable_compile=True)
+
+        def once():
+            return gm.generate(prompt, **kw)
     else:
-        from ..transforms.hipgraph import HipGraphTransform
+        model, cfg = _build(args.model, args.prompt_len + args.new_tokens + 8, device, args.n_layer)
+        prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), device=device)
+        if mode == "eager":
+            fwd = model
+        elif mode == "thunder":
+            fwd = thunder.jit(model)
+        else:
+            from ..transforms.hipgraph import HipGraphTransform
 
-        fwd = thunder.jit(model, transforms=[HipGraphTransform()])
+            fwd = thunder.jit(model, transforms=[HipGraphTransform()])
 
-    def once():
-        return generate(model, prompt, args.new_tokens, forward=fwd)
+        def once():
+            return generate(model, prompt, args.new_tokens, forward=fwd)
 
     t0 = time.perf_counter()
     out = once()
@@ -77,6 +113,7 @@ def run(mode: str, args) -> dict:
     ms = 1000 * sum(times) / len(times)
     res = {
         "metric": f"{args.model} greedy generate latency ({args.new_tokens} new tokens, static KV cache)",
+        "model_impl": "transformers.LlamaForCausalLM" if mode.startswith("hf_") else "lightning_thunder_amd litgpt GPT",
         "mode": mode, "value": round(ms, 2), "unit": "ms", "higher_is_better": False,
         "ms_per_token": round(ms / args.new_tokens, 3), "first_call_s": round(first, 2),
         "prompt_len": args.prompt_len, "new_tokens": args.new_tokens, "dtype": "bf16",

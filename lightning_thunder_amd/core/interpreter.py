@@ -488,8 +488,15 @@ def _library_lookasides(interp=None) -> dict:
     return out
 
 
+# set by the HF recipe while a call runs on static-cache storage it allocated up front: the layers'
+# lazy initialisation is then a no-op inside the traced program (state stays as the guards saw it)
+STATIC_CACHE_PREALLOCATED = [False]
+
+
 def _eager_cache_init(orig, interp):
     def lookaside(layer, *args, **kwargs):
+        if STATIC_CACHE_PREALLOCATED[0] and getattr(layer, "keys", None) is not None:
+            return None
         from .jit_ext import _disabled_mode
         from .proxies import TensorProxy
 
@@ -532,6 +539,7 @@ class Interpreter:
                  opaque: Callable[[Any], bool] | None = None, tensor_hook: Callable | None = None):
         self.lookasides = dict(lookasides or {})
         self.tensor_hook = tensor_hook
+        self.obj_prov: dict[int, Prov] = {}
         self.history: list | None = [] if record_history else None
         self.record_instructions = record_history == "instructions"
         self.sharp_edges = sharp_edges
@@ -579,11 +587,23 @@ class Interpreter:
         return self.tensor_hook(t, p)
 
     def mprov(self, v, p):
-        """Provenance for ``v``: ``p`` or, for submodules of the compiled module, its path."""
+        """Provenance for ``v``: ``p`` or, for submodules of the compiled module, its path.
+
+        Plain objects remember the first provenance they were reached with, so a value that later
+        arrives through a path that drops it (``*args/**kwargs`` forwarding decorators, opaque
+        helpers) is still re-fetched, not captured: e.g. a KV-cache object handed through HF's
+        output-capturing wrappers, whose length tensor must stay a per-call input."""
         path = self.module_paths.get(id(v))
         if path is not None and isinstance(v, torch.nn.Module):
             return Prov("module", key=path)
-        return p
+        if v is None or isinstance(v, (bool, int, float, str, bytes, type, types.ModuleType, types.FunctionType)):
+            return p
+        if p is not None:
+            if id(v) not in self.obj_prov:
+                self.obj_prov[id(v)] = p
+                self._keepalive.append(v)
+            return p
+        return self.obj_prov.get(id(v))
 
     def maybe_guard(self, owner, key, v, p):
         """Record a guard when a guardable scalar was read through a provenance chain."""
@@ -1184,7 +1204,8 @@ def _load_fast(interp, f, arg, argval, target):
     v = f.fast[arg]
     if v is NULL:
         raise UnboundLocalError(f"local variable '{argval}' referenced before assignment")
-    f.push(v, f.fprov[arg])
+    p = f.fprov[arg]
+    f.push(v, interp.mprov(v, p) if (p is not None or interp.obj_prov) else p)
 
 
 @handler("STORE_FAST")

@@ -206,6 +206,7 @@ class AcquiredProgram:
         self.param_accessors: list[tuple[torch.nn.Module, str, str]] = []  # (module, name, kind)
         self.constants: list[torch.Tensor] = []
         self.output_spec = None
+        self.output_arg_refs: list[tuple[int, int]] = []
         self.epilogue_writes: list[tuple[torch.nn.Module, str]] = []
         self.alias_pattern = None
         self.guards: list = []  # (Prov, value) read by the program through module/global/closure state
@@ -484,7 +485,12 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             return x
 
         result = tree_map(fix_out, result)
-        out_spec = tree_flatten(result)[1]
+        out_leaves, out_spec = tree_flatten(result)
+        # non-tensor objects returned from the inputs (an HF cache passed in and handed back in the
+        # ModelOutput) must be the caller's objects of *this* call, not the ones seen while tracing
+        arg_ids = {id(a): j for j, a in enumerate(flat_args)
+                   if not isinstance(a, (torch.Tensor, Proxy, bool, int, float, str, type(None)))}
+        prog.output_arg_refs = [(i, arg_ids[id(v)]) for i, v in enumerate(out_leaves) if id(v) in arg_ids]
         epi_values = [tracker.refresh(v) or v for v in epi_values]
         result = tracker.finish(result)
         comp.alias_tracker = None
