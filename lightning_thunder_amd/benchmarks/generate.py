@@ -55,6 +55,7 @@ def _build_hf(device, n_layer=None):
                          tie_word_embeddings=True,
                          rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
                                        "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    torch.manual_seed(0)  # the same random weights in every mode: generated tokens are comparable
     with torch.device(device):
         model = tf.LlamaForCausalLM(cfg).to(torch.bfloat16)
     model.requires_grad_(False)
@@ -75,7 +76,8 @@ def run(mode: str, args) -> dict:
         else:
             gm = thunder.compile(model, recipe="hf-transformers",
                                  plugins="reduce-overhead" if mode == "hf_hipgraph" else None)
-        prompt = torch.randint(1, cfg.vocab_size, (1, args.prompt_len), device=device)
+        prompt = torch.randint(1, cfg.vocab_size, (1, args.prompt_len), device=device,
+                               generator=torch.Generator(device).manual_seed(1))
         kw = dict(max_new_tokens=args.new_tokens, min_new_tokens=args.new_tokens, do_sample=False,
                   cache_implementation="static", pad_token_id=0, disable_compile=True)
 
