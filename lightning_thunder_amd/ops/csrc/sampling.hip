@@ -1,7 +1,8 @@
 // Greedy sampling: row-wise argmax over the vocabulary (the decode loop's `logits[:, -1].argmax(-1)`).
 // PyTorch's generic reduction takes ~40 us for one 128k-wide bf16 row on MI355X; one 1024-thread
-// workgroup per row with 16-byte loads (8 x bf16 per lane, 8 independent loads in flight per lane) finishes in a few microseconds.  Ties resolve to the smallest index and NaN
-// wins, as torch.argmax does.
+// workgroup per row with 16-byte loads (8 x bf16 per lane, 8 independent loads in flight per
+// lane) needs a fraction of that.  Ties resolve to the smallest index and NaN wins, as
+// torch.argmax does.
 #include "common.h"
 
 namespace lta {
