@@ -56,24 +56,24 @@ struct Log2<1> {
 // GATED: the block streams 4 rows of w and the same 4 rows of w2 and writes act(x w^T) * (x w2^T)
 //   (SwiGLU / GeGLU: the two up-projections and the gate in one launch); both products are
 //   rounded to T first, as the unfused linear -> swiglu chain stores them.
-template <typename T, int MM, bool NORM, bool GATED, int U>
+template <typename T, int MM, bool NORM, bool GATED, int U, int KR>
 __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                    const T* __restrict__ w2, const T* __restrict__ g, float eps,
                                                    const T* __restrict__ bias, const T* __restrict__ res,
                                                    T* __restrict__ y, int M, int N, int K, int64_t ldx, int64_t ldw,
                                                    int64_t ldy, int64_t ldr, int act) {
-  constexpr int V = MM * kRows;  // partial sums per lane (power of two, <= 64)
+  constexpr int V = MM * KR;  // partial sums per lane (power of two, <= 64)
   constexpr int LOGV = Log2<V>::value;
   constexpr int NV = Vec16<T>::N;
-  constexpr int COLS = GATED ? kRows / 2 : kRows;  // output columns per block
+  constexpr int COLS = GATED ? KR / 2 : KR;  // output columns per block
   static_assert(V <= 64 && (V & (V - 1)) == 0, "V must be a power of two <= 64");
   __shared__ float part[kWaves][V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n0 = blockIdx.x * COLS;
 
-  const T* wrow[kRows];
+  const T* wrow[KR];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
+  for (int r = 0; r < KR; ++r) {
     const int c = GATED ? (r % COLS) : r;
     const T* base = (GATED && r >= COLS) ? w2 : w;
     wrow[r] = base + (int64_t)min(n0 + c, N - 1) * ldw;  // clamp: read valid rows, never write them
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
 
   // Loads are issued a group of U wave-steps at a time, x pieces first and then every weight row
   // piece of the group (vmcnt retires in order: waiting for x never waits for the weights), so up
-  // to U * kRows 16-byte weight loads per lane are in flight before the first FMA.  U is chosen
+  // to U * KR 16-byte weight loads per lane are in flight before the first FMA.  U is chosen
   // per launch from K (a group covers the whole row when it can) within the VGPR budget.
   constexpr int kStride = kWaves * kStep;
   const int kbase = wv * kStep + lane * NV;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
 
   for (int s0 = 0; s0 < steps; s0 += U) {
     Vec16<T> xv[U][MM];
-    Vec16<T> wr[U][kRows];
+    Vec16<T> wr[U][KR];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = kbase + (s0 + u) * kStride;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
       const int k = kbase + (s0 + u) * kStride;
       if (k < K) {
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) wr[u][r] = load16(wrow[r] + k);
+        for (int r = 0; r < KR; ++r) wr[u][r] = load16(wrow[r] + k);
       }
     }
     if (NORM && steps <= U) {
@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
               float xf = to_f32(xv[u][m].v[e]);
               if constexpr (NORM) xf = to_f32(from_f32<T>(xf * rstd[m] * (g ? to_f32(gv.v[e]) : 1.f)));
 #pragma unroll
-              for (int r = 0; r < kRows; ++r)
-                acc[m * kRows + r] = fmaf(xf, to_f32(wr[u][r].v[e]), acc[m * kRows + r]);
+              for (int r = 0; r < KR; ++r)
+                acc[m * KR + r] = fmaf(xf, to_f32(wr[u][r].v[e]), acc[m * KR + r]);
             }
           }
         }
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
 
   if (threadIdx.x < V) {
     const int e = threadIdx.x;
-    const int m = e / kRows, r = e % kRows;
+    const int m = e / KR, r = e % KR;
     if (GATED) {
       const int nn = n0 + r;
       if (r < COLS && m < M && nn < N) {
@@ -227,22 +227,33 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
   }
 }
 
+template <typename T, int MM, bool NORM, bool GATED, int KR>
+void launch_kr(const T* x, const T* w, const T* w2, const T* g, float eps, const T* bias, const T* res, T* y, int M,
+               int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
+  constexpr int COLS = GATED ? KR / 2 : KR;
+  dim3 grid((N + COLS - 1) / COLS), block(256);
+  const int steps = (K + kWaves * kStep - 1) / (kWaves * kStep);
+  // weight registers: U * KR * 4 VGPRs; MM <= 2 affords U = 4, MM = 4 U = 2, MM = 8 U = 1
+  if (MM <= 2 && steps >= 3)
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 2 ? 4 : 1), KR>), grid, block, 0, s, x, w, w2, g, eps,
+                       bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act);
+  else if (MM <= 4 && steps >= 2)
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 4 ? 2 : 1), KR>), grid, block, 0, s, x, w, w2, g, eps,
+                       bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act);
+  else
+    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, 1, KR>), grid, block, 0, s, x, w, w2, g, eps, bias, res, y, M,
+                       N, K, ldx, ldw, ldy, ldr, act);
+}
+
 template <typename T, int MM, bool NORM, bool GATED>
 void launch_mm(const T* x, const T* w, const T* w2, const T* g, float eps, const T* bias, const T* res, T* y, int M,
                int N, int K, int64_t ldx, int64_t ldw, int64_t ldy, int64_t ldr, int act, hipStream_t s) {
-  constexpr int COLS = GATED ? kRows / 2 : kRows;
-  dim3 grid((N + COLS - 1) / COLS), block(256);
-  const int steps = (K + kWaves * kStep - 1) / (kWaves * kStep);
-  // weight registers: U * kRows * 4 VGPRs; MM <= 2 affords U = 4, MM = 4 U = 2, MM = 8 U = 1
-  if (MM <= 2 && steps >= 3)
-    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 2 ? 4 : 1)>), grid, block, 0, s, x, w, w2, g, eps, bias,
-                       res, y, M, N, K, ldx, ldw, ldy, ldr, act);
-  else if (MM <= 4 && steps >= 2)
-    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, (MM <= 4 ? 2 : 1)>), grid, block, 0, s, x, w, w2, g, eps, bias,
-                       res, y, M, N, K, ldx, ldw, ldy, ldr, act);
+  // narrow outputs (N < 4096: the 2048-wide projections of a 1B model) would leave one workgroup
+  // per CU with 8-row tiles: 4-row tiles double the workgroups and the waves streaming per CU
+  if (!GATED && MM <= 2 && N < 4096)
+    launch_kr<T, MM, NORM, GATED, 4>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
   else
-    hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, GATED, 1>), grid, block, 0, s, x, w, w2, g, eps, bias, res, y, M, N,
-                       K, ldx, ldw, ldy, ldr, act);
+    launch_kr<T, MM, NORM, GATED, kRows>(x, w, w2, g, eps, bias, res, y, M, N, K, ldx, ldw, ldy, ldr, act, s);
 }
 
 template <typename T, bool NORM, bool GATED>
