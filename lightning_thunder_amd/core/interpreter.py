@@ -476,6 +476,15 @@ def _library_lookasides(interp=None) -> dict:
         w = getattr(pm, "warn_if_padding_and_no_attention_mask", None) if pm is not None else None
         if w is not None:
             out[w] = lambda *a, **k: None
+        # Llama-style RMSNorm modules (fp32 statistics, ``weight * x.to(dtype)``) become one
+        # ``rms_norm`` so the fused kernel (and the decode GEMV's norm prologue) claims them
+        for mname, mod in list(sys.modules.items()):
+            if not mname.startswith("transformers.models.") or ".modeling_" not in mname or mod is None:
+                continue
+            for cname, c in list(vars(mod).items()):
+                fwd = c.__dict__.get("forward") if isinstance(c, type) and cname.endswith("RMSNorm") else None
+                if fwd is not None and fwd not in out and _is_llama_rmsnorm(fwd):
+                    out[fwd] = _rmsnorm_lookaside(fwd)
         # static KV caches allocate their storage lazily on the first ``update`` (inside the traced
         # forward): allocate it eagerly as real tensors, so the cache object never holds proxies and
         # later calls reach the storage as provenance-tracked inputs updated in place
@@ -486,6 +495,28 @@ def _library_lookasides(interp=None) -> dict:
             if init is not None:
                 out[init] = _eager_cache_init(init, interp)
     return out
+
+
+def _is_llama_rmsnorm(fwd) -> bool:
+    import inspect
+
+    try:
+        src = inspect.getsource(fwd)
+    except (OSError, TypeError):
+        return False
+    return ("self.weight * hidden_states.to(input_dtype)" in src and "variance_epsilon" in src
+            and "pow(2).mean(-1, keepdim=True)" in src)
+
+
+def _rmsnorm_lookaside(orig):
+    def lookaside(module, hidden_states):
+        w = getattr(module, "weight", None)
+        eps = getattr(module, "variance_epsilon", None)
+        if w is None or eps is None or getattr(w, "dtype", None) != getattr(hidden_states, "dtype", None):
+            return orig(module, hidden_states)
+        return torch.nn.functional.rms_norm(hidden_states, (hidden_states.shape[-1],), w, eps)
+
+    return lookaside
 
 
 # set by the HF recipe while a call runs on static-cache storage it allocated up front: the layers'

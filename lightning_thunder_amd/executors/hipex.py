@@ -301,6 +301,34 @@ def _fuse_decode_gemv(trace):
         drop.update((ja, jg))
         n_gated += 1
 
+    # the same pair written out (HF LlamaMLP): y = mul(silu(a), b)
+    for i, b in enumerate(bsyms):
+        if i in drop or b.sym.name != "mul" or len(b.args) != 2 or not all(isinstance(a, TensorProxy) for a in b.args):
+            continue
+        for s_arg, g_arg in (b.args, b.args[::-1]):
+            js = producer.get(s_arg.name)
+            if js is None or js in drop or bsyms[js].sym.name != "silu" or uses.get(s_arg.name) != 1:
+                continue
+            sb = bsyms[js]
+            a = sb.args[0] if sb.args else None
+            if len(sb.args) > 1 and sb.args[1] not in (False, None):
+                continue
+            ja, jg = producer.get(getattr(a, "name", None)), producer.get(g_arg.name)
+            if ja is None or jg is None or ja in drop or jg in drop or ja == jg:
+                continue
+            la, lg = bsyms[ja], bsyms[jg]
+            if la.sym is not hip_linear or lg.sym is not hip_linear or uses.get(a.name) != 1 or uses.get(g_arg.name) != 1:
+                continue
+            pa, pg = _linear_parts(la), _linear_parts(lg)
+            if pa["x"].name != pg["x"].name or any(p.get(k) is not None for p in (pa, pg) for k in ("bias", "residual", "act")):
+                continue
+            if _rows(pa["x"]) > _GEMV_MAX_ROWS or tuple(pa["w"].shape) != tuple(pg["w"].shape) or b.output.dtype != a.dtype:
+                continue
+            bind(i, pa["x"], pa["w"], None, None, "silu", pg["w"], False, None, 1e-5, output=b.output)
+            drop.update((ja, jg, js))
+            n_gated += 1
+            break
+
     # RMSNorm prologues
     uses = count_uses(drop)
     for i, b in enumerate(bsyms):

@@ -484,3 +484,24 @@ def test_argmax_rows_kernel(dtype, R, V):
     assert torch.equal(argmax_last(x), x.argmax(-1))
     logits = torch.randn(2, 5, V + 1, device="cuda", dtype=dtype)[..., :V]  # strided rows fall back or run aligned
     assert torch.equal(argmax_last(logits[:, -1], keepdim=True), logits[:, -1].argmax(-1, keepdim=True))
+
+
+def test_decode_gemv_fusion_in_hf_llama_decode():
+    tf = pytest.importorskip("transformers")
+    import lightning_thunder_amd as thunder
+
+    cfg = tf.LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
+    torch.manual_seed(0)
+    with torch.device("cuda"):
+        m = tf.LlamaForCausalLM(cfg).to(torch.bfloat16).eval()
+    m.requires_grad_(False)
+    x = torch.randint(1, 512, (1, 8), device="cuda")
+    kw = dict(do_sample=False, max_new_tokens=6, min_new_tokens=6, cache_implementation="static", pad_token_id=0,
+              disable_compile=True)
+    ref = m.generate(x, **kw)
+    tm = thunder.compile(m, recipe="hf-transformers")
+    out = tm.generate(x, **kw)
+    trace = str(thunder.last_traces(tm)[-1])
+    assert "hip_decode_linear" in trace and "'silu'" in trace, trace
+    assert (out == ref).float().mean() > 0.8  # greedy tokens of a random model: bf16 rounding may flip a late one
