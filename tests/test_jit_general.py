@@ -193,3 +193,30 @@ def test_auto_registered_torch_op_fwd_bwd():
     torch.testing.assert_close(g, x.grad)
     names = thunder.get_auto_registered_torch_op_names()
     assert any("i0" in n for n in names)
+
+
+class _Box:
+    def __init__(self, t):
+        self.t = t
+        self.n = torch.zeros((), dtype=torch.int64)
+
+
+def _forward_through(*args, **kwargs):  # a forwarding decorator-style wrapper (drops nothing, hides provenance)
+    return _use_box(*args, **kwargs)
+
+
+def _use_box(x, box):
+    box.n.add_(1)
+    return {"y": x + box.t, "box": box}
+
+
+def test_returned_input_objects_and_forwarded_provenance():
+    jf = thunder.jit(lambda x, box: _forward_through(x, box=box))
+    x = torch.randn(3)
+    b1, b2 = _Box(torch.ones(3)), _Box(torch.full((3,), 2.0))
+    o1 = jf(x, b1)
+    o2 = jf(x, b2)  # same program (cache hit) on another object
+    assert thunder.cache_hits(jf) == 1
+    assert o1["box"] is b1 and o2["box"] is b2  # the caller's objects of each call come back
+    torch.testing.assert_close(o2["y"], x + 2)
+    assert int(b1.n) == 1 and int(b2.n) == 1  # in-place updates land on each call's own tensor
