@@ -66,9 +66,12 @@ class HipGraphRunner:
     """Graph cache for one region (reference ``CUDAGraphRunner``)."""
 
     def __init__(self, fn, name: str, pool_owner: "HipGraphTransform", copy_outputs: bool = False,
-                 private_inputs: tuple = ()):
+                 private_inputs: tuple = (), mutated_inputs: tuple = ()):
         self.fn = fn
         self.private_inputs = private_inputs
+        # caller-owned inputs the graph updates in place (KV caches handed in per call): captured on
+        # the caller's storage, not a private clone; a later call with other storage copies in and back
+        self.mutated_inputs = mutated_inputs
         self.name = name
         self.owner = pool_owner
         self.copy_outputs = copy_outputs
@@ -101,6 +104,9 @@ class HipGraphRunner:
             if isinstance(a, torch.Tensor) and a.data_ptr() != s.data_ptr():
                 s.copy_(a)
         graph.replay()
+        for s, a, mut in zip(ins, args, self.mutated_inputs):
+            if mut and isinstance(a, torch.Tensor) and a.data_ptr() != s.data_ptr():
+                a.copy_(s)
         self.replays += 1
         if self.copy_outputs:
             return tuple(o.clone() if isinstance(o, torch.Tensor) else o for o in outs)
@@ -108,7 +114,9 @@ class HipGraphRunner:
 
     def _capture(self, key, args):
         priv = self.private_inputs
-        ins = tuple(a.clone() if (i < len(priv) and priv[i] and isinstance(a, torch.Tensor)) else a
+        mut = self.mutated_inputs
+        ins = tuple(a.clone() if (i < len(priv) and priv[i] and not (i < len(mut) and mut[i])
+                                  and isinstance(a, torch.Tensor)) else a
                     for i, a in enumerate(args))
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
@@ -209,8 +217,14 @@ class HipGraphTransform(Transform):
             sub.bound_symbols = list(r) + [prims.python_return.bind(tuple(outputs), output=None)]
             sub = del_last_used(sub)
             fn = sub.python_callable()
+            # inputs written in place by the region (functionalized write-backs, in-place cache updates)
+            from ..core.prims import OpTags
+
+            written = {a.name for b in r if OpTags.IN_PLACE in getattr(b.sym, "tags", ()) for a in b.flat_proxy_args}
             private = tuple(isinstance(p, TensorProxy) and p.name in caller_owned for p in inputs)
-            runner = HipGraphRunner(fn, name, self, copy_outputs=self.copy_outputs, private_inputs=private)
+            mutated = tuple(isinstance(p, TensorProxy) and p.name in written for p in inputs)
+            runner = HipGraphRunner(fn, name, self, copy_outputs=self.copy_outputs, private_inputs=private,
+                                    mutated_inputs=mutated)
             self.runners.append(runner)
             sym = Symbol(name, meta=None, is_prim=True, is_fusion=True)
             nb = BoundSymbol(sym, args=tuple(inputs), kwargs={}, output=tuple(outputs), subsymbols=list(r),

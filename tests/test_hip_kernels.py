@@ -505,3 +505,24 @@ def test_decode_gemv_fusion_in_hf_llama_decode():
     trace = str(thunder.last_traces(tm)[-1])
     assert "hip_decode_linear" in trace and "'silu'" in trace, trace
     assert (out == ref).float().mean() > 0.8  # greedy tokens of a random model: bf16 rounding may flip a late one
+
+
+def test_hf_generate_hipgraph_matches_uncaptured():
+    """The decode step replayed as a hipGraph must update the caller's static cache (in-place
+    inputs are written back), so its tokens equal the same compiled program run without graphs."""
+    tf = pytest.importorskip("transformers")
+    import lightning_thunder_amd as thunder
+
+    cfg = tf.LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
+    torch.manual_seed(0)
+    with torch.device("cuda"):
+        m = tf.LlamaForCausalLM(cfg).to(torch.bfloat16).eval()
+    m.requires_grad_(False)
+    x = torch.randint(1, 512, (1, 8), device="cuda")
+    kw = dict(do_sample=False, max_new_tokens=12, min_new_tokens=12, cache_implementation="static", pad_token_id=0,
+              disable_compile=True)
+    plain = thunder.compile(m, recipe="hf-transformers").generate(x, **kw)
+    graphed = thunder.compile(m, recipe="hf-transformers", plugins="reduce-overhead")
+    for _ in range(2):  # the second generate() hands in a new cache: copied in and back around the replay
+        assert torch.equal(graphed.generate(x, **kw), plain)
