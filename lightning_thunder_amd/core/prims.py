@@ -855,6 +855,28 @@ def _copy__meta(copy_from, copy_to):
 
 
 copy_ = make_prim(PrimIDs.COPY_, "copy_", meta=_copy__meta, tags=(OpTags.DONT_DCE, OpTags.IN_PLACE))
+copy_.written_args = (1,)
+
+
+def written_args(bsym) -> list:
+    """The proxy arguments an ``IN_PLACE`` bound symbol actually writes.
+
+    A symbol declares them with a ``written_args`` attribute: positional indices or keyword names
+    (``copy_`` writes its destination, ``index_copy_inplace`` its buffer, the fused RoPE+KV-cache
+    kernel its two caches).  An ``IN_PLACE`` symbol that declares nothing is taken to write every
+    tensor argument (conservative).  Non-``IN_PLACE`` symbols write nothing."""
+    sym = bsym.sym
+    if OpTags.IN_PLACE not in getattr(sym, "tags", ()):
+        return []
+    idx = getattr(sym, "written_args", None)
+    if idx is None:
+        return [a for a in bsym.flat_proxy_args if isinstance(a, _proxies.TensorProxy)]
+    out = []
+    for i in idx:
+        a = bsym.args[i] if isinstance(i, int) and i < len(bsym.args) else bsym.kwargs.get(i) if isinstance(i, str) else None
+        if isinstance(a, _proxies.TensorProxy):
+            out.append(a)
+    return out
 
 
 def _item_meta(a):

@@ -68,10 +68,12 @@ def get_model_state_dict(module, options: StateDictOptions = StateDictOptions(),
     for k, v in sd.items():
         if k in fsdp.original_shapes and isinstance(v, torch.Tensor):
             full = fsdp.original_shapes[k]
-            local = v
-            pad = local.shape[0] * len(ranks) - full[0]
-            if pad and tdist.get_rank(group) == len(ranks) - 1:
-                local = local[: local.shape[0] - pad]
+            # shard_tensor pads dim 0 to chunk * world (chunk = ceil(n / world)), so the padding can
+            # cover several trailing ranks: rank r holds rows [r*chunk, min((r+1)*chunk, n)) of the
+            # real tensor, possibly none (torch.chunk / Shard(0) placement semantics)
+            chunk = v.shape[0]
+            real = max(0, min(chunk, full[0] - tdist.get_rank(group) * chunk))
+            local = v[:real]
             out[k] = DTensor.from_local(local.cpu() if options.cpu_offload else local, mesh, [Shard(0)],
                                         run_check=False, shape=torch.Size(full),
                                         stride=torch.empty(full, device="meta").stride())
@@ -95,11 +97,15 @@ def load_model_state_dict(state_dict: dict[str, Any], module, options: StateDict
             v = v.to_local()
         local[k] = v
     if fsdp is not None:
+        # a Shard(0) local holds this rank's real rows (none on fully padded ranks): re-pad to the
+        # module's chunk-sized shard
         own = module.state_dict()
         for k, v in list(local.items()):
-            if k in own and isinstance(v, torch.Tensor) and v.shape != own[k].shape:
+            if k in fsdp.original_shapes and k in own and isinstance(v, torch.Tensor) and v.shape != own[k].shape:
                 pad = own[k].shape[0] - v.shape[0]
-                local[k] = torch.cat([v, v.new_zeros((pad,) + tuple(v.shape[1:]))]) if pad > 0 else v
+                if pad < 0 or tuple(v.shape[1:]) != tuple(own[k].shape[1:]):
+                    raise ValueError(f"{k}: checkpoint shard {tuple(v.shape)} does not fit local shard {tuple(own[k].shape)}")
+                local[k] = torch.cat([v.to(own[k].device), v.new_zeros((pad,) + tuple(v.shape[1:]), device=own[k].device)])
     module.load_state_dict(local, strict=options.strict)
 
 

@@ -92,6 +92,8 @@ def _register():
         out = dist_prims.reduce_scatter(input, to_reduce_op(op), _group(group), False, 0)
         prims.copy_(prims.reshape(out, tuple(output.shape)), output)
 
+    for f in (all_reduce_, broadcast_, all_gather_, reduce_scatter_):
+        f.written_args = (0,)  # the tensor / output_tensor argument; inputs are only read
     for f in (all_reduce, all_gather, reduce_scatter, broadcast, wait, all_reduce_, broadcast_, all_gather_,
               reduce_scatter_):
         setattr(ltorch, f.name, f)

@@ -389,6 +389,7 @@ def _qkv_rope_cache_impl(qkv, cos, sin, n_head, n_query_groups, head_size, rope_
 
 hip_qkv_rope_cache = ex.register_operator("hip_qkv_rope_cache", meta=_qkv_rope_cache_meta, fn=_qkv_rope_cache_impl,
                                           tags=(OpTags.DONT_DCE, OpTags.IN_PLACE))
+hip_qkv_rope_cache.written_args = (7, 8)  # kc, vc; qkv/cos/sin/pos are only read
 
 
 def _fuse_kv_cache_writes(trace):

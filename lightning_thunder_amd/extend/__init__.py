@@ -130,6 +130,8 @@ class Executor:
         else:
             sym._exec_fn = None
         sym.impl_fn = fn
+        if like is not None and getattr(like, "written_args", None) is not None:
+            sym.written_args = like.written_args
         self.opmap[name] = sym
         self.implmap[sym.id] = ImplInfo(symbol=sym)
         register_symbol(sym)

@@ -254,9 +254,12 @@ class LLaMAMoE(nn.Module):
         self.fc_1 = nn.Parameter(torch.empty(E, I, D))
         self.fc_2 = nn.Parameter(torch.empty(E, I, D))
         self.proj = nn.Parameter(torch.empty(E, D, I))
-        for w in (self.fc_1, self.fc_2, self.proj):
-            nn.init.normal_(w, std=0.02)
         self.config = config
+        self.reset_parameters()
+
+    def reset_parameters(self, std: float = 0.02) -> None:
+        for w in (self.fc_1, self.fc_2, self.proj):
+            nn.init.normal_(w, std=std)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, T, D = x.shape
@@ -377,7 +380,12 @@ class GPT(nn.Module):
 
 
 def init_weights(model: GPT, std: float = 0.02) -> None:
-    """Random init (synthetic benchmark weights; no checkpoints are available offline)."""
+    """Random init (synthetic benchmark weights; no checkpoints are available offline).
+
+    Every parameter and buffer is initialised — a model materialised with ``to_empty`` holds
+    uninitialised memory otherwise: Linear/Embedding weights N(0, std), biases zero, and every other
+    module with a ``reset_parameters`` (RMSNorm/LayerNorm weights to one, KV caches to zero, MoE
+    routers) through it."""
     for m in model.modules():
         if isinstance(m, nn.Linear):
             nn.init.normal_(m.weight, mean=0.0, std=std)
@@ -385,6 +393,13 @@ def init_weights(model: GPT, std: float = 0.02) -> None:
                 nn.init.zeros_(m.bias)
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, mean=0.0, std=std)
+        elif isinstance(m, nn.LayerNorm):
+            if m.weight is not None:
+                nn.init.ones_(m.weight)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif hasattr(m, "reset_parameters"):
+            m.reset_parameters()
 
 
 def flops_per_token(config: Config, seq_len: int, training: bool = True) -> float:

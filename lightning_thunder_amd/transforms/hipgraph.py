@@ -13,10 +13,11 @@ MI355X design:
   tensors become the graph's static inputs and on replay an input is copied only if it lives
   at a different address.  Parameters/buffers never move and the backward consumes the
   forward graph's outputs (graph pool, fixed addresses), so a training step copies only the
-  token batch and the incoming loss gradient.  Tensors the *caller* passed in (arguments of
-  a forward/computation trace that are not parameters/buffers) are cloned into private
-  static buffers at capture: the caller may keep using its tensor (e.g. ``generate`` keeps
-  every sampled token), and later replays must not write into it.
+  token batch and the incoming loss gradient.  Read-only tensors the *caller* passed in
+  (arguments of a forward/computation trace that are not parameters/buffers) are cloned into
+  private static buffers at capture: the caller may keep using its tensor (e.g. ``generate``
+  keeps every sampled token), and later replays must not write into it.  Caller tensors the
+  region writes (static KV caches) bind a graph to their storage (see ``HipGraphRunner``).
 * One private memory pool is shared by every graph of the transform (fw and bw graphs
   replay in capture order), so graphed memory ~= eager peak.
 * First call per signature runs eagerly (warm-up: lazy library init, hiprtc compiles of
@@ -63,19 +64,45 @@ def default_capturable(bsym: BoundSymbol, *, capture_collectives: bool = False) 
 
 
 class HipGraphRunner:
-    """Graph cache for one region (reference ``CUDAGraphRunner``)."""
+    """Graph cache for one region (reference ``CUDAGraphRunner``, ``thunder/transforms/cudagraph.py:26-163``).
+
+    Inputs fall in three groups:
+
+    * framework-owned (parameters, buffers, saved tensors, the previous graph's outputs): the
+      captured call's tensors are the graph's static inputs; a replay copies one only when it
+      arrives at another address.
+    * caller-owned, read-only (token ids, ``cache_position``): cloned into private static buffers at
+      capture and copied in when the caller hands in other storage, so replays never write into
+      a tensor the caller keeps.
+    * caller-owned and written in place by the region (static KV caches handed in per call): the
+      first storage seen for a signature gets a graph captured on that storage itself, so a decode
+      loop over one long-lived cache replays with zero copies.  Any *other* storage replays a
+      second graph captured on private static buffers: the caller's tensors are copied in before
+      the replay (skipped when it is the storage the previous replay wrote back to and the caller
+      has not modified it since, tracked by the tensor version counter) and copied back after it,
+      each direction in one ``_foreach_copy_``.  A graph bound to one caller's storage is never
+      replayed for another caller, so an earlier ``generate``'s ``past_key_values`` stay intact.
+    """
 
     def __init__(self, fn, name: str, pool_owner: "HipGraphTransform", copy_outputs: bool = False,
                  private_inputs: tuple = (), mutated_inputs: tuple = ()):
         self.fn = fn
         self.private_inputs = private_inputs
-        # caller-owned inputs the graph updates in place (KV caches handed in per call): captured on
-        # the caller's storage, not a private clone; a later call with other storage copies in and back
         self.mutated_inputs = mutated_inputs
+        n = max(len(private_inputs), len(mutated_inputs))
+        priv = tuple(private_inputs) + (False,) * (n - len(private_inputs))
+        mut = tuple(mutated_inputs) + (False,) * (n - len(mutated_inputs))
+        # caller-owned inputs written by the region / caller-owned read-only inputs
+        self._bound = tuple(i for i in range(n) if priv[i] and mut[i])
+        self._clone = tuple(i for i in range(n) if priv[i] and not mut[i])
+        self._bound_set = frozenset(self._bound)
         self.name = name
         self.owner = pool_owner
         self.copy_outputs = copy_outputs
         self.entries: dict = {}
+        self._warm: set = set()
+        self._bound_storage: dict = {}  # signature -> storage key the zero-copy graph is bound to
+        self._written_back: dict = {}  # signature -> ((ptr, version) of each bound arg after the last write-back)
         self._lock = threading.Lock()
         self.replays = 0
         self.captures = 0
@@ -91,33 +118,44 @@ class HipGraphRunner:
         return tuple(k)
 
     def __call__(self, *args):
-        key = self._key(args)
+        sig = self._key(args)
+        if sig not in self._warm:
+            self._warm.add(sig)
+            return self.fn(*args)
+        private = False
+        if self._bound:
+            storage = tuple(args[i].data_ptr() for i in self._bound)
+            private = self._bound_storage.setdefault(sig, storage) != storage
+        key = (sig, private)
         e = self.entries.get(key)
         if e is None:
-            self.entries[key] = "warm"
-            return self.fn(*args)
-        if e == "warm":
             with self._lock:
-                e = self._capture(key, args)
+                e = self._capture(key, args, private)
         ins, graph, outs = e
-        for s, a in zip(ins, args):
-            if isinstance(a, torch.Tensor) and a.data_ptr() != s.data_ptr():
+        if private:
+            self._copy_in_bound(sig, ins, args)
+        skip = self._bound_set if private else ()
+        for i, (s, a) in enumerate(zip(ins, args)):
+            if isinstance(a, torch.Tensor) and i not in skip and a.data_ptr() != s.data_ptr():
                 s.copy_(a)
         graph.replay()
-        for s, a, mut in zip(ins, args, self.mutated_inputs):
-            if mut and isinstance(a, torch.Tensor) and a.data_ptr() != s.data_ptr():
-                a.copy_(s)
+        if private:
+            dst = [args[i] for i in self._bound]
+            torch._foreach_copy_(dst, [ins[i] for i in self._bound])
+            self._written_back[sig] = tuple((t.data_ptr(), t._version) for t in dst)
         self.replays += 1
         if self.copy_outputs:
             return tuple(o.clone() if isinstance(o, torch.Tensor) else o for o in outs)
         return outs
 
-    def _capture(self, key, args):
-        priv = self.private_inputs
-        mut = self.mutated_inputs
-        ins = tuple(a.clone() if (i < len(priv) and priv[i] and not (i < len(mut) and mut[i])
-                                  and isinstance(a, torch.Tensor)) else a
-                    for i, a in enumerate(args))
+    def _copy_in_bound(self, sig, ins, args):
+        cur = tuple((args[i].data_ptr(), args[i]._version) for i in self._bound)
+        if self._written_back.get(sig) != cur:  # other storage, or the caller changed it since
+            torch._foreach_copy_([ins[i] for i in self._bound], [args[i] for i in self._bound])
+
+    def _capture(self, key, args, private: bool):
+        clone = set(self._clone) | (set(self._bound) if private else set())
+        ins = tuple(a.clone() if i in clone and isinstance(a, torch.Tensor) else a for i, a in enumerate(args))
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         with torch.cuda.graph(g, pool=self.owner.pool()):
@@ -218,9 +256,7 @@ class HipGraphTransform(Transform):
             sub = del_last_used(sub)
             fn = sub.python_callable()
             # inputs written in place by the region (functionalized write-backs, in-place cache updates)
-            from ..core.prims import OpTags
-
-            written = {a.name for b in r if OpTags.IN_PLACE in getattr(b.sym, "tags", ()) for a in b.flat_proxy_args}
+            written = {a.name for b in r for a in prims.written_args(b)}
             private = tuple(isinstance(p, TensorProxy) and p.name in caller_owned for p in inputs)
             mutated = tuple(isinstance(p, TensorProxy) and p.name in written for p in inputs)
             runner = HipGraphRunner(fn, name, self, copy_outputs=self.copy_outputs, private_inputs=private,

@@ -26,6 +26,7 @@ def _meta(buf, dim, index, src):
 
 index_copy_inplace = Symbol("index_copy_inplace", _meta, id="lta.index_copy_inplace", is_prim=True,
                             tags=(OpTags.DONT_DCE, OpTags.IN_PLACE))
+index_copy_inplace.written_args = (0,)
 register_symbol(index_copy_inplace)
 
 

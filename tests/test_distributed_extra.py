@@ -20,7 +20,15 @@ def _model():
     return torch.nn.Sequential(torch.nn.Linear(8, 15), torch.nn.GELU(), torch.nn.Linear(15, 3)).double()
 
 
-def _ckpt_worker(rank, world, port, d):
+def _tiny_rows_model():
+    # dim 0 smaller than the world size (3 rows on 4 ranks) and padding spanning several ranks
+    # (5 rows -> shards of 2, 2, 1, 0)
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(8, 3), torch.nn.Tanh(), torch.nn.Linear(3, 5)).double()
+
+
+def _ckpt_worker(rank, world, port, d, make=None):
+    make = make or _model
     import lightning_thunder_amd as thunder
     from lightning_thunder_amd.distributed import fsdp
     from lightning_thunder_amd.distributed import checkpoint as ck
@@ -28,7 +36,7 @@ def _ckpt_worker(rank, world, port, d):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        jm = fsdp(thunder.jit(_model()))
+        jm = fsdp(thunder.jit(make()))
         with torch.no_grad():
             for p in jm.parameters():
                 p.mul_(1.5)
@@ -36,12 +44,16 @@ def _ckpt_worker(rank, world, port, d):
         ck.save(sd, os.path.join(d, "ckpt"))
         full = ck.get_model_state_dict(jm, ck.StateDictOptions(full_state_dict=True, rank0_only=True))
         # a fresh sharded model, loaded from the sharded checkpoint
-        jm2 = fsdp(thunder.jit(_model()))
+        jm2 = fsdp(thunder.jit(make()))
         sd2 = ck.get_model_state_dict(jm2, ck.StateDictOptions(full_state_dict=False))
         ck.load(sd2, os.path.join(d, "ckpt"))
         ck.load_model_state_dict(sd2, jm2, ck.StateDictOptions(full_state_dict=False))
         diff = max((a - b).abs().max().item() for a, b in zip(jm.parameters(), jm2.parameters()))
-        torch.save({"diff": diff, "full_keys": sorted(full), "full_shapes": {k: tuple(v.shape) for k, v in full.items()}},
+        # every sharded entry reassembles to the full (scaled) parameter
+        ref = {k: v * 1.5 for k, v in make().state_dict().items()}
+        full_err = max((sd[k].full_tensor() - ref[k]).abs().max().item() for k in ref)
+        local_rows = {k: tuple(sd[k].to_local().shape) for k in ref}
+        torch.save({"diff": diff, "full_err": full_err, "local_rows": local_rows, "full_keys": sorted(full), "full_shapes": {k: tuple(v.shape) for k, v in full.items()}},
                    os.path.join(d, f"r{rank}.pt"))
     finally:
         torch.distributed.destroy_process_group()
@@ -55,6 +67,20 @@ def test_fsdp_dcp_roundtrip():
         r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=False)
     assert r0["diff"] == 0.0 and r1["diff"] == 0.0
     assert r0["full_shapes"]["0.weight"] == (15, 8) and r1["full_keys"] == []
+    assert r0["full_err"] == 0.0 and r1["full_err"] == 0.0
+
+
+def test_fsdp_dcp_roundtrip_padding_spans_ranks():
+    world = 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ckpt_worker, args=(world, _free_port(), d, _tiny_rows_model), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+    for r in res:
+        assert r["diff"] == 0.0 and r["full_err"] == 0.0
+    assert [r["local_rows"]["2.bias"] for r in res] == [(2,), (2,), (1,), (0,)]
+    assert [r["local_rows"]["0.weight"] for r in res] == [(1, 8), (1, 8), (1, 8), (0, 8)]
+    assert res[0]["full_shapes"]["2.weight"] == (5, 3)
 
 
 def _hybrid_worker(rank, world, port, d):

@@ -524,5 +524,15 @@ def test_hf_generate_hipgraph_matches_uncaptured():
               disable_compile=True)
     plain = thunder.compile(m, recipe="hf-transformers").generate(x, **kw)
     graphed = thunder.compile(m, recipe="hf-transformers", plugins="reduce-overhead")
-    for _ in range(2):  # the second generate() hands in a new cache: copied in and back around the replay
-        assert torch.equal(graphed.generate(x, **kw), plain)
+    kept = None
+    for i in range(3):  # later generate() calls hand in new caches: replayed on private buffers
+        out = graphed.generate(x, return_dict_in_generate=True, **kw)
+        assert torch.equal(out.sequences, plain)
+        if i == 0:
+            kept = out.past_key_values
+            snap = [(l.keys.clone(), l.values.clone()) for l in kept.layers]
+        else:
+            assert out.past_key_values is not kept
+    # the cache the first call returned (the storage its decode graph was captured on) is untouched
+    for l, (k, v) in zip(kept.layers, snap):
+        assert torch.equal(l.keys, k) and torch.equal(l.values, v)

@@ -3,7 +3,7 @@ import pytest
 import torch
 
 import lightning_thunder_amd as thunder
-from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform, default_capturable
+from lightning_thunder_amd.transforms.hipgraph import HipGraphRunner, HipGraphTransform, default_capturable
 
 
 def test_region_structure_cpu():
@@ -77,3 +77,86 @@ def test_hipgraph_with_hip_kernels_gpu():
         torch.testing.assert_close(out, ref)
         out.float().sum().backward()
     assert sum(r.replays for r in t.runners) >= 1
+
+
+def test_region_marks_only_written_inputs_cpu():
+    """Only the destination of an in-place op is a written input: the index and source of a cache
+    update stay read-only (private clones, no write-back)."""
+    from lightning_thunder_amd.transforms import hipgraph as hg
+
+    t = HipGraphTransform(is_capturable=lambda b: b.sym.id not in hg._NOT_CAPTURABLE_IDS and not hg._is_unpack(b))
+
+    def f(cache, pos, val):
+        cache.index_copy_(0, pos, val)
+        return cache * 2
+
+    jf = thunder.jit(f, transforms=[t])
+    cache, pos, val = torch.zeros(6, 3), torch.tensor([1, 4]), torch.ones(2, 3)
+    out = jf(cache, pos, val)
+    torch.testing.assert_close(out, f(torch.zeros(6, 3), pos, val))
+    trace = str(thunder.last_traces(jf)[-1])
+    assert "index_copy_inplace" in trace or "copy_" in trace, trace
+    (r,) = [r for r in t.runners]
+    region = [b for b in thunder.last_traces(jf)[-1].bound_symbols if b.sym.name == r.name][0]
+    names = [a.name for a in region.args]
+    written = {n for n, m in zip(names, r.mutated_inputs) if m}
+    caller = {n for n, p in zip(names, r.private_inputs) if p}
+    assert len(written) == 1 and written <= caller, (names, r.mutated_inputs)
+    assert len(caller) == 3
+
+
+def test_written_args_table():
+    from lightning_thunder_amd.core import prims
+    from lightning_thunder_amd.core.proxies import TensorProxy
+    from lightning_thunder_amd.core.trace import TraceCtx, tracectx
+    from lightning_thunder_amd.transforms.inplace_index_copy import index_copy_inplace
+    from lightning_thunder_amd.executors.hipex import hip_qkv_rope_cache
+
+    with tracectx(TraceCtx()):
+        a = TensorProxy(shape=(4, 4), device="cpu", dtype=torch.float32)
+        b = TensorProxy(shape=(4, 4), device="cpu", dtype=torch.float32)
+        i = TensorProxy(shape=(2,), device="cpu", dtype=torch.int64)
+        s = TensorProxy(shape=(2, 4), device="cpu", dtype=torch.float32)
+        cp = prims.copy_.bind(a, b, output=b)
+        ic = index_copy_inplace.bind(a, 0, i, s, output=a)
+        assert [p.name for p in prims.written_args(cp)] == [b.name]
+        assert [p.name for p in prims.written_args(ic)] == [a.name]
+        assert hip_qkv_rope_cache.written_args == (7, 8)
+        # not in place: writes nothing
+        assert prims.written_args(prims.python_return.bind(a, output=None)) == []
+
+
+@pytest.mark.gpu
+def test_runner_never_writes_other_callers_storage_gpu():
+    """A graph captured on caller A's cache is not replayed for caller B's cache; B runs on private
+    buffers with copy-in/back; read-only caller inputs are private clones; A stays intact."""
+    def f(cache, pos, val):
+        cache.index_copy_(0, pos, val)
+        return (cache.sum(0),)
+
+    t = HipGraphTransform()
+    r = HipGraphRunner(f, "t", t, private_inputs=(True, True, True), mutated_inputs=(True, False, False))
+
+    def run(cache, start, n, scale):
+        ref = cache.clone()
+        for p in range(start, start + n):
+            pos = torch.tensor([p], device="cuda")
+            val = torch.full((1, 4), float(p + 1) * scale, device="cuda")
+            (s,) = r(cache, pos, val)
+            ref[p] = val[0]
+            torch.testing.assert_close(s, ref.sum(0))
+            assert pos.item() == p  # caller's read-only input untouched
+        torch.testing.assert_close(cache, ref)
+
+    A = torch.zeros(16, 4, device="cuda")
+    B = torch.zeros(16, 4, device="cuda")
+    run(A, 0, 4, 1.0)
+    snap_a = A.clone()
+    run(B, 0, 6, -2.0)            # other storage: private graph, copied in and back
+    torch.testing.assert_close(A, snap_a)
+    B.zero_()                     # caller modifies its cache between calls: copy-in must not be skipped
+    run(B, 6, 2, 3.0)
+    run(A, 4, 3, 1.0)             # back on A: zero-copy bound graph
+    assert r.captures == 2
+    (ins_bound, _, _), = [e for k, e in r.entries.items() if not k[1]]
+    assert ins_bound[0] is A and ins_bound[1] is not None

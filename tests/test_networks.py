@@ -155,3 +155,25 @@ def test_hf_generate_static_cache_through_recipe():
         assert torch.equal(out, ref), (out, ref)
     assert thunder.cache_misses(tm) == 2  # one prefill and one decode program
     assert thunder.cache_hits(tm) >= 25
+
+
+@pytest.mark.parametrize("name", ["llama2-like", "mixtral-like"])
+def test_litgpt_init_weights_after_to_empty(name):
+    """A model materialised from meta with ``to_empty`` is fully initialised by ``init_weights``:
+    norm weights one, expert weights finite and random (benchmarks build models this way)."""
+    from lightning_thunder_amd.models.litgpt import GPT, Config, RMSNorm, init_weights
+
+    with torch.device("meta"):
+        m = GPT(Config.from_name(name))
+    m = m.to_empty(device="cpu")
+    for p in m.parameters():
+        p.data.fill_(float("nan"))
+    init_weights(m)
+    for n, p in m.named_parameters():
+        assert torch.isfinite(p).all(), n
+    norms = [mod for mod in m.modules() if isinstance(mod, (RMSNorm, torch.nn.LayerNorm))]
+    assert norms and all(torch.equal(mod.weight, torch.ones_like(mod.weight)) for mod in norms)
+    m.set_rope_cache(16, device="cpu")
+    idx = torch.randint(0, m.config.vocab_size, (1, 16))
+    logits = m(idx)
+    assert torch.isfinite(logits).all() and logits.std() > 0
