@@ -122,8 +122,17 @@ def run(mode: str, args) -> dict:
         "data": "synthetic prompt, random-init weights", "n_gpus": 1,
         "reference_ms": {"thunder+cudagraphs (1xH100)": 542, "eager (1xH100)": 1493},
     }
-    res["tokens"] = out[0, -4:].tolist()
+    res["tokens"] = out[0, -args.new_tokens:].tolist()
     return res
+
+
+def _prefix_match(a, b) -> int:
+    n = 0
+    for x, y in zip(a, b):
+        if x != y:
+            break
+        n += 1
+    return n
 
 
 def main(argv=None):
@@ -137,14 +146,21 @@ def main(argv=None):
     p.add_argument("--n-layer", type=int, default=None, help="debug only")
     args = p.parse_args(argv)
     results = []
+    ref = {}  # model family -> tokens of its eager mode
     for mode in args.modes.split(","):
         r = run(mode, args)
+        fam = "hf" if mode.startswith("hf_") else "litgpt"
+        if mode in ("eager", "hf_eager"):
+            ref[fam] = r["tokens"]
+        if fam in ref:
+            # greedy decoding of a random-init model: logits are nearly flat, so one bf16 rounding
+            # difference flips an argmax and the continuation diverges; the leading tokens that agree
+            # with eager are the numerics check
+            r["prefix_match_vs_eager"] = _prefix_match(r["tokens"], ref[fam])
+        r["tokens"] = r["tokens"][:8]
         results.append(r)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
-    toks = {tuple(r["tokens"]) for r in results}
-    if len(toks) > 1:
-        print(f"warning: modes generated different tokens: {toks}", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -428,7 +428,10 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                     if c is not None and c[0] is t:
                         return c[1]
                     p = tensorproxy(t, name=comp.make_unique_name("tp"))
-                    p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
+                    if root != "input":
+                        # module / global / closure state lives across calls; tensors reached through
+                        # an argument (a cache object handed in per call) belong to the caller
+                        p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
                     tracker.register_input(p)
                     prov_inputs[id(t)] = (t, p, prov)
                     return p

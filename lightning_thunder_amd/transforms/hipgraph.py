@@ -74,7 +74,8 @@ class HipGraphRunner:
     * caller-owned, read-only (token ids, ``cache_position``): cloned into private static buffers at
       capture and copied in when the caller hands in other storage, so replays never write into
       a tensor the caller keeps.
-    * caller-owned and written in place by the region (static KV caches handed in per call): the
+    * written in place by the region (static KV caches, handed in per call or held as module
+      buffers that may be re-allocated): the
       first storage seen for a signature gets a graph captured on that storage itself, so a decode
       loop over one long-lived cache replays with zero copies.  Any *other* storage replays a
       second graph captured on private static buffers: the caller's tensors are copied in before
@@ -92,8 +93,8 @@ class HipGraphRunner:
         n = max(len(private_inputs), len(mutated_inputs))
         priv = tuple(private_inputs) + (False,) * (n - len(private_inputs))
         mut = tuple(mutated_inputs) + (False,) * (n - len(mutated_inputs))
-        # caller-owned inputs written by the region / caller-owned read-only inputs
-        self._bound = tuple(i for i in range(n) if priv[i] and mut[i])
+        # inputs written by the region (graphs are bound to their storage) / caller-owned read-only inputs
+        self._bound = tuple(i for i in range(n) if mut[i])
         self._clone = tuple(i for i in range(n) if priv[i] and not mut[i])
         self._bound_set = frozenset(self._bound)
         self.name = name
