@@ -183,6 +183,239 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_kernel(const __hip_bfloa
 }
 
 // ---------------------------------------------------------------------------------------------
+// 8-phase pipelined variant (cdna_hip_programming.md §5, "256² 8-phase template"; T2/T3+T4/T5).
+// Same tile, waves and swizzle as above, but each K-tile (BK = 64) is staged as four 16 KiB
+// half-tiles (A rows of m-half 0 / 1 of every wave, B rows of n-half 0 / 1) and consumed in
+// four phases of 16 MFMAs (one C-quadrant each):
+//   ph1 read A0,B0 -> Q(0,0) | ph2 read B1 -> Q(0,1) | ph3 read A1 -> Q(1,1) | ph4 -> Q(1,0)
+// Two K-tiles per loop iteration (even LDS buffer: phases 1-4, odd: 5-8).  Each phase issues ONE
+// half-tile of global_load_lds prefetch (2 per lane) into the buffer half that was last read a
+// phase earlier, so three half-tiles stay in flight across every barrier: the wait is a counted
+// `s_waitcnt vmcnt(6)` at phases 4 and 8 only (never 0 in steady state), barriers are raw
+// s_barrier (a __syncthreads() would drain the DMA queue), and all LDS lives in one array.
+// Measured on the Llama-2-7B shapes (random data): 6-11 % SLOWER than the 2-buffer loop above
+// (profiles/gemm_microbench.json), so variant 0 stays the default; kept for the A/B.
+// ---------------------------------------------------------------------------------------------
+constexpr int HALF_BYTES = 128 * BK * 2;  // 16 KiB: 128 rows x 128 B
+
+template <int ACT, bool BIAS, bool RES>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_8ph_kernel(const __hip_bfloat16* __restrict__ A,
+                                                                  const __hip_bfloat16* __restrict__ B,
+                                                                  __hip_bfloat16* __restrict__ C,
+                                                                  const __hip_bfloat16* __restrict__ bias,
+                                                                  const __hip_bfloat16* __restrict__ R, int M, int N,
+                                                                  int K, int lda, int ldb, int ldc, int ldr,
+                                                                  float alpha) {
+  __shared__ __attribute__((aligned(1024))) char smem[8 * HALF_BYTES];  // [buffer 2][part 4] half-tiles
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: half-tile `part` (0 = A m-half 0, 1 = A m-half 1, 2 = B n-half 0, 3 = B n-half 1) of
+  // K-tile kt.  Local row lr of an A part maps to tile row (lr>>6)*128 + part*64 + (lr&63) (wave-row
+  // wm = lr>>6 owns local rows 64wm..64wm+63); of a B part to tile column (lr>>5)*64 + h*32 + (lr&31).
+  const int sr = lane >> 3, sc = (lane & 7) ^ sr;  // lane's row within an 8-row chunk, swizzled 16-B source chunk
+  auto stage = [&](int kt, int part) {
+    char* dst = smem + ((kt & 1) * 4 + part) * HALF_BYTES;
+    const int k0 = kt * BK + sc * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int chunk = i * 8 + wave;
+      const int lr = chunk * 8 + sr;
+      const __hip_bfloat16* src;
+      if (part < 2) {
+        src = A + (int64_t)(m0 + (lr >> 6) * 128 + part * 64 + (lr & 63)) * lda + k0;
+      } else {
+        src = B + (int64_t)(n0 + (lr >> 5) * 64 + (part - 2) * 32 + (lr & 31)) * ldb + k0;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + chunk * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 af[4][2], bfr[2][2][2];  // A: 4 m-tiles x 2 k-halves of one part; B: 2 parts x 2 n-tiles x 2 k-halves
+
+  auto read_a = [&](int buf, int part) {
+    const char* base = smem + (buf * 4 + part) * HALF_BYTES;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int lr = wm * 64 + m * 16 + fr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fq;
+        af[m][kk] = *reinterpret_cast<const bf16x8*>(base + lr * 128 + ((c ^ (lr & 7)) << 4));
+      }
+    }
+  };
+  auto read_b = [&](int buf, int h) {
+    const char* base = smem + (buf * 4 + 2 + h) * HALF_BYTES;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int lr = wn * 32 + n * 16 + fr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fq;
+        bfr[h][n][kk] = *reinterpret_cast<const bf16x8*>(base + lr * 128 + ((c ^ (lr & 7)) << 4));
+      }
+    }
+  };
+  // C-quadrant (mh, nh): m-tiles 4mh..4mh+3 x n-tiles 2nh, 2nh+1 of the wave's 8x4 accumulator grid
+  auto quadrant = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[mh * 4 + m][nh * 2 + n] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], bfr[nh][n][kk], acc[mh * 4 + m][nh * 2 + n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define LTA_PH_SYNC()                                 \
+  __builtin_amdgcn_s_barrier();                       \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#define LTA_PH_END() __builtin_amdgcn_s_barrier();
+
+  const int nk = K / BK;  // even (K % 128 == 0)
+  // prologue: K-tile 0 whole, K-tile 1 but its A m-half 1 (issued in phase 1)
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  stage(1, 0);
+  stage(1, 2);
+  stage(1, 3);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int t0 = 0; t0 < nk; t0 += 2) {
+    const int t1 = t0 + 1;
+    const bool more = t0 + 2 < nk;
+    // ---- even buffer (K-tile t0) ----
+    read_a(0, 0);
+    read_b(0, 0);
+    stage(t1, 1);
+    LTA_PH_SYNC();
+    quadrant(0, 0);
+    LTA_PH_END();
+
+    read_b(0, 1);
+    if (more) stage(t0 + 2, 0);
+    LTA_PH_SYNC();
+    quadrant(0, 1);
+    LTA_PH_END();
+
+    read_a(0, 1);
+    if (more) stage(t0 + 2, 2);
+    LTA_PH_SYNC();
+    quadrant(1, 1);
+    LTA_PH_END();
+
+    if (more) {
+      stage(t0 + 2, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    LTA_PH_SYNC();
+    quadrant(1, 0);
+    LTA_PH_END();
+
+    // ---- odd buffer (K-tile t1) ----
+    read_a(1, 0);
+    read_b(1, 0);
+    if (more) stage(t0 + 2, 1);
+    LTA_PH_SYNC();
+    quadrant(0, 0);
+    LTA_PH_END();
+
+    read_b(1, 1);
+    if (more) stage(t1 + 2, 0);
+    LTA_PH_SYNC();
+    quadrant(0, 1);
+    LTA_PH_END();
+
+    read_a(1, 1);
+    if (more) stage(t1 + 2, 2);
+    LTA_PH_SYNC();
+    quadrant(1, 1);
+    LTA_PH_END();
+
+    if (more) {
+      stage(t1 + 2, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+    LTA_PH_SYNC();
+    quadrant(1, 0);
+    LTA_PH_END();
+  }
+#undef LTA_PH_SYNC
+#undef LTA_PH_END
+
+  // ---- epilogue (as gemm_nt_bf16_kernel): registers -> swizzled bf16 LDS image -> 16-B stores ----
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 64 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        float v = acc[m][n][j] * alpha + bv;
+        v = act_fn<ACT>(v);
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) = __float2bfloat16(v);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+    const int64_t grow = m0 + wm * 128 + row;
+    const int gcol = n0 + wn * 64 + ch * 8;
+    if constexpr (RES) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
+      v = o.u;
+    }
+    *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // FP8 (OCP e4m3fn / e5m2) NT GEMM on the block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4,
 // 2x the bf16 rate).  Same geometry and LDS image as the bf16 kernel: BK = 128 fp8 = 128-B rows,
 // so staging (glds) and the XOR swizzle are byte-identical.  Per-tensor scaling: the operands
@@ -423,16 +656,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_grouped_nt_bf16_kernel(const __h
 
 template <int ACT>
 int launch_act(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
-               int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
+               int ldb, int ldc, int ldr, float alpha, int variant, hipStream_t s) {
   dim3 grid((M / BM) * (N / BN)), block(NTHR);
+  const bool eight = variant == 1 && K % (2 * BK) == 0;
 #define LTA_GEMM(BI, RE)                                                                                              \
-  hipLaunchKernelGGL((gemm_nt_bf16_kernel<ACT, BI, RE>), grid, block, 0, s, (const __hip_bfloat16*)A,                 \
-                     (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                       \
-                     (const __hip_bfloat16*)R, M, N, K, lda, ldb, ldc, ldr, alpha)
-  if (bias && R) LTA_GEMM(true, true);
-  else if (bias) LTA_GEMM(true, false);
-  else if (R) LTA_GEMM(false, true);
-  else LTA_GEMM(false, false);
+  if (eight)                                                                                                          \
+    hipLaunchKernelGGL((gemm_nt_bf16_8ph_kernel<ACT, BI, RE>), grid, block, 0, s, (const __hip_bfloat16*)A,           \
+                       (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                     \
+                       (const __hip_bfloat16*)R, M, N, K, lda, ldb, ldc, ldr, alpha);                                 \
+  else                                                                                                                \
+    hipLaunchKernelGGL((gemm_nt_bf16_kernel<ACT, BI, RE>), grid, block, 0, s, (const __hip_bfloat16*)A,               \
+                       (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                     \
+                       (const __hip_bfloat16*)R, M, N, K, lda, ldb, ldc, ldr, alpha)
+  if (bias && R) { LTA_GEMM(true, true); }
+  else if (bias) { LTA_GEMM(true, false); }
+  else if (R) { LTA_GEMM(false, true); }
+  else { LTA_GEMM(false, false); }
 #undef LTA_GEMM
   return (int)hipGetLastError();
 }
@@ -475,15 +714,22 @@ LTA_EXPORT int lta_gemm_tile_k() { return BK; }
 
 // C = act(alpha * A @ B^T + bias) + R ; A [M,K] (lda), B [N,K] (ldb), C/R [M,N] (ldc/ldr), all bf16.
 // Requires M % 256 == 0, N % 256 == 0, K % 64 == 0 and 16-B aligned rows (checked by the caller).
-LTA_EXPORT int lta_gemm_nt_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
-                                int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, hipStream_t stream) {
+// variant: 0 = 2-buffer loop, 1 = 8-phase pipelined loop (falls back to 0 unless K % 128 == 0).
+LTA_EXPORT int lta_gemm_nt_bf16_v(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                                  int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int variant,
+                                  hipStream_t stream) {
   if (M % BM || N % BN || K % BK) return -2;
   switch (act) {
-    case kNone: return launch_act<kNone>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
-    case kGeluTanh: return launch_act<kGeluTanh>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
-    case kGeluErf: return launch_act<kGeluErf>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
-    case kSilu: return launch_act<kSilu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
-    case kRelu: return launch_act<kRelu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, stream);
+    case kNone: return launch_act<kNone>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, variant, stream);
+    case kGeluTanh: return launch_act<kGeluTanh>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, variant, stream);
+    case kGeluErf: return launch_act<kGeluErf>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, variant, stream);
+    case kSilu: return launch_act<kSilu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, variant, stream);
+    case kRelu: return launch_act<kRelu>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, variant, stream);
   }
   return -1;
+}
+
+LTA_EXPORT int lta_gemm_nt_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                                int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, hipStream_t stream) {
+  return lta_gemm_nt_bf16_v(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, 0, stream);
 }

@@ -1,6 +1,8 @@
 """Python bindings of the hand-written CDNA4 GEMMs (``csrc/gemm.hip``, K2)."""
 from __future__ import annotations
 
+import os as _os
+
 import torch
 
 import ctypes
@@ -12,6 +14,8 @@ TILE_M, TILE_N, TILE_K = 256, 256, 64
 
 register_signature("lta_gemm_nt_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_float, c_int, c_void_p])
+register_signature("lta_gemm_nt_bf16_v", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                          c_int, c_int, c_int, c_float, c_int, c_int, c_void_p])
 
 
 def _rowmajor_2d(t: torch.Tensor) -> bool:
@@ -37,18 +41,23 @@ def gemm_nt_supported(a: torch.Tensor, b: torch.Tensor, bias=None, residual=None
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=None, alpha: float = 1.0,
-            out: torch.Tensor | None = None) -> torch.Tensor:
-    """``act(alpha * a @ b.T + bias) + residual`` with the hand-written MFMA kernel."""
+            out: torch.Tensor | None = None, variant: int | None = None) -> torch.Tensor:
+    """``act(alpha * a @ b.T + bias) + residual`` with the hand-written MFMA kernel.
+
+    ``variant`` (``LTA_GEMM_VARIANT``): 0 (default) the 2-buffer glds loop, 1 the 8-phase pipelined
+    loop (K % 128 == 0; 6-11 % slower on the Llama shapes, profiles/gemm_microbench.json)."""
     lib = require()
     M, K = a.shape
     N = b.shape[0]
+    if variant is None:
+        variant = int(_os.environ.get("LTA_GEMM_VARIANT", "0"))
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    rc = lib.lta_gemm_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(),
-                              None if bias is None else bias.data_ptr(),
-                              None if residual is None else residual.data_ptr(), M, N, K, a.stride(0), b.stride(0),
-                              out.stride(0), 0 if residual is None else residual.stride(0), alpha, ACT[act],
-                              stream_ptr(a.device))
+    rc = lib.lta_gemm_nt_bf16_v(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                None if bias is None else bias.data_ptr(),
+                                None if residual is None else residual.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                out.stride(0), 0 if residual is None else residual.stride(0), alpha, ACT[act], variant,
+                                stream_ptr(a.device))
     check(rc, "lta_gemm_nt_bf16")
     return out
 
