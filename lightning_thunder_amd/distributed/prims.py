@@ -140,6 +140,18 @@ def _grad_sync_meta(g, group, distparallel_type, world_size, replicate_group=Non
 grad_sync = _make("grad_sync", _grad_sync_meta, tags=(NON_DIFFERENTIABLE_TAG,))
 
 
+# ---- FSDP no_sync: unsharded-gradient stash ---------------------------------------------------------
+def _stash_grad_meta(g, shard):
+    return TensorProxy(like=shard, requires_grad=False)
+
+
+# Under ``no_sync`` the FSDP backward does not reduce-scatter: the full (padded) gradient is added
+# to a buffer attached to the parameter shard (``_lc_unsharded_grad``) and a zero gradient of the
+# shard's shape is returned; leaving ``no_sync`` reduce-scatters every stash once (reference
+# ``stash_grad_for_fsdp``, thunder/distributed/prims.py:282-363, torchex.py:2266-2333).
+stash_grad_for_fsdp = _make("stash_grad_for_fsdp", _stash_grad_meta, tags=(NON_DIFFERENTIABLE_TAG, OpTags.DONT_DCE))
+
+
 # ---- bucketing helpers ----------------------------------------------------------------------------
 def _numel(t):
     import math
@@ -298,6 +310,16 @@ def _synchronize_impl(a, group, distparallel_type=None, replicate_group=None):
     return a
 
 
+def _stash_grad_impl(g, shard):
+    prev = getattr(shard, "_lc_unsharded_grad", None)
+    if prev is None:
+        shard._lc_unsharded_grad = g.detach().clone()
+    else:
+        prev.add_(g)
+    # zero gradient of the shard's shape, no storage (the real one arrives when no_sync exits)
+    return torch.zeros((), dtype=shard.dtype, device=shard.device).expand(shard.shape)
+
+
 def _pack_impl(tensors, bucket_key):
     return torch.cat([t.reshape(-1) for t in tensors])
 
@@ -367,6 +389,7 @@ def _register_torch_impls():
         (broadcast, _broadcast_impl), (wait, _wait_impl), (synchronize, _synchronize_impl), (pack, _pack_impl),
         (unpack, _unpack_impl), (pack_for_fsdp, _pack_for_fsdp_impl), (unpack_for_fsdp, _unpack_for_fsdp_impl),
         (synchronize_tensor_parallel_output, _tp_out_impl), (synchronize_tensor_parallel_input, _tp_in_impl),
+        (stash_grad_for_fsdp, _stash_grad_impl),
     ):
         op = torchex.ex.register_operator(f"dist_{sym.name}", like=sym, fn=fn)
         torchex.ex.register_implementation(sym, op)
@@ -395,6 +418,8 @@ def _register_vjps():
         def bwd(g):
             if dpt is DistParallelType.REPLICATED and get_skip_data_parallel_grad_sync():
                 return (g,)
+            if dpt is DistParallelType.FULLY_SHARDED and get_skip_data_parallel_grad_sync():
+                return (stash_grad_for_fsdp(g, a),)
             if replicate_group is not None and dpt is DistParallelType.FULLY_SHARDED:
                 # hybrid sharding (2-D mesh): the bucketing pass adds an all-reduce over the replicas
                 return (grad_sync(g, group, dpt, w, replicate_group),)

@@ -171,6 +171,33 @@ class FSDPTransform(Transform):
                     done[id(p)] = newp
                     m._parameters[pname] = newp
         model._lc_fsdp = self
+        replicate = self.replicate_process_group
+
+        def sync_grads():
+            """Leaving ``no_sync``: reduce-scatter (AVG) every stashed unsharded gradient in one
+            collective (interleaved pack: rank r's chunk holds its rows of every gradient) and add
+            the shards to ``.grad`` (reference ``_sync_grads``, thunder/distributed/__init__.py:144-182)."""
+            from .. import prims as dp
+
+            params = [p for p in inner.parameters() if getattr(p, "_lc_unsharded_grad", None) is not None]
+            if not params:
+                return
+            grads = [p._lc_unsharded_grad for p in params]
+            for p in params:
+                del p._lc_unsharded_grad
+            buf = dp._pack_for_fsdp_impl(grads, world, "scatter")
+            shards = dp._reduce_scatter_impl(buf, dp.DistributedReduceOps.AVG, group)
+            if replicate is not None:
+                shards = dp._all_reduce_impl(shards, dp.DistributedReduceOps.AVG, replicate, skip_clone=True)
+            with torch.no_grad():
+                for p, g in zip(params, dp._unpack_for_fsdp_impl(shards, grads, world, "scatter")):
+                    g = g.to(p.dtype)
+                    if p.grad is None or p.grad.stride() == (0,) * p.grad.dim():
+                        p.grad = g.clone()
+                    else:
+                        p.grad.add_(g)
+
+        model._lc_sync_grads = sync_grads
 
     def transform_traces_pre_prologue(self, prologue_trace, computation_trace, epilogue_trace, **kwargs):
         from ... import torch as ltorch

@@ -106,6 +106,29 @@ def _nosync_worker(rank, port, out_dir):
         torch.distributed.destroy_process_group()
 
 
+def _fsdp_nosync_worker(rank, port, out_dir):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import fsdp
+
+    _init(rank, port)
+    try:
+        m = _model()
+        jm = fsdp(thunder.jit(m))
+        with jm.no_sync():
+            for mb in range(2):
+                jm(_data(rank, mb)).pow(2).mean().backward()
+            stashed = sorted(n for n, p in m.named_parameters() if getattr(p, "_lc_unsharded_grad", None) is not None)
+        bw_nosync = str(thunder.last_backward_traces(jm)[-1])
+        jm(_data(rank, 2)).pow(2).mean().backward()
+        bw_sync = str(thunder.last_backward_traces(jm)[-1])
+        grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        left = [n for n, p in m.named_parameters() if getattr(p, "_lc_unsharded_grad", None) is not None]
+        torch.save({"grads": grads, "bw_nosync": bw_nosync, "bw_sync": bw_sync, "stashed": stashed, "left": left},
+                   os.path.join(out_dir, f"rank{rank}.pt"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
 def _run(worker):
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
@@ -138,3 +161,22 @@ def test_ddp_no_sync_grad_accumulation():
             torch.testing.assert_close(r["grads"][n], p.grad)
         assert "all_reduce" not in r["bw_nosync"]
         assert "all_reduce" in r["bw_sync"]
+
+
+def test_fsdp_no_sync_grad_accumulation():
+    """FSDP under no_sync: the backward stashes unsharded gradients (no reduce-scatter); leaving the
+    context reduce-scatters them once; a later synced step accumulates on top (reference
+    test_fsdp.py no_sync tests)."""
+    from lightning_thunder_amd.distributed.transforms import shard_tensor
+
+    res = _run(_fsdp_nosync_worker)
+    m = _model()
+    loss = sum(m(_data(r, mb)).pow(2).mean() for r in range(WORLD) for mb in range(3)) / WORLD
+    loss.backward()
+    for rank, r in enumerate(res):
+        assert r["stashed"] == sorted(n for n, _ in m.named_parameters()) and r["left"] == []
+        for n, p in m.named_parameters():
+            expected, _ = shard_tensor(p.grad, rank, WORLD)
+            torch.testing.assert_close(r["grads"][n], expected)
+        assert "reduce_scatter" not in r["bw_nosync"] and "stash_grad_for_fsdp" in r["bw_nosync"]
+        assert "reduce_scatter" in r["bw_sync"]
