@@ -113,16 +113,48 @@ hip_fp8_quantize = ex.register_operator("hip_fp8_quantize", meta=_fp8_quant_meta
 hip_fp8_gemm = ex.register_operator("hip_fp8_gemm", meta=_fp8_gemm_meta, fn=_fp8_gemm_impl)
 
 
-def _fp8_vjp(x, w, bias=None):
+def _fp8_quant_delayed_meta(t, e5m2, key, slot):
+    return _fp8_quant_meta(t, e5m2)
+
+
+def _fp8_quant_delayed_impl(t, e5m2, key, slot):
+    from ..ops.fp8 import quantize_delayed
+
+    return quantize_delayed(t, e5m2, key, slot)
+
+
+def _fp8_update_impl(key):
+    from ..ops.fp8 import delayed_update
+
+    delayed_update(key)
+
+
+# delayed scaling: quantize against the slot's amax history (its own amax recorded while casting);
+# the history advances once per forward (first op of the program), after an amax all-reduce
+hip_fp8_quantize_delayed = ex.register_operator("hip_fp8_quantize_delayed", meta=_fp8_quant_delayed_meta,
+                                                fn=_fp8_quant_delayed_impl)
+hip_fp8_delayed_update = ex.register_operator("hip_fp8_delayed_update", meta=lambda key: None, fn=_fp8_update_impl,
+                                              tags=(OpTags.DONT_DCE,))
+hip_fp8_delayed_update.not_capturable = True  # may all-reduce over the data-parallel group
+
+
+def _quant(t, e5m2, key, slot):
+    if key is None:
+        return hip_fp8_quantize(t, e5m2)
+    return hip_fp8_quantize_delayed(t, e5m2, key, slot)
+
+
+def _fp8_vjp(x, w, bias=None, key=None, slots=None):
     from .. import torch as ltorch
 
-    qx, qxT, sx = hip_fp8_quantize(x, False)
-    qw, qwT, sw = hip_fp8_quantize(w, False)
+    sl = slots or (None, None, None)
+    qx, qxT, sx = _quant(x, False, key, sl[0])
+    qw, qwT, sw = _quant(w, False, key, sl[1])
     out_shape = tuple(x.shape[:-1]) + (w.shape[0],)
     y = hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, out_shape)
 
     def bwd(g):
-        qg, qgT, sg = hip_fp8_quantize(g, True)
+        qg, qgT, sg = _quant(g, True, key, sl[2])
         dx = hip_fp8_gemm(qg, qwT, sg, sw, 1, 0, None, tuple(x.shape))
         dw = hip_fp8_gemm(qgT, qxT, sg, sx, 1, 0, None, tuple(w.shape))
         if bias is None:
@@ -133,18 +165,20 @@ def _fp8_vjp(x, w, bias=None):
     return y, bwd
 
 
-def _fp8_exec(x, w, bias=None):
-    qx, _, sx = hip_fp8_quantize(x, False)
-    qw, _, sw = hip_fp8_quantize(w, False)
+def _fp8_exec(x, w, bias=None, key=None, slots=None):
+    sl = slots or (None, None, None)
+    qx, _, sx = _quant(x, False, key, sl[0])
+    qw, _, sw = _quant(w, False, key, sl[1])
     return hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
 
 
 def _register_fp8():
-    from ..transforms.fp8 import fp8_linear, eligible
+    from ..transforms.fp8 import fp8_linear, fp8_delayed_update, eligible
     from ..core.transforms import register_vjp
 
     ex.register_implementation(fp8_linear, checker=eligible, execution_transform=_fp8_exec)
     register_vjp(fp8_linear)(_fp8_vjp)
+    ex.register_implementation(fp8_delayed_update, hip_fp8_delayed_update)
 
 
 _register_fp8()

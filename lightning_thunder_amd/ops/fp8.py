@@ -116,3 +116,97 @@ def quantize(t: torch.Tensor, e5m2: bool = False):
 def gemm(qa: torch.Tensor, qb: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int, fmt_b: int,
          bias: torch.Tensor | None, out_shape) -> torch.Tensor:
     return gemm_nt_fp8(qa, qb, sa, sb, fmt_a, fmt_b, bias).reshape(out_shape)
+
+
+# ---------------------------------------------------------------------------------------------
+# Delayed scaling (TransformerEngine ``DelayedScaling`` recipe; reference
+# thunder/executors/transformer_engineex_impl.py:49-515, te_fp8_amax_and_scale_update)
+# ---------------------------------------------------------------------------------------------
+class DelayedScaling:
+    """Scale of each quantised tensor = fp8_max / max(amax history) / 2^margin.
+
+    Every quantisation folds its tensor's amax into the current-step slot *while casting* (the cast
+    kernel's amax output), so no separate amax pass runs; the history advances once per forward
+    (``delayed_update``), after an all-reduce(MAX) of the current amaxes over ``process_group``
+    (default: the world group when torch.distributed is initialised, ``reduce_amax=True``), so every
+    data-parallel rank uses identical scales.  A slot's first use falls back to current scaling."""
+
+    def __init__(self, amax_history_len: int = 16, margin: int = 0, reduce_amax: bool = True, process_group=None):
+        self.amax_history_len = amax_history_len
+        self.margin = margin
+        self.reduce_amax = reduce_amax
+        self.process_group = process_group
+
+    def __repr__(self):
+        return f"DelayedScaling(amax_history_len={self.amax_history_len}, margin={self.margin}, " \
+               f"reduce_amax={self.reduce_amax})"
+
+
+class _DelayedState:
+    def __init__(self, recipe: DelayedScaling, n_slots: int):
+        self.recipe = recipe
+        self.n = n_slots
+        self.hist = self.cur = self.hmax = None
+        self.seen = [False] * n_slots
+        self.updates = 0
+
+    def ensure(self, device):
+        if self.hist is None:
+            z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=device)  # noqa: E731
+            self.hist, self.cur, self.hmax = z(self.recipe.amax_history_len, self.n), z(self.n), z(self.n)
+
+    def group(self):
+        import torch.distributed as tdist
+
+        if not self.recipe.reduce_amax or not tdist.is_available() or not tdist.is_initialized():
+            return None
+        g = self.recipe.process_group
+        return g if g is not None else tdist.distributed_c10d._get_default_group()
+
+
+_DELAYED: dict[int, _DelayedState] = {}
+
+
+def new_delayed_state(recipe: DelayedScaling, n_slots: int) -> int:
+    key = len(_DELAYED)
+    _DELAYED[key] = _DelayedState(recipe, n_slots)
+    return key
+
+
+def delayed_state(key: int) -> _DelayedState:
+    return _DELAYED[key]
+
+
+def delayed_update(key: int) -> None:
+    """Advance the amax history by one step (device-only: graph-capturable but for the collective)."""
+    st = _DELAYED[key]
+    if st.hist is None:
+        return
+    g = st.group()
+    if g is not None and torch.distributed.get_world_size(g) > 1:
+        torch.distributed.all_reduce(st.cur, op=torch.distributed.ReduceOp.MAX, group=g)
+    h = st.hist
+    if h.shape[0] > 1:
+        h[1:] = h[:-1].clone()
+    h[0] = st.cur
+    torch.amax(h, 0, out=st.hmax)
+    st.cur.zero_()
+    st.updates += 1
+
+
+def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
+    """As :func:`quantize`, scaled from the slot's amax history; the tensor's own amax goes to the
+    slot's current-step entry.  Returns (q, q^T, scale) with a private scale scalar."""
+    st = _DELAYED[key]
+    st.ensure(t.device)
+    t2 = t.reshape(-1, t.shape[-1])
+    fmax = (E5M2_MAX if e5m2 else E4M3_MAX) * 2.0 ** -st.recipe.margin
+    scale = torch.empty((), dtype=torch.float32, device=t.device)
+    if st.seen[slot]:
+        amax_in = st.hmax[slot]
+    else:  # first use of the slot: no history yet -> current scaling for this call
+        st.seen[slot] = True
+        amax_in = torch.zeros((), dtype=torch.float32, device=t.device)
+        amax_into(t2, amax_in)
+    q, qT = cast_transpose(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=st.cur[slot])
+    return q, qT, scale

@@ -17,20 +17,26 @@ from __future__ import annotations
 
 import torch
 
+from ..core.prims import OpTags
 from ..core.proxies import TensorProxy
 from ..core.symbol import Symbol
 from ..core.trace import from_trace, tracectx, TraceProvenance
 from ..core.transform_common import Transform
 
 
-def _fp8_linear_meta(x, w, bias=None):
+def _fp8_linear_meta(x, w, bias=None, key=None, slots=None):
     return TensorProxy(like=x, shape=tuple(x.shape[:-1]) + (w.shape[0],))
 
 
+# key/slots: None for current scaling; else the delayed-scaling state key and the (x, w, dy) slots
 fp8_linear = Symbol("fp8_linear", _fp8_linear_meta, id="lta.fp8_linear", is_prim=True)
 
+# advances the delayed-scaling amax histories (first op of every forward)
+fp8_delayed_update = Symbol("fp8_delayed_update", lambda key: None, id="lta.fp8_delayed_update", is_prim=True,
+                            tags=(OpTags.DONT_DCE,))
 
-def eligible(x, w, bias=None) -> bool:
+
+def eligible(x, w, bias=None, key=None, slots=None) -> bool:
     if not all(isinstance(t, TensorProxy) for t in (x, w)):
         return False
     if x.device.type != "cuda" or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.ndim != 2 or x.ndim < 2:
@@ -45,11 +51,22 @@ def eligible(x, w, bias=None) -> bool:
 
 
 class FP8LinearTransform(Transform):
-    def __init__(self, recipe: str = "current", amax_history_len: int = 16, skip: tuple[str, ...] = ()):
+    """``recipe``: ``"current"`` (per-tensor current scaling: one amax pass per cast), ``"delayed"``
+    or a :class:`~lightning_thunder_amd.ops.fp8.DelayedScaling` (amax history, scales from earlier
+    steps, amax all-reduced over the data-parallel group; reference TE ``DelayedScaling``)."""
+
+    def __init__(self, recipe="current", amax_history_len: int = 16, skip: tuple[str, ...] = ()):
+        from ..ops.fp8 import DelayedScaling
+
+        if recipe == "delayed":
+            recipe = DelayedScaling(amax_history_len=amax_history_len)
+        if not (recipe == "current" or isinstance(recipe, DelayedScaling)):
+            raise ValueError(f"unknown FP8 recipe {recipe!r}")
         self.recipe = recipe
         self.amax_history_len = amax_history_len
         self.skip = skip
         self.n_converted = 0
+        self.state_key = None
 
     def transform_traces_pre_prologue(self, prologue_trace, computation_trace, epilogue_trace, **kwargs):
         from ..executors import hipex  # noqa: F401  (registers fp8_linear's implementation + VJP)
@@ -59,6 +76,13 @@ class FP8LinearTransform(Transform):
         new.scopes = [new.bound_symbols]
         swap: dict = {}
         n = 0
+        delayed = self.recipe != "current"
+        slots: dict = {}  # ("x"|"w", proxy name) / ("dy", site) -> history slot; siblings reading one x share it
+
+        def slot(k):
+            return slots.setdefault(k, len(slots))
+
+        sites = []
         with tracectx(new):
             for b in computation_trace.bound_symbols:
                 nb = b.swap_proxies(swap, skip_output=True)
@@ -66,7 +90,12 @@ class FP8LinearTransform(Transform):
                     x, w = nb.args[0], nb.args[1]
                     bias = nb.args[2] if len(nb.args) > 2 else nb.kwargs.get("bias")
                     if eligible(x, w, bias) and not any(s in w.name for s in self.skip):
-                        y = fp8_linear(x, w, bias)
+                        if delayed:
+                            sl = (slot(("x", x.name)), slot(("w", w.name)), slot(("dy", n)))
+                            sites.append(len(new.bound_symbols))
+                            y = fp8_linear(x, w, bias, -1, sl)  # key patched below (slot count known last)
+                        else:
+                            y = fp8_linear(x, w, bias)
                         swap[b.output.name] = y
                         n += 1
                         continue
@@ -74,5 +103,15 @@ class FP8LinearTransform(Transform):
         self.n_converted = n
         if not n:
             return prologue_trace, computation_trace, epilogue_trace
-        new.set_provenance(TraceProvenance(f"FP8 linear ({n} linears -> e4m3/e5m2 GEMMs)"))
+        if delayed:
+            from ..ops.fp8 import new_delayed_state
+
+            self.state_key = key = new_delayed_state(self.recipe, len(slots))
+            for i in sites:
+                b = new.bound_symbols[i]
+                new.bound_symbols[i] = b.from_bsym(args=b.args[:3] + (key,) + b.args[4:])
+            upd = fp8_delayed_update.bind(key, output=None)
+            new.bound_symbols.insert(0, upd)
+        what = f"{self.recipe!r}" if delayed else "current scaling"
+        new.set_provenance(TraceProvenance(f"FP8 linear ({n} linears -> e4m3/e5m2 GEMMs, {what})"))
         return prologue_trace, new, epilogue_trace

@@ -47,7 +47,7 @@ def _is_unpack(b) -> bool:
 
 
 def default_capturable(bsym: BoundSymbol, *, capture_collectives: bool = False) -> bool:
-    if bsym.sym.id in _NOT_CAPTURABLE_IDS or _is_unpack(bsym):
+    if bsym.sym.id in _NOT_CAPTURABLE_IDS or _is_unpack(bsym) or getattr(bsym.sym, "not_capturable", False):
         return False
     if not capture_collectives and (getattr(bsym.sym, "module", None) == "dist_prims"
                                     or (isinstance(bsym.sym.id, str) and bsym.sym.id.startswith("dist."))):

@@ -279,6 +279,38 @@ def test_fp8_linear_training_close_to_bf16():
 
 
 @pytest.mark.gpu
+def test_fp8_delayed_scaling_training():
+    """DelayedScaling recipe: scales come from the amax history of earlier steps (recorded while
+    casting); results stay close to bf16 over several steps, siblings share the x slot, and the
+    history advances once per forward."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling, delayed_state
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 1024), torch.nn.GELU(), torch.nn.Linear(1024, 512)).cuda().bfloat16()
+    t = FP8LinearTransform(recipe=DelayedScaling(amax_history_len=4))
+    jm = thunder.jit(m, transforms=[t])
+    for step in range(4):
+        x = torch.randn(4, 64, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        out = jm(x)
+        ref = m(x)
+        rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
+        assert rel < 0.08, (step, rel)
+        g = torch.randn_like(out)
+        gx, gw = torch.autograd.grad(out, (x, m[0].weight), g)
+        rx, rw = torch.autograd.grad(ref, (x, m[0].weight), g)
+        for a, b in ((gx, rx), (gw, rw)):
+            cos = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+            assert cos > 0.99, (step, cos)
+    st = delayed_state(t.state_key)
+    assert t.n_converted == 2 and st.n == 6 and st.updates == 3 and all(st.seen)  # the first forward has no history yet
+    torch.testing.assert_close(st.hmax[1], m[0].weight.detach().abs().max().float())
+    fw = str(thunder.last_traces(jm)[-1])
+    assert "hip_fp8_quantize_delayed" in fw and "hip_fp8_delayed_update" in fw
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols", [768, 2560, 1000])
 def test_layer_norm_kernel(dtype, cols):
