@@ -44,6 +44,8 @@ def parse_args():
                         "e.g. --model Llama-3-8B --parallel tp; strong scaling)")
     p.add_argument("--executors", default=None, help="comma separated executor names (default: framework defaults)")
     p.add_argument("--fp8", action="store_true")
+    p.add_argument("--fp8-recipe", default="current", choices=["current", "delayed", "mxfp8"],
+                   help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling) or MXFP8 blocks")
     p.add_argument("--hipgraph", action="store_true")
     p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
     p.add_argument("--eager-baseline", action="store_true", help="also time PyTorch eager (1 GPU) for speedup")
@@ -103,7 +105,7 @@ def run(args, rank, world, device, mode):
         if args.fp8:
             from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
 
-            transforms.append(FP8LinearTransform())
+            transforms.append(FP8LinearTransform(recipe=args.fp8_recipe))
 
         class TrainStep(torch.nn.Module):
             """Model + loss in one compiled program so the fused cross-entropy kernel is used."""
@@ -237,7 +239,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if data_parallel else "strong",
             "vs_baseline": round(per_gpu / base, 4) if data_parallel else None,  # no published TP number
-            "dtype": "fp8" if args.fp8 else "bf16",
+            "dtype": (f"fp8 ({args.fp8_recipe} scaling) linears, bf16 elsewhere" if args.fp8 else "bf16"),
             "data": "synthetic token ids, random-init weights",
             "config": {
                 "model": args.model + ("" if args.n_layer is None else f"-{args.n_layer}L(debug)"),

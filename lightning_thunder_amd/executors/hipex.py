@@ -138,6 +138,56 @@ hip_fp8_delayed_update = ex.register_operator("hip_fp8_delayed_update", meta=lam
 hip_fp8_delayed_update.not_capturable = True  # may all-reduce over the data-parallel group
 
 
+def _mx_quant_meta(t, e5m2):
+    C = t.shape[-1]
+    R = 1
+    for d in t.shape[:-1]:
+        R *= d
+    u8 = torch.uint8
+    mk = lambda shape: TensorProxy(like=t, shape=shape, dtype=u8, requires_grad=False)  # noqa: E731
+    return mk((R, C)), mk((R, C // 32)), mk((C, R)), mk((C, R // 32))
+
+
+def _mx_quant_impl(t, e5m2):
+    from ..ops.fp8 import mx_quantize
+
+    return mx_quantize(t, e5m2)
+
+
+def _mx_gemm_meta(qa, sa, qb, sb, fmt_a, fmt_b, bias, out_shape):
+    return TensorProxy(like=qa, shape=tuple(out_shape), dtype=torch.bfloat16)
+
+
+def _mx_gemm_impl(qa, sa, qb, sb, fmt_a, fmt_b, bias, out_shape):
+    from ..ops.fp8 import gemm_nt_mx
+
+    return gemm_nt_mx(qa, sa, qb, sb, fmt_a, fmt_b, bias).reshape(out_shape)
+
+
+# MXFP8: one pass emits both orientations with their 32-block E8M0 scales; the GEMM feeds the scales
+# to the block-scaled MFMA per lane
+hip_mx_quantize = ex.register_operator("hip_mx_quantize", meta=_mx_quant_meta, fn=_mx_quant_impl)
+hip_mx_gemm = ex.register_operator("hip_mx_gemm", meta=_mx_gemm_meta, fn=_mx_gemm_impl)
+
+
+def _mx_vjp(x, w, bias=None):
+    from .. import torch as ltorch
+
+    qx, sx, qxT, sxT = hip_mx_quantize(x, False)
+    qw, sw, qwT, swT = hip_mx_quantize(w, False)
+    y = hip_mx_gemm(qx, sx, qw, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
+
+    def bwd(g):
+        qg, sg, qgT, sgT = hip_mx_quantize(g, True)
+        dx = hip_mx_gemm(qg, sg, qwT, swT, 1, 0, None, tuple(x.shape))
+        dw = hip_mx_gemm(qgT, sgT, qxT, sxT, 1, 0, None, tuple(w.shape))
+        if bias is None:
+            return dx, dw
+        return dx, dw, ltorch.sum(g, tuple(range(g.ndim - 1)))
+
+    return y, bwd
+
+
 def _quant(t, e5m2, key, slot):
     if key is None:
         return hip_fp8_quantize(t, e5m2)
@@ -147,6 +197,8 @@ def _quant(t, e5m2, key, slot):
 def _fp8_vjp(x, w, bias=None, key=None, slots=None):
     from .. import torch as ltorch
 
+    if key == "mxfp8":
+        return _mx_vjp(x, w, bias)
     sl = slots or (None, None, None)
     qx, qxT, sx = _quant(x, False, key, sl[0])
     qw, qwT, sw = _quant(w, False, key, sl[1])
@@ -166,6 +218,10 @@ def _fp8_vjp(x, w, bias=None, key=None, slots=None):
 
 
 def _fp8_exec(x, w, bias=None, key=None, slots=None):
+    if key == "mxfp8":
+        qx, sx, _, _ = hip_mx_quantize(x, False)
+        qw, sw, _, _ = hip_mx_quantize(w, False)
+        return hip_mx_gemm(qx, sx, qw, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
     sl = slots or (None, None, None)
     qx, _, sx = _quant(x, False, key, sl[0])
     qw, _, sw = _quant(w, False, key, sl[1])

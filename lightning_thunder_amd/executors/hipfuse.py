@@ -4,9 +4,10 @@ Reference parity:
 * ``FusionExecutor.fusion_pass`` — ``thunder/executors/nvfuserex_impl.py:794-915`` (flatten
   claimed bound symbols, partition, build fusion regions, name them ``nvFusionN``).
 * partitioners — ``thunder/executors/data_dependent_partition.py`` (``consecutive`` /
-  ``dataflow``).  Here a single dataflow partitioner is used: a Kahn toposort inside each
-  side-effect-free segment that keeps scheduling ready bound symbols into the open region
-  as long as the region's iteration domain admits them (see ``hipfuse_codegen.Plan``).
+  ``dataflow``).  The default is dataflow: a Kahn toposort inside each side-effect-free segment
+  that keeps scheduling ready bound symbols into the open region as long as the region's
+  iteration domain admits them (see ``hipfuse_codegen.Plan``); compile option
+  ``fusion_type="consecutive"`` admits only the next bound symbol in program order.
 * optimization fuel — ``THUNDER_HIPFUSE_FUEL`` bounds the number of regions created.
 
 Each region becomes one ``hipFusionN`` callable: Python generates HIP source per call
@@ -377,10 +378,19 @@ def _schedule_segment(seg: list, used_outside: set | None = None) -> list:
         add_to_group(extra + [i])
         return True
 
+    from ..common import get_compile_option
+
+    fusion_type = get_compile_option(
+        "fusion_type", "hipfuse partitioner: 'dataflow' (default: any ready, connected bound symbol may join the "
+        "open region) or 'consecutive' (only the next bound symbol in program order)", "dataflow")
+    if fusion_type not in ("dataflow", "consecutive"):
+        raise ValueError(f"fusion_type must be 'dataflow' or 'consecutive', got {fusion_type!r}")
+    consecutive = fusion_type == "consecutive"
+
     while ready:
         pick = None
         if plan is not None:
-            for i in sorted(ready):
+            for i in (sorted(ready)[:1] if consecutive else sorted(ready)):
                 if fusible[i] and (_connected(names, ins, seg[i]) or _external_view(names, seg[i]) or
                                    any(d in in_group or _connected(names, ins, seg[d]) for d in lazy_deps[i])) \
                         and try_admit(i):

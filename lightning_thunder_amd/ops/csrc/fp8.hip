@@ -122,6 +122,101 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const T* __restrict
   if ((threadIdx.x & 63) == 0 && amax != nullptr) atomic_max_pos(amax, m);
 }
 
+// ---------------------------------------------------------------------------------------------
+// MXFP8 (OCP microscaling): blocks of 32 consecutive elements along the GEMM reduction dim share one
+// E8M0 scale X = 2^ceil(log2(amax_block / fp8_max)) (the OCP floor(log2 amax) - emax choice
+// saturates blocks whose amax mantissa exceeds 1.75; rounding the exponent up never clips);
+// elements are x / X in fp8.  One 64x64 tile pass emits both orientations the training GEMMs read:
+// q [R, C] with scales s [R, C/32] (blocks along C) and q^T [C, R] with s^T [C, R/32] (blocks along
+// R), so fprop, dgrad and wgrad all reduce over 32-blocks of their own K.
+// ---------------------------------------------------------------------------------------------
+template <bool E5M2>
+__device__ __forceinline__ uint32_t mx_exp(float amax) {
+  // biased E8M0 exponent of the block scale: the smallest 2^s with amax / 2^s <= fp8 max
+  // (fp8 max = 1.75 * 2^emax), so no element saturates; amax == 0 -> 2^-127 (the block is zeros)
+  if (!(amax > 0.f)) return 0u;
+  const uint32_t bits = __float_as_uint(amax);
+  const int e = (int)((bits >> 23) & 0xff) - 127;        // floor(log2(amax)) for a normal amax
+  const bool above = (bits & 0x7fffff) > 0x600000u;     // mantissa > 1.75
+  const int s = e - (E5M2 ? 15 : 8) + (above ? 1 : 0);
+  return (uint32_t)min(max(s + 127, 0), 254);
+}
+
+template <bool E5M2>
+__device__ __forceinline__ uint32_t mx_q(float v, float inv) {
+  return E5M2 ? to_e5m2(v * inv) : to_e4m3(v * inv);
+}
+
+__device__ __forceinline__ float e8m0_inv(uint32_t be) {
+  // 2^-(be - 127) exactly (be in [0, 254])
+  const int f = 254 - (int)be;  // float exponent field of 2^(127 - be)
+  return __uint_as_float(f > 0 ? (uint32_t)f << 23 : 0x00400000u);  // be = 254: 2^-127 (subnormal)
+}
+
+template <typename T, bool E5M2>
+__global__ __launch_bounds__(256) void mx_cast_transpose_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
+                                                                uint8_t* __restrict__ sq, uint8_t* __restrict__ qt,
+                                                                uint8_t* __restrict__ sqt, int R, int C) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x, tr = t >> 2, tq = t & 3;  // row (or column) tr, 16-element segment tq
+  // ---- rowwise: thread owns x[r0+tr][c0 + 16 tq .. +16]; blocks of 32 = segments (0,1), (2,3) ----
+  float v[16];
+  {
+    const T* src = x + (int64_t)(r0 + tr) * C + c0 + tq * 16;
+    const Vec16<T> a = load16(src), b = load16(src + 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = to_f32(a.v[j]);
+      v[8 + j] = to_f32(b.v[j]);
+    }
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    m = fmaxf(m, fabsf(v[j]));
+    tile[tr][tq * 16 + j] = v[j];
+  }
+  m = fmaxf(m, __shfl_xor(m, 1));
+  {
+    const uint32_t be = mx_exp<E5M2>(m);
+    const float inv = e8m0_inv(be);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= mx_q<E5M2>(v[j], inv) << (8 * (j & 3));
+    *reinterpret_cast<uint4*>(q + (int64_t)(r0 + tr) * C + c0 + tq * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    if ((tq & 1) == 0) sq[(int64_t)(r0 + tr) * (C / 32) + c0 / 32 + (tq >> 1)] = (uint8_t)be;
+  }
+  __syncthreads();
+  // ---- columnwise: thread owns column c0+tr, rows r0 + 16 tq .. +16 -> q^T[c0+tr][r0 + 16 tq ..] ----
+  m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    v[j] = tile[tq * 16 + j][tr];
+    m = fmaxf(m, fabsf(v[j]));
+  }
+  m = fmaxf(m, __shfl_xor(m, 1));
+  {
+    const uint32_t be = mx_exp<E5M2>(m);
+    const float inv = e8m0_inv(be);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= mx_q<E5M2>(v[j], inv) << (8 * (j & 3));
+    *reinterpret_cast<uint4*>(qt + (int64_t)(c0 + tr) * R + r0 + tq * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    if ((tq & 1) == 0) sqt[(int64_t)(c0 + tr) * (R / 32) + r0 / 32 + (tq >> 1)] = (uint8_t)be;
+  }
+}
+
+// one wave, 16x16x128 block-scaled MFMA with per-lane E8M0 scale registers (scale-operand probe)
+__global__ void mfma_scale_probe_kernel(const v8i* __restrict__ a, const v8i* __restrict__ b,
+                                        const int* __restrict__ sa, const int* __restrict__ sb,
+                                        f32x4* __restrict__ c) {
+  const int l = threadIdx.x;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 0, 0, 0, sa[l], 0, sb[l]);
+  c[l] = acc;
+}
+
 // one wave: C = A . B^T for a 16x16x128 tile from raw per-lane registers (layout probe)
 __global__ void mfma_probe_kernel(const v8i* __restrict__ a, const v8i* __restrict__ b, f32x4* __restrict__ c,
                                   int fmt_a, int fmt_b) {
@@ -195,6 +290,34 @@ LTA_EXPORT int lta_fp8_cast_transpose(int in_dtype, int e5m2, const void* x, voi
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// x [R, C] -> q [R, C] + s [R, C/32] and q^T [C, R] + s^T [C, R/32] (MXFP8); R, C multiples of 64.
+LTA_EXPORT int lta_mx_cast_transpose(int in_dtype, int e5m2, const void* x, void* q, void* s, void* qt, void* st, int R,
+                                     int C, hipStream_t stream) {
+  if (R % 64 || C % 64) return -2;
+  dim3 grid(C / 64, R / 64), block(256);
+#define LTA_MX(T, E5)                                                                                             \
+  hipLaunchKernelGGL((mx_cast_transpose_kernel<T, E5>), grid, block, 0, stream, (const T*)x, (uint8_t*)q,          \
+                     (uint8_t*)s, (uint8_t*)qt, (uint8_t*)st, R, C)
+  if (in_dtype == kBF16) {
+    if (e5m2) LTA_MX(__hip_bfloat16, true);
+    else LTA_MX(__hip_bfloat16, false);
+  } else if (in_dtype == kF32) {
+    if (e5m2) LTA_MX(float, true);
+    else LTA_MX(float, false);
+  } else {
+    return -1;
+  }
+#undef LTA_MX
+  return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_fp8_mfma_scale_probe(const void* a, const void* b, const void* sa, const void* sb, void* c,
+                                        hipStream_t s) {
+  hipLaunchKernelGGL(mfma_scale_probe_kernel, dim3(1), dim3(64), 0, s, (const v8i*)a, (const v8i*)b, (const int*)sa,
+                     (const int*)sb, (f32x4*)c);
   return (int)hipGetLastError();
 }
 

@@ -420,7 +420,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_8ph_kernel(const __hip_b
 // 2x the bf16 rate).  Same geometry and LDS image as the bf16 kernel: BK = 128 fp8 = 128-B rows,
 // so staging (glds) and the XOR swizzle are byte-identical.  Per-tensor scaling: the operands
 // hold x * s_x; the MFMA block scales are 1.0 and alpha = 1 / (s_a * s_b) is applied in the
-// epilogue.  Lane l holds A[row l&15][k = 32 (l>>4) .. +32] (two 16-B LDS reads).
+// epilogue.  Operand k order of the 16x16x128 f8 MFMA (measured, scripts/mx_debug.py): lane group
+// g = l>>4 holds k = 16g..16g+15 in its first 16 bytes and k = 64+16g..+15 in its last 16, and the
+// E8M0 scale of lane group g applies to k-block g (k = 32g..32g+31) of its row; so lane l reads
+// 16-B chunks g and 4+g of the K-step's 128-B row.
 // ---------------------------------------------------------------------------------------------
 typedef int v8i __attribute__((ext_vector_type(8)));
 
@@ -449,13 +452,23 @@ __device__ __forceinline__ f32x4 mfma_fp8(const v8i& a, const v8i& b, const f32x
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
 }
 
-template <int FA, int FB, bool BIAS>
+// MXFP8: the E8M0 scale in byte 0 of lane l's scale register applies to k-block l>>4 of row l&15
+// (lta_fp8_mfma_scale_probe and the k order above pin this)
+template <int FA, int FB>
+__device__ __forceinline__ f32x4 mfma_mx(const v8i& a, const v8i& b, const f32x4& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, sa, 0, sb);
+}
+
+// MX = true: block-scaled operands; SA [M][K/32] / SB [N][K/32] E8M0 scales (sa / sb unused)
+template <int FA, int FB, bool BIAS, bool MX = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                              __hip_bfloat16* __restrict__ C,
                                                              const __hip_bfloat16* __restrict__ bias, int M, int N,
                                                              int K, int lda, int ldb, int ldc,
                                                              const float* __restrict__ sa,
-                                                             const float* __restrict__ sb) {
+                                                             const float* __restrict__ sb,
+                                                             const uint8_t* __restrict__ SA = nullptr,
+                                                             const uint8_t* __restrict__ SB = nullptr) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -479,38 +492,70 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BKB;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ksc = K / 32;  // scale columns
+  int scA[8], scB[4], nxA[8], nxB[4];  // this / next K-step's per-lane scales (MX)
+  auto load_scales = [&](int t, int* a_, int* b_) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      a_[m] = *reinterpret_cast<const int*>(SA + (int64_t)(m0 + wm * 128 + m * 16 + fr) * ksc + t * 4);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      b_[n] = *reinterpret_cast<const int*>(SB + (int64_t)(n0 + wn * 64 + n * 16 + fr) * ksc + t * 4);
+  };
+  if constexpr (MX) load_scales(0, scA, scB);
   stage_tile_bytes(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int fr = lane & 15, fq = lane >> 4;
   for (int t = 0; t < nk; ++t) {
     char* cur = smem + (t & 1) * STAGE_BYTES;
-    if (t + 1 < nk) stage_tile_bytes(A, B, lda, ldb, m0, n0, (t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+    if (t + 1 < nk) {
+      stage_tile_bytes(A, B, lda, ldb, m0, n0, (t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+      if constexpr (MX) load_scales(t + 1, nxA, nxB);
+    }
     v8i af[8], bfr[4];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = wm * 128 + m * 16 + fr;
-      const uint4 lo = *reinterpret_cast<const uint4*>(cur + row * 128 + (((2 * fq) ^ (row & 7)) << 4));
-      const uint4 hi = *reinterpret_cast<const uint4*>(cur + row * 128 + (((2 * fq + 1) ^ (row & 7)) << 4));
+      const uint4 lo = *reinterpret_cast<const uint4*>(cur + row * 128 + ((fq ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(cur + row * 128 + (((4 + fq) ^ (row & 7)) << 4));
       af[m] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int row = wn * 64 + n * 16 + fr;
       const char* base = cur + TILE_BYTES + row * 128;
-      const uint4 lo = *reinterpret_cast<const uint4*>(base + (((2 * fq) ^ (row & 7)) << 4));
-      const uint4 hi = *reinterpret_cast<const uint4*>(base + (((2 * fq + 1) ^ (row & 7)) << 4));
+      const uint4 lo = *reinterpret_cast<const uint4*>(base + ((fq ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(base + (((4 + fq) ^ (row & 7)) << 4));
       bfr[n] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
+    if constexpr (MX) {
+      int ea[8], eb[4];
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < 8; ++m) ea[m] = (scA[m] >> (8 * fq)) & 0xff;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = mfma_fp8<FA, FB>(af[m], bfr[n], acc[m][n]);
+      for (int n = 0; n < 4; ++n) eb[n] = (scB[n] >> (8 * fq)) & 0xff;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma_mx<FA, FB>(af[m], bfr[n], acc[m][n], ea[m], eb[n]);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma_fp8<FA, FB>(af[m], bfr[n], acc[m][n]);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (MX) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) scA[m] = nxA[m];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) scB[n] = nxB[n];
+    }
   }
 
-  const float alpha = 1.f / (*sa * *sb);
+  const float alpha = MX ? 1.f : 1.f / (*sa * *sb);
   char* wbuf = smem + wave * (128 * 128);
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -695,6 +740,26 @@ LTA_EXPORT int lta_gemm_nt_fp8(const void* A, const void* B, void* C, const void
   else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_F8(0, 1, true); else LTA_F8(0, 1, false); }
   else return -1;
 #undef LTA_F8
+  return (int)hipGetLastError();
+}
+
+// MXFP8: C[M,N] (bf16) = A . B^T with E8M0 block scales SA [M][K/32], SB [N][K/32] (+ bias);
+// A [M,K], B [N,K] fp8 (fmt 0 = e4m3fn, 1 = e5m2), M, N % 256 == 0, K % 128 == 0.
+LTA_EXPORT int lta_gemm_nt_mxfp8(const void* A, const void* B, void* C, const void* bias, const void* SA, const void* SB,
+                                 int M, int N, int K, int lda, int ldb, int ldc, int fmt_a, int fmt_b,
+                                 hipStream_t stream) {
+  if (M % BM || N % BN || K % 128) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_MX8(FA, FB, BI)                                                                                      \
+  hipLaunchKernelGGL((gemm_nt_fp8_kernel<FA, FB, BI, true>), grid, block, 0, stream, (const char*)A,              \
+                     (const char*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias, M, N, K, lda, ldb, ldc,       \
+                     (const float*)nullptr, (const float*)nullptr, (const uint8_t*)SA, (const uint8_t*)SB)
+  const bool bi = bias != nullptr;
+  if (fmt_a == 0 && fmt_b == 0) { if (bi) LTA_MX8(0, 0, true); else LTA_MX8(0, 0, false); }
+  else if (fmt_a == 1 && fmt_b == 0) { if (bi) LTA_MX8(1, 0, true); else LTA_MX8(1, 0, false); }
+  else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_MX8(0, 1, true); else LTA_MX8(0, 1, false); }
+  else return -1;
+#undef LTA_MX8
   return (int)hipGetLastError();
 }
 

@@ -210,3 +210,68 @@ def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
         amax_into(t2, amax_in)
     q, qT = cast_transpose(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=st.cur[slot])
     return q, qT, scale
+
+
+# ---------------------------------------------------------------------------------------------
+# MXFP8 block scaling (reference: TE ``MXFP8BlockScaling``; CDNA4 runs it natively on
+# v_mfma_scale_f32_16x16x128_f8f6f4 with per-32-element E8M0 scales)
+# ---------------------------------------------------------------------------------------------
+register_signature("lta_mx_cast_transpose", [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                             c_int, c_void_p])
+register_signature("lta_gemm_nt_mxfp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                         c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+register_signature("lta_fp8_mfma_scale_probe", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+
+MX_BLOCK = 32
+
+
+class MXFP8BlockScaling:
+    """OCP MX: every 32 consecutive elements along a GEMM's reduction dim share one E8M0 scale;
+    e4m3 for activations / weights, e5m2 for gradients (no history, no amax all-reduce)."""
+
+    def __repr__(self):
+        return "MXFP8BlockScaling()"
+
+
+def mx_quantize(t: torch.Tensor, e5m2: bool = False):
+    """t [..., C] -> (q [R, C], s [R, C/32], q^T [C, R], s^T [C, R/32]): fp8 as uint8, E8M0 scales as
+    uint8; blocks along C for q, along R for q^T (each is the reduction dim of the GEMM reading it)."""
+    lib = require()
+    t2 = t.reshape(-1, t.shape[-1])
+    R, C = t2.shape
+    u8 = dict(dtype=torch.uint8, device=t.device)
+    q, s, qt, st = (torch.empty((R, C), **u8), torch.empty((R, C // MX_BLOCK), **u8), torch.empty((C, R), **u8),
+                    torch.empty((C, R // MX_BLOCK), **u8))
+    check(lib.lta_mx_cast_transpose(DTYPE_CODE[t2.dtype], int(e5m2), t2.data_ptr(), q.data_ptr(), s.data_ptr(),
+                                    qt.data_ptr(), st.data_ptr(), R, C, stream_ptr(t.device)), "lta_mx_cast_transpose")
+    return q, s, qt, st
+
+
+def mx_dequantize(q: torch.Tensor, s: torch.Tensor, e5m2: bool = False) -> torch.Tensor:
+    """Reference dequantisation (fp32) of an MX-quantised [R, C] tensor (tests / debugging)."""
+    f = (torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn)
+    x = q.view(f).float().reshape(q.shape[0], -1, MX_BLOCK)
+    scale = torch.exp2(s.float() - 127.0).unsqueeze(-1)
+    return (x * scale).reshape(q.shape)
+
+
+def gemm_nt_mx(a: torch.Tensor, sa: torch.Tensor, b: torch.Tensor, sb: torch.Tensor, fmt_a: int = 0, fmt_b: int = 0,
+               bias: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 [M, N] = a [M,K] . b [N,K]^T with E8M0 block scales sa [M, K/32], sb [N, K/32]."""
+    lib = require()
+    M, K = a.shape
+    N = b.shape[0]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    check(lib.lta_gemm_nt_mxfp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), None if bias is None else bias.data_ptr(),
+                                sa.data_ptr(), sb.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0), fmt_a,
+                                fmt_b, stream_ptr(a.device)), "lta_gemm_nt_mxfp8")
+    return out
+
+
+def mfma_scale_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) with per-lane operand/scale registers:
+    a, b [64, 32] uint8, sa, sb [64] int32 -> [64, 4] fp32 accumulator registers."""
+    c = torch.empty((64, 4), dtype=torch.float32, device=a.device)
+    check(require().lta_fp8_mfma_scale_probe(a.data_ptr(), b.data_ptr(), sa.data_ptr(), sb.data_ptr(), c.data_ptr(),
+                                             stream_ptr(a.device)), "lta_fp8_mfma_scale_probe")
+    return c

@@ -53,14 +53,18 @@ def eligible(x, w, bias=None, key=None, slots=None) -> bool:
 class FP8LinearTransform(Transform):
     """``recipe``: ``"current"`` (per-tensor current scaling: one amax pass per cast), ``"delayed"``
     or a :class:`~lightning_thunder_amd.ops.fp8.DelayedScaling` (amax history, scales from earlier
-    steps, amax all-reduced over the data-parallel group; reference TE ``DelayedScaling``)."""
+    steps, amax all-reduced over the data-parallel group; reference TE ``DelayedScaling``), or
+    ``"mxfp8"`` / :class:`~lightning_thunder_amd.ops.fp8.MXFP8BlockScaling` (E8M0 scale per 32
+    elements of each GEMM's reduction dim, on the block-scaled MFMA; reference TE ``MXFP8BlockScaling``)."""
 
     def __init__(self, recipe="current", amax_history_len: int = 16, skip: tuple[str, ...] = ()):
-        from ..ops.fp8 import DelayedScaling
+        from ..ops.fp8 import DelayedScaling, MXFP8BlockScaling
 
         if recipe == "delayed":
             recipe = DelayedScaling(amax_history_len=amax_history_len)
-        if not (recipe == "current" or isinstance(recipe, DelayedScaling)):
+        elif recipe == "mxfp8":
+            recipe = MXFP8BlockScaling()
+        if not (recipe == "current" or isinstance(recipe, (DelayedScaling, MXFP8BlockScaling))):
             raise ValueError(f"unknown FP8 recipe {recipe!r}")
         self.recipe = recipe
         self.amax_history_len = amax_history_len
@@ -74,9 +78,12 @@ class FP8LinearTransform(Transform):
         new = from_trace(computation_trace)
         new.bound_symbols = []
         new.scopes = [new.bound_symbols]
+        from ..ops.fp8 import MXFP8BlockScaling
+
         swap: dict = {}
         n = 0
-        delayed = self.recipe != "current"
+        mx = isinstance(self.recipe, MXFP8BlockScaling)
+        delayed = self.recipe != "current" and not mx
         slots: dict = {}  # ("x"|"w", proxy name) / ("dy", site) -> history slot; siblings reading one x share it
 
         def slot(k):
@@ -94,6 +101,8 @@ class FP8LinearTransform(Transform):
                             sl = (slot(("x", x.name)), slot(("w", w.name)), slot(("dy", n)))
                             sites.append(len(new.bound_symbols))
                             y = fp8_linear(x, w, bias, -1, sl)  # key patched below (slot count known last)
+                        elif mx:
+                            y = fp8_linear(x, w, bias, "mxfp8")
                         else:
                             y = fp8_linear(x, w, bias)
                         swap[b.output.name] = y
@@ -112,6 +121,6 @@ class FP8LinearTransform(Transform):
                 new.bound_symbols[i] = b.from_bsym(args=b.args[:3] + (key,) + b.args[4:])
             upd = fp8_delayed_update.bind(key, output=None)
             new.bound_symbols.insert(0, upd)
-        what = f"{self.recipe!r}" if delayed else "current scaling"
+        what = "current scaling" if self.recipe == "current" else f"{self.recipe!r}"
         new.set_provenance(TraceProvenance(f"FP8 linear ({n} linears -> e4m3/e5m2 GEMMs, {what})"))
         return prologue_trace, new, epilogue_trace

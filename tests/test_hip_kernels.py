@@ -279,6 +279,97 @@ def test_fp8_linear_training_close_to_bf16():
 
 
 @pytest.mark.gpu
+def test_mfma_scale_operand_is_per_lane_block():
+    """Pins the block-scaled MFMA's scale operand: lane l's E8M0 byte (opsel 0) scales lane l's 32
+    operand bytes = row l&15, k-block l>>4 of the 16x16x128 tile (what the MXFP8 GEMM relies on)."""
+    from lightning_thunder_amd.ops.fp8 import mfma_scale_probe
+
+    ones = torch.full((64, 32), 0x38, dtype=torch.uint8, device="cuda")  # e4m3fn 1.0
+    la = torch.arange(64, device="cuda")
+    ea = 127 + (la % 5) - 2
+    eb = 127 + (la % 3) - 1
+    c = mfma_scale_probe(ones, ones, ea.int(), eb.int()).cpu()
+    ea, eb = ea.cpu().double() - 127, eb.cpu().double() - 127
+    exp = torch.zeros(16, 16, dtype=torch.float64)
+    for i in range(16):
+        for j in range(16):
+            exp[i, j] = sum(32 * 2 ** ea[b * 16 + i] * 2 ** eb[b * 16 + j] for b in range(4))
+    got = torch.zeros(16, 16, dtype=torch.float64)
+    for l in range(64):
+        for r in range(4):
+            got[(l >> 4) * 4 + r, l & 15] = c[l, r]
+    torch.testing.assert_close(got, exp)
+
+
+def _mx_reference(x: torch.Tensor, e5m2: bool):
+    """Pure-torch OCP MX quantisation along the last dim (blocks of 32): (q bytes, E8M0 bytes)."""
+    R, C = x.shape
+    xb = x.float().reshape(R, C // 32, 32)
+    amax = xb.abs().amax(-1)
+    m, e = torch.frexp(amax)  # amax = m 2^e, m in [0.5, 1): floor(log2 amax) = e - 1
+    emax = 15 if e5m2 else 8
+    up = (m > 0.875).to(e.dtype)  # mantissa above fp8 max's 1.75: next power of two (no clipping)
+    be = torch.where(amax > 0, (e - 1 - emax + up + 127).clamp(0, 254), torch.zeros_like(e))
+    fmax, f8 = (57344.0, torch.float8_e5m2) if e5m2 else (448.0, torch.float8_e4m3fn)
+    q = (xb * torch.exp2(127.0 - be.float()).unsqueeze(-1)).clamp(-fmax, fmax).to(f8)
+    return q.reshape(R, C).view(torch.uint8), be.to(torch.uint8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e5m2", [False, True])
+def test_mx_quantize_matches_reference(e5m2):
+    from lightning_thunder_amd.ops.fp8 import mx_quantize
+
+    torch.manual_seed(0)
+    x = (torch.randn(256, 512, device="cuda") * torch.logspace(-3, 3, 512, device="cuda")).bfloat16()
+    x[:, :32] = 0  # an all-zero block
+    q, s, qt, st = mx_quantize(x, e5m2)
+    rq, rs = _mx_reference(x, e5m2)
+    rqt, rst = _mx_reference(x.t().contiguous(), e5m2)
+    assert torch.equal(s, rs) and torch.equal(st, rst)
+    assert (q != rq).float().mean() < 1e-3 and (qt != rqt).float().mean() < 1e-3
+
+
+@pytest.mark.gpu
+def test_gemm_nt_mxfp8():
+    from lightning_thunder_amd.ops.fp8 import mx_quantize, mx_dequantize, gemm_nt_mx
+
+    torch.manual_seed(0)
+    a = (torch.randn(512, 1024, device="cuda") * torch.logspace(-2, 2, 1024, device="cuda")).bfloat16()
+    b = torch.randn(768, 1024, device="cuda").bfloat16()
+    bias = torch.randn(768, device="cuda").bfloat16()
+    qa, sa, _, _ = mx_quantize(a)
+    qb, sb, _, _ = mx_quantize(b, True)
+    out = gemm_nt_mx(qa, sa, qb, sb, 0, 1, bias).float()
+    ref = mx_dequantize(qa, sa) @ mx_dequantize(qb, sb, True).t() + bias.float()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
+def test_fp8_mxfp8_training_close_to_bf16():
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 1024), torch.nn.GELU(), torch.nn.Linear(1024, 512)).cuda().bfloat16()
+    t = FP8LinearTransform(recipe="mxfp8")
+    jm = thunder.jit(m, transforms=[t])
+    x = torch.randn(4, 64, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    out = jm(x)
+    assert t.n_converted == 2 and "hip_mx_gemm" in str(thunder.last_traces(jm)[-1])
+    ref = m(x)
+    rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
+    assert rel < 0.06, rel
+    g = torch.randn_like(out)
+    gx, gw = torch.autograd.grad(out, (x, m[0].weight), g)
+    rx, rw = torch.autograd.grad(ref, (x, m[0].weight), g)
+    for a, b in ((gx, rx), (gw, rw)):
+        cos = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+        assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
 def test_fp8_delayed_scaling_training():
     """DelayedScaling recipe: scales come from the amax history of earlier steps (recorded while
     casting); results stay close to bf16 over several steps, siblings share the x slot, and the

@@ -91,6 +91,40 @@ def test_single_region_for_norm_chain(cpu_fusion):
     assert all(b.sym.name in ("python_return", "python_del", "unpack_trivial") for b in compute), [b.sym.name for b in compute]
 
 
+def test_fusion_type_consecutive_vs_dataflow(cpu_fusion):
+    """``fusion_type`` compile option (reference data_dependent_partition.py): 'consecutive' only
+    extends a region with the next bound symbol in program order, so two independent chains that
+    the program interleaves are not fused at all, while 'dataflow' fuses each chain."""
+    def f(a, b):
+        x = a.exp()
+        y = b.sin()  # interleaved, independent of x (different shape: cannot share x's region)
+        x = x * 2.0
+        y = y + 1.0
+        x = x.tanh()
+        y = y.cos()
+        return x, y
+
+    a, b = torch.randn(64, 32), torch.randn(16, 8)
+    counts = {}
+    for ft in ("dataflow", "consecutive"):
+        jf = thunder.jit(f, executors=["hipfuse", "torch"], fusion_type=ft)
+        out = jf(a, b)
+        for o, r in zip(out, f(a, b)):
+            torch.testing.assert_close(o, r)
+        counts[ft] = len(hipfuse.fusions(thunder.last_traces(jf)[-1]))
+    assert counts == {"dataflow": 2, "consecutive": 0}, counts
+
+    def g(a):
+        return a.exp().mul(2.0).tanh()
+
+    for ft in ("dataflow", "consecutive"):
+        jg = thunder.jit(g, executors=["hipfuse", "torch"], fusion_type=ft)
+        torch.testing.assert_close(jg(a), g(a))
+        assert len(hipfuse.fusions(thunder.last_traces(jg)[-1])) == 1
+    with pytest.raises(ValueError):
+        thunder.jit(f, executors=["hipfuse", "torch"], fusion_type="bogus")(a, b)
+
+
 @pytest.mark.skipif(not os.path.exists(LIB), reason="native library not built")
 @pytest.mark.parametrize("case", sorted(CASES))
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
