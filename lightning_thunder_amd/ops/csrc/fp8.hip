@@ -74,52 +74,68 @@ __global__ __launch_bounds__(256) void cast_kernel(const T* __restrict__ x, uint
     }
     *reinterpret_cast<uint2*>(y + i * 8) = make_uint2(lo, hi);
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && amax != nullptr) atomic_max_pos(amax, m);
+  if (amax != nullptr) {  // one atomic per workgroup
+    __shared__ float red[4];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
 }
 
-// x [R, C] row-major -> y [R, C] and yt [C, R] (64x64 tiles through LDS)
+// x [R, C] row-major -> y [R, C] and yt [C, R] (64x64 tiles through LDS).  A capped grid loops over
+// the tiles so the amax (delayed scaling) costs one atomic per workgroup, not one per tile-wave:
+// same-address atomics serialise (MI355X_MICROARCH.md, global atomics contention row).
 template <typename T, bool E5M2>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const T* __restrict__ x, uint8_t* __restrict__ y,
                                                              uint8_t* __restrict__ yt, int R, int C,
                                                              const float* __restrict__ amax_in, float fmax,
                                                              float* __restrict__ scale_out, float* __restrict__ amax) {
   __shared__ uint8_t tile[64][64 + 4];
+  __shared__ float red[4];
   const float s = dev_scale(amax_in, fmax, scale_out);
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tr = threadIdx.x / 8, tc = (threadIdx.x % 8) * 8;  // 32 rows x 8 chunks of 8 per pass
+  const int tiles_c = C / 64, ntiles = tiles_c * (R / 64);
   float m = 0.f;
+  for (int tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+    const int r0 = (tile_id / tiles_c) * 64, c0 = (tile_id % tiles_c) * 64;
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int r = tr + 32 * p;
-    const Vec16<T> v = load16(x + (int64_t)(r0 + r) * C + c0 + tc);
-    uint32_t lo = 0, hi = 0;
+    for (int p = 0; p < 2; ++p) {
+      const int r = tr + 32 * p;
+      const Vec16<T> v = load16(x + (int64_t)(r0 + r) * C + c0 + tc);
+      uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = to_f32(v.v[j]);
-      m = fmaxf(m, fabsf(f));
-      const uint32_t q = E5M2 ? to_e5m2(f * s) : to_e4m3(f * s);
-      tile[r][tc + j] = (uint8_t)q;
-      if (j < 4) lo |= q << (8 * j);
-      else hi |= q << (8 * (j - 4));
+      for (int j = 0; j < 8; ++j) {
+        const float f = to_f32(v.v[j]);
+        m = fmaxf(m, fabsf(f));
+        const uint32_t q = E5M2 ? to_e5m2(f * s) : to_e4m3(f * s);
+        tile[r][tc + j] = (uint8_t)q;
+        if (j < 4) lo |= q << (8 * j);
+        else hi |= q << (8 * (j - 4));
+      }
+      if (y != nullptr) *reinterpret_cast<uint2*>(y + (int64_t)(r0 + r) * C + c0 + tc) = make_uint2(lo, hi);
     }
-    if (y != nullptr) *reinterpret_cast<uint2*>(y + (int64_t)(r0 + r) * C + c0 + tc) = make_uint2(lo, hi);
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int c = tr + 32 * p;  // output row = input column
-    uint32_t lo = 0, hi = 0;
+    for (int p = 0; p < 2; ++p) {
+      const int c = tr + 32 * p;  // output row = input column
+      uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t q = tile[tc + j][c];
-      if (j < 4) lo |= q << (8 * j);
-      else hi |= q << (8 * (j - 4));
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t q = tile[tc + j][c];
+        if (j < 4) lo |= q << (8 * j);
+        else hi |= q << (8 * (j - 4));
+      }
+      *reinterpret_cast<uint2*>(yt + (int64_t)(c0 + c) * R + r0 + tc) = make_uint2(lo, hi);
     }
-    *reinterpret_cast<uint2*>(yt + (int64_t)(c0 + c) * R + r0 + tc) = make_uint2(lo, hi);
+    __syncthreads();  // the tile is rewritten by the next iteration
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && amax != nullptr) atomic_max_pos(amax, m);
+  if (amax != nullptr) {
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -234,7 +250,7 @@ __global__ void mfma_probe_kernel(const v8i* __restrict__ a, const v8i* __restri
 template <typename T, bool E5>
 static void launch_cast(const void* x, void* y, int64_t n, const void* amax_in, float fmax, void* scale_out,
                         void* amax, hipStream_t s) {
-  dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 4096)), block(256);
+  dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 1024)), block(256);
   hipLaunchKernelGGL((cast_kernel<T, E5>), grid, block, 0, s, (const T*)x, (uint8_t*)y, n, (const float*)amax_in, fmax,
                      (float*)scale_out, (float*)amax);
 }
@@ -242,7 +258,7 @@ static void launch_cast(const void* x, void* y, int64_t n, const void* amax_in, 
 template <typename T, bool E5>
 static void launch_cast_t(const void* x, void* y, void* yt, int R, int C, const void* amax_in, float fmax,
                           void* scale_out, void* amax, hipStream_t s) {
-  dim3 grid(C / 64, R / 64), block(256);
+  dim3 grid((unsigned)std::min<int64_t>((int64_t)(C / 64) * (R / 64), 1024)), block(256);
   hipLaunchKernelGGL((cast_transpose_kernel<T, E5>), grid, block, 0, s, (const T*)x, (uint8_t*)y, (uint8_t*)yt, R, C,
                      (const float*)amax_in, fmax, (float*)scale_out, (float*)amax);
 }

@@ -459,7 +459,9 @@ __device__ __forceinline__ f32x4 mfma_mx(const v8i& a, const v8i& b, const f32x4
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, sa, 0, sb);
 }
 
-// MX = true: block-scaled operands; SA [M][K/32] / SB [N][K/32] E8M0 scales (sa / sb unused)
+// MX = true: block-scaled operands; SA [M][K/32] / SB [N][K/32] E8M0 scales (sa / sb unused).  Each
+// K-step's scales (4 bytes per tile row: 256 A rows + 256 B rows) are staged into LDS by one 4-byte
+// global_load_lds per lane beside the operand tiles, and read back as single bytes.
 template <int FA, int FB, bool BIAS, bool MX = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                              __hip_bfloat16* __restrict__ C,
@@ -469,7 +471,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
                                                              const float* __restrict__ sb,
                                                              const uint8_t* __restrict__ SA = nullptr,
                                                              const uint8_t* __restrict__ SB = nullptr) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  constexpr int SCALE_BYTES = MX ? 2 * 256 * 4 : 0;  // per stage: A rows then B rows, 4 B each
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES + 2 * SCALE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -494,24 +497,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
   const int nk = K / BKB;
   const int fr = lane & 15, fq = lane >> 4;
   const int ksc = K / 32;  // scale columns
-  int scA[8], scB[4], nxA[8], nxB[4];  // this / next K-step's per-lane scales (MX)
-  auto load_scales = [&](int t, int* a_, int* b_) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-      a_[m] = *reinterpret_cast<const int*>(SA + (int64_t)(m0 + wm * 128 + m * 16 + fr) * ksc + t * 4);
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      b_[n] = *reinterpret_cast<const int*>(SB + (int64_t)(n0 + wn * 64 + n * 16 + fr) * ksc + t * 4);
+  char* const sc_base = smem + 2 * STAGE_BYTES;
+  auto stage_scales = [&](int t, int buf) {
+    // wave w: rows 64 (w & 3) + lane of A (w < 4) or B (w >= 4), the K-step's 4 scale bytes each
+    const int row = (wave & 3) * 64 + lane;
+    const uint8_t* src = wave < 4 ? SA + (int64_t)(m0 + row) * ksc + t * 4 : SB + (int64_t)(n0 + row) * ksc + t * 4;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sc_base + buf * SCALE_BYTES + wave * 256), 4, 0, 0);
   };
-  if constexpr (MX) load_scales(0, scA, scB);
   stage_tile_bytes(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
+  if constexpr (MX) stage_scales(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     char* cur = smem + (t & 1) * STAGE_BYTES;
     if (t + 1 < nk) {
       stage_tile_bytes(A, B, lda, ldb, m0, n0, (t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
-      if constexpr (MX) load_scales(t + 1, nxA, nxB);
+      if constexpr (MX) stage_scales(t + 1, (t + 1) & 1);
     }
     v8i af[8], bfr[4];
 #pragma unroll
@@ -530,11 +531,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
       bfr[n] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
     if constexpr (MX) {
+      const uint8_t* scs = reinterpret_cast<const uint8_t*>(sc_base + (t & 1) * SCALE_BYTES);
       int ea[8], eb[4];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) ea[m] = (scA[m] >> (8 * fq)) & 0xff;
+      for (int m = 0; m < 8; ++m) ea[m] = scs[(wm * 128 + m * 16 + fr) * 4 + fq];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) eb[n] = (scB[n] >> (8 * fq)) & 0xff;
+      for (int n = 0; n < 4; ++n) eb[n] = scs[1024 + (wn * 64 + n * 16 + fr) * 4 + fq];
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
@@ -547,12 +549,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if constexpr (MX) {
-#pragma unroll
-      for (int m = 0; m < 8; ++m) scA[m] = nxA[m];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) scB[n] = nxB[n];
-    }
   }
 
   const float alpha = MX ? 1.f : 1.f / (*sa * *sb);
