@@ -77,6 +77,40 @@ def _register_linear():
 _register_linear()
 
 
+# K2 GEMM for the prim matmul: the backward's dgrad (g @ W) and wgrad (g^T @ x) read their
+# transposed operands through the transposing LDS read (csrc/gemm.hip, MN-major images)
+def _mm_impl(a, b, residual=None):
+    from ..ops.gemm import matmul
+
+    return matmul(a, b, residual)
+
+
+def _mm_checker(a, b):
+    if not _gpu(a, b) or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or b.ndim != 2 or a.ndim < 2:
+        return False
+    M = 1
+    for s in a.shape[:-1]:
+        M *= s
+    K, N = b.shape
+    return a.shape[-1] == K and M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+
+
+def _mm_meta(a, b, residual=None):
+    return TensorProxy(like=a, shape=tuple(a.shape[:-1]) + (b.shape[1],))
+
+
+hip_matmul = ex.register_operator("hip_matmul", meta=_mm_meta, fn=_mm_impl)
+
+
+def _register_matmul():
+    from ..core import prims as P
+
+    ex.register_implementation(P.matmul, checker=_mm_checker, execution_transform=lambda a, b: hip_matmul(a, b))
+
+
+_register_matmul()
+
+
 # =========================================================================================
 # K8 FP8 linear (fwd/bwd on the block-scaled MFMA GEMM)
 # =========================================================================================
@@ -264,12 +298,22 @@ def _fuse_linear_epilogues(trace):
         for pos in (0, 1):
             y, r = b.args[pos], b.args[1 - pos]
             j = producer.get(y.name)
-            if j is None or j in drop or bsyms[j].sym is not hip_linear or uses.get(y.name, 0) != 1:
+            if j is None or j in drop or bsyms[j].sym not in (hip_linear, hip_matmul) or uses.get(y.name, 0) != 1:
                 continue
             lb = bsyms[j]
-            if len(lb.args) > 3 and lb.args[3] is not None:
-                continue
             if tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype or tuple(b.output.shape) != tuple(y.shape):
+                continue
+            if producer.get(r.name, -1) > j:
+                continue  # the residual is produced after the GEMM: the fused op could not see it
+            if lb.sym is hip_matmul:
+                if len(lb.args) > 2 and lb.args[2] is not None:
+                    continue
+                nb = hip_matmul.bind(lb.args[0], lb.args[1], r, output=b.output)
+                nb = ex.bind_call_ctx(nb)
+                replace[j] = nb  # computed where the GEMM was (the add's consumers come later)
+                drop.add(i)
+                break
+            if len(lb.args) > 3 and lb.args[3] is not None:
                 continue
             bias = lb.args[2] if len(lb.args) > 2 else lb.kwargs.get("bias")
             nb = hip_linear.bind(lb.args[0], lb.args[1], bias, r, output=b.output)
@@ -524,8 +568,56 @@ def _fuse_kv_cache_writes(trace):
     return new
 
 
+def _fuse_rms_bwd_residual(trace):
+    """``(dx, dw) = hip_rms_norm_bwd(g, x, w, rstd); z = dx + r`` (dx used nowhere else) ->
+    ``(z, dw) = hip_rms_norm_bwd(g, x, w, rstd, r)``: the residual stream's gradient is added in the
+    normalisation backward's store pass instead of a separate elementwise launch."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = trace.bound_symbols
+    uses: dict[str, int] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            uses[a.name] = uses.get(a.name, 0) + 1
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym.name not in ("torch_add", "add") or b.kwargs.get("alpha") not in (None, 1):
+            continue
+        if len(b.args) < 2 or not all(isinstance(a, TensorProxy) for a in b.args[:2]):
+            continue
+        for pos in (0, 1):
+            y, r = b.args[pos], b.args[1 - pos]
+            j = producer.get(y.name)
+            if j is None or j in drop or j in replace or bsyms[j].sym is not hip_rms_norm_bwd or uses.get(y.name, 0) != 1:
+                continue
+            rb = bsyms[j]
+            if len(rb.args) > 4 and rb.args[4] is not None:
+                continue
+            outs = rb.output
+            if outs[0] is not y or tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype:
+                continue
+            if tuple(b.output.shape) != tuple(y.shape) or b.output.dtype != y.dtype or producer.get(r.name, -1) > j:
+                continue
+            nb = ex.bind_call_ctx(hip_rms_norm_bwd.bind(*rb.args[:4], r, output=(b.output, outs[1])))
+            replace[j] = nb
+            drop.add(i)
+            break
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} residual-gradient add(s) fused into RMSNorm backward"))
+    return new
+
+
 def _post_claim(trace):
-    return _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_linear_epilogues(trace)))
+    return _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace))))
 
 
 ex.post_claim_pass = _post_claim
@@ -547,14 +639,14 @@ def _rms_fwd_impl(x, weight, eps):
     return rms_norm_fwd(x, weight, eps)
 
 
-def _rms_bwd_meta(dy, x, weight, rstd):
+def _rms_bwd_meta(dy, x, weight, rstd, residual=None):
     return TensorProxy(like=x), (None if weight is None else TensorProxy(like=weight))
 
 
-def _rms_bwd_impl(dy, x, weight, rstd):
+def _rms_bwd_impl(dy, x, weight, rstd, residual=None):
     from ..ops.rmsnorm import rms_norm_bwd
 
-    return rms_norm_bwd(dy, x, weight, rstd)
+    return rms_norm_bwd(dy, x, weight, rstd, residual)
 
 
 hip_rms_norm_fwd = ex.register_operator("hip_rms_norm_fwd", meta=_rms_fwd_meta, fn=_rms_fwd_impl)

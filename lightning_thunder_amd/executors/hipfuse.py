@@ -260,7 +260,8 @@ def compile_source(ks: cg.KernelSource) -> bytes:
 def load_kernel(ks: cg.KernelSource):
     data = compile_source(ks)
     lib = _lib()
-    key = int(hashlib.sha1(ks.src.encode()).hexdigest()[:15], 16)
+    # one source may define several kernels: the function cache is keyed on (kernel name, source)
+    key = int(hashlib.sha1((ks.name + "\0" + ks.src).encode()).hexdigest()[:15], 16)
     fn = ctypes.c_void_p()
     buf = ctypes.create_string_buffer(data, len(data))
     rc = lib.lta_rtc_load(key, buf, len(data), ks.name.encode(), ctypes.byref(fn))

@@ -1,6 +1,7 @@
 """K3 flash attention wrappers (kernels in ``csrc/attention_fwd.hip`` / ``attention_bwd.hip``)."""
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -12,6 +13,11 @@ register_signature("lta_attn_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_
 register_signature("lta_attn_bwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_float, c_int, c_void_p])
+register_signature("lta_attn_fwd_s", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                      c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p])
+register_signature("lta_attn_bwd_s", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_float, c_int, c_void_p, c_void_p])
 
 SUPPORTED_HEAD_DIMS = (64, 128)
 
@@ -34,17 +40,33 @@ def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
-def attn_fwd(q, k, v, causal: bool, scale: float | None = None):
-    """q [B, Hq, T, D], k/v [B, Hkv, S, D] -> (o [B, Hq, T, D], lse [B, Hq, T] fp32)."""
+def _strides3(t):
+    return (ctypes.c_int64 * 3)(*t.stride()[:3])
+
+
+def _rows_ok(t) -> bool:
+    """Head dim contiguous, 16-byte aligned rows: any [B, H, T] strides are read in place."""
+    return t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
+
+
+def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str = "bshd"):
+    """q [B, Hq, T, D], k/v [B, Hkv, S, D] -> (o [B, Hq, T, D], lse [B, Hq, T] fp32).
+
+    ``out_layout="bshd"`` (default) stores O as [B, T, Hq, D] and returns its [B, Hq, T, D]
+    transposed view: the usual ``o.transpose(1, 2).reshape(B, T, Hq * D)`` before the output
+    projection is then a view instead of a copy, and the backward reads it (and dO) in place."""
     lib = require()
     q, k, v = _c(q), _c(k), _c(v)
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
-    o = torch.empty_like(q)
+    if out_layout == "bshd":
+        o = torch.empty((B, T, Hq, D), device=q.device, dtype=q.dtype).transpose(1, 2)
+    else:
+        o = torch.empty_like(q)
     lse = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
-    rc = lib.lta_attn_fwd(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc), int(causal),
-                          stream_ptr(q.device))
+    rc = lib.lta_attn_fwd_s(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
+                            int(causal), ctypes.cast(_strides3(o), c_void_p), stream_ptr(q.device))
     check(rc, "lta_attn_fwd")
     return o, lse
 
@@ -52,7 +74,9 @@ def attn_fwd(q, k, v, causal: bool, scale: float | None = None):
 def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None):
     """Returns (dq, dk, dv) with dk/dv summed over the query heads of each kv group."""
     lib = require()
-    do, q, k, v, o = _c(do), _c(q), _c(k), _c(v), _c(o)
+    q, k, v = _c(q), _c(k), _c(v)
+    do = do if _rows_ok(do) else do.contiguous()
+    o = o if _rows_ok(o) else o.contiguous()
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -60,8 +84,10 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None):
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)
     delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
-    rc = lib.lta_attn_bwd(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
-                          ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal), stream_ptr(q.device))
+    st = (ctypes.c_int64 * 6)(*do.stride()[:3], *o.stride()[:3])
+    rc = lib.lta_attn_bwd_s(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
+                            ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p),
+                            stream_ptr(q.device))
     check(rc, "lta_attn_bwd")
     return dq, dk, dv
 

@@ -29,16 +29,24 @@ template <int D> struct BCfg {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Row strides: dO and O may be any [B,H,T] strided layout with the head dim contiguous (e.g. the
+// [B,T,H,D] storage that the output projection reads without a copy); s*[0..2] = batch/head/token.
+struct RowStrides {
+  int64_t b, h, t;
+};
+
 template <typename T, int D>
 __global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__ dO, const T* __restrict__ O,
-                                                           float* __restrict__ delta, int64_t rows) {
+                                                           float* __restrict__ delta, int64_t rows, int H, int Tq,
+                                                           RowStrides sdo, RowStrides so) {
   // 8 lanes per row (16 B each per step)
   const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 8;
   const int sub = threadIdx.x & 7;
   float acc = 0.f;
   if (row < rows) {
-    const T* a = dO + row * D;
-    const T* b = O + row * D;
+    const int64_t t = row % Tq, bh = row / Tq, hh = bh % H, bb = bh / H;
+    const T* a = dO + bb * sdo.b + hh * sdo.h + t * sdo.t;
+    const T* b = O + bb * so.b + hh * so.h + t * so.t;
 #pragma unroll
     for (int c = sub * 8; c < D; c += 64) {
       const Vec16<T> x = load16(a + c), y = load16(b + c);
@@ -64,7 +72,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
                                                                     const float* __restrict__ LSE,
                                                                     const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                     T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                    float scale, float scale_log2) {
+                                                                    float scale, float scale_log2, RowStrides sdo) {
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
   // Double-buffered Q / dO tiles: the global loads of tile i+1 are issued before the MFMAs of
@@ -119,14 +127,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
     const int hq = hk * group + it / nq;
     const int qbase = (qt_begin + it % nq) * kQT;
     const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
-    const T* dOb = dO + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* dOb = dO + b * sdo.b + hq * sdo.h;
 #pragma unroll
     for (int c = 0; c < LOADS; ++c) {
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
       const int qc = min(qbase + row, Tq - 1);
       pq[c] = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
-      po[c] = *reinterpret_cast<const uint4*>(dOb + (int64_t)qc * D + ch * 8);
+      po[c] = *reinterpret_cast<const uint4*>(dOb + qc * sdo.t + ch * 8);
     }
     if (tid < kQT) {
       const int qc = min(qbase + tid, Tq - 1);
@@ -261,7 +269,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
                                                                   const float* __restrict__ LSE,
                                                                   const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                   int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                  float scale_log2) {
+                                                                  float scale_log2, RowStrides sdo) {
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[2 * kBN * C::RSTR + kBN * C::TSTR];
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
   const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
-  const T* dOb = dO + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* dOb = dO + b * sdo.b + hq * sdo.h;
   const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
   const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
 
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
     qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
-    of[s] = load_frag<F>(dOb + (int64_t)qrow * D + 16 * s + 8 * h);
+    of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
   }
   const float lse2 = LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
   const float dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
@@ -408,38 +416,56 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
                void* dQ, void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, int causal,
-               hipStream_t s) {
+               RowStrides sdo, RowStrides so, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                     (const T*)dO, (const T*)O, (float*)DELTA, rows);
+                     (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
   if (causal) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
+                       sdo);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
+                       sdo);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
   }
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
+// strides: optional int64[6] = dO (batch, head, token), O (batch, head, token) element strides
+// (head dim contiguous); null = contiguous [B,H,T,D] for both.
+LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                              const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, void* workspace, int B, int Hq,
+                              int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
+                              hipStream_t stream) {
+  if (Hq % Hkv != 0) return -2;
+  const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
+  const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
+  const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
+#define LTA_B(TT, DD) \
+  return launch_bwd<TT, DD>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, stream)
+  if (dtype == kBF16) {
+    if (D == 128) LTA_B(__hip_bfloat16, 128);
+    if (D == 64) LTA_B(__hip_bfloat16, 64);
+  } else if (dtype == kF16) {
+    if (D == 128) LTA_B(__half, 128);
+    if (D == 64) LTA_B(__half, 64);
+  }
+#undef LTA_B
+  return -1;
+}
+
 LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
                             const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, void* workspace, int B, int Hq,
                             int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
-  if (Hq % Hkv != 0) return -2;
-  if (dtype == kBF16) {
-    if (D == 128) return launch_bwd<__hip_bfloat16, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-    if (D == 64) return launch_bwd<__hip_bfloat16, 64>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-  } else if (dtype == kF16) {
-    if (D == 128) return launch_bwd<__half, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-    if (D == 64) return launch_bwd<__half, 64>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-  }
-  return -1;
+  return lta_attn_bwd_s(dtype, dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, workspace, B, Hq, Hkv, Tq, Sk, D, scale, causal,
+                        nullptr, stream);
 }

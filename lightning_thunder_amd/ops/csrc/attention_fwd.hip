@@ -38,7 +38,8 @@ template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                const T* __restrict__ V, T* __restrict__ O,
                                                                float* __restrict__ LSE, int Hq, int Hkv, int Tq,
-                                                               int Sk, float scale_log2) {
+                                                               int Sk, float scale_log2, int64_t so_b, int64_t so_h,
+                                                               int64_t so_t) {
   using C = Cfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[kBN * C::KSTR + kBN * C::VSTR];
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   // ---- epilogue: O = O^T / l ; LSE --------------------------------------------------------------
   if (qi < Tq) {
     const float inv = (l > 0.f) ? 1.f / l : 0.f;
-    T* orow = O + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+    T* orow = O + b * so_b + hq * so_h + qi * so_t;  // any [B,H,T] strides (e.g. [B,T,H,D] storage)
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -217,29 +218,38 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
 
 template <typename T, int D>
 int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
-           float scale, int causal, hipStream_t s) {
+           float scale, int causal, const int64_t* so, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   dim3 grid(B * Hq, (Tq + kBM - 1) / kBM), block(kThreads);
+  const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * D, sh = so ? so[1] : (int64_t)Tq * D, st = so ? so[2] : D;
   if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<T, D, true>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
-                       (float*)lse, Hq, Hkv, Tq, Sk, sl2);
+                       (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<T, D, false>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
-                       (float*)lse, Hq, Hkv, Tq, Sk, sl2);
+                       (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
-                            int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
+// o_strides: optional int64[3] (batch, head, token) element strides of O (head dim contiguous);
+// null = contiguous [B,H,T,D].  [B,T,H,D] storage lets the output projection read O without a copy.
+LTA_EXPORT int lta_attn_fwd_s(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                              int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
+                              hipStream_t stream) {
   if (Hq % Hkv != 0) return -2;
   if (dtype == kBF16) {
-    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
+    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
   } else if (dtype == kF16) {
-    if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
-    if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, stream);
+    if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
+    if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
   }
   return -1;
+}
+
+LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                            int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
+  return lta_attn_fwd_s(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, nullptr, stream);
 }

@@ -54,28 +54,82 @@ __device__ __forceinline__ int xcd_tile(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-// stage one BMxBK (A) and one BNxBK (B) tile into LDS buffer `sbase`
-__device__ __forceinline__ void stage_tile(const __hip_bfloat16* __restrict__ A, const __hip_bfloat16* __restrict__ B,
-                                           int lda, int ldb, int m0, int n0, int k0, char* sbase, int wave, int lane) {
-  const int r = lane >> 3, p = lane & 7;
-  const int c = p ^ r;  // swizzled source chunk (row & 7 == r: chunks start at multiples of 8 rows)
+// ---- operand images -------------------------------------------------------------------------
+// K-major operand (A [M][K] / B [N][K], the nn.Linear forward): 128-B rows of 64 k, 16-B chunk c of
+// row r at chunk c ^ (r & 7); fragments are ds_read_b128 of 8 consecutive k.
+// MN-major operand (stored [K][M] / [K][N]: the transposed operands of dgrad and wgrad): 512-B rows
+// of 256 m (or n) per k, 16-B chunk c of row k at chunk c ^ tr_swz(k); fragments are two
+// ds_read_b64_tr_b16 (cdna_hip_programming.md T10) of rows k..k+3 and k+4..k+7, which deliver the
+// 8 consecutive k of column m in natural order.  tr_swz makes every transposed read conflict-free:
+// a 32-lane half reads rows {k0+q, k0+8+q} (q < 4) at chunks {c0, c0+1}, and tr_swz maps those 8
+// rows to 8 distinct even chunk offsets in the 16-slot bank row.
+__device__ __forceinline__ int tr_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+// one 64 x 256 MN-major tile (64 rows of 512 B) -> LDS at `dst` with global_load_lds: each
+// wave-instruction fills two rows (1 KiB, lane-linear), so the swizzle goes on the global source
+template <bool MN>
+__device__ __forceinline__ void stage_operand(const __hip_bfloat16* __restrict__ X, int ldx, int r0, int k0, char* dst,
+                                              int wave, int lane) {
+  if constexpr (!MN) {
+    const int r = lane >> 3, p = lane & 7;
+    const int c = p ^ r;  // swizzled source chunk (row & 7 == r: chunks start at multiples of 8 rows)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int chunk = i * 8 + wave;  // 8 rows per wave-instruction
-    const int row = chunk * 8 + r;
-    const __hip_bfloat16* ga = A + (int64_t)(m0 + row) * lda + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)ga, (lds_void*)(sbase + chunk * 1024), 16, 0, 0);
-  }
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;  // 8 rows per wave-instruction
+      const int row = chunk * 8 + r;
+      const __hip_bfloat16* g = X + (int64_t)(r0 + row) * ldx + k0 + c * 8;
+      __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(dst + chunk * 1024), 16, 0, 0);
+    }
+  } else {
+    const int half = lane >> 5, slot = lane & 31;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int chunk = i * 8 + wave;
-    const int row = chunk * 8 + r;
-    const __hip_bfloat16* gb = B + (int64_t)(n0 + row) * ldb + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)gb, (lds_void*)(sbase + TILE_BYTES + chunk * 1024), 16, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;  // rows 2*chunk, 2*chunk + 1
+      const int krow = chunk * 2 + half;
+      const int c = slot ^ tr_swz(krow);
+      const __hip_bfloat16* g = X + (int64_t)(k0 + krow) * ldx + r0 + c * 8;
+      __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(dst + chunk * 1024), 16, 0, 0);
+    }
   }
 }
 
-template <int ACT, bool BIAS, bool RES>
+// stage one BMxBK (A) and one BNxBK (B) tile into LDS buffer `sbase`
+template <bool AT = false, bool BT = false>
+__device__ __forceinline__ void stage_tile(const __hip_bfloat16* __restrict__ A, const __hip_bfloat16* __restrict__ B,
+                                           int lda, int ldb, int m0, int n0, int k0, char* sbase, int wave, int lane) {
+  stage_operand<AT>(A, lda, m0, k0, sbase, wave, lane);
+  stage_operand<BT>(B, ldb, n0, k0, sbase + TILE_BYTES, wave, lane);
+}
+
+// 8-element fragment (k = kb + 8*fq .. +7 of row / column `rc`) of a staged operand image
+template <bool MN>
+__device__ __forceinline__ bf16x8 read_frag(const char* img, int rc, int kk, int fr, int fq) {
+  if constexpr (!MN) {
+    const int c = kk * 4 + fq;
+    return *reinterpret_cast<const bf16x8*>(img + rc * 128 + ((c ^ (rc & 7)) << 4));
+  } else {
+    // rc = first column of this 16-lane group's block (multiple of 16); lane 4q+p of the group
+    // addresses row k0 + q, columns rc + 4p .. +3
+    const int q = fr >> 2, p = fr & 3;
+    const int k = kk * 32 + fq * 8 + q;
+    const int c = (rc >> 3) + (p >> 1);
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const char* p0 = img + k * 512 + ((c ^ tr_swz(k)) << 4) + 8 * (p & 1);
+    const char* p1 = img + (k + 4) * 512 + ((c ^ tr_swz(k + 4)) << 4) + 8 * (p & 1);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(__attribute__((address_space(3))) char*)p0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(__attribute__((address_space(3))) char*)p1);
+    union {
+      struct { s16x4 a, b; } s;
+      bf16x8 f;
+    } u;
+    u.s.a = lo;
+    u.s.b = hi;
+    return u.f;
+  }
+}
+
+template <int ACT, bool BIAS, bool RES, bool AT = false, bool BT = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_kernel(const __hip_bfloat16* __restrict__ A,
                                                               const __hip_bfloat16* __restrict__ B,
                                                               __hip_bfloat16* __restrict__ C,
@@ -107,28 +161,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_bf16_kernel(const __hip_bfloa
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
-  stage_tile(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
+  stage_tile<AT, BT>(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int t = 0; t < nk; ++t) {
     char* cur = smem + (t & 1) * STAGE_BYTES;
-    if (t + 1 < nk) stage_tile(A, B, lda, ldb, m0, n0, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+    if (t + 1 < nk)
+      stage_tile<AT, BT>(A, B, lda, ldb, m0, n0, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + fq;
       bf16x8 af[8], bfr[4];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int row = wm * 128 + m * 16 + fr;
-        af[m] = *reinterpret_cast<const bf16x8*>(cur + row * 128 + ((c ^ (row & 7)) << 4));
-      }
+      for (int m = 0; m < 8; ++m)
+        af[m] = read_frag<AT>(cur, wm * 128 + m * 16 + (AT ? 0 : fr), kk, fr, fq);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row = wn * 64 + n * 16 + fr;
-        bfr[n] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + row * 128 + ((c ^ (row & 7)) << 4));
-      }
+      for (int n = 0; n < 4; ++n)
+        bfr[n] = read_frag<BT>(cur + TILE_BYTES, wn * 64 + n * 16 + (BT ? 0 : fr), kk, fr, fq);
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
@@ -776,6 +826,29 @@ LTA_EXPORT int lta_gemm_tile_k() { return BK; }
 // C = act(alpha * A @ B^T + bias) + R ; A [M,K] (lda), B [N,K] (ldb), C/R [M,N] (ldc/ldr), all bf16.
 // Requires M % 256 == 0, N % 256 == 0, K % 64 == 0 and 16-B aligned rows (checked by the caller).
 // variant: 0 = 2-buffer loop, 1 = 8-phase pipelined loop (falls back to 0 unless K % 128 == 0).
+// C[M,N] (+)= A . B with either operand stored K-major or MN-major (the backward GEMMs):
+//   at = 0: A [M][K] (lda = row pitch);   at = 1: A stored [K][M] (A^T row-major, lda = its pitch)
+//   bt = 0: B given as [N][K] (B^T);      bt = 1: B stored [K][N] (row-major, ldb = its pitch)
+// R (optional, [M][N] with pitch ldr) is added in the epilogue (gradient accumulation).
+LTA_EXPORT int lta_gemm_bf16_layout(const void* A, const void* B, void* C, const void* R, int M, int N, int K, int lda,
+                                    int ldb, int ldc, int ldr, float alpha, int at, int bt, hipStream_t s) {
+  if (M % BM || N % BN || K % BK) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_GL(AT_, BT_, RE)                                                                                    \
+  hipLaunchKernelGGL((gemm_nt_bf16_kernel<kNone, false, RE, AT_, BT_>), grid, block, 0, s, (const __hip_bfloat16*)A, \
+                     (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, (const __hip_bfloat16*)R, M, N, K, lda, ldb, \
+                     ldc, ldr, alpha)
+#define LTA_GL2(AT_, BT_) \
+  if (R) { LTA_GL(AT_, BT_, true); } else { LTA_GL(AT_, BT_, false); }
+  if (!at && !bt) { LTA_GL2(false, false) }
+  else if (!at && bt) { LTA_GL2(false, true) }
+  else if (at && !bt) { LTA_GL2(true, false) }
+  else { LTA_GL2(true, true) }
+#undef LTA_GL2
+#undef LTA_GL
+  return (int)hipGetLastError();
+}
+
 LTA_EXPORT int lta_gemm_nt_bf16_v(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
                                   int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int variant,
                                   hipStream_t stream) {

@@ -85,7 +85,8 @@ template <typename T, int CHUNKS>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                const T* __restrict__ w, const float* __restrict__ rstd,
                                                                T* __restrict__ dx, float* __restrict__ dw_partial,
-                                                               int64_t rows, int cols, int rows_per_block) {
+                                                               int64_t rows, int cols, int rows_per_block,
+                                                               const T* __restrict__ res) {
   constexpr int V = Vec16<T>::N;
   __shared__ float smem[kWaves];
   float dw_acc[CHUNKS][V];
@@ -132,12 +133,14 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
     for (int c = 0; c < CHUNKS; ++c) {
       const int idx = (c * kThreads + threadIdx.x) * V;
       if (idx < cols) {
-        Vec16<T> o;
+        Vec16<T> o, rv;
+        if (res != nullptr) rv = load16(res + row * cols + idx);  // gradient arriving through the residual
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const float xh = to_f32(xv[c].v[j]) * r;
           const float gw = to_f32(gv[c].v[j]) * to_f32(wv[c].v[j]);
-          o.v[j] = from_f32<T>(r * (gw - xh * dot));
+          const float add = res != nullptr ? to_f32(rv.v[j]) : 0.f;
+          o.v[j] = from_f32<T>(r * (gw - xh * dot) + add);
         }
         store16(dx + row * cols + idx, o);
       }
@@ -160,7 +163,8 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x,
                                                                 const T* __restrict__ w, const float* __restrict__ rstd,
                                                                 T* __restrict__ dx, float* __restrict__ dw_partial,
-                                                                int64_t rows, int cols, int rows_per_block) {
+                                                                int64_t rows, int cols, int rows_per_block,
+                                                                const T* __restrict__ res) {
   __shared__ float smem[kWaves];
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
@@ -179,7 +183,8 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_generic(const T* __restr
       const float wv = w ? to_f32(w[i]) : 1.f;
       const float xh = to_f32(x[row * cols + i]) * r;
       const float g = to_f32(dy[row * cols + i]);
-      dx[row * cols + i] = from_f32<T>(r * (g * wv - xh * dot));
+      const float add = res != nullptr ? to_f32(res[row * cols + i]) : 0.f;
+      dx[row * cols + i] = from_f32<T>(r * (g * wv - xh * dot) + add);
       if (dw_partial) dw_partial[(int64_t)blockIdx.x * cols + i] += g * xh;
     }
   }
@@ -232,7 +237,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* rstd, int64_t rows, 
 
 template <typename T>
 int launch_bwd(const void* dy, const void* x, const void* w, const void* rstd, void* dx, void* dw, void* workspace,
-               int64_t rows, int cols, int nblocks, hipStream_t s) {
+               int64_t rows, int cols, int nblocks, const void* res, hipStream_t s) {
   constexpr int V = Vec16<T>::N;
   const int per_pass = kThreads * V;
   const int chunks = (cols + per_pass - 1) / per_pass;
@@ -245,12 +250,14 @@ int launch_bwd(const void* dy, const void* x, const void* w, const void* rstd, v
   const float* R = (const float*)rstd;
   T* DX = (T*)dx;
   float* Pp = dw ? P : nullptr;
-  if (cols % V != 0 || chunks > 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) || ((uintptr_t)dx % 16) || (w && ((uintptr_t)w % 16))) {
-    hipLaunchKernelGGL((rmsnorm_bwd_generic<T>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb);
+  const T* RES = (const T*)res;
+  if (cols % V != 0 || chunks > 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) || ((uintptr_t)dx % 16) || (w && ((uintptr_t)w % 16)) ||
+      ((uintptr_t)res % 16)) {
+    hipLaunchKernelGGL((rmsnorm_bwd_generic<T>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb, RES);
   } else {
     switch (chunks) {
 #define LTA_CASE(C) \
-  case C: hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, C>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb); break;
+  case C: hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, C>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb, RES); break;
       LTA_CASE(1) LTA_CASE(2) LTA_CASE(3) LTA_CASE(4)
 #undef LTA_CASE
     }
@@ -274,12 +281,19 @@ LTA_EXPORT int lta_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y,
   return -1;
 }
 
-LTA_EXPORT int lta_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const void* rstd, void* dx,
-                               void* dw, void* workspace, int64_t rows, int64_t cols, int nblocks, hipStream_t stream) {
+// res (optional, same shape as dx): added to dx in the same pass (the residual stream's gradient)
+LTA_EXPORT int lta_rmsnorm_bwd_res(int dtype, const void* dy, const void* x, const void* w, const void* rstd, void* dx,
+                                   void* dw, void* workspace, int64_t rows, int64_t cols, int nblocks, const void* res,
+                                   hipStream_t stream) {
   switch (dtype) {
-    case kBF16: return launch_bwd<__hip_bfloat16>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
-    case kF16: return launch_bwd<__half>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
-    case kF32: return launch_bwd<float>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, stream);
+    case kBF16: return launch_bwd<__hip_bfloat16>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
+    case kF16: return launch_bwd<__half>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
+    case kF32: return launch_bwd<float>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
   }
   return -1;
+}
+
+LTA_EXPORT int lta_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const void* rstd, void* dx,
+                               void* dw, void* workspace, int64_t rows, int64_t cols, int nblocks, hipStream_t stream) {
+  return lta_rmsnorm_bwd_res(dtype, dy, x, w, rstd, dx, dw, workspace, rows, cols, nblocks, nullptr, stream);
 }

@@ -84,6 +84,8 @@ def _timeit(fn, iters: int = 5) -> float:
 
 
 def _torch_linear(x2, w, bias, residual, act):
+    if residual is not None and act is None and bias is None and x2.dim() == 2:
+        return torch.addmm(residual, x2, w.t())  # hipBLASLt with beta = 1: the add rides in the GEMM
     y = torch.nn.functional.linear(x2, w, bias)
     if act == "gelu_tanh":
         y = torch.nn.functional.gelu(y, approximate="tanh")
@@ -174,6 +176,104 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
     else:
         y = _torch_linear(x2, w, bias, r2, act)
     return y.reshape(*x.shape[:-1], N)
+
+
+# ---------------------------------------------------------------------------------------------
+# general-layout bf16 matmul (the backward GEMMs: dgrad = g @ W, wgrad = g^T @ x)
+# ---------------------------------------------------------------------------------------------
+register_signature("lta_gemm_bf16_layout", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                            c_int, c_int, c_float, c_int, c_int, c_void_p])
+
+
+def _operand_layout(t: torch.Tensor, rows: int, cols: int):
+    """(contiguous dim, pitch) of a 2-D [rows, cols] operand with 16-byte aligned rows, or None."""
+    if t.dim() != 2 or t.data_ptr() % 16:
+        return None
+    s0, s1 = t.stride()
+    if s1 == 1 and s0 % 8 == 0 and s0 >= cols:
+        return 1, s0
+    if s0 == 1 and s1 % 8 == 0 and s1 >= rows:
+        return 0, s1
+    return None
+
+
+def matmul_layout(a: torch.Tensor, b: torch.Tensor):
+    """(at, bt, lda, ldb) of ``a [M,K] @ b [K,N]`` for ``lta_gemm_bf16_layout``, or None."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda or a.dim() != 2 or b.dim() != 2:
+        return None
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K or M % TILE_M or N % TILE_N or K % TILE_K:
+        return None
+    la, lb = _operand_layout(a, M, K), _operand_layout(b, K, N)
+    if la is None or lb is None:
+        return None
+    at = 0 if la[0] == 1 else 1  # a row-major [M][K] -> K-major; column-major -> stored [K][M]
+    bt = 1 if lb[0] == 1 else 0  # b row-major [K][N] -> stored [K][N]; column-major -> [N][K]
+    return at, bt, la[1], lb[1]
+
+
+def matmul_hip(a: torch.Tensor, b: torch.Tensor, *, residual: torch.Tensor | None = None,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b (+ residual)`` on the MFMA kernel, reading transposed operands through the
+    hardware-transposing LDS read instead of materialising them (2-D bf16, tile-divisible)."""
+    lay = matmul_layout(a, b)
+    if lay is None:
+        raise ValueError(f"matmul_hip: unsupported operands {tuple(a.shape)}{a.stride()} @ {tuple(b.shape)}{b.stride()}")
+    at, bt, lda, ldb = lay
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if residual is not None:
+        assert residual.shape == (M, N) and residual.stride(1) == 1 and residual.dtype == torch.bfloat16
+    rc = require().lta_gemm_bf16_layout(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                        None if residual is None else residual.data_ptr(), M, N, K, lda, ldb,
+                                        out.stride(0), 0 if residual is None else residual.stride(0), 1.0, at, bt,
+                                        stream_ptr(a.device))
+    check(rc, "lta_gemm_bf16_layout")
+    return out
+
+
+_mm_choice: dict = {}
+
+
+def _torch_mm(a, b, residual=None):
+    return torch.matmul(a, b) if residual is None else torch.addmm(residual, a, b)
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b (+ residual)`` for the prim matmul (leading dims of ``a`` flattened): the MFMA kernel
+    where it is faster than hipBLASLt for this shape, operand layout and epilogue (timed once per
+    key), else torch (``addmm`` with beta = 1 when there is a residual)."""
+    if a.dim() > 2 and b.dim() == 2:
+        lead = a.shape[:-1]
+        a2 = a.reshape(-1, a.shape[-1])
+        r2 = None if residual is None else residual.reshape(-1, b.shape[1])
+        return matmul(a2, b, r2).reshape(*lead, b.shape[1])
+    mode = _os.environ.get("LTA_GEMM", "auto")
+    lay = matmul_layout(a, b) if mode != "torch" else None
+    if residual is not None and (residual.dtype != torch.bfloat16 or residual.stride(1) != 1
+                                 or residual.stride(0) % 8 or residual.data_ptr() % 16):
+        lay = None
+    if lay is None:
+        return _torch_mm(a, b, residual)
+    key = (a.shape[0], b.shape[1], a.shape[1], lay[0], lay[1], residual is not None)
+    use = True if mode == "hip" else _mm_choice.get(key)
+    if use is None:
+        if torch.cuda.is_current_stream_capturing():
+            use = True
+        else:
+            t_h = _timeit(lambda: matmul_hip(a, b, residual=residual))
+            t_t = _timeit(lambda: _torch_mm(a, b, residual))
+            use = t_h <= t_t
+        _mm_choice[key] = use
+    return matmul_hip(a, b, residual=residual) if use else _torch_mm(a, b, residual)
+
+
+def matmul_selection_table() -> dict:
+    """(M, N, K, a stored transposed, b stored row-major, residual) -> True if the HIP kernel was selected."""
+    return dict(_mm_choice)
 
 
 def selection_table() -> dict:

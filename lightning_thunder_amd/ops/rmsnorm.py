@@ -3,7 +3,10 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import require, dcode, ptr, stream_ptr, check
+from ._lib import require, dcode, ptr, stream_ptr, check, register_signature, c_int, c_int64, c_void_p
+
+register_signature("lta_rmsnorm_bwd_res", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_int64, c_int64, c_int, c_void_p, c_void_p])
 
 
 def _as_2d(x: torch.Tensor):
@@ -30,17 +33,20 @@ def _bwd_blocks(rows: int) -> int:
     return max(1, min(rows, 512))
 
 
-def rms_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor | None, rstd: torch.Tensor):
+def rms_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor | None, rstd: torch.Tensor,
+                 residual: torch.Tensor | None = None):
+    """(dx, dw); ``residual`` (same shape as x) is added to dx in the same pass."""
     lib = require()
     x2, rows, cols = _as_2d(x)
     dy2, _, _ = _as_2d(dy)
+    r2 = None if residual is None else _as_2d(residual)[0]
     w = None if weight is None else weight.contiguous()
     dx = torch.empty_like(x2)
     nblocks = _bwd_blocks(rows)
     dw = None if weight is None else torch.empty_like(w)
     ws = torch.empty((nblocks, cols), device=x.device, dtype=torch.float32) if weight is not None else None
-    rc = lib.lta_rmsnorm_bwd(dcode(x2), ptr(dy2), ptr(x2), ptr(w), ptr(rstd), ptr(dx), ptr(dw), ptr(ws), rows, cols,
-                             nblocks, stream_ptr(x.device))
+    rc = lib.lta_rmsnorm_bwd_res(dcode(x2), ptr(dy2), ptr(x2), ptr(w), ptr(rstd), ptr(dx), ptr(dw), ptr(ws), rows, cols,
+                                 nblocks, ptr(r2), stream_ptr(x.device))
     check(rc, "lta_rmsnorm_bwd")
     return dx.view(x.shape), dw
 

@@ -237,6 +237,41 @@ def test_fp8_cast_and_transpose(e5m2):
     assert torch.equal(y2, y) and torch.equal(yt, y.t().contiguous())
 
 
+@pytest.mark.parametrize("layout", ["nn", "tn", "tt", "nt"])
+@pytest.mark.parametrize("shape", [(256, 512, 128), (512, 768, 320), (1024, 256, 4096)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_gemm_bf16_layouts(layout, shape, residual):
+    """dgrad / wgrad GEMMs: either operand stored transposed (MN-major LDS image + ds_read_b64_tr_b16)."""
+    from lightning_thunder_amd.ops.gemm import matmul_hip, matmul_layout
+
+    torch.manual_seed(0)
+    M, N, K = shape
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    if layout[0] == "t":  # a stored [K][M] (column-major view), padded pitch
+        a = torch.randn(K, M + 64, device="cuda", dtype=torch.bfloat16)[:, :M].t()
+    if layout[1] == "n":  # b stored [N][K]
+        b = (torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5).t()
+    lay = matmul_layout(a, b)
+    assert lay is not None and lay[0] == (layout[0] == "t") and lay[1] == (layout[1] == "t")
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if residual else None
+    out = matmul_hip(a, b, residual=r)
+    ref = a.float() @ b.float()
+    if r is not None:
+        ref = ref.bfloat16().float() + r.float()
+    err = (out.float() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item() / 4), err
+    # integer data: exact, catches any k-order or swizzle mistake
+    ai = torch.randint(-3, 4, a.shape, device="cuda").to(torch.bfloat16)
+    bi = torch.randint(-3, 4, b.shape, device="cuda").to(torch.bfloat16)
+    if layout[0] == "t":
+        ai = ai.t().contiguous().t()
+    if layout[1] == "n":
+        bi = bi.t().contiguous().t()
+    exact = matmul_hip(ai, bi)
+    torch.testing.assert_close(exact.float(), (ai.float() @ bi.float()).bfloat16().float(), atol=0, rtol=0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmts", [(0, 0), (1, 0)])
 def test_gemm_nt_fp8(fmts):
