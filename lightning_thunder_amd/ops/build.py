@@ -40,10 +40,16 @@ def _sources():
     return hip, cpp
 
 
+# Per-file device flags.  attention_bwd: MFMAs written as intrinsics take VGPR destinations, so the
+# S / dP tiles stay where their softmax reads them while the dK / dV accumulators (inline-asm MFMAs)
+# own the AGPR file (without it hipcc swaps them through AGPRs every tile).
+FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:
     cmd = [_hipcc(), "-c", src, "-o", obj, "-fPIC", "-O3", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
     if is_device:
-        cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + FILE_FLAGS.get(os.path.basename(src), [])
     else:
         cmd += ["-D__HIP_PLATFORM_AMD__"]
     if verbose:

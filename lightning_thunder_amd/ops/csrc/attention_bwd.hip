@@ -19,6 +19,8 @@ using namespace lta::attn;
 namespace {
 
 constexpr int kThreads = 256;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 template <int D> struct BCfg {
   static constexpr int RSTR = D + 8;    // row-read image stride (ds_read_b128 conflict-free)
@@ -258,6 +260,344 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
 }
 
 // ---------------------------------------------------------------------------------------------
+// dK / dV, D = 128 (v2).  Same decomposition as above; restructured after PMC counters showed the
+// v1 loop VALU-bound (355 VALU per wave-iteration against 32 MFMAs, 20 % MFMA busy, 296 VGPRs with
+// the S/dP accumulators shuttled through AGPRs):
+//  * Q and dO tiles reach LDS by global_load_lds (no VGPR staging, no stash pass) as ONE image per
+//    tile that serves both the row reads (ds_read_b128, A operand of S and dP) and the transposed
+//    reads (ds_read_b64_tr_b16, A operand of dV^T and dK^T): 8-row x 32-column subtiles of 512 B
+//    (cdna_hip_programming.md T10, layout (a)), the swizzle applied to the DMA source address; both
+//    read kinds are conflict-free, and every transposed read of a lane is one of two base
+//    addresses plus an immediate;
+//  * the transposed reads are issued from inline asm: as intrinsics hipcc cannot tell them from
+//    the stage the DMA in flight is writing and drains the DMA queue (vmcnt(0)) in front of them;
+//  * V lives in LDS (read each tile as the dP B operand), K stays in registers: the loop fits the
+//    256 architectural VGPRs;
+//  * the causal / bounds mask runs only on the tiles that straddle the diagonal or an edge (a
+//    wave-uniform branch); rows past Tq are clamped copies whose P and dS are masked to zero.
+// ---------------------------------------------------------------------------------------------
+// layout (a): byte offset of 16-B chunk ch (0..15) of row r in a [32][128 x 16-bit] image
+__device__ __forceinline__ int du_off(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// 16 transposed reads (4 d-tiles x {rows 4h.., 8+4h.., 16+4h.., 24+4h..}) of one image -> the 8 A
+// fragments of an X^T . P product (frag 2*dt: query rows 0..15, 2*dt+1: rows 16..31 of the k
+// order the P fragment carries), one wait at the end.  ba / bb: the lane's byte address of rows
+// 4h+q / 8+4h+q of d-tile 0; d-tile dt adds 512*dt, rows 16.. add 4096.
+__device__ __forceinline__ void tr_frags8(bf16x8 (&f)[8], unsigned ba, unsigned bb) {
+  typedef short s16x4v __attribute__((ext_vector_type(4)));
+  s16x4v x[16];
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
+      "ds_read_b64_tr_b16 %2, %16 offset:4096\n\tds_read_b64_tr_b16 %3, %17 offset:4096\n\t"
+      "ds_read_b64_tr_b16 %4, %16 offset:512\n\tds_read_b64_tr_b16 %5, %17 offset:512\n\t"
+      "ds_read_b64_tr_b16 %6, %16 offset:4608\n\tds_read_b64_tr_b16 %7, %17 offset:4608\n\t"
+      "ds_read_b64_tr_b16 %8, %16 offset:1024\n\tds_read_b64_tr_b16 %9, %17 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %10, %16 offset:5120\n\tds_read_b64_tr_b16 %11, %17 offset:5120\n\t"
+      "ds_read_b64_tr_b16 %12, %16 offset:1536\n\tds_read_b64_tr_b16 %13, %17 offset:1536\n\t"
+      "ds_read_b64_tr_b16 %14, %16 offset:5632\n\tds_read_b64_tr_b16 %15, %17 offset:5632\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7]),
+        "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11]), "=&v"(x[12]), "=&v"(x[13]), "=&v"(x[14]), "=&v"(x[15])
+      : "v"(ba), "v"(bb)
+      : "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    union {
+      struct { s16x4v a, b; } s;
+      bf16x8 f;
+    } u;
+    u.s.a = x[2 * i];
+    u.s.b = x[2 * i + 1];
+    f[i] = u.f;
+  }
+}
+__device__ __forceinline__ void tr_frags8(f16x8 (&f)[8], unsigned ba, unsigned bb) {
+  bf16x8 t[8];
+  tr_frags8(t, ba, bb);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = __builtin_bit_cast(f16x8, t[i]);
+}
+
+// dK^T / dV^T accumulate in the accumulator (AGPR) file through inline-asm MFMAs: they are only
+// ever MFMA C/D operands, and pinning them there leaves the 256 architectural VGPRs to K, the S / dP
+// tiles and their softmax (hipcc otherwise parks S / dP in AGPRs and copies them out every tile).
+// `s_nop 1` covers the VALU (cvt_pk) write -> MFMA operand read; an accumulate chain needs none.
+__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const f16x8& a, const f16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                       const T* __restrict__ V, const T* __restrict__ dO,
+                                                                       const float* __restrict__ LSE,
+                                                                       const float* __restrict__ DELTA, T* __restrict__ dK,
+                                                                       T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
+                                                                       float scale, float scale_log2, RowStrides sdo) {
+  constexpr int D = 128;
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  // Three-stage DMA ring: tile it+2 is issued while tile it is multiplied, and the end-of-tile wait
+  // only retires tile it+1 (counted vmcnt, raw barrier), so a DMA has two tiles of compute to land.
+  // Stage = {Q image 8 KB, dO image 8 KB, LSE 128 B, delta 128 B}; the statistics come through
+  // registers of wave 0 (loaded before its DMAs, so retiring them never waits on a DMA) and are
+  // written into their stage at the end of the tile before.
+  constexpr int NST = 3;
+  constexpr int IMG = kQT * 256;           // one 32-row image (bytes)
+  constexpr int STAGE = 2 * IMG + 256;
+  constexpr int VOFF = NST * STAGE;        // V rows after the stages
+  constexpr int VBYTES = kKB * C::RSTR * 2;
+  constexpr int KOFF = VOFF + VBYTES;      // K rows
+  // ONE __shared__ object: a second one can make hipcc drain the DMA queue before every ds_read
+  __shared__ __attribute__((aligned(1024))) char smem[KOFF + VBYTES];
+  short* Vs = reinterpret_cast<short*>(smem + VOFF);
+  short* Ks = reinterpret_cast<short*>(smem + KOFF);
+
+  const int kb = (int)blockIdx.y;
+  const int bh = blockIdx.x;
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int group = Hq / Hkv;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  const int kw = kb * kKB + wave * 32;
+  const int key = kw + r;
+  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+
+  // K and V rows of this workgroup's 128 keys -> LDS (padded rows: conflict-free B-operand reads);
+  // held there rather than in registers so the loop carries nothing but the AGPR accumulators
+#pragma unroll
+  for (int c = 0; c < kKB * C::CH / kThreads; ++c) {
+    const int id = c * kThreads + tid;
+    const int row = id / C::CH, ch = id % C::CH;
+    const int vr = min(kb * kKB + row, Sk - 1);
+    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * D + ch * 8);
+    *reinterpret_cast<uint4*>(Ks + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Kb + (int64_t)vr * D + ch * 8);
+  }
+
+  f32x16 dkacc[C::DT], dvacc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dkacc[dt][i] = 0.f;
+      dvacc[dt][i] = 0.f;
+    }
+
+  const int n_qt = (Tq + kQT - 1) / kQT;
+  const int qt_begin = CAUSAL ? min((kb * kKB) / kQT, n_qt) : 0;
+  const int nq = n_qt - qt_begin;
+  const int total = group * nq;
+
+  float plse = 0.f, pdel = 0.f;
+  auto stash_stats = [&](int st) {
+    if (wave == 0 && lane < kQT) {
+      float* sp = reinterpret_cast<float*>(smem + st * STAGE + 2 * IMG);
+      sp[lane] = plse;
+      sp[kQT + lane] = pdel;
+    }
+  };
+  // DMA tile (query head hk*group + hi, query tile qt_begin + ti) into stage `st`: wave w stages
+  // rows 8w .. 8w+7 of the Q and dO images (4 loads), wave 0 also the LSE / delta rows (2 loads)
+  auto issue = [&](int hi, int ti, int st) {
+    const int hq = hk * group + hi;
+    const int qbase = (qt_begin + ti) * kQT;
+    const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* dOb = dO + b * sdo.b + hq * sdo.h;
+    char* qimg = smem + st * STAGE;
+    if (wave == 0) {
+      // asm loads: hipcc would otherwise wait for them with vmcnt(0), i.e. behind this tile's DMAs;
+      // they are issued first, so the vmcnt(4) that retires the tile before covers them
+      const int64_t srow = ((int64_t)b * Hq + hq) * Tq + min(qbase + (lane & 31), Tq - 1);
+      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off"
+                   : "=&v"(plse), "=&v"(pdel)
+                   : "v"(LSE + srow), "v"(DELTA + srow)
+                   : "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // wave-instruction k = 2*wave + i fills 16-B units u = 64k + lane of the image (lane-linear);
+      // invert layout (a): u = 128 (row>>3) + 32 (ch>>2) + 4 (row&7) + ((ch&3) ^ ((row>>2)&3))
+      const int k = wave * 2 + i;
+      const int u = 64 * k + lane;
+      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
+      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
+      const int qc = min(qbase + row, Tq - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * D + ch * 8),
+                                       (lds_void*)(qimg + k * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
+                                       (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
+    }
+  };
+  // wait for every load of this wave except the newest tile's 4 DMAs (the statistics loads of
+  // the newest tile, issued before them, land too)
+  auto wait_all_but_newest = [&]() { asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory"); };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed
+  int nhi = 0, nti = 0;  // next tile to issue
+  auto advance = [&]() {
+    if (++nti == nq) {
+      nti = 0;
+      ++nhi;
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V staging loads
+  if (total > 0) {
+    issue(nhi, nti, 0);
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(plse), "+v"(pdel)::"memory");
+    stash_stats(0);
+  }
+  if (total > 1) {
+    issue(nhi, nti, 1);
+    advance();
+    wait_all_but_newest();
+    stash_stats(1);
+  }
+  __syncthreads();
+
+  // transposed-read base addresses of this lane (layout (a)): group lane 4q+p reads row 4h+q (ba)
+  // or 8+4h+q (bb), columns 16(g&1) + 4p .. +3 of d-tile 0
+  unsigned tr_a, tr_b;
+  {
+    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
+    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
+  }
+  int ti = 0;  // current tile's query-tile index
+  int st = 0;  // current stage
+  for (int it = 0; it < total; ++it) {
+    const bool issue_next = it + 2 < total;
+    const int st2 = st >= 1 ? st - 1 : 2;  // (st + 2) % 3: the stage tile it-1 used
+    if (issue_next) issue(nhi, nti, st2);
+    const int qbase = (qt_begin + ti) * kQT;
+    const char* qimg = smem + st * STAGE;
+    const char* oimg = qimg + IMG;
+    const float* sl = reinterpret_cast<const float*>(qimg + 2 * IMG);
+
+    // S = Q K^T (rows: this tile's queries, columns: this wave's keys)
+    f32x16 sacc, pacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sacc[i] = 0.f;
+      pacc[i] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F kb_ = load_frag<F>(Ks + (wave * 32 + r) * C::RSTR + 16 * s + 8 * h);
+      sacc = mfma(load_frag<F>(qimg + du_off(r, 2 * s + h)), kb_, sacc);
+    }
+    // dP = dO V^T, overlapping the exponentials of P
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F vb = load_frag<F>(Vs + (wave * 32 + r) * C::RSTR + 16 * s + 8 * h);
+      pacc = mfma(load_frag<F>(oimg + du_off(r, 2 * s + h)), vb, pacc);
+    }
+    // statistics rows 8a + 4h .. +3 (a = 0..3) of LSE and delta.  Read in ONE asm statement with
+    // its own wait: as plain loads hipcc cannot tell them from the stage the DMA in flight is
+    // writing and would drain the DMA queue (vmcnt(0)) in front of them.
+    f32x4v L[4], Dl[4];
+    {
+      const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(sl + 4 * h);
+      asm volatile(
+          "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
+          "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
+          "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(Dl[0]), "=&v"(Dl[1]), "=&v"(Dl[2]), "=&v"(Dl[3])
+          : "v"(addr)
+          : "memory");
+    }
+    constexpr float kLog2e = 1.44269504088896340736f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float li = L[i >> 2][i & 3];
+      sacc[i] = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - li * kLog2e);
+    }
+    // wave-uniform: only tiles that straddle the causal diagonal or an edge need the mask (rows
+    // past Tq are clamped copies: P = 0 there also zeroes their dS)
+    const bool masked = (CAUSAL && kw + 31 > qbase) || kw + 32 > Sk || qbase + kQT > Tq;
+    if (masked) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qq = qbase + acc_row(i, h);
+        if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) sacc[i] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float di = Dl[i >> 2][i & 3];
+      pacc[i] = sacc[i] * (pacc[i] - di);  // dS
+    }
+    F pf0, pf1, df0, df1;
+    pack_frag(pf0, sacc, 0);
+    pack_frag(pf1, sacc, 1);
+    pack_frag(df0, pacc, 0);
+    pack_frag(df1, pacc, 1);
+    {
+      F xt[8];
+      tr_frags8(xt, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        mfma_acc_agpr(dvacc[dt], xt[2 * dt], pf0);
+        mfma_acc_agpr(dvacc[dt], xt[2 * dt + 1], pf1);
+      }
+      tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // Q^T
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        mfma_acc_agpr(dkacc[dt], xt[2 * dt], df0);
+        mfma_acc_agpr(dkacc[dt], xt[2 * dt + 1], df1);
+      }
+    }
+    // tile it+1 must have landed (tile it+2 may stay in flight); every wave's reads of stage st are
+    // done before the barrier, after which tile it+3 may be DMA'd into it
+    if (issue_next) {
+      advance();
+      wait_all_but_newest();
+      stash_stats(st2);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    ti = ti + 1 == nq ? 0 : ti + 1;
+    st = st == 2 ? 0 : st + 1;
+  }
+  // the last asm MFMAs' results must be complete before any other instruction reads them
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[dt]), "+a"(dvacc[dt]));
+
+  if (key < Sk) {
+    T* dkrow = dK + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+    T* dvrow = dV + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        union {
+          T v[4];
+          uint2 u;
+        } pk, pv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pk.v[e] = from_f32<T>(dkacc[dt][4 * a + e] * scale);
+          pv.v[e] = from_f32<T>(dvacc[dt][4 * a + e]);
+        }
+        *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
+        *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // dQ
 // ---------------------------------------------------------------------------------------------
 constexpr int kBM = 128;
@@ -416,22 +756,34 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
                void* dQ, void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, int causal,
-               RowStrides sdo, RowStrides so, hipStream_t s) {
+               RowStrides sdo, RowStrides so, int dkdv_v2, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
-  if (causal) {
+  if (D == 128 && dkdv_v2) {
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                         sl2, sdo);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                         sl2, sdo);
+  } else if (causal) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
                        sdo);
+  }
+  if (causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
-                       sdo);
+    if (!(D == 128 && dkdv_v2))
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                         sl2, sdo);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
   }
@@ -450,8 +802,12 @@ LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const vo
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
   const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
+  static const int v2 = [] {
+    const char* e = getenv("LTA_ATTN_BWD_V1");  // A/B switch: the v1 dK/dV kernel
+    return (e && e[0] == '1') ? 0 : 1;
+  }();
 #define LTA_B(TT, DD) \
-  return launch_bwd<TT, DD>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, stream)
+  return launch_bwd<TT, DD>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, v2, stream)
   if (dtype == kBF16) {
     if (D == 128) LTA_B(__hip_bfloat16, 128);
     if (D == 64) LTA_B(__hip_bfloat16, 64);

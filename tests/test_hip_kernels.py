@@ -122,8 +122,11 @@ def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
     q = torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
     k = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype)
     v = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype)
-    do = torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
+    # dO in [B, T, H, D] storage (what the output projection's backward produces), read in place
+    do = torch.randn(B, T, Hq, D, device="cuda", dtype=dtype).transpose(1, 2) if T % 2 else \
+        torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
     o, lse = attn_fwd(q, k, v, causal)
+    assert o.transpose(1, 2).is_contiguous()  # O stored [B, T, H, D]
     qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
     ref = _sdpa_ref(qf, kf, vf, causal)
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
