@@ -19,7 +19,7 @@ import torch
 from . import dtypes, prims
 from .prims import PrimIDs
 from .proxies import TensorProxy, Proxy, NumberProxy, pyval
-from .pytree import tree_flatten, tree_unflatten
+from .pytree import tree_flatten, tree_unflatten, tree_map
 
 _vjp_rules: dict[Any, Callable] = {}
 
@@ -678,3 +678,156 @@ def add_transform(cfn, *, transform, disable_torch_autograd_support=False, _lega
         debug_options=cd.debug_options,
         **cd.compile_options,
     )
+
+
+# -----------------------------------------------------------------------------------------
+# Joint-style gradient registration (reference ``register_grad`` :620 with ``get_grad`` /
+# ``put_grad``): ``gradfn(*args)`` computes the forward, reads output cotangents with
+# ``get_grad(out)`` and deposits input gradients with ``put_grad(arg, g)`` -- one function for both
+# directions.  Here it is converted into a VJP rule by recording what gradfn traces: the ops that
+# depend on a ``get_grad`` placeholder (transitively) are the backward and are replayed, with the
+# real cotangents substituted, when autodiff reaches the op; the rest stay in the forward trace.
+# -----------------------------------------------------------------------------------------
+import threading as _threading
+
+_joint = _threading.local()
+
+
+def get_grad(x):
+    """The cotangent of forward value ``x`` (only inside a ``register_grad`` gradient function)."""
+    st = getattr(_joint, "state", None)
+    if st is None:
+        raise RuntimeError("get_grad is only valid inside a gradient function registered with register_grad")
+    if not isinstance(x, TensorProxy):
+        return None
+    ph = TensorProxy(like=x, requires_grad=False, prefix="gct")
+    st["get"][ph.name] = x
+    return ph
+
+
+def put_grad(x, g) -> None:
+    """Accumulates ``g`` into the gradient of ``x`` (only inside a ``register_grad`` gradient function)."""
+    st = getattr(_joint, "state", None)
+    if st is None:
+        raise RuntimeError("put_grad is only valid inside a gradient function registered with register_grad")
+    if isinstance(x, TensorProxy) and g is not None:
+        st["put"].append((x, g))
+
+
+def register_grad(sym_or_id, gradfn: Callable) -> None:
+    """Registers a joint forward/backward gradient function for a symbol (see ``get_grad`` /
+    ``put_grad``); it takes precedence like any registered VJP rule."""
+    from .trace import get_tracectx
+
+    def rule(*args, **kwargs):
+        trc = get_tracectx()
+        scope = trc.scopes[-1]
+        n0 = len(scope)
+        prev = getattr(_joint, "state", None)
+        _joint.state = st = {"get": {}, "put": []}
+        try:
+            out = gradfn(*args, **kwargs)
+        finally:
+            _joint.state = prev
+        recorded = scope[n0:]
+        del scope[n0:]
+        # split: backward = ops reached from a get_grad placeholder
+        tainted = set(st["get"])
+        fwd, bwd_ops = [], []
+        for b in recorded:
+            if any(a.name in tainted for a in b.flat_proxy_args):
+                bwd_ops.append(b)
+                tainted.update(o.name for o in b.flat_proxy_outs)
+            else:
+                fwd.append(b)
+        scope.extend(fwd)
+        flat_out = [o for o in tree_flatten(out)[0] if isinstance(o, TensorProxy)]
+        puts = st["put"]
+        placeholders = dict(st["get"])
+
+        def backward(*cts):
+            swap = {}
+            for ph_name, x in placeholders.items():
+                ct = None
+                for o, c in zip(flat_out, cts):
+                    if o is x or o.name == x.name:
+                        ct = c
+                        break
+                if ct is None:
+                    ct = P.full(tuple(x.shape), 0, device=x.device, dtype=x.dtype)
+                swap[ph_name] = ct
+            cur = get_tracectx()
+            for b in bwd_ops:
+                cur.scopes[-1].append(b.swap_proxies(swap, skip_output=True))
+            grads = {}
+            for x, g in puts:
+                if isinstance(g, Proxy) and g.name in swap:
+                    g = swap[g.name]
+                grads[x.name] = g if x.name not in grads else _ltorch().add(grads[x.name], g)
+            return tuple(grads.get(a.name) if isinstance(a, TensorProxy) else None for a in args)
+
+        return out, backward
+
+    register_vjp(sym_or_id)(rule)
+
+
+# -----------------------------------------------------------------------------------------
+# Functional transforms (reference ``vjp`` :3041, ``value_and_grad`` :3068, ``grad`` :1518):
+# evaluated through the compiled program's own forward/backward traces.
+# -----------------------------------------------------------------------------------------
+def _diff_inputs(primals):
+    out = []
+    for p in primals:
+        if isinstance(p, torch.Tensor) and (p.is_floating_point() or p.is_complex()):
+            out.append(p.detach().requires_grad_(True))
+        else:
+            out.append(p)
+    return out
+
+
+def _vjp_run(jf, primals, kwargs, make_cotangents):
+    ins = _diff_inputs(primals)
+    out = jf(*ins, **kwargs)
+    cotangents = make_cotangents(out)
+    flat_out = [o for o in tree_flatten(out)[0] if isinstance(o, torch.Tensor)]
+    flat_ct = tree_flatten(cotangents)[0] if cotangents is not None else []
+    pairs = [(o, c) for o, c in zip(flat_out, flat_ct) if c is not None and o.requires_grad]
+    diff = [p for p in ins if isinstance(p, torch.Tensor) and p.requires_grad]
+    if pairs and diff:
+        grads = torch.autograd.grad([o for o, _ in pairs], diff, [c for _, c in pairs], allow_unused=True)
+    else:
+        grads = [None] * len(diff)
+    it = iter(grads)
+    full = tuple(next(it) if isinstance(p, torch.Tensor) and p.requires_grad else None for p in ins)
+    return out, full
+
+
+def vjp(func):
+    """``vjp(func)(primals, cotangents, **kwargs) -> (outputs, grads)``: outputs of ``func(*primals)``
+    and the vector-Jacobian products of ``cotangents`` w.r.t. each primal (None where not
+    differentiable), computed by the compiled forward and backward programs."""
+    from .. import jit
+
+    jf = jit(func)
+
+    def _vjp(primals, cotangents, **kwargs):
+        if not isinstance(primals, (tuple, list)):
+            primals = (primals,)
+        return _vjp_run(jf, primals, kwargs, lambda out: cotangents)
+
+    return _vjp
+
+
+def value_and_grad(func):
+    """``value_and_grad(func)(*args, **kwargs) -> (value, grads)``: all-ones cotangents."""
+    from .. import jit
+
+    jf = jit(func)
+
+    def ones(out):
+        return tree_map(lambda o: torch.ones_like(o) if isinstance(o, torch.Tensor) and o.is_floating_point() else None, out)
+
+    def _value_and_grad(*args, **kwargs):
+        return _vjp_run(jf, args, kwargs, ones)
+
+    return _value_and_grad
