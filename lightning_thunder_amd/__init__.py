@@ -195,7 +195,8 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
                                "interpretation", "'python interpreter' (bytecode interpreter, default) or "
                                "'torch function mode'", "python interpreter"),
                            record_history=record, sharp_edges=cd.sharp_edges.value,
-                           show_progress=dbg.show_interpreter_progress)
+                           show_progress=dbg.show_interpreter_progress,
+                           symbolic_numbers=cd.cache_option is CACHE_OPTIONS.SYMBOLIC_VALUES)
         cs.last_trace_tracing_stop = time.perf_counter_ns()
         pro, comp, epi = prog.prologue_trace, prog.computation_trace, prog.epilogue_trace
         computation_traces = [comp]
@@ -224,6 +225,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
         pro_exec = transform_for_execution(pro, [pyex])[-1]
         entry.prologue_fn = pro_exec.python_callable()
         entry.prologue_traces = [pro, pro_exec]
+        specialized_at_prologue = set(prog.specialized_args)
 
         requires_grad = (
             entry.grad_enabled
@@ -281,6 +283,22 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             _check_traces(ex_traces, cd)
             entry.computation_fn = c.python_callable()
             entry.computation_traces = computation_traces + ex_traces
+        late = prog.specialized_args - specialized_at_prologue
+        if late:
+            # a transform read a symbolic number's value after the prologue was built: the program
+            # is specialized on it, so the cache entry must check that value too
+            from .executors.pythonex import _check_number
+
+            flat_now, _ = tree_flatten((args, kwargs))
+            vals = {i: flat_now[i] for i in late}
+            base = entry.prologue_fn
+
+            def prologue_with_late_checks(fa, *rest, _base=base, _vals=vals):
+                for i, v in _vals.items():
+                    _check_number(fa[i], v)
+                return _base(fa, *rest)
+
+            entry.prologue_fn = prologue_with_late_checks
     finally:
         _compile_data_ctx.reset(tok)
     return entry

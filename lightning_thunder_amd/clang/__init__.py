@@ -119,11 +119,14 @@ def maybe_convert_to_dtype(a, dtype, *, enforce_safe_casting: bool = False):
             return a
         return prims.convert_element_type(a, dtype)
     if isinstance(a, (Number, NumberProxy)):
-        v = pyval(a)
         if isinstance(dtype, torch.dtype):
             pt = dtypes.dtype_to_numbertype(dtype)
         else:
             pt = dtype
+        if isinstance(a, NumberProxy) and (pt is a.python_type or (pt is float and a.python_type is int)
+                                           or (pt is complex and a.python_type in (int, float))):
+            return a  # a widening conversion the operation performs itself: the number stays symbolic
+        v = pyval(a)
         if pt is int and isinstance(v, float):
             return int(v)
         if pt is bool:

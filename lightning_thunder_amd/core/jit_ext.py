@@ -214,13 +214,20 @@ class AcquiredProgram:
         self.interpreter_log = None
         self.sharp_edges: list[str] = []
         self.n_instructions = 0
+        self.symbolic_args: dict[int, NumberProxy] = {}  # flat-arg index -> symbolic number input
+        self.specialized_args: set[int] = set()  # symbolic inputs whose value the program read
 
 
 def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
             lookasides: dict | None = None, prune_param_checks: bool = True,
             python_lookasides: list | None = None, interpretation: str = "python interpreter",
-            record_history: bool | str = False, sharp_edges: str = "allow", show_progress: bool = False) -> AcquiredProgram:
+            record_history: bool | str = False, sharp_edges: str = "allow", show_progress: bool = False,
+            symbolic_numbers: bool = False) -> AcquiredProgram:
     """Traces ``fn(*args, **kwargs)`` and builds prologue / computation / epilogue traces.
+
+    ``symbolic_numbers`` (``cache="symbolic values"``): int / float arguments become number inputs
+    of the computation, checked by type only, unless the program reads their value (see
+    ``NumberProxy.concrete``), in which case that input is specialized and value-checked.
 
     ``interpretation``: ``"python interpreter"`` (default) runs the user's Python on the bytecode
     interpreter (:mod:`.interpreter`: provenance guards, lookasides on any callable, sharp
@@ -237,6 +244,7 @@ def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module 
             setattr(owner, attr, repl)
     try:
         return _acquire(fn, args, kwargs, module=module, lookasides=lookasides, prune_param_checks=prune_param_checks,
+                        symbolic_numbers=symbolic_numbers,
                         interp_options=None if interpretation != "python interpreter" else dict(
                             record_history=record_history, sharp_edges=sharp_edges, show_progress=show_progress))
     finally:
@@ -297,7 +305,7 @@ def _storage_ptr(x: torch.Tensor):
 
 def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
              lookasides: dict | None = None, prune_param_checks: bool = True,
-             interp_options: dict | None = None) -> AcquiredProgram:
+             interp_options: dict | None = None, symbolic_numbers: bool = False) -> AcquiredProgram:
     prog = AcquiredProgram()
     comp = TraceCtx(fn if not isinstance(fn, torch.nn.Module) else type(fn).forward)
     comp.fn_name = "computation"
@@ -340,6 +348,19 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                         if sp in by_storage:
                             tracker.partial_alias.update((id(p), id(by_storage[sp])))
                         by_storage.setdefault(sp, p)
+            elif symbolic_numbers and type(x) in (int, float):
+                from .proxies import IntegerProxy, FloatProxy
+
+                cls = IntegerProxy if type(x) is int else FloatProxy
+                p = cls(x, name=comp.make_unique_name("i" if type(x) is int else "f"))
+
+                def _specialize(i=i):
+                    prog.specialized_args.add(i)
+
+                p._on_value = _specialize
+                prog.symbolic_args[i] = p
+                proxied_flat.append(p)
+                prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
             else:
                 proxied_flat.append(x)
         pargs, pkwargs = tree_unflatten(proxied_flat, arg_spec)
@@ -635,6 +656,8 @@ def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks
                 prims.check_none(u)
             elif isinstance(x, str):
                 prims.check_string_value(u, x)
+            elif i in prog.symbolic_args and i not in prog.specialized_args:
+                prims.check_number_type(u, type(x))
             elif isinstance(x, (bool, int, float, complex)):
                 prims.check_number_type_and_value(u, x)
             elif isinstance(x, (torch.dtype, torch.device)):

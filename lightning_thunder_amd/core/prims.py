@@ -39,6 +39,7 @@ class PrimIDs(Enum):
     UNPACK_BUFFER = auto()
     CHECK_TENSOR_SHAPE_AND_METADATA = auto()
     CHECK_NUMBER_TYPE_AND_VALUE = auto()
+    CHECK_NUMBER_TYPE = auto()
     CHECK_LEN = auto()
     CHECK_NONE = auto()
     CHECK_STRING_VALUE = auto()
@@ -254,6 +255,9 @@ check_tensor_shape_and_metadata = make_prim(
 check_number_type_and_value = make_prim(
     PrimIDs.CHECK_NUMBER_TYPE_AND_VALUE, "check_number_type_and_value", meta=lambda n, v: None, tags=(OpTags.DONT_DCE,)
 )
+check_number_type = make_prim(
+    PrimIDs.CHECK_NUMBER_TYPE, "check_number_type", meta=lambda n, typ: None, tags=(OpTags.DONT_DCE,)
+)  # symbolic-values inputs: only the Python type is part of the cache key
 check_len = make_prim(PrimIDs.CHECK_LEN, "check_len", meta=lambda x, n: None, tags=(OpTags.DONT_DCE,))
 check_none = make_prim(PrimIDs.CHECK_NONE, "check_none", meta=lambda x: None, tags=(OpTags.DONT_DCE,))
 check_string_value = make_prim(PrimIDs.CHECK_STRING_VALUE, "check_string_value", meta=lambda s, v: None, tags=(OpTags.DONT_DCE,))

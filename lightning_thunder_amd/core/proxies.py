@@ -120,17 +120,78 @@ class NumberProxy(Proxy):
     def type_string(self):
         return self.python_type.__name__
 
+    # A symbolic number (``cache="symbolic values"`` input) stays a trace input only while the
+    # program passes it along to operations; anything that reads its value (Python arithmetic,
+    # comparisons, branching, shapes, ``pyval``) specializes the program on that value: the hook
+    # turns the input's prologue check back into a value check.
+    _on_value = None
+
+    def concrete(self):
+        hook = self._on_value
+        if hook is not None:
+            hook()
+        return self.value
+
     def __index__(self):
-        return int(self.value)
+        return int(self.concrete())
 
     def __int__(self):
-        return int(self.value)
+        return int(self.concrete())
 
     def __float__(self):
-        return float(self.value)
+        return float(self.concrete())
 
     def __bool__(self):
-        return bool(self.value)
+        return bool(self.concrete())
+
+    def __eq__(self, other):
+        if isinstance(other, Proxy):
+            return self is other
+        return self.concrete() == other
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    __hash__ = Proxy.__hash__
+
+    def __round__(self, ndigits=None):
+        return round(self.concrete(), ndigits)
+
+    def __neg__(self):
+        return -self.concrete()
+
+    def __pos__(self):
+        return +self.concrete()
+
+    def __abs__(self):
+        return abs(self.concrete())
+
+
+def _number_binop(name):
+    import operator
+
+    op = getattr(operator, name)
+
+    def fwd(self, other):
+        if isinstance(other, Proxy) and not isinstance(other, NumberProxy):
+            return NotImplemented  # e.g. a tensor: its reflected operator records the op
+        return op(self.concrete(), other.concrete() if isinstance(other, NumberProxy) else other)
+
+    def rev(self, other):
+        if isinstance(other, Proxy) and not isinstance(other, NumberProxy):
+            return NotImplemented
+        return op(other.concrete() if isinstance(other, NumberProxy) else other, self.concrete())
+
+    return fwd, rev
+
+
+for _n in ("add", "sub", "mul", "truediv", "floordiv", "mod", "pow", "and_", "or_", "xor", "lshift", "rshift"):
+    _f, _r = _number_binop(_n)
+    _dn = _n.rstrip("_")
+    setattr(NumberProxy, f"__{_dn}__", _f)
+    setattr(NumberProxy, f"__r{_dn}__", _r)
+for _n in ("lt", "le", "gt", "ge"):
+    setattr(NumberProxy, f"__{_n}__", _number_binop(_n)[0])
 
 
 class IntegerProxy(NumberProxy):
@@ -659,9 +720,9 @@ def proxy(x: Any, *, name: str | None = None):
 
 
 def pyval(x):
-    """Value of a number proxy (or the value itself)."""
+    """Value of a number proxy (or the value itself); reading a symbolic number's value specializes it."""
     if isinstance(x, NumberProxy):
-        return x.value
+        return x.concrete()
     return x
 
 

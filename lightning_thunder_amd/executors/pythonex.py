@@ -57,6 +57,11 @@ def _check_number(n, value):
         raise ThunderCacheMiss(f"number mismatch: {n!r} vs {value!r}")
 
 
+def _check_number_type(n, typ):
+    if type(n) is not typ:
+        raise ThunderCacheMiss(f"number type mismatch: {type(n).__name__} vs {typ.__name__}")
+
+
 def _check_len(x, n):
     if len(x) != n:
         raise ThunderCacheMiss(f"length mismatch: {len(x)} vs {n}")
@@ -80,6 +85,7 @@ def _check_literal_like(x, v):
 for prim, fn, name in (
     (prims.check_tensor_shape_and_metadata, _check_tensor, "check_tensor_metadata"),
     (prims.check_number_type_and_value, _check_number, "check_number_type_and_value"),
+    (prims.check_number_type, _check_number_type, "check_number_type"),
     (prims.check_len, _check_len, "check_len"),
     (prims.check_none, _check_none, "check_none"),
     (prims.check_string_value, _check_string, "check_string_value"),

@@ -220,3 +220,58 @@ def test_returned_input_objects_and_forwarded_provenance():
     assert o1["box"] is b1 and o2["box"] is b2  # the caller's objects of each call come back
     torch.testing.assert_close(o2["y"], x + 2)
     assert int(b1.n) == 1 and int(b2.n) == 1  # in-place updates land on each call's own tensor
+
+
+# ---- cache="symbolic values" (reference CACHE_OPTIONS.SYMBOLIC_VALUES, thunder/core/options.py:45-88) ----
+def test_symbolic_values_reuse_program_across_numbers():
+    def f(x, a, b):
+        return x * a + b
+
+    jf = thunder.jit(f, cache="symbolic values")
+    x = torch.randn(4)
+    for a, b in [(2.0, 1), (3.5, 2), (-1.0, 7)]:
+        torch.testing.assert_close(jf(x, a, b), f(x, a, b))
+    assert thunder.cache_misses(jf) == 1 and thunder.cache_hits(jf) == 2
+    pro = str(thunder.last_prologue_traces(jf)[-1])
+    assert "check_number_type(" in pro and "check_number_type_and_value" not in pro
+    comp = str(thunder.last_traces(jf)[-1])
+    assert "2.0" not in comp  # the number is an input of the program, not a baked constant
+    # a different Python type is a different program
+    jf(x, 2, 1)
+    assert thunder.cache_misses(jf) == 2
+
+
+def test_symbolic_values_specialize_when_value_is_read():
+    def g(x, n):
+        if n > 2:  # branching reads the value: this input is specialized and value-checked
+            return x * n
+        return x - n
+
+    jg = thunder.jit(g, cache="symbolic values")
+    x = torch.randn(6)
+    for n in (3, 5, 1, 3):
+        torch.testing.assert_close(jg(x, n), g(x, n))
+    assert thunder.cache_misses(jg) == 3 and thunder.cache_hits(jg) == 1
+    assert "check_number_type_and_value" in str(thunder.last_prologue_traces(jg)[-1])
+
+    def h(x, n):  # used as a shape
+        return x.reshape(n, -1).sum(0) * n
+
+    jh = thunder.jit(h, cache="symbolic values")
+    for n in (2, 3, 2):
+        torch.testing.assert_close(jh(x, n), h(x, n))
+    assert thunder.cache_misses(jh) == 2
+
+
+def test_symbolic_values_backward():
+    def f(x, a):
+        return (x * a).sin().sum()
+
+    jf = thunder.jit(f, cache="symbolic values")
+    for a in (2.0, 3.0, -0.5):
+        x = torch.randn(5, requires_grad=True)
+        jf(x, a).backward()
+        x2 = x.detach().requires_grad_()
+        f(x2, a).backward()
+        torch.testing.assert_close(x.grad, x2.grad)
+    assert thunder.cache_misses(jf) == 1
