@@ -507,6 +507,124 @@ def _fuse_decode_gemv(trace):
     return new
 
 
+def _decode_group_meta(x, weights, norm=False, norm_weight=None, eps=1e-5, packed=False):
+    if packed:
+        return TensorProxy(like=x, shape=tuple(x.shape[:-1]) + (sum(w.shape[0] for w in weights),))
+    return tuple(TensorProxy(like=x, shape=tuple(x.shape[:-1]) + (w.shape[0],)) for w in weights)
+
+
+def _decode_group_impl(x, weights, norm=False, norm_weight=None, eps=1e-5, packed=False):
+    from ..ops.gemm import gemv_group, gemv_supported
+
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    ok = all(gemv_supported(x2, w) for w in weights)
+    if ok and norm_weight is not None:
+        ok = norm_weight.is_contiguous() and norm_weight.dtype == x.dtype
+    if ok:
+        outs = gemv_group(x2, list(weights), norm=norm, norm_weight=norm_weight, eps=eps, packed=packed)
+    else:
+        if norm:
+            from ..ops.rmsnorm import rms_norm_fwd
+
+            x2, _ = rms_norm_fwd(x2, norm_weight, eps)
+        outs = [torch.nn.functional.linear(x2, w) for w in weights]
+        if packed:
+            outs = torch.cat(outs, -1)
+    if packed:
+        return outs.reshape(*x.shape[:-1], outs.shape[-1])
+    return tuple(o.reshape(*x.shape[:-1], o.shape[-1]) for o in outs)
+
+
+hip_decode_linear_group = ex.register_operator("hip_decode_linear_group", meta=_decode_group_meta,
+                                               fn=_decode_group_impl)
+
+
+def _group_decode_projections(trace):
+    """Sibling decode projections of one input (HF attention's q / k / v: ``hip_decode_linear`` or
+    ``hip_linear`` with <= 8 rows, same x and norm prologue, no bias / residual / activation / gate)
+    -> one ``hip_decode_linear_group`` launch streaming all their weights (up to 3 per launch)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+    groups: dict = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is hip_decode_linear:
+            a = list(b.args) + [None] * (9 - len(b.args))
+            x, w, bias, res, act, gate, norm, g, eps = a[:9]
+            if any(v is not None for v in (bias, res, act, gate)):
+                continue
+        elif b.sym is hip_linear:
+            p = _linear_parts(b)
+            x, w = p["x"], p["w"]
+            if any(p.get(k) is not None for k in ("bias", "residual", "act")):
+                continue
+            norm, g, eps = False, None, 1e-5
+        else:
+            continue
+        if not isinstance(x, TensorProxy) or _rows(x) > _GEMV_MAX_ROWS or w.ndim != 2:
+            continue
+        key = (x.name, bool(norm), getattr(g, "name", None), float(eps) if isinstance(eps, (int, float)) else eps)
+        groups.setdefault(key, []).append(i)
+    replace: dict[int, object] = {}
+    drop: set[int] = set()
+    n = 0
+    # cat(p0, p1, p2, dim=-1) of sibling projections used only by the cat -> one packed launch
+    uses: dict[str, int] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            uses[a.name] = uses.get(a.name, 0) + 1
+    producer = {o.name: i for i, b in enumerate(bsyms) for o in b.flat_proxy_outs}
+    member = {i: key for key, idxs in groups.items() for i in idxs}
+    for ci, cb in enumerate(bsyms):
+        if cb.sym.name not in ("cat", "torch_cat", "cat_prim") or not cb.args or not isinstance(cb.args[0], (list, tuple)):
+            continue
+        parts = cb.args[0]
+        dim = cb.args[1] if len(cb.args) > 1 else cb.kwargs.get("dim", 0)
+        if not 2 <= len(parts) <= 3 or not all(isinstance(p, TensorProxy) for p in parts) or dim not in (-1, parts[0].ndim - 1):
+            continue
+        js = [producer.get(p.name) for p in parts]
+        if any(j is None or j in drop or j in replace or uses.get(p.name) != 1 for j, p in zip(js, parts)):
+            continue
+        keys = {member.get(j) for j in js}
+        if len(keys) != 1 or None in keys:
+            continue
+        (xname, norm, gname, eps), = keys
+        first = bsyms[js[0]]
+        g = (first.args[7] if len(first.args) > 7 else first.kwargs.get("norm_weight")) if norm else None
+        ws = tuple(bsyms[j].args[1] for j in js)
+        replace[ci] = ex.bind_call_ctx(hip_decode_linear_group.bind(first.args[0], ws, norm, g, eps, True,
+                                                                    output=cb.output))
+        drop.update(js)
+        for key_idxs in groups.values():
+            for j in js:
+                if j in key_idxs:
+                    key_idxs.remove(j)
+        n += 1
+    for (xname, norm, gname, eps), idxs in groups.items():
+        for c0 in range(0, len(idxs) - 1, 3):
+            chunk = idxs[c0:c0 + 3]
+            if len(chunk) < 2:
+                continue
+            first = bsyms[chunk[0]]
+            x = first.args[0]
+            g = None
+            if norm:
+                g = first.args[7] if len(first.args) > 7 else first.kwargs.get("norm_weight")
+            ws = tuple(bsyms[j].args[1] for j in chunk)
+            outs = tuple(bsyms[j].output for j in chunk)
+            replace[chunk[0]] = ex.bind_call_ctx(hip_decode_linear_group.bind(x, ws, norm, g, eps, output=outs))
+            drop.update(chunk[1:])
+            n += 1
+    if not n:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {n} grouped decode projection launch(es)"))
+    return new
+
+
 def _qkv_rope_cache_meta(qkv, cos, sin, n_head, n_query_groups, head_size, rope_n, kc, vc, pos):
     B, T, _ = qkv.shape
     return TensorProxy(like=qkv, shape=(B, n_head, T, head_size)), TensorProxy(like=kc), TensorProxy(like=vc)
@@ -556,9 +674,20 @@ def _fuse_kv_cache_writes(trace):
             continue
         if pk.dtype != torch.int64 or bk.dtype != k.dtype or bv.dtype != v.dtype:
             continue
-        nb = hip_qkv_rope_cache.bind(*b.args, bk, bv, pk, output=(q, ck.output, cv.output))
-        replace[i] = ex.bind_call_ctx(nb)
-        drop.update((uk[0], uv[0]))
+        nb = ex.bind_call_ctx(hip_qkv_rope_cache.bind(*b.args, bk, bv, pk, output=(q, ck.output, cv.output)))
+        # the fused op needs the caches and positions: emit it where the RoPE was when they exist
+        # there (LitGPT), else at the later cache write (HF computes the positions after the RoPE),
+        # provided nothing reads q in between
+        producer_pos = {o.name: j for j, bb in enumerate(bsyms) for o in bb.flat_proxy_outs}
+        ready = max([producer_pos.get(x.name, -1) for x in (bk, bv, pk)] + [-1])
+        if ready < i:
+            at = i
+        else:
+            at = max(uk[0], uv[0])
+            if any(i < j < at for j in uses.get(q.name, [])) or ready >= at:
+                continue
+        replace[at] = nb
+        drop.update({i, uk[0], uv[0]} - {at})
     if not replace:
         return trace
     new = from_trace(trace)
@@ -617,7 +746,8 @@ def _fuse_rms_bwd_residual(trace):
 
 
 def _post_claim(trace):
-    return _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace))))
+    return _group_decode_projections(
+        _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace)))))
 
 
 ex.post_claim_pass = _post_claim

@@ -56,12 +56,22 @@ struct Log2<1> {
 // GATED: the block streams 4 rows of w and the same 4 rows of w2 and writes act(x w^T) * (x w2^T)
 //   (SwiGLU / GeGLU: the two up-projections and the gate in one launch); both products are
 //   rounded to T first, as the unfused linear -> swiglu chain stores them.
-template <typename T, int MM, bool NORM, bool GATED, int U, int KR>
-__global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w,
+// GROUP: up to 3 projections of the same x (e.g. attention q / k / v, each with its own weight and
+// output) in one launch; blocks [0, b0) compute segment 0, [b0, b0 + b1) segment 1, the rest 2.
+struct GemvGroup {
+  const void* w[3];
+  void* y[3];
+  int n[3];
+  int blocks[2];
+  int64_t ldw[3], ldy[3];
+};
+
+template <typename T, int MM, bool NORM, bool GATED, int U, int KR, bool GROUP = false>
+__global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, const T* __restrict__ w_,
                                                    const T* __restrict__ w2, const T* __restrict__ g, float eps,
                                                    const T* __restrict__ bias, const T* __restrict__ res,
-                                                   T* __restrict__ y, int M, int N, int K, int64_t ldx, int64_t ldw,
-                                                   int64_t ldy, int64_t ldr, int act) {
+                                                   T* __restrict__ y_, int M, int N_, int K, int64_t ldx, int64_t ldw_,
+                                                   int64_t ldy_, int64_t ldr, int act, GemvGroup grp = GemvGroup{}) {
   constexpr int V = MM * KR;  // partial sums per lane (power of two, <= 64)
   constexpr int LOGV = Log2<V>::value;
   constexpr int NV = Vec16<T>::N;
@@ -69,7 +79,28 @@ __global__ __launch_bounds__(256) void gemv_kernel(const T* __restrict__ x, cons
   static_assert(V <= 64 && (V & (V - 1)) == 0, "V must be a power of two <= 64");
   __shared__ float part[kWaves][V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * COLS;
+  const T* w = w_;
+  T* y = y_;
+  int N = N_;
+  int64_t ldw = ldw_, ldy = ldy_;
+  int blk = blockIdx.x;
+  if constexpr (GROUP) {
+    int sg = 0;
+    if (blk >= grp.blocks[0]) {
+      blk -= grp.blocks[0];
+      sg = 1;
+      if (blk >= grp.blocks[1]) {
+        blk -= grp.blocks[1];
+        sg = 2;
+      }
+    }
+    w = (const T*)grp.w[sg];
+    y = (T*)grp.y[sg];
+    N = grp.n[sg];
+    ldw = grp.ldw[sg];
+    ldy = grp.ldy[sg];
+  }
+  const int n0 = blk * COLS;
 
   const T* wrow[KR];
 #pragma unroll
@@ -283,8 +314,66 @@ int launch(const void* x, const void* w, const void* w2, const void* g, int norm
   return (int)hipGetLastError();
 }
 
+template <typename T, int MM, bool NORM, int KR>
+void launch_group(const T* x, const T* g, float eps, int M, int K, int64_t ldx, GemvGroup grp, int nseg,
+                  hipStream_t s) {
+  int total = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const int b = (grp.n[i] + KR - 1) / KR;
+    if (i < 2) grp.blocks[i] = b;
+    total += b;
+  }
+  for (int i = nseg; i < 2; ++i) grp.blocks[i] = 1 << 30;
+  const int steps = (K + kWaves * kStep - 1) / (kWaves * kStep);
+  dim3 grid(total), block(256);
+#define LTA_G(UU)                                                                                                  \
+  hipLaunchKernelGGL((gemv_kernel<T, MM, NORM, false, UU, KR, true>), grid, block, 0, s, x, (const T*)nullptr,      \
+                     (const T*)nullptr, g, eps, (const T*)nullptr, (const T*)nullptr, (T*)nullptr, M, 0, K, ldx,    \
+                     (int64_t)0, (int64_t)0, (int64_t)0, 0, grp)
+  if (MM <= 2 && steps >= 3) { LTA_G((MM <= 2 ? 4 : 1)); }
+  else if (MM <= 4 && steps >= 2) { LTA_G((MM <= 4 ? 2 : 1)); }
+  else { LTA_G(1); }
+#undef LTA_G
+}
+
+template <typename T, bool NORM>
+int launch_group_m(const void* x, const void* g, float eps, int M, int K, int64_t ldx, GemvGroup grp, int nseg,
+                   hipStream_t s) {
+  const T* xp = (const T*)x;
+  const T* gp = (const T*)g;
+  if (M == 1) launch_group<T, 1, NORM, 4>(xp, gp, eps, M, K, ldx, grp, nseg, s);
+  else if (M == 2) launch_group<T, 2, NORM, 4>(xp, gp, eps, M, K, ldx, grp, nseg, s);
+  else if (M <= 4) launch_group<T, 4, NORM, kRows>(xp, gp, eps, M, K, ldx, grp, nseg, s);
+  else launch_group<T, 8, NORM, kRows>(xp, gp, eps, M, K, ldx, grp, nseg, s);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 }  // namespace lta
+
+// Grouped decode projections: y_i[M, N_i] = x' w_i^T for i < nseg (<= 3) in one launch, x' = x or
+// rmsnorm(x, g, eps) (norm != 0).  w_i [N_i, K] (row stride ldw_i), y_i row stride ldy_i.
+LTA_EXPORT int lta_gemv_group(int dtype, const void* x, const void* g, int norm, float eps, int nseg,
+                              const void* const* ws, void* const* ys, const int* ns, const int64_t* ldws,
+                              const int64_t* ldys, int M, int K, int64_t ldx, void* stream) {
+  using namespace lta;
+  if (M < 1 || M > 8 || nseg < 1 || nseg > 3 || K < 8 || K % 8 || ldx % 8) return (int)hipErrorInvalidValue;
+  GemvGroup grp{};
+  for (int i = 0; i < nseg; ++i) {
+    if (ldws[i] % 8 || ns[i] < 1) return (int)hipErrorInvalidValue;
+    grp.w[i] = ws[i];
+    grp.y[i] = ys[i];
+    grp.n[i] = ns[i];
+    grp.ldw[i] = ldws[i];
+    grp.ldy[i] = ldys[i];
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == kBF16) return norm ? launch_group_m<__hip_bfloat16, true>(x, g, eps, M, K, ldx, grp, nseg, s)
+                                  : launch_group_m<__hip_bfloat16, false>(x, g, eps, M, K, ldx, grp, nseg, s);
+  if (dtype == kF16) return norm ? launch_group_m<__half, true>(x, g, eps, M, K, ldx, grp, nseg, s)
+                                 : launch_group_m<__half, false>(x, g, eps, M, K, ldx, grp, nseg, s);
+  return (int)hipErrorInvalidValue;
+}
 
 // x [M, K] (row stride ldx), w (and w2) [N, K] (row stride ldw), y [M, N]; K % 8 == 0, 16-byte aligned
 // rows.  norm != 0: x -> rmsnorm(x, g, eps) first; w2 != null: y = act(x w^T) * (x w2^T) (no bias/residual).

@@ -147,6 +147,42 @@ def gemv_nt(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, act=N
     return out
 
 
+register_signature("lta_gemv_group", [c_int, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_int, c_int, ctypes.c_int64, c_void_p])
+
+
+def gemv_group(x: torch.Tensor, weights, *, norm: bool = False, norm_weight=None, eps: float = 1e-5,
+               packed: bool = False):
+    """``[x' @ w.T for w in weights]`` (<= 3 weights sharing x, e.g. attention q / k / v) in ONE
+    weight-streaming launch; ``x' = rmsnorm(x) * norm_weight`` when ``norm``.  ``packed``: the
+    outputs are adjacent column ranges of one [M, sum N] tensor (returned alone), e.g. the fused
+    qkv row a RoPE kernel splits."""
+    assert 1 <= len(weights) <= 3
+    lib = require()
+    M, K = x.shape
+    if packed:
+        total = sum(w.shape[0] for w in weights)
+        buf = torch.empty((M, total), dtype=x.dtype, device=x.device)
+        outs, off = [], 0
+        for w in weights:
+            outs.append(buf[:, off:off + w.shape[0]])
+            off += w.shape[0]
+    else:
+        outs = [torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device) for w in weights]
+    n = len(weights)
+    ws = (ctypes.c_void_p * 3)(*[w.data_ptr() for w in weights], *([None] * (3 - n)))
+    ys = (ctypes.c_void_p * 3)(*[o.data_ptr() for o in outs], *([None] * (3 - n)))
+    ns = (ctypes.c_int * 3)(*[w.shape[0] for w in weights], *([0] * (3 - n)))
+    ldw = (ctypes.c_int64 * 3)(*[w.stride(0) for w in weights], *([0] * (3 - n)))
+    ldy = (ctypes.c_int64 * 3)(*[o.stride(0) for o in outs], *([0] * (3 - n)))
+    rc = lib.lta_gemv_group(dcode(x), x.data_ptr(), None if norm_weight is None else norm_weight.data_ptr(), int(norm),
+                            float(eps), n, ctypes.cast(ws, c_void_p), ctypes.cast(ys, c_void_p), ctypes.cast(ns, c_void_p),
+                            ctypes.cast(ldw, c_void_p), ctypes.cast(ldy, c_void_p), M, K, x.stride(0),
+                            stream_ptr(x.device))
+    check(rc, "lta_gemv_group")
+    return buf if packed else outs
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` choosing, once per shape, the faster of the hand-written
     kernel (MFMA GEMM, or the weight-streaming GEMV for M <= 8; epilogue fused) and hipBLASLt +

@@ -17,6 +17,8 @@ from .base import BaseRecipe
 
 
 from ..transforms.inplace_index_copy import InplaceIndexCopyTransform  # noqa: E402
+from ..transforms.sdpa_gqa import SDPAGQATransform  # noqa: E402
+from ..transforms.hf_rope import HFRoPETransform  # noqa: E402
 
 
 class HFTransformers(BaseRecipe):
@@ -39,7 +41,7 @@ class HFTransformers(BaseRecipe):
         return cfg
 
     def setup_transforms(self):
-        return super().setup_transforms() + [InplaceIndexCopyTransform()]
+        return super().setup_transforms() + [HFRoPETransform(), SDPAGQATransform(), InplaceIndexCopyTransform()]
 
     def apply(self, model):
         """Compiles ``model`` and makes HF generation run on the compiled forward.

@@ -665,6 +665,9 @@ def test_decode_gemv_fusion_in_hf_llama_decode():
     out = tm.generate(x, **kw)
     trace = str(thunder.last_traces(tm)[-1])
     assert "hip_decode_linear" in trace and "'silu'" in trace, trace
+    # HF attention prologue: packed q/k/v projection, fused split-RoPE writing the static caches
+    assert "hip_decode_linear_group" in trace and "hip_qkv_rope_cache" in trace, trace
+    assert "index_copy" not in trace, trace
     assert (out == ref).float().mean() > 0.8  # greedy tokens of a random model: bf16 rounding may flip a late one
 
 
@@ -697,3 +700,23 @@ def test_hf_generate_hipgraph_matches_uncaptured():
     # the cache the first call returned (the storage its decode graph was captured on) is untouched
     for l, (k, v) in zip(kept.layers, snap):
         assert torch.equal(l.keys, k) and torch.equal(l.values, v)
+
+
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("ns", [(2048, 512, 512), (384, 1000)])
+def test_gemv_group_matches_separate_projections(M, norm, ns):
+    """Grouped decode projections (q / k / v of HF attention) in one launch."""
+    from lightning_thunder_amd.ops.gemm import gemv_group
+
+    torch.manual_seed(0)
+    K = 2048
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    ws = [torch.randn(n, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5 for n in ns]
+    g = torch.randn(K, device="cuda", dtype=torch.bfloat16) if norm else None
+    outs = gemv_group(x, ws, norm=norm, norm_weight=g, eps=1e-5)
+    xf = x.float()
+    if norm:
+        xf = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()).bfloat16().float()
+    for o, w in zip(outs, ws):
+        torch.testing.assert_close(o.float(), xf @ w.float().t(), atol=2e-2, rtol=2e-2)

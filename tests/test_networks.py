@@ -155,6 +155,9 @@ def test_hf_generate_static_cache_through_recipe():
         assert torch.equal(out, ref), (out, ref)
     assert thunder.cache_misses(tm) == 2  # one prefill and one decode program
     assert thunder.cache_hits(tm) >= 25
+    # repeat_kv is not materialised: SDPA reads the grouped KV cache directly
+    comp = [t for t in thunder.last_traces(tm) if "SDPAGQATransform" in str(t.get_provenance())]
+    assert comp and "enable_gqa=True" in str(comp[-1]) and "expand(" not in str(comp[-1])
 
 
 @pytest.mark.parametrize("name", ["llama2-like", "mixtral-like"])
@@ -177,3 +180,22 @@ def test_litgpt_init_weights_after_to_empty(name):
     idx = torch.randint(0, m.config.vocab_size, (1, 16))
     logits = m(idx)
     assert torch.isfinite(logits).all() and logits.std() > 0
+
+
+def test_hf_rope_transform_rewrites_attention_prologue():
+    """HF rotate-half RoPE on q / k (three projections of one input) -> one concatenated projection
+    + the fused split-RoPE op (trace structure; the GPU test runs it)."""
+    from lightning_thunder_amd.transforms.hf_rope import HFRoPETransform
+
+    cfg = tf.LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
+    m = tf.LlamaForCausalLM(cfg).eval()
+    m.requires_grad_(False)
+    comp = thunder.trace(m, torch.randint(1, 128, (1, 8)))
+    _, new, _ = HFRoPETransform(require_gpu=False).transform_traces_pre_prologue(None, comp, None)
+    s = str(new)
+    assert s.count("hip_qkv_rope(") == 2  # one per layer
+    assert "ltorch.neg(" not in s  # the rotate_half chains are gone
+    # on CPU tensors the transform stays off by default
+    _, same, _ = HFRoPETransform().transform_traces_pre_prologue(None, comp, None)
+    assert same is comp
