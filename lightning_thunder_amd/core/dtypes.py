@@ -34,12 +34,19 @@ float8_e4m3fnuz = torch.float8_e4m3fnuz
 float8_e5m2fnuz = torch.float8_e5m2fnuz
 
 float8_dtypes = (float8_e4m3fn, float8_e5m2, float8_e4m3fnuz, float8_e5m2fnuz)
-low_precision_dtypes = (bfloat16, float16, complex32) + float8_dtypes
+# Microscaling (OCP MX) storage types, both native to the CDNA4 block-scaled MFMA
+# (v_mfma_scale_f32_*_f8f6f4): packed fp4 e2m1 (two values per byte) and the E8M0 power-of-two
+# block scale.  Tensors of these types are storage (quantized weights, scales); arithmetic happens
+# in the kernels that consume them.
+float4_e2m1fn_x2 = getattr(torch, "float4_e2m1fn_x2", None)
+float8_e8m0fnu = getattr(torch, "float8_e8m0fnu", None)
+mx_storage_dtypes = tuple(d for d in (float4_e2m1fn_x2, float8_e8m0fnu) if d is not None)
+low_precision_dtypes = (bfloat16, float16, complex32) + float8_dtypes + mx_storage_dtypes
 float_dtypes = (bfloat16, float16, float32, float64) + float8_dtypes
 complex_dtypes = (complex32, complex64, complex128)
 signed_int_dtypes = (int8, int16, int32, int64)
 int_dtypes = (uint8,) + signed_int_dtypes
-all_dtypes = (bool8,) + int_dtypes + float_dtypes + complex_dtypes
+all_dtypes = (bool8,) + int_dtypes + float_dtypes + complex_dtypes + mx_storage_dtypes
 
 _short_names = {
     bool8: "b8",
@@ -60,6 +67,10 @@ _short_names = {
     float8_e4m3fnuz: "f8_e4m3fnuz",
     float8_e5m2fnuz: "f8_e5m2fnuz",
 }
+if float4_e2m1fn_x2 is not None:
+    _short_names[float4_e2m1fn_x2] = "f4_e2m1x2"
+if float8_e8m0fnu is not None:
+    _short_names[float8_e8m0fnu] = "f8_e8m0"
 
 number_types = (bool, int, float, complex)
 
@@ -119,6 +130,11 @@ def is_low_precision_dtype(d) -> bool:
 
 def is_float8_dtype(d) -> bool:
     return d in float8_dtypes
+
+
+def is_mx_storage_dtype(d) -> bool:
+    """Packed fp4 (e2m1 x2) or E8M0 scale storage."""
+    return d in mx_storage_dtypes
 
 
 def is_weak_dtype(d) -> bool:
@@ -263,5 +279,6 @@ __all__ = [
     "bool8", "uint8", "int8", "int16", "int32", "int64", "bfloat16", "float16", "float32", "float64",
     "complex32", "complex64", "complex128", "float8_e4m3fn", "float8_e5m2", "float8_e4m3fnuz", "float8_e5m2fnuz",
     "to_dtype", "to_torch_dtype", "is_float_dtype", "is_integer_dtype", "is_complex_dtype", "is_boolean_dtype",
-    "is_low_precision_dtype", "is_float8_dtype", "itemsize", "short_name",
+    "is_low_precision_dtype", "is_float8_dtype", "is_mx_storage_dtype", "itemsize", "short_name",
+    "float4_e2m1fn_x2", "float8_e8m0fnu", "mx_storage_dtypes",
 ]

@@ -21,4 +21,6 @@ with open(os.path.join(out_dir, "decode_final.py"), "w") as f:
     f.write(str(traces[-1]))
 with open(os.path.join(out_dir, "decode_first.py"), "w") as f:
     f.write(str(traces[0]))
+with open(os.path.join(out_dir, "decode_pregraph.py"), "w") as f:
+    f.write(str(traces[-2]))
 print("ok", len(traces))
