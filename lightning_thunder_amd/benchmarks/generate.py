@@ -93,7 +93,13 @@ def run(mode: str, args) -> dict:
         else:
             from ..transforms.hipgraph import HipGraphTransform
 
-            fwd = thunder.jit(model, transforms=[HipGraphTransform()])
+            transforms = [HipGraphTransform()]
+            if mode == "hipgraph_mxfp4":
+                # 4-bit weights (OCP MXFP4, every linear incl. the LM head), bf16 activations
+                from ..transforms.mxfp4_inference import MXFP4InferenceTransform
+
+                transforms.insert(0, MXFP4InferenceTransform(skip=()))
+            fwd = thunder.jit(model, transforms=transforms)
 
         def once():
             return generate(model, prompt, args.new_tokens, forward=fwd)
@@ -118,7 +124,8 @@ def run(mode: str, args) -> dict:
         "model_impl": "transformers.LlamaForCausalLM" if mode.startswith("hf_") else "lightning_thunder_amd litgpt GPT",
         "mode": mode, "value": round(ms, 2), "unit": "ms", "higher_is_better": False,
         "ms_per_token": round(ms / args.new_tokens, 3), "first_call_s": round(first, 2),
-        "prompt_len": args.prompt_len, "new_tokens": args.new_tokens, "dtype": "bf16",
+        "prompt_len": args.prompt_len, "new_tokens": args.new_tokens,
+        "dtype": "mxfp4 weights, bf16 activations" if mode.endswith("mxfp4") else "bf16",
         "data": "synthetic prompt, random-init weights", "n_gpus": 1,
         "reference_ms": {"thunder+cudagraphs (1xH100)": 542, "eager (1xH100)": 1493},
     }

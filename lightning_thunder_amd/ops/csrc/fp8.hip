@@ -37,14 +37,32 @@ __device__ __forceinline__ float dev_scale(const float* amax_in, float fmax, flo
   return s;
 }
 
+// 8 consecutive elements as fp32 (one 16-B load for bf16, two for fp32)
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float (&o)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const Vec16<T> a = load16(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = to_f32(a.v[j]);
+  } else {
+    const Vec16<T> a = load16(p), b = load16(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = to_f32(a.v[j]);
+      o[4 + j] = to_f32(b.v[j]);
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void amax_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ amax) {
   float m = 0.f;
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const Vec16<T> v = load16(x + i * 8);
+    float v[8];
+    load8(x + i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(to_f32(v.v[j])));
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
   }
   // one atomic per workgroup: same-address atomics serialise in L2 (MI355X_MICROARCH.md §atomics)
   __shared__ float red[4];
@@ -62,11 +80,12 @@ __global__ __launch_bounds__(256) void cast_kernel(const T* __restrict__ x, uint
   float m = 0.f;
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const Vec16<T> v = load16(x + i * 8);
+    float v[8];
+    load8(x + i * 8, v);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float f = to_f32(v.v[j]);
+      const float f = v[j];
       m = fmaxf(m, fabsf(f));
       const uint32_t q = E5M2 ? to_e5m2(f * s) : to_e4m3(f * s);
       if (j < 4) lo |= q << (8 * j);
@@ -102,11 +121,12 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const T* __restrict
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int r = tr + 32 * p;
-      const Vec16<T> v = load16(x + (int64_t)(r0 + r) * C + c0 + tc);
+      float v[8];
+      load8(x + (int64_t)(r0 + r) * C + c0 + tc, v);
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float f = to_f32(v.v[j]);
+        const float f = v[j];
         m = fmaxf(m, fabsf(f));
         const uint32_t q = E5M2 ? to_e5m2(f * s) : to_e4m3(f * s);
         tile[r][tc + j] = (uint8_t)q;
@@ -180,11 +200,13 @@ __global__ __launch_bounds__(256) void mx_cast_transpose_kernel(const T* __restr
   float v[16];
   {
     const T* src = x + (int64_t)(r0 + tr) * C + c0 + tq * 16;
-    const Vec16<T> a = load16(src), b = load16(src + 8);
+    float a[8], b[8];
+    load8(src, a);
+    load8(src + 8, b);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      v[j] = to_f32(a.v[j]);
-      v[8 + j] = to_f32(b.v[j]);
+      v[j] = a[j];
+      v[8 + j] = b[j];
     }
   }
   float m = 0.f;
@@ -223,6 +245,54 @@ __global__ __launch_bounds__(256) void mx_cast_transpose_kernel(const T* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// MXFP4: blocks of 32 consecutive elements along the last dim share an E8M0 scale
+// X = 2^ceil-variant(log2(amax / 6)) (as MXFP8 above: the exponent is rounded up when amax's
+// mantissa exceeds 1.5, so no element saturates); elements x / X round to nearest-even e2m1
+// {0, .5, 1, 1.5, 2, 3, 4, 6} and are packed two per byte, low nibble first.  One thread per
+// block: 64 B of bf16 in, 16 B + 1 scale byte out.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t e2m1_code(float v) {
+  const float a = fabsf(v);
+  uint32_t c = a <= 0.25f ? 0u : a < 0.75f ? 1u : a <= 1.25f ? 2u : a < 1.75f ? 3u
+             : a <= 2.5f ? 4u : a < 3.5f ? 5u : a <= 5.f ? 6u : 7u;
+  return c | (v < 0.f && c != 0u ? 8u : 0u);
+}
+
+__device__ __forceinline__ uint32_t mx4_exp(float amax) {
+  if (!(amax > 0.f)) return 0u;
+  const uint32_t bits = __float_as_uint(amax);
+  const int e = (int)((bits >> 23) & 0xff) - 127;
+  const bool above = (bits & 0x7fffff) > 0x400000u;  // mantissa > 1.5 (e2m1 max = 1.5 * 2^2)
+  return (uint32_t)min(max(e - 2 + (above ? 1 : 0) + 127, 0), 254);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mx4_cast_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
+                                                       uint8_t* __restrict__ sq, int64_t nblocks) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const T* src = x + b * 32;
+  float v[32];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float a[8];
+    load8(src + 8 * i, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[8 * i + j] = a[j];
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) m = fmaxf(m, fabsf(v[j]));
+  const uint32_t be = mx4_exp(m);
+  const float inv = e8m0_inv(be);
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 32; ++j) w[j >> 3] |= e2m1_code(v[j] * inv) << (4 * (j & 7));
+  *reinterpret_cast<uint4*>(q + b * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  sq[b] = (uint8_t)be;
+}
+
 // one wave, 16x16x128 block-scaled MFMA with per-lane E8M0 scale registers (scale-operand probe)
 __global__ void mfma_scale_probe_kernel(const v8i* __restrict__ a, const v8i* __restrict__ b,
                                         const int* __restrict__ sa, const int* __restrict__ sb,
@@ -242,6 +312,12 @@ __global__ void mfma_probe_kernel(const v8i* __restrict__ a, const v8i* __restri
     acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   else if (fmt_a == 1 && fmt_b == 0)
     acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 1, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  else if (fmt_a == 4 && fmt_b == 4)  // fp4 e2m1 x fp4 e2m1: 16 operand bytes per lane
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 4, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  else if (fmt_a == 0 && fmt_b == 4)  // fp8 e4m3 x fp4 e2m1
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 0, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  else if (fmt_a == 4 && fmt_b == 0)
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 4, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   c[l] = acc;
 }
 
@@ -327,6 +403,21 @@ LTA_EXPORT int lta_mx_cast_transpose(int in_dtype, int e5m2, const void* x, void
     return -1;
   }
 #undef LTA_MX
+  return (int)hipGetLastError();
+}
+
+// x [R, C] (C % 32 == 0, contiguous) -> q [R, C/2] packed e2m1 + s [R, C/32] E8M0 (MXFP4).
+LTA_EXPORT int lta_mxfp4_cast(int in_dtype, const void* x, void* q, void* s, int64_t numel, hipStream_t stream) {
+  if (numel % 32) return -2;
+  const int64_t nb = numel / 32;
+  dim3 grid((unsigned)((nb + 255) / 256)), block(256);
+  if (in_dtype == kBF16)
+    hipLaunchKernelGGL(mx4_cast_kernel<__hip_bfloat16>, grid, block, 0, stream, (const __hip_bfloat16*)x,
+                       (uint8_t*)q, (uint8_t*)s, nb);
+  else if (in_dtype == kF32)
+    hipLaunchKernelGGL(mx4_cast_kernel<float>, grid, block, 0, stream, (const float*)x, (uint8_t*)q, (uint8_t*)s, nb);
+  else
+    return -1;
   return (int)hipGetLastError();
 }
 

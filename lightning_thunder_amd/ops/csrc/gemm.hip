@@ -630,6 +630,123 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_fp8_kernel(const char* __rest
 }
 
 // ---------------------------------------------------------------------------------------------
+// MXFP4 (OCP e2m1 elements, E8M0 scale per 32 along K) NT GEMM on the same block-scaled MFMA with
+// format 4 (4x the bf16 rate per clock).  Operands are packed two elements per byte (low nibble =
+// even k), so a K-step of 256 elements is the same 128-B LDS row as the fp8 kernel's and staging /
+// swizzle are byte-identical; each K-step runs two 16x16x128 sub-steps.  e2m1 operand map of the
+// MFMA (measured, tests/test_mxfp4.py): lane l holds row l&15, k = 32 (l>>4) + 2 j + nibble in
+// byte j of its first four registers, i.e. 16-B chunk 4 s + (l>>4) of sub-step s; the scale of lane
+// group g is that of k-block g of the sub-step.  Scales: 8 per row per K-step, staged as two 4-byte
+// global_load_lds per lane (halves h = 0, 1 hold k-blocks 4h..4h+3).
+// ---------------------------------------------------------------------------------------------
+template <bool BIAS>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_mxfp4_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                               __hip_bfloat16* __restrict__ C,
+                                                               const __hip_bfloat16* __restrict__ bias, int M, int N,
+                                                               int K, int lda, int ldb, int ldc,
+                                                               const uint8_t* __restrict__ SA,
+                                                               const uint8_t* __restrict__ SB) {
+  constexpr int SCALE_BYTES = 2 * 2 * 256 * 4;  // per stage: 2 halves x (A rows, B rows) x 4 B
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES + 2 * SCALE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  constexpr int BKB = 128;  // bytes (= 256 e2m1 elements) per K-step
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / 256;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ksc = K / 32;
+  char* const sc_base = smem + 2 * STAGE_BYTES;
+  auto stage_scales = [&](int t, int buf) {
+    const int row = (wave & 3) * 64 + lane;
+    const uint8_t* src = wave < 4 ? SA + (int64_t)(m0 + row) * ksc + t * 8 : SB + (int64_t)(n0 + row) * ksc + t * 8;
+    char* dst = sc_base + buf * SCALE_BYTES + wave * 256;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 4), (lds_void*)(dst + 2048), 4, 0, 0);
+  };
+  stage_tile_bytes(A, B, lda, ldb, m0, n0, 0, smem, wave, lane);
+  stage_scales(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) {
+      stage_tile_bytes(A, B, lda, ldb, m0, n0, (t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+      stage_scales(t + 1, (t + 1) & 1);
+    }
+    const uint8_t* scs = reinterpret_cast<const uint8_t*>(sc_base + (t & 1) * SCALE_BYTES);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 4 * h + fq;
+      v8i af[8], bfr[4];
+      int ea[8], eb[4];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int row = wm * 128 + m * 16 + fr;
+        const uint4 v = *reinterpret_cast<const uint4*>(cur + row * 128 + ((c ^ (row & 7)) << 4));
+        af[m] = v8i{(int)v.x, (int)v.y, (int)v.z, (int)v.w, 0, 0, 0, 0};
+        ea[m] = scs[h * 2048 + row * 4 + fq];
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row = wn * 64 + n * 16 + fr;
+        const uint4 v = *reinterpret_cast<const uint4*>(cur + TILE_BYTES + row * 128 + ((c ^ (row & 7)) << 4));
+        bfr[n] = v8i{(int)v.x, (int)v.y, (int)v.z, (int)v.w, 0, 0, 0, 0};
+        eb[n] = scs[h * 2048 + 1024 + row * 4 + fq];
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma_mx<4, 4>(af[m], bfr[n], acc[m][n], ea[m], eb[n]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 64 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) =
+            __float2bfloat16(acc[m][n][j] + bv);
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+    *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * ldc + n0 + wn * 64 + ch * 8) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // K10: grouped NT GEMM for mixture-of-experts: rows [off[g-1], off[g]) of A are multiplied by
 // expert g's weight W[g] ([N, K], K-contiguous like nn.Linear), out[M, N] bf16.  The grid is
 // sized for the worst case (ceil(M/256) + G row tiles per column tile); each workgroup finds
@@ -806,6 +923,22 @@ LTA_EXPORT int lta_gemm_nt_mxfp8(const void* A, const void* B, void* C, const vo
   else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_MX8(0, 1, true); else LTA_MX8(0, 1, false); }
   else return -1;
 #undef LTA_MX8
+  return (int)hipGetLastError();
+}
+
+// MXFP4: A [M, K/2], B [N, K/2] packed e2m1 (lda / ldb in bytes), SA [M, K/32], SB [N, K/32] E8M0.
+LTA_EXPORT int lta_gemm_nt_mxfp4(const void* A, const void* B, void* C, const void* bias, const void* SA, const void* SB,
+                                 int M, int N, int K, int lda, int ldb, int ldc, hipStream_t stream) {
+  if (M % BM || N % BN || K % 256 || lda % 16 || ldb % 16) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+  if (bias != nullptr)
+    hipLaunchKernelGGL((gemm_nt_mxfp4_kernel<true>), grid, block, 0, stream, (const char*)A, (const char*)B,
+                       (__hip_bfloat16*)C, (const __hip_bfloat16*)bias, M, N, K, lda, ldb, ldc, (const uint8_t*)SA,
+                       (const uint8_t*)SB);
+  else
+    hipLaunchKernelGGL((gemm_nt_mxfp4_kernel<false>), grid, block, 0, stream, (const char*)A, (const char*)B,
+                       (__hip_bfloat16*)C, (const __hip_bfloat16*)nullptr, M, N, K, lda, ldb, ldc, (const uint8_t*)SA,
+                       (const uint8_t*)SB);
   return (int)hipGetLastError();
 }
 

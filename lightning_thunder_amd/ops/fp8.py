@@ -221,6 +221,7 @@ register_signature("lta_mx_cast_transpose", [c_int, c_int, c_void_p, c_void_p, c
 register_signature("lta_gemm_nt_mxfp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                          c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
 register_signature("lta_fp8_mfma_scale_probe", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+register_signature("lta_fp8_mfma_probe", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p])
 
 MX_BLOCK = 32
 
@@ -266,6 +267,16 @@ def gemm_nt_mx(a: torch.Tensor, sa: torch.Tensor, b: torch.Tensor, sb: torch.Ten
                                 sa.data_ptr(), sb.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0), fmt_a,
                                 fmt_b, stream_ptr(a.device)), "lta_gemm_nt_mxfp8")
     return out
+
+
+def mfma_probe(a: torch.Tensor, b: torch.Tensor, fmt_a: int, fmt_b: int) -> torch.Tensor:
+    """One unscaled v_mfma_scale_f32_16x16x128_f8f6f4 from raw per-lane operand registers (formats:
+    0 e4m3, 1 e5m2, 4 e2m1): a, b [64, 32] uint8 -> [64, 4] fp32 accumulator registers."""
+    assert a.shape == (64, 32) and b.shape == (64, 32) and a.dtype == b.dtype == torch.uint8
+    c = torch.empty((64, 4), dtype=torch.float32, device=a.device)
+    check(require().lta_fp8_mfma_probe(a.contiguous().data_ptr(), b.contiguous().data_ptr(), c.data_ptr(), fmt_a,
+                                       fmt_b, stream_ptr(a.device)), "lta_fp8_mfma_probe")
+    return c
 
 
 def mfma_scale_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
