@@ -69,6 +69,40 @@ import os as _os
 
 _choice: dict = {}
 
+# Library GEMM solutions pre-selected on MI355X for the shapes of the Llama-2-7B training step
+# (PyTorch TunableOp results: rocBLAS / hipBLASLt solution per (layout, M, N, K), measured with
+# rotating buffers on random data by scripts/tunable_probe.py on this image).  hipBLASLt's
+# default heuristic picks a 0.9 PF/s kernel for N = 11008 where a rocBLAS solution reaches
+# 1.46 PF/s; the per-shape selection below then compares the hand-written kernel against the
+# tuned library call.  The file's validators (PyTorch / HIP / rocBLAS / hipBLASLt versions, arch)
+# must match the running stack or TunableOp ignores it.  ``LTA_TUNED_GEMMS=0`` disables.
+TUNED_GEMMS = _os.path.join(_os.path.dirname(__file__), "tuned", "gemm_mi355x_bf16.csv")
+_tuned_state: dict = {}
+
+
+def enable_tuned_gemms() -> bool:
+    """Load the shipped TunableOp results once per process (tuning itself stays off, so shapes
+    not in the file use the library default).  Returns whether the results are active."""
+    if "active" in _tuned_state:
+        return _tuned_state["active"]
+    active = False
+    tun = getattr(torch.cuda, "tunable", None)
+    if (_os.environ.get("LTA_TUNED_GEMMS", "1") != "0" and torch.version.hip is not None and tun is not None
+            and _os.path.exists(TUNED_GEMMS) and torch.cuda.is_available()):
+        try:
+            if not tun.is_enabled():
+                import tempfile
+
+                # TunableOp may write its table back on exit: keep that out of the package
+                tun.set_filename(_os.path.join(tempfile.gettempdir(), f"lta_tunableop_{_os.getpid()}.csv"))
+                tun.tuning_enable(False)
+                tun.enable(True)
+            active = bool(tun.read_file(TUNED_GEMMS))
+        except Exception:  # an older/newer stack without the API: library defaults
+            active = False
+    _tuned_state["active"] = active
+    return active
+
 
 def _timeit(fn, iters: int = 5) -> float:
     for _ in range(2):
@@ -191,6 +225,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
     N = w.shape[0]
     x2 = x.reshape(-1, K)
     r2 = None if residual is None else residual.reshape(-1, N)
+    if x.is_cuda:
+        enable_tuned_gemms()
     mode = _os.environ.get("LTA_GEMM", "auto")
     if mode != "torch" and gemv_supported(x2, w, bias, r2):
         return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
@@ -292,6 +328,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = Non
     if residual is not None and (residual.dtype != torch.bfloat16 or residual.stride(1) != 1
                                  or residual.stride(0) % 8 or residual.data_ptr() % 16):
         lay = None
+    if a.is_cuda:
+        enable_tuned_gemms()
     if lay is None:
         return _torch_mm(a, b, residual)
     key = (a.shape[0], b.shape[1], a.shape[1], lay[0], lay[1], residual is not None)
