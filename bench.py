@@ -189,6 +189,13 @@ def run(args, rank, world, device, mode):
         dt = t.item()
     mem = torch.cuda.max_memory_allocated(device) / 1e9
     log(rank, f"[{mode}] {args.steps} steps in {dt:.3f}s, loss={loss.item():.4f}, peak mem {mem:.1f} GB")
+    if mode == "thunder":
+        from lightning_thunder_amd.ops import gemm as _g
+
+        hand = lambda tab: sorted(k[:3] for k, v in tab.items() if v)  # noqa: E731
+        log(rank, f"[gemm] hand-kernel shapes: linear {hand(_g.selection_table())}, "
+                  f"matmul {hand(_g.matmul_selection_table())}; tuned library table active: "
+                  f"{_g.enable_tuned_gemms()}")
     del model, opt, fwd, params
     return dt, cfg, mem, parallel
 

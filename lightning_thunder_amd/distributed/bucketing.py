@@ -110,3 +110,69 @@ def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> T
             new.bound_symbols.append(bsym.swap_proxies(swap))
     new.set_provenance(TraceProvenance(f"Gradient bucketing ({bucket_size_mb} MiB buckets)"))
     return new
+
+
+# ---------------------------------------------------------------------------------------------
+# FSDP forward: per-layer / per-block coalesced parameter all-gathers
+# ---------------------------------------------------------------------------------------------
+import re
+
+_BLOCK_RE = re.compile(r"^(.*?_(?:h|layers|layer|blocks|block)_\d+)_")
+
+
+def fsdp_bucket_name(name: str, strategy: str) -> str:
+    """Bucket of a parameter-shard proxy (reference ``get_extract_bucket_name_from_tensor_proxy``,
+    thunder/distributed/__init__.py): ``layer`` = its module (name minus the parameter name),
+    ``block`` = the enclosing numbered block (``..._h_3_...``, ``..._layers_3_...``); parameters
+    outside any block (embeddings, final norm, head) form one bucket."""
+    base = name[: -len("_shard")] if name.endswith("_shard") else name
+    if strategy == "block":
+        m = _BLOCK_RE.match(base)
+        return m.group(1) if m else "__outside_blocks__"
+    return base.rsplit("_", 1)[0]
+
+
+def _is_fsdp_param_gather(b: BoundSymbol) -> bool:
+    if b.sym is not dist_prims.all_gather or len(b.args) < 3 or not b.args[2]:
+        return False
+    a = b.args[0]
+    return isinstance(a, TensorProxy) and "parameter" in getattr(a, "tags", ()) and (len(b.args) < 4 or b.args[3] == 0)
+
+
+def has_fsdp_param_gathers(trace: TraceCtx) -> bool:
+    return any(_is_fsdp_param_gather(b) for b in trace.bound_symbols)
+
+
+def bucket_fsdp_all_gathers(trace: TraceCtx, strategy: str) -> TraceCtx:
+    """Replaces the per-parameter async all-gathers of an FSDP forward with one coalesced
+    all-gather per bucket (``strategy``: ``"layer"`` or ``"block"``), issued where the bucket's
+    first gather was; every parameter keeps its own future and ``wait``."""
+    if strategy not in ("layer", "block"):
+        return trace
+    gathers = [b for b in trace.bound_symbols if _is_fsdp_param_gather(b)]
+    if len(gathers) < 2:
+        return trace
+    buckets: "OrderedDict[tuple, list]" = OrderedDict()
+    for b in gathers:
+        key = (fsdp_bucket_name(b.args[0].name, strategy), id(b.args[1]))
+        buckets.setdefault(key, []).append(b)
+    first_of = {id(members[0]): members for members in buckets.values()}
+    grouped = {id(b) for members in buckets.values() for b in members}
+    new = from_trace(trace)
+    new.bound_symbols = []
+    new.scopes = [new.bound_symbols]
+    swap: dict[str, Proxy] = {}
+    with tracectx(new):
+        for bsym in trace.bound_symbols:
+            if id(bsym) in grouped:
+                members = first_of.get(id(bsym))
+                if members is None:
+                    continue  # issued with its bucket
+                futs = dist_prims.all_gather_coalesced([m.args[0] for m in members], members[0].args[1], True)
+                for m, f in zip(members, futs):
+                    swap[m.output.name] = f
+                continue
+            new.bound_symbols.append(bsym.swap_proxies(swap))
+    new.set_provenance(TraceProvenance(f"FSDP all-gather bucketing ({strategy}: {len(gathers)} gathers -> "
+                                       f"{len(buckets)} coalesced)"))
+    return new

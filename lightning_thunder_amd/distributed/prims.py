@@ -86,6 +86,16 @@ def _all_gather_meta(a, group, do_async=False, dim=0):
 all_gather = _make("all_gather", _all_gather_meta)
 
 
+# ---- coalesced all_gather (FSDP per-block buckets: one grouped RCCL launch for many shards) ----------
+def _all_gather_coalesced_meta(shards, group, do_async=True):
+    w = _world(group)
+    return [_maybe_future(TensorProxy(like=s, shape=(s.shape[0] * w,) + tuple(s.shape[1:]),
+                                      distparallel_type=DistParallelType.NONE), do_async) for s in shards]
+
+
+all_gather_coalesced = _make("all_gather_coalesced", _all_gather_coalesced_meta)
+
+
 # ---- reduce_scatter (along dim) -----------------------------------------------------------------
 def _reduce_scatter_meta(a, op, group, do_async=False, dim=0):
     w = _world(group)
@@ -272,6 +282,27 @@ def _all_gather_impl(a, group, do_async=False, dim=0):
     return FutureHandle(work, out) if do_async else out
 
 
+def _all_gather_coalesced_impl(shards, group, do_async=True):
+    """All-gathers (dim 0) of several shards as ONE grouped collective: RCCL runs them under a
+    single group launch (``_coalescing_manager`` -> ``allgather_into_tensor_coalesced``), so a
+    transformer block's parameters cost one launch and share the xGMI links, instead of one
+    collective per parameter."""
+    if len(shards) == 1 or tdist.get_backend(group) == "gloo":
+        return [_all_gather_impl(s, group, do_async) for s in shards]
+    from torch.distributed.distributed_c10d import _coalescing_manager
+
+    w = _world(group)
+    shards = [s.contiguous() for s in shards]
+    outs = [torch.empty((s.shape[0] * w,) + tuple(s.shape[1:]), dtype=s.dtype, device=s.device) for s in shards]
+    with _coalescing_manager(group=group, device=shards[0].device, async_ops=True) as cm:
+        for o, s in zip(outs, shards):
+            tdist.all_gather_into_tensor(o, s, group=group)
+    if not do_async:
+        cm.wait()
+        return outs
+    return [FutureHandle(cm, o) for o in outs]
+
+
 def _reduce_scatter_impl(a, op, group, do_async=False, dim=0):
     w = _world(group)
     if dim != 0:
@@ -386,6 +417,7 @@ def _register_torch_impls():
 
     for sym, fn in (
         (all_reduce, _all_reduce_impl), (all_gather, _all_gather_impl), (reduce_scatter, _reduce_scatter_impl),
+        (all_gather_coalesced, _all_gather_coalesced_impl),
         (broadcast, _broadcast_impl), (wait, _wait_impl), (synchronize, _synchronize_impl), (pack, _pack_impl),
         (unpack, _unpack_impl), (pack_for_fsdp, _pack_for_fsdp_impl), (unpack_for_fsdp, _unpack_for_fsdp_impl),
         (synchronize_tensor_parallel_output, _tp_out_impl), (synchronize_tensor_parallel_input, _tp_in_impl),

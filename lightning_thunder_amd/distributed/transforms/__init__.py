@@ -98,6 +98,10 @@ class FSDPType:
 
 
 class FSDPBucketingStrategy:
+    """Granularity of the FSDP forward parameter all-gathers (reference ``FSDPBucketingStrategy``,
+    unwired there): per parameter, per module (LAYER) or per numbered block (BLOCK, ~400 MB per
+    Llama-2-7B block: one grouped collective that loads all 7 xGMI links)."""
+
     NONE = "none"
     LAYER = "layer"
     BLOCK = "block"
@@ -142,6 +146,9 @@ class FSDPTransform(Transform):
         cd = getattr(model, "_lc_cd", None)
         if cd is not None:
             cd.compile_options.setdefault("lta_bucket_size_mb", self.bucket_size_in_mb)
+            # forward all-gathers: one coalesced RCCL launch per layer / block instead of one per
+            # parameter (executors/passes.py -> distributed/bucketing.py:bucket_fsdp_all_gathers)
+            cd.compile_options.setdefault("lta_fsdp_bucketing", self.bucketing_strategy)
         group = self._group()
         rank, world = tdist.get_rank(group), tdist.get_world_size(group)
         inner = model._model
@@ -226,8 +233,14 @@ class FSDPTransform(Transform):
         if zero3:
             from ...core.symbol import BoundSymbolTag
 
+            gathered = set()
             for b in comp.bound_symbols:
                 if b.sym is dist_prims.synchronize:
+                    b.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
+                    gathered.add(b.output.name)
+                elif "narrow" in b.sym.name and b.args and getattr(b.args[0], "name", None) in gathered:
+                    # the padding trim of a gathered parameter is re-done with the gather, so the
+                    # backward saves the shard, not the full parameter
                     b.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
         comp.set_provenance(TraceProvenance(f"FSDP ({self.sharding_strategy}): parameters all-gathered"))
         return prologue_trace, comp, epilogue_trace

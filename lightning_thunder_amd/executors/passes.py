@@ -90,6 +90,15 @@ def transform_for_execution(trace: TraceCtx, executors: Sequence[Executor]) -> l
 
         trace = bucket_grad_syncs(trace, get_compile_option("lta_bucket_size_mb", "DDP/FSDP gradient bucket size (MiB)"))
         traces.append(trace)
+    from ..distributed.bucketing import has_fsdp_param_gathers, bucket_fsdp_all_gathers
+
+    if has_fsdp_param_gathers(trace):
+        from ..common import get_compile_option
+
+        strategy = get_compile_option("lta_fsdp_bucketing", "FSDP parameter all-gather buckets: none|layer|block")
+        if strategy in ("layer", "block"):
+            trace = bucket_fsdp_all_gathers(trace, strategy)
+            traces.append(trace)
     trace = dce(trace)
     traces.append(trace)
     trace = _transform_for_operator_executor_execution(trace, executors)

@@ -117,6 +117,18 @@ def _timeit(fn, iters: int = 5) -> float:
     return s.elapsed_time(e) / iters
 
 
+def _faster_is_first(f_a, f_b, rounds: int | None = None) -> bool:
+    """A/B timing interleaved over a few rounds (min of each): one-shot timings of two kernels
+    taken back to back pick up clock (DVFS) swings as if they were kernel differences."""
+    if rounds is None:
+        rounds = int(_os.environ.get("LTA_GEMM_SELECT_ROUNDS", "3"))
+    ta, tb = float("inf"), float("inf")
+    for _ in range(rounds):
+        ta = min(ta, _timeit(f_a))
+        tb = min(tb, _timeit(f_b))
+    return ta <= tb
+
+
 def _torch_linear(x2, w, bias, residual, act):
     if residual is not None and act is None and bias is None and x2.dim() == 2:
         return torch.addmm(residual, x2, w.t())  # hipBLASLt with beta = 1: the add rides in the GEMM
@@ -239,9 +251,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
         if torch.cuda.is_current_stream_capturing():
             use = True
         else:
-            t_h = _timeit(lambda: gemm_nt(x2, w, bias=bias, residual=r2, act=act))
-            t_t = _timeit(lambda: _torch_linear(x2, w, bias, r2, act))
-            use = t_h <= t_t
+            use = _faster_is_first(lambda: gemm_nt(x2, w, bias=bias, residual=r2, act=act),
+                                   lambda: _torch_linear(x2, w, bias, r2, act))
         _choice[key] = use
     if use:
         y = gemm_nt(x2, w, bias=bias, residual=r2, act=act)
@@ -338,9 +349,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = Non
         if torch.cuda.is_current_stream_capturing():
             use = True
         else:
-            t_h = _timeit(lambda: matmul_hip(a, b, residual=residual))
-            t_t = _timeit(lambda: _torch_mm(a, b, residual))
-            use = t_h <= t_t
+            use = _faster_is_first(lambda: matmul_hip(a, b, residual=residual), lambda: _torch_mm(a, b, residual))
         _mm_choice[key] = use
     return matmul_hip(a, b, residual=residual) if use else _torch_mm(a, b, residual)
 

@@ -45,7 +45,7 @@ def _reference_grads():
 def _worker(rank, port, mode, out_dir):
     import lightning_thunder_amd as thunder
     from lightning_thunder_amd.distributed import ddp, fsdp
-    from lightning_thunder_amd.distributed.transforms import FSDPType
+    from lightning_thunder_amd.distributed.transforms import FSDPType, FSDPBucketingStrategy
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -61,13 +61,19 @@ def _worker(rank, port, mode, out_dir):
             jm = fsdp(jm)
         elif mode == "fsdp_zero3":
             jm = fsdp(jm, sharding_strategy=FSDPType.ZERO3)
+        elif mode == "fsdp_layer":
+            jm = fsdp(jm, bucketing_strategy=FSDPBucketingStrategy.LAYER)
+        elif mode == "fsdp_block_zero3":
+            jm = fsdp(jm, sharding_strategy=FSDPType.ZERO3, bucketing_strategy=FSDPBucketingStrategy.BLOCK)
         out = jm(_data(rank))
         loss = out.pow(2).mean()
         loss.backward()
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         shapes = {n: tuple(p.shape) for n, p in m.named_parameters()}
         bw = str(thunder.last_backward_traces(jm)[-1])
-        torch.save({"grads": grads, "shapes": shapes, "bw": bw}, os.path.join(out_dir, f"rank{rank}.pt"))
+        fw = str(thunder.last_traces(jm)[-1])
+        torch.save({"grads": grads, "shapes": shapes, "bw": bw, "fw": fw, "out": out.detach()},
+                   os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         torch.distributed.destroy_process_group()
 
@@ -91,7 +97,7 @@ def test_ddp_gloo(mode):
         assert "pack" in res[0]["bw"]
 
 
-@pytest.mark.parametrize("mode", ["fsdp", "fsdp_zero3"])
+@pytest.mark.parametrize("mode", ["fsdp", "fsdp_zero3", "fsdp_layer", "fsdp_block_zero3"])
 def test_fsdp_gloo(mode):
     from lightning_thunder_amd.distributed.transforms import shard_tensor
 
@@ -103,3 +109,14 @@ def test_fsdp_gloo(mode):
             assert r["shapes"][n] == tuple(expected.shape)
             torch.testing.assert_close(r["grads"][n], expected)
     assert "reduce_scatter" in res[0]["bw"]
+    if mode == "fsdp_layer":
+        # one coalesced gather per Linear (weight + bias), not one per parameter
+        assert res[0]["fw"].count("all_gather_coalesced(") == 3, res[0]["fw"]
+    if mode == "fsdp_block_zero3":
+        # no numbered blocks in a Sequential: everything is one bucket, also for the backward's
+        # re-gathers
+        assert res[0]["fw"].count("all_gather_coalesced(") == 1
+        assert res[0]["bw"].count("all_gather_coalesced(") == 1
+    if "zero3" in mode:
+        # ZeRO-3 saves shards and re-gathers (also when the padding trim follows the gather)
+        assert "all_gather" in res[0]["bw"]
