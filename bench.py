@@ -42,6 +42,9 @@ def parse_args():
     p.add_argument("--parallel", default="auto", choices=["auto", "fsdp", "ddp", "tp", "none"],
                    help="auto: fsdp for N>1; tp: Megatron tensor parallel over all ranks (BASELINE config 4, "
                         "e.g. --model Llama-3-8B --parallel tp; strong scaling)")
+    p.add_argument("--fsdp-bucketing", default="block", choices=["none", "layer", "block"],
+                   help="FSDP forward all-gather granularity: per parameter, per module or per transformer block "
+                        "(one coalesced RCCL launch per ~400 MB block of Llama-2-7B)")
     p.add_argument("--executors", default=None, help="comma separated executor names (default: framework defaults)")
     p.add_argument("--fp8", action="store_true")
     p.add_argument("--fp8-recipe", default="current", choices=["current", "delayed", "mxfp8"],
@@ -85,6 +88,10 @@ def make_optimizer(params, mode="eager"):
         return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, foreach=True)
 
 
+def _force_dist() -> bool:
+    return os.environ.get("LTA_BENCH_FORCE_DIST") == "1"
+
+
 def run(args, rank, world, device, mode):
     import lightning_thunder_amd as thunder
 
@@ -119,15 +126,15 @@ def run(args, rank, world, device, mode):
                 return torch.nn.functional.cross_entropy(logits.reshape(-1, V), y.reshape(-1))
 
         jm = thunder.jit(TrainStep(model), transforms=transforms, **kwargs)
-        if world > 1 and parallel == "fsdp":
+        if (world > 1 or _force_dist()) and parallel == "fsdp":
             from lightning_thunder_amd.distributed import fsdp
 
-            jm = fsdp(jm)
-        elif world > 1 and parallel == "ddp":
+            jm = fsdp(jm, bucketing_strategy=args.fsdp_bucketing)
+        elif (world > 1 or _force_dist()) and parallel == "ddp":
             from lightning_thunder_amd.distributed import ddp
 
             jm = ddp(jm)
-        elif world > 1 and parallel == "tp":
+        elif (world > 1 or _force_dist()) and parallel == "tp":
             from lightning_thunder_amd.distributed import column_parallel, row_parallel
 
             n = cfg.n_layer
@@ -212,7 +219,10 @@ def main():
     backend = os.environ.get("LTA_DIST_BACKEND", "nccl")
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
+    # LTA_BENCH_FORCE_DIST=1: run the data/tensor-parallel path even at world size 1 (a one-GPU
+    # rehearsal of the RCCL program: bucketed / coalesced collectives at full model size)
+    force = os.environ.get("LTA_BENCH_FORCE_DIST") == "1"
+    if world > 1 or force:
         os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=device)

@@ -12,6 +12,11 @@ before the return:
 * FULLY_SHARDED (FSDP): ``pack_for_fsdp`` (interleaved: rank r's chunk holds its shard of
   every gradient) → ``reduce_scatter(AVG)`` → ``unpack_for_fsdp``
 
+On RCCL a bucket is instead ONE grouped collective over its gradients
+(``all_reduce_coalesced`` / ``reduce_scatter_coalesced``): the same single launch per bucket,
+without the pack and unpack copies (for Llama-2-7B 13.5 GB of gradient bytes read and written
+each step, ~9 ms at HBM speed).
+
 Bucket sizes default to 256 MiB: large messages saturate all 7 xGMI links per MI355X
 and 288 GB of HBM makes the staging buffers free.
 """
@@ -36,13 +41,35 @@ def _key(b: BoundSymbol):
     return (id(group), dpt, g.dtype, str(g.device), id(rg))
 
 
+def _default_coalesce(trace: TraceCtx) -> bool:
+    import os
+
+    import torch.distributed as tdist
+
+    env = os.environ.get("LTA_COALESCED_GRAD_SYNC")
+    if env is not None:
+        return env == "1"
+    for b in trace.bound_symbols:
+        if b.sym is dist_prims.grad_sync:
+            try:
+                return tdist.get_backend(b.args[1]) != "gloo"
+            except Exception:
+                return False
+    return False
+
+
 def has_grad_syncs(trace: TraceCtx) -> bool:
     return any(b.sym is dist_prims.grad_sync for b in trace.bound_symbols)
 
 
-def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> TraceCtx:
+def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None, coalesce: bool | None = None) -> TraceCtx:
+    """``coalesce``: issue each bucket as one grouped collective over its gradients (RCCL
+    ``*_coalesced``: no pack / unpack copies of 13.5 GB of Llama-2-7B gradients per step);
+    default: on for the RCCL backend, off for gloo (which runs the packed-buffer form)."""
     if not has_grad_syncs(trace):
         return trace
+    if coalesce is None:
+        coalesce = _default_coalesce(trace)
     if bucket_size_mb is None:
         bucket_size_mb = DEFAULT_BUCKET_SIZE_MB
     limit = bucket_size_mb * 1024 * 1024
@@ -57,7 +84,14 @@ def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> T
         entries = open_buckets.pop(key)
         grads = [b.args[0] for b in entries]
         _, group, dpt, world = entries[0].args[:4]
-        if dpt is DistParallelType.FULLY_SHARDED:
+        if coalesce and len(grads) > 1:
+            # one grouped collective over the bucket's gradients: no pack / unpack copies
+            if dpt is DistParallelType.FULLY_SHARDED:
+                futs = dist_prims.reduce_scatter_coalesced(grads, dist_prims.DistributedReduceOps.AVG, group, True)
+            else:
+                futs = dist_prims.all_reduce_coalesced(grads, dist_prims.DistributedReduceOps.AVG, group, True)
+            pending.append((futs, entries, "coalesced"))
+        elif dpt is DistParallelType.FULLY_SHARDED:
             if len(grads) == 1:
                 fut = dist_prims.reduce_scatter(grads[0], dist_prims.DistributedReduceOps.AVG, group, True, 0)
                 pending.append((fut, entries, "rs1"))
@@ -78,10 +112,18 @@ def bucket_grad_syncs(trace: TraceCtx, bucket_size_mb: float | None = None) -> T
         for key in list(open_buckets.keys()):
             issue(key)
         for fut, entries, kind in pending:
+            rg = entries[0].args[4] if len(entries[0].args) > 4 else None
+            if kind == "coalesced":
+                for b, f in zip(entries, fut):
+                    res = dist_prims.wait(f)
+                    if rg is not None:
+                        res = dist_prims.wait(dist_prims.all_reduce(res, dist_prims.DistributedReduceOps.AVG, rg, True,
+                                                                    True))
+                    swap[b.output.name] = res
+                continue
             res = dist_prims.wait(fut)
             grads = [b.args[0] for b in entries]
             world = entries[0].args[3]
-            rg = entries[0].args[4] if len(entries[0].args) > 4 else None
             if rg is not None:
                 # hybrid mesh: average the reduce-scattered shards over the replica group
                 res = dist_prims.wait(dist_prims.all_reduce(res, dist_prims.DistributedReduceOps.AVG, rg, True, True))

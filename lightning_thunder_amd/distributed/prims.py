@@ -96,6 +96,23 @@ def _all_gather_coalesced_meta(shards, group, do_async=True):
 all_gather_coalesced = _make("all_gather_coalesced", _all_gather_coalesced_meta)
 
 
+# ---- coalesced reduce_scatter / all_reduce (gradient buckets without pack/unpack copies) -------------
+def _reduce_scatter_coalesced_meta(tensors, op, group, do_async=True):
+    w = _world(group)
+    return [_maybe_future(TensorProxy(like=t, shape=(t.shape[0] // w,) + tuple(t.shape[1:]), requires_grad=False),
+                          do_async) for t in tensors]
+
+
+reduce_scatter_coalesced = _make("reduce_scatter_coalesced", _reduce_scatter_coalesced_meta)
+
+
+def _all_reduce_coalesced_meta(tensors, op, group, do_async=True):
+    return [_maybe_future(TensorProxy(like=t, requires_grad=False), do_async) for t in tensors]
+
+
+all_reduce_coalesced = _make("all_reduce_coalesced", _all_reduce_coalesced_meta, tags=(OpTags.DONT_DCE,))
+
+
 # ---- reduce_scatter (along dim) -----------------------------------------------------------------
 def _reduce_scatter_meta(a, op, group, do_async=False, dim=0):
     w = _world(group)
@@ -303,6 +320,46 @@ def _all_gather_coalesced_impl(shards, group, do_async=True):
     return [FutureHandle(cm, o) for o in outs]
 
 
+def _coalesced(group, device):
+    from torch.distributed.distributed_c10d import _coalescing_manager
+
+    return _coalescing_manager(group=group, device=device, async_ops=True)
+
+
+def _reduce_scatter_coalesced_impl(tensors, op, group, do_async=True):
+    """Reduce-scatter (dim 0) of every tensor of a gradient bucket in ONE grouped RCCL launch: each
+    gradient is reduced straight into its own shard, so the bucket needs no interleaved pack copy
+    before and no unpack after (``reduce_scatter_tensor_coalesced``)."""
+    if len(tensors) == 1 or tdist.get_backend(group) == "gloo":
+        return [_reduce_scatter_impl(t, op, group, do_async, 0) for t in tensors]
+    w = _world(group)
+    tensors = [t.contiguous() for t in tensors]
+    outs = [torch.empty((t.shape[0] // w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors]
+    op_t = to_torch_reduce_op(op)
+    with _coalesced(group, tensors[0].device) as cm:
+        for o, t in zip(outs, tensors):
+            tdist.reduce_scatter_tensor(o, t, op_t, group=group)
+    if not do_async:
+        cm.wait()
+        return outs
+    return [FutureHandle(cm, o) for o in outs]
+
+
+def _all_reduce_coalesced_impl(tensors, op, group, do_async=True):
+    """In-place all-reduce of every gradient of a bucket in one grouped RCCL launch (no pack copy)."""
+    if len(tensors) == 1 or tdist.get_backend(group) == "gloo":
+        return [_all_reduce_impl(t, op, group, do_async, True) for t in tensors]
+    tensors = [t if t.is_contiguous() else t.contiguous() for t in tensors]
+    op_t = to_torch_reduce_op(op)
+    with _coalesced(group, tensors[0].device) as cm:
+        for t in tensors:
+            tdist.all_reduce(t, op_t, group=group)
+    if not do_async:
+        cm.wait()
+        return tensors
+    return [FutureHandle(cm, t) for t in tensors]
+
+
 def _reduce_scatter_impl(a, op, group, do_async=False, dim=0):
     w = _world(group)
     if dim != 0:
@@ -418,6 +475,7 @@ def _register_torch_impls():
     for sym, fn in (
         (all_reduce, _all_reduce_impl), (all_gather, _all_gather_impl), (reduce_scatter, _reduce_scatter_impl),
         (all_gather_coalesced, _all_gather_coalesced_impl),
+        (reduce_scatter_coalesced, _reduce_scatter_coalesced_impl), (all_reduce_coalesced, _all_reduce_coalesced_impl),
         (broadcast, _broadcast_impl), (wait, _wait_impl), (synchronize, _synchronize_impl), (pack, _pack_impl),
         (unpack, _unpack_impl), (pack_for_fsdp, _pack_for_fsdp_impl), (unpack_for_fsdp, _unpack_for_fsdp_impl),
         (synchronize_tensor_parallel_output, _tp_out_impl), (synchronize_tensor_parallel_input, _tp_in_impl),
