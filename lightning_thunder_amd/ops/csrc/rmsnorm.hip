@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
                                                                int64_t rows, int cols, int rows_per_block,
                                                                const T* __restrict__ res) {
   constexpr int V = Vec16<T>::N;
-  __shared__ float smem[kWaves];
+  __shared__ float smem[2 * kWaves];
   float dw_acc[CHUNKS][V];
 #pragma unroll
   for (int c = 0; c < CHUNKS; ++c)
@@ -109,40 +109,83 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
-  for (int64_t row = r0; row < r1; ++row) {
-    const float r = rstd[row];
-    Vec16<T> xv[CHUNKS], gv[CHUNKS];
-    float dot = 0.f;
+  // two rows per iteration: both rows' loads are in flight together and their dot products share
+  // one block reduction (one barrier pair per two rows); the kernel is latency-bound otherwise
+  for (int64_t row = r0; row < r1; row += 2) {
+    const bool two = row + 1 < r1;
+    const float ra = rstd[row], rb = two ? rstd[row + 1] : 0.f;
+    Vec16<T> xv[2][CHUNKS], gv[2][CHUNKS];
 #pragma unroll
     for (int c = 0; c < CHUNKS; ++c) {
       const int idx = (c * kThreads + threadIdx.x) * V;
       if (idx < cols) {
-        xv[c] = load16(x + row * cols + idx);
-        gv[c] = load16(dy + row * cols + idx);
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-          const float xh = to_f32(xv[c].v[j]) * r;
-          const float g = to_f32(gv[c].v[j]);
-          dot += g * to_f32(wv[c].v[j]) * xh;
-          dw_acc[c][j] += g * xh;
+        xv[0][c] = load16(x + row * cols + idx);
+        gv[0][c] = load16(dy + row * cols + idx);
+        if (two) {
+          xv[1][c] = load16(x + (row + 1) * cols + idx);
+          gv[1][c] = load16(dy + (row + 1) * cols + idx);
         }
       }
     }
-    dot = block_sum<kWaves>(dot, smem) / (float)cols;
+    float dota = 0.f, dotb = 0.f;
 #pragma unroll
     for (int c = 0; c < CHUNKS; ++c) {
       const int idx = (c * kThreads + threadIdx.x) * V;
       if (idx < cols) {
-        Vec16<T> o, rv;
-        if (res != nullptr) rv = load16(res + row * cols + idx);  // gradient arriving through the residual
 #pragma unroll
         for (int j = 0; j < V; ++j) {
-          const float xh = to_f32(xv[c].v[j]) * r;
-          const float gw = to_f32(gv[c].v[j]) * to_f32(wv[c].v[j]);
-          const float add = res != nullptr ? to_f32(rv.v[j]) : 0.f;
-          o.v[j] = from_f32<T>(r * (gw - xh * dot) + add);
+          const float wj = to_f32(wv[c].v[j]);
+          const float xa = to_f32(xv[0][c].v[j]) * ra, ga = to_f32(gv[0][c].v[j]);
+          dota += ga * wj * xa;
+          dw_acc[c][j] += ga * xa;
+          if (two) {
+            const float xb = to_f32(xv[1][c].v[j]) * rb, gb = to_f32(gv[1][c].v[j]);
+            dotb += gb * wj * xb;
+            dw_acc[c][j] += gb * xb;
+          }
         }
-        store16(dx + row * cols + idx, o);
+      }
+    }
+    dota = wave_sum(dota);
+    dotb = wave_sum(dotb);
+    {
+      const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+      __syncthreads();  // the previous iteration's reads of smem are done
+      if (lane == 0) {
+        smem[wid] = dota;
+        smem[kWaves + wid] = dotb;
+      }
+      __syncthreads();
+      dota = 0.f;
+      dotb = 0.f;
+#pragma unroll
+      for (int i = 0; i < kWaves; ++i) {
+        dota += smem[i];
+        dotb += smem[kWaves + i];
+      }
+      dota /= (float)cols;
+      dotb /= (float)cols;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int64_t rr = row + h;
+      const float r = h ? rb : ra, dot = h ? dotb : dota;
+#pragma unroll
+      for (int c = 0; c < CHUNKS; ++c) {
+        const int idx = (c * kThreads + threadIdx.x) * V;
+        if (idx < cols) {
+          Vec16<T> o, rv;
+          if (res != nullptr) rv = load16(res + rr * cols + idx);  // gradient arriving through the residual
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const float xh = to_f32(xv[h][c].v[j]) * r;
+            const float gw = to_f32(gv[h][c].v[j]) * to_f32(wv[c].v[j]);
+            const float add = res != nullptr ? to_f32(rv.v[j]) : 0.f;
+            o.v[j] = from_f32<T>(r * (gw - xh * dot) + add);
+          }
+          store16(dx + rr * cols + idx, o);
+        }
       }
     }
   }

@@ -16,7 +16,7 @@ def _lib():
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("shape", [(4, 4096), (3, 7, 4096), (5, 1000), (2, 11008), (16, 64)])
+@pytest.mark.parametrize("shape", [(4, 4096), (3, 7, 4096), (5, 1000), (2, 11008), (16, 64), (1537, 4096), (4096, 4096)])
 def test_rmsnorm_fwd_bwd(dtype, shape):
     from lightning_thunder_amd.ops.rmsnorm import rms_norm_fwd, rms_norm_bwd
 
