@@ -50,6 +50,8 @@ def parse_args():
     p.add_argument("--fp8-recipe", default="current", choices=["current", "delayed", "mxfp8"],
                    help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling) or MXFP8 blocks")
     p.add_argument("--hipgraph", action="store_true")
+    p.add_argument("--checkpoint-activations", action="store_true",
+                   help="recompute every transformer block in the backward (memory for longer sequences)")
     p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
     p.add_argument("--eager-baseline", action="store_true", help="also time PyTorch eager (1 GPU) for speedup")
     p.add_argument("--profile-dir", default=None)
@@ -74,6 +76,7 @@ def build_model(args, device):
     torch.manual_seed(1234)
     init_weights(model)
     model.set_rope_cache(args.seq, device=device)
+    model.activation_checkpointing = args.checkpoint_activations
     return model, cfg
 
 

@@ -693,8 +693,10 @@ class Interpreter:
             p = self.mprov(v, p)
             self.maybe_guard(args[0], args[1], v, p)
             return v, p
-        if _hashable(fn) and (getattr(fn, "__module__", None) or "").startswith("torch.distributed"):
-            # c10d collectives have no __torch_function__ hook: route them to their ltorch symbols
+        if _hashable(fn) and (getattr(fn, "__module__", None) or "").startswith(("torch.distributed",
+                                                                                  "torch.utils.checkpoint")):
+            # c10d collectives and activation checkpointing have no __torch_function__ hook: route
+            # them to their ltorch symbols
             from .. import torch as ltorch
             from .jit_ext import dispatch_torch_function
 

@@ -18,6 +18,7 @@ from typing import Optional
 
 import torch
 import torch.nn as nn
+import torch.utils.checkpoint
 import torch.nn.functional as F
 
 
@@ -312,6 +313,7 @@ class GPT(nn.Module):
     def __init__(self, config: Config):
         super().__init__()
         self.config = config
+        self.activation_checkpointing = False  # per-Block torch.utils.checkpoint in training forwards
         self.lm_head = nn.Linear(config.n_embd, config.padded_vocab_size, bias=config.lm_head_bias if hasattr(config, "lm_head_bias") else False)
         self.transformer = nn.ModuleDict(
             dict(
@@ -370,7 +372,12 @@ class GPT(nn.Module):
             mask = None
         x = self.transformer.wte(idx)
         for block in self.transformer.h:
-            x = block(x, cos, sin, mask, input_pos)
+            if self.activation_checkpointing and input_pos is None:
+                # recompute the block's intermediates in the backward (LitGPT / benchmark_litgpt
+                # ``--checkpoint_activations``); traced as ltorch.checkpoint
+                x = torch.utils.checkpoint.checkpoint(block, x, cos, sin, mask, None, use_reentrant=False)
+            else:
+                x = block(x, cos, sin, mask, input_pos)
         x = self.transformer.ln_f(x)
         return self.lm_head(x)
 
