@@ -183,6 +183,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             python_lookasides.extend(_dt_lookasides())
         from .transforms.autocast import autocast_ctx
 
+        default_dtype = _torch.get_default_dtype()
         with autocast_ctx(entry.autocast_key):
             dbg = cd.debug_options
             record = cd.get_compile_option("record_interpreter_history", "Record the interpreter log", None)
@@ -198,6 +199,14 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
                            show_progress=dbg.show_interpreter_progress,
                            symbolic_numbers=cd.cache_option is CACHE_OPTIONS.SYMBOLIC_VALUES)
         cs.last_trace_tracing_stop = time.perf_counter_ns()
+        # global modes user code flipped while it was being interpreted: grad mode is recorded per
+        # op (BoundSymbolTag.NO_GRAD) and restored; a changed default dtype would make the program
+        # disagree with the cache key (reference: same error in thunder/__init__.py)
+        _torch.set_grad_enabled(entry.grad_enabled)
+        if _torch.get_default_dtype() != default_dtype:
+            _torch.set_default_dtype(default_dtype)
+            raise RuntimeError("Default dtype is changed during the execution of jitted function. "
+                               "This is currently unsupported.")
         pro, comp, epi = prog.prologue_trace, prog.computation_trace, prog.epilogue_trace
         computation_traces = [comp]
         for t in cd.transforms:
@@ -301,6 +310,7 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             entry.prologue_fn = prologue_with_late_checks
     finally:
         _compile_data_ctx.reset(tok)
+        _torch.set_grad_enabled(entry.grad_enabled)
     return entry
 
 

@@ -9,6 +9,7 @@ composite op whole or fall through to its decomposition.
 """
 from __future__ import annotations
 
+import torch
 from enum import Enum, auto
 from types import ModuleType
 from typing import Any, Callable, Sequence
@@ -30,6 +31,7 @@ class BoundSymbolTag(Enum):
     RECOMPUTE_IN_BACKWARD = auto()
     BACKWARD = auto()
     DONT_AUTO_RECOMPUTE_IN_BACKWARD = auto()
+    NO_GRAD = auto()  # recorded while grad mode was off (torch.no_grad / set_grad_enabled(False) in user code)
 
 
 class Symbol:
@@ -160,6 +162,14 @@ class Symbol:
         bsym = self.bind(*args, output=result, subsymbols=subsymbols, _call_ctx=call_ctx, **kwargs)
         if called_fn is not None:
             bsym.torch_fn = called_fn
+        if len(trace.scopes) == 1 and not torch.is_grad_enabled():
+            # user code switched autograd off around this op (the interpreter runs torch.no_grad /
+            # set_grad_enabled for real): its outputs are constants for the backward (reference:
+            # grad-mode tracking in jit_ext / ltorch._set_grad_enabled_with_warning)
+            bsym.tags.add(BoundSymbolTag.NO_GRAD)
+            for o in bsym.flat_proxy_outs:
+                if isinstance(o, TensorProxy):
+                    o.requires_grad = False
         if self.is_prim or subsymbols or self.name in _LAYOUT_IDENTITIES or not _is_identity(bsym):
             # an op that decomposed to nothing and returns its own input (dropout in eval, a
             # same-dtype .to, cat of one tensor) is not recorded: a line "t1 = op(t1)" would

@@ -207,6 +207,13 @@ class TraceCtx:
         self.obj_ctx.update(obj_ctx)
         return "\n".join(lines) + "\n"
 
+    def save_trace(self, filename) -> None:
+        """Writes the program (``python()``) to ``filename`` (reference ``TraceCtx.save_trace``)."""
+        import os
+
+        with open(os.fspath(filename), "w") as f:
+            f.write(self.python())
+
     def python_callable(self, *, global_dicts: dict | None = None, **kwargs) -> Callable:
         src = self.python(**kwargs)
         ctx = self.python_ctx()

@@ -831,3 +831,12 @@ def value_and_grad(func):
         return _vjp_run(jf, args, kwargs, ones)
 
     return _value_and_grad
+
+
+def eval_trace(trace, *args, symbol_mapper=None, with_env: bool = False, **kwargs):
+    """Evaluates ``trace`` on ``args`` bound symbol by bound symbol, each through
+    ``symbol_mapper(bsym)`` (default: the symbol itself) — reference ``core/transforms.py``
+    ``eval_trace``; see ``core/trace_interpreter.interpret_trace``."""
+    from .trace_interpreter import interpret_trace
+
+    return interpret_trace(trace, *args, symbol_mapper=symbol_mapper, with_env=with_env, **kwargs)

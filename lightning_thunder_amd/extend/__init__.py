@@ -16,6 +16,7 @@ import torch
 
 from ..core.symbol import Symbol, BoundSymbol, register_symbol
 from ..core.proxies import TensorProxy
+from ..core import dtypes
 
 
 class ImplInfo:
@@ -168,11 +169,25 @@ class Executor:
             if tfn is not None:
                 path = _resolve_printable_path(tfn)
                 key = path if path is not None else f"_torchfn_{getattr(tfn, '__name__', 'op')}_{id(tfn) & 0xFFFF}"
+                kwargs = bsym.kwargs
+                if original.sym.id in _FACTORY_IDS and isinstance(bsym.output, TensorProxy):
+                    # factory calls resolve dtype / device from torch's global defaults at trace
+                    # time; pin them so the replay does not depend on the defaults at run time
+                    kwargs = dict(kwargs)
+                    if kwargs.get("dtype") is None:
+                        kwargs["dtype"] = dtypes.to_torch_dtype(bsym.output.dtype)
+                    if kwargs.get("device") is None:
+                        kwargs["device"] = bsym.output.device
+                    return bsym.from_bsym(kwargs=kwargs, _call_ctx={key: tfn})
                 return bsym.from_bsym(_call_ctx={key: tfn})
         fn = getattr(bsym.sym, "_exec_fn", None)
         if fn is not None:
             return bsym.from_bsym(_call_ctx={bsym.sym.name: fn})
         return bsym
+
+
+_FACTORY_IDS = frozenset(f"torch.{n}" for n in ("ones", "zeros", "empty", "full", "rand", "randn", "arange", "linspace",
+                                                  "logspace", "eye", "randint", "randperm"))
 
 
 class OperatorExecutor(Executor):

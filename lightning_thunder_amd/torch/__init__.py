@@ -520,7 +520,7 @@ def to(a, *args, **kwargs):
     dtype = kwargs.pop("dtype", None)
     kwargs.pop("non_blocking", None)
     kwargs.pop("copy", None)
-    kwargs.pop("memory_format", None)
+    memory_format = kwargs.pop("memory_format", None)
     for x in args:
         if isinstance(x, torch.dtype):
             dtype = x
@@ -533,6 +533,10 @@ def to(a, *args, **kwargs):
         out = clang.device_put(out, device)
     if dtype is not None:
         out = clang.maybe_convert_to_dtype(out, dtype)
+    if memory_format is not None and memory_format is not torch.preserve_format:
+        # a layout change: recorded (so the call is replayed with its memory_format) even when
+        # dtype and device already match
+        out = contiguous(out, memory_format=memory_format)
     return out
 
 

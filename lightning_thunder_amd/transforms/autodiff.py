@@ -57,7 +57,7 @@ class _Record:
 
 
 def _is_differentiable_bsym(bsym: BoundSymbol) -> bool:
-    if NON_DIFFERENTIABLE_TAG in bsym.sym.tags:
+    if NON_DIFFERENTIABLE_TAG in bsym.sym.tags or BoundSymbolTag.NO_GRAD in bsym.tags:
         return False
     if bsym.sym.id in (PrimIDs.RETURN, PrimIDs.DEL, PrimIDs.COMMENT):
         return False

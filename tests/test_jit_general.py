@@ -275,3 +275,90 @@ def test_symbolic_values_backward():
         f(x2, a).backward()
         torch.testing.assert_close(x.grad, x2.grad)
     assert thunder.cache_misses(jf) == 1
+
+
+# ---- grad mode, default dtype / device, layout, trace I/O (reference test_core.py parity) --------
+def test_no_grad_region_inside_jitted_function():
+    def f(a):
+        with torch.no_grad():
+            b = a * 2
+        return a * b
+
+    a = torch.randn(3, requires_grad=True)
+    thunder.jit(f)(a).sum().backward()
+    a2 = a.detach().clone().requires_grad_(True)
+    f(a2).sum().backward()
+    torch.testing.assert_close(a.grad, a2.grad)
+    assert torch.is_grad_enabled()
+
+
+def test_set_grad_enabled_inside_jitted_function():
+    def f(a):
+        torch.set_grad_enabled(False)
+        b = a.exp()
+        torch.set_grad_enabled(True)
+        return (a * b).sum()
+
+    a = torch.randn(4, requires_grad=True)
+    thunder.jit(f)(a).backward()
+    torch.testing.assert_close(a.grad, a.detach().exp())  # b is a constant for autograd
+
+
+def test_change_default_dtype_in_jitted_fn_raises():
+    def fn(x):
+        torch.set_default_dtype(torch.float16)
+        return torch.ones(x.shape)
+
+    with pytest.raises(RuntimeError, match="Default dtype is changed during the execution of jitted function"):
+        thunder.jit(fn)(torch.randn(3, 3))
+    assert torch.get_default_dtype() == torch.float32
+
+
+def test_factory_dtype_resolved_at_trace_time():
+    def fn():
+        torch.set_default_dtype(torch.float64)
+        r = torch.ones(2)
+        torch.set_default_dtype(torch.float32)
+        return r
+
+    jf = thunder.jit(fn)
+    assert jf().dtype == torch.float64 and jf().dtype == torch.float64
+    assert "dtype=torch.float64" in str(thunder.last_traces(jf)[-1])
+
+
+def test_to_memory_format():
+    def fn(a):
+        return a.to(memory_format=torch.channels_last)
+
+    a = torch.randn(2, 3, 4, 5)
+    out = thunder.jit(fn)(a)
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(out, a)
+
+
+def _serialize_fn(a, b, arr):
+    res = a + b
+    for t in arr:
+        res = res + t
+    return res
+
+
+def test_serialize_and_save_trace(tmp_path):
+    import dill
+
+    from lightning_thunder_amd.core.transforms import eval_trace
+
+    tm = thunder.jit(_serialize_fn)
+    a, b = torch.randn(2, 5)
+    tm(a, b, [a, b])
+    trace = thunder.last_traces(tm)[0]
+    assert str(dill.loads(dill.dumps(trace))) == str(trace)
+    pro = thunder.last_prologue_traces(tm)[0]
+    assert str(dill.loads(dill.dumps(pro))) == str(pro)
+    assert dill.loads(dill.dumps(thunder.dtypes.float32)) is thunder.dtypes.float32
+    p = tmp_path / "trace.py"
+    trace.save_trace(p)
+    assert p.read_text() == trace.python()
+    final = thunder.last_traces(tm)[-1]
+    out = eval_trace(final, *[a, b, a, b][: len(final.args)])  # the computation takes flattened inputs
+    torch.testing.assert_close(out if isinstance(out, torch.Tensor) else out[0], _serialize_fn(a, b, [a, b]))
