@@ -366,6 +366,32 @@ def _frame_locals(f: Frame) -> dict:
     return d
 
 
+def _flat_classes(cls):
+    if isinstance(cls, tuple):
+        for c in cls:
+            yield from _flat_classes(c)
+    else:
+        yield cls
+
+
+@register_lookaside(isinstance)
+def _isinstance_lookaside(interp, obj, cls):
+    """A parameter's proxy is an ``nn.Parameter`` to user code (``isinstance(m.weight,
+    nn.Parameter)`` branches must take the eager path)."""
+    from .proxies import TensorProxy
+
+    tags = getattr(obj, "tags", ()) if isinstance(obj, TensorProxy) else ()
+    if "parameter" in tags or "nn_parameter" in tags:
+        if any(c is torch.nn.Parameter for c in _flat_classes(cls)):
+            return True
+    return isinstance(obj, cls)
+
+
+@register_lookaside(torch.compile)
+def _torch_compile_lookaside(interp, *args, **kwargs):
+    raise NotImplementedError("Using torch.compile within a function to be JIT-compiled by Thunder is not supported.")
+
+
 @register_lookaside(super)
 def _super_lookaside(interp, *args):
     if args:
@@ -683,6 +709,14 @@ class Interpreter:
         gla = _global_lookasides.get(fn) if _hashable(fn) else None
         if gla is not None:
             return gla(self, *args, **kwargs), None
+        cd_inner = getattr(fn, "_lc_cd", None) if callable(fn) else None
+        if cd_inner is not None:
+            # a function or module compiled with jit called inside a jitted program: inlined
+            # (interpreted from its original callable), one program for the whole call tree
+            inner = getattr(fn, "_model", None) if isinstance(fn, torch.nn.Module) else None
+            target = inner if inner is not None else cd_inner.fn
+            self.log("inline jitted callable", _name(target))
+            return self._call(target, args, kwargs, None, arg_provs, kw_provs)
         if fn is getattr and len(args) >= 2 and isinstance(args[1], str) and not kwargs:
             if len(args) == 3 and not hasattr(args[0], args[1]):
                 return args[2], None  # the default: no provenance (nothing to re-fetch)

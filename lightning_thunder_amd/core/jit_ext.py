@@ -262,6 +262,12 @@ def _needs_restructure(spec) -> bool:
     return any(_needs_restructure(c) for c in spec.children)
 
 
+def _has_opaque_container(spec) -> bool:
+    if spec.kind in ("dataclass", "namedtuple", "structseq") or (spec.kind == "dict" and len(spec.ctx) > 2):
+        return True
+    return any(_has_opaque_container(c) for c in spec.children)
+
+
 def _argument_provenance(args, kwargs):
     """``Prov("input", key=flat_index)`` for every top-level argument that is a pytree leaf."""
     from .interpreter import Prov
@@ -449,6 +455,8 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                     if c is not None and c[0] is t:
                         return c[1]
                     p = tensorproxy(t, name=comp.make_unique_name("tp"))
+                    if isinstance(t, torch.nn.Parameter):
+                        p.tags.add("nn_parameter")  # isinstance(.., nn.Parameter) holds for user code
                     if root != "input":
                         # module / global / closure state lives across calls; tensors reached through
                         # an argument (a cache object handed in per call) belong to the caller
@@ -523,6 +531,10 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
             if all(t is not c for c in prog.constants):
                 prog.constants.append(t)
                 prog.input_specs.append(InputSpec("const", proxy=tracker.original(p), value=t))
+        if _has_opaque_container(out_spec):
+            # dataclasses / namedtuples are not printable in the program: it returns the flat
+            # leaves and the runtime rebuilds the container from ``output_spec``
+            result = tuple(tree_flatten(result)[0])
         if epi_values:
             prims.python_return((result, tuple(epi_values)))
         else:

@@ -71,7 +71,13 @@ def tree_flatten(tree, is_leaf: Callable | None = None) -> tuple[list, TreeSpec]
             return TreeSpec("list", None, [rec(v) for v in x])
         if isinstance(x, dict):
             keys = list(x.keys())
-            return TreeSpec("dict", (type(x), tuple(keys)), [rec(x[k]) for k in keys])
+            # a dataclass that subclasses dict (diffusers / HF model outputs): fields that are not
+            # (yet) keys travel as extra children so the rebuilt object has every attribute
+            extra = ()
+            if dataclasses.is_dataclass(x) and not isinstance(x, type):
+                extra = tuple(f.name for f in dataclasses.fields(x) if f.name not in x)
+            ctx = (type(x), tuple(keys)) if not extra else (type(x), tuple(keys), extra)
+            return TreeSpec("dict", ctx, [rec(x[k]) for k in keys] + [rec(getattr(x, f, None)) for f in extra])
         if dataclasses.is_dataclass(x) and not isinstance(x, type):
             fields = [f.name for f in dataclasses.fields(x)]
             return TreeSpec("dataclass", (type(x), tuple(fields)), [rec(getattr(x, f)) for f in fields])
@@ -98,18 +104,23 @@ def tree_unflatten(leaves, spec: TreeSpec):
         if s.kind == "structseq":
             return s.ctx(vals)
         if s.kind == "dict":
-            typ, keys = s.ctx
+            typ, keys = s.ctx[0], s.ctx[1]
+            extra = s.ctx[2] if len(s.ctx) > 2 else ()
+            extra_vals = dict(zip(extra, vals[len(keys):]))
+            vals = vals[:len(keys)]
             d = OrderedDict(zip(keys, vals)) if typ is OrderedDict else dict(zip(keys, vals))
             if typ not in (dict, OrderedDict):
                 if dataclasses.is_dataclass(typ):  # e.g. transformers ModelOutput (OrderedDict + dataclass)
                     try:
-                        return typ(**d)
+                        return typ(**d, **extra_vals)
                     except Exception:
                         pass
                 try:
                     nd = typ.__new__(typ)
                     dict.__init__(nd)
                     nd.update(d)
+                    for f, v in extra_vals.items():
+                        object.__setattr__(nd, f, v)
                     return nd
                 except Exception:
                     return d

@@ -362,3 +362,74 @@ def test_serialize_and_save_trace(tmp_path):
     final = thunder.last_traces(tm)[-1]
     out = eval_trace(final, *[a, b, a, b][: len(final.args)])  # the computation takes flattened inputs
     torch.testing.assert_close(out if isinstance(out, torch.Tensor) else out[0], _serialize_fn(a, b, [a, b]))
+
+
+def test_dataclass_outputs_hold_tensors():
+    import dataclasses
+
+    @dataclasses.dataclass
+    class Out:
+        a: torch.Tensor
+        d: dict
+
+    def f(x):
+        return Out(x * 2, {"k": x + 1})
+
+    r = thunder.jit(f)(torch.ones(2))
+    assert isinstance(r, Out) and type(r.a) is torch.Tensor and type(r.d["k"]) is torch.Tensor
+    torch.testing.assert_close(r.d["k"], torch.full((2,), 2.0))
+
+
+def test_dataclass_dict_output():
+    import dataclasses
+
+    @dataclasses.dataclass
+    class Foo(dict):  # diffusers-style output
+        musthave: int
+
+    def fn():
+        return Foo(musthave=1)
+
+    assert fn() == thunder.jit(fn)()
+    assert thunder.jit(fn)().musthave == 1
+
+
+def test_isinstance_parameter():
+    class Model(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(1, 1)
+
+        def forward(self, x):
+            return x + 1 if isinstance(self.fc.weight, torch.nn.Parameter) else x
+
+    m = Model()
+    x = torch.ones(1)
+    torch.testing.assert_close(thunder.jit(m)(x), m(x))
+    # a parameter reached through a closure
+    w = torch.nn.Parameter(torch.ones(1))
+    torch.testing.assert_close(thunder.jit(lambda x: x * 2 if isinstance(w, torch.nn.Parameter) else x)(x), x * 2)
+
+
+def test_compile_within_jit():
+    def model(a, b, c):
+        return a @ b + c
+
+    def jit_me(a, b, c):
+        return torch.compile(model)(a, b, c)
+
+    with pytest.raises(NotImplementedError, match="Using torch.compile within a function"):
+        thunder.jit(jit_me)(torch.randn(2, 2), torch.randn(2, 2), torch.randn(2, 2))
+
+
+def test_jitted_callable_inlined_in_jit():
+    g = thunder.jit(lambda x: x * 2)
+    lin = thunder.jit(torch.nn.Linear(2, 2))
+
+    def f(x):
+        return g(x) + lin(x).sum()
+
+    x = torch.randn(3, 2)
+    jf = thunder.jit(f)
+    torch.testing.assert_close(jf(x), x * 2 + lin._model(x).sum())
+    assert len(thunder.last_traces(jf)) > 0
