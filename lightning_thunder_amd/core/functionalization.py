@@ -87,11 +87,18 @@ def _const(x):
     return f(x)
 
 
+def _apply_view(v, name, args, kwargs):
+    if name == "as_strided_rel":  # an argument that is a strided window of another argument
+        size, stride, rel = args
+        return v.as_strided(size, stride, v.storage_offset() + rel)
+    return getattr(v, name)(*args, **kwargs)
+
+
 def _view_scatter_impl(base, src, chain):
     out = base.clone()
     v = out
     for name, args, kwargs, idx in chain:
-        v = getattr(v, name)(*args, **kwargs)
+        v = _apply_view(v, name, args, kwargs)
         if idx is not None:
             v = v[idx]
     v.copy_(src)
@@ -105,7 +112,7 @@ _view_scatter_impl.__module__ = "thunder"
 def _replay_impl(base, chain):
     v = base
     for name, args, kwargs, idx in chain:
-        v = getattr(v, name)(*args, **kwargs)
+        v = _apply_view(v, name, args, kwargs)
         if idx is not None:
             v = v[idx]
     return v
@@ -115,6 +122,7 @@ def storage_alias_pattern(flat_args) -> tuple:
     """Canonical storage-sharing pattern of the tensor arguments (cache key part)."""
     groups: dict = {}
     exact: dict = {}
+    first: dict = {}
     pat = []
     for x in flat_args:
         if not isinstance(x, torch.Tensor) or isinstance(x, Proxy) or x.device.type == "meta":
@@ -125,7 +133,11 @@ def storage_alias_pattern(flat_args) -> tuple:
             sp = id(x)
         g = groups.setdefault(sp, len(groups))
         e = exact.setdefault((sp, x.storage_offset(), tuple(x.shape), tuple(x.stride())), len(exact))
-        pat.append((g, e))
+        x0 = first.setdefault(sp, x)
+        if x0 is x:
+            pat.append((g, e))
+        else:  # a window of an earlier argument: the program replays it at this relative offset
+            pat.append((g, e, x.storage_offset() - x0.storage_offset(), tuple(x.shape), tuple(x.stride())))
     return tuple(pat)
 
 
@@ -159,6 +171,11 @@ class AliasTracker:
 
     def register_identity_alias(self, p: TensorProxy, base: TensorProxy) -> None:
         self.views[id(p)] = _ViewInfo(p, base, (), self.version.setdefault(id(base), 0))
+
+    def register_window_alias(self, p: TensorProxy, base: TensorProxy, size, stride, rel: int) -> None:
+        """``p`` is a strided window (``as_strided`` at element offset ``rel``) of the argument ``base``."""
+        chain = (("as_strided_rel", (tuple(size), tuple(stride), int(rel)), {}, None),)
+        self.views[id(p)] = _ViewInfo(p, base, chain, self.version.setdefault(id(base), 0))
 
     def original(self, p: TensorProxy) -> TensorProxy:
         """The proxy naming the caller's tensor for an input that may have been re-bound."""

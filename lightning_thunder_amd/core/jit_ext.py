@@ -262,6 +262,15 @@ def _needs_restructure(spec) -> bool:
     return any(_needs_restructure(c) for c in spec.children)
 
 
+def _is_window_of(x: torch.Tensor, x0: torch.Tensor) -> bool:
+    """Every element of ``x`` lies inside the (contiguous) argument ``x0``."""
+    if not x0.is_contiguous() or x.dtype != x0.dtype or x.numel() == 0:
+        return False
+    lo = x.storage_offset()
+    hi = lo + sum((n - 1) * st for n, st in zip(x.shape, x.stride()) if n > 0)
+    return x0.storage_offset() <= lo and hi < x0.storage_offset() + x0.numel() and min(x.stride(), default=1) >= 0
+
+
 def _has_opaque_container(spec) -> bool:
     if spec.kind in ("dataclass", "namedtuple", "structseq") or (spec.kind == "dict" and len(spec.ctx) > 2):
         return True
@@ -352,8 +361,15 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                     else:
                         by_view[key] = p
                         if sp in by_storage:
-                            tracker.partial_alias.update((id(p), id(by_storage[sp])))
-                        by_storage.setdefault(sp, p)
+                            x0, p0 = by_storage[sp]
+                            if _is_window_of(x, x0):
+                                # a strided window of an earlier argument (e.g. ``f(a, a[1:])``): an
+                                # in-place write to either is seen by the other through the view
+                                tracker.register_window_alias(p, p0, x.shape, x.stride(),
+                                                              x.storage_offset() - x0.storage_offset())
+                            else:
+                                tracker.partial_alias.update((id(p), id(p0)))
+                        by_storage.setdefault(sp, (x, p))
             elif symbolic_numbers and type(x) in (int, float):
                 from .proxies import IntegerProxy, FloatProxy
 

@@ -130,6 +130,12 @@ class NumberProxy(Proxy):
         hook = self._on_value
         if hook is not None:
             hook()
+        if self.value is None:
+            raise NotImplementedError(
+                f"the value of {self.name} ({self.python_type.__name__}) depends on tensor data (e.g. Tensor.item()) "
+                "and is unknown while the program is traced: data-dependent Python control flow or arithmetic "
+                "is not supported; express it with tensor operations (torch.where, masking) or move it out of "
+                "the compiled function")
         return self.value
 
     def __index__(self):

@@ -161,3 +161,36 @@ class _Mut(torch.nn.Module):
     def forward(self, x):
         self.lin.weight.add_(1)
         return self.lin(x)
+
+
+def test_inplace_through_argument_windows():
+    """Arguments that are strided windows of another argument (reference test_update_aliases
+    ``test_aliased_input`` / different-shape views): writes to either are seen through the other."""
+    import lightning_thunder_amd as thunder
+
+    def f(a, b):
+        a.add_(1)
+        return b * 2
+
+    def g(a, b):
+        b.mul_(3)
+        return a.sum()
+
+    for fn in (f, g):
+        jf = thunder.jit(fn)
+        for sl in (slice(1, None), slice(2, 6), slice(0, 3)):
+            x = torch.arange(8.0)
+            x2 = x.clone()
+            out = jf(x, x[sl])
+            ref = fn(x2, x2[sl])
+            torch.testing.assert_close(out, ref)
+            torch.testing.assert_close(x, x2)
+    # a 2-D window with a different shape
+    def h(a, b):
+        a.mul_(2)
+        return b + 1
+
+    x = torch.arange(12.0).reshape(3, 4)
+    x2 = x.clone()
+    torch.testing.assert_close(thunder.jit(h)(x, x[:, 1:3]), h(x2, x2[:, 1:3]))
+    torch.testing.assert_close(x, x2)
