@@ -261,3 +261,16 @@ def test_numerics_check_transform_cpu():
     assert any("non-finite" in m for m in t.findings)
     jd = thunder.jit(f, debug_options=thunder.DebugOptions(sync_after_each_kernel=True))
     torch.testing.assert_close(jd(x, y), f(x, y))
+
+
+def test_reference_module_paths():
+    import torch
+
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.dev_utils.nvtx_profile_transform import NvtxProfileTransform
+    from lightning_thunder_amd.examine.memory_calculation import get_alloc_memory
+
+    jf = thunder.jit(lambda x: (x * 2).sin(), transforms=[NvtxProfileTransform()])
+    jf(torch.ones(4))
+    peak, _ = get_alloc_memory(thunder.last_traces(jf)[-1])
+    assert peak > 0
