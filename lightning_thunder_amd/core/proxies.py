@@ -241,8 +241,22 @@ def _ltorch():
     return ltorch
 
 
+def _capture_real(x):
+    """A real tensor meeting a proxy in an operator (e.g. a constant built by an opaque call while
+    tracing) becomes a constant input of the program."""
+    if isinstance(x, torch.Tensor) and not isinstance(x, Proxy):
+        from .jit_ext import _current_state
+
+        st = _current_state()
+        if st is not None:
+            return st.proxify_constant(x)
+    return x
+
+
 def _method(name):
     def fn(self, *args, **kwargs):
+        if args:
+            args = tuple(_capture_real(a) for a in args)
         return getattr(_ltorch(), name)(self, *args, **kwargs)
 
     fn.__name__ = name
@@ -251,7 +265,7 @@ def _method(name):
 
 def _rmethod(name):
     def fn(self, other):
-        return getattr(_ltorch(), name)(other, self)
+        return getattr(_ltorch(), name)(_capture_real(other), self)
 
     fn.__name__ = "r" + name
     return fn

@@ -1009,7 +1009,11 @@ def triu(a, diagonal: int = 0):
 
 @torchsymbol(*_tfn("nn.functional.pad"))
 def pad(a, pad, mode: str = "constant", value=None):
-    check(mode == "constant", lambda: f"pad: only constant mode is supported, got {mode}")
+    if mode != "constant":
+        # reflect / replicate / circular: ATen's kernels (and their autograd) as an opaque op
+        from .default_torch_ops import opaque_symbol
+
+        return opaque_symbol(torch.nn.functional.pad, "nn.functional.pad")(a, tuple(pyval(p) for p in pad), mode=mode)
     value = 0 if value is None else pyval(value)
     cfg = [(0, 0, 0)] * a.ndim
     for i in range(len(pad) // 2):

@@ -915,7 +915,15 @@ def sdpa_reference_backward(q, k, v, attn_mask, is_causal, scale, g):
         shp = list(k.shape)
         dk = ltorch.sum(ltorch.reshape(dk, tuple(shp[:-3]) + (shp[-3], rep) + tuple(shp[-2:])), -3)
         dv = ltorch.sum(ltorch.reshape(dv, tuple(shp[:-3]) + (shp[-3], rep) + tuple(shp[-2:])), -3)
-    return (clang.maybe_convert_to_dtype(dq, q.dtype), clang.maybe_convert_to_dtype(dk, k.dtype), clang.maybe_convert_to_dtype(dv, v.dtype))
+    grads = (clang.maybe_convert_to_dtype(dq, q.dtype), clang.maybe_convert_to_dtype(dk, k.dtype),
+             clang.maybe_convert_to_dtype(dv, v.dtype))
+    if attn_mask is not None and attn_mask.dtype != torch.bool and attn_mask.requires_grad:
+        # an additive float mask enters the scores unscaled: its gradient is dS, reduced over the
+        # dimensions the mask was broadcast along
+        from ..core.transforms import sum_to_shape
+
+        grads += (clang.maybe_convert_to_dtype(sum_to_shape(ds, attn_mask.shape), attn_mask.dtype),)
+    return grads
 
 
 _installed = False
