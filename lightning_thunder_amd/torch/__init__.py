@@ -1095,6 +1095,9 @@ def _getitem_sym(a, key):
     tensor_keys = [k for k in key if isinstance(k, TensorProxy)]
     if tensor_keys:
         return _advanced_getitem(a, key)
+    if builtins.any(isinstance(k, builtins.list) for k in key):
+        # a list of indices (``x[[-2]]``, ``x[:, [0, 2]]``): advanced indexing with constant indices
+        return _opaque_index(a, tuple(pyval(k) if isinstance(k, NumberProxy) else k for k in key))
     # expand ellipsis
     n_specified = builtins.sum(1 for k in key if k is not None and k is not Ellipsis)
     if builtins.any(k is Ellipsis for k in key):

@@ -199,3 +199,58 @@ def test_hf_rope_transform_rewrites_attention_prologue():
     # on CPU tensors the transform stays off by default
     _, same, _ = HFRoPETransform().transform_traces_pre_prologue(None, comp, None)
     assert same is comp
+
+
+def _hf_arch(name):
+    import transformers as tf
+
+    ids = torch.randint(0, 100, (2, 12), generator=torch.Generator().manual_seed(0))
+    small = dict(vocab_size=100, hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=4,
+                 max_position_embeddings=64)
+    if name == "gpt2":
+        return tf.GPT2LMHeadModel(tf.GPT2Config(vocab_size=100, n_embd=32, n_layer=2, n_head=2, n_positions=64)), {"input_ids": ids}
+    if name == "mistral":
+        return tf.MistralForCausalLM(tf.MistralConfig(**small, num_key_value_heads=2)), {"input_ids": ids}
+    if name == "qwen2":
+        return tf.Qwen2ForCausalLM(tf.Qwen2Config(**small, num_key_value_heads=2)), {"input_ids": ids}
+    if name == "phi":
+        return tf.PhiForCausalLM(tf.PhiConfig(**small)), {"input_ids": ids}
+    if name == "gemma":
+        return tf.GemmaForCausalLM(tf.GemmaConfig(**small, num_key_value_heads=1, head_dim=8)), {"input_ids": ids}
+    if name == "t5":
+        cfg = tf.T5Config(vocab_size=100, d_model=32, d_kv=8, d_ff=64, num_layers=2, num_heads=4)
+        return tf.T5ForConditionalGeneration(cfg), {"input_ids": ids, "decoder_input_ids": ids[:, :5]}
+    if name == "vit":
+        cfg = tf.ViTConfig(hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64, image_size=16,
+                           patch_size=4)
+        return tf.ViTModel(cfg), {"pixel_values": torch.randn(2, 3, 16, 16, generator=torch.Generator().manual_seed(1))}
+    if name == "roberta":
+        cfg = tf.RobertaConfig(vocab_size=100, hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64)
+        return tf.RobertaModel(cfg), {"input_ids": ids}
+    if name == "mixtral":
+        return tf.MixtralForCausalLM(tf.MixtralConfig(**small, num_key_value_heads=2, num_local_experts=4,
+                                                      num_experts_per_tok=2)), {"input_ids": ids}
+    if name == "falcon":
+        return tf.FalconForCausalLM(tf.FalconConfig(vocab_size=100, hidden_size=32, num_hidden_layers=2,
+                                                    num_attention_heads=4)), {"input_ids": ids}
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name", ["gpt2", "mistral", "qwen2", "phi", "gemma", "t5", "vit", "roberta", "mixtral", "falcon"])
+def test_hf_architectures_fwd_bwd(name):
+    """HF transformers architectures through the interpreter: outputs and parameter gradients
+    match eager (reference analogue: thunder/tests/test_networks.py HF model tests)."""
+    torch.manual_seed(0)
+    model, inputs = _hf_arch(name)
+    model.eval()
+    key = "logits" if hasattr(model, "lm_head") or name == "t5" else "last_hidden_state"
+    ref = getattr(model(**inputs), key)
+    ref.float().pow(2).mean().backward()
+    ref_grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad()
+    out = getattr(thunder.jit(model)(**inputs), key)
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+    out.float().pow(2).mean().backward()
+    for n, g in ref_grads.items():
+        p = dict(model.named_parameters())[n]
+        torch.testing.assert_close(p.grad, g, atol=1e-4, rtol=1e-3, msg=n)

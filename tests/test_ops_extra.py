@@ -113,3 +113,17 @@ def test_data_dependent_branch_error_is_clear():
 
     with pytest.raises(NotImplementedError, match="depends on tensor data"):
         thunder.jit(f)(torch.ones(3))
+
+
+def test_list_index():
+    def f(a):
+        return a[[-2]] + a[:, [0, 2]].sum()
+
+    a = X(4, 3).requires_grad_(True)
+    b = a.detach().clone().requires_grad_(True)
+    out = thunder.jit(f)(a)
+    ref = f(b)
+    torch.testing.assert_close(out, ref)
+    out.sum().backward()
+    ref.sum().backward()
+    torch.testing.assert_close(a.grad, b.grad)
