@@ -254,3 +254,30 @@ def test_hf_architectures_fwd_bwd(name):
     for n, g in ref_grads.items():
         p = dict(model.named_parameters())[n]
         torch.testing.assert_close(p.grad, g, atol=1e-4, rtol=1e-3, msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gpt2", "mistral", "qwen2", "phi", "gemma", "t5", "vit", "roberta", "mixtral", "falcon"])
+def test_hf_architectures_gpu_bf16(name):
+    """The same architectures in bf16 on the MI355X with the HIP executors claiming what they can
+    (flash attention, RMSNorm / LayerNorm, GEMMs, fused elementwise): close to eager bf16."""
+    torch.manual_seed(0)
+    model, inputs = _hf_arch(name)
+    model = model.to("cuda", torch.bfloat16).eval()
+    inputs = {k: (v.to("cuda", torch.bfloat16) if v.is_floating_point() else v.cuda()) for k, v in inputs.items()}
+    key = "logits" if hasattr(model, "lm_head") or name == "t5" else "last_hidden_state"
+    ref = getattr(model(**inputs), key).float()
+    ref.pow(2).mean().backward()
+    ref_grads = {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad()
+    out = getattr(thunder.jit(model)(**inputs), key).float()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    out.pow(2).mean().backward()
+    scale = max(g.norm().item() for g in ref_grads.values())
+    for n, g in ref_grads.items():
+        p = dict(model.named_parameters())[n]
+        if g.norm() < 1e-3 * scale:
+            continue  # e.g. attention key biases: exactly zero in exact arithmetic (softmax shift invariance)
+        cos = torch.nn.functional.cosine_similarity(p.grad.float().flatten(), g.flatten(), dim=0).item()
+        assert cos > 0.98, (n, cos)
