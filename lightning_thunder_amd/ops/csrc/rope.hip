@@ -133,6 +133,93 @@ __global__ __launch_bounds__(256) void qkv_rope_bwd_kernel(const T* __restrict__
   }
 }
 
+// Full-width RoPE (rope_n == hs, the Llama case), one token row per workgroup: each work item owns a
+// chunk and its rotation partner half a head away, so no lane idles, and the item -> (head, chunk)
+// split is a shift (no 64-bit division); cos / sin rows are read as 16-B vectors.
+template <typename C>
+__device__ __forceinline__ void load_cs8(const C* p, float (&o)[8]) {
+  if constexpr (sizeof(C) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  } else {
+    const Vec16<C> v = load16(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = to_f32(v.v[j]);
+  }
+}
+
+template <typename T, typename C, bool BWD>
+__global__ __launch_bounds__(256) void qkv_rope_row_kernel(const T* __restrict__ in0, const T* __restrict__ in1,
+                                                           const T* __restrict__ in2, const C* __restrict__ cos_,
+                                                           const C* __restrict__ sin_, T* __restrict__ out0,
+                                                           T* __restrict__ out1, T* __restrict__ out2,
+                                                           const int64_t* __restrict__ pos, KVDst st, int Tn, int nh,
+                                                           int ng, int hs, int pair_shift) {
+  // fwd: in0 = qkv, out0/1/2 = q/k/v (k/v through st); bwd: in0/1/2 = dq/dk/dv, out0 = dqkv
+  constexpr int VW = 8;
+  const int row = blockIdx.x;  // b * Tn + t
+  const int t = row % Tn, b = row / Tn;
+  const int heads = nh + 2 * ng, half = hs / 2;
+  const int items = heads << pair_shift;
+  const C* cr = cos_ + (int64_t)t * hs;
+  const C* sr = sin_ + (int64_t)t * hs;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int h = it >> pair_shift, d0 = (it & ((1 << pair_shift) - 1)) * VW;
+    const T* src;
+    T* dst;
+    if constexpr (!BWD) {
+      src = in0 + ((int64_t)row * heads + h) * hs;
+      if (h < nh) {
+        dst = out0 + (((int64_t)b * nh + h) * Tn + t) * hs;
+      } else {
+        const int64_t s = pos ? pos[t] : t;
+        dst = h < nh + ng ? out1 + b * st.ksb + (h - nh) * st.ksg + s * st.kss
+                          : out2 + b * st.vsb + (h - nh - ng) * st.vsg + s * st.vss;
+      }
+    } else {
+      dst = out0 + ((int64_t)row * heads + h) * hs;
+      src = h < nh ? in0 + (((int64_t)b * nh + h) * Tn + t) * hs
+                   : (h < nh + ng ? in1 + (((int64_t)b * ng + (h - nh)) * Tn + t) * hs
+                                  : in2 + (((int64_t)b * ng + (h - nh - ng)) * Tn + t) * hs);
+    }
+    const Vec16<T> x1 = load16(src + d0), x2 = load16(src + d0 + half);
+    if (h >= nh + ng) {  // v: layout change only
+      store16(dst + d0, x1);
+      store16(dst + d0 + half, x2);
+      continue;
+    }
+    float c1[8], s1[8], c2[8], s2[8];
+    load_cs8(cr + d0, c1);
+    load_cs8(sr + d0, s1);
+    load_cs8(cr + d0 + half, c2);
+    load_cs8(sr + d0 + half, s2);
+    Vec16<T> o1, o2;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const float a = to_f32(x1.v[j]), bb = to_f32(x2.v[j]);
+      if constexpr (!BWD) {
+        o1.v[j] = from_f32<T>(a * c1[j] - bb * s1[j]);
+        o2.v[j] = from_f32<T>(bb * c2[j] + a * s2[j]);
+      } else {  // transpose of the rotation
+        o1.v[j] = from_f32<T>(a * c1[j] + bb * s2[j]);
+        o2.v[j] = from_f32<T>(bb * c2[j] - a * s1[j]);
+      }
+    }
+    store16(dst + d0, o1);
+    store16(dst + d0 + half, o2);
+  }
+}
+
+// shift with (1 << shift) == hs / 16 (chunk pairs per head), or -1 when the row kernel does not apply
+int row_pair_shift(int dtype, int hs, int rope_n) {
+  if (dtype == kF32 || rope_n != hs || hs % 16) return -1;
+  const int pairs = hs / 16;
+  if (pairs & (pairs - 1)) return -1;
+  int sh = 0;
+  while ((1 << sh) < pairs) ++sh;
+  return sh;
+}
+
 int grid_for(int64_t total) {
   int64_t g = (total + 255) / 256;
   if (g > 256 * 16) g = 256 * 16;
@@ -162,6 +249,14 @@ static int qkv_rope_fwd_launch(int dtype, int cdtype, const void* qkv, const voi
                                void* k, void* v, const int64_t* pos, KVDst st, int B, int Tn, int nh, int ng, int hs,
                                int rope_n, hipStream_t stream) {
   if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
+  const int sh = row_pair_shift(dtype, hs, rope_n);
+  if (sh >= 0) {
+    LTA_DISPATCH_TC(dtype, cdtype,
+                    hipLaunchKernelGGL((qkv_rope_row_kernel<T, C, false>), dim3(B * Tn), dim3(256), 0, stream,
+                                       (const T*)qkv, (const T*)nullptr, (const T*)nullptr, (const C*)cos_,
+                                       (const C*)sin_, (T*)q, (T*)k, (T*)v, pos, st, Tn, nh, ng, hs, sh));
+    return (int)hipGetLastError();
+  }
   const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / (dtype == kF32 ? 4 : 8));
   LTA_DISPATCH_TC(dtype, cdtype,
                   hipLaunchKernelGGL((qkv_rope_fwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
@@ -193,6 +288,15 @@ LTA_EXPORT int lta_qkv_rope_bwd(int dtype, int cdtype, const void* dq, const voi
                                 const void* sin_, void* dqkv, int B, int Tn, int nh, int ng, int hs, int rope_n,
                                 hipStream_t stream) {
   if (hs % 8 || rope_n % 16 || rope_n > hs) return -2;
+  const int sh = row_pair_shift(dtype, hs, rope_n);
+  if (sh >= 0) {
+    LTA_DISPATCH_TC(dtype, cdtype,
+                    hipLaunchKernelGGL((qkv_rope_row_kernel<T, C, true>), dim3(B * Tn), dim3(256), 0, stream,
+                                       (const T*)dq, (const T*)dk, (const T*)dv, (const C*)cos_, (const C*)sin_,
+                                       (T*)dqkv, (T*)nullptr, (T*)nullptr, (const int64_t*)nullptr, KVDst{0, 0, 0, 0, 0, 0},
+                                       Tn, nh, ng, hs, sh));
+    return (int)hipGetLastError();
+  }
   const int64_t total = (int64_t)B * Tn * (nh + 2 * ng) * (hs / (dtype == kF32 ? 4 : 8));
   LTA_DISPATCH_TC(dtype, cdtype,
                   hipLaunchKernelGGL((qkv_rope_bwd_kernel<T, C>), dim3(grid_for(total)), dim3(256), 0, stream,
