@@ -380,11 +380,22 @@ def _isinstance_lookaside(interp, obj, cls):
     nn.Parameter)`` branches must take the eager path)."""
     from .proxies import TensorProxy
 
-    tags = getattr(obj, "tags", ()) if isinstance(obj, TensorProxy) else ()
-    if "parameter" in tags or "nn_parameter" in tags:
-        if any(c is torch.nn.Parameter for c in _flat_classes(cls)):
-            return True
+    if isinstance(obj, TensorProxy):
+        # a traced tensor is a torch.Tensor to user code (HF code branches on
+        # ``isinstance(mask, torch.Tensor)``); a parameter's proxy is also an nn.Parameter
+        tags = getattr(obj, "tags", ())
+        is_param = "parameter" in tags or "nn_parameter" in tags
+        for c in _flat_classes(cls):
+            if c is torch.Tensor or (c is torch.nn.Parameter and is_param):
+                return True
     return isinstance(obj, cls)
+
+
+@register_lookaside(torch.is_tensor)
+def _is_tensor_lookaside(interp, obj):
+    from .proxies import TensorProxy
+
+    return isinstance(obj, (torch.Tensor, TensorProxy))
 
 
 @register_lookaside(torch.compile)

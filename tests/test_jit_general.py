@@ -433,3 +433,15 @@ def test_jitted_callable_inlined_in_jit():
     jf = thunder.jit(f)
     torch.testing.assert_close(jf(x), x * 2 + lin._model(x).sum())
     assert len(thunder.last_traces(jf)) > 0
+
+
+def test_isinstance_tensor_and_is_tensor_in_user_code():
+    def f(x, m):
+        y = x * 2 if isinstance(x, torch.Tensor) else x
+        if torch.is_tensor(m):
+            y = y + m
+        return y
+
+    x = torch.ones(2)
+    torch.testing.assert_close(thunder.jit(f)(x, x), f(x, x))
+    torch.testing.assert_close(thunder.jit(f)(x, None), f(x, None))
