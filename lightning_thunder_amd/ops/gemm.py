@@ -85,6 +85,8 @@ def enable_tuned_gemms() -> bool:
     not in the file use the library default).  Returns whether the results are active."""
     if "active" in _tuned_state:
         return _tuned_state["active"]
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return False  # never switch TunableOp on inside a graph capture; the next eager call will
     active = False
     tun = getattr(torch.cuda, "tunable", None)
     if (_os.environ.get("LTA_TUNED_GEMMS", "1") != "0" and torch.version.hip is not None and tun is not None

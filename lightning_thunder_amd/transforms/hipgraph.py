@@ -159,8 +159,18 @@ class HipGraphRunner:
         ins = tuple(a.clone() if i in clone and isinstance(a, torch.Tensor) else a for i, a in enumerate(args))
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, pool=self.owner.pool()):
-            outs = self.fn(*ins)
+        # TunableOp's GEMM path creates a BLAS handle per stream on first use, which a capture
+        # stream cannot do: capture with the library's default solutions
+        tun = getattr(torch.cuda, "tunable", None)
+        tuned = tun is not None and tun.is_enabled()
+        if tuned:
+            tun.enable(False)
+        try:
+            with torch.cuda.graph(g, pool=self.owner.pool()):
+                outs = self.fn(*ins)
+        finally:
+            if tuned:
+                tun.enable(True)
         outs = tuple(outs) if isinstance(outs, (tuple, list)) else (outs,)
         e = (ins, g, outs)
         self.entries[key] = e

@@ -1,4 +1,6 @@
 """HipGraphTransform tests (reference: ``thunder/tests/test_transforms.py`` CUDAGraph tests)."""
+import os
+
 import pytest
 import torch
 
@@ -160,3 +162,29 @@ def test_runner_never_writes_other_callers_storage_gpu():
     assert r.captures == 2
     (ins_bound, _, _), = [e for k, e in r.entries.items() if not k[1]]
     assert ins_bound[0] is A and ins_bound[1] is not None
+
+
+@pytest.mark.gpu
+def test_capture_with_tuned_gemm_table_active():
+    """The shipped TunableOp table is active for the GEMM selector; a hipGraph capture that runs a
+    library GEMM first on the capture stream must still work (TunableOp off while capturing).
+    Fresh process: the capture stream must not have a BLAS handle from earlier tests."""
+    import subprocess
+    import sys
+
+    code = (
+        "import torch, lightning_thunder_amd as thunder\n"
+        "from lightning_thunder_amd.ops.gemm import enable_tuned_gemms\n"
+        "from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform\n"
+        "assert enable_tuned_gemms() or True\n"
+        "f = lambda a, b: (a @ b).sin() + 1\n"
+        "jf = thunder.jit(f, transforms=[HipGraphTransform()])\n"
+        "a = torch.randn(64, 32, device='cuda'); b = torch.randn(32, 48, device='cuda')\n"
+        "for _ in range(3):\n"
+        "    torch.testing.assert_close(jf(a, b), f(a, b), atol=1e-4, rtol=1e-4)\n"
+        "print('OK')\n"
+    )
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.abspath(__file__))) + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
