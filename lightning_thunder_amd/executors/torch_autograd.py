@@ -41,7 +41,18 @@ class ThunderFunction(torch.autograd.Function):
     def backward(ctx, *grads):
         entry = ctx.entry
         args = ctx.saved
-        ctx.saved = None
+        keep = False
+        try:  # backward(retain_graph=True): the saved tensors must survive this pass
+            keep = torch._C._autograd._get_current_graph_task_keep_graph()
+        except (AttributeError, RuntimeError):
+            pass
+        if args is None:
+            raise RuntimeError("Trying to backward through the graph a second time (or directly access saved tensors "
+                               "after they have already been freed); specify retain_graph=True on the first backward")
+        if keep:
+            args = list(args)  # the backward program clears the list it is handed
+        else:
+            ctx.saved = None
         # align tensor-output grads with the differentiable outputs
         gi = iter(grads)
         cts = []

@@ -538,12 +538,22 @@ def _install_ltorch_rules():
 
         return out, bwd
 
+    def _cj(t):
+        if isinstance(t, TensorProxy) and dtypes.is_complex_dtype(t.dtype):
+            from ..torch.default_torch_ops import opaque_symbol
+
+            return opaque_symbol(torch.conj_physical)(t)
+        if isinstance(t, complex):
+            return t.conjugate()
+        return t
+
     @register_vjp(ltorch.mul)
     def _mul(a, b):
         out = ltorch.mul(a, b)
 
         def bwd(g):
-            return (ltorch.mul(g, b) if rg(a) else None), (ltorch.mul(g, a) if rg(b) else None)
+            # complex operands: PyTorch's convention is grad_a = g * conj(b)
+            return (ltorch.mul(g, _cj(b)) if rg(a) else None), (ltorch.mul(g, _cj(a)) if rg(b) else None)
 
         return out, bwd
 
@@ -590,6 +600,17 @@ def _install_ltorch_rules():
     @register_vjp(ltorch.neg)
     def _neg(a):
         return ltorch.neg(a), lambda g: (ltorch.neg(g),)
+
+    # complex parts (PyTorch's convention: real(z) -> g + 0j, imag(z) -> g * 1j)
+    from ..core import prims as _prims
+
+    @register_vjp(_prims.real)
+    def _real(a):
+        return _prims.real(a), lambda g: (clang.maybe_convert_to_dtype(g, a.dtype),)
+
+    @register_vjp(_prims.imag)
+    def _imag(a):
+        return _prims.imag(a), lambda g: (ltorch.mul(clang.maybe_convert_to_dtype(g, a.dtype), 1j),)
 
     @register_vjp(ltorch.exp)
     def _exp(a):

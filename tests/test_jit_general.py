@@ -445,3 +445,38 @@ def test_isinstance_tensor_and_is_tensor_in_user_code():
     x = torch.ones(2)
     torch.testing.assert_close(thunder.jit(f)(x, x), f(x, x))
     torch.testing.assert_close(thunder.jit(f)(x, None), f(x, None))
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_complex_gradients(k):
+    fns = [lambda x: (x * x.conj()).real.sum(), lambda x: (x * 3).imag.sum(), lambda x: (x.real * x.imag).sum(),
+           lambda x: torch.view_as_real(x * 2).sum()]
+    f = fns[k]
+    x = torch.randn(3, dtype=torch.complex64, requires_grad=True)
+    y = x.detach().clone().requires_grad_(True)
+    thunder.jit(f)(x).backward()
+    f(y).backward()
+    torch.testing.assert_close(x.grad, y.grad)
+
+
+def test_backward_retain_graph():
+    x = torch.randn(3, requires_grad=True)
+    out = thunder.jit(lambda x: (x ** 2).sum())(x)
+    out.backward(retain_graph=True)
+    out.backward()
+    torch.testing.assert_close(x.grad, 4 * x.detach())
+    with pytest.raises(RuntimeError, match="second time"):
+        out.backward()
+
+
+def test_train_eval_switch_retraces():
+    m = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Dropout(0.5))
+    jm = thunder.jit(m)
+    x = torch.ones(8, 4)
+    m.eval()
+    torch.testing.assert_close(jm(x), m(x))
+    m.train()
+    torch.manual_seed(0)
+    out = jm(x)
+    assert (out == 0).any()  # dropout active again
+    assert thunder.cache_misses(jm) == 2
