@@ -71,6 +71,9 @@ from .transforms import autodiff as _autodiff  # noqa: E402
 _autodiff.install()
 
 
+from .core.profile import annotate_for_profile as _annotate_for_profile  # noqa: E402
+
+
 def _default_executor_list():
     return get_default_executors()
 
@@ -380,6 +383,7 @@ def jit(
     cs = CompileStats()
     holder: dict[str, Any] = {"module": None}
 
+    @_annotate_for_profile("get_computation_and_inputs")
     def get_computation_and_inputs(args, kwargs):
         cs.last_trace_cache_start = time.perf_counter_ns()
         flat_args, _ = tree_flatten((args, kwargs))
@@ -417,6 +421,7 @@ def jit(
         inps = entry.prologue_fn(flat_args, entry.module_state(), entry.constants, entry.guard_roots)
         return entry, inps
 
+    @_annotate_for_profile("fn_")
     def fn_(*args, **kwargs):
         cs.calls += 1
         cs.last_trace_host_start = time.perf_counter_ns()

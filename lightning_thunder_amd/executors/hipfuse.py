@@ -26,6 +26,7 @@ import threading
 
 import torch
 
+from ..core import profile as _profile
 from ..core.prims import PrimIDs, OpTags
 from ..core.proxies import TensorProxy, Proxy
 from ..core.pytree import tree_flatten, tree_map
@@ -159,6 +160,12 @@ class HipFusion:
             return v
 
     def __call__(self, *args):
+        if _profile.profiling_enabled():
+            with _profile.add_markers(self.name):
+                return self._call(args)
+        return self._call(args)
+
+    def _call(self, args):
         tensors = [args[i] for i in self.tensor_pos]
         dev = tensors[0].device if tensors else None
         if dev is None or dev.type != "cuda":

@@ -35,6 +35,7 @@ from ..core.symbol import BoundSymbol, BoundSymbolTag, Symbol, NON_DIFFERENTIABL
 from ..core.trace import TraceCtx, tracectx, from_trace, TraceProvenance, get_tracectx
 from ..core.transforms import get_vjp_rule, register_vjp, _vjp_rules, grad_like, sum_to_shape, linear_backward, _requires
 from ..core.transform_common import dce
+from ..common import get_compile_option
 
 
 class GradsWithKwargs:
@@ -214,6 +215,21 @@ class ForwardBackward:
         self.diff_output_mask = diff_output_mask
 
 
+_EXPENSIVE_NAME_PARTS = ("matmul", "linear", "scaled_dot_product", "attention", "grouped_mm", "conv", "bmm", "einsum")
+
+
+def _never_auto_recompute(b: BoundSymbol) -> bool:
+    """Ops ``auto_recompute_intermediates`` leaves saved: GEMM/attention-shaped and random ops
+    (reference: ``DONT_AUTO_RECOMPUTE_IN_BACKWARD`` on sdpa/matmul, ``RANDOM_OP``)."""
+    tags = set(b.sym.tags or ())
+    if tags & {OpTags.RANDOM_OP, OpTags.MATMUL_OP, OpTags.DONT_AUTO_RECOMPUTE_IN_BACKWARD}:
+        return True
+    if BoundSymbolTag.DONT_AUTO_RECOMPUTE_IN_BACKWARD in b.tags:
+        return True
+    name = b.sym.name.lower()
+    return any(part in name for part in _EXPENSIVE_NAME_PARTS)
+
+
 def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> ForwardBackward:
     start = time.perf_counter_ns()
     fw = from_trace(trace)
@@ -235,6 +251,10 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
         return x
 
     ret_bsym = None
+    auto_recompute = bool(get_compile_option(
+        "auto_recompute_intermediates",
+        "Recompute the intermediates of differentiated decompositions in the backward instead of "
+        "saving them (fewer saved tensors, more compute); matmul/attention/random ops are never recomputed"))
 
     def process(bsym: BoundSymbol, recompute: bool = False):
         nonlocal ret_bsym
@@ -250,7 +270,7 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
         if BoundSymbolTag.RECOMPUTE_IN_BACKWARD in bsym.tags:
             recompute = True
         if not _is_differentiable_bsym(b):
-            if recompute:
+            if recompute and not (recompute == "auto" and _never_auto_recompute(b)):
                 b.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
             fw.bound_symbols.append(b)
             return
@@ -280,12 +300,21 @@ def forward_and_backward_from_trace(trace: TraceCtx, *, executors=()) -> Forward
             del fw.bound_symbols[n_before:]  # the rule declined (unsupported options)
         if res is None:  # differentiate the decomposition
             if b.subsymbols:
+                auto = auto_recompute and not recompute and not _never_auto_recompute(b)
                 for s in b.subsymbols:
-                    process(s, recompute)
+                    process(s, "auto" if auto else recompute)
+                if auto:
+                    # auto_recompute_intermediates (reference trace_interpreter.py:204-222): the
+                    # decomposition's intermediates are recomputed in the backward instead of
+                    # saved; the decomposed op's own outputs stay ordinary forward values.
+                    finals = {sw(o).name for o in bsym.flat_proxy_outs}
+                    for nb in fw.bound_symbols[n_before:]:
+                        if any(o.name in finals for o in nb.flat_proxy_outs):
+                            nb.tags.discard(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
                 return
             raise NotImplementedError(f"No VJP rule for {b.sym.name} ({b.sym.id}) and it has no decomposition")
         out, bwd = res
-        if recompute:
+        if recompute and not (recompute == "auto" and _never_auto_recompute(b)):
             for nb in fw.bound_symbols[n_before:]:
                 nb.tags.add(BoundSymbolTag.RECOMPUTE_IN_BACKWARD)
         old_flat = [o for o in tree_flatten(bsym.output)[0]]

@@ -64,3 +64,26 @@ def test_litgpt_activation_checkpointing():
     for n, g in outs[False][0].items():
         torch.testing.assert_close(outs[True][0][n], g, rtol=1e-4, atol=1e-5)
     assert outs[True][1] < outs[False][1]
+
+
+def test_auto_recompute_intermediates():
+    """``auto_recompute_intermediates=True`` (reference ``core/trace_interpreter.py:204-222``):
+    intermediates of differentiated decompositions are recomputed in the backward, so fewer
+    tensors are saved; gradients are unchanged."""
+    def f(x, w):
+        return torch.logsumexp(x * w, -1).sum()
+
+    x0 = torch.arange(128.0).reshape(8, 16).sin()
+    w0 = torch.linspace(-1, 1, 16)
+    res = {}
+    for opt in (False, True):
+        x, w = x0.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+        jf = thunder.jit(f, auto_recompute_intermediates=opt)
+        jf(x, w).backward()
+        res[opt] = (len(_saved(jf)), x.grad, w.grad)
+    assert res[True][0] < res[False][0], (res[True][0], res[False][0])
+    x, w = x0.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+    f(x, w).backward()
+    for opt in (False, True):
+        torch.testing.assert_close(res[opt][1], x.grad)
+        torch.testing.assert_close(res[opt][2], w.grad)

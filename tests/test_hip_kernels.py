@@ -144,15 +144,17 @@ def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
         assert err < (2e-2 if dtype == torch.bfloat16 else 5e-3), (name, err)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_fused_adamw_matches_torch(dtype):
+@pytest.mark.parametrize("dtype,state_dtype", [(torch.bfloat16, torch.float32), (torch.float32, torch.float32),
+                                               (torch.bfloat16, torch.bfloat16)])
+def test_fused_adamw_matches_torch(dtype, state_dtype):
     from lightning_thunder_amd.optim import AdamW
 
     torch.manual_seed(0)
-    shapes = [(33,), (128, 64), (7, 5, 3), (4096,)]
+    # (3, 9000): chunks whose tail leaves a single vector step (unrolled loop + remainder loop)
+    shapes = [(33,), (128, 64), (7, 5, 3), (4096,), (3, 9000), (40000,)]
     ps = [torch.randn(s, device="cuda", dtype=dtype, requires_grad=True) for s in shapes]
     qs = [p.detach().clone().float().requires_grad_(True) for p in ps]
-    o1 = AdamW(ps, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, state_dtype=torch.float32)
+    o1 = AdamW(ps, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, state_dtype=state_dtype)
     o2 = torch.optim.AdamW(qs, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
     for _ in range(3):
         for p, q in zip(ps, qs):
