@@ -47,36 +47,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
   const bool vec = ((end - start) % VP == 0) && ((uintptr_t)(P + start) % 16 == 0) && ((uintptr_t)(G + start) % 16 == 0) &&
                    (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0);
   if (vec) {
-    // Two 16-byte vectors per stream per lane per iteration: all eight loads are issued
-    // before any math so each lane keeps 128 B in flight (one vector each reached ~5.9 TB/s).
-    constexpr int64_t kStep = 256 * VP;
-    int64_t i = start + (int64_t)threadIdx.x * VP;
-    for (; i + kStep < end; i += 2 * kStep) {
-      Vec16<TP> pv[2], gv[2];
-      Vec16<TS> mv[2], vv[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        pv[u] = load16(P + i + u * kStep);
-        gv[u] = load16(G + i + u * kStep);
-        mv[u] = load16(M + i + u * kStep);
-        vv[u] = load16(V + i + u * kStep);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-#pragma unroll
-        for (int j = 0; j < VP; ++j) {
-          float p = to_f32(pv[u].v[j]), m = to_f32(mv[u].v[j]), v = to_f32(vv[u].v[j]);
-          adamw_elem<TP, TS>(p, to_f32(gv[u].v[j]) * grad_scale, m, v, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
-          pv[u].v[j] = from_f32<TP>(p);
-          mv[u].v[j] = from_f32<TS>(m);
-          vv[u].v[j] = from_f32<TS>(v);
-        }
-        store16(P + i + u * kStep, pv[u]);
-        store16(M + i + u * kStep, mv[u]);
-        store16(V + i + u * kStep, vv[u]);
-      }
-    }
-    for (; i < end; i += kStep) {
+    for (int64_t i = start + (int64_t)threadIdx.x * VP; i < end; i += 256 * VP) {
       Vec16<TP> pv = load16(P + i), gv = load16(G + i);
       Vec16<TS> mv = load16(M + i), vv = load16(V + i);
 #pragma unroll
