@@ -319,7 +319,9 @@ _OPAQUE_TOP = {"torch", "lightning_thunder_amd", "numpy", "einops", "typing_exte
                "networkx", "safetensors", "pydantic", "pydantic_core"}
 # model code shipped inside this package is user code, and so are torch.nn modules (their
 # attribute reads, e.g. ``self.training``, must become guards of the program): interpret them
-_INTERPRETED_PREFIXES = ("lightning_thunder_amd.models", "torch.nn.modules")
+_INTERPRETED_PREFIXES = ("lightning_thunder_amd.models", "torch.nn.modules",
+                         # distribute_module's hook lambdas: user input/output functions run interpreted
+                         "torch.distributed.tensor._api")
 _STDLIB = set(getattr(sys, "stdlib_module_names", ())) | {"builtins", "__future__"}
 
 
@@ -383,11 +385,18 @@ def _isinstance_lookaside(interp, obj, cls):
 
     if isinstance(obj, TensorProxy):
         # a traced tensor is a torch.Tensor to user code (HF code branches on
-        # ``isinstance(mask, torch.Tensor)``); a parameter's proxy is also an nn.Parameter
+        # ``isinstance(mask, torch.Tensor)``); a parameter's proxy is also an nn.Parameter, and
+        # a DTensor's proxy a DTensor
+        from .proxies import DTensorProxy
+
         tags = getattr(obj, "tags", ())
         is_param = "parameter" in tags or "nn_parameter" in tags
+        is_dt = isinstance(obj, DTensorProxy)
         for c in _flat_classes(cls):
             if c is torch.Tensor or (c is torch.nn.Parameter and is_param):
+                return True
+            if is_dt and getattr(c, "__name__", "") == "DTensor" and (getattr(c, "__module__", "") or "").startswith(
+                    "torch.distributed.tensor"):
                 return True
     return isinstance(obj, cls)
 
@@ -801,13 +810,49 @@ class Interpreter:
                  or _tm._global_forward_hooks or _tm._global_forward_pre_hooks or _tm._global_backward_hooks
                  or getattr(_tm, "_global_backward_pre_hooks", None))
         if hooks:
-            return self._opaque(m, args, kwargs), None
+            if (m._backward_hooks or getattr(m, "_backward_pre_hooks", None) or _tm._global_backward_hooks
+                    or getattr(_tm, "_global_backward_pre_hooks", None)):
+                return self._opaque(m, args, kwargs), None
+            return self._call_module_with_forward_hooks(m, args, kwargs, fn_prov, arg_provs, kw_provs), None
+        return self._call_forward(m, args, kwargs, fn_prov, arg_provs, kw_provs)
+
+    def _call_forward(self, m, args, kwargs, fn_prov, arg_provs, kw_provs):
         mp = self.mprov(m, fn_prov)
         fwd = m.__dict__.get("forward")
         if fwd is not None:
             return self._call(fwd, args, kwargs, None, arg_provs, kw_provs)
         fwd = type(m).forward
         return self._call(fwd, (m,) + args, kwargs, None, [mp] + list(arg_provs or [None] * len(args)), kw_provs)
+
+    def _call_module_with_forward_hooks(self, m, args, kwargs, fn_prov, arg_provs, kw_provs):
+        """``Module._call_impl`` for forward (pre-)hooks, with the hooks *interpreted*: hook code
+        sees traced tensors as ``torch.Tensor`` (e.g. DTensor ``distribute_module`` input/output
+        functions converting plain tensors), and the hooks' effects are part of the program."""
+        from torch.nn.modules import module as _tm
+
+        pre = list(_tm._global_forward_pre_hooks.items()) + list(m._forward_pre_hooks.items())
+        pre_kw = getattr(m, "_forward_pre_hooks_with_kwargs", {})
+        for hid, hook in pre:
+            if hid in pre_kw:
+                res, _ = self._call(hook, (m, args, kwargs), {})
+                if res is not None:
+                    args, kwargs = res
+            else:
+                res, _ = self._call(hook, (m, args), {})
+                if res is not None:
+                    args = res if isinstance(res, tuple) else (res,)
+            arg_provs, kw_provs = None, None  # values may have been replaced by the hook
+        result, _ = self._call_forward(m, args, kwargs, fn_prov, arg_provs, kw_provs)
+        post = list(_tm._global_forward_hooks.items()) + list(m._forward_hooks.items())
+        post_kw = getattr(m, "_forward_hooks_with_kwargs", {})
+        for hid, hook in post:
+            if hid in post_kw:
+                res, _ = self._call(hook, (m, args, kwargs, result), {})
+            else:
+                res, _ = self._call(hook, (m, args, result), {})
+            if res is not None:
+                result = res
+        return result
 
     # ---------------------------------------------------------------------------------------
     def _bind(self, fn, args, kwargs):

@@ -155,7 +155,11 @@ def _torch_vjp_impl(fn, args, kwargs, cotangents):
     with torch.enable_grad():
         out = fn(*a, **k)
         outs, _ = tree_flatten(out)
-        pairs = [(o, c) for o, c in zip([o for o in outs if isinstance(o, torch.Tensor)], cotangents) if c is not None and o.requires_grad]
+        # expanded cotangents (e.g. from sum's backward: stride 0) are made dense — some
+        # backward kernels (grouped_mm) reject zero strides
+        pairs = [(o, c if c.is_contiguous() else c.contiguous())
+                 for o, c in zip([o for o in outs if isinstance(o, torch.Tensor)], cotangents)
+                 if c is not None and o.requires_grad]
         if not pairs:
             return tuple(None for _ in inputs)
         grads = torch.autograd.grad([p[0] for p in pairs], inputs, [p[1] for p in pairs], allow_unused=True)
