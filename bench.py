@@ -47,8 +47,9 @@ def parse_args():
                         "(one coalesced RCCL launch per ~400 MB block of Llama-2-7B)")
     p.add_argument("--executors", default=None, help="comma separated executor names (default: framework defaults)")
     p.add_argument("--fp8", action="store_true")
-    p.add_argument("--fp8-recipe", default="current", choices=["current", "delayed", "mxfp8"],
-                   help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling) or MXFP8 blocks")
+    p.add_argument("--fp8-recipe", default="current", choices=["current", "delayed", "mxfp8", "mxfp4"],
+                   help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling), MXFP8 blocks, "
+                        "or mxfp4 (MXFP4 forward GEMMs, MXFP8 backward)")
     p.add_argument("--hipgraph", action="store_true")
     p.add_argument("--checkpoint-activations", action="store_true",
                    help="recompute every transformer block in the backward (memory for longer sequences)")
@@ -259,7 +260,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if data_parallel else "strong",
             "vs_baseline": round(per_gpu / base, 4) if data_parallel else None,  # no published TP number
-            "dtype": (f"fp8 ({args.fp8_recipe} scaling) linears, bf16 elsewhere" if args.fp8 else "bf16"),
+            "dtype": (("mxfp4 forward / mxfp8 backward linears, bf16 elsewhere" if args.fp8_recipe == "mxfp4" else
+                       f"fp8 ({args.fp8_recipe} scaling) linears, bf16 elsewhere") if args.fp8 else "bf16"),
             "data": "synthetic token ids, random-init weights",
             "config": {
                 "model": args.model + ("" if args.n_layer is None else f"-{args.n_layer}L(debug)"),

@@ -222,6 +222,62 @@ def _mx_vjp(x, w, bias=None):
     return y, bwd
 
 
+def _mx4_quant_meta(t):
+    C = t.shape[-1]
+    R = 1
+    for d in t.shape[:-1]:
+        R *= d
+    u8 = torch.uint8
+    return (TensorProxy(like=t, shape=(R, C // 2), dtype=u8, requires_grad=False),
+            TensorProxy(like=t, shape=(R, C // 32), dtype=u8, requires_grad=False))
+
+
+def _mx4_quant_impl(t):
+    from ..ops.mxfp4 import quantize
+
+    return quantize(t)
+
+
+def _mx4_gemm_impl(qa, sa, qb, sb, bias, out_shape):
+    from ..ops.mxfp4 import gemm_nt
+
+    return gemm_nt(qa, sa, qb, sb, bias).reshape(out_shape)
+
+
+# MXFP4 recipe: packed e2m1 + E8M0/32 operands of the forward GEMM (csrc/fp8.hip mx4 cast,
+# csrc/gemm.hip gemm_nt_mxfp4_kernel)
+hip_mx4_quantize = ex.register_operator("hip_mx4_quantize", meta=_mx4_quant_meta, fn=_mx4_quant_impl)
+hip_mx4_gemm = ex.register_operator(
+    "hip_mx4_gemm", meta=lambda qa, sa, qb, sb, bias, out_shape: TensorProxy(like=qa, shape=tuple(out_shape),
+                                                                            dtype=torch.bfloat16),
+    fn=_mx4_gemm_impl)
+
+
+def _mx4_fwd(x, w, bias):
+    qx4, sx4 = hip_mx4_quantize(x)
+    qw4, sw4 = hip_mx4_quantize(w)
+    return hip_mx4_gemm(qx4, sx4, qw4, sw4, bias, tuple(x.shape[:-1]) + (w.shape[0],))
+
+
+def _mx4_vjp(x, w, bias=None):
+    """MXFP4 forward, MXFP8 backward: the backward reads e4m3 MX copies of x^T and w^T."""
+    from .. import torch as ltorch
+
+    y = _mx4_fwd(x, w, bias)
+    _, _, qxT, sxT = hip_mx_quantize(x, False)
+    _, _, qwT, swT = hip_mx_quantize(w, False)
+
+    def bwd(g):
+        qg, sg, qgT, sgT = hip_mx_quantize(g, True)
+        dx = hip_mx_gemm(qg, sg, qwT, swT, 1, 0, None, tuple(x.shape))
+        dw = hip_mx_gemm(qgT, sgT, qxT, sxT, 1, 0, None, tuple(w.shape))
+        if bias is None:
+            return dx, dw
+        return dx, dw, ltorch.sum(g, tuple(range(g.ndim - 1)))
+
+    return y, bwd
+
+
 def _quant(t, e5m2, key, slot):
     if key is None:
         return hip_fp8_quantize(t, e5m2)
@@ -233,6 +289,8 @@ def _fp8_vjp(x, w, bias=None, key=None, slots=None):
 
     if key == "mxfp8":
         return _mx_vjp(x, w, bias)
+    if key == "mxfp4":
+        return _mx4_vjp(x, w, bias)
     sl = slots or (None, None, None)
     qx, qxT, sx = _quant(x, False, key, sl[0])
     qw, qwT, sw = _quant(w, False, key, sl[1])
@@ -256,6 +314,8 @@ def _fp8_exec(x, w, bias=None, key=None, slots=None):
         qx, sx, _, _ = hip_mx_quantize(x, False)
         qw, sw, _, _ = hip_mx_quantize(w, False)
         return hip_mx_gemm(qx, sx, qw, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
+    if key == "mxfp4":
+        return _mx4_fwd(x, w, bias)
     sl = slots or (None, None, None)
     qx, _, sx = _quant(x, False, key, sl[0])
     qw, _, sw = _quant(w, False, key, sl[1])

@@ -234,6 +234,17 @@ class MXFP8BlockScaling:
         return "MXFP8BlockScaling()"
 
 
+class MXFP4BlockScaling:
+    """4-bit training recipe on CDNA4 (the MI355X counterpart of TE's ``NVFP4BlockScaling``,
+    reference ``transformer_engineex_impl.py``): the forward GEMM runs on OCP MXFP4 (e2m1
+    elements, E8M0 scale per 32 along K) on the block-scaled MFMA at 2x the fp8 rate; the
+    backward GEMMs (dgrad, wgrad) stay MXFP8 (e5m2 gradients, e4m3 saved operands), where
+    4-bit gradients would need stochastic rounding / Hadamard transforms to train stably."""
+
+    def __repr__(self):
+        return "MXFP4BlockScaling()"
+
+
 def mx_quantize(t: torch.Tensor, e5m2: bool = False):
     """t [..., C] -> (q [R, C], s [R, C/32], q^T [C, R], s^T [C, R/32]): fp8 as uint8, E8M0 scales as
     uint8; blocks along C for q, along R for q^T (each is the reduction dim of the GEMM reading it)."""

@@ -55,16 +55,20 @@ class FP8LinearTransform(Transform):
     or a :class:`~lightning_thunder_amd.ops.fp8.DelayedScaling` (amax history, scales from earlier
     steps, amax all-reduced over the data-parallel group; reference TE ``DelayedScaling``), or
     ``"mxfp8"`` / :class:`~lightning_thunder_amd.ops.fp8.MXFP8BlockScaling` (E8M0 scale per 32
-    elements of each GEMM's reduction dim, on the block-scaled MFMA; reference TE ``MXFP8BlockScaling``)."""
+    elements of each GEMM's reduction dim, on the block-scaled MFMA; reference TE ``MXFP8BlockScaling``),
+    or ``"mxfp4"`` / :class:`~lightning_thunder_amd.ops.fp8.MXFP4BlockScaling` (forward GEMM in
+    MXFP4, backward in MXFP8; the counterpart of TE ``NVFP4BlockScaling``)."""
 
     def __init__(self, recipe="current", amax_history_len: int = 16, skip: tuple[str, ...] = ()):
-        from ..ops.fp8 import DelayedScaling, MXFP8BlockScaling
+        from ..ops.fp8 import DelayedScaling, MXFP8BlockScaling, MXFP4BlockScaling
 
         if recipe == "delayed":
             recipe = DelayedScaling(amax_history_len=amax_history_len)
         elif recipe == "mxfp8":
             recipe = MXFP8BlockScaling()
-        if not (recipe == "current" or isinstance(recipe, (DelayedScaling, MXFP8BlockScaling))):
+        elif recipe == "mxfp4":
+            recipe = MXFP4BlockScaling()
+        if not (recipe == "current" or isinstance(recipe, (DelayedScaling, MXFP8BlockScaling, MXFP4BlockScaling))):
             raise ValueError(f"unknown FP8 recipe {recipe!r}")
         self.recipe = recipe
         self.amax_history_len = amax_history_len
@@ -78,11 +82,12 @@ class FP8LinearTransform(Transform):
         new = from_trace(computation_trace)
         new.bound_symbols = []
         new.scopes = [new.bound_symbols]
-        from ..ops.fp8 import MXFP8BlockScaling
+        from ..ops.fp8 import MXFP8BlockScaling, MXFP4BlockScaling
 
         swap: dict = {}
         n = 0
-        mx = isinstance(self.recipe, MXFP8BlockScaling)
+        mx = "mxfp8" if isinstance(self.recipe, MXFP8BlockScaling) else (
+            "mxfp4" if isinstance(self.recipe, MXFP4BlockScaling) else None)
         delayed = self.recipe != "current" and not mx
         slots: dict = {}  # ("x"|"w", proxy name) / ("dy", site) -> history slot; siblings reading one x share it
 
@@ -102,7 +107,7 @@ class FP8LinearTransform(Transform):
                             sites.append(len(new.bound_symbols))
                             y = fp8_linear(x, w, bias, -1, sl)  # key patched below (slot count known last)
                         elif mx:
-                            y = fp8_linear(x, w, bias, "mxfp8")
+                            y = fp8_linear(x, w, bias, mx)
                         else:
                             y = fp8_linear(x, w, bias)
                         swap[b.output.name] = y

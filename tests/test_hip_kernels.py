@@ -410,6 +410,42 @@ def test_fp8_mxfp8_training_close_to_bf16():
 
 
 @pytest.mark.gpu
+def test_mxfp4_training_recipe():
+    """MXFP4BlockScaling: forward GEMMs on the fp4 block-scaled MFMA, backward in MXFP8."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 1024), torch.nn.GELU(), torch.nn.Linear(1024, 512)).cuda().bfloat16()
+    t = FP8LinearTransform(recipe="mxfp4")
+    jm = thunder.jit(m, transforms=[t])
+    x = torch.randn(4, 64, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    out = jm(x)
+    fwd_src = str(thunder.last_traces(jm)[-1])
+    assert t.n_converted == 2 and "hip_mx4_gemm" in fwd_src
+    assert "hip_mx_gemm" in str(thunder.last_backward_traces(jm)[-1])
+    ref = m(x)
+    cos = torch.nn.functional.cosine_similarity(out.float().flatten(), ref.float().flatten(), dim=0).item()
+    rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
+    assert cos > 0.97 and rel < 0.25, (cos, rel)
+    # the forward matches the exact product of the MXFP4-dequantised operands (first linear)
+    from lightning_thunder_amd.ops import mxfp4
+
+    x2 = x.detach().reshape(-1, 512)
+    qx, sx = mxfp4.quantize(x2)
+    qw, sw = mxfp4.quantize(m[0].weight.detach())
+    exact = mxfp4.dequantize(qx, sx) @ mxfp4.dequantize(qw, sw).T + m[0].bias.float()
+    got = mxfp4.gemm_nt(qx, sx, qw, sw, m[0].bias.detach())
+    assert ((got.float() - exact).norm() / exact.norm()).item() < 1e-2
+    g = torch.randn_like(out)
+    gx, gw = torch.autograd.grad(out, (x, m[0].weight), g)
+    rx, rw = torch.autograd.grad(ref, (x, m[0].weight), g)
+    for a, b in ((gx, rx), (gw, rw)):
+        c = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+        assert c > 0.97, c
+
+
+@pytest.mark.gpu
 def test_fp8_delayed_scaling_training():
     """DelayedScaling recipe: scales come from the amax history of earlier steps (recorded while
     casting); results stay close to bf16 over several steps, siblings share the x slot, and the

@@ -274,3 +274,24 @@ def test_reference_module_paths():
     jf(torch.ones(4))
     peak, _ = get_alloc_memory(thunder.last_traces(jf)[-1])
     assert peak > 0
+
+
+def test_fp8_training_recipes_parse():
+    """Recipe names of ``FP8LinearTransform`` / the ``fp8`` plugin (TE DelayedScaling,
+    MXFP8BlockScaling, and MXFP4BlockScaling as the counterpart of NVFP4BlockScaling); CPU
+    programs keep their linears (the fp8 GEMMs need a gfx950 device)."""
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling, MXFP8BlockScaling, MXFP4BlockScaling
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    assert FP8LinearTransform("current").recipe == "current"
+    assert isinstance(FP8LinearTransform("delayed").recipe, DelayedScaling)
+    assert isinstance(FP8LinearTransform("mxfp8").recipe, MXFP8BlockScaling)
+    assert isinstance(FP8LinearTransform("mxfp4").recipe, MXFP4BlockScaling)
+    with pytest.raises(ValueError):
+        FP8LinearTransform("nvfp4")
+    m = torch.nn.Linear(256, 256)
+    t = FP8LinearTransform("mxfp4")
+    jm = thunder.jit(m, transforms=[t])
+    x = torch.randn(256, 256)
+    torch.testing.assert_close(jm(x), m(x))
+    assert t.n_converted == 0
