@@ -129,6 +129,10 @@ def python_lookasides() -> list:
     orig = DTensor.from_local
 
     def from_local(local_tensor, device_mesh=None, placements=None, *, run_check=False, shape=None, stride=None):
+        if isinstance(local_tensor, DTensorProxy):
+            # already a DTensor: native torch code (parallel styles) cannot see that through
+            # isinstance on the proxy and would wrap it again; torch skips from_local for DTensors
+            return local_tensor
         if not isinstance(local_tensor, TensorProxy):
             return orig(local_tensor, device_mesh, placements, run_check=run_check, shape=shape, stride=stride)
         if device_mesh is None:

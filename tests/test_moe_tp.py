@@ -103,6 +103,35 @@ def _worker(rank, world, port, d):
             res[f"{mode}_bwd"] = all(
                 torch.allclose(getattr(pm, n).weight.grad.full_tensor().float(), getattr(ref, n).weight.grad.float(),
                                atol=5e-2, rtol=5e-2) for n in ("gate_proj", "up_proj", "down_proj"))
+        # the full Llama-4 MoE block with the reference's plan (test_moe.py:parallelize_moe_model)
+        from torch.distributed.tensor import Shard
+        from torch.distributed.tensor.parallel import ColwiseParallel, RowwiseParallel
+        from lightning_thunder_amd.models.llama4_moe import Llama4MoE, MoEConfig
+
+        torch.manual_seed(0)
+        cfg = MoEConfig(hidden_size=32, intermediate_size=64, num_routed_experts=4)
+        m = Llama4MoE(cfg).bfloat16()
+        ref = Llama4MoE(cfg).bfloat16()
+        ref.load_state_dict(m.state_dict())
+        plan = {
+            "shared_experts.gate_proj": ColwiseParallel(use_local_output=False, output_layouts=Shard(2)),
+            "shared_experts.up_proj": ColwiseParallel(use_local_output=False, output_layouts=Shard(2)),
+            "shared_experts.down_proj": RowwiseParallel(),
+            "routed_experts.gate_proj": Col(),
+            "routed_experts.up_proj": Col(),
+            "routed_experts.down_proj": Row(),
+        }
+        pm = parallelize_module(m, mesh, plan)
+        x = torch.randn(1, 16, 32, dtype=torch.bfloat16)
+        out, want = thunder.jit(pm)(x), ref(x)
+        res["llama4_fwd"] = torch.allclose(out.float(), want.float(), atol=5e-2, rtol=5e-2)
+        out.float().pow(2).sum().backward()
+        want.float().pow(2).sum().backward()
+        names = ["routed_experts.gate_proj", "routed_experts.down_proj", "shared_experts.up_proj", "shared_experts.down_proj"]
+        gp, gr = dict(pm.named_parameters()), dict(ref.named_parameters())
+        res["llama4_bwd"] = all(
+            torch.allclose(gp[n + ".weight"].grad.full_tensor().float(), gr[n + ".weight"].grad.float(), atol=8e-2, rtol=8e-2)
+            for n in names)
         torch.save(res, os.path.join(d, f"r{rank}.pt"))
     finally:
         torch.distributed.destroy_process_group()
@@ -114,7 +143,7 @@ def test_moe_grouped_expert_tensor_parallel():
         mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
         for r in range(world):
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
-            assert set(res) == {"jit_fwd", "jit_bwd", "thunderfx_fwd", "thunderfx_bwd"}, res
+            assert set(res) == {"jit_fwd", "jit_bwd", "thunderfx_fwd", "thunderfx_bwd", "llama4_fwd", "llama4_bwd"}, res
             bad = {k: v for k, v in res.items() if v is not True}
             assert not bad, bad
 
