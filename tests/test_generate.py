@@ -62,3 +62,20 @@ def test_generate_gpu_bf16(graphs):
     # flip a later greedy token: the prompt and the first generated tokens must agree
     assert torch.equal(out[:, :12], ref[:, :12])
     assert torch.equal(out, out2)  # replays are deterministic
+
+
+@pytest.mark.gpu
+def test_inference_benchmark_prefill_decode(capsys):
+    """``benchmarks/inference.py`` (reference ``benchmark_inference.py``): TTFT / TBOT / throughput
+    per mode for a batched prefill + decode on a two-layer model."""
+    import json
+
+    from lightning_thunder_amd.benchmarks import inference
+
+    inference.main(["--model", "Llama-3.2-1B", "--n-layer", "2", "--batch-size", "2", "--input-length", "64",
+                    "--output-length", "8", "--num-iterations", "2", "--warmup-iterations", "1",
+                    "--modes", "eager,thunder,hipgraph"])
+    lines = [json.loads(ln) for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+    assert [r["mode"] for r in lines] == ["eager", "thunder", "hipgraph"]
+    for r in lines:
+        assert r["ttft_ms"]["mean"] > 0 and r["tbot_ms"]["mean"] > 0 and r["decode_tokens_per_s"] > 0
