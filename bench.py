@@ -51,6 +51,9 @@ def parse_args():
                    help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling), MXFP8 blocks, "
                         "or mxfp4 (MXFP4 forward GEMMs, MXFP8 backward)")
     p.add_argument("--hipgraph", action="store_true")
+    p.add_argument("--lora", type=int, default=0, metavar="R",
+                   help="LoRA fine-tuning of every transformer linear at rank R (base weights frozen; reference "
+                        "benchmark_peft.py); not the pretraining headline")
     p.add_argument("--checkpoint-activations", action="store_true",
                    help="recompute every transformer block in the backward (memory for longer sequences)")
     p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
@@ -129,6 +132,12 @@ def run(args, rank, world, device, mode):
                 logits = self.m(x)
                 return torch.nn.functional.cross_entropy(logits.reshape(-1, V), y.reshape(-1))
 
+        if args.lora:
+            from lightning_thunder_amd.transforms.qlora import LORATransform
+
+            model.requires_grad_(False)  # only the adapters train
+            transforms.insert(0, LORATransform(r=args.lora, lora_alpha=2 * args.lora,
+                                               weights=["attn", "proj", "fc_1", "fc_2"]))
         jm = thunder.jit(TrainStep(model), transforms=transforms, **kwargs)
         if (world > 1 or _force_dist()) and parallel == "fsdp":
             from lightning_thunder_amd.distributed import fsdp
@@ -146,7 +155,7 @@ def run(args, rank, world, device, mode):
             rows = [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.proj", "mlp.proj")]
             jm = row_parallel(column_parallel(jm, cols), rows)
         fwd = jm
-        params = list(jm.parameters())
+        params = [p for p in jm.parameters() if p.requires_grad]
     else:
         fwd = model
         if world > 1:
@@ -250,7 +259,7 @@ def main():
     base = BASELINE_TOKENS_PER_SEC_PER_GPU_1 if world == 1 else BASELINE_TOKENS_PER_SEC_PER_GPU_FSDP
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not args.lora else f"tokens/sec/GPU {args.model} LoRA r={args.lora} fine-tuning (LitGPT)",
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -259,7 +268,8 @@ def main():
             "ms_per_step": round(dt / args.steps * 1000, 3),
             "higher_is_better": True,
             "scaling": "weak" if data_parallel else "strong",
-            "vs_baseline": round(per_gpu / base, 4) if data_parallel else None,  # no published TP number
+            # no published TP or LoRA number to compare with
+            "vs_baseline": round(per_gpu / base, 4) if data_parallel and not args.lora else None,
             "dtype": (("mxfp4 forward / mxfp8 backward linears, bf16 elsewhere" if args.fp8_recipe == "mxfp4" else
                        f"fp8 ({args.fp8_recipe} scaling) linears, bf16 elsewhere") if args.fp8 else "bf16"),
             "data": "synthetic token ids, random-init weights",
@@ -269,7 +279,7 @@ def main():
                 "micro_batch": args.mbs,
                 "seq_len": args.seq,
                 "parallelism": f"{parallel}{world}" if world > 1 else "single",
-                "mode": args.mode,
+                "mode": args.mode + (f"+lora-r{args.lora}" if args.lora else ""),
                 "optimizer": "AdamW",
             },
             "tokens_per_sec_per_gpu": round(per_gpu, 2),
