@@ -1,0 +1,388 @@
+// K2 (v2): bf16 GEMM on CDNA4 MFMA, one 256x256 output tile per 4-wave workgroup.
+//
+//   C[M,N] = act(alpha * A . B + bias[col]) (+ R)        (reference: cuBLAS(Lt) behind ATen linear /
+//                                                          matmul, thunder/executors/torchex.py; nvFuser
+//                                                          linear/matmul, nvfuserex_impl.py:2437-2488)
+// A is [M][K] (K-major, AT = 0) or stored [K][M] (MN-major, AT = 1); B is [N][K] (the nn.Linear
+// weight, BT = 0) or stored [K][N] (BT = 1).  The three layouts of a training linear are
+//   forward  Y  = X  . W^T : AT 0, BT 0      dgrad dX = dY . W : AT 0, BT 1      wgrad dW = dY^T . X : AT 1, BT 1
+// so no operand is ever transposed in memory.
+//
+// Why this shape (cdna_hip_programming.md §5; MI355X_MICROARCH.md §LDS, §Two waves per SIMD):
+//   * 4 waves (one per SIMD), each owning a 128x128 quadrant = 8x8 v_mfma_f32_16x16x32_bf16 tiles
+//     (256 fp32 accumulators per lane).  Per 32-deep k-step a wave issues 64 MFMAs (1024 cycles) for
+//     16 fragment reads: half the LDS read bytes per FLOP of a 2x4-wave 128x64 split, and the
+//     16x16x32 shape holds a higher clock than 32x32x16 on random data (DVFS give-back item 7).
+//   * Operands are staged HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR round trip) into
+//     two 64 KiB stages (BK = 64).  K-major images are 128-B rows with the 16-B chunk c of row r at
+//     c ^ (r & 7) (conflict-free ds_read_b128); MN-major images are 512-B k-rows read with
+//     ds_read_b64_tr_b16 (T10) under the tr_swz XOR (conflict-free transposed reads).  glds writes
+//     lane-linearly, so both swizzles are applied to the per-lane SOURCE address (rule 21).
+//   * ONE barrier per 64-deep K-tile, placed in the middle of the second k-step's MFMA stream: the
+//     MFMAs before it use fragments already in registers, the ones after it hide the next tile's
+//     first fragment reads and the prefetch of the tile after that.  So the only exposed cost per
+//     K-tile is the barrier skew, not a read-after-barrier latency:
+//        phase A  (k-step 0): 64 MFMA  | ds_read k-step-1 fragments of tile t
+//        phase B1 (k-step 1): 32 MFMA  | -
+//        vmcnt(0) lgkmcnt(0) s_barrier          (tile t+1 landed everywhere; tile t fully read)
+//        phase B2 (k-step 1): 32 MFMA  | ds_read k-step-0 fragments of tile t+1, glds of tile t+2
+//     The glds of tile t+2 go into the buffer of tile t (free after that barrier) and must land by
+//     the next barrier, ~96 MFMAs (1500+ cycles) later.  VAR selects how the 16 glds per wave and
+//     tile are split between phase B2 and the first half of the next phase A.
+//   * Instruction order inside each phase is pinned with sched_barrier(0) after every MFMA group.
+//   * blockIdx -> tile: bijective XCD remap, then groups of 8 tile-rows (L2 reuse of A and B panels).
+//   * Epilogue: fp32 alpha / bias / activation in registers -> bf16 in a per-wave swizzled LDS image
+//     -> 16-B row-contiguous stores (+ residual, same rounding points as ATen's linear then add).
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
+constexpr int OP_BYTES = BM * BK * 2;  // 32 KiB per operand per stage
+constexpr int STAGE = 2 * OP_BYTES;    // 64 KiB
+
+enum Act : int { kNone = 0, kGeluTanh = 1, kGeluErf = 2, kSilu = 3, kRelu = 4 };
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+  if constexpr (ACT == kGeluTanh) {
+    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  } else if constexpr (ACT == kGeluErf) {
+    return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+  } else if constexpr (ACT == kSilu) {
+    return x / (1.f + __expf(-x));
+  } else if constexpr (ACT == kRelu) {
+    return x > 0.f ? x : 0.f;
+  } else {
+    return x;
+  }
+}
+
+__device__ __forceinline__ int xcd_tile(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// MN-major image swizzle: the 16-B chunk c of k-row k sits at chunk c ^ tr_swz(k).  A 32-lane half
+// of a transposed fragment read touches rows {k0+q, k0+4+q} (q < 4) at chunks {c0, c0+1}; tr_swz
+// maps those rows to distinct even chunk offsets of the 256-B bank row.
+__device__ __forceinline__ int tr_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+// Per-lane LDS-DMA source of one operand (buffer_load ... lds through a buffer resource, so the
+// per-lane part is ONE 32-bit VGPR offset and the per-instruction / per-K-tile parts are scalar
+// soffsets).  Instruction i (0..7) of wave w fills LDS bytes [(4i + w) KiB, +1 KiB) of the image.
+template <bool MN>
+struct Stager {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff0, voff1;      // K-major: voff0 for every i; MN-major: even / odd i
+  int istride, kstride;  // bytes between consecutive i / consecutive K-tiles
+  // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length
+  __device__ __forceinline__ void init(const __hip_bfloat16* X, int ld, int r0, int K, int wave, int lane) {
+    if constexpr (!MN) {
+      // 8 rows of 128 B per instruction: lane -> row 8(4i + w) + (lane >> 3), stored chunk lane & 7,
+      // which holds logical chunk (lane & 7) ^ row & 7
+      const __hip_bfloat16* base = X + (int64_t)r0 * ld;
+      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (BM - 1) * ld * 2 + K * 2, 0x00020000);
+      const int r = lane >> 3, c = (lane & 7) ^ r;
+      voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
+      voff1 = voff0;
+      istride = 32 * ld * 2;
+      kstride = BK * 2;
+    } else {
+      // 2 k-rows of 512 B per instruction: lane -> k-row 2(4i + w) + (lane >> 5), stored chunk
+      // lane & 31 holding logical chunk (lane & 31) ^ tr_swz(k-row); tr_swz flips bit 3 with i & 1
+      const __hip_bfloat16* base = X + r0;
+      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (K - 1) * ld * 2 + BM * 2, 0x00020000);
+      const int half = lane >> 5, slot = lane & 31;
+      const int kr = 2 * wave + half;  // k-row for i = 0
+      const int c0 = slot ^ tr_swz(kr);
+      voff0 = (kr * ld + c0 * 8) * 2;
+      voff1 = (kr * ld + (c0 ^ 8) * 8) * 2;
+      istride = 8 * ld * 2;
+      kstride = BK * ld * 2;
+    }
+  }
+  __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(img + (i * 4 + wave) * 1024), 16,
+                                             (MN && (i & 1)) ? voff1 : voff0, i * istride + kt * kstride, 0, 0);
+  }
+};
+
+// 8-element fragment (k = 32 kk + 8 fq .. +7 of row/column `rc + fr`) of a staged operand image.
+template <bool MN>
+__device__ __forceinline__ bf16x8 read_frag(const char* img, int rc, int kk, int fr, int fq) {
+  if constexpr (!MN) {
+    const int row = rc + fr;
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + (((kk * 4 + fq) ^ (fr & 7)) << 4));
+  } else {
+    // lane 4q+p of the 16-lane group addresses k-row k0 + q, columns rc + 4p .. +3
+    const int q = fr >> 2, p = fr & 3;
+    const int k = kk * 32 + fq * 8 + q;
+    const int c = (rc >> 3) + (p >> 1);
+    const char* a0 = img + k * 512 + ((c ^ tr_swz(k)) << 4) + 8 * (p & 1);
+    const char* a1 = img + (k + 4) * 512 + ((c ^ tr_swz(k + 4)) << 4) + 8 * (p & 1);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(__attribute__((address_space(3))) char*)a0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(__attribute__((address_space(3))) char*)a1);
+    union {
+      struct {
+        s16x4 a, b;
+      } s;
+      bf16x8 f;
+    } u;
+    u.s.a = lo;
+    u.s.b = hi;
+    return u.f;
+  }
+}
+
+#define LTA_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// The 256 accumulators live in the AGPR file through inline-asm MFMAs ("+a"): as intrinsics hipcc
+// splits them between the VGPR and AGPR files and spills.  Fragments come straight from ds_read
+// (waited by hipcc's lgkmcnt), so no VALU->MFMA operand hazard needs padding; the AGPR results are
+// read only after the explicit s_nop drain before the epilogue.
+__device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR>
+__global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat16* __restrict__ A,
+                                                            const __hip_bfloat16* __restrict__ B,
+                                                            __hip_bfloat16* __restrict__ C,
+                                                            const __hip_bfloat16* __restrict__ bias,
+                                                            const __hip_bfloat16* __restrict__ R, int M, int N, int K,
+                                                            int lda, int ldb, int ldc, int ldr, float alpha) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];  // the ONLY LDS object (rule 4a)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  Stager<AT> sa;
+  Stager<BT> sb;
+  sa.init(A, lda, m0, K, wave, lane);
+  sb.init(B, ldb, n0, K, wave, lane);
+  // glds j (0..15) of a K-tile: j < 8 -> A instruction j, else B instruction j - 8
+  auto glds = [&](int j, int kt, char* stage) {
+    if (j < 8)
+      sa.issue(j, kt, stage, wave);
+    else
+      sb.issue(j - 8, kt, stage + OP_BYTES, wave);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  // fragment read r (0..15) of one k-step, in the order the MFMAs consume them: A0, B0..B7, A1..A7
+  auto read_one = [&](const char* stage, int kk, int r, bf16x8* fa, bf16x8* fb) {
+    if (r == 0)
+      fa[0] = read_frag<AT>(stage, wm * 128, kk, fr, fq);
+    else if (r <= 8)
+      fb[r - 1] = read_frag<BT>(stage + OP_BYTES, wn * 128 + (r - 1) * 16, kk, fr, fq);
+    else
+      fa[r - 8] = read_frag<AT>(stage, wm * 128 + (r - 8) * 16, kk, fr, fq);
+  };
+
+  // glds split: NB2 instructions of tile t+2 in phase B2 of tile t, the rest (16 - NB2) in the first
+  // half of phase A of tile t+1
+  constexpr int NB2 = VAR == 0 ? 16 : (VAR == 1 ? 8 : 4);
+  constexpr int NA = 16 - NB2;
+
+  const int nk = K / BK;
+  // ---- prologue: tile 0 whole, tile 1's phase-B2 share; wait for tile 0 ----
+#pragma unroll
+  for (int j = 0; j < 16; ++j) glds(j, 0, smem);
+#pragma unroll
+  for (int j = 0; j < NB2; ++j) glds(j, 1, smem + STAGE);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB2) : "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) read_one(smem, 0, r, fa0, fb0);
+
+  // one K-tile; CUR = its stage buffer.  No branch inside the pinned instruction stream: past the
+  // last K-tile the prefetch re-stages tile nk-1 (an L2 hit into a buffer nobody reads again) and the
+  // next-tile fragment reads read a stale buffer whose values are never used.
+  auto body = [&](int t, auto cur_c) {
+    constexpr int CUR = decltype(cur_c)::value;
+    char* const bc = smem + CUR * STAGE;
+    char* const bn = smem + (CUR ^ 1) * STAGE;
+    const int t1 = min(t + 1, nk - 1), t2 = min(t + 2, nk - 1);
+    // phase A: k-step 0 of tile t from (fa0, fb0); read k-step 1; finish tile t+1's staging
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
+      if ((i & 3) == 0) read_one(bc, 1, i >> 2, fa1, fb1);
+      if (NA > 0 && (i & 3) == 2 && (i >> 2) < NA) glds(NB2 + (i >> 2), t1, bn);
+      LTA_FENCE();
+    }
+    // phase B1: rows 0..3 of k-step 1
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      LTA_FENCE();
+    }
+    // tile t+1 has landed for this wave and tile t is fully read by it; then for everyone
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    LTA_FENCE();
+    // phase B2: rows 4..7 of k-step 1; read k-step 0 of tile t+1; stage tile t+2 into this buffer
+#pragma unroll
+    for (int i = 32; i < 64; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      const int s = i - 32;
+      if ((s & 1) == 0)
+        read_one(bn, 0, s >> 1, fa0, fb0);
+      else if (NB2 == 16 || ((s & 3) == 1 && (s >> 2) < NB2))
+        glds(NB2 == 16 ? (s >> 1) : (s >> 2), t2, bc);
+      LTA_FENCE();
+    }
+  };
+  // nk is even (K % 128 == 0, checked by the host)
+  for (int t = 0; t < nk; t += 2) {
+    body(t, std::integral_constant<int, 0>{});
+    body(t + 1, std::integral_constant<int, 1>{});
+  }
+
+  // the last asm MFMAs' results must be complete before the epilogue reads the accumulators
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+
+  // ---- epilogue: every wave has passed the last barrier after its final LDS read, so the stage
+  // buffers are free: registers -> swizzled bf16 image (per wave 128 x 128, 256-B rows) -> stores
+  char* wbuf = smem + wave * (128 * 256);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int col = n * 16 + fr;
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 128 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        float v = acc[m][n][j] * alpha + bv;
+        v = act_fn<ACT>(v);
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4) + co) = __float2bfloat16(v);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one accumulator column block at a time: bounded VGPR use
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 4, ch = id & 15;
+    uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+    const int64_t grow = m0 + wm * 128 + row;
+    const int gcol = n0 + wn * 128 + ch * 8;
+    if constexpr (RES) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
+      v = o.u;
+    }
+    *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = v;
+  }
+}
+
+#undef LTA_FENCE
+
+template <int ACT, bool AT, bool BT, int VAR>
+int launch4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
+            int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_G4(BI, RE)                                                                                            \
+  hipLaunchKernelGGL((gemm4_bf16_kernel<ACT, BI, RE, AT, BT, VAR>), grid, block, 0, s, (const __hip_bfloat16*)A,  \
+                     (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                  \
+                     (const __hip_bfloat16*)R, M, N, K, lda, ldb, ldc, ldr, alpha)
+  if (bias && R) { LTA_G4(true, true); }
+  else if (bias) { LTA_G4(true, false); }
+  else if (R) { LTA_G4(false, true); }
+  else { LTA_G4(false, false); }
+#undef LTA_G4
+  return (int)hipGetLastError();
+}
+
+template <int VAR>
+int dispatch_layout(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                    int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt, hipStream_t s) {
+  if (!at && !bt) {
+    switch (act) {
+      case kNone: return launch4<kNone, false, false, VAR>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+      case kGeluTanh: return launch4<kGeluTanh, false, false, VAR>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+      case kGeluErf: return launch4<kGeluErf, false, false, VAR>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+      case kSilu: return launch4<kSilu, false, false, VAR>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+      case kRelu: return launch4<kRelu, false, false, VAR>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+      default: return -1;
+    }
+  }
+  if (act != kNone || bias) return -1;  // backward layouts carry no epilogue but the residual
+  if (!at && bt) return launch4<kNone, false, true, VAR>(A, B, C, nullptr, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+  if (at && !bt) return launch4<kNone, true, false, VAR>(A, B, C, nullptr, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+  return launch4<kNone, true, true, VAR>(A, B, C, nullptr, R, M, N, K, lda, ldb, ldc, ldr, alpha, s);
+}
+
+}  // namespace
+
+// C[M,N] = act(alpha * opA . opB + bias) (+ R), bf16 in / fp32 accumulate / bf16 out.
+//   at = 0: A [M][K] (lda = row pitch)        at = 1: A stored [K][M] (lda = its row pitch)
+//   bt = 0: B [N][K] (nn.Linear weight)       bt = 1: B stored [K][N]
+// act/bias only with at = bt = 0.  Requires M, N % 256 == 0, K % 128 == 0, 16-B aligned rows and
+// operands under 2 GiB (32-bit buffer offsets).
+// variant: glds split (0: all in the barrier phase, 1: half, 2: a quarter; see the header).
+LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                              int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
+                              int variant, hipStream_t s) {
+  if (M % BM || N % BN || K % (2 * BK) || M <= 0 || N <= 0 || K <= 0) return -2;
+  // buffer-resource byte offsets are 32-bit
+  const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
+  if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
+  if (variant == 0) return dispatch_layout<0>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, s);
+  // the other glds splits exist for A/B measurement: plain products only
+  if (act != kNone || bias || R) return -1;
+#define LTA_G4V(V)                                                                                              \
+  if (!at && !bt) return launch4<kNone, false, false, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s); \
+  if (!at && bt) return launch4<kNone, false, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
+  if (at && !bt) return launch4<kNone, true, false, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
+  return launch4<kNone, true, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);
+  if (variant == 1) { LTA_G4V(1) }
+  if (variant == 2) { LTA_G4V(2) }
+#undef LTA_G4V
+  return -1;
+}

@@ -63,6 +63,60 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
 
 
 # ---------------------------------------------------------------------------------------------
+# K2 v2: the 4-wave 256x256 kernel (csrc/gemm4.hip), every training layout through one entry
+# ---------------------------------------------------------------------------------------------
+register_signature("lta_gemm4_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p])
+
+
+def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
+    """(at, bt, lda, ldb) of ``a [M,K] @ b [K,N]`` for ``lta_gemm4_bf16``, or None when the operands
+    are not bf16 2-D GPU tensors with one unit-stride dim, 16-B aligned rows and tile-divisible
+    shapes (M, N % 256, K % 128)."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda or a.dim() != 2 or b.dim() != 2:
+        return None
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K or M % 256 or N % 256 or K % 128 or M == 0 or N == 0 or K == 0:
+        return None
+    la, lb = _operand_layout(a, M, K), _operand_layout(b, K, N)
+    if la is None or lb is None:
+        return None
+    at = 0 if la[0] == 1 else 1
+    bt = 1 if lb[0] == 1 else 0
+    # 32-bit buffer offsets
+    if (K if at else M) * la[1] * 2 >= 2 ** 31 or (K if bt else N) * lb[1] * 2 >= 2 ** 31:
+        return None
+    return at, bt, la[1], lb[1]
+
+
+def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=None, alpha: float = 1.0,
+            out: torch.Tensor | None = None, variant: int = 0) -> torch.Tensor:
+    """``act(alpha * a @ b + bias) + residual`` on the 4-wave MFMA kernel.  ``a``/``b`` may be
+    transposed views (the backward GEMMs read dY^T / W / X in place); bias and act only for the
+    forward layout (a row-major, b = W^T)."""
+    lay = gemm4_layout(a, b)
+    if lay is None:
+        raise ValueError(f"matmul4: unsupported operands {tuple(a.shape)}{a.stride()} @ {tuple(b.shape)}{b.stride()}")
+    at, bt, lda, ldb = lay
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if residual is not None:
+        assert residual.shape == (M, N) and residual.stride(1) == 1 and residual.dtype == torch.bfloat16
+    if bias is not None:
+        assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
+    rc = require().lta_gemm4_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                  None if bias is None else bias.data_ptr(),
+                                  None if residual is None else residual.data_ptr(), M, N, K, lda, ldb, out.stride(0),
+                                  0 if residual is None else residual.stride(0), alpha, ACT[act], at, bt, variant,
+                                  stream_ptr(a.device))
+    check(rc, "lta_gemm4_bf16")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
 # linear with per-shape kernel selection
 # ---------------------------------------------------------------------------------------------
 import os as _os

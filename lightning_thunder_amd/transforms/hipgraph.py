@@ -103,7 +103,7 @@ class HipGraphRunner:
         self.entries: dict = {}
         self._warm: set = set()
         self._bound_storage: dict = {}  # signature -> storage key the zero-copy graph is bound to
-        self._written_back: dict = {}  # signature -> ((ptr, version) of each bound arg after the last write-back)
+        self._written_back: dict = {}  # signature -> ((ptr, version, epoch) of each bound arg after its write-back)
         self._lock = threading.Lock()
         self.replays = 0
         self.captures = 0
@@ -140,19 +140,34 @@ class HipGraphRunner:
             if isinstance(a, torch.Tensor) and i not in skip and a.data_ptr() != s.data_ptr():
                 s.copy_(a)
         graph.replay()
-        if private:
+        if self._bound:
             dst = [args[i] for i in self._bound]
-            torch._foreach_copy_(dst, [ins[i] for i in self._bound])
-            self._written_back[sig] = tuple((t.data_ptr(), t._version) for t in dst)
+            if private:
+                torch._foreach_copy_(dst, [ins[i] for i in self._bound])
+            # graph replays write caller storage without bumping tensor versions: every write to a
+            # bound storage (by this runner or any other runner of the transform) advances its epoch,
+            # which invalidates any other signature's "already written back" record for it
+            epochs = self.owner._bump_epochs([t.data_ptr() for t in dst])
+            if private and not any(t.is_inference() for t in dst):
+                self._written_back[sig] = tuple((t.data_ptr(), t._version, ep) for t, ep in zip(dst, epochs))
+            else:
+                self._written_back.pop(sig, None)
         self.replays += 1
         if self.copy_outputs:
             return tuple(o.clone() if isinstance(o, torch.Tensor) else o for o in outs)
         return outs
 
     def _copy_in_bound(self, sig, ins, args):
-        cur = tuple((args[i].data_ptr(), args[i]._version) for i in self._bound)
-        if self._written_back.get(sig) != cur:  # other storage, or the caller changed it since
-            torch._foreach_copy_([ins[i] for i in self._bound], [args[i] for i in self._bound])
+        """Copy the caller's tensors into the private graph's static buffers unless they are exactly
+        what this signature's last replay wrote back (same storage, tensor version and write epoch).
+        Inference-mode tensors carry no version counter: always copied."""
+        src = [args[i] for i in self._bound]
+        rec = self._written_back.get(sig)
+        if rec is not None and not any(t.is_inference() for t in src):
+            cur = tuple((t.data_ptr(), t._version, self.owner._epoch(t.data_ptr())) for t in src)
+            if cur == rec:
+                return
+        torch._foreach_copy_([ins[i] for i in self._bound], src)
 
     def _capture(self, key, args, private: bool):
         clone = set(self._clone) | (set(self._bound) if private else set())
@@ -189,6 +204,7 @@ class HipGraphTransform(Transform):
         self.min_region_size = min_region_size
         self.is_capturable = is_capturable
         self._pool = None
+        self._epochs: dict = {}  # data_ptr -> number of graph replays that wrote that caller storage
         self.runners: list[HipGraphRunner] = []
         self._count = 0
 
@@ -196,6 +212,17 @@ class HipGraphTransform(Transform):
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         return self._pool
+
+    def _bump_epochs(self, ptrs) -> list:
+        out = []
+        for p in ptrs:
+            e = self._epochs.get(p, 0) + 1
+            self._epochs[p] = e
+            out.append(e)
+        return out
+
+    def _epoch(self, ptr) -> int:
+        return self._epochs.get(ptr, 0)
 
     def _capturable(self, b) -> bool:
         if self.is_capturable is not None:

@@ -188,3 +188,80 @@ def test_capture_with_tuned_gemm_table_active():
     env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.abspath(__file__))) + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
+
+
+class _FakeGraph:
+    """CPU stand-in for a captured graph: replay re-runs the region on the captured inputs and writes
+    the results into the captured outputs (the semantics of a hipGraph replay)."""
+
+    def __init__(self, fn, ins, outs):
+        self.fn, self.ins, self.outs = fn, ins, outs
+
+    def replay(self):
+        # .data aliases the storage with its own version counter: like a real replay, no version bump
+        new = self.fn(*[a.data if isinstance(a, torch.Tensor) else a for a in self.ins])
+        new = new if isinstance(new, tuple) else (new,)
+        for o, n in zip(self.outs, new):
+            o.copy_(n)
+
+
+class _CpuRunner(HipGraphRunner):
+    """HipGraphRunner whose capture builds a _FakeGraph (capture itself runs nothing on the inputs)."""
+
+    def _capture(self, key, args, private):
+        clone = set(self._clone) | (set(self._bound) if private else set())
+        ins = tuple(a.clone() if i in clone and isinstance(a, torch.Tensor) else a for i, a in enumerate(args))
+        outs = self.fn(*[a.clone() if isinstance(a, torch.Tensor) else a for a in ins])
+        outs = tuple(outs) if isinstance(outs, (tuple, list)) else (outs,)
+        e = (ins, _FakeGraph(self.fn, ins, outs), outs)
+        self.entries[key] = e
+        self.captures += 1
+        return e
+
+
+def _write_rows(cache, x, pos):
+    cache.index_copy_(0, pos, x)
+    return cache.sum(0)
+
+
+def _runner(owner):
+    # inputs: cache (written in place), x and pos (caller-owned, read-only)
+    return _CpuRunner(_write_rows, "HipGraphT", owner, private_inputs=(True, True, True),
+                      mutated_inputs=(True, False, False))
+
+
+def test_runner_epoch_invalidates_stale_writeback_cpu():
+    """A bound replay of one signature writes cache B in-graph (no version bump); another signature's
+    private graph must then copy B in again instead of trusting its last write-back."""
+    owner = HipGraphTransform()
+    r = _runner(owner)
+    D = 4
+    A, B = torch.zeros(8, D), torch.zeros(8, D)
+    ref_B = torch.zeros(8, D)
+    dec = lambda c, v, p: r(c, torch.full((1, D), float(v)), torch.tensor([p]))
+    pre = lambda c, v: r(c, torch.full((4, D), float(v)), torch.arange(4))
+    for v in range(3):  # decode signature: warm-up, then bound to A
+        dec(A, v, 7)
+    for v in range(2):  # prefill signature first seen with B: warm-up, then a graph bound to B
+        pre(B, 10 + v)
+    dec(B, 5, 6)  # decode on B: private graph, write-back recorded
+    pre(B, 20)  # bound replay writes B's rows 0..3 in-graph: no version bump
+    dec(B, 6, 5)  # private decode on B again: must copy B in, or it writes stale rows 0..3 back
+    ref_B[:4] = 20
+    ref_B[6] = 5
+    ref_B[5] = 6
+    torch.testing.assert_close(B, ref_B)
+    assert r.replays >= 5
+
+
+def test_runner_inference_mode_cpu():
+    """Inference tensors carry no version counter: a private replay must copy them in."""
+    owner = HipGraphTransform()
+    r = _runner(owner)
+    D = 4
+    with torch.inference_mode():
+        for gen in range(2):  # two "generate" calls, each with a fresh cache
+            A = torch.zeros(8, D)
+            for step in range(4):
+                r(A, torch.full((1, D), float(gen * 10 + step)), torch.tensor([step]))
+            torch.testing.assert_close(A[:4, 0], torch.tensor([gen * 10 + s for s in range(4)], dtype=A.dtype))
