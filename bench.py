@@ -150,8 +150,11 @@ def run(args, rank, world, device, mode):
         elif (world > 1 or _force_dist()) and parallel == "tp":
             from lightning_thunder_amd.distributed import column_parallel, row_parallel
 
+            # Megatron layout: head-parallel attention (qkv by heads, proj by rows), column fc_1/fc_2 +
+            # row proj MLP, vocab-parallel embedding and lm_head with a vocab-parallel cross-entropy
             n = cfg.n_layer
             cols = [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.attn", "mlp.fc_1", "mlp.fc_2")]
+            cols += ["m.lm_head"] + ([] if cfg.tie_embeddings else ["m.transformer.wte"])
             rows = [f"m.transformer.h.{i}.{s}" for i in range(n) for s in ("attn.proj", "mlp.proj")]
             jm = row_parallel(column_parallel(jm, cols), rows)
         fwd = jm

@@ -405,6 +405,11 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
                             # FSDP transform re-types the input as the local shard + all-gather.
                             p._shape = tuple(full_shape)
                             p.tags.add("sharded")
+                        tp_kind = getattr(param, "_lc_tp_kind", None)
+                        if tp_kind in ("head_qkv", "head_proj"):
+                            # head-parallel attention weight: traced with its LOCAL shape (the
+                            # attention module's config was localized to this rank's heads)
+                            p.tags.add("tp_" + tp_kind)
                         p.tags.add(ProxyTag.STATIC_MEMORY_LOCATION)
                         p.tags.add("parameter")
                         seen[id(param)] = p

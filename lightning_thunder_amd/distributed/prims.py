@@ -253,6 +253,30 @@ def _tp_in_meta(a, group, layer_type):
 synchronize_tensor_parallel_input = _make("synchronize_tensor_parallel_input", _tp_in_meta)
 
 
+# ---- vocab-parallel cross-entropy (tensor-parallel lm_head: logits stay sharded by vocabulary) ----
+# reference: Megatron-style vocab-parallel loss; the reference thunder gathers the full logits instead
+# (column_wise.py post-process).  Forward: 2 tiny all-reduces per row (max, sum-exp) + 1 (target
+# logit); backward: purely local (softmax_local - onehot_local), no communication.
+def _vp_ce_fwd_meta(logits, target, group, vocab_start, ignore_index=-100):
+    from ..core import dtypes
+
+    n = logits.shape[0]
+    acc = dtypes.float64 if logits.dtype == dtypes.float64 else dtypes.float32
+    rows = TensorProxy(like=logits, shape=(n,), dtype=acc)
+    lse = TensorProxy(like=logits, shape=(n,), dtype=acc)
+    return rows, lse
+
+
+vocab_parallel_cross_entropy_fwd = _make("vocab_parallel_cross_entropy_fwd", _vp_ce_fwd_meta)
+
+
+def _vp_ce_bwd_meta(g_rows, logits, target, lse, vocab_start, ignore_index=-100):
+    return TensorProxy(like=logits)
+
+
+vocab_parallel_cross_entropy_bwd = _make("vocab_parallel_cross_entropy_bwd", _vp_ce_bwd_meta)
+
+
 # =========================================================================================
 # Runtime (torch executor) implementations: RCCL via torch.distributed
 # =========================================================================================
@@ -469,6 +493,36 @@ def _tp_in_impl(a, group, layer_type):
     return a
 
 
+def _vp_ce_fwd_impl(logits, target, group, vocab_start, ignore_index=-100):
+    x = logits if logits.dtype == torch.float64 else logits.float()
+    V = x.shape[-1]
+    m = x.amax(-1)
+    tdist.all_reduce(m, tdist.ReduceOp.MAX, group=group)
+    s = (x - m[:, None]).exp().sum(-1)
+    t = target.long() - vocab_start
+    inr = (t >= 0) & (t < V)
+    tl = torch.where(inr, x.gather(1, t.clamp(0, V - 1)[:, None]).squeeze(1), torch.zeros((), device=x.device))
+    # one all-reduce for the sum-exp and the target logit
+    st = torch.stack((s, tl))
+    tdist.all_reduce(st, tdist.ReduceOp.SUM, group=group)
+    lse = m + st[0].log()
+    valid = target != ignore_index
+    rows = torch.where(valid, lse - st[1], torch.zeros((), device=x.device))
+    return rows, lse
+
+
+def _vp_ce_bwd_impl(g_rows, logits, target, lse, vocab_start, ignore_index=-100):
+    x = logits if logits.dtype == torch.float64 else logits.float()
+    V = x.shape[-1]
+    p = (x - lse[:, None]).exp()
+    t = target.long() - vocab_start
+    inr = (t >= 0) & (t < V) & (target != ignore_index)
+    rows = torch.nonzero(inr).squeeze(1)
+    p[rows, t[rows]] -= 1.0
+    scale = torch.where(target != ignore_index, g_rows.to(x.dtype), torch.zeros((), device=x.device, dtype=x.dtype))
+    return (p * scale[:, None]).to(logits.dtype)
+
+
 def _register_torch_impls():
     from ..executors import torchex
 
@@ -479,7 +533,8 @@ def _register_torch_impls():
         (broadcast, _broadcast_impl), (wait, _wait_impl), (synchronize, _synchronize_impl), (pack, _pack_impl),
         (unpack, _unpack_impl), (pack_for_fsdp, _pack_for_fsdp_impl), (unpack_for_fsdp, _unpack_for_fsdp_impl),
         (synchronize_tensor_parallel_output, _tp_out_impl), (synchronize_tensor_parallel_input, _tp_in_impl),
-        (stash_grad_for_fsdp, _stash_grad_impl),
+        (stash_grad_for_fsdp, _stash_grad_impl), (vocab_parallel_cross_entropy_fwd, _vp_ce_fwd_impl),
+        (vocab_parallel_cross_entropy_bwd, _vp_ce_bwd_impl),
     ):
         op = torchex.ex.register_operator(f"dist_{sym.name}", like=sym, fn=fn)
         torchex.ex.register_implementation(sym, op)
@@ -553,6 +608,16 @@ def _register_vjps():
             return (g,)
 
         return out, bwd
+
+
+    @register_vjp(vocab_parallel_cross_entropy_fwd)
+    def _vp_ce_vjp(logits, target, group, vocab_start, ignore_index=-100):
+        rows, lse = vocab_parallel_cross_entropy_fwd(logits, target, group, vocab_start, ignore_index)
+
+        def bwd(g_rows, g_lse=None):
+            return (vocab_parallel_cross_entropy_bwd(g_rows, logits, target, lse, vocab_start, ignore_index), None)
+
+        return (rows, lse), bwd
 
 
 _register_vjps()

@@ -16,6 +16,16 @@ Design (MI355X, RCCL over xGMI):
     row embed     : y = all_gather_lastdim(embedding(idx, W_r))
   The rewrite happens before autodiff, so the backward's collectives come from the VJPs of the
   TP sync prims (``distributed/prims.py``).
+* Head-parallel attention (LitGPT convention: a module ``P`` with ``P.attn`` column-parallel, ``P.proj``
+  row-parallel and a ``P.config`` carrying ``n_head`` / ``n_query_groups`` / ``head_size``): the fused
+  qkv weight is sharded by *heads* (rank r keeps its n_head/W query heads and n_query_groups/W kv
+  groups), ``P.config`` is localized to those counts, and both weights are traced with their local
+  shapes.  The rank then runs qkv-split, RoPE and SDPA on its own heads and the row-parallel proj
+  all-reduces once: no all-gather inside the block (Megatron attention).  The reference gathers the
+  column output and runs attention on all heads on every rank (``column_wise.py:35-254``).
+* A column-parallel (vocab-sharded) ``lm_head`` whose gathered logits only feed ``cross_entropy`` is
+  rewritten to a vocab-parallel cross-entropy on the local logits (two small all-reduces per row in
+  the forward, a purely local backward), so the [tokens, vocab] logits are never gathered.
 * ``remove_redundant_comms`` then deletes all_gather -> slice pairs between a column-parallel and
   a row-parallel linear, *including through elementwise chains* (e.g. ``silu(fc_1) * fc_2`` between
   ``fc_1``/``fc_2`` column-parallel and ``proj`` row-parallel: the chain is recomputed on the
@@ -36,7 +46,8 @@ from ...core.transform_common import Transform, dce
 from .. import prims as dist_prims
 from ..prims import TPLayerType
 
-__all__ = ["column_parallel", "row_parallel", "TensorParallelTransform", "remove_redundant_comms", "TPLayerType"]
+__all__ = ["column_parallel", "row_parallel", "TensorParallelTransform", "remove_redundant_comms", "vocab_parallel_loss",
+           "TPLayerType"]
 
 COLUMN, ROW = "column", "row"
 
@@ -44,10 +55,14 @@ COLUMN, ROW = "column", "row"
 class TensorParallelTransform(Transform):
     """Shards ``target_modules`` (name -> 'column' | 'row') over ``process_group``."""
 
-    def __init__(self, target_modules: dict[str, str], process_group=None, optimize_comms: bool = True):
+    def __init__(self, target_modules: dict[str, str], process_group=None, optimize_comms: bool = True,
+                 head_parallel: bool = True, vocab_parallel_loss: bool = True):
         self.targets = dict(target_modules)
         self.process_group = process_group
         self.optimize_comms = optimize_comms
+        self.head_parallel = head_parallel
+        self.vocab_parallel_loss = vocab_parallel_loss
+        self.head_info: dict[str, tuple] = {}  # "attn.attn.weight" -> (n_head, n_query_groups, head_size)
         self.param_kinds: dict[str, tuple[str, type]] = {}  # "mod.weight" -> (kind, module type)
         self.original_shapes: dict[str, torch.Size] = {}
 
@@ -61,13 +76,90 @@ class TensorParallelTransform(Transform):
             self.targets[k] = v
 
     # --- module ------------------------------------------------------------------------------
+    def _head_groups(self, mods) -> list:
+        """(parent, qkv name, proj name) of attention modules that can run head-parallel."""
+        out = []
+        for name, kind in self.targets.items():
+            if kind != COLUMN or not name.endswith(".attn") and name != "attn":
+                continue
+            parent = name[: -len(".attn")] if name.endswith(".attn") else ""
+            proj = f"{parent}.proj" if parent else "proj"
+            pm = mods.get(parent)
+            cfg = getattr(pm, "config", None)
+            if self.targets.get(proj) != ROW or cfg is None:
+                continue
+            if not all(hasattr(cfg, a) for a in ("n_head", "n_query_groups", "head_size")):
+                continue
+            if not isinstance(mods.get(name), torch.nn.Linear) or not isinstance(mods.get(proj), torch.nn.Linear):
+                continue
+            out.append((parent, name, proj))
+        return out
+
+    @staticmethod
+    def _qkv_rows(nh, ng, hs, world, rank):
+        """Row indices of rank ``rank``'s heads in a fused [q | k | v] weight (litgpt layout)."""
+        nhl, ngl = nh // world, ng // world
+        q = torch.arange(rank * nhl * hs, (rank + 1) * nhl * hs)
+        k = nh * hs + torch.arange(rank * ngl * hs, (rank + 1) * ngl * hs)
+        v = (nh + ng) * hs + torch.arange(rank * ngl * hs, (rank + 1) * ngl * hs)
+        return torch.cat((q, k, v))
+
     def transform_module(self, model) -> None:
+        from dataclasses import replace
+
         group = self._group()
         rank, world = tdist.get_rank(group), tdist.get_world_size(group)
         inner = model._model
         mods = dict(inner.named_modules())
+        head_done = set()
         with torch.no_grad():
+            if self.head_parallel:
+                for parent, qkv_name, proj_name in self._head_groups(mods):
+                    pm, qm, prm = mods[parent], mods[qkv_name], mods[proj_name]
+                    qkind = getattr(qm.weight, "_lc_tp_kind", None)
+                    if qkind == "head_qkv" or getattr(prm.weight, "_lc_tp_kind", None) is not None:
+                        head_done.update((qkv_name, proj_name))
+                        continue
+                    cfg = pm.config
+                    nh, ng, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
+                    full_rows = getattr(qm.weight, "_lc_full_shape", tuple(qm.weight.shape))[0]
+                    if nh % world or ng % world or full_rows != (nh + 2 * ng) * hs:
+                        continue  # not shardable by heads: plain column/row handling below
+                    rows = self._qkv_rows(nh, ng, hs, world, rank).to(qm.weight.device)
+                    self.head_info[f"{qkv_name}.weight"] = (nh, ng, hs)
+                    for pname in ("weight", "bias"):
+                        t = getattr(qm, pname, None)
+                        if t is None:
+                            continue
+                        if getattr(t, "_lc_tp_kind", None) in (COLUMN, "column_bias"):
+                            # column_parallel() ran before row_parallel() named the proj: re-assemble
+                            # the plain dim-0 shards (a collective every rank makes) and re-shard by heads
+                            parts = [torch.empty_like(t) for _ in range(world)]
+                            tdist.all_gather(parts, t.detach().contiguous(), group=group)
+                            t_full = torch.cat(parts, 0)
+                        else:
+                            t_full = t
+                        newp = torch.nn.Parameter(t_full.detach().index_select(0, rows).clone(), requires_grad=t.requires_grad)
+                        newp._lc_tp_kind = "head_qkv"
+                        newp.distparallel_type = DistParallelType.COLUMN_WISE
+                        self.original_shapes[f"{qkv_name}.{pname}"] = t_full.shape
+                        self.param_kinds[f"{qkv_name}.{pname}"] = ("head_qkv", type(qm))
+                        self.head_info[f"{qkv_name}.{pname}"] = (nh, ng, hs)
+                        qm._parameters[pname] = newp
+                    w = prm.weight
+                    n = w.shape[1] // world
+                    newp = torch.nn.Parameter(w.detach().narrow(1, rank * n, n).clone(), requires_grad=w.requires_grad)
+                    newp._lc_tp_kind = "head_proj"
+                    newp.distparallel_type = DistParallelType.ROW_WISE
+                    self.original_shapes[f"{proj_name}.weight"] = w.shape
+                    self.param_kinds[f"{proj_name}.weight"] = (ROW, type(prm))
+                    prm._parameters["weight"] = newp
+                    # the attention code now sees this rank's heads only
+                    pm.config = replace(cfg, n_head=nh // world, n_query_groups=ng // world)
+                    head_done.update((qkv_name, proj_name))
             for name, kind in self.targets.items():
+                if name in head_done:
+                    continue
                 m = mods.get(name)
                 if m is None:
                     raise ValueError(f"{name} is not a submodule of the model")
@@ -112,6 +204,11 @@ class TensorParallelTransform(Transform):
             if not isinstance(a, TensorProxy) or a.distparallel_type not in (DistParallelType.COLUMN_WISE,
                                                                                DistParallelType.ROW_WISE):
                 continue
+            if "tp_head_qkv" in a.tags or "tp_head_proj" in a.tags:
+                # traced with the local shape already (head-parallel attention)
+                kinds[a.name] = "head_qkv" if "tp_head_qkv" in a.tags else "head_proj"
+                local[a.name] = a
+                continue
             if "sharded" not in a.tags:
                 continue
             shape = list(a.shape)
@@ -145,7 +242,20 @@ class TensorParallelTransform(Transform):
                     bias = nb.args[2] if name == "linear" and len(nb.args) > 2 else nb.kwargs.get("bias")
                     if bias is not None and bias.name in local:
                         bias = local[bias.name]
-                    if name == "linear" and kind == COLUMN:
+                    if name == "linear" and kind == "head_qkv":
+                        # this rank's heads: the local qkv feeds the local attention, no gather
+                        x2 = col_inputs.get(x.name)
+                        if x2 is None:
+                            x2 = dist_prims.synchronize_tensor_parallel_input(x, group, TPLayerType.COLUMN_LINEAR)
+                            col_inputs[x.name] = x2
+                        y = ltorch.linear(x2, wl, bias)
+                    elif name == "linear" and kind == "head_proj":
+                        # input already holds this rank's heads: no slice, one all-reduce
+                        y = ltorch.linear(x, wl, None)
+                        y = dist_prims.synchronize_tensor_parallel_output(y, group, TPLayerType.ROW_LINEAR)
+                        if bias is not None:
+                            y = ltorch.add(y, bias)
+                    elif name == "linear" and kind == COLUMN:
                         x2 = col_inputs.get(x.name)
                         if x2 is None:
                             x2 = dist_prims.synchronize_tensor_parallel_input(x, group, TPLayerType.COLUMN_LINEAR)
@@ -179,6 +289,8 @@ class TensorParallelTransform(Transform):
                 new.bound_symbols.append(b.swap_proxies(swap))
         if self.optimize_comms:
             new = remove_redundant_comms(new)
+        if self.vocab_parallel_loss:
+            new = vocab_parallel_loss(new, group)
         new.set_provenance(TraceProvenance("Tensor parallel (column/row-wise)"))
         return prologue_trace, new, epilogue_trace
 
@@ -191,6 +303,10 @@ class TensorParallelTransform(Transform):
             full = f"{submodule_name}.{k}" if submodule_name else k
             if full in self.original_shapes and isinstance(v, torch.Tensor):
                 kind = self.param_kinds.get(full, (COLUMN, None))[0]
+                if kind == "head_qkv":
+                    nh, ng, hs = self.head_info[full]
+                    out[k] = v.index_select(0, self._qkv_rows(nh, ng, hs, world, rank).to(v.device)).clone()
+                    continue
                 dim = 0 if (kind == COLUMN or k.endswith("bias")) else 1
                 n = v.shape[dim] // world
                 out[k] = v.narrow(dim, rank * n, n).clone()
@@ -206,9 +322,17 @@ class TensorParallelTransform(Transform):
             full = f"{submodule_name}.{k}" if submodule_name else k
             if full in self.original_shapes and isinstance(v, torch.Tensor):
                 kind = self.param_kinds.get(full, (COLUMN, None))[0]
-                dim = 0 if (kind == COLUMN or k.endswith("bias")) else 1
                 parts = [torch.empty_like(v) for _ in range(world)]
                 tdist.all_gather(parts, v.contiguous(), group=group)
+                if kind == "head_qkv":
+                    nh, ng, hs = self.head_info[full]
+                    full_t = torch.empty((self.original_shapes[full][0],) + tuple(v.shape[1:]), dtype=v.dtype,
+                                         device=v.device)
+                    for r, part in enumerate(parts):
+                        full_t.index_copy_(0, self._qkv_rows(nh, ng, hs, world, r).to(v.device), part)
+                    out[k] = full_t
+                    continue
+                dim = 0 if (kind == COLUMN or k.endswith("bias")) else 1
                 out[k] = torch.cat(parts, dim)
             else:
                 out[k] = v
@@ -290,6 +414,96 @@ def remove_redundant_comms(trace):
         return trace
     new = dce(new)
     new.set_provenance(TraceProvenance("Remove redundant tensor-parallel communication"))
+    return new
+
+
+# ---------------------------------------------------------------------------------------------
+# Vocab-parallel loss
+# ---------------------------------------------------------------------------------------------
+_RESHAPES = ("reshape", "view", "flatten")
+
+
+def vocab_parallel_loss(trace, group):
+    """Rewrites ``cross_entropy(reshape*(all_gather_lastdim(linear(x, W_vocab_shard))), target)`` into
+    a vocab-parallel cross-entropy on the local logits (weight None, no label smoothing, 2-D logits
+    after the reshapes, mean / sum reduction)."""
+    from ... import torch as ltorch
+
+    consumers: dict[str, list] = {}
+    producers: dict[str, BoundSymbol] = {}
+    for b in trace.bound_symbols:
+        for a in b.flat_proxy_args:
+            consumers.setdefault(a.name, []).append(b)
+        for o in b.flat_proxy_outs:
+            producers[o.name] = b
+    plans = {}
+    for b in trace.bound_symbols:
+        if b.sym.name != "cross_entropy":
+            continue
+        args = list(b.args)
+        kw = dict(b.kwargs)
+        inp = args[0]
+        target = args[1] if len(args) > 1 else kw.get("target")
+        weight = args[2] if len(args) > 2 else kw.get("weight")
+        ignore_index = args[4] if len(args) > 4 else kw.get("ignore_index", -100)
+        reduction = args[6] if len(args) > 6 else kw.get("reduction", "mean")
+        smoothing = args[7] if len(args) > 7 else kw.get("label_smoothing", 0.0)
+        if weight is not None or smoothing or reduction not in ("mean", "sum") or not isinstance(inp, TensorProxy):
+            continue
+        if inp.ndim != 2 or target is None:
+            continue
+        chain = []
+        p = inp
+        ok = False
+        while True:
+            pb = producers.get(p.name)
+            if pb is None:
+                break
+            if len(consumers.get(p.name, ())) != 1:
+                break
+            if _is_tp(pb, TPLayerType.COLUMN_LINEAR, out=True):
+                ok = True
+                break
+            if pb.sym.name in _RESHAPES and isinstance(pb.args[0], TensorProxy):
+                chain.append(pb)
+                p = pb.args[0]
+                continue
+            break
+        if not ok:
+            continue
+        sync = producers[p.name]
+        local = sync.args[0]
+        if tuple(local.shape[:-1]) != tuple(p.shape[:-1]) or inp.shape[-1] != p.shape[-1]:
+            continue  # the reshapes must only flatten the token dims
+        plans[b.output.name if isinstance(b.output, TensorProxy) else id(b)] = (b, local, target, ignore_index, reduction)
+    if not plans:
+        return trace
+    rank, world = tdist.get_rank(group), tdist.get_world_size(group)
+    new = from_trace(trace)
+    new.bound_symbols = []
+    new.scopes = [new.bound_symbols]
+    swap: dict = {}
+    targets = {id(v[0]): v for v in plans.values()}
+    with tracectx(new):
+        for b in trace.bound_symbols:
+            if id(b) in targets:
+                _, local, target, ignore_index, reduction = targets[id(b)]
+                local = swap.get(local.name, local)
+                target = swap.get(target.name, target) if isinstance(target, TensorProxy) else target
+                vl = local.shape[-1]
+                l2 = ltorch.reshape(local, (-1, vl))
+                t2 = ltorch.reshape(target, (-1,))
+                rows, _lse = dist_prims.vocab_parallel_cross_entropy_fwd(l2, t2, group, rank * vl, ignore_index)
+                total = ltorch.sum(rows)
+                if reduction == "mean":
+                    cnt = ltorch.sum(ltorch.to(ltorch.ne(t2, ignore_index), rows.dtype))
+                    total = ltorch.true_divide(total, cnt)
+                loss = ltorch.to(total, b.output.dtype)
+                swap[b.output.name] = loss
+                continue
+            new.bound_symbols.append(b.swap_proxies(swap))
+    new = dce(new)
+    new.set_provenance(TraceProvenance("Vocab-parallel cross-entropy"))
     return new
 
 

@@ -125,37 +125,44 @@ _choice: dict = {}
 
 # Library GEMM solutions pre-selected on MI355X for the shapes of the Llama-2-7B training step
 # (PyTorch TunableOp results: rocBLAS / hipBLASLt solution per (layout, M, N, K), measured with
-# rotating buffers on random data by scripts/tunable_probe.py on this image).  hipBLASLt's
-# default heuristic picks a 0.9 PF/s kernel for N = 11008 where a rocBLAS solution reaches
-# 1.46 PF/s; the per-shape selection below then compares the hand-written kernel against the
-# tuned library call.  The file's validators (PyTorch / HIP / rocBLAS / hipBLASLt versions, arch)
-# must match the running stack or TunableOp ignores it.  ``LTA_TUNED_GEMMS=0`` disables.
+# rotating buffers on random data by scripts/tunable_probe.py on this image).  OPT-IN
+# (``LTA_TUNED_GEMMS=1``): TunableOp is a process-wide switch that also changes every GEMM of user
+# code, so the framework never turns it on by itself; the hand-written kernels (csrc/gemm4.hip)
+# are the default GEMM path.  When enabled, the shipped table is read first and TunableOp is
+# switched on only if the table matched this stack (validators: PyTorch / HIP / rocBLAS / hipBLASLt
+# versions, arch); tuning and write-on-exit stay off.
 TUNED_GEMMS = _os.path.join(_os.path.dirname(__file__), "tuned", "gemm_mi355x_bf16.csv")
 _tuned_state: dict = {}
 
 
 def enable_tuned_gemms() -> bool:
-    """Load the shipped TunableOp results once per process (tuning itself stays off, so shapes
-    not in the file use the library default).  Returns whether the results are active."""
+    """Load the shipped TunableOp results once per process when ``LTA_TUNED_GEMMS=1``.  Returns
+    whether they are active; on any mismatch TunableOp's state is left exactly as it was."""
     if "active" in _tuned_state:
         return _tuned_state["active"]
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return False  # never switch TunableOp on inside a graph capture; the next eager call will
     active = False
     tun = getattr(torch.cuda, "tunable", None)
-    if (_os.environ.get("LTA_TUNED_GEMMS", "1") != "0" and torch.version.hip is not None and tun is not None
+    if (_os.environ.get("LTA_TUNED_GEMMS", "0") == "1" and torch.version.hip is not None and tun is not None
             and _os.path.exists(TUNED_GEMMS) and torch.cuda.is_available()):
+        prev = None
         try:
-            if not tun.is_enabled():
-                import tempfile
-
-                # TunableOp may write its table back on exit: keep that out of the package
-                tun.set_filename(_os.path.join(tempfile.gettempdir(), f"lta_tunableop_{_os.getpid()}.csv"))
+            prev = (tun.is_enabled(), tun.tuning_is_enabled())
+            if tun.read_file(TUNED_GEMMS):
+                if hasattr(tun, "write_file_on_exit"):
+                    tun.write_file_on_exit(False)
                 tun.tuning_enable(False)
                 tun.enable(True)
-            active = bool(tun.read_file(TUNED_GEMMS))
+                active = True
         except Exception:  # an older/newer stack without the API: library defaults
             active = False
+        if not active and prev is not None:
+            try:
+                tun.enable(prev[0])
+                tun.tuning_enable(prev[1])
+            except Exception:
+                pass
     _tuned_state["active"] = active
     return active
 

@@ -49,6 +49,11 @@ def _worker(rank, port, mode, out_dir):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if mode.endswith("_coalesced"):
+        # the grouped-collective bucket form RCCL runs by default: trace plumbing,
+        # per-gradient futures / waits and shard shapes exercised on gloo
+        os.environ["LTA_COALESCED_GRAD_SYNC"] = "1"
+        mode = mode[: -len("_coalesced")]
     torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         m = _model().double()
@@ -65,6 +70,8 @@ def _worker(rank, port, mode, out_dir):
             jm = fsdp(jm, bucketing_strategy=FSDPBucketingStrategy.LAYER)
         elif mode == "fsdp_block_zero3":
             jm = fsdp(jm, sharding_strategy=FSDPType.ZERO3, bucketing_strategy=FSDPBucketingStrategy.BLOCK)
+        elif mode == "fsdp_block":
+            jm = fsdp(jm, bucketing_strategy=FSDPBucketingStrategy.BLOCK)
         out = jm(_data(rank))
         loss = out.pow(2).mean()
         loss.backward()
@@ -85,7 +92,7 @@ def _run(mode):
         return [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=False) for r in range(WORLD)]
 
 
-@pytest.mark.parametrize("mode", ["ddp", "ddp_nobucket"])
+@pytest.mark.parametrize("mode", ["ddp", "ddp_nobucket", "ddp_coalesced"])
 def test_ddp_gloo(mode):
     ref, _ = _reference_grads()
     res = _run(mode)
@@ -95,9 +102,12 @@ def test_ddp_gloo(mode):
     assert "all_reduce" in res[0]["bw"]
     if mode == "ddp":  # buckets: packed buffer (gloo) or one coalesced collective (RCCL)
         assert "pack" in res[0]["bw"] or "all_reduce_coalesced" in res[0]["bw"]
+    if mode == "ddp_coalesced":
+        assert "all_reduce_coalesced" in res[0]["bw"] and "pack(" not in res[0]["bw"]
 
 
-@pytest.mark.parametrize("mode", ["fsdp", "fsdp_zero3", "fsdp_layer", "fsdp_block_zero3"])
+@pytest.mark.parametrize("mode", ["fsdp", "fsdp_zero3", "fsdp_layer", "fsdp_block_zero3", "fsdp_block_coalesced",
+                                  "fsdp_zero3_coalesced"])
 def test_fsdp_gloo(mode):
     from lightning_thunder_amd.distributed.transforms import shard_tensor
 
@@ -109,6 +119,8 @@ def test_fsdp_gloo(mode):
             assert r["shapes"][n] == tuple(expected.shape)
             torch.testing.assert_close(r["grads"][n], expected)
     assert "reduce_scatter" in res[0]["bw"]
+    if mode.endswith("_coalesced"):
+        assert "reduce_scatter_coalesced" in res[0]["bw"] and "pack_for_fsdp" not in res[0]["bw"]
     if mode == "fsdp_layer":
         # one coalesced gather per Linear (weight + bias), not one per parameter
         assert res[0]["fw"].count("all_gather_coalesced(") == 3, res[0]["fw"]

@@ -83,7 +83,9 @@ def test_fsdp_dcp_roundtrip_padding_spans_ranks():
     assert res[0]["full_shapes"]["2.weight"] == (5, 3)
 
 
-def _hybrid_worker(rank, world, port, d):
+def _hybrid_worker(rank, world, port, d, coalesced=False):
+    if coalesced:
+        os.environ["LTA_COALESCED_GRAD_SYNC"] = "1"
     import lightning_thunder_amd as thunder
     from lightning_thunder_amd.plugins import FSDP
     from torch.distributed.device_mesh import init_device_mesh
@@ -98,12 +100,17 @@ def _hybrid_worker(rank, world, port, d):
         x = torch.randn(4, 8, generator=g, dtype=torch.float64)
         tm(x).pow(2).mean().backward()
         grads = {n: p.grad.clone() for n, p in m.named_parameters()}
-        torch.save({"grads": grads}, os.path.join(d, f"r{rank}.pt"))
+        bw = str(thunder.last_backward_traces(tm)[-1])
+        torch.save({"grads": grads, "bw": bw}, os.path.join(d, f"r{rank}.pt"))
     finally:
         torch.distributed.destroy_process_group()
 
 
-def test_hybrid_mesh_fsdp_plugin():
+import pytest
+
+
+@pytest.mark.parametrize("coalesced", [False, True])
+def test_hybrid_mesh_fsdp_plugin(coalesced):
     from lightning_thunder_amd.distributed.transforms import shard_tensor
 
     world = 4
@@ -114,10 +121,13 @@ def test_hybrid_mesh_fsdp_plugin():
         loss = loss + ref(torch.randn(4, 8, generator=g, dtype=torch.float64)).pow(2).mean() / world
     loss.backward()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_hybrid_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_hybrid_worker, args=(world, _free_port(), d, coalesced), nprocs=world, join=True,
+                           start_method="spawn")
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
     for rank, r in enumerate(res):
         fsdp_rank = rank % 2
         for n, p in ref.named_parameters():
             expected, _ = shard_tensor(p.grad, fsdp_rank, 2)
             torch.testing.assert_close(r["grads"][n], expected)
+        if coalesced:  # grouped reduce-scatter per bucket, then the replica-group all-reduce per gradient
+            assert "reduce_scatter_coalesced" in r["bw"] and "all_reduce" in r["bw"], r["bw"]
