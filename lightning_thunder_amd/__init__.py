@@ -257,6 +257,12 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             bw = bw_traces[-1]
             fw = maybe_sort_waits(fw)
             bw = maybe_sort_waits(bw)
+            window = cd.compile_options.get("lta_fsdp_allgather_window")
+            if window:
+                from .distributed.utils import schedule_allgathers
+
+                fw = schedule_allgathers(fw, int(window))
+                bw = schedule_allgathers(bw, int(window))
             fw = del_last_used(fw)
             bw = del_last_used(bw)
             bw.unpack_list_arg = True
@@ -288,6 +294,11 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             ex_traces = transform_for_execution(comp, executors)
             c = ex_traces[-1]
             c = maybe_sort_waits(c)
+            window = cd.compile_options.get("lta_fsdp_allgather_window")
+            if window:
+                from .distributed.utils import schedule_allgathers
+
+                c = schedule_allgathers(c, int(window))
             c = del_last_used(c)
             for t in _post_transforms(cd):
                 c = t.transform_trace_post_optimization(c, compile_data=cd)

@@ -149,6 +149,10 @@ class FSDPTransform(Transform):
             # forward all-gathers: one coalesced RCCL launch per layer / block instead of one per
             # parameter (executors/passes.py -> distributed/bucketing.py:bucket_fsdp_all_gathers)
             cd.compile_options.setdefault("lta_fsdp_bucketing", self.bucketing_strategy)
+            if self.sharding_strategy == FSDPType.ZERO3:
+                # ZeRO-3 frees gathered parameters after use: bound the in-flight gathers to a
+                # 2-bucket prefetch window (distributed/utils.py:schedule_allgathers)
+                cd.compile_options.setdefault("lta_fsdp_allgather_window", 2)
         group = self._group()
         rank, world = tdist.get_rank(group), tdist.get_world_size(group)
         inner = model._model

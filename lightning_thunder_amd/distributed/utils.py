@@ -3,9 +3,10 @@
 
 ``sort_waits`` reorders a trace (respecting data dependencies) so that collectives are
 issued as early as possible and their ``wait`` s as late as possible — RCCL on its own
-stream then overlaps with compute.  ``limit_in_flight_allgathers`` bounds how many
-FSDP all-gathers are outstanding (memory vs overlap; with 288 GB of HBM the default is
-unbounded).
+stream then overlaps with compute.  ``schedule_allgathers`` / ``limit_in_flight_allgathers``
+then re-place the parameter all-gathers in a sliding window (ZeRO-3: bounded gathered-parameter
+memory; ZeRO-2 keeps every gathered block for the backward anyway, so there the window is off
+and all gathers are issued at the start — 288 GB of HBM holds them).
 """
 from __future__ import annotations
 
@@ -60,25 +61,39 @@ def sort_waits(trace: TraceCtx) -> TraceCtx:
     indeg = [len(d) for d in deps]
     import heapq
 
-    def prio(i):
+    # collectives first, then ordinary ops (both in program order), waits last; among ready waits,
+    # the one that completes the inputs of some consumer ("useful") goes first, so the compute stream
+    # is not made to wait for collectives whose results are needed only later (e.g. the backward's
+    # ZeRO-3 re-gathers, consumed in reverse layer order)
+    ready_coll, ready_ops, ready_waits = [], [], []
+
+    def push(i):
         b = body[i]
         if _is_collective(b):
-            return (0, i)
-        if _is_wait(b):
-            return (2, i)
-        return (1, i)
+            heapq.heappush(ready_coll, i)
+        elif _is_wait(b):
+            ready_waits.append(i)
+        else:
+            heapq.heappush(ready_ops, i)
 
-    ready = [prio(i) for i in range(len(body)) if indeg[i] == 0]
-    heapq.heapify(ready)
+    for i in range(len(body)):
+        if indeg[i] == 0:
+            push(i)
     order = []
-    while ready:
-        # waits only when nothing else is ready
-        p, i = heapq.heappop(ready)
+    while ready_coll or ready_ops or ready_waits:
+        if ready_coll:
+            i = heapq.heappop(ready_coll)
+        elif ready_ops:
+            i = heapq.heappop(ready_ops)
+        else:
+            useful = [w for w in ready_waits if any(indeg[u] == 1 for u in users[w])]
+            i = min(useful) if useful else min(ready_waits)
+            ready_waits.remove(i)
         order.append(i)
         for u in users[i]:
             indeg[u] -= 1
             if indeg[u] == 0:
-                heapq.heappush(ready, prio(u))
+                push(u)
     if len(order) != len(body):  # cycle guard (should not happen)
         return trace
     new = from_trace(trace)
@@ -94,33 +109,85 @@ def maybe_sort_waits(trace: TraceCtx) -> TraceCtx:
     return trace
 
 
-def limit_in_flight_allgathers(trace: TraceCtx, max_in_flight: int = 4) -> TraceCtx:
-    """Reorders so at most ``max_in_flight`` all-gathers are outstanding (their waits pulled earlier)."""
+def _flat_futures(b: BoundSymbol) -> list[str]:
+    from ..core.pytree import tree_flatten
+
+    return [o.name for o in tree_flatten(b.output)[0] if isinstance(o, Proxy)]
+
+
+def schedule_allgathers(trace: TraceCtx, prefetch: int = 2) -> TraceCtx:
+    """Sliding-window placement of the (coalesced) parameter all-gathers (reference
+    ``sort_communication_ops`` + ``limit_in_flight_allgathers``, thunder/distributed/utils.py:61-117,
+    197-298).  Gathers are ordered by their first ``wait``; gather i is issued right after the last
+    wait of gather i - ``prefetch`` (the first ``prefetch`` ones at the program start), so while block
+    k computes, the gathers of blocks k+1 .. k+prefetch-1 are in flight and at most ``prefetch``
+    gathered blocks are live: ZeRO-3 memory stays bounded without serializing RCCL behind compute.
+    Every other op keeps its relative order."""
     bsyms = list(trace.bound_symbols)
+    gathers = [b for b in bsyms if _is_collective(b) and "all_gather" in b.sym.name]
+    if len(gathers) <= prefetch or prefetch < 1:
+        return trace
+    fut_owner: dict[str, int] = {}
+    for gi, g in enumerate(gathers):
+        for n in _flat_futures(g):
+            fut_owner[n] = gi
+    first_wait: dict[int, int] = {}
+    last_wait: dict[int, int] = {}
+    for pos, b in enumerate(bsyms):
+        if _is_wait(b) and b.args and isinstance(b.args[0], Proxy) and b.args[0].name in fut_owner:
+            gi = fut_owner[b.args[0].name]
+            first_wait.setdefault(gi, pos)
+            last_wait[gi] = pos
+    if len(first_wait) != len(gathers):
+        return trace  # a gather without waits (or a non-gather future): leave the program alone
+    order = sorted(range(len(gathers)), key=lambda gi: first_wait[gi])
+    gather_ids = {id(g) for g in gathers}
+    after: dict[int, list] = {}  # position of a wait -> gathers to issue right after it
+    head = []
+    for k, gi in enumerate(order):
+        if k < prefetch:
+            head.append(gathers[gi])
+        else:
+            after.setdefault(last_wait[order[k - prefetch]], []).append(gathers[gi])
+    # a gather must also come after whatever produces its inputs (normally trace inputs)
     out = []
-    inflight: list[BoundSymbol] = []
-    waits_by_future = {}
-    for b in bsyms:
-        if _is_wait(b):
-            waits_by_future[b.args[0].name] = b
-    emitted_waits = set()
-    for b in bsyms:
-        if _is_wait(b) and id(b) in emitted_waits:
+    ret = bsyms[-1] if bsyms and bsyms[-1].sym.id == PrimIDs.RETURN else None
+    produced_at: dict[str, int] = {}
+    for pos, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            produced_at.setdefault(o.name, pos)
+    late_head = []
+    for g in head:
+        if any(a.name in produced_at for a in g.flat_proxy_args):
+            late_head.append(g)
+    head = [g for g in head if g not in late_head]
+    out.extend(head)
+    pending_late = list(late_head)
+    for pos, b in enumerate(bsyms):
+        if id(b) in gather_ids:
             continue
-        if _is_collective(b) and "all_gather" in b.sym.name and len(inflight) >= max_in_flight:
-            oldest = inflight.pop(0)
-            w = waits_by_future.get(oldest.output.name) if isinstance(oldest.output, Proxy) else None
-            if w is not None and id(w) not in emitted_waits:
-                out.append(w)
-                emitted_waits.add(id(w))
+        if b is ret:
+            break
         out.append(b)
-        if _is_wait(b):
-            emitted_waits.add(id(b))
-            inflight = [c for c in inflight if not (isinstance(c.output, Proxy) and c.output.name == b.args[0].name)]
-        elif _is_collective(b) and "all_gather" in b.sym.name:
-            inflight.append(b)
+        if pending_late:
+            ready = [g for g in pending_late
+                     if all(produced_at.get(a.name, -1) <= pos for a in g.flat_proxy_args)]
+            out.extend(ready)
+            pending_late = [g for g in pending_late if g not in ready]
+        out.extend(after.get(pos, ()))
+    out.extend(pending_late)
+    if ret is not None:
+        out.append(ret)
+    if len(out) != len(bsyms):
+        return trace
     new = from_trace(trace)
     new.bound_symbols = out
     new.scopes = [new.bound_symbols]
-    new.set_provenance(TraceProvenance(f"Limit in-flight all-gathers ({max_in_flight})"))
+    new.set_provenance(TraceProvenance(f"Schedule all-gathers (prefetch window {prefetch})"))
     return new
+
+
+def limit_in_flight_allgathers(trace: TraceCtx, max_in_flight: int = 2) -> TraceCtx:
+    """At most ``max_in_flight`` parameter all-gathers outstanding: ``schedule_allgathers`` with that
+    window (reference name, thunder/distributed/utils.py:197-298)."""
+    return schedule_allgathers(trace, max_in_flight)

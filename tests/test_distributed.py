@@ -28,13 +28,27 @@ def _model():
                                torch.nn.Linear(5, 3))
 
 
+class _Blocks(torch.nn.Module):
+    """Numbered blocks (``layers.<i>``): one FSDP block bucket each."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.layers = torch.nn.ModuleList([torch.nn.Linear(8, 8) for _ in range(5)])
+
+    def forward(self, x):
+        for l in self.layers:
+            x = torch.tanh(l(x))
+        return x
+
+
 def _data(rank):
     g = torch.Generator().manual_seed(100 + rank)
     return torch.randn(4, 8, generator=g, dtype=torch.float64)
 
 
-def _reference_grads():
-    m = _model().double()
+def _reference_grads(make=None):
+    m = (make or _model)().double()
     x = torch.cat([_data(r) for r in range(WORLD)])
     # each rank averages its local mean loss; the global objective is the mean over ranks
     loss = sum(m(_data(r)).pow(2).mean() for r in range(WORLD)) / WORLD
@@ -56,9 +70,11 @@ def _worker(rank, port, mode, out_dir):
         mode = mode[: -len("_coalesced")]
     torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
-        m = _model().double()
+        m = (_Blocks() if mode.startswith("blocks_") else _model()).double()
         jm = thunder.jit(m)
-        if mode == "ddp":
+        if mode == "blocks_zero3":
+            jm = fsdp(jm, sharding_strategy=FSDPType.ZERO3, bucketing_strategy=FSDPBucketingStrategy.BLOCK)
+        elif mode == "ddp":
             jm = ddp(jm, bucket_size_in_mb=0.0005)
         elif mode == "ddp_nobucket":
             jm = ddp(jm, bucket_size_in_mb=0)
@@ -132,3 +148,23 @@ def test_fsdp_gloo(mode):
     if "zero3" in mode:
         # ZeRO-3 saves shards and re-gathers (also when the padding trim follows the gather)
         assert "all_gather" in res[0]["bw"]
+
+
+def test_fsdp_zero3_allgather_window():
+    """ZeRO-3 with per-block buckets: the parameter all-gathers are issued in a 2-block sliding window
+    (not all at the program start) in the forward and the backward re-gathers, and grads match."""
+    from lightning_thunder_amd.distributed.transforms import shard_tensor
+
+    ref, _ = _reference_grads(_Blocks)
+    res = _run("blocks_zero3")
+    for rank, r in enumerate(res):
+        for n, g in ref.items():
+            expected, _ = shard_tensor(g, rank, WORLD)
+            torch.testing.assert_close(r["grads"][n], expected)
+    for key in ("fw", "bw"):
+        lines = [l.strip() for l in res[0][key].splitlines()]
+        gathers = [i for i, l in enumerate(lines) if "all_gather_coalesced(" in l]
+        waits = [i for i, l in enumerate(lines) if "wait(" in l]
+        assert len(gathers) >= 4, res[0][key]
+        # gather of block 2 comes after the first wait: at most two blocks in flight
+        assert gathers[2] > waits[0], (key, gathers, waits)
