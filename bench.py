@@ -215,10 +215,8 @@ def run(args, rank, world, device, mode):
     if mode == "thunder":
         from lightning_thunder_amd.ops import gemm as _g
 
-        hand = lambda tab: sorted(k[:3] for k, v in tab.items() if v)  # noqa: E731
-        log(rank, f"[gemm] hand-kernel shapes: linear {hand(_g.selection_table())}, "
-                  f"matmul {hand(_g.matmul_selection_table())}; tuned library table active: "
-                  f"{_g.enable_tuned_gemms()}")
+        log(rank, f"[gemm] calls per backend since start (gemm4 = hand MFMA kernel, torch = library): "
+                  f"{_g.last_gemm_backend_counts()}")
     del model, opt, fwd, params
     return dt, cfg, mem, parallel
 

@@ -117,11 +117,8 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
 
 
 # ---------------------------------------------------------------------------------------------
-# linear with per-shape kernel selection
+# linear / matmul dispatch (static rules, no run-time timing)
 # ---------------------------------------------------------------------------------------------
-import os as _os
-
-_choice: dict = {}
 
 # Library GEMM solutions pre-selected on MI355X for the shapes of the Llama-2-7B training step
 # (PyTorch TunableOp results: rocBLAS / hipBLASLt solution per (layout, M, N, K), measured with
@@ -165,31 +162,6 @@ def enable_tuned_gemms() -> bool:
                 pass
     _tuned_state["active"] = active
     return active
-
-
-def _timeit(fn, iters: int = 5) -> float:
-    for _ in range(2):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
-
-
-def _faster_is_first(f_a, f_b, rounds: int | None = None) -> bool:
-    """A/B timing interleaved over a few rounds (min of each): one-shot timings of two kernels
-    taken back to back pick up clock (DVFS) swings as if they were kernel differences."""
-    if rounds is None:
-        rounds = int(_os.environ.get("LTA_GEMM_SELECT_ROUNDS", "3"))
-    ta, tb = float("inf"), float("inf")
-    for _ in range(rounds):
-        ta = min(ta, _timeit(f_a))
-        tb = min(tb, _timeit(f_b))
-    return ta <= tb
 
 
 def _torch_linear(x2, w, bias, residual, act):
@@ -292,36 +264,59 @@ def gemv_group(x: torch.Tensor, weights, *, norm: bool = False, norm_weight=None
     return buf if packed else outs
 
 
+_backend_counts: dict = {}
+
+
+def _count(backend: str) -> None:
+    _backend_counts[backend] = _backend_counts.get(backend, 0) + 1
+
+
+def last_gemm_backend_counts(reset: bool = False) -> dict:
+    """How many GEMM calls each backend served since the last reset: ``gemm4`` (csrc/gemm4.hip),
+    ``gemm`` (csrc/gemm.hip, K % 128 != 0), ``gemv`` (decode rows), ``torch`` (library fallback:
+    shapes no hand kernel tiles, or ``LTA_GEMM=torch``)."""
+    out = dict(_backend_counts)
+    if reset:
+        _backend_counts.clear()
+    return out
+
+
+def gemm4_variant(at: int, bt: int, M: int, N: int, K: int) -> int:
+    """Static, deterministic kernel-variant table (no run-time timing: every process runs the same
+    kernels, so numerics never depend on a benchmark's noise).  Variant = the LDS-DMA split of
+    csrc/gemm4.hip; 0 everywhere unless a measured row below says otherwise."""
+    return _GEMM4_VARIANTS.get((at, bt, N, K), _GEMM4_VARIANTS.get((at, bt), 0))
+
+
+# (at, bt[, N, K]) -> variant, from profiles/gemm4_microbench.json
+_GEMM4_VARIANTS: dict = {}
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
-    """``act(x @ w.T + bias) + residual`` choosing, once per shape, the faster of the hand-written
-    kernel (MFMA GEMM, or the weight-streaming GEMV for M <= 8; epilogue fused) and hipBLASLt +
-    separate epilogue (``LTA_GEMM=hip|torch|auto``)."""
+    """``act(x @ w.T + bias) + residual`` on the hand-written kernels, chosen by a static rule:
+    the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip) when M, N % 256
+    and K % 128, the 8-wave kernel (csrc/gemm.hip) when K % 64, else torch (``LTA_GEMM=torch``
+    forces torch)."""
     K = x.shape[-1]
     N = w.shape[0]
     x2 = x.reshape(-1, K)
     r2 = None if residual is None else residual.reshape(-1, N)
-    if x.is_cuda:
-        enable_tuned_gemms()
     mode = _os.environ.get("LTA_GEMM", "auto")
-    if mode != "torch" and gemv_supported(x2, w, bias, r2):
-        return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
-    ok = gemm_nt_supported(x2, w, bias, r2)
-    if not ok or mode == "torch":
-        return _torch_linear(x2, w, bias, r2, act).reshape(*x.shape[:-1], N)
-    key = (x2.shape[0], N, K, bias is not None, residual is not None, act)
-    use = True if mode == "hip" else _choice.get(key)
-    if use is None:
-        if torch.cuda.is_current_stream_capturing():
-            use = True
-        else:
-            use = _faster_is_first(lambda: gemm_nt(x2, w, bias=bias, residual=r2, act=act),
-                                   lambda: _torch_linear(x2, w, bias, r2, act))
-        _choice[key] = use
-    if use:
-        y = gemm_nt(x2, w, bias=bias, residual=r2, act=act)
-    else:
-        y = _torch_linear(x2, w, bias, r2, act)
-    return y.reshape(*x.shape[:-1], N)
+    if mode != "torch":
+        if gemv_supported(x2, w, bias, r2):
+            _count("gemv")
+            return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
+        wt = w.t()
+        lay = gemm4_layout(x2, wt)
+        if lay is not None and gemm_nt_supported(x2, w, bias, r2):
+            _count("gemm4")
+            y = matmul4(x2, wt, bias=bias, residual=r2, act=act, variant=gemm4_variant(0, 0, x2.shape[0], N, K))
+            return y.reshape(*x.shape[:-1], N)
+        if gemm_nt_supported(x2, w, bias, r2):
+            _count("gemm")
+            return gemm_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
+    _count("torch")
+    return _torch_linear(x2, w, bias, r2, act).reshape(*x.shape[:-1], N)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -381,50 +376,43 @@ def matmul_hip(a: torch.Tensor, b: torch.Tensor, *, residual: torch.Tensor | Non
     return out
 
 
-_mm_choice: dict = {}
-
-
 def _torch_mm(a, b, residual=None):
     return torch.matmul(a, b) if residual is None else torch.addmm(residual, a, b)
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
-    """``a @ b (+ residual)`` for the prim matmul (leading dims of ``a`` flattened): the MFMA kernel
-    where it is faster than hipBLASLt for this shape, operand layout and epilogue (timed once per
-    key), else torch (``addmm`` with beta = 1 when there is a residual)."""
+    """``a @ b (+ residual)`` for the prim matmul (leading dims of ``a`` flattened) — the backward's
+    dgrad / wgrad read their transposed operands in place.  Static rule as :func:`linear`: the
+    4-wave kernel, else the 8-wave kernel, else torch."""
     if a.dim() > 2 and b.dim() == 2:
         lead = a.shape[:-1]
         a2 = a.reshape(-1, a.shape[-1])
         r2 = None if residual is None else residual.reshape(-1, b.shape[1])
         return matmul(a2, b, r2).reshape(*lead, b.shape[1])
     mode = _os.environ.get("LTA_GEMM", "auto")
-    lay = matmul_layout(a, b) if mode != "torch" else None
-    if residual is not None and (residual.dtype != torch.bfloat16 or residual.stride(1) != 1
-                                 or residual.stride(0) % 8 or residual.data_ptr() % 16):
-        lay = None
-    if a.is_cuda:
-        enable_tuned_gemms()
-    if lay is None:
-        return _torch_mm(a, b, residual)
-    key = (a.shape[0], b.shape[1], a.shape[1], lay[0], lay[1], residual is not None)
-    use = True if mode == "hip" else _mm_choice.get(key)
-    if use is None:
-        if torch.cuda.is_current_stream_capturing():
-            use = True
-        else:
-            use = _faster_is_first(lambda: matmul_hip(a, b, residual=residual), lambda: _torch_mm(a, b, residual))
-        _mm_choice[key] = use
-    return matmul_hip(a, b, residual=residual) if use else _torch_mm(a, b, residual)
+    res_ok = residual is None or (residual.dtype == torch.bfloat16 and residual.stride(1) == 1
+                                  and residual.stride(0) % 8 == 0 and residual.data_ptr() % 16 == 0)
+    if mode != "torch" and res_ok:
+        lay = gemm4_layout(a, b)
+        if lay is not None:
+            _count("gemm4")
+            return matmul4(a, b, residual=residual,
+                           variant=gemm4_variant(lay[0], lay[1], a.shape[0], b.shape[1], a.shape[1]))
+        if matmul_layout(a, b) is not None:
+            _count("gemm")
+            return matmul_hip(a, b, residual=residual)
+    _count("torch")
+    return _torch_mm(a, b, residual)
 
 
 def matmul_selection_table() -> dict:
-    """(M, N, K, a stored transposed, b stored row-major, residual) -> True if the HIP kernel was selected."""
-    return dict(_mm_choice)
+    """Kept for API compatibility: the selection is a static rule now (see :func:`matmul`)."""
+    return {}
 
 
 def selection_table() -> dict:
-    """(M, N, K, bias, residual, act) -> True if the HIP kernel was selected."""
-    return dict(_choice)
+    """Kept for API compatibility: the selection is a static rule now (see :func:`linear`)."""
+    return {}
 
 
 # ---------------------------------------------------------------------------------------------

@@ -186,6 +186,7 @@ def test_capture_with_tuned_gemm_table_active():
     )
     env = dict(os.environ)
     env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.abspath(__file__))) + os.pathsep + env.get("PYTHONPATH", "")
+    env["LTA_TUNED_GEMMS"] = "1"  # opt-in
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
 
