@@ -746,6 +746,12 @@ def _fuse_kv_cache_writes(trace):
             at = max(uk[0], uv[0])
             if any(i < j < at for j in uses.get(q.name, [])) or ready >= at:
                 continue
+            # moving the first cache write later: nothing in between may read its result or the
+            # cache it writes
+            lo = min(uk[0], uv[0])
+            watch = {ck.output.name, cv.output.name, bk.name, bv.name}
+            if any(lo < j < at for w in watch for j in uses.get(w, [])):
+                continue
         replace[at] = nb
         drop.update({i, uk[0], uv[0]} - {at})
     if not replace:

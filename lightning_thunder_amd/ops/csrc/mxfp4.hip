@@ -101,6 +101,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_mxfp4_kernel(const __hip_bflo
 LTA_EXPORT int lta_gemv_mxfp4(const void* x, const void* w, const void* s, const void* bias, void* y, int M, int N,
                               int K, int ldx, int ldy, hipStream_t stream) {
   if (M < 1 || M > MAXM || K % 32 || ldx % 8) return -2;
+  if (reinterpret_cast<uintptr_t>(x) % 16) return -2;  // x is read with 16-B vector loads
   // columns per wave: 8 amortise each activation load over more weight rows (the kernel is
   // bound by L1 traffic otherwise); 4 keep enough workgroups in flight for narrow outputs
   const bool wide = N >= 8192;

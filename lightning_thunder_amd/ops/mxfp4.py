@@ -128,8 +128,10 @@ def gemv(x: torch.Tensor, q: torch.Tensor, s: torch.Tensor, bias: torch.Tensor |
     N = q.shape[0]
     if M > GEMV_MAX_ROWS or q.shape[1] * 2 != K or s.shape != (N, K // BLOCK) or x2.dtype != torch.bfloat16:
         raise ValueError(f"gemv_mxfp4: unsupported operands x {tuple(x2.shape)} {x2.dtype}, q {tuple(q.shape)}")
-    if x2.stride(-1) != 1 or x2.stride(0) % 8:
-        x2 = x2.contiguous()
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()  # the kernel reads x with 16-B vector loads
+        if x2.data_ptr() % 16:
+            x2 = x2.clone()
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     if bias is not None:
         bias = bias.to(torch.bfloat16).contiguous()

@@ -131,3 +131,47 @@ def test_hybrid_mesh_fsdp_plugin(coalesced):
             torch.testing.assert_close(r["grads"][n], expected)
         if coalesced:  # grouped reduce-scatter per bucket, then the replica-group all-reduce per gradient
             assert "reduce_scatter_coalesced" in r["bw"] and "all_reduce" in r["bw"], r["bw"]
+
+
+def _sd_worker(rank, world, port, d):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import fsdp
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        jm = fsdp(thunder.jit(_model()))
+        x = torch.randn(4, 8, dtype=torch.float64, generator=torch.Generator().manual_seed(rank))
+        y0 = jm(x).detach()
+        sd = jm.state_dict()  # this rank's shards
+        full = jm.original_state_dict()  # reverse hooks: full tensors
+        ref = _model().state_dict()
+        full_err = max((full[k] - ref[k]).abs().max().item() for k in ref)
+        shapes_ok = all(tuple(full[k].shape) == tuple(ref[k].shape) for k in ref)
+        # assign-load of the transformed state: new Parameter objects keep the sharding metadata
+        jm.load_state_dict({k: v.clone() * 2 for k, v in sd.items()}, assign=True)
+        y2 = jm(x).detach()
+        # forward hooks: loading the full (original) dict re-shards it
+        jm.load_original_state_dict(full)
+        y3 = jm(x).detach()
+        bad_shape = False
+        try:
+            jm.load_state_dict({k: v for k, v in full.items()})
+        except RuntimeError:
+            bad_shape = True
+        torch.save({"full_err": full_err, "shapes_ok": shapes_ok, "changed": (y2 - y0).abs().max().item(),
+                    "restored": (y3 - y0).abs().max().item(), "bad_shape": bad_shape}, os.path.join(d, f"r{rank}.pt"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_thunder_module_state_dict_hooks_fsdp():
+    """state_dict = transformed shards, original_state_dict = reverse hooks (full tensors),
+    load_state_dict(assign=True) keeps the program working, load_original_state_dict re-shards."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_sd_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+    for r in res:
+        assert r["full_err"] == 0.0 and r["shapes_ok"], r
+        assert r["changed"] > 0 and r["restored"] < 1e-12 and r["bad_shape"], r
