@@ -60,12 +60,43 @@ def _target_name(node) -> str:
     return t if isinstance(t, str) else getattr(t, "__name__", str(t))
 
 
+def _hint(v):
+    """Concrete example value of a symbolic scalar (dynamo's hint for the traced size)."""
+    if isinstance(v, (torch.SymInt, torch.SymFloat, torch.SymBool)):
+        node = v.node
+        h = getattr(node, "hint", None)
+        if h is None:
+            h = node.shape_env.size_hint(node.expr) if getattr(node, "shape_env", None) is not None else None
+        if h is None:
+            raise ValueError(f"symbolic value {v} has no hint")
+        if isinstance(v, torch.SymBool):
+            return bool(h)
+        return float(h) if isinstance(v, torch.SymFloat) else int(h)
+    return v
+
+
 def _proxy_of(v, trc):
-    from ..core.proxies import tensorproxy, TensorProxy
+    from ..core.proxies import TensorProxy
 
     if isinstance(v, torch.Tensor):
-        return tensorproxy(v, name=trc.make_unique_name("fx"))
-    return v
+        # symbolic sizes (dynamic=True graphs) are checked at their example (hint) values: the op's
+        # support does not depend on the size, and the compiled submodule re-specializes per shape
+        shape = tuple(_hint(d) for d in v.shape)
+        return TensorProxy(trc.make_unique_name("fx"), shape=shape, device=v.device, dtype=v.dtype,
+                           requires_grad=v.requires_grad)
+    return _hint(v)
+
+
+def _is_dynamic(gm: torch.fx.GraphModule) -> bool:
+    for n in gm.graph.nodes:
+        if n.op != "placeholder":
+            continue
+        ev = n.meta.get("example_value", n.meta.get("val"))
+        if isinstance(ev, (torch.SymInt, torch.SymFloat, torch.SymBool)):
+            return True
+        if isinstance(ev, torch.Tensor) and any(isinstance(d, torch.SymInt) for d in ev.shape):
+            return True
+    return False
 
 
 def is_node_supported(node: torch.fx.Node) -> tuple[bool, SplitReason | None]:
@@ -88,9 +119,6 @@ def is_node_supported(node: torch.fx.Node) -> tuple[bool, SplitReason | None]:
 
     args = torch.fx.node.map_arg(node.args, example)
     kwargs = torch.fx.node.map_arg(node.kwargs, example)
-    flat = torch.utils._pytree.tree_leaves((args, kwargs))
-    if any(isinstance(a, torch.SymInt) for a in flat):
-        return False, SplitReason(SplitReasonType.UNSUPPORTED_NODE, f"{name}: symbolic shapes are not supported")
     trc = TraceCtx()
     try:
         with tracectx(trc):
@@ -133,6 +161,24 @@ class ThunderCompiler:
         self.thunder_options = thunder_options
         self.subgraph_infos: list[SubgraphInfo] = []
 
+    def _options(self, gm) -> dict:
+        """Per-graph jit options (reference ``thunder/dynamo/compiler.py:51-84,132-154``): the
+        dataflow fusion partitioner, and — for static graphs, whose input shapes / dtypes / devices
+        dynamo already guards — an extraction-only prologue (no redundant per-call checks).  Dynamic
+        graphs keep the checks: a new size must miss the cache and re-specialize."""
+        from ..transforms.prune_prologue_checks import ExtractionOnlyPrologueTransform
+
+        opts = dict(self.thunder_options)
+        opts.setdefault("fusion_type", "dataflow")
+        if not _is_dynamic(gm) and opts.pop("extraction_only_prologue", True):
+            ts = list(opts.get("transforms") or [])
+            if not any(isinstance(t, ExtractionOnlyPrologueTransform) for t in ts):
+                ts.append(ExtractionOnlyPrologueTransform())
+            opts["transforms"] = ts
+        else:
+            opts.pop("extraction_only_prologue", None)
+        return opts
+
     def __call__(self, gm: torch.fx.GraphModule, sample_args):
         from .. import jit
 
@@ -142,7 +188,7 @@ class ThunderCompiler:
         compiled = []
         mapping = {}
         if all(ok for _, ok in part.values()):
-            fn = jit(gm, **self.thunder_options)
+            fn = jit(gm, **self._options(gm))
             compiled.append(fn)
             self.subgraph_infos.append(SubgraphInfo(gm, None, compiled, {"whole": fn}, reasons))
             return fn
@@ -154,7 +200,7 @@ class ThunderCompiler:
             sub = getattr(split_gm, n.target)
             supported = any(ok for (i, ok) in part.values() if i == idx)
             if supported:
-                fn = jit(sub, **self.thunder_options)
+                fn = jit(sub, **self._options(gm))
                 setattr(split_gm, n.target, fn)
                 compiled.append(fn)
                 mapping[n.target] = fn

@@ -41,3 +41,54 @@ def test_recipe_fx_interpreter():
     cm = thunder.compile(m, recipe=BaseRecipe(fuser=None, interpreter="thunder.fx"))
     x = torch.randn(2, 4)
     torch.testing.assert_close(cm(x), m(x))
+
+
+def test_thunderfx_dynamic_shapes_no_eager_fallback():
+    """dynamic=True: dynamo hands over ONE graph with symbolic sizes; every node is supported
+    (checked at its example sizes), the whole graph runs compiled and re-specializes per length."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.dynamo import thunderfx
+
+    torch.manual_seed(0)
+    mlp = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.GELU(), torch.nn.Linear(32, 8))
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.m = mlp
+
+        def forward(self, x):
+            y = self.m(x)
+            return torch.nn.functional.softmax(y.reshape(x.shape[0], x.shape[1], -1), -1).sum(1)
+
+    mm = M()
+    f = thunderfx(mm, dynamic=True)
+    for T in (5, 7, 9):
+        x = torch.randn(3, T, 16, requires_grad=True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y = f(x)
+        ref = mm(x2)
+        torch.testing.assert_close(y, ref)
+        y.sum().backward()
+        ref.sum().backward()
+        torch.testing.assert_close(x.grad, x2.grad)
+    infos = f.subgraph_infos
+    assert len(infos) == 1 and not infos[0].split_reasons and infos[0].split_graph_module is None
+    (fn,) = infos[0].thunder_compiled_fns
+    assert thunder.cache_misses(fn) == 3
+
+
+def test_thunderfx_static_graph_extraction_only_prologue():
+    """Static graphs (dynamo guards the inputs) get an extraction-only prologue."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.dynamo import thunderfx
+    from lightning_thunder_amd.transforms.prune_prologue_checks import ExtractionOnlyPrologueTransform
+
+    m = torch.nn.Linear(4, 4)
+    f = thunderfx(m)
+    x = torch.randn(2, 4)
+    torch.testing.assert_close(f(x), m(x))
+    (fn,) = f.subgraph_infos[0].thunder_compiled_fns
+    assert any(isinstance(t, ExtractionOnlyPrologueTransform) for t in fn._lc_cd.transforms)
+    pro = str(thunder.last_prologue_traces(fn)[-1])
+    assert "check_tensor_shape_and_metadata" not in pro, pro
