@@ -452,6 +452,45 @@ def _index_add_rule(a, indices, value, dim):
     return out, bwd
 
 
+@register_vjp(PrimIDs.INDEX_PUT)
+def _index_put_rule(a, indices, values, accumulate):
+    """``out = a; out[indices] (+)= values`` (advanced indexing on the leading dims).  The values'
+    gradient is the cotangent gathered at the same indices (summed back to a broadcast value's shape);
+    with ``accumulate=False`` the overwritten positions get no gradient in ``a``."""
+    out = P.index_put(a, indices, values, accumulate)
+
+    def bwd(g):
+        ga = g
+        if not accumulate:
+            zero = P.full(tuple(values.shape), 0, device=g.device, dtype=g.dtype)
+            ga = P.index_put(g, indices, zero, False)
+        gv = None
+        if _requires(values):
+            gv = _ltorch().getitem(g, tuple(indices))
+            if tuple(gv.shape) != tuple(values.shape):
+                gv = sum_to_shape(gv, values.shape)
+            if gv.dtype != values.dtype:
+                gv = _clang().maybe_convert_to_dtype(gv, values.dtype)
+        return ga, None, gv, None
+
+    return out, bwd
+
+
+@register_vjp(PrimIDs.SCATTER)
+def _scatter_rule(a, index, src, dim):
+    """``out = a; out[index] = src`` along ``dim``: overwritten positions get no gradient in ``a``;
+    ``src`` receives the cotangent gathered at ``index``."""
+    out = P.scatter(a, index, src, dim)
+
+    def bwd(g):
+        zero = P.full(tuple(index.shape), 0, device=g.device, dtype=g.dtype)
+        ga = P.scatter(g, index, zero, dim)
+        gs = P.take_along_axis(g, index, dim) if _requires(src) else None
+        return ga, None, gs, None
+
+    return out, bwd
+
+
 @register_vjp(PrimIDs.SCATTER_ADD)
 def _scatter_add_rule(a, index, value, dim):
     out = P.scatter_add(a, index, value, dim)

@@ -1783,3 +1783,4 @@ def checkpoint(function, *args, **kwargs):
 # Distributed torch ops are defined in ..distributed.prims and registered there.
 
 from . import default_torch_ops  # noqa: E402,F401  (auto-registration of the long tail)
+from . import nn_ops  # noqa: E402,F401  (conv / pooling / normalization / activation decompositions)

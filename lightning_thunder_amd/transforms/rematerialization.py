@@ -104,6 +104,7 @@ def rematerialize_forward_and_backward(fb):
         return fb
 
     g = nx.DiGraph()
+    g.add_node("SOURCE")  # saved values recomputable from nothing (e.g. full) leave SOURCE edgeless
     inf = float("inf")
     for n, t in closure.items():
         cost = 1 if n in fw_inputs else max(1, _nbytes(t))

@@ -455,3 +455,200 @@ OPS: list[OpInfo] = [
 ]
 
 OPS_BY_NAME = {o.name: o for o in OPS}
+
+
+# =========================================================================================
+# Convolution / pooling / normalization / activations / shape utilities (torch/nn_ops.py)
+# =========================================================================================
+def _conv_samples(n):
+    def gen(device, dtype, requires_grad):
+        sp = (7,) * n
+        x = _t((2, 4) + sp, device, dtype, requires_grad)
+        w = _t((6, 4) + (3,) * n, device, dtype, requires_grad)
+        b = _t((6,), device, dtype, requires_grad)
+        yield SampleInput((x, w, b))
+        yield SampleInput((x, w), {"stride": 2, "padding": 1})
+        yield SampleInput((x, w, b), {"padding": "same", "dilation": 2})
+        wg = _t((6, 2) + (2,) * n, device, dtype, requires_grad)
+        yield SampleInput((x, wg), {"groups": 2, "padding": "same"})  # even kernel: asymmetric 'same'
+
+    return gen
+
+
+def _pool_samples(n, kind):
+    def gen(device, dtype, requires_grad):
+        x = _t((2, 3) + (9,) * n, device, dtype, requires_grad)
+        yield SampleInput((x, 3))
+        yield SampleInput((x, 3), {"stride": 2, "padding": 1})
+        if kind == "max":
+            yield SampleInput((x, 2), {"stride": 2, "dilation": 2})
+            yield SampleInput((x, 3), {"stride": 2, "ceil_mode": True})
+        else:
+            yield SampleInput((x, 3), {"stride": 2, "padding": 1, "count_include_pad": False})
+
+    return gen
+
+
+def _bn_samples(training):
+    def gen(device, dtype, requires_grad):
+        x = _t((4, 3, 5, 5), device, dtype, requires_grad)
+        w = _t((3,), device, dtype, requires_grad, 0.5, 1.5)
+        b = _t((3,), device, dtype, requires_grad)
+        rm = torch.zeros(3, device=device, dtype=dtype)
+        rv = torch.ones(3, device=device, dtype=dtype)
+        yield SampleInput((x, rm.clone(), rv.clone(), w, b), {"training": training})
+        yield SampleInput((x, rm.clone(), rv.clone()), {"training": training, "momentum": 0.2, "eps": 1e-3})
+
+    return gen
+
+
+def _interp_samples(mode, n):
+    def gen(device, dtype, requires_grad):
+        x = _t((2, 3) + (5,) * n, device, dtype, requires_grad)
+        kw = {"mode": mode}
+        yield SampleInput((x,), dict(kw, size=(8,) * n))
+        yield SampleInput((x,), dict(kw, scale_factor=2.0))
+        yield SampleInput((x,), dict(kw, size=(3,) * n))
+        if mode != "nearest":
+            yield SampleInput((x,), dict(kw, size=(8,) * n, align_corners=True))
+
+    return gen
+
+
+def _prelu_samples(device, dtype, requires_grad):
+    yield SampleInput((_t((2, 3, 4), device, dtype, requires_grad), _t((3,), device, dtype, requires_grad, 0.1, 0.5)))
+    yield SampleInput((_t((2, 3), device, dtype, requires_grad), _t((1,), device, dtype, requires_grad, 0.1, 0.5)))
+
+
+def _index_copy_samples(device, dtype, requires_grad):
+    x = _t((5, 3), device, dtype, requires_grad)
+    src = _t((2, 3), device, dtype, requires_grad)
+    yield SampleInput((x, 0, torch.tensor([4, 1], device=device), src))
+    x2 = _t((3, 5), device, dtype, requires_grad)
+    yield SampleInput((x2, 1, torch.tensor([0, 3], device=device), _t((3, 2), device, dtype, requires_grad)))
+
+
+def _multi_dot_samples(device, dtype, requires_grad):
+    yield SampleInput(([_t((3, 4), device, dtype, requires_grad), _t((4, 5), device, dtype, requires_grad),
+                        _t((5, 2), device, dtype, requires_grad)],))
+
+
+OPS += [
+    # activations
+    elementwise_unary("celu", F.celu),
+    OpInfo("celu_alpha", lambda x: F.celu(x, alpha=0.5), unary_samples()),
+    elementwise_unary("selu", F.selu),
+    elementwise_unary("hardshrink", F.hardshrink),
+    elementwise_unary("softshrink", F.softshrink),
+    elementwise_unary("hardsigmoid", F.hardsigmoid, low=-4.0, high=4.0),
+    elementwise_unary("softsign", F.softsign),
+    elementwise_unary("tanhshrink", F.tanhshrink),
+    OpInfo("threshold", lambda x: F.threshold(x, 0.3, -1.0), unary_samples()),
+    OpInfo("glu", F.glu, unary_samples(shapes=[(3, 4), (2, 6)])),
+    OpInfo("glu_dim0", lambda x: F.glu(x, 0), unary_samples(shapes=[(4, 3)])),
+    OpInfo("prelu", F.prelu, _prelu_samples),
+    OpInfo("rrelu_eval", lambda x: F.rrelu(x, training=False), unary_samples()),
+    OpInfo("softmin", lambda x: F.softmin(x, dim=-1), unary_samples(shapes=[(3, 4)])),
+    OpInfo("ldexp", torch.ldexp, lambda d, t, r: iter([SampleInput((_t((3, 4), d, t, r), torch.randint(-2, 3, (3, 4), device=d)))]),
+           dtypes=FLOAT32),
+    # shape utilities
+    OpInfo("atleast_1d", torch.atleast_1d, unary_samples(shapes=[(), (3,), (2, 3)])),
+    OpInfo("atleast_2d", torch.atleast_2d, unary_samples(shapes=[(), (3,), (2, 3)])),
+    OpInfo("atleast_3d", torch.atleast_3d, unary_samples(shapes=[(), (3,), (2, 3), (2, 3, 4)])),
+    OpInfo("diagonal", torch.diagonal, _shape_samples([((4, 4), (), {}), ((3, 5), (1,), {}), ((5, 3), (-2,), {}),
+                                                        ((2, 3, 4), (0, 1, 2), {})])),
+    OpInfo("unfold", lambda x, *a: x.unfold(*a), _shape_samples([((7,), (0, 3, 2), {}), ((2, 8, 3), (1, 4, 1), {})])),
+    OpInfo("index_copy", torch.index_copy, _index_copy_samples),
+    OpInfo("multi_dot", torch.linalg.multi_dot, _multi_dot_samples, atol=1e-2, rtol=1e-2),
+    # convolution
+    OpInfo("conv1d", F.conv1d, _conv_samples(1), atol=2e-2, rtol=2e-2),
+    OpInfo("conv2d", F.conv2d, _conv_samples(2), atol=2e-2, rtol=2e-2),
+    OpInfo("conv3d", F.conv3d, _conv_samples(3), atol=2e-2, rtol=2e-2, dtypes=FLOAT32),
+    # pooling
+    OpInfo("max_pool1d", F.max_pool1d, _pool_samples(1, "max")),
+    OpInfo("max_pool2d", F.max_pool2d, _pool_samples(2, "max")),
+    OpInfo("max_pool3d", F.max_pool3d, _pool_samples(3, "max"), dtypes=FLOAT32),
+    OpInfo("avg_pool1d", F.avg_pool1d, _pool_samples(1, "avg"), atol=1e-2, rtol=1e-2),
+    OpInfo("avg_pool2d", F.avg_pool2d, _pool_samples(2, "avg"), atol=1e-2, rtol=1e-2),
+    OpInfo("avg_pool3d", F.avg_pool3d, _pool_samples(3, "avg"), atol=1e-2, rtol=1e-2, dtypes=FLOAT32),
+    OpInfo("adaptive_avg_pool2d", F.adaptive_avg_pool2d,
+           lambda d, t, r: iter([SampleInput((_t((2, 3, 8, 6), d, t, r), (4, 3))), SampleInput((_t((2, 3, 8, 6), d, t, r), 1))]),
+           atol=1e-2, rtol=1e-2),
+    # normalization
+    OpInfo("batch_norm_train", F.batch_norm, _bn_samples(True), atol=2e-2, rtol=2e-2),
+    OpInfo("batch_norm_eval", F.batch_norm, _bn_samples(False), atol=2e-2, rtol=2e-2),
+    OpInfo("instance_norm", F.instance_norm,
+           lambda d, t, r: iter([SampleInput((_t((2, 3, 6), d, t, r),)),
+                                 SampleInput((_t((2, 3, 4, 4), d, t, r),), {"weight": _t((3,), d, t, r, 0.5, 1.5),
+                                                                           "bias": _t((3,), d, t, r)})]),
+           atol=2e-2, rtol=2e-2),
+    # (ATen's CPU kernels do not run LRN / ldexp-with-int in reduced precision: fp32 reference only)
+    OpInfo("local_response_norm", lambda x: F.local_response_norm(x, 3), unary_samples(shapes=[(2, 5, 4), (2, 4, 3, 3)]),
+           dtypes=FLOAT32),
+    # interpolation
+    OpInfo("interpolate_nearest", F.interpolate, _interp_samples("nearest", 2)),
+    OpInfo("interpolate_bilinear", F.interpolate, _interp_samples("bilinear", 2), atol=2e-2, rtol=2e-2),
+    OpInfo("interpolate_linear", F.interpolate, _interp_samples("linear", 1), atol=2e-2, rtol=2e-2),
+]
+
+OPS_BY_NAME = {o.name: o for o in OPS}
+
+
+# =========================================================================================
+# More coverage of existing ltorch symbols
+# =========================================================================================
+def _bool_pair(device, dtype, requires_grad):
+    yield SampleInput((torch.rand(3, 4, device=device) > 0.5, torch.rand(3, 4, device=device) > 0.3))
+
+
+def _scatter_samples(device, dtype, requires_grad):
+    x = _t((3, 5), device, dtype, requires_grad)
+    idx = torch.tensor([[0, 1, 2], [4, 3, 2], [1, 3, 0]], device=device)  # no duplicates per row
+    yield SampleInput((x, 1, idx, _t((3, 3), device, dtype, requires_grad)))
+
+
+def _index_put_samples(device, dtype, requires_grad):
+    x = _t((5, 3), device, dtype, requires_grad)
+    yield SampleInput((x, (torch.tensor([0, 3], device=device),), _t((2, 3), device, dtype, requires_grad)))
+    yield SampleInput((x, (torch.tensor([1, 1, 4], device=device),), _t((3, 3), device, dtype, requires_grad)),
+                      {"accumulate": True})
+
+
+OPS += [
+    OpInfo("clone", torch.clone, unary_samples()),
+    OpInfo("floor_divide", torch.floor_divide, binary_samples(low=1.0, high=5.0, scalar=False), differentiable=False),
+    OpInfo("clamp_min", lambda x: torch.clamp_min(x, -0.5), unary_samples()),
+    OpInfo("clamp_max", lambda x: torch.clamp_max(x, 0.5), unary_samples()),
+    OpInfo("logical_and", torch.logical_and, _bool_pair, dtypes=(torch.bool,), differentiable=False),
+    OpInfo("logical_or", torch.logical_or, _bool_pair, dtypes=(torch.bool,), differentiable=False),
+    OpInfo("logical_xor", torch.logical_xor, _bool_pair, dtypes=(torch.bool,), differentiable=False),
+    OpInfo("logical_not", lambda a, b: torch.logical_not(a), _bool_pair, dtypes=(torch.bool,), differentiable=False),
+    OpInfo("bitwise_or", torch.bitwise_or, binary_samples(scalar=False), dtypes=INTS, differentiable=False),
+    OpInfo("bitwise_left_shift", torch.bitwise_left_shift, binary_samples(low=0, high=4, scalar=False), dtypes=INTS,
+           differentiable=False),
+    OpInfo("repeat_interleave", lambda x: torch.repeat_interleave(x, 2, 1), unary_samples(shapes=[(3, 4)])),
+    OpInfo("tensor_split", lambda x: torch.tensor_split(x, 3, 1), unary_samples(shapes=[(2, 7)])),
+    OpInfo("unflatten", lambda x: x.unflatten(1, (2, 3)), unary_samples(shapes=[(4, 6)])),
+    OpInfo("select", lambda x: x.select(1, 2), unary_samples(shapes=[(3, 4, 2)])),
+    OpInfo("expand_as", lambda x: x.expand_as(torch.empty(4, 3, 5)), unary_samples(shapes=[(3, 1)])),
+    OpInfo("sort", lambda x: torch.sort(x, 1, descending=True), unary_samples(shapes=[(3, 6)])),
+    OpInfo("argsort", lambda x: torch.argsort(x, -1), unary_samples(shapes=[(3, 6)]), differentiable=False),
+    OpInfo("scatter", torch.scatter, _scatter_samples),
+    OpInfo("index_put", torch.index_put, _index_put_samples),
+    OpInfo("baddbmm", torch.baddbmm, lambda d, t, r: iter([SampleInput((_t((2, 3, 5), d, t, r), _t((2, 3, 4), d, t, r),
+                                                                        _t((2, 4, 5), d, t, r)))]),
+           atol=1e-2, rtol=1e-2),
+    OpInfo("mm", torch.mm, lambda d, t, r: iter([SampleInput((_t((3, 4), d, t, r), _t((4, 5), d, t, r)))]),
+           atol=1e-2, rtol=1e-2),
+    OpInfo("t", lambda x: x.t(), unary_samples(shapes=[(3, 4)])),
+    OpInfo("zeros_like_add", lambda x: torch.zeros_like(x) + x, unary_samples()),
+    OpInfo("full_like_mul", lambda x: torch.full_like(x, 2.5) * x, unary_samples()),
+    OpInfo("isinf", torch.isinf, unary_samples(), differentiable=False),
+    OpInfo("signbit", torch.signbit, unary_samples(), differentiable=False),
+    OpInfo("masked_fill_tensor", lambda x: x.masked_fill(x > 0.5, -1.0), unary_samples()),
+    OpInfo("cumsum_dim0", lambda x: torch.cumsum(x, 0), unary_samples(shapes=[(4, 3)])),
+    OpInfo("logsumexp_dim0", lambda x: torch.logsumexp(x, 0), unary_samples(shapes=[(4, 3)])),
+    OpInfo("amax_keepdim", lambda x: torch.amax(x, (0, 2), keepdim=True), unary_samples(shapes=[(2, 3, 4)])),
+]
+
+OPS_BY_NAME = {o.name: o for o in OPS}
