@@ -12,7 +12,8 @@ import math
 import torch
 
 from ..core.prims import OpTags
-from ..core.proxies import TensorProxy
+from ..core.proxies import TensorProxy, pyval
+from ..core import dtypes
 from ..core.pytree import tree_flatten
 from ..extend import OperatorExecutor, register_executor, add_default_executor
 
@@ -1132,6 +1133,35 @@ hip_attn_bwd = ex.register_operator(
 )
 
 
+# masked / dropout variant (additive or boolean mask, counter-based dropout of P, optional mask
+# gradient): the same kernels with the extra terms compiled in (ops/attention.py: lta_attn_*_ex)
+def _attn_fwd_ex_meta(q, k, v, mask, causal, scale, dropout_p, seed, offset):
+    B, H, L, E = q.shape
+    return TensorProxy(like=q), TensorProxy(like=q, shape=(B, H, L), dtype=torch.float32, requires_grad=False)
+
+
+def _attn_fwd_ex_impl(q, k, v, mask, causal, scale, dropout_p, seed, offset):
+    from ..ops.attention import attn_fwd
+
+    return attn_fwd(q, k, v, causal, scale, mask=mask, dropout_p=dropout_p, seed=seed, offset=offset)
+
+
+def _attn_bwd_ex_meta(g, q, k, v, o, lse, mask, causal, scale, dropout_p, seed, offset, mask_grad):
+    outs = (TensorProxy(like=q), TensorProxy(like=k), TensorProxy(like=v))
+    return outs + ((TensorProxy(like=mask),) if mask_grad else ())
+
+
+def _attn_bwd_ex_impl(g, q, k, v, o, lse, mask, causal, scale, dropout_p, seed, offset, mask_grad):
+    from ..ops.attention import attn_bwd
+
+    return attn_bwd(g, q, k, v, o, lse, causal, scale, mask=mask, dropout_p=dropout_p, seed=seed, offset=offset,
+                    mask_grad=mask_grad)
+
+
+hip_attn_fwd_ex = ex.register_operator("hip_flash_attn_fwd_ex", meta=_attn_fwd_ex_meta, fn=_attn_fwd_ex_impl)
+hip_attn_bwd_ex = ex.register_operator("hip_flash_attn_bwd_ex", meta=_attn_bwd_ex_meta, fn=_attn_bwd_ex_impl)
+
+
 def _decode_attn_meta(q, k, v, mask, causal, scale):
     return TensorProxy(like=q)
 
@@ -1165,12 +1195,25 @@ def _is_decode(query, key, attn_mask) -> bool:
 
 
 def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
-    if dropout_p != 0.0 or not _gpu(query, key, value):
-        return False
-    if attn_mask is not None and not (query.ndim == 4 and _is_decode(query, key, attn_mask)):
+    if not _gpu(query, key, value):
         return False
     if query.ndim != 4 or key.ndim != 4 or value.ndim != 4:
         return False
+    try:
+        p = float(pyval(dropout_p))
+    except Exception:  # a symbolic dropout probability: let the decomposition run
+        return False
+    if not 0.0 <= p < 1.0:
+        return False
+    if attn_mask is not None:
+        if not isinstance(attn_mask, TensorProxy) or attn_mask.device.type != "cuda":
+            return False
+        if attn_mask.dtype != torch.bool and not dtypes.is_float_dtype(attn_mask.dtype):
+            return False
+        if not _broadcastable(tuple(attn_mask.shape), (query.shape[0], query.shape[1], query.shape[2], key.shape[2])):
+            return False
+        if is_causal and attn_mask is not None:
+            return False  # torch rejects the combination as well
     if query.dtype not in (torch.bfloat16, torch.float16) or key.dtype != query.dtype or value.dtype != query.dtype:
         return False
     D = query.shape[-1]
@@ -1187,28 +1230,203 @@ def _sc(q, scale):
     return scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
 
 
+def _p(dropout_p) -> float:
+    return float(pyval(dropout_p))
+
+
+def _rng(query, key, p):
+    """(seed, offset) of the framework's Philox stream, advanced by one draw per score."""
+    if not p:
+        return 0, 0
+    from ..core import prims as P
+
+    B, H, L, _ = query.shape
+    return P.get_rng_seed_offset(B * H * L * key.shape[2])
+
+
 def _sdpa_exec(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
-    if attn_mask is not None:
+    p = _p(dropout_p)
+    if attn_mask is not None and not p and _is_decode(query, key, attn_mask):
         return hip_decode_attn(query, key, value, attn_mask, bool(is_causal), _sc(query, scale))
-    out, _ = hip_attn_fwd(query, key, value, bool(is_causal), _sc(query, scale))
+    if attn_mask is None and not p:
+        out, _ = hip_attn_fwd(query, key, value, bool(is_causal), _sc(query, scale))
+        return out
+    seed, offset = _rng(query, key, p)
+    out, _ = hip_attn_fwd_ex(query, key, value, attn_mask, bool(is_causal), _sc(query, scale), p, seed, offset)
     return out
 
 
 def _sdpa_grad(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, *, scale=None, enable_gqa=False):
-    if attn_mask is not None:
-        return None  # decline: the generic rule differentiates; the forward still runs on K3d
     sc = _sc(query, scale)
-    out, lse = hip_attn_fwd(query, key, value, bool(is_causal), sc)
+    p = _p(dropout_p)
+    if attn_mask is None and not p:
+        out, lse = hip_attn_fwd(query, key, value, bool(is_causal), sc)
+
+        def bwd(g):
+            dq, dk, dv = hip_attn_bwd(g, query, key, value, out, lse, bool(is_causal), sc)
+            return dq, dk, dv
+
+        return out, bwd
+    seed, offset = _rng(query, key, p)
+    out, lse = hip_attn_fwd_ex(query, key, value, attn_mask, bool(is_causal), sc, p, seed, offset)
+    mask_grad = bool(attn_mask is not None and attn_mask.dtype != torch.bool and attn_mask.requires_grad)
 
     def bwd(g):
-        dq, dk, dv = hip_attn_bwd(g, query, key, value, out, lse, bool(is_causal), sc)
-        return dq, dk, dv
+        res = hip_attn_bwd_ex(g, query, key, value, out, lse, attn_mask, bool(is_causal), sc, p, seed, offset, mask_grad)
+        if mask_grad:
+            return res[0], res[1], res[2], res[3]
+        return res[0], res[1], res[2]
 
     return out, bwd
 
 
+# =========================================================================================
+# K11 embedding backward / index_add, K12 topk / sort / cumsum (csrc/index_ops.hip)
+# =========================================================================================
+_SORT_DT = (torch.float32, torch.float16, torch.bfloat16, torch.int32)
+_ROW_DT = (torch.float32, torch.float16, torch.bfloat16)
+_SORT_MAX = 16384
+
+
+def _topk_meta(a, k, dim, largest, sorted):
+    shape = list(a.shape)
+    shape[dim] = k
+    return TensorProxy(like=a, shape=tuple(shape)), TensorProxy(like=a, shape=tuple(shape), dtype=torch.int64,
+                                                                requires_grad=False)
+
+
+def _topk_impl(a, k, dim, largest, sorted):
+    from ..ops import index_ops
+
+    return index_ops.topk(a, k, dim, largest, sorted)
+
+
+def _sort_meta(a, dim, descending, stable):
+    return TensorProxy(like=a), TensorProxy(like=a, dtype=torch.int64, requires_grad=False)
+
+
+def _sort_impl(a, dim, descending, stable):
+    from ..ops import index_ops
+
+    return index_ops.sort(a, dim, descending, stable)
+
+
+def _cumsum_meta(a, dim):
+    return TensorProxy(like=a, dtype=torch.int64 if a.dtype in (torch.int32, torch.int64) else a.dtype)
+
+
+def _cumsum_impl(a, dim):
+    from ..ops import index_ops
+
+    return index_ops.cumsum(a, dim)
+
+
+def _emb_bwd_meta(grad, indices, num_weights, padding_idx, scale_grad_by_freq):
+    return TensorProxy(like=grad, shape=(num_weights, grad.shape[-1]))
+
+
+def _emb_bwd_impl(grad, indices, num_weights, padding_idx, scale_grad_by_freq):
+    from ..ops import index_ops
+
+    return index_ops.embedding_backward(grad, indices, num_weights, padding_idx, scale_grad_by_freq)
+
+
+def _index_add_meta(a, index, src):
+    return TensorProxy(like=a)
+
+
+def _index_add_impl(a, index, src):
+    from ..ops import index_ops
+
+    return index_ops.index_add(a, index, src)
+
+
+hip_topk = ex.register_operator("hip_topk", meta=_topk_meta, fn=_topk_impl)
+hip_sort = ex.register_operator("hip_sort", meta=_sort_meta, fn=_sort_impl)
+hip_cumsum = ex.register_operator("hip_cumsum", meta=_cumsum_meta, fn=_cumsum_impl)
+hip_embedding_backward = ex.register_operator("hip_embedding_backward", meta=_emb_bwd_meta, fn=_emb_bwd_impl)
+hip_index_add = ex.register_operator("hip_index_add", meta=_index_add_meta, fn=_index_add_impl)
+
+
+def _numel(shape) -> int:
+    n = 1
+    for d in shape:
+        n *= int(d)
+    return n
+
+
+def _topk_checker(a, k, dim, largest, sorted):
+    if not (_gpu(a) and a.dtype in _SORT_DT and a.ndim >= 1 and _numel(a.shape) > 0):
+        return False
+    n = a.shape[dim]
+    return 1 <= pyval(k) <= n <= _SORT_MAX
+
+
+def _topk_exec(a, k, dim, largest, sorted):
+    return hip_topk(a, pyval(k), dim, bool(largest), bool(sorted))
+
+
+def _sort_checker(a, dim, descending, stable):
+    if a.dtype == torch.int64:  # 64-bit keys + separate positions: half the LDS capacity
+        return _gpu(a) and a.ndim >= 1 and _numel(a.shape) > 0 and a.shape[dim] <= _SORT_MAX // 2
+    return (_gpu(a) and a.dtype in _SORT_DT and a.ndim >= 1 and _numel(a.shape) > 0
+            and a.shape[dim] <= _SORT_MAX)
+
+
+def _sort_exec(a, dim, descending, stable):
+    return hip_sort(a, dim, bool(descending), bool(stable))
+
+
+def _cumsum_checker(a, dim, *, dtype=None):
+    if not (_gpu(a) and a.ndim >= 1 and 0 < _numel(a.shape) < 2**31):
+        return False
+    if a.dtype in _ROW_DT:
+        return dtype is None or dtype == a.dtype
+    # integer scans produce int64: the prim's output dtype must say so
+    return (a.dtype == torch.int64 and dtype in (None, torch.int64)) or (a.dtype == torch.int32 and dtype == torch.int64)
+
+
+def _cumsum_exec(a, dim, *, dtype=None):
+    return hip_cumsum(a, dim)
+
+
+def _emb_bwd_checker(grad, indices, num_weights, padding_idx, scale_grad_by_freq, sparse):
+    if sparse or not _gpu(grad, indices) or grad.dtype not in _ROW_DT or indices.dtype not in (torch.int32, torch.int64):
+        return False
+    D = grad.shape[-1]
+    return (D % (16 // grad.dtype.itemsize) == 0 and 0 < pyval(num_weights) < 2**31
+            and _numel(indices.shape) * D == _numel(grad.shape))
+
+
+def _emb_bwd_exec(grad, indices, num_weights, padding_idx, scale_grad_by_freq, sparse):
+    pidx = pyval(padding_idx)
+    return hip_embedding_backward(grad, indices, pyval(num_weights), -1 if pidx is None else pidx,
+                                  bool(scale_grad_by_freq))
+
+
+def _index_add_checker(a, indices, value, dim):
+    if not (_gpu(a, indices, value) and a.ndim >= 1 and dim == 0 and a.dtype in _ROW_DT and value.dtype == a.dtype):
+        return False
+    if indices.dtype not in (torch.int32, torch.int64) or indices.ndim > 1 or value.ndim != a.ndim:
+        return False
+    D = _numel(a.shape[1:])
+    return (D > 0 and D % (16 // a.dtype.itemsize) == 0 and tuple(value.shape[1:]) == tuple(a.shape[1:])
+            and value.shape[0] == _numel(indices.shape))
+
+
+def _index_add_exec(a, indices, value, dim):
+    return hip_index_add(a, indices, value)
+
+
 def _register_all():
     from .. import torch as ltorch
+    from ..core import prims as P
+
+    ex.register_implementation(P.topk, checker=_topk_checker, execution_transform=_topk_exec)
+    ex.register_implementation(P.sort, checker=_sort_checker, execution_transform=_sort_exec)
+    ex.register_implementation(P.cumsum, checker=_cumsum_checker, execution_transform=_cumsum_exec)
+    ex.register_implementation(P.embedding_backward, checker=_emb_bwd_checker, execution_transform=_emb_bwd_exec)
+    ex.register_implementation(P.index_add, checker=_index_add_checker, execution_transform=_index_add_exec)
     from ..core.transforms import register_vjp
     from ..models import litgpt
 

@@ -19,7 +19,34 @@ register_signature("lta_attn_bwd_s", [c_int, c_void_p, c_void_p, c_void_p, c_voi
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_float, c_int, c_void_p, c_void_p])
 
+register_signature("lta_attn_fwd_ex", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                       c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p, c_int, c_int, c_float,
+                                       ctypes.c_uint64, ctypes.c_uint64, c_void_p])
+register_signature("lta_attn_bwd_ex", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                       c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
+                                       ctypes.c_uint64, c_void_p])
+
 SUPPORTED_HEAD_DIMS = (64, 128)
+
+
+def prepare_mask(mask: torch.Tensor, B: int, Hq: int, Tq: int, Sk: int):
+    """Additive fp32 image of an SDPA mask for the kernels: ``[Bm, Hm, Tq, Skp]`` (Bm in {1, B},
+    Hm in {1, Hq}, key dim padded to a multiple of 64 with -inf).  A boolean mask (True = attend)
+    becomes 0 / -inf.  Returns (image, mask_b, mask_h)."""
+    m = mask
+    while m.dim() < 4:
+        m = m.unsqueeze(0)
+    mb = m.shape[0] == B and B > 1
+    mh = m.shape[1] == Hq and Hq > 1
+    m = m.expand(B if mb else 1, Hq if mh else 1, Tq, Sk)
+    skp = (Sk + 63) // 64 * 64
+    out = torch.full((m.shape[0], m.shape[1], Tq, skp), float("-inf"), device=m.device, dtype=torch.float32)
+    if m.dtype == torch.bool:
+        out[..., :Sk].masked_fill_(m, 0.0)
+    else:
+        out[..., :Sk].copy_(m)
+    return out, int(mb), int(mh)
 
 
 def supported(q, k, v) -> bool:
@@ -49,7 +76,8 @@ def _rows_ok(t) -> bool:
     return t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
 
 
-def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str = "bshd"):
+def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str = "bshd", mask=None,
+             dropout_p: float = 0.0, seed: int = 0, offset: int = 0):
     """q [B, Hq, T, D], k/v [B, Hkv, S, D] -> (o [B, Hq, T, D], lse [B, Hq, T] fp32).
 
     ``out_layout="bshd"`` (default) stores O as [B, T, Hq, D] and returns its [B, Hq, T, D]
@@ -65,14 +93,22 @@ def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str 
     else:
         o = torch.empty_like(q)
     lse = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
-    rc = lib.lta_attn_fwd_s(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
-                            int(causal), ctypes.cast(_strides3(o), c_void_p), stream_ptr(q.device))
+    if mask is None and not dropout_p:
+        rc = lib.lta_attn_fwd_s(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
+                                int(causal), ctypes.cast(_strides3(o), c_void_p), stream_ptr(q.device))
+    else:
+        mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
+        rc = lib.lta_attn_fwd_ex(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
+                                 int(causal), ctypes.cast(_strides3(o), c_void_p), ptr(mimg), mb, mh, float(dropout_p),
+                                 int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), stream_ptr(q.device))
     check(rc, "lta_attn_fwd")
     return o, lse
 
 
-def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None):
-    """Returns (dq, dk, dv) with dk/dv summed over the query heads of each kv group."""
+def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask=None, dropout_p: float = 0.0,
+             seed: int = 0, offset: int = 0, mask_grad: bool = False):
+    """Returns (dq, dk, dv) with dk/dv summed over the query heads of each kv group; with
+    ``mask_grad`` (a float mask) a 4th result: the mask's gradient, reduced to its shape."""
     lib = require()
     q, k, v = _c(q), _c(k), _c(v)
     do = do if _rows_ok(do) else do.contiguous()
@@ -85,11 +121,33 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None):
     dv = torch.empty_like(v)
     delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
     st = (ctypes.c_int64 * 6)(*do.stride()[:3], *o.stride()[:3])
-    rc = lib.lta_attn_bwd_s(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
-                            ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p),
-                            stream_ptr(q.device))
+    if mask is None and not dropout_p:
+        rc = lib.lta_attn_bwd_s(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq),
+                                ptr(dk), ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal),
+                                ctypes.cast(st, c_void_p), stream_ptr(q.device))
+        check(rc, "lta_attn_bwd")
+        return dq, dk, dv
+    mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
+    dmask = None
+    if mask_grad:
+        assert mask is not None and mask.dtype != torch.bool
+        dmask = torch.empty((B, Hq, T, S), device=q.device, dtype=torch.float32)
+    rc = lib.lta_attn_bwd_ex(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
+                             ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
+                             mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),
+                             int(offset) & (2 ** 64 - 1), stream_ptr(q.device))
     check(rc, "lta_attn_bwd")
-    return dq, dk, dv
+    if not mask_grad:
+        return dq, dk, dv
+    # the mask broadcasts over some dims: its gradient is dS summed over them
+    g = dmask
+    shape = tuple(mask.shape)
+    lead = g.dim() - len(shape)
+    g = g.sum(tuple(range(lead))) if lead else g
+    dims = tuple(i for i, n in enumerate(shape) if n == 1 and g.shape[i] != 1)
+    if dims:
+        g = g.sum(dims, keepdim=True)
+    return dq, dk, dv, g.to(mask.dtype)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -67,5 +67,39 @@ __device__ __forceinline__ void pack_frag(f16x8& f, const f32x16& x, int s) {
 
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// ---------------------------------------------------------------------------------------------
+// Attention masks and dropout (reference: cuDNN SDPA additive / boolean masks + dropout seed and
+// offset, thunder/executors/cudnn_sdpa.py; aten flash dropout, sdpaex.py:274-336).
+// EX bit flags of a kernel instantiation (compile-time: the plain causal path carries no cost):
+enum : int { kExMask = 1, kExDrop = 2, kExMaskGrad = 4 };
+
+struct AttnExtra {
+  const float* mask;      // additive mask (natural-log domain), fp32 [Bm][Hm][Tq][Skp], key dim padded to 64
+  int64_t mb, mh, mq;     // element strides (0 for a broadcast batch / head)
+  float* dmask;           // kExMaskGrad: dS written as fp32 [B][Hq][Tq][Sk] (reduced over broadcast dims by the host)
+  float keep_scale;       // 1 / (1 - p)
+  unsigned keep_thresh;   // keep iff hash >= p * 2^32
+  unsigned seed_lo, seed_hi, offset;
+};
+
+// Counter-based dropout mask: a pure function of (seed, offset, query head, query, key), so the
+// forward and both backward kernels regenerate the same keep bit in any iteration order.
+__device__ __forceinline__ unsigned fmix32(unsigned h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ unsigned rng_head(const AttnExtra& e, int bh) {
+  return fmix32((unsigned)bh * 0x9e3779b9u ^ fmix32(e.seed_lo ^ (e.offset * 0x27d4eb2fu)) ^ e.seed_hi);
+}
+__device__ __forceinline__ unsigned rng_q(unsigned head, int q) { return fmix32((unsigned)q * 0x61c88647u + head); }
+__device__ __forceinline__ unsigned rng_k(int k) { return fmix32((unsigned)k * 0x7feb352du + 0x3c6ef372u); }
+__device__ __forceinline__ bool rng_keep(const AttnExtra& e, unsigned qterm, unsigned kterm) {
+  return fmix32(qterm ^ kterm) >= e.keep_thresh;
+}
+
 }  // namespace attn
 }  // namespace lta

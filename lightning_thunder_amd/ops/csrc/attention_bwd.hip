@@ -68,13 +68,15 @@ __global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__
 constexpr int kKB = 128;  // keys per workgroup
 constexpr int kQT = 32;   // queries per inner tile
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EX = 0>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                     const T* __restrict__ V, const T* __restrict__ dO,
                                                                     const float* __restrict__ LSE,
                                                                     const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                     T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                    float scale, float scale_log2, RowStrides sdo) {
+                                                                    float scale, float scale_log2, RowStrides sdo,
+                                                                    AttnExtra ex) {
+  constexpr bool MASK = EX & kExMask, DROP = EX & kExDrop, MGRAD = EX & kExMaskGrad;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
   // Double-buffered Q / dO tiles: the global loads of tile i+1 are issued before the MFMAs of
@@ -204,14 +206,34 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       pacc = mfma(oa, vf[s], pacc);  // dP = dO V^T
     }
     // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
+    [[maybe_unused]] const int hq_it = hk * group + it / nq;
+    [[maybe_unused]] unsigned head_rng = 0, kterm = 0;
+    if constexpr (DROP) {
+      head_rng = rng_head(ex, b * Hq + hq_it);
+      kterm = rng_k(key);
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qr = acc_row(i, h);
       const int qq = qbase + qr;
-      float p = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - sl[qr]);
+      float sv = sacc[i] * scale_log2;
+      if constexpr (MASK)
+        sv += ex.mask[b * ex.mb + hq_it * ex.mh + (int64_t)min(qq, Tq - 1) * ex.mq + min(key, Sk - 1)] *
+              1.44269504088896340736f;
+      float p = __builtin_amdgcn_exp2f(sv - sl[qr]);
       p = (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) ? 0.f : p;
-      sacc[i] = p;                           // P
-      pacc[i] = p * (pacc[i] - sd[qr]);      // dS
+      float dp = pacc[i];
+      float pd = p;
+      if constexpr (DROP) {  // dropped P feeds dV; dS = P (dP_dropped * keep / (1-p) - delta)
+        const bool keep = rng_keep(ex, rng_q(head_rng, qq), kterm);
+        pd = keep ? p * ex.keep_scale : 0.f;
+        dp = keep ? dp * ex.keep_scale : 0.f;
+      }
+      sacc[i] = pd;                          // P (after dropout)
+      pacc[i] = p * (dp - sd[qr]);           // dS
+      if constexpr (MGRAD) {
+        if (key < Sk && qq < Tq) ex.dmask[(((int64_t)b * Hq + hq_it) * Tq + qq) * Sk + key] = pacc[i];
+      }
     }
     F pf0, pf1, df0, df1;
     pack_frag(pf0, sacc, 0);
@@ -603,13 +625,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
 constexpr int kBM = 128;
 constexpr int kBN = 64;
 
-template <typename T, int D, bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+template <typename T, int D, bool CAUSAL, int EX = 0>
+__global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                   const T* __restrict__ V, const T* __restrict__ dO,
                                                                   const float* __restrict__ LSE,
                                                                   const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                   int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                  float scale_log2, RowStrides sdo) {
+                                                                  float scale_log2, RowStrides sdo, AttnExtra ex) {
+  constexpr bool MASK = EX & kExMask, DROP = EX & kExDrop;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[2 * kBN * C::RSTR + kBN * C::TSTR];
@@ -643,6 +666,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   }
   const float lse2 = LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
   const float dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
+  const float* mrow = nullptr;
+  if constexpr (MASK) mrow = ex.mask + b * ex.mb + hq * ex.mh + (int64_t)qrow * ex.mq;
+  unsigned qterm = 0;
+  if constexpr (DROP) qterm = rng_q(rng_head(ex, bh), qi);
 
   f32x16 dqacc[C::DT];
 #pragma unroll
@@ -704,14 +731,31 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
       }
     }
     const int kbase = t * kBN;
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 mv = *reinterpret_cast<const float4*>(mrow + kbase + kt * 32 + 8 * j + 4 * h);
+          sacc[kt][4 * j + 0] = sacc[kt][4 * j + 0] * scale_log2 + mv.x * 1.44269504088896340736f;
+          sacc[kt][4 * j + 1] = sacc[kt][4 * j + 1] * scale_log2 + mv.y * 1.44269504088896340736f;
+          sacc[kt][4 * j + 2] = sacc[kt][4 * j + 2] * scale_log2 + mv.z * 1.44269504088896340736f;
+          sacc[kt][4 * j + 3] = sacc[kt][4 * j + 3] * scale_log2 + mv.w * 1.44269504088896340736f;
+        }
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kbase + kt * 32 + acc_row(i, h);
-        float p = __builtin_amdgcn_exp2f(sacc[kt][i] * scale_log2 - lse2);
+        float p = __builtin_amdgcn_exp2f((MASK ? sacc[kt][i] : sacc[kt][i] * scale_log2) - lse2);
         p = (kk >= Sk || (CAUSAL && kk > qi)) ? 0.f : p;
-        pacc[kt][i] = p * (pacc[kt][i] - dlt);  // dS^T
+        float dp = pacc[kt][i];
+        if constexpr (DROP) {
+          const bool keep = rng_keep(ex, qterm, rng_k(kk));
+          dp = keep ? dp * ex.keep_scale : 0.f;
+        }
+        pacc[kt][i] = p * (dp - dlt);  // dS^T
       }
     }
     F df[2][2];
@@ -753,14 +797,55 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const T* __res
   }
 }
 
+template <typename T, int D, int EX>
+void launch_masked(const void* dO, const void* Q, const void* K, const void* V, const void* LSE, void* DELTA, void* dQ,
+                   void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, float sl2, int causal,
+                   RowStrides sdo, const AttnExtra& ex, hipStream_t s) {
+  dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
+  constexpr int EXQ = EX & (kExMask | kExDrop);
+#define LTA_DKDV(CA)                                                                                               \
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, CA, EX>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,   \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
+                     sdo, ex)
+#define LTA_DQ(CA)                                                                                                 \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, CA, EXQ>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,    \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex)
+  if (causal) {
+    LTA_DKDV(true);
+    LTA_DQ(true);
+  } else {
+    LTA_DKDV(false);
+    LTA_DQ(false);
+  }
+#undef LTA_DKDV
+#undef LTA_DQ
+}
+
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
                void* dQ, void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, int causal,
-               RowStrides sdo, RowStrides so, int dkdv_v2, hipStream_t s) {
+               RowStrides sdo, RowStrides so, int dkdv_v2, const AttnExtra& ex, int exf, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
+  if (exf) {  // masks / dropout: the plain-HIP dK/dV kernel with the extra terms compiled in
+    switch (exf) {
+#define LTA_M(F)                                                                                                  \
+  case F:                                                                                                         \
+    launch_masked<T, D, F>(dO, Q, K, V, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, sl2, causal, sdo, ex, s); \
+    break;
+      LTA_M(kExMask)
+      LTA_M(kExDrop)
+      LTA_M(kExMask | kExDrop)
+      LTA_M(kExMask | kExMaskGrad)
+      LTA_M(kExMask | kExDrop | kExMaskGrad)
+#undef LTA_M
+      default:
+        return -1;
+    }
+    return (int)hipGetLastError();
+  }
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
   if (D == 128 && dkdv_v2) {
     if (causal)
@@ -774,18 +859,18 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   } else if (causal) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
-                       sdo);
+                       sdo, ex);
   }
   if (causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
   } else {
     if (!(D == 128 && dkdv_v2))
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo);
+                         sl2, sdo, ex);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
   }
   return (int)hipGetLastError();
 }
@@ -793,12 +878,15 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
 }  // namespace
 
 // strides: optional int64[6] = dO (batch, head, token), O (batch, head, token) element strides
-// (head dim contiguous); null = contiguous [B,H,T,D] for both.
-LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
-                              const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, void* workspace, int B, int Hq,
-                              int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
-                              hipStream_t stream) {
-  if (Hq % Hkv != 0) return -2;
+// (head dim contiguous); null = contiguous [B,H,T,D] for both.  mask / dropout as lta_attn_fwd_ex;
+// dmask (optional, needs mask): fp32 [B][Hq][Tq][Sk] receives dS, the additive mask's gradient
+// before the reduction over its broadcast dims.
+LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                               const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
+                               int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
+                               int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
+                               hipStream_t stream) {
+  if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f || (dmask && !mask)) return -2;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
   const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
@@ -806,8 +894,31 @@ LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const vo
     const char* e = getenv("LTA_ATTN_BWD_V1");  // A/B switch: the v1 dK/dV kernel
     return (e && e[0] == '1') ? 0 : 1;
   }();
-#define LTA_B(TT, DD) \
-  return launch_bwd<TT, DD>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, v2, stream)
+  AttnExtra ex{};
+  int exf = 0;
+  if (mask) {
+    const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
+    ex.mask = (const float*)mask;
+    ex.mq = skp;
+    ex.mh = mask_h ? (int64_t)Tq * skp : 0;
+    ex.mb = mask_b ? (int64_t)(mask_h ? Hq : 1) * Tq * skp : 0;
+    exf |= kExMask;
+    if (dmask) {
+      ex.dmask = (float*)dmask;
+      exf |= kExMaskGrad;
+    }
+  }
+  if (dropout_p > 0.f) {
+    ex.keep_scale = 1.f / (1.f - dropout_p);
+    ex.keep_thresh = (unsigned)fmin((double)dropout_p * 4294967296.0, 4294967295.0);
+    ex.seed_lo = (unsigned)seed;
+    ex.seed_hi = (unsigned)(seed >> 32);
+    ex.offset = (unsigned)offset;
+    exf |= kExDrop;
+  }
+#define LTA_B(TT, DD)                                                                                             \
+  return launch_bwd<TT, DD>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, v2, ex, \
+                            exf, stream)
   if (dtype == kBF16) {
     if (D == 128) LTA_B(__hip_bfloat16, 128);
     if (D == 64) LTA_B(__hip_bfloat16, 64);
@@ -817,6 +928,14 @@ LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const vo
   }
 #undef LTA_B
   return -1;
+}
+
+LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                              const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, void* workspace, int B, int Hq,
+                              int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
+                              hipStream_t stream) {
+  return lta_attn_bwd_ex(dtype, dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, D, scale, causal, strides,
+                         nullptr, 0, 0, nullptr, 0.f, 0, 0, stream);
 }
 
 LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,

@@ -34,12 +34,13 @@ template <int D> struct Cfg {
   static constexpr int DT = D / 32;                // 32-wide d tiles
 };
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EX = 0>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                const T* __restrict__ V, T* __restrict__ O,
                                                                float* __restrict__ LSE, int Hq, int Hkv, int Tq,
                                                                int Sk, float scale_log2, int64_t so_b, int64_t so_h,
-                                                               int64_t so_t) {
+                                                               int64_t so_t, AttnExtra ex) {
+  constexpr bool MASK = EX & kExMask, DROP = EX & kExDrop;
   using C = Cfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[kBN * C::KSTR + kBN * C::VSTR];
@@ -64,6 +65,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int q0 = qt * kBM + wave * 32;
   const int qi = q0 + r;  // this lane's query
+  const float* mrow = nullptr;
+  if constexpr (MASK) mrow = ex.mask + b * ex.mb + hq * ex.mh + (int64_t)min(qi, Tq - 1) * ex.mq;
+  unsigned qterm = 0;
+  if constexpr (DROP) qterm = rng_q(rng_head(ex, bh), qi);
 
   // Q fragments (B operand of S^T = K Q^T): Q[qi][16s + 8h .. +7]
   F qf[C::KS];
@@ -135,11 +140,23 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     const int kbase = t * kBN;
     const bool need_mask = (kbase + kBN > Sk) || (CAUSAL && kbase + kBN - 1 > q0);
     float mx = -INFINITY;
+    if constexpr (MASK) {  // additive mask, 4 consecutive keys per 16-B load (key dim padded to 64)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 mv = *reinterpret_cast<const float4*>(mrow + kbase + kt * 32 + 8 * j + 4 * h);
+          sacc[kt][4 * j + 0] = sacc[kt][4 * j + 0] * scale_log2 + mv.x * 1.44269504088896340736f;
+          sacc[kt][4 * j + 1] = sacc[kt][4 * j + 1] * scale_log2 + mv.y * 1.44269504088896340736f;
+          sacc[kt][4 * j + 2] = sacc[kt][4 * j + 2] * scale_log2 + mv.z * 1.44269504088896340736f;
+          sacc[kt][4 * j + 3] = sacc[kt][4 * j + 3] * scale_log2 + mv.w * 1.44269504088896340736f;
+        }
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float v = sacc[kt][i] * scale_log2;
+        float v = MASK ? sacc[kt][i] : sacc[kt][i] * scale_log2;
         if (need_mask) {  // wave-uniform branch; per-element select
           const int key = kbase + kt * 32 + acc_row(i, h);
           v = (key >= Sk || (CAUSAL && key > qi)) ? -INFINITY : v;
@@ -165,6 +182,15 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
     m = m_new;
+    if constexpr (DROP) {  // the normalizer keeps every probability; only P.V sees the dropped ones
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bool keep = rng_keep(ex, qterm, rng_k(kbase + kt * 32 + acc_row(i, h)));
+          sacc[kt][i] = keep ? sacc[kt][i] * ex.keep_scale : 0.f;
+        }
+    }
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -216,37 +242,78 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   }
 }
 
-template <typename T, int D>
-int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
-           float scale, int causal, const int64_t* so, hipStream_t s) {
+template <typename T, int D, int EX>
+int launch_ex(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
+              float scale, int causal, const int64_t* so, const AttnExtra& ex, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   dim3 grid(B * Hq, (Tq + kBM - 1) / kBM), block(kThreads);
   const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * D, sh = so ? so[1] : (int64_t)Tq * D, st = so ? so[2] : D;
   if (causal)
-    hipLaunchKernelGGL((attn_fwd_kernel<T, D, true>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
-                       (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, D, true, EX>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v,
+                       (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st, ex);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<T, D, false>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o,
-                       (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, D, false, EX>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v,
+                       (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, sl2, sb, sh, st, ex);
   return (int)hipGetLastError();
+}
+
+template <typename T, int D>
+int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
+           float scale, int causal, const int64_t* so, const AttnExtra& ex, int exf, hipStream_t s) {
+  switch (exf) {
+    case 0: return launch_ex<T, D, 0>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, so, ex, s);
+    case kExMask: return launch_ex<T, D, kExMask>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, so, ex, s);
+    case kExDrop: return launch_ex<T, D, kExDrop>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, so, ex, s);
+    case kExMask | kExDrop:
+      return launch_ex<T, D, kExMask | kExDrop>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, so, ex, s);
+  }
+  return -1;
 }
 
 }  // namespace
 
 // o_strides: optional int64[3] (batch, head, token) element strides of O (head dim contiguous);
 // null = contiguous [B,H,T,D].  [B,T,H,D] storage lets the output projection read O without a copy.
+// mask: optional fp32 additive mask [Bm][Hm][Tq][Skp] (Bm in {1,B}, Hm in {1,Hq}, Skp = Sk rounded up
+// to 64, padding -inf); dropout_p > 0: counter-based dropout of P (seed, offset: the generator state).
+LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                               int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
+                               const void* mask, int mask_b, int mask_h, float dropout_p, uint64_t seed,
+                               uint64_t offset, hipStream_t stream) {
+  if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f) return -2;
+  AttnExtra ex{};
+  int exf = 0;
+  if (mask) {
+    const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
+    ex.mask = (const float*)mask;
+    ex.mq = skp;
+    ex.mh = mask_h ? (int64_t)Tq * skp : 0;
+    ex.mb = mask_b ? (int64_t)(mask_h ? Hq : 1) * Tq * skp : 0;
+    exf |= kExMask;
+  }
+  if (dropout_p > 0.f) {
+    ex.keep_scale = 1.f / (1.f - dropout_p);
+    ex.keep_thresh = (unsigned)fmin((double)dropout_p * 4294967296.0, 4294967295.0);
+    ex.seed_lo = (unsigned)seed;
+    ex.seed_hi = (unsigned)(seed >> 32);
+    ex.offset = (unsigned)offset;
+    exf |= kExDrop;
+  }
+  if (dtype == kBF16) {
+    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+  } else if (dtype == kF16) {
+    if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+    if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+  }
+  return -1;
+}
+
 LTA_EXPORT int lta_attn_fwd_s(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
                               int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
                               hipStream_t stream) {
-  if (Hq % Hkv != 0) return -2;
-  if (dtype == kBF16) {
-    if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
-    if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
-  } else if (dtype == kF16) {
-    if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
-    if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, stream);
-  }
-  return -1;
+  return lta_attn_fwd_ex(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, nullptr, 0, 0, 0.f,
+                         0, 0, stream);
 }
 
 LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,

@@ -42,6 +42,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -80,9 +81,18 @@ __device__ __forceinline__ int tr_swz(int k) { return ((k & 3) | (((k >> 3) & 1)
 // Per-lane LDS-DMA source of one operand (buffer_load ... lds through a buffer resource, so the
 // per-lane part is ONE 32-bit VGPR offset and the per-instruction / per-K-tile parts are scalar
 // soffsets).  Instruction i (0..7) of wave w fills LDS bytes [(4i + w) KiB, +1 KiB) of the image.
+// Issued as inline asm: hipcc cannot prove that the transposed fragment reads (ds_read_b64_tr_b16)
+// miss the DMA's destination and puts an s_waitcnt vmcnt(0) in front of EVERY one of them,
+// draining the prefetch (measured: MN-major layouts at 1/3 of the K-major rate).  Completion of
+// the DMA is therefore tracked only by the explicit vmcnt waits of the main loop and epilogue.
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), bytes, 0x00020000};
+}
+
 template <bool MN>
 struct Stager {
-  __amdgpu_buffer_rsrc_t rsrc;
+  i32x4 rsrc;
   int voff0, voff1;      // K-major: voff0 for every i; MN-major: even / odd i
   int istride, kstride;  // bytes between consecutive i / consecutive K-tiles
   // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length
@@ -91,7 +101,7 @@ struct Stager {
       // 8 rows of 128 B per instruction: lane -> row 8(4i + w) + (lane >> 3), stored chunk lane & 7,
       // which holds logical chunk (lane & 7) ^ row & 7
       const __hip_bfloat16* base = X + (int64_t)r0 * ld;
-      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (BM - 1) * ld * 2 + K * 2, 0x00020000);
+      rsrc = make_rsrc(base, (BM - 1) * ld * 2 + K * 2);
       const int r = lane >> 3, c = (lane & 7) ^ r;
       voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
       voff1 = voff0;
@@ -101,7 +111,7 @@ struct Stager {
       // 2 k-rows of 512 B per instruction: lane -> k-row 2(4i + w) + (lane >> 5), stored chunk
       // lane & 31 holding logical chunk (lane & 31) ^ tr_swz(k-row); tr_swz flips bit 3 with i & 1
       const __hip_bfloat16* base = X + r0;
-      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (K - 1) * ld * 2 + BM * 2, 0x00020000);
+      rsrc = make_rsrc(base, (K - 1) * ld * 2 + BM * 2);
       const int half = lane >> 5, slot = lane & 31;
       const int kr = 2 * wave + half;  // k-row for i = 0
       const int c0 = slot ^ tr_swz(kr);
@@ -112,8 +122,11 @@ struct Stager {
     }
   }
   __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(img + (i * 4 + wave) * 1024), 16,
-                                             (MN && (i & 1)) ? voff1 : voff0, i * istride + kt * kstride, 0, 0);
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(dst), "v"((MN && (i & 1)) ? voff1 : voff0), "s"(rsrc), "s"(i * istride + kt * kstride)
+                 : "memory", "m0");
   }
 };
 
@@ -274,6 +287,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
 #pragma unroll
     for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  // the last K-tile's (dummy) prefetch of every wave must have landed before any wave overwrites
+  // the stage buffers with its output image
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   // ---- epilogue: every wave has passed the last barrier after its final LDS read, so the stage
   // buffers are free: registers -> swizzled bf16 image (per wave 128 x 128, 256-B rows) -> stores

@@ -284,11 +284,13 @@ def last_gemm_backend_counts(reset: bool = False) -> dict:
 def gemm4_variant(at: int, bt: int, M: int, N: int, K: int) -> int:
     """Static, deterministic kernel-variant table (no run-time timing: every process runs the same
     kernels, so numerics never depend on a benchmark's noise).  Variant = the LDS-DMA split of
-    csrc/gemm4.hip; 0 everywhere unless a measured row below says otherwise."""
-    return _GEMM4_VARIANTS.get((at, bt, N, K), _GEMM4_VARIANTS.get((at, bt), 0))
+    csrc/gemm4.hip (how many of a K-tile's 16 LDS-DMA loads issue in the second half of the previous
+    tile).  Variant 1 (8 / 8) is the fastest or within 1 % of it on all 18 Llama-2-7B training GEMMs
+    in profiles/gemm4_microbench.json; a measured row below overrides it for one shape."""
+    return _GEMM4_VARIANTS.get((at, bt, N, K), _GEMM4_VARIANTS.get((at, bt), 1))
 
 
-# (at, bt[, N, K]) -> variant, from profiles/gemm4_microbench.json
+# (at, bt[, N, K]) -> variant (profiles/gemm4_microbench.json)
 _GEMM4_VARIANTS: dict = {}
 
 

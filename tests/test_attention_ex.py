@@ -1,0 +1,167 @@
+"""Flash attention with masks, dropout and the mask gradient on the HIP kernels (VERDICT r2 item 3;
+reference: cuDNN SDPA masks + dropout, thunder/executors/cudnn_sdpa.py; aten flash dropout,
+thunder/executors/sdpaex.py:274-336).
+
+Numerics are compared against an fp32 PyTorch reference of the same op.  For dropout the reference
+regenerates the kernels' keep mask from the same counter-based hash (mirrored below in int64 torch
+arithmetic), so forward AND gradients are checked exactly, not statistically.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h & M32
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & M32
+    h = h ^ (h >> 16)
+    return h
+
+
+def keep_mask(seed, offset, B, H, T, S, p, device):
+    """Mirror of attention.h rng_head / rng_q / rng_k / rng_keep."""
+    lo, hi = seed & M32, (seed >> 32) & M32
+    base = _fmix32(torch.tensor(lo ^ ((offset * 0x27D4EB2F) & M32), dtype=torch.int64, device=device)) ^ hi
+    bh = torch.arange(B * H, dtype=torch.int64, device=device)
+    head = _fmix32(((bh * 0x9E3779B9) & M32) ^ base)  # [BH]
+    q = torch.arange(T, dtype=torch.int64, device=device)
+    k = torch.arange(S, dtype=torch.int64, device=device)
+    qterm = _fmix32(((q[None, :] * 0x61C88647) & M32) + head[:, None])  # [BH, T]
+    kterm = _fmix32(((k * 0x7FEB352D) & M32) + 0x3C6EF372)  # [S]
+    h = _fmix32(qterm[:, :, None] ^ kterm[None, None, :])
+    p32 = float(torch.tensor(p, dtype=torch.float32))  # the kernels receive p as fp32
+    thresh = min(int(p32 * 4294967296.0), 4294967295)
+    return (h >= thresh).reshape(B, H, T, S)
+
+
+def ref_attn(q, k, v, mask=None, causal=False, keep=None, p=0.0, scale=None):
+    D = q.shape[-1]
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    Hq, Hkv = q.shape[1], k.shape[1]
+    if Hq != Hkv:
+        k = k.repeat_interleave(Hq // Hkv, 1)
+        v = v.repeat_interleave(Hq // Hkv, 1)
+    s = (q.float() @ k.float().transpose(-1, -2)) * sc
+    if mask is not None:
+        s = s + (torch.where(mask, 0.0, float("-inf")) if mask.dtype == torch.bool else mask.float())
+    if causal:
+        T, S = s.shape[-2:]
+        s = s.masked_fill(torch.ones(T, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    pm = torch.softmax(s, -1)
+    if keep is not None:
+        pm = pm * keep / (1.0 - p)
+    return pm @ v.float()
+
+
+def _qkv(B, Hq, Hkv, T, S, D, dtype=torch.bfloat16):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q = torch.randn(B, Hq, T, D, device="cuda", dtype=dtype, generator=g)
+    k = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype, generator=g)
+    v = torch.randn(B, Hkv, S, D, device="cuda", dtype=dtype, generator=g)
+    return q, k, v
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("kind", ["bool_padding", "float_bias", "bool_full"])
+@pytest.mark.parametrize("D", [64, 128])
+def test_masked_attention_fwd_bwd(kind, D):
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+    B, Hq, Hkv, T, S = 2, 4, 2, 200, 200  # ragged: neither length a multiple of the tiles
+    q, k, v = _qkv(B, Hq, Hkv, T, S, D)
+    if kind == "bool_padding":
+        mask = torch.ones(B, 1, 1, S, dtype=torch.bool, device="cuda")
+        mask[1, ..., 150:] = False
+    elif kind == "float_bias":
+        mask = torch.randn(1, Hq, T, S, device="cuda") * 2.0
+    else:
+        mask = torch.rand(B, Hq, T, S, device="cuda") > 0.3
+        mask[..., 0] = True  # no fully masked row
+    o, lse = attn_fwd(q, k, v, False, mask=mask, out_layout="bhsd")
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = ref_attn(qr, kr, vr, mask=mask)
+    assert _rel(o, ref) < 1e-2, _rel(o, ref)
+    do = torch.randn_like(o)
+    dq, dk, dv = attn_bwd(do, q, k, v, o, lse, False, mask=mask)
+    ref.backward(do.float())
+    for got, want in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
+        assert _rel(got, want) < 2e-2, _rel(got, want)
+
+
+def test_mask_gradient():
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+    B, Hq, Hkv, T, S, D = 2, 4, 4, 128, 192, 64
+    q, k, v = _qkv(B, Hq, Hkv, T, S, D)
+    bias = (torch.randn(1, Hq, T, S, device="cuda") * 0.5).requires_grad_(True)
+    o, lse = attn_fwd(q, k, v, False, mask=bias.detach(), out_layout="bhsd")
+    do = torch.randn_like(o)
+    dq, dk, dv, dmask = attn_bwd(do, q, k, v, o, lse, False, mask=bias.detach(), mask_grad=True)
+    ref = ref_attn(q.float(), k.float(), v.float(), mask=bias)
+    ref.backward(do.float())
+    assert dmask.shape == bias.shape
+    assert _rel(dmask, bias.grad) < 2e-2, _rel(dmask, bias.grad)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_dropout_matches_regenerated_mask(causal):
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+    B, Hq, Hkv, T, S, D, p = 1, 4, 2, 256, 256, 128, 0.2
+    seed, offset = 1234567890123, 4096
+    q, k, v = _qkv(B, Hq, Hkv, T, S, D)
+    o, lse = attn_fwd(q, k, v, causal, dropout_p=p, seed=seed, offset=offset, out_layout="bhsd")
+    o2, _ = attn_fwd(q, k, v, causal, dropout_p=p, seed=seed, offset=offset, out_layout="bhsd")
+    assert torch.equal(o, o2)  # deterministic in (seed, offset)
+    keep = keep_mask(seed, offset, B, Hq, T, S, p, "cuda")
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = ref_attn(qr, kr, vr, causal=causal, keep=keep, p=p)
+    assert _rel(o, ref) < 1e-2, _rel(o, ref)
+    do = torch.randn_like(o)
+    dq, dk, dv = attn_bwd(do, q, k, v, o, lse, causal, dropout_p=p, seed=seed, offset=offset)
+    ref.backward(do.float())
+    for got, want in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
+        assert _rel(got, want) < 2e-2, _rel(got, want)
+
+
+def test_sdpa_with_mask_and_dropout_claimed_by_hipex():
+    """Through the compiler: masked and dropout SDPA are claimed by the HIP executor (no ATen
+    fallback), and a padded-mask training step matches eager."""
+    import lightning_thunder_amd as thunder
+
+    B, H, T, D = 2, 4, 128, 64
+    q, k, v = (t.requires_grad_(True) for t in _qkv(B, H, H, T, T, D))
+    mask = torch.ones(B, 1, 1, T, dtype=torch.bool, device="cuda")
+    mask[0, ..., 100:] = False
+
+    def f(q, k, v):
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+
+    jf = thunder.jit(f)
+    out = jf(q, k, v)
+    ref = f(q.float(), k.float(), v.float())
+    assert _rel(out, ref) < 1e-2
+    out.sum().backward()
+    assert "hip_flash_attn_fwd_ex" in str(thunder.last_traces(jf)[-1])
+    assert "hip_flash_attn_bwd_ex" in str(thunder.last_backward_traces(jf)[-1])
+
+    def g(q, k, v):
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, dropout_p=0.1, is_causal=True)
+
+    jg = thunder.jit(g)
+    y = jg(q, k, v)
+    y.float().pow(2).mean().backward()
+    assert torch.isfinite(y).all()
+    assert "hip_flash_attn_fwd_ex" in str(thunder.last_traces(jg)[-1])

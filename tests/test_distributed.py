@@ -98,6 +98,7 @@ def _worker(rank, port, mode, out_dir):
         torch.save({"grads": grads, "shapes": shapes, "bw": bw, "fw": fw, "out": out.detach()},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

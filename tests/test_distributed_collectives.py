@@ -73,6 +73,7 @@ def _collectives_worker(rank, port, out_dir):
         }
         torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -103,6 +104,7 @@ def _nosync_worker(rank, port, out_dir):
         torch.save({"grads": grads, "bw_nosync": bw_nosync, "bw_sync": bw_sync},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -126,6 +128,7 @@ def _fsdp_nosync_worker(rank, port, out_dir):
         torch.save({"grads": grads, "bw_nosync": bw_nosync, "bw_sync": bw_sync, "stashed": stashed, "left": left},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

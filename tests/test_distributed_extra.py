@@ -56,6 +56,7 @@ def _ckpt_worker(rank, world, port, d, make=None):
         torch.save({"diff": diff, "full_err": full_err, "local_rows": local_rows, "full_keys": sorted(full), "full_shapes": {k: tuple(v.shape) for k, v in full.items()}},
                    os.path.join(d, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -103,6 +104,7 @@ def _hybrid_worker(rank, world, port, d, coalesced=False):
         bw = str(thunder.last_backward_traces(tm)[-1])
         torch.save({"grads": grads, "bw": bw}, os.path.join(d, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -162,6 +164,7 @@ def _sd_worker(rank, world, port, d):
         torch.save({"full_err": full_err, "shapes_ok": shapes_ok, "changed": (y2 - y0).abs().max().item(),
                     "restored": (y3 - y0).abs().max().item(), "bad_shape": bad_shape}, os.path.join(d, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

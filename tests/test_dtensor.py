@@ -70,6 +70,7 @@ def _worker(rank, world, port, d):
             torch.allclose(pm[i].weight.grad.full_tensor(), ref[i].weight.grad, atol=1e-5) for i in (0, 2))
         torch.save(res, os.path.join(d, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

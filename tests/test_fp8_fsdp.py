@@ -42,7 +42,7 @@ def _run_steps(tm, params, data_fn, parts=1):
     # loss = sum over the `parts` row blocks of each block's mean: every block's dy (and so its
     # amax) is the one a rank sees in the distributed run
     for step in range(STEPS):
-        for p in params:
+        for _, p in params:
             p.grad = None
         out = tm(data_fn(step))
         out.float().pow(2).reshape(parts, TOK, -1).mean((1, 2)).sum().backward()
@@ -70,6 +70,7 @@ def _worker(rank, port, out_dir):
         torch.save({"grads": grads, "hist": st.hist.cpu(), "updates": st.updates, "fw": fw},
                    os.path.join(out_dir, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

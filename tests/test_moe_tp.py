@@ -134,6 +134,7 @@ def _worker(rank, world, port, d):
             for n in names)
         torch.save(res, os.path.join(d, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 

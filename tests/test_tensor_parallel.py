@@ -79,6 +79,7 @@ def _worker(rank, port, mode, out_dir):
         res["n_sync_bw"] = sum(1 for b in bw.bound_symbols if "dist_" in b.sym.name)
         torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -156,6 +157,7 @@ def _litgpt_worker(rank, port, out_dir):
         res["grad"] = gmax
         torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
@@ -235,6 +237,7 @@ def _megatron_llama_worker(rank, port, out_dir):
         res["n_layer"] = n
         torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     finally:
+        torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
 
 
