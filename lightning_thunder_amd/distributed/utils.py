@@ -26,78 +26,38 @@ def _is_wait(b: BoundSymbol) -> bool:
 
 
 def sort_waits(trace: TraceCtx) -> TraceCtx:
-    """List scheduling: among ready bound symbols prefer collectives, then regular ops, waits last."""
+    """List scheduling over the bound-symbol DAG (:func:`core.dag.toposort_bsym_dag`): among the
+    eligible bound symbols prefer collectives, then regular ops (both in program order), waits
+    last; among ready waits, the one that completes the inputs of some consumer ("useful") goes
+    first, so the compute stream is not made to wait for collectives whose results are needed only
+    later (e.g. the backward's ZeRO-3 re-gathers, consumed in reverse layer order)."""
+    from ..core.dag import bsym_list_to_dag, toposort_bsym_dag
+
     bsyms = list(trace.bound_symbols)
     if not any(_is_wait(b) for b in bsyms):
         return trace
     ret = bsyms[-1] if bsyms and bsyms[-1].sym.id == PrimIDs.RETURN else None
     body = bsyms[:-1] if ret is not None else bsyms
-    producers: dict[str, int] = {}
-    for i, b in enumerate(body):
-        for o in b.flat_proxy_outs:
-            producers[o.name] = i
-    deps = []
-    users: list[list[int]] = [[] for _ in body]
-    for i, b in enumerate(body):
-        d = set()
-        for a in b.flat_proxy_args:
-            j = producers.get(a.name)
-            if j is not None and j != i:
-                d.add(j)
-        # keep side-effecting ops (in-place copies, deletes) in original relative order
-        deps.append(d)
-        for j in d:
-            users[j].append(i)
-    # side effects: keep relative order among DONT_DCE / IN_PLACE ops
-    from ..core.prims import OpTags
+    _, _, nodes = bsym_list_to_dag(body)
 
-    last_effect = None
-    for i, b in enumerate(body):
-        if OpTags.IN_PLACE in b.sym.tags or b.sym.id == PrimIDs.DEL:
-            if last_effect is not None:
-                deps[i].add(last_effect)
-                users[last_effect].append(i)
-            last_effect = i
-    indeg = [len(d) for d in deps]
-    import heapq
-
-    # collectives first, then ordinary ops (both in program order), waits last; among ready waits,
-    # the one that completes the inputs of some consumer ("useful") goes first, so the compute stream
-    # is not made to wait for collectives whose results are needed only later (e.g. the backward's
-    # ZeRO-3 re-gathers, consumed in reverse layer order)
-    ready_coll, ready_ops, ready_waits = [], [], []
-
-    def push(i):
-        b = body[i]
+    def rank(n) -> tuple:
+        b = n.bsym
         if _is_collective(b):
-            heapq.heappush(ready_coll, i)
-        elif _is_wait(b):
-            ready_waits.append(i)
-        else:
-            heapq.heappush(ready_ops, i)
+            return (0, n.index)
+        if not _is_wait(b):
+            return (1, n.index)
+        useful = any(c.pending == 1 for c in n.children)
+        return (2 if useful else 3, n.index)
 
-    for i in range(len(body)):
-        if indeg[i] == 0:
-            push(i)
-    order = []
-    while ready_coll or ready_ops or ready_waits:
-        if ready_coll:
-            i = heapq.heappop(ready_coll)
-        elif ready_ops:
-            i = heapq.heappop(ready_ops)
-        else:
-            useful = [w for w in ready_waits if any(indeg[u] == 1 for u in users[w])]
-            i = min(useful) if useful else min(ready_waits)
-            ready_waits.remove(i)
-        order.append(i)
-        for u in users[i]:
-            indeg[u] -= 1
-            if indeg[u] == 0:
-                push(u)
-    if len(order) != len(body):  # cycle guard (should not happen)
+    def selector(eligible) -> int:
+        return min(range(len(eligible)), key=lambda i: rank(eligible[i]))
+
+    try:
+        order = toposort_bsym_dag(nodes, selector=selector)
+    except RuntimeError:  # cycle guard (should not happen)
         return trace
     new = from_trace(trace)
-    new.bound_symbols = [body[i] for i in order] + ([ret] if ret is not None else [])
+    new.bound_symbols = order + ([ret] if ret is not None else [])
     new.scopes = [new.bound_symbols]
     new.set_provenance(TraceProvenance("Sort waits (collectives early, waits late)"))
     return new

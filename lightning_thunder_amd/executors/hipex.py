@@ -1051,7 +1051,7 @@ def swiglu_lookaside(a, b):
 # =========================================================================================
 # K7 softmax cross-entropy
 # =========================================================================================
-def _ce_fwd_meta(logits, target, ignore_index, reduction, label_smoothing):
+def _ce_fwd_meta(logits, target, ignore_index, reduction, label_smoothing, weight=None):
     rows = logits.shape[0]
     loss = TensorProxy(like=logits, shape=(rows,) if reduction == "none" else ())
     lse = TensorProxy(like=logits, shape=(rows,), dtype=torch.float32, requires_grad=False)
@@ -1059,30 +1059,31 @@ def _ce_fwd_meta(logits, target, ignore_index, reduction, label_smoothing):
     return loss, lse, stats
 
 
-def _ce_fwd_impl(logits, target, ignore_index, reduction, label_smoothing):
+def _ce_fwd_impl(logits, target, ignore_index, reduction, label_smoothing, weight=None):
     from ..ops.fused import cross_entropy_fwd
 
-    return cross_entropy_fwd(logits, target, ignore_index, reduction, label_smoothing)
+    return cross_entropy_fwd(logits, target, ignore_index, reduction, label_smoothing, weight)
 
 
-def _ce_bwd_impl(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing):
+def _ce_bwd_impl(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing, weight=None):
     from ..ops.fused import cross_entropy_bwd
 
-    return cross_entropy_bwd(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing)
+    return cross_entropy_bwd(g, logits, target, lse, stats, ignore_index, reduction, label_smoothing, weight)
 
 
 hip_cross_entropy_fwd = ex.register_operator("hip_cross_entropy_fwd", meta=_ce_fwd_meta, fn=_ce_fwd_impl)
 hip_cross_entropy_bwd = ex.register_operator(
-    "hip_cross_entropy_bwd", meta=lambda g, logits, *a: TensorProxy(like=logits), fn=_ce_bwd_impl
+    "hip_cross_entropy_bwd", meta=lambda g, logits, *a, **k: TensorProxy(like=logits), fn=_ce_bwd_impl
 )
 
 
 def _ce_checker(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
     return (
-        _gpu(a, target)
+        _gpu(a, target, weight)
         and a.ndim == 2
         and target.ndim == 1
-        and weight is None
+        and (weight is None or (weight.ndim == 1 and weight.shape[0] == a.shape[1]
+                                and weight.dtype in (torch.float32, torch.bfloat16, torch.float16)))
         and size_average is None
         and reduce is None
         and reduction in ("mean", "sum", "none")
@@ -1092,15 +1093,20 @@ def _ce_checker(a, target, weight=None, size_average=None, ignore_index=-100, re
 
 
 def _ce_exec(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
-    loss, _, _ = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing)
+    if weight is None:
+        loss, _, _ = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing)
+    else:
+        loss, _, _ = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing, weight)
     return loss
 
 
 def _ce_grad(a, target, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean", label_smoothing=0.0):
-    loss, lse, stats = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing)
+    # class weights (reference: triton_crossentropy_impl.py:49-151) are a constant of the loss: no grad
+    extra = () if weight is None else (weight,)
+    loss, lse, stats = hip_cross_entropy_fwd(a, target, ignore_index, reduction, label_smoothing, *extra)
 
     def bwd(g):
-        return (hip_cross_entropy_bwd(g, a, target, lse, stats, ignore_index, reduction, label_smoothing),)
+        return (hip_cross_entropy_bwd(g, a, target, lse, stats, ignore_index, reduction, label_smoothing, *extra),)
 
     return loss, bwd
 

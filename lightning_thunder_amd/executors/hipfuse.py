@@ -118,6 +118,7 @@ class HipFusion:
         self._lock = threading.Lock()
         nwords = len(self.tensor_pos) + max(len(outputs), 1) + len(self.number_pos)
         self._argbuf_t = ctypes.c_uint64 * nwords
+        self._argbuf_ws_t = ctypes.c_uint64 * (nwords + 1)  # + the workspace pointer (column mode)
 
     def __repr__(self):
         return f"HipFusion({self.name}, {len(self.nodes)} prims)"
@@ -154,8 +155,8 @@ class HipFusion:
             for p, t in zip((self.inputs[i] for i in self.tensor_pos), tensors):
                 targs[p.name] = cg.TensorArg(tuple(t.shape), tuple(t.stride()), t.dtype, t.data_ptr() % 16 == 0)
             ks = cg.generate(self.plan, self.inputs, self.outputs, targs)
-            fn = load_kernel(ks)
-            v = (fn, ks)
+            fns = [load_kernel(ks)] + [load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.extra]
+            v = (fns, ks)
             self._variants[key] = v
             return v
 
@@ -173,8 +174,8 @@ class HipFusion:
         outs = [torch.empty(tuple(o.shape), dtype=o.dtype, device=dev) for o in self.outputs]
         if any(o.numel() == 0 for o in outs) or any(t.numel() == 0 for t in tensors):
             return tuple(outs)
-        (fn, ks) = self._variant(tensors)
-        buf = self._argbuf_t()
+        (fns, ks) = self._variant(tensors)
+        buf = self._argbuf_ws_t() if ks.ws_bytes else self._argbuf_t()
         k = 0
         for t in tensors:
             buf[k] = t.data_ptr()
@@ -187,12 +188,19 @@ class HipFusion:
         for i in self.number_pos:
             buf[k] = _double_bits(args[i])
             k += 1
+        ws = None
+        if ks.ws_bytes:
+            ws = torch.empty(ks.ws_bytes, dtype=torch.uint8, device=dev)  # stream-ordered by the allocator
+            buf[k] = ws.data_ptr()
         from ..ops._lib import stream_ptr
 
-        rc = _lib().lta_rtc_launch(fn, ks.grid[0], ks.grid[1], ks.grid[2], ks.block[0], ks.block[1], ks.block[2], 0,
-                                   stream_ptr(dev), ctypes.cast(buf, ctypes.c_void_p), ctypes.sizeof(buf))
-        if rc != 0:
-            raise RuntimeError(f"{self.name}: hipModuleLaunchKernel failed with {rc}")
+        launches = [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
+        for fn, (grid, block) in zip(fns, launches):
+            rc = _lib().lta_rtc_launch(fn, grid[0], grid[1], grid[2], block[0], block[1], block[2], 0, stream_ptr(dev),
+                                       ctypes.cast(buf, ctypes.c_void_p), ctypes.sizeof(buf))
+            if rc != 0:
+                raise RuntimeError(f"{self.name}: hipModuleLaunchKernel failed with {rc}")
+        del ws
         return tuple(outs)
 
 
@@ -264,16 +272,17 @@ def compile_source(ks: cg.KernelSource) -> bytes:
     return data
 
 
-def load_kernel(ks: cg.KernelSource):
+def load_kernel(ks: cg.KernelSource, name: str | None = None):
     data = compile_source(ks)
     lib = _lib()
+    name = name or ks.name
     # one source may define several kernels: the function cache is keyed on (kernel name, source)
-    key = int(hashlib.sha1((ks.name + "\0" + ks.src).encode()).hexdigest()[:15], 16)
+    key = int(hashlib.sha1((name + "\0" + ks.src).encode()).hexdigest()[:15], 16)
     fn = ctypes.c_void_p()
     buf = ctypes.create_string_buffer(data, len(data))
-    rc = lib.lta_rtc_load(key, buf, len(data), ks.name.encode(), ctypes.byref(fn))
+    rc = lib.lta_rtc_load(key, buf, len(data), name.encode(), ctypes.byref(fn))
     if rc != 0:
-        raise RuntimeError(f"loading {ks.name} failed with HIP error {rc}")
+        raise RuntimeError(f"loading {name} failed with HIP error {rc}")
     return fn.value
 
 

@@ -19,6 +19,13 @@ The design is CDNA4-first rather than a translation:
   global memory, which stays L2-resident for a row), combined with 64-lane
   ``__shfl_xor`` butterflies and (for T>64) a 4-slot LDS exchange; values that do not
   vary along the reduced dims are hoisted to row scope and computed once.
+* **Column mode** (reductions over the LEADING dims, e.g. bias-grad ``sum(dy, 0)`` or LayerNorm
+  dgamma/dbeta ``sum(dy * xhat, 0)``): two kernels.  The first tiles the kept (trailing) dims
+  over workgroups (64 lanes x ``VEC`` columns) and the reduced rows over a second grid dim of
+  ``S`` splits (4 waves stride the split's rows); it writes any full-domain outputs on the way,
+  combines its 4 waves in LDS and stores one fp32/fp64/int64 partial per (split, column) to a
+  workspace.  The second sums the ``S`` partials of a column in split order (deterministic, no
+  atomics) and evaluates the column-shaped epilogue (casts, scaling, further elementwise).
 * Low-precision values live in fp32 registers and are rounded to bf16/fp16 exactly where
   the trace produces a bf16/fp16 tensor, so results are bit-identical to op-by-op
   execution up to fp32 reassociation in reductions.
@@ -117,14 +124,16 @@ def _sq(shape):
 class Plan:
     domain: tuple | None = None
     red: int = 0  # number of trailing reduced domain dims
+    colred: int = 0  # number of LEADING reduced domain dims (column mode; exclusive with red)
     has_reduction: bool = False
     nodes: list = field(default_factory=list)
     maps: dict = field(default_factory=dict)  # internal value name -> map tuple
     arg_maps: list = field(default_factory=list)  # per node: {arg position: map} for tensor args
+    post: set = field(default_factory=set)  # column mode: values computed from a column reduction
 
     def copy(self) -> "Plan":
-        return Plan(self.domain, self.red, self.has_reduction, list(self.nodes), dict(self.maps),
-                    [dict(m) for m in self.arg_maps])
+        return Plan(self.domain, self.red, self.colred, self.has_reduction, list(self.nodes), dict(self.maps),
+                    [dict(m) for m in self.arg_maps], set(self.post))
 
     # --- maps ----------------------------------------------------------------------------
     def _identity(self, shape):
@@ -146,6 +155,21 @@ class Plan:
             m[i] = d
         return tuple(m)
 
+    def _col_map(self, shape):
+        """Column mode: map a value shaped like the kept (trailing) dims."""
+        if self.domain is None or self.colred == 0:
+            return None
+        kdims = [d for d in range(self.colred, len(self.domain)) if self.domain[d] != 1]
+        nz = [i for i, s in enumerate(shape) if s != 1]
+        if len(nz) != len(kdims):
+            return None
+        m = [None] * len(shape)
+        for i, d in zip(nz, kdims):
+            if shape[i] != self.domain[d]:
+                return None
+            m[i] = d
+        return tuple(m)
+
     def _map_for_shape(self, shape):
         """Map for a value of ``shape`` with no other information (an all-external op)."""
         shape = tuple(shape)
@@ -153,7 +177,13 @@ class Plan:
             return "new"
         if shape == self.domain:
             return self._identity(shape)
+        if self.colred:
+            return self._col_map(shape)
         return self._row_map(shape)
+
+    def covers_reduced(self, m) -> bool:
+        """Column mode: does a value with map ``m`` vary along the reduced (leading) dims?"""
+        return m is not None and any(x is not None and x < self.colred for x in m)
 
     def _internal(self, a):
         return isinstance(a, TensorProxy) and a.name in self.maps
@@ -230,6 +260,14 @@ class Plan:
             if m is None:
                 raise NotFusible("full shape")
             self.maps[out.name] = m
+        if self.colred and sid not in REDUCTIONS:
+            ins = [a for a in bsym.flat_args if isinstance(a, TensorProxy) and a.name in self.post]
+            if ins:
+                # the column epilogue: everything downstream of a column reduction must stay column-shaped
+                for o in outs:
+                    if self.covers_reduced(self.maps.get(o.name)):
+                        raise NotFusible("column-reduced value broadcast back over the reduced dims")
+                    self.post.add(o.name)
         self.nodes.append(bsym)
         self.arg_maps.append(am)
 
@@ -357,7 +395,10 @@ class Plan:
                 raise NotFusible("reduction of non-domain external")
             am[0] = self._identity(a.shape)
         nd, k = len(self.domain), len(dims)
-        if dims != tuple(range(nd - k, nd)):
+        if dims != tuple(range(nd - k, nd)) or self.colred:
+            if dims == tuple(range(k)) and k < nd:
+                self._add_column_reduction(bsym, a, k)
+                return
             raise NotFusible("non-trailing reduction")
         if self.red and self.red != k:
             raise NotFusible("different reduction dims")
@@ -378,6 +419,32 @@ class Plan:
             if m is None:
                 raise NotFusible("reduction output shape")
             self.maps[o.name] = m
+
+    def _add_column_reduction(self, bsym, a, k):
+        if self.red:
+            raise NotFusible("column reduction in a row-reduction region")
+        if bsym.sym.id not in (PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD):
+            raise NotFusible("column var_mean")
+        if self.colred and self.colred != k:
+            raise NotFusible("different column reduction dims")
+        if self._internal(a) and a.name in self.post:
+            raise NotFusible("dependent column reductions")
+        if bsym.sym.id == PrimIDs.SUM and bsym.kwargs.get("output_dtype") not in (None, bsym.output.dtype):
+            raise NotFusible("sum output dtype")
+        if bsym.sym.id == PrimIDs.PROD and a.dtype not in _FLOATS:
+            raise NotFusible("int prod")
+        if self.has_reduction and not self.colred:
+            raise NotFusible("mixed reductions")
+        # a full-domain value already consumed by a later (column) node cannot exist: nodes before the
+        # first column reduction are all full-domain or column-shaped values of externals
+        self.colred = k
+        self.has_reduction = True
+        for o in bsym.flat_outs:
+            m = self._col_map(o.shape)
+            if m is None:
+                raise NotFusible("column reduction output shape")
+            self.maps[o.name] = m
+            self.post.add(o.name)
 
 
 # -----------------------------------------------------------------------------------------
@@ -456,8 +523,12 @@ class TensorArg:
 
 
 class KernelSource:
-    def __init__(self, name, src, grid, block, vec, mode):
+    def __init__(self, name, src, grid, block, vec, mode, extra=(), ws_bytes=0):
         self.name, self.src, self.grid, self.block, self.vec, self.mode = name, src, grid, block, vec, mode
+        # further kernels launched after the main one with the same arguments: (name suffix, grid, block)
+        self.extra = list(extra)
+        # bytes of scratch the kernels share (passed as the last Args field), 0 = none
+        self.ws_bytes = ws_bytes
 
 
 def _contig_strides(shape):
@@ -479,7 +550,7 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
     name = f"{kernel_prefix}_{h}"
     src = src.replace("__KERNEL_NAME__", name)
-    return KernelSource(name, src, grid, block, vec, mode)
+    return KernelSource(name, src, grid, block, vec, mode, extra=g.extra, ws_bytes=g.ws_bytes)
 
 
 class _Gen:
@@ -491,6 +562,10 @@ class _Gen:
         self.D = plan.domain if plan.domain is not None else ()
         self.nd = len(self.D)
         self.red = plan.red
+        self.colred = plan.colred
+        self.force_scalar = False  # column epilogue kernel: every load is one element
+        self.extra: list = []
+        self.ws_bytes = 0
         self.tensor_inputs = [a for a in inputs if isinstance(a, TensorProxy)]
         self.number_inputs = [a for a in inputs if not isinstance(a, TensorProxy)]
         self.in_index = {a.name: i for i, a in enumerate(self.tensor_inputs)}
@@ -577,6 +652,8 @@ class _Gen:
         big = numel >= 2**31 or any(
             sum((s - 1) * st for s, st in zip(t.shape, t.strides)) >= 2**31 for t in self.targs.values())
         self.IT = "unsigned long long" if big else "unsigned"
+        if self.colred:
+            return self._build_col(numel)
         if self.red:
             return self._build_row(numel)
         return self._build_pointwise(numel)
@@ -589,6 +666,8 @@ class _Gen:
         fields.append(f"void* out[{max(nout, 1)}];")
         if ns:
             fields.append(f"double s[{ns}];")
+        if self.colred:
+            fields.append("void* ws;")
         return "struct Args { " + " ".join(fields) + " };"
 
     def _ptr(self, t: TensorProxy, is_out: bool) -> str:
@@ -756,6 +835,8 @@ class _Gen:
                     out.append(f"{indent}const {ct} r_{name} = {e};")
 
     def _load_dep(self, amap) -> bool:
+        if self.force_scalar:
+            return False
         red = self._reduced_dims()
         return self.red == 0 or any(x in red for x in amap if x is not None)
 
@@ -1075,6 +1156,142 @@ class _Gen:
                 self._emit_store(o, True, body, ind)
             body.append("  }")
         return self._wrap(body, block), (grid, 1, 1), (block, 1, 1), V, f"row(T={T})"
+
+    # --- column kernel (reductions over the leading dims) ------------------------------------
+    def _red_acc(self, b):
+        a = b.args[0]
+        sid = b.sym.id
+        act = "double" if a.dtype == torch.float64 else ("long long" if a.dtype in _INTS + (torch.bool,) else "float")
+        if sid in (PrimIDs.AMAX, PrimIDs.AMIN):
+            act = _CTYPE[a.dtype] if a.dtype != torch.bool else "int"
+            if act == "int":
+                act = "long long"
+            if act in ("float", "double"):
+                init = _lit(float("-inf") if sid == PrimIDs.AMAX else float("inf"), act)
+            else:
+                init = "(-9223372036854775807LL - 1)" if sid == PrimIDs.AMAX else "9223372036854775807LL"
+            return act, init, ("nmax" if sid == PrimIDs.AMAX else "nmin")
+        if sid == PrimIDs.PROD:
+            return act, _lit(1.0, act), "*"
+        return act, ("0" if act == "long long" else _lit(0.0, act)), "+"
+
+    def _build_col(self, numel):
+        V, IT = self.vec, self.IT
+        nd, k, D = self.nd, self.colred, self.D
+        C = math.prod(D[k:])
+        R = math.prod(D[:k])
+        ncs = (C // V + 63) // 64
+        # row splits: enough workgroups for ~2 per CU, >= 32 rows (8 per wave) per split
+        S = max(1, min(-(-512 // ncs), -(-R // 32)))
+        RPS = -(-R // S)
+        S = -(-R // RPS)
+        post = self.p.post
+        red_nodes = [i for i, b in enumerate(self.p.nodes) if b.sym.id in REDUCTIONS]
+        full_outs = [o for o in self.outputs if self.p.covers_reduced(self.p.maps.get(o.name))]
+        full_names = {o.name for o in full_outs}
+        col_outs = [o for o in self.outputs if o.name not in full_names]
+        self.load_names, self.loaded, self.idx_avail = {}, set(), set()
+        for kk, b in enumerate(self.p.nodes):
+            for i, a in enumerate(b.args):
+                if isinstance(a, TensorProxy) and a.name not in self.producer:
+                    self.ref(a, kk, i, "j")
+        accs = []
+        for n, kk in enumerate(red_nodes):
+            act, init, comb = self._red_acc(self.p.nodes[kk])
+            accs.append((n, kk, act, init, comb))
+
+        def cf(comb, act, u, v):
+            return f"({u} {comb} {v})" if comb in ("+", "*") else f"{comb}<{act}>({u}, {v})"
+
+        # ---- kernel 1: partial reductions (+ full-domain outputs) ----
+        self._scope_id = "vec"
+        body: list[str] = []
+        body.append("  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;")
+        body.append(f"  const {IT} e = (({IT})blockIdx.x * 64u + lane) * {V}u;")
+        body.append(f"  const bool cvalid = e < {C}u;")
+        body.append(f"  const {IT} ec = cvalid ? e : 0u;")
+        self._decompose("ec", list(range(k, nd)), body, "  ")
+        self.flat_index = f"((unsigned long long)r * {C}ull + (unsigned long long)ec + (unsigned long long)j)"
+        for n, kk, act, init, comb in accs:
+            body.append(f"  {act} acc{n}[{V}];")
+            body.append(f"  #pragma unroll")
+            body.append(f"  for (int j = 0; j < {V}; ++j) acc{n}[j] = {init};")
+        body.append(f"  const {IT} r0 = ({IT})blockIdx.y * {RPS}u;")
+        body.append(f"  const {IT} r1 = r0 + {RPS}u < {R}u ? r0 + {RPS}u : {R}u;")
+        body.append(f"  for ({IT} r = r0 + wv; r < (cvalid ? r1 : 0u); r += 4u) {{")
+        ind = "    "
+        self._decompose("r", list(range(k)), body, ind)
+        need = {o.name for o in full_outs}
+        for n, kk, act, init, comb in accs:
+            a = self.p.nodes[kk].args[0]
+            if a.name in self.producer:
+                need.add(a.name)
+        emitted: set = set()
+        self._emit_nodes(need, "vec", emitted, body, ind)
+        for n, kk, act, init, comb in accs:
+            b = self.p.nodes[kk]
+            x = self.ref(b.args[0], kk, 0, "j")
+            self._materialize_loads(b, kk, True, body, ind)
+            body.append(f"{ind}#pragma unroll")
+            if comb in ("+", "*"):
+                body.append(f"{ind}for (int j = 0; j < {V}; ++j) acc{n}[j] {comb}= ({act})({x});")
+            else:
+                body.append(f"{ind}for (int j = 0; j < {V}; ++j) acc{n}[j] = {comb}<{act}>(acc{n}[j], ({act})({x}));")
+        for o in full_outs:
+            self._emit_store(o, True, body, ind)
+        body.append("  }")
+        # combine the 4 waves (fixed order) and store this split's partial
+        ws_off = 0
+        offs = []
+        for n, kk, act, init, comb in accs:
+            offs.append(ws_off)
+            ws_off += S * C * 8
+            body.append(f"  __shared__ {act} sm{n}[4][{64 * V}];")
+            body.append(f"  #pragma unroll")
+            body.append(f"  for (int j = 0; j < {V}; ++j) sm{n}[wv][lane * {V}u + j] = acc{n}[j];")
+        body.append("  __syncthreads();")
+        body.append("  if (wv == 0u && cvalid) {")
+        for (n, kk, act, init, comb), off in zip(accs, offs):
+            body.append(f"    {act}* ws{n} = ({act}*)((char*)A.ws + {off}ull) + ({IT})blockIdx.y * {C}u;")
+            body.append(f"    #pragma unroll")
+            body.append(f"    for (int j = 0; j < {V}; ++j) {{")
+            expr = f"sm{n}[0][lane * {V}u + j]"
+            for w in range(1, 4):
+                expr = cf(comb, act, expr, f"sm{n}[{w}][lane * {V}u + j]")
+            body.append(f"      ws{n}[e + j] = {expr};")
+            body.append("    }")
+        body.append("  }")
+        main = self._wrap(body, 256)
+
+        # ---- kernel 2: combine the splits, column epilogue ----
+        self.force_scalar = True
+        self._scope_id = "fin"
+        self.idx_avail = set()
+        fin: list[str] = []
+        fin.append(f"  const {IT} e = ({IT})blockIdx.x * 256u + threadIdx.x;")
+        fin.append(f"  if (e >= {C}u) return;")
+        self._decompose("e", list(range(k, nd)), fin, "  ")
+        done: set = set()
+        for (n, kk, act, init, comb), off in zip(accs, offs):
+            b = self.p.nodes[kk]
+            o = b.output
+            fin.append(f"  const {act}* ws{n} = (const {act}*)((const char*)A.ws + {off}ull);")
+            fin.append(f"  {act} t{n} = ws{n}[e];")
+            fin.append(f"  for (unsigned s = 1; s < {S}u; ++s) t{n} = {cf(comb, act, f't{n}', f'ws{n}[({IT})s * {C}u + e]')};")
+            out_ct = _CTYPE[o.dtype]
+            fin.append(f"  const {out_ct} r_{o.name} = {_rnd(o.dtype, f'({out_ct})(t{n})')};")
+            done.add(o.name)
+        self._emit_nodes({o.name for o in col_outs}, "row", done, fin, "  ")
+        for o in col_outs:
+            st, _ = self._out_strides(o)
+            off = " + ".join(f"(({IT})i{d} * {st[d]}u)" for d in range(nd) if st[d]) or "0"
+            fin.append(f"  {self._ptr(o, True)}[{off}] = {_store_conv(o.dtype, f'r_{o.name}')};")
+        self.force_scalar = False
+        fin_src = "\n".join([f'extern "C" __global__ void __launch_bounds__(256) __KERNEL_NAME___fin(Args A) {{'] + fin
+                            + ["}"]) + "\n"
+        self.extra = [("_fin", ((C + 255) // 256, 1, 1), (256, 1, 1))]
+        self.ws_bytes = ws_off
+        return main + fin_src, (ncs, S, 1), (256, 1, 1), V, f"col(S={S})"
 
     def _row_deps(self, name) -> set:
         """Row-scope (loop-invariant) internal values in the cone of ``name``."""

@@ -382,7 +382,8 @@ int dispatch_layout(const void* A, const void* B, void* C, const void* bias, con
 //   bt = 0: B [N][K] (nn.Linear weight)       bt = 1: B stored [K][N]
 // act/bias only with at = bt = 0.  Requires M, N % 256 == 0, K % 128 == 0, 16-B aligned rows and
 // operands under 2 GiB (32-bit buffer offsets).
-// variant: glds split (0: all in the barrier phase, 1: half, 2: a quarter; see the header).
+// variant: glds split (0: all in the barrier phase, 1: half, 2: a quarter; see the header).  Variant 1
+// is the production kernel (every epilogue); 0 and 2 are plain products kept for A/B measurement.
 LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
                               int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
                               int variant, hipStream_t s) {
@@ -390,7 +391,7 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   // buffer-resource byte offsets are 32-bit
   const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
   if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
-  if (variant == 0) return dispatch_layout<0>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, s);
+  if (variant == 1) return dispatch_layout<1>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, s);
   // the other glds splits exist for A/B measurement: plain products only
   if (act != kNone || bias || R) return -1;
 #define LTA_G4V(V)                                                                                              \
@@ -398,7 +399,7 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   if (!at && bt) return launch4<kNone, false, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
   if (at && !bt) return launch4<kNone, true, false, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
   return launch4<kNone, true, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);
-  if (variant == 1) { LTA_G4V(1) }
+  if (variant == 0) { LTA_G4V(0) }
   if (variant == 2) { LTA_G4V(2) }
 #undef LTA_G4V
   return -1;

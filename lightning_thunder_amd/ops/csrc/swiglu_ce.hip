@@ -78,8 +78,11 @@ int ew_grid(int64_t n_items) {
 constexpr int kCeThreads = 256;
 constexpr int kCeWaves = kCeThreads / 64;
 
+// Class weights w (optional, fp32 [V]) follow torch: row loss (1-eps) w_t (lse - x_t)
+// + eps/V * sum_c w_c (lse - x_c), and 'mean' divides by sum of w_t over the kept rows.
 template <typename T>
 __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                            const float* __restrict__ weight,
                                                             float* __restrict__ loss, float* __restrict__ lse_out,
                                                             int64_t rows, int V, int64_t ignore_index,
                                                             float label_smoothing) {
@@ -87,8 +90,9 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict_
   __shared__ float sm[kCeWaves];
   const int64_t row = blockIdx.x;
   const T* x = logits + row * (int64_t)V;
-  float m = -INFINITY, s = 0.f, sum_x = 0.f;
+  float m = -INFINITY, s = 0.f, sum_x = 0.f, sum_w = 0.f;
   const bool vec = (V % VEC == 0) && (((uintptr_t)logits) % 16 == 0);
+  const bool wsm = weight != nullptr && label_smoothing != 0.f;
   if (vec) {
     for (int i = threadIdx.x * VEC; i < V; i += kCeThreads * VEC) {
       const Vec16<T> xv = load16(x + i);
@@ -101,7 +105,12 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict_
       for (int j = 0; j < VEC; ++j) {
         const float f = to_f32(xv.v[j]);
         acc += __expf(f - nm);
-        sum_x += f;
+        if (wsm) {
+          sum_x += weight[i + j] * f;
+          sum_w += weight[i + j];
+        } else {
+          sum_x += f;
+        }
       }
       s = acc;
       m = nm;
@@ -112,7 +121,12 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict_
       const float nm = fmaxf(m, f);
       s = s * __expf(m - nm) + __expf(f - nm);
       m = nm;
-      sum_x += f;
+      if (wsm) {
+        sum_x += weight[i] * f;
+        sum_w += weight[i];
+      } else {
+        sum_x += f;
+      }
     }
   }
   // combine (m, s) across the block
@@ -122,6 +136,8 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict_
   const float gs = block_sum<kCeWaves>(scaled, sm);
   __syncthreads();
   const float gsum_x = (label_smoothing != 0.f) ? block_sum<kCeWaves>(sum_x, sm) : 0.f;
+  __syncthreads();
+  const float gsum_w = wsm ? block_sum<kCeWaves>(sum_w, sm) : (float)V;
   if (threadIdx.x == 0) {
     const float lse = gm + __logf(gs);
     lse_out[row] = lse;
@@ -130,34 +146,39 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_kernel(const T* __restrict_
       loss[row] = 0.f;
     } else {
       const float xt = to_f32(x[t]);
-      float l = lse - xt;
-      if (label_smoothing != 0.f) l = (1.f - label_smoothing) * l + label_smoothing * (lse - gsum_x / (float)V);
+      const float wt = weight ? weight[t] : 1.f;
+      float l = wt * (lse - xt);
+      if (label_smoothing != 0.f)
+        l = (1.f - label_smoothing) * l + label_smoothing * (lse * gsum_w - gsum_x) / (float)V;
       loss[row] = l;
     }
   }
 }
 
 // reduction: out[0] = sum(loss)/max(count,1) (mean) or sum; out[1] = count of valid rows
+// (weighted: the count is the sum of the kept rows' target weights)
 __global__ __launch_bounds__(256) void ce_reduce_kernel(const float* __restrict__ loss, const int64_t* __restrict__ target,
-                                                        float* __restrict__ out, int64_t rows, int64_t ignore_index,
-                                                        int mean) {
+                                                        const float* __restrict__ weight, float* __restrict__ out,
+                                                        int64_t rows, int64_t ignore_index, int mean) {
   __shared__ float sm[4];
   float s = 0.f, c = 0.f;
   for (int64_t i = threadIdx.x; i < rows; i += 256) {
     s += loss[i];
-    c += (target[i] != ignore_index) ? 1.f : 0.f;
+    const int64_t t = target[i];
+    c += (t != ignore_index) ? (weight ? weight[t] : 1.f) : 0.f;
   }
   const float ts = block_sum<4>(s, sm);
   __syncthreads();
   const float tc = block_sum<4>(c, sm);
   if (threadIdx.x == 0) {
-    out[0] = mean ? ts / fmaxf(tc, 1.f) : ts;
+    out[0] = mean ? (weight ? ts / tc : ts / fmaxf(tc, 1.f)) : ts;
     out[1] = tc;
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(kCeThreads) void ce_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                            const float* __restrict__ weight,
                                                             const float* __restrict__ lse, const float* __restrict__ gscale,
                                                             const float* __restrict__ stats, T* __restrict__ dlogits,
                                                             int64_t rows, int V, int64_t ignore_index, int mean,
@@ -172,12 +193,23 @@ __global__ __launch_bounds__(kCeThreads) void ce_bwd_kernel(const T* __restrict_
     g = gscale[row];
   } else {
     g = gscale[0];
-    if (mean) g = g / fmaxf(stats[1], 1.f);
+    if (mean) g = weight ? g / stats[1] : g / fmaxf(stats[1], 1.f);
   }
   if (t == ignore_index) g = 0.f;
   const float l = lse[row];
   const float smooth = label_smoothing / (float)V;
   const float on = 1.f - label_smoothing;
+  // d/dx_j = p_j * pc - on * w_t [j == t] - smooth * w_j, pc = on * w_t + smooth * sum_c w_c
+  float wt = 1.f, pc = 1.f;
+  if (weight) {
+    __shared__ float sm[kCeWaves];
+    float sw = 0.f;
+    if (label_smoothing != 0.f)
+      for (int i = threadIdx.x; i < V; i += kCeThreads) sw += weight[i];
+    sw = label_smoothing != 0.f ? block_sum<kCeWaves>(sw, sm) : 0.f;
+    wt = (t == ignore_index) ? 0.f : weight[t];
+    pc = on * wt + smooth * sw;
+  }
   const bool vec = (V % VEC == 0) && (((uintptr_t)logits) % 16 == 0) && (((uintptr_t)dlogits) % 16 == 0);
   if (vec) {
     for (int i = threadIdx.x * VEC; i < V; i += kCeThreads * VEC) {
@@ -186,16 +218,18 @@ __global__ __launch_bounds__(kCeThreads) void ce_bwd_kernel(const T* __restrict_
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const float p = __expf(to_f32(xv.v[j]) - l);
-        const float oh = (i + j == t) ? on : 0.f;
-        o.v[j] = from_f32<T>(g * (p - oh - smooth));
+        const float oh = (i + j == t) ? on * wt : 0.f;
+        const float sj = weight ? smooth * weight[i + j] : smooth;
+        o.v[j] = from_f32<T>(g * (p * pc - oh - sj));
       }
       store16(dx + i, o);
     }
   } else {
     for (int i = threadIdx.x; i < V; i += kCeThreads) {
       const float p = __expf(to_f32(x[i]) - l);
-      const float oh = (i == t) ? on : 0.f;
-      dx[i] = from_f32<T>(g * (p - oh - smooth));
+      const float oh = (i == t) ? on * wt : 0.f;
+      const float sj = weight ? smooth * weight[i] : smooth;
+      dx[i] = from_f32<T>(g * (p * pc - oh - sj));
     }
   }
 }
@@ -224,25 +258,41 @@ LTA_EXPORT int lta_swiglu_bwd(int dtype, const void* g, const void* a, const voi
 }
 
 // reduction: 0 = none (per-row losses returned), 1 = mean, 2 = sum
+// weight: optional fp32 [V] class weights (null = unweighted)
+LTA_EXPORT int lta_ce_fwd_w(int dtype, const void* logits, const int64_t* target, const void* weight, void* loss_rows,
+                            void* lse, void* out, int64_t rows, int64_t V, int64_t ignore_index, int reduction,
+                            float label_smoothing, hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
+                                           (const T*)logits, target, (const float*)weight, (float*)loss_rows,
+                                           (float*)lse, rows, (int)V, ignore_index, label_smoothing));
+  if (reduction != 0) {
+    hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, stream, (const float*)loss_rows, target,
+                       (const float*)weight, (float*)out, rows, ignore_index, reduction == 1 ? 1 : 0);
+  }
+  return (int)hipGetLastError();
+}
+
 LTA_EXPORT int lta_ce_fwd(int dtype, const void* logits, const int64_t* target, void* loss_rows, void* lse, void* out,
                           int64_t rows, int64_t V, int64_t ignore_index, int reduction, float label_smoothing,
                           hipStream_t stream) {
-  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
-                                           (const T*)logits, target, (float*)loss_rows, (float*)lse, rows, (int)V,
-                                           ignore_index, label_smoothing));
-  if (reduction != 0) {
-    hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, stream, (const float*)loss_rows, target, (float*)out,
-                       rows, ignore_index, reduction == 1 ? 1 : 0);
-  }
+  return lta_ce_fwd_w(dtype, logits, target, nullptr, loss_rows, lse, out, rows, V, ignore_index, reduction,
+                      label_smoothing, stream);
+}
+
+LTA_EXPORT int lta_ce_bwd_w(int dtype, const void* logits, const int64_t* target, const void* weight, const void* lse,
+                            const void* gscale, const void* stats, void* dlogits, int64_t rows, int64_t V,
+                            int64_t ignore_index, int reduction, float label_smoothing, hipStream_t stream) {
+  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
+                                           (const T*)logits, target, (const float*)weight, (const float*)lse,
+                                           (const float*)gscale,
+                                           (const float*)stats, (T*)dlogits, rows, (int)V, ignore_index,
+                                           reduction == 1 ? 1 : 0, reduction == 0 ? 1 : 0, label_smoothing));
   return (int)hipGetLastError();
 }
 
 LTA_EXPORT int lta_ce_bwd(int dtype, const void* logits, const int64_t* target, const void* lse, const void* gscale,
                           const void* stats, void* dlogits, int64_t rows, int64_t V, int64_t ignore_index,
                           int reduction, float label_smoothing, hipStream_t stream) {
-  LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kCeThreads), 0, stream,
-                                           (const T*)logits, target, (const float*)lse, (const float*)gscale,
-                                           (const float*)stats, (T*)dlogits, rows, (int)V, ignore_index,
-                                           reduction == 1 ? 1 : 0, reduction == 0 ? 1 : 0, label_smoothing));
-  return (int)hipGetLastError();
+  return lta_ce_bwd_w(dtype, logits, target, nullptr, lse, gscale, stats, dlogits, rows, V, ignore_index, reduction,
+                      label_smoothing, stream);
 }

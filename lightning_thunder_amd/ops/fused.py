@@ -19,6 +19,10 @@ register_signature("lta_ce_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_float, c_void_p])
 register_signature("lta_ce_bwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                   c_int64, c_int, c_float, c_void_p])
+register_signature("lta_ce_fwd_w", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                    c_int64, c_int, c_float, c_void_p])
+register_signature("lta_ce_bwd_w", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                    c_int64, c_int64, c_int, c_float, c_void_p])
 
 
 def _c(t):
@@ -114,8 +118,15 @@ def swiglu_bwd(g, a, b):
 _REDUCTION = {"none": 0, "mean": 1, "sum": 2}
 
 
-def cross_entropy_fwd(logits, target, ignore_index: int = -100, reduction: str = "mean", label_smoothing: float = 0.0):
-    """Returns (loss [in logits dtype; per-row when reduction='none'], lse [rows] fp32, stats [2] fp32)."""
+def _ce_weight(weight):
+    return None if weight is None else _c(weight.to(torch.float32))
+
+
+def cross_entropy_fwd(logits, target, ignore_index: int = -100, reduction: str = "mean", label_smoothing: float = 0.0,
+                      weight=None):
+    """Returns (loss [in logits dtype; per-row when reduction='none'], lse [rows] fp32, stats [2] fp32).
+    ``weight``: optional [V] class weights (torch semantics: 'mean' divides by the kept rows' target
+    weights; stats[1] holds that sum)."""
     lib = require()
     logits = _c(logits)
     target = _c(target.to(torch.int64))
@@ -124,8 +135,9 @@ def cross_entropy_fwd(logits, target, ignore_index: int = -100, reduction: str =
     lse = torch.empty(rows, device=logits.device, dtype=torch.float32)
     stats = torch.empty(2, device=logits.device, dtype=torch.float32)
     r = _REDUCTION[reduction]
-    check(lib.lta_ce_fwd(dcode(logits), ptr(logits), ptr(target), ptr(loss_rows), ptr(lse), ptr(stats), rows, V,
-                         int(ignore_index), r, float(label_smoothing), stream_ptr(logits.device)), "lta_ce_fwd")
+    w = _ce_weight(weight)
+    check(lib.lta_ce_fwd_w(dcode(logits), ptr(logits), ptr(target), ptr(w), ptr(loss_rows), ptr(lse), ptr(stats), rows,
+                           V, int(ignore_index), r, float(label_smoothing), stream_ptr(logits.device)), "lta_ce_fwd")
     if r == 0:
         loss = loss_rows.to(logits.dtype)
     else:
@@ -134,14 +146,15 @@ def cross_entropy_fwd(logits, target, ignore_index: int = -100, reduction: str =
 
 
 def cross_entropy_bwd(g, logits, target, lse, stats, ignore_index: int = -100, reduction: str = "mean",
-                      label_smoothing: float = 0.0):
+                      label_smoothing: float = 0.0, weight=None):
     lib = require()
     logits = _c(logits)
     target = _c(target.to(torch.int64))
     rows, V = logits.shape
     gs = _c(g.float().reshape(-1))
     dl = torch.empty_like(logits)
-    check(lib.lta_ce_bwd(dcode(logits), ptr(logits), ptr(target), ptr(lse), ptr(gs), ptr(stats), ptr(dl), rows, V,
-                         int(ignore_index), _REDUCTION[reduction], float(label_smoothing), stream_ptr(logits.device)),
-          "lta_ce_bwd")
+    w = _ce_weight(weight)
+    check(lib.lta_ce_bwd_w(dcode(logits), ptr(logits), ptr(target), ptr(w), ptr(lse), ptr(gs), ptr(stats), ptr(dl), rows,
+                           V, int(ignore_index), _REDUCTION[reduction], float(label_smoothing),
+                           stream_ptr(logits.device)), "lta_ce_bwd")
     return dl

@@ -85,7 +85,7 @@ def test_fp8_delayed_under_fsdp_matches_single_process():
         mp.start_processes(_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
     # the FP8 GEMMs run on the gathered weights, and the amax history is the same everywhere
-    assert "fp8_linear" in res[0]["fw"] and "all_gather" in res[0]["fw"], res[0]["fw"]
+    assert "hip_fp8_gemm" in res[0]["fw"] and "all_gather" in res[0]["fw"], res[0]["fw"]
     assert res[0]["updates"] >= STEPS - 1
     torch.testing.assert_close(res[0]["hist"], res[1]["hist"], rtol=0, atol=0)
     assert res[0]["hist"].abs().sum() > 0
