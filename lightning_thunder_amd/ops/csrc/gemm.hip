@@ -862,6 +862,126 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_grouped_nt_bf16_kernel(const __h
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Grouped FP8 NT GEMM for quantized mixture-of-experts inference (reference te_groupedmm_fp8,
+// thunder/transforms/te_inference.py:17-113): rows [off[g-1], off[g]) of the e4m3 activations A
+// (one per-tensor scale *sa) times expert g's e4m3 weight W[g] ([N, K], per-expert scale sw[g]),
+// out bf16 = acc / (sa * sw[g]).  Row-tile search, clamped loads and masked stores as the bf16
+// grouped kernel; the K loop, LDS image and fragment map are those of gemm_nt_fp8_kernel.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHR, 1) void gemm_grouped_nt_fp8_kernel(const char* __restrict__ A,
+                                                                      const char* __restrict__ W,
+                                                                      __hip_bfloat16* __restrict__ C,
+                                                                      const int* __restrict__ offs, int G, int M,
+                                                                      int N, int K, int64_t wstride,
+                                                                      const float* __restrict__ sa,
+                                                                      const float* __restrict__ sw) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int slot = blockIdx.x, g = 0, start = 0, end = 0;
+  bool found = false;
+  for (; g < G; ++g) {
+    end = offs[g];
+    const int tiles = (end - start + BM - 1) / BM;
+    if (slot < tiles) {
+      found = true;
+      break;
+    }
+    slot -= tiles;
+    start = end;
+  }
+  if (!found) return;  // uniform across the workgroup
+  const int m0 = start + slot * BM, n0 = blockIdx.y * BN;
+  const char* B = W + (int64_t)g * wstride;
+  const int last = end - 1;
+  constexpr int BKB = 128;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int k0, char* sbase) {
+    const int r = lane >> 3, p = lane & 7;
+    const int c = p ^ r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;
+      const int row = min(m0 + chunk * 8 + r, last);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * K + k0 + c * 16),
+                                       (lds_void*)(sbase + chunk * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int chunk = i * 8 + wave;
+      const int row = n0 + chunk * 8 + r;
+      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)row * K + k0 + c * 16),
+                                       (lds_void*)(sbase + TILE_BYTES + chunk * 1024), 16, 0, 0);
+    }
+  };
+  const int nk = K / BKB;
+  stage(0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) stage((t + 1) * BKB, smem + ((t + 1) & 1) * STAGE_BYTES);
+    v8i af[8], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = wm * 128 + m * 16 + fr;
+      const uint4 lo = *reinterpret_cast<const uint4*>(cur + row * 128 + ((fq ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(cur + row * 128 + (((4 + fq) ^ (row & 7)) << 4));
+      af[m] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int row = wn * 64 + n * 16 + fr;
+      const char* base = cur + TILE_BYTES + row * 128;
+      const uint4 lo = *reinterpret_cast<const uint4*>(base + ((fq ^ (row & 7)) << 4));
+      const uint4 hi = *reinterpret_cast<const uint4*>(base + (((4 + fq) ^ (row & 7)) << 4));
+      bfr[n] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = mfma_fp8<0, 0>(af[m], bfr[n], acc[m][n]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const float alpha = 1.f / (*sa * sw[g]);
+  char* wbuf = smem + wave * (128 * 128);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n * 16 + fr;
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fq * 4 + j;
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4) + co) =
+            __float2bfloat16(acc[m][n][j] * alpha);
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 3, ch = id & 7;
+    const int grow = m0 + wm * 128 + row;
+    if (grow < end) {
+      const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+      *reinterpret_cast<uint4*>(C + (int64_t)grow * N + n0 + wn * 64 + ch * 8) = v;
+    }
+  }
+}
+
 template <int ACT>
 int launch_act(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
                int ldb, int ldc, int ldr, float alpha, int variant, hipStream_t s) {
@@ -949,6 +1069,17 @@ LTA_EXPORT int lta_gemm_grouped_nt_bf16(const void* A, const void* W, void* C, c
   dim3 grid((M + BM - 1) / BM + G, N / BN), block(NTHR);
   hipLaunchKernelGGL(gemm_grouped_nt_bf16_kernel, grid, block, 0, stream, (const __hip_bfloat16*)A,
                      (const __hip_bfloat16*)W, (__hip_bfloat16*)C, (const int*)offs, G, M, N, K, wstride);
+  return (int)hipGetLastError();
+}
+
+// FP8 grouped: A [M, K] e4m3 (scale *sa), W [G, N, K] e4m3 (scales sw[G]), offs int32 row ends ->
+// out [M, N] bf16 = (A_g . W[g]^T) / (sa * sw[g]).  N % 256 == 0, K % 128 == 0.
+LTA_EXPORT int lta_gemm_grouped_nt_fp8(const void* A, const void* W, void* C, const void* offs, int G, int M, int N,
+                                       int K, int64_t wstride, const void* sa, const void* sw, hipStream_t stream) {
+  if (N % BN || K % 128) return -2;
+  dim3 grid((M + BM - 1) / BM + G, N / BN), block(NTHR);
+  hipLaunchKernelGGL(gemm_grouped_nt_fp8_kernel, grid, block, 0, stream, (const char*)A, (const char*)W,
+                     (__hip_bfloat16*)C, (const int*)offs, G, M, N, K, wstride, (const float*)sa, (const float*)sw);
   return (int)hipGetLastError();
 }
 

@@ -5,9 +5,14 @@ Linear weights -> NF4 qweight + absmax + code; ``linear`` -> ``bnb_matmul_nf4``)
 
 MI355X design: the quantized linear is a ``torch.library`` custom op
 (``lta::nf4_linear``) so it is traced like any other op (``thunder.torch.custom_op`` support)
-and also runs eagerly.  On the GPU it dequantizes with the HIP kernel
-``ops/csrc/nf4.hip`` (16 weights per lane, code book in registers) straight into a bf16 buffer
-and runs the GEMM on hipBLASLt; the weight never exists in bf16 outside that transient buffer.
+and also runs eagerly.  On the GPU:
+
+* decode (<= 8 activation rows): ONE fused kernel, ``lta_gemv_nf4`` (ops/csrc/nf4.hip), streams the
+  4-bit weight once and decodes it in registers against the activations -- the weight is never
+  materialised in bf16 and the HBM traffic is a quarter of a bf16 GEMV's;
+* prefill / QLoRA training (more rows): the HIP dequant kernel writes a transient bf16 weight and
+  the hand-written MFMA GEMM (``ops.gemm.linear``) consumes it.
+
 Gradients flow to the activations (QLoRA: frozen base weights + LoRA adapters).
 """
 from __future__ import annotations
@@ -57,10 +62,44 @@ def dequantize_nf4(packed: torch.Tensor, absmax: torch.Tensor, shape, dtype=torc
     return vals.reshape(shape).to(dtype)
 
 
+def gemv_nf4_supported(x: torch.Tensor, in_features: int, blocksize: int) -> bool:
+    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16) or x.shape[-1] != in_features:
+        return False
+    rows = x.numel() // max(in_features, 1)
+    return 1 <= rows <= 8 and in_features % 32 == 0 and blocksize % 32 == 0
+
+
+def gemv_nf4(x: torch.Tensor, qweight: torch.Tensor, absmax: torch.Tensor, code: torch.Tensor, out_features: int,
+             blocksize: int, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused NF4 decode GEMV: ``x [.., K] . dequant(qweight)^T (+ bias)`` without a bf16 weight."""
+    from ..ops._lib import require, stream_ptr, check, register_signature, c_int, c_void_p, DTYPE_CODE
+
+    register_signature("lta_gemv_nf4", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                        c_int, c_int, c_int, c_int, c_int, c_void_p])
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    y = torch.empty((M, out_features), dtype=x.dtype, device=x.device)
+    code = code.to(device=x.device, dtype=torch.float32).contiguous()
+    b = None if bias is None else bias.to(x.dtype).contiguous()
+    check(require().lta_gemv_nf4(DTYPE_CODE[x.dtype], x2.data_ptr(), qweight.data_ptr(), absmax.data_ptr(),
+                                 code.data_ptr(), None if b is None else b.data_ptr(), y.data_ptr(), M, out_features,
+                                 K, x2.stride(0), out_features, blocksize, stream_ptr(x.device)), "lta_gemv_nf4")
+    return y.reshape(*x.shape[:-1], out_features)
+
+
 @torch.library.custom_op("lta::nf4_linear", mutates_args=())
 def nf4_linear(x: torch.Tensor, qweight: torch.Tensor, absmax: torch.Tensor, code: torch.Tensor, out_features: int,
                in_features: int, blocksize: int, bias: torch.Tensor | None = None) -> torch.Tensor:
+    if gemv_nf4_supported(x, in_features, blocksize):
+        return gemv_nf4(x, qweight, absmax, code, out_features, blocksize, bias)
     w = dequantize_nf4(qweight, absmax, (out_features, in_features), x.dtype, blocksize, code)
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        from ..ops.gemm import linear
+
+        return linear(x, w, bias)
     return torch.nn.functional.linear(x, w, bias)
 
 

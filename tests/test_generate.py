@@ -94,11 +94,12 @@ def test_decode_logits_teacher_forced_gpu(graphs):
     seq = torch.randint(0, 300, (1, 24), device="cuda")
 
     def run(model, fwd):
+        # graph replays return the graph's static output buffer: copy each step's logits out
         model.set_kv_cache(1, 64, device=torch.device("cuda"))
-        outs = [fwd(seq[:, :8], torch.arange(8, device="cuda"))[:, -1]]
+        outs = [fwd(seq[:, :8], torch.arange(8, device="cuda"))[:, -1].float().clone()]
         for i in range(8, 23):
-            outs.append(fwd(seq[:, i:i + 1], torch.tensor([i], device="cuda"))[:, -1])
-        return torch.stack(outs).float()
+            outs.append(fwd(seq[:, i:i + 1], torch.tensor([i], device="cuda"))[:, -1].float().clone())
+        return torch.stack(outs)
 
     transforms = []
     if graphs:

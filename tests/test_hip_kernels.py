@@ -222,6 +222,28 @@ def test_nf4_dequant_kernel(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 3, 8, 64])
+@pytest.mark.parametrize("bias", [False, True])
+def test_nf4_fused_gemv_and_prefill(M, bias):
+    """K9: decode rows take the fused NF4 GEMV (4-bit weight decoded in registers), prefill rows the
+    dequant + hand GEMM; both against an fp32 product with the fp32-dequantized weight."""
+    from lightning_thunder_amd.transforms.quantization import (quantize_nf4, dequantize_nf4, nf4_linear, NF4_CODE,
+                                                               gemv_nf4_supported)
+
+    torch.manual_seed(0)
+    N, K = 768, 1024
+    w = torch.randn(N, K, device="cuda") * 0.05
+    q, a = quantize_nf4(w)
+    wd = dequantize_nf4(q.cpu(), a.cpu(), w.shape, torch.float32).cuda()
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) if bias else None
+    assert gemv_nf4_supported(x, K, 64) == (M <= 8)
+    y = nf4_linear(x, q, a, NF4_CODE.cuda(), N, K, 64, b)
+    ref = x.float() @ wd.t() + (b.float() if bias else 0.0)
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 2048, 1024)])
 @pytest.mark.parametrize("epi", ["plain", "bias_gelu", "residual", "bias_silu_residual"])
 def test_gemm_nt_bf16(shape, epi):
