@@ -759,6 +759,14 @@ class Interpreter:
                 self.log("lookaside", _name(fn))
                 return dispatch_torch_function(fn, args, kwargs), None
         t = type(fn)
+        if t.__name__ == "CustomOpDef" or (t.__name__ == "OpOverload" and "::" in getattr(getattr(fn, "_schema", None),
+                                                                                         "name", "")):
+            from ..torch.custom_op import opdef_of, custom_op_symbol
+
+            od = opdef_of(fn)
+            if od is not None:
+                self.log("lookaside", f"custom op {od._namespace}::{od._name}")
+                return custom_op_symbol(od)(*args, **kwargs), None
         if t is types.MethodType and isinstance(fn.__self__, type) and issubclass(fn.__self__, torch.autograd.Function) \
                 and fn.__func__ is _FUNCTION_APPLY:
             from ..torch import autograd_function

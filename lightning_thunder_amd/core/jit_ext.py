@@ -131,6 +131,12 @@ def dispatch_torch_function(func, args, kwargs):
 
         return dtensor_symbol(func)(*args, **kwargs)
 
+    if sym is None:
+        from ..torch.custom_op import opdef_of, custom_op_symbol
+
+        od = opdef_of(func)
+        if od is not None:  # torch.library custom op: its own symbol, fake-impl meta, registered autograd
+            return custom_op_symbol(od)(*args, **kwargs)
     if sym is not None:
         from .symbol import CALLED_TORCH_FN
 

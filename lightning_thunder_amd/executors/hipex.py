@@ -1317,14 +1317,16 @@ def _sort_impl(a, dim, descending, stable):
     return index_ops.sort(a, dim, descending, stable)
 
 
-def _cumsum_meta(a, dim):
-    return TensorProxy(like=a, dtype=torch.int64 if a.dtype in (torch.int32, torch.int64) else a.dtype)
+def _cumsum_meta(a, dim, out_i32=False):
+    if a.dtype in (torch.int32, torch.int64):
+        return TensorProxy(like=a, dtype=torch.int32 if out_i32 else torch.int64)
+    return TensorProxy(like=a)
 
 
-def _cumsum_impl(a, dim):
+def _cumsum_impl(a, dim, out_i32=False):
     from ..ops import index_ops
 
-    return index_ops.cumsum(a, dim)
+    return index_ops.cumsum(a, dim, torch.int32 if out_i32 else None)
 
 
 def _emb_bwd_meta(grad, indices, num_weights, padding_idx, scale_grad_by_freq):
@@ -1388,12 +1390,14 @@ def _cumsum_checker(a, dim, *, dtype=None):
         return False
     if a.dtype in _ROW_DT:
         return dtype is None or dtype == a.dtype
-    # integer scans produce int64: the prim's output dtype must say so
-    return (a.dtype == torch.int64 and dtype in (None, torch.int64)) or (a.dtype == torch.int32 and dtype == torch.int64)
+    # integer scans accumulate in int64; the output dtype is the prim's (int64, or int32 for an
+    # int32 scan, which is what ltorch.cumsum(..., dtype=torch.int32) lowers to)
+    return a.dtype in (torch.int32, torch.int64) and dtype in (None, torch.int64, torch.int32)
 
 
 def _cumsum_exec(a, dim, *, dtype=None):
-    return hip_cumsum(a, dim)
+    out = dtype or a.dtype
+    return hip_cumsum(a, dim, out == torch.int32)
 
 
 def _emb_bwd_checker(grad, indices, num_weights, padding_idx, scale_grad_by_freq, sparse):
@@ -1424,9 +1428,54 @@ def _index_add_exec(a, indices, value, dim):
     return hip_index_add(a, indices, value)
 
 
+def _cdim(a, dim):
+    d = pyval(dim)
+    return d % a.ndim if a.ndim else 0
+
+
+# ltorch-level claims (the torch executor would otherwise take ltorch.argsort / cumsum whole)
+def _lt_topk_checker(a, k, dim=-1, largest=True, sorted=True):
+    return a.ndim >= 1 and _topk_checker(a, k, _cdim(a, dim), largest, sorted)
+
+
+def _lt_topk_exec(a, k, dim=-1, largest=True, sorted=True):
+    return hip_topk(a, pyval(k), _cdim(a, dim), bool(pyval(largest)), bool(pyval(sorted)))
+
+
+def _lt_sort_checker(a, dim=-1, descending=False, stable=False):
+    return a.ndim >= 1 and _sort_checker(a, _cdim(a, dim), descending, stable)
+
+
+def _lt_sort_exec(a, dim=-1, descending=False, stable=False):
+    return hip_sort(a, _cdim(a, dim), bool(pyval(descending)), bool(pyval(stable)))
+
+
+def _lt_argsort_exec(a, dim=-1, descending=False, stable=False):
+    return hip_sort(a, _cdim(a, dim), bool(pyval(descending)), bool(pyval(stable)))[1]
+
+
+def _lt_cumsum_checker(a, dim, *, dtype=None):
+    if not (_gpu(a) and a.ndim >= 1 and 0 < _numel(a.shape) < 2**31):
+        return False
+    if a.dtype in _ROW_DT:
+        return dtype is None or dtype == a.dtype
+    return a.dtype in (torch.int32, torch.int64, torch.bool, torch.uint8, torch.int8, torch.int16) and \
+        dtype in (None, torch.int64, torch.int32) and a.dtype in (torch.int32, torch.int64)
+
+
+def _lt_cumsum_exec(a, dim, *, dtype=None):
+    # torch: integer cumsum promotes to int64 unless dtype says otherwise
+    return hip_cumsum(a, _cdim(a, dim), dtype == torch.int32)
+
+
 def _register_all():
     from .. import torch as ltorch
     from ..core import prims as P
+
+    ex.register_implementation(ltorch.topk, checker=_lt_topk_checker, execution_transform=_lt_topk_exec)
+    ex.register_implementation(ltorch.sort, checker=_lt_sort_checker, execution_transform=_lt_sort_exec)
+    ex.register_implementation(ltorch.argsort, checker=_lt_sort_checker, execution_transform=_lt_argsort_exec)
+    ex.register_implementation(ltorch.cumsum, checker=_lt_cumsum_checker, execution_transform=_lt_cumsum_exec)
 
     ex.register_implementation(P.topk, checker=_topk_checker, execution_transform=_topk_exec)
     ex.register_implementation(P.sort, checker=_sort_checker, execution_transform=_sort_exec)

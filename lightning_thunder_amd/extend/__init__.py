@@ -302,9 +302,13 @@ def get_always_executors() -> tuple[Executor, ...]:
     return tuple(_always_executors)
 
 
-def add_default_executor(ex: Executor) -> None:
+def add_default_executor(ex: Executor, *, last: bool = False) -> None:
+    """Highest priority by default; ``last=True`` appends (below every registered default)."""
     remove_default_executor(ex.name)
-    _default_executors.insert(0, ex)
+    if last:
+        _default_executors.append(ex)
+    else:
+        _default_executors.insert(0, ex)
 
 
 def add_always_executor(ex: Executor) -> None:
@@ -359,3 +363,4 @@ def _ensure_builtin_executors():
     _builtin_loaded = True
     from ..executors import pythonex, torchex  # noqa: F401  (register themselves)
     from ..executors import hipex, hipfuse  # noqa: F401
+    from ..executors import custom_opex  # noqa: F401

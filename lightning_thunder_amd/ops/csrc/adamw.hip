@@ -47,20 +47,38 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
   const bool vec = ((end - start) % VP == 0) && ((uintptr_t)(P + start) % 16 == 0) && ((uintptr_t)(G + start) % 16 == 0) &&
                    (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0);
   if (vec) {
-    for (int64_t i = start + (int64_t)threadIdx.x * VP; i < end; i += 256 * VP) {
-      Vec16<TP> pv = load16(P + i), gv = load16(G + i);
-      Vec16<TS> mv = load16(M + i), vv = load16(V + i);
+    // U vectors per lane per trip, all loads issued before any math: 4U 16-B loads in flight per lane
+    constexpr int U = 4;
+    for (int64_t i0 = start + (int64_t)threadIdx.x * VP; i0 < end; i0 += 256 * VP * U) {
+      Vec16<TP> pv[U], gv[U];
+      Vec16<TS> mv[U], vv[U];
 #pragma unroll
-      for (int j = 0; j < VP; ++j) {
-        float p = to_f32(pv.v[j]), m = to_f32(mv.v[j]), v = to_f32(vv.v[j]);
-        adamw_elem<TP, TS>(p, to_f32(gv.v[j]) * grad_scale, m, v, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
-        pv.v[j] = from_f32<TP>(p);
-        mv.v[j] = from_f32<TS>(m);
-        vv.v[j] = from_f32<TS>(v);
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * 256 * VP;
+        if (i < end) {
+          pv[u] = load16(P + i);
+          gv[u] = load16(G + i);
+          mv[u] = load16(M + i);
+          vv[u] = load16(V + i);
+        }
       }
-      store16(P + i, pv);
-      store16(M + i, mv);
-      store16(V + i, vv);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * 256 * VP;
+        if (i < end) {
+#pragma unroll
+          for (int j = 0; j < VP; ++j) {
+            float p = to_f32(pv[u].v[j]), m = to_f32(mv[u].v[j]), v = to_f32(vv[u].v[j]);
+            adamw_elem<TP, TS>(p, to_f32(gv[u].v[j]) * grad_scale, m, v, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+            pv[u].v[j] = from_f32<TP>(p);
+            mv[u].v[j] = from_f32<TS>(m);
+            vv[u].v[j] = from_f32<TS>(v);
+          }
+          store16(P + i, pv[u]);
+          store16(M + i, mv[u]);
+          store16(V + i, vv[u]);
+        }
+      }
     }
   } else {
     for (int64_t i = start + threadIdx.x; i < end; i += 256) {

@@ -377,10 +377,23 @@ LTA_EXPORT int lta_topk_rows(int dtype, const void* x, int64_t ldx, void* vals, 
 }
 
 // Inclusive scan of R rows of N values (row stride ldx) into y [R, N] contiguous.  Float inputs
-// accumulate in fp32 and keep their dtype; int32 / int64 inputs accumulate and store int64.
-LTA_EXPORT int lta_cumsum_rows(int dtype, const void* x, int64_t ldx, void* y, int R, int64_t N, hipStream_t s) {
+// accumulate in fp32 and keep their dtype; int32 / int64 inputs accumulate in int64 and store
+// int64, or int32 when out_i32 (torch.cumsum(..., dtype=torch.int32), MoE routing offsets).
+LTA_EXPORT int lta_cumsum_rows(int dtype, const void* x, int64_t ldx, void* y, int R, int64_t N, int out_i32,
+                               hipStream_t s) {
   if (R < 1 || N < 1) return (int)hipErrorInvalidValue;
   const dim3 grid(R), block(256);
+  if (out_i32) {
+    if (dtype == kI32)
+      hipLaunchKernelGGL((cumsum_rows_kernel<int32_t, int64_t, int32_t>), grid, block, 0, s, (const int32_t*)x, ldx,
+                         (int32_t*)y, N);
+    else if (dtype == kI64)
+      hipLaunchKernelGGL((cumsum_rows_kernel<int64_t, int64_t, int32_t>), grid, block, 0, s, (const int64_t*)x, ldx,
+                         (int32_t*)y, N);
+    else
+      return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+  }
   switch (dtype) {
     case kF32:
       hipLaunchKernelGGL((cumsum_rows_kernel<float, float, float>), grid, block, 0, s, (const float*)x, ldx, (float*)y, N);

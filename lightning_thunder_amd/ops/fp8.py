@@ -70,6 +70,24 @@ def gemm_nt_fp8(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Te
     return out
 
 
+register_signature("lta_gemm_grouped_nt_fp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                                c_int64, c_void_p, c_void_p, c_void_p])
+
+
+def grouped_mm_fp8(qa: torch.Tensor, qw: torch.Tensor, sa: torch.Tensor, sw: torch.Tensor,
+                   offs: torch.Tensor) -> torch.Tensor:
+    """bf16 [M, N]: rows of group g of ``qa`` ([M, K] e4m3 as uint8, device scalar scale ``sa``)
+    times expert g's ``qw[g]`` ([G, N, K] e4m3, scales ``sw`` [G]); ``offs`` int32 row ends."""
+    lib = require()
+    M, K = qa.shape
+    G, N, _ = qw.shape
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=qa.device)
+    check(lib.lta_gemm_grouped_nt_fp8(qa.data_ptr(), qw.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
+                                      qw.stride(0), sa.data_ptr(), sw.data_ptr(), stream_ptr(qa.device)),
+          "lta_gemm_grouped_nt_fp8")
+    return out
+
+
 def fp8_linear_supported(M: int, N: int, K: int) -> bool:
     return M % 256 == 0 and N % 256 == 0 and K % 256 == 0
 

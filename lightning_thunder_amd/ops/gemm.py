@@ -91,7 +91,7 @@ def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
 
 
 def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=None, alpha: float = 1.0,
-            out: torch.Tensor | None = None, variant: int = 0) -> torch.Tensor:
+            out: torch.Tensor | None = None, variant: int = 1) -> torch.Tensor:
     """``act(alpha * a @ b + bias) + residual`` on the 4-wave MFMA kernel.  ``a``/``b`` may be
     transposed views (the backward GEMMs read dY^T / W / X in place); bias and act only for the
     forward layout (a row-major, b = W^T)."""

@@ -15,7 +15,7 @@ from ._lib import require, stream_ptr, check, register_signature, c_int, c_int64
 
 register_signature("lta_sort_rows", [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
 register_signature("lta_topk_rows", [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
-register_signature("lta_cumsum_rows", [c_int, c_void_p, c_int64, c_void_p, c_int, c_int64, c_void_p])
+register_signature("lta_cumsum_rows", [c_int, c_void_p, c_int64, c_void_p, c_int, c_int64, c_int, c_void_p])
 register_signature("lta_sort_index_keys", [c_void_p, c_int, c_void_p, c_void_p])
 register_signature("lta_index_rows_sum", [c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64,
                                           c_int64, c_int64, c_int64, c_int, c_float, c_void_p])
@@ -95,21 +95,23 @@ def topk(x: torch.Tensor, k: int, dim: int = -1, largest: bool = True, sorted: b
 def cumsum_supported(x: torch.Tensor, dim: int, dtype=None) -> bool:
     if not x.is_cuda or x.numel() == 0 or x.numel() >= 2**31:
         return False
-    out_dtype = dtype or x.dtype
     if x.dtype in _ROW_DTYPES:
-        return out_dtype == x.dtype
-    return x.dtype in (torch.int32, torch.int64) and out_dtype == torch.int64
+        return dtype in (None, x.dtype)
+    return x.dtype in (torch.int32, torch.int64) and dtype in (None, torch.int64, torch.int32)
 
 
 def cumsum(x: torch.Tensor, dim: int, dtype=None) -> torch.Tensor:
     """Inclusive scan along ``dim``: float inputs accumulate in fp32 and keep their dtype; integer
-    inputs give int64 (torch's promotion)."""
+    inputs accumulate in int64 and give int64 (torch's promotion) or ``dtype=torch.int32``."""
     x2, shp, d = _rows(x, dim)
     R, N = x2.shape
-    out_dtype = torch.int64 if x.dtype in (torch.int32, torch.int64) else x.dtype
+    if x.dtype in (torch.int32, torch.int64):
+        out_dtype = torch.int32 if dtype == torch.int32 else torch.int64
+    else:
+        out_dtype = x.dtype
     y = torch.empty((R, N), dtype=out_dtype, device=x.device)
     check(require().lta_cumsum_rows(_CODE[x.dtype], x2.data_ptr(), x2.stride(0), y.data_ptr(), R, N,
-                                    stream_ptr(x.device)), "lta_cumsum_rows")
+                                    int(out_dtype == torch.int32), stream_ptr(x.device)), "lta_cumsum_rows")
     return _back(y, shp, d, x.ndim)
 
 

@@ -8,8 +8,10 @@ per-tensor scaling (one amax pass + one cast pass, ``ops/fp8.py``) and multiplie
 block-scaled MFMA fp8 GEMM (``csrc/gemm.hip`` ``gemm_nt_fp8_kernel``, the dequantisation
 ``1/(sx*sw)`` folded into the epilogue).  Rows are padded to the GEMM's 256-row tile so decode
 (M = batch) runs on the same kernel; the weight is read from HBM in fp8, i.e. half the bytes of a
-bf16 GEMV.  Grouped (MoE) experts are quantized per expert and run as fp8-dequantized bf16 grouped
-GEMMs.
+bf16 GEMV.  Grouped (MoE) experts (``GroupedLinear``, weight [G, N, K]) are quantized per expert
+(one scale per expert) and run on the grouped fp8 MFMA kernel ``lta_gemm_grouped_nt_fp8``
+(``lta::fp8_grouped_mm_inference``, the ``te_groupedmm_fp8`` counterpart): each workgroup finds
+its (expert, row tile) from the device offsets, so routing needs no host synchronisation.
 
 The quantized linear is a ``torch.library`` custom op (``lta::fp8_linear_inference``), so it is
 traced as an ordinary op and also runs eagerly.  Activation gradients flow (the weights are
@@ -86,6 +88,69 @@ def _backward(ctx, g):
 fp8_linear_inference.register_autograd(_backward, setup_context=_setup)
 
 
+def quantize_experts_e4m3(w: torch.Tensor):
+    """w [G, N, K] -> (uint8 e4m3 [G, N, K], fp32 scales [G]) with one scale per expert."""
+    wf = w.detach().float()
+    amax = wf.abs().amax(dim=(1, 2)).clamp_min(1e-12)
+    scale = (E4M3_MAX / amax).to(torch.float32)
+    q = (wf * scale[:, None, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q.contiguous(), scale.contiguous()
+
+
+@torch.library.custom_op("lta::fp8_grouped_mm_inference", mutates_args=())
+def fp8_grouped_mm_inference(x: torch.Tensor, qweight: torch.Tensor, w_scale: torch.Tensor,
+                             offsets: torch.Tensor) -> torch.Tensor:
+    """``x [M, K]`` (rows grouped by expert, int32 row ends ``offsets``) times the fp8 experts
+    ``qweight [G, N, K]`` -> bf16 [M, N]."""
+    G, N, K = qweight.shape
+    if x.is_cuda and x.dtype == torch.bfloat16 and K % 128 == 0 and N % 256 == 0 and x.shape[0] > 0:
+        from ..ops import fp8 as f8
+
+        xc = x.contiguous()
+        st = torch.zeros(2, dtype=torch.float32, device=x.device)
+        f8.amax_into(xc, st[0])
+        qx = f8.cast(xc, st[0], E4M3_MAX, st[1])
+        return f8.grouped_mm_fp8(qx, qweight, st[1], w_scale, offsets.to(torch.int32))
+    w = (qweight.view(torch.float8_e4m3fn).float() / w_scale[:, None, None]).to(x.dtype)
+    outs, start = [], 0
+    for g, end in enumerate(offsets.tolist()):
+        outs.append(x[start:end] @ w[g].t())
+        start = end
+    return torch.cat(outs) if outs else x.new_empty((0, N))
+
+
+@fp8_grouped_mm_inference.register_fake
+def _fp8_grouped_fake(x, qweight, w_scale, offsets):
+    return x.new_empty((x.shape[0], qweight.shape[1]))
+
+
+def _g_setup(ctx, inputs, output):
+    x, qweight, w_scale, offsets = inputs
+    ctx.save_for_backward(qweight, w_scale, offsets)
+
+
+def _g_backward(ctx, g):
+    qweight, w_scale, offsets = ctx.saved_tensors
+    w = (qweight.view(torch.float8_e4m3fn).float() / w_scale[:, None, None]).to(g.dtype)  # [G, N, K]
+    gx, start = [], 0
+    for e, end in enumerate(offsets.tolist()):
+        gx.append(g[start:end] @ w[e])
+        start = end
+    return (torch.cat(gx) if gx else g.new_empty((0, w.shape[2]))), None, None, None
+
+
+fp8_grouped_mm_inference.register_autograd(_g_backward, setup_context=_g_setup)
+
+
+class _FP8GroupedForward:
+    def __init__(self, mod):
+        self.mod = mod
+
+    def __call__(self, x, offsets):
+        m = self.mod
+        return fp8_grouped_mm_inference(x, m.fp8_weight, m.fp8_scale, offsets)
+
+
 class _FP8Forward:
     def __init__(self, mod):
         self.mod = mod
@@ -104,7 +169,20 @@ class FP8InferenceTransform(Transform):
         self.quantized: list[str] = []
 
     def transform_module(self, model) -> None:
+        from ..models.llama4_moe import GroupedLinear
+
         for name, m in model._model.named_modules():
+            if isinstance(m, GroupedLinear) and not hasattr(m, "fp8_weight"):
+                if (self.modules is not None and name not in self.modules) or any(name.endswith(s) for s in self.skip):
+                    continue
+                q, s = quantize_experts_e4m3(m.weight)
+                dev = m.weight.device
+                del m.weight
+                m.register_buffer("fp8_weight", q.to(dev))
+                m.register_buffer("fp8_scale", s.to(dev))
+                m.forward = _FP8GroupedForward(m)
+                self.quantized.append(name)
+                continue
             if not isinstance(m, torch.nn.Linear) or hasattr(m, "fp8_weight"):
                 continue
             if self.modules is not None and name not in self.modules:
@@ -123,7 +201,8 @@ class FP8InferenceTransform(Transform):
         if submodule_name not in self.quantized or "weight" not in state_dict:
             return state_dict
         sd = dict(state_dict)
-        sd["fp8_weight"], sd["fp8_scale"] = quantize_weight_e4m3(sd.pop("weight"))
+        w = sd.pop("weight")
+        sd["fp8_weight"], sd["fp8_scale"] = quantize_experts_e4m3(w) if w.ndim == 3 else quantize_weight_e4m3(w)
         return sd
 
 

@@ -584,6 +584,30 @@ def test_fp8_inference_linear_gpu(M):
     assert err < 0.06, err
 
 
+@pytest.mark.gpu
+def test_fp8_grouped_mm_inference_gpu():
+    """Grouped fp8 MoE GEMM (lta_gemm_grouped_nt_fp8): ragged expert groups incl. an empty one,
+    against the fp32 product with the dequantized experts and the fp8-quantized activations."""
+    from lightning_thunder_amd.transforms.fp8_inference import fp8_grouped_mm_inference, quantize_experts_e4m3
+
+    torch.manual_seed(0)
+    G, N, K = 4, 512, 768
+    w = torch.randn(G, N, K, device="cuda") / K ** 0.5
+    q, s = quantize_experts_e4m3(w)
+    sizes = [300, 0, 37, 700]
+    offs = torch.tensor(sizes, device="cuda").cumsum(0).to(torch.int32)
+    x = torch.randn(sum(sizes), K, device="cuda", dtype=torch.bfloat16)
+    y = fp8_grouped_mm_inference(x, q, s, offs)
+    deq = q.view(torch.float8_e4m3fn).float() / s[:, None, None]
+    ref, start = [], 0
+    for g, n in enumerate(sizes):
+        ref.append(x[start:start + n].float() @ deq[g].t())
+        start += n
+    ref = torch.cat(ref)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 0.05
+
+
 def _decode_sdpa_ref(q, k, v, mask, causal, scale):
     qf, kf, vf = q.float(), k.float(), v.float()
     rep = q.shape[1] // k.shape[1]

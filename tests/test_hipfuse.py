@@ -44,7 +44,7 @@ def _log_softmax_nll(x):
 
 
 def _bias_grad(dy):
-    return dy.float().sum(0).to(dy.dtype) * 0.5
+    return (dy * 0.5).sum(0)
 
 
 def _ln_dgamma_dbeta(dy, x, mean, rstd):

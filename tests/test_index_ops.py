@@ -66,6 +66,8 @@ def test_cumsum(dtype, shape, dim):
     if dtype in (torch.int32, torch.int64):
         assert y.dtype == torch.int64
         assert torch.equal(y, torch.cumsum(x, dim, dtype=torch.int64))
+        y32 = index_ops.cumsum(x, dim, torch.int32)  # MoE routing offsets are int32
+        assert y32.dtype == torch.int32 and torch.equal(y32, torch.cumsum(x, dim, dtype=torch.int32))
     else:
         ref = torch.cumsum(x.double(), dim)
         assert y.dtype == dtype

@@ -187,6 +187,47 @@ def test_custom_op_traced_with_autograd():
     x.grad = None
     f(x).backward()
     torch.testing.assert_close(g, x.grad)
+    # the op is its own symbol (custom_op executor), and the backward calls the registered
+    # backward on exactly what setup_context saved -- the forward is not re-run
+    fw = str(thunder.last_traces(jf)[-1])
+    bw = str(thunder.last_backward_traces(jf)[-1])
+    assert "custom_op_lta_test_scaled_sin" in fw, fw
+    assert "custom_op_bwd_lta_test_scaled_sin" in bw and "custom_op_lta_test_scaled_sin(" not in bw, bw
+
+
+def test_custom_op_saves_output_and_computed_attrs():
+    """setup_context saving the OUTPUT and a computed non-tensor attribute (reference
+    thunder/tests/test_torch_library_custom_op.py)."""
+    calls = {"fwd": 0}
+
+    @torch.library.custom_op("lta_test::exp_cast", mutates_args=())
+    def exp_cast(x: torch.Tensor) -> torch.Tensor:
+        calls["fwd"] += 1
+        return torch.exp(x)
+
+    @exp_cast.register_fake
+    def _(x):
+        return torch.empty_like(x)
+
+    def setup(ctx, inputs, output):
+        ctx.save_for_backward(output)
+        ctx.in_dtype = inputs[0].dtype
+        ctx.scale = inputs[0].shape[-1] * 0 + 2.0
+
+    def bwd(ctx, g):
+        (y,) = ctx.saved_tensors
+        return (g * y * (ctx.scale / 2.0)).to(ctx.in_dtype)
+
+    exp_cast.register_autograd(bwd, setup_context=setup)
+
+    x = torch.randn(3, 4, requires_grad=True)
+    jf = thunder.jit(lambda x: exp_cast(x * 0.5).sum())
+    jf(x).backward()
+    assert calls["fwd"] == 1  # executed once: the backward does not re-run the forward
+    g = x.grad.clone()
+    x.grad = None
+    exp_cast(x * 0.5).sum().backward()
+    torch.testing.assert_close(g, x.grad)
 
 
 def test_examine_patterns_and_memory(capsys):
@@ -243,6 +284,31 @@ def test_fp8_inference_transform_cpu():
     out.sum().backward()
     assert x.grad is not None
     assert any("fp8_linear_inference" in b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols)
+
+
+def test_fp8_inference_transform_moe_experts_cpu():
+    """Grouped experts are quantized per expert (te_groupedmm_fp8 counterpart) and traced as the
+    grouped fp8 custom op; the CPU path matches the model within fp8 error."""
+    from lightning_thunder_amd.models.llama4_moe import Llama4MoE, MoEConfig
+    from lightning_thunder_amd.transforms.fp8_inference import FP8InferenceTransform, quantize_experts_e4m3
+
+    torch.manual_seed(0)
+    w = torch.randn(4, 32, 16)
+    w[2] *= 100.0  # one expert with a far larger range: per-expert scales keep the others precise
+    q, s = quantize_experts_e4m3(w)
+    assert q.shape == w.shape and s.shape == (4,)
+    deq = q.view(torch.float8_e4m3fn).float() / s[:, None, None]
+    assert ((deq - w).abs().amax(dim=(1, 2)) / w.abs().amax(dim=(1, 2))).max() < 0.07
+    m = Llama4MoE(MoEConfig(hidden_size=64, intermediate_size=128, num_routed_experts=4))
+    x = torch.randn(2, 8, 64)
+    ref = m(x)
+    t = FP8InferenceTransform(skip=())
+    jm = thunder.jit(m, transforms=[t])
+    out = jm(x)
+    assert any(n.endswith("routed_experts.gate_proj") for n in t.quantized)
+    assert (out - ref).abs().max() / ref.abs().max() < 0.15
+    names = [b.sym.name for b in thunder.last_traces(jm)[-1].bound_symbols]
+    assert any("fp8_grouped_mm_inference" in n for n in names), names
 
 
 def test_numerics_check_transform_cpu():
