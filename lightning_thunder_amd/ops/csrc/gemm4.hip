@@ -93,7 +93,6 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
 template <bool MN>
 struct Stager {
   i32x4 rsrc;
-  __amdgpu_buffer_rsrc_t brsrc;  // the same descriptor for the compiler-visible register loads
   int voff0, voff1;      // K-major: voff0 for every i; MN-major: even / odd i
   int istride, kstride;  // bytes between consecutive i / consecutive K-tiles
   // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length
@@ -103,7 +102,6 @@ struct Stager {
       // which holds logical chunk (lane & 7) ^ row & 7
       const __hip_bfloat16* base = X + (int64_t)r0 * ld;
       rsrc = make_rsrc(base, (BM - 1) * ld * 2 + K * 2);
-      brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (BM - 1) * ld * 2 + K * 2, 0x00020000);
       const int r = lane >> 3, c = (lane & 7) ^ r;
       voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
       voff1 = voff0;
@@ -114,7 +112,6 @@ struct Stager {
       // lane & 31 holding logical chunk (lane & 31) ^ tr_swz(k-row); tr_swz flips bit 3 with i & 1
       const __hip_bfloat16* base = X + r0;
       rsrc = make_rsrc(base, (K - 1) * ld * 2 + BM * 2);
-      brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (K - 1) * ld * 2 + BM * 2, 0x00020000);
       const int half = lane >> 5, slot = lane & 31;
       const int kr = 2 * wave + half;  // k-row for i = 0
       const int c0 = slot ^ tr_swz(kr);
@@ -130,14 +127,6 @@ struct Stager {
                  :
                  : "s"(dst), "v"((MN && (i & 1)) ? voff1 : voff0), "s"(rsrc), "s"(i * istride + kt * kstride)
                  : "memory", "m0");
-  }
-  // register staging (VAR 3): the same 1-KiB piece into four VGPRs; written to LDS lane-linearly
-  // later by put(), so the LDS image is byte-identical to the LDS-DMA one
-  __device__ __forceinline__ i32x4 gload(int i, int kt) const {
-    return __builtin_amdgcn_raw_buffer_load_b128(brsrc, (MN && (i & 1)) ? voff1 : voff0, i * istride + kt * kstride, 0);
-  }
-  __device__ __forceinline__ static void put(char* img, int i, int wave, int lane, const i32x4& v) {
-    *reinterpret_cast<i32x4*>(img + (i * 4 + wave) * 1024 + lane * 16) = v;
   }
 };
 
@@ -233,36 +222,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   };
 
   // glds split: NB2 instructions of tile t+2 in phase B2 of tile t, the rest (16 - NB2) in the first
-  // half of phase A of tile t+1.  VAR 3 stages through registers instead (no LDS-DMA at all).
-  constexpr bool REG = VAR == 3;
-  constexpr int NB2 = REG ? 0 : (VAR == 0 ? 16 : (VAR == 1 ? 8 : 4));
-  constexpr int NA = REG ? 0 : 16 - NB2;
-  i32x4 stg[16];  // VAR 3: the next K-tile's 16 pieces (A: 0..7, B: 8..15)
-  auto gload = [&](int j, int kt) { stg[j] = j < 8 ? sa.gload(j, kt) : sb.gload(j - 8, kt); };
-  auto put = [&](int j, char* stage) {
-    if (j < 8)
-      Stager<AT>::put(stage, j, wave, lane, stg[j]);
-    else
-      Stager<BT>::put(stage + OP_BYTES, j - 8, wave, lane, stg[j]);
-  };
+  // half of phase A of tile t+1.  (Staging through registers + ds_write_b128 instead of LDS-DMA
+  // was measured 5-10 % slower for K-major operands and 35-50 % slower for the wgrad layout,
+  // where its 64 staging VGPRs spill: profiles/gemm4_microbench.json history, round 3.)
+  constexpr int NB2 = VAR == 0 ? 16 : (VAR == 1 ? 8 : 4);
+  constexpr int NA = 16 - NB2;
 
   const int nk = K / BK;
   // ---- prologue: tile 0 whole, tile 1's phase-B2 share; wait for tile 0 ----
-  if constexpr (REG) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) gload(j, 0);
+  for (int j = 0; j < 16; ++j) glds(j, 0, smem);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) put(j, smem);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) gload(j, min(1, nk - 1));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) glds(j, 0, smem);
-#pragma unroll
-    for (int j = 0; j < NB2; ++j) glds(j, 1, smem + STAGE);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB2) : "memory");
-  }
+  for (int j = 0; j < NB2; ++j) glds(j, 1, smem + STAGE);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB2) : "memory");
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int r = 0; r < 16; ++r) read_one(smem, 0, r, fa0, fb0);
@@ -275,21 +247,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     char* const bc = smem + CUR * STAGE;
     char* const bn = smem + (CUR ^ 1) * STAGE;
     const int t1 = min(t + 1, nk - 1), t2 = min(t + 2, nk - 1);
-    (void)t1;
     // phase A: k-step 0 of tile t from (fa0, fb0); read k-step 1; finish tile t+1's staging
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
       mfma16(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
       if ((i & 3) == 0) read_one(bc, 1, i >> 2, fa1, fb1);
       if (NA > 0 && (i & 3) == 2 && (i >> 2) < NA) glds(NB2 + (i >> 2), t1, bn);
-      if constexpr (REG) {
-        // tile t+1 (in registers since the previous tile) -> its LDS buffer, then the register
-        // reloads with tile t+2: a whole K-tile of MFMAs hides the load latency
-        if ((i & 3) == 2) {
-          put(i >> 2, bn);
-          gload(i >> 2, t2);
-        }
-      }
       LTA_FENCE();
     }
     // phase B1: rows 0..3 of k-step 1
@@ -299,10 +262,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
       LTA_FENCE();
     }
     // tile t+1 has landed for this wave and tile t is fully read by it; then for everyone
-    if constexpr (REG)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the t+2 register loads stay in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     LTA_FENCE();
     // phase B2: rows 4..7 of k-step 1; read k-step 0 of tile t+1; stage tile t+2 into this buffer
@@ -443,7 +403,6 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   return launch4<kNone, true, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);
   if (variant == 0) { LTA_G4V(0) }
   if (variant == 2) { LTA_G4V(2) }
-  if (variant == 3) { LTA_G4V(3) }
 #undef LTA_G4V
   return -1;
 }

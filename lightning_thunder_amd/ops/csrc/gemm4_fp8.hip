@@ -1,0 +1,228 @@
+// K8 (v2): FP8 (OCP e4m3 / e5m2) NT GEMM, C[M,N] bf16 = (A . B^T) / (sa * sb) (+ bias), one 256x256
+// output tile per 4-wave workgroup on v_mfma_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate).
+// (reference: TransformerEngine's cuBLASLt FP8 GEMMs, thunder/executors/transformer_engineex_impl.py)
+//
+// Same skeleton as csrc/gemm4.hip (one wave per SIMD, 128x128 per wave in 256 AGPR accumulators,
+// LDS-DMA staging through buffer resources issued as inline asm, XCD-aware bijective tile map),
+// re-timed for the fp8 MFMA, whose K of 128 makes one K-tile (128-B rows, the bf16 kernel's LDS
+// image byte for byte) a single k-step:
+//
+//   top of tile t:  vmcnt(0) lgkmcnt(0), s_barrier   (tile t+1 landed; every wave holds tile t's
+//                                                      fragments, so tile t's buffer is free)
+//   rows 0..7 of 8 MFMAs (32 cycles each) on the fragments of tile t (registers):
+//     rows 0..3: the 16 LDS-DMA pieces of tile t+2 into tile t's buffer, one per 2 MFMAs
+//     row m >= 1: read tile t+1's A fragment m-1 (its register's last use was row m-1)
+//     row 7: after MFMA (7, n) read tile t+1's B fragment n, after (7, 7) A fragment 7
+//
+// so the DMA of a tile has a whole tile (2048 MFMA cycles) to land and every LDS read overlaps
+// MFMAs.  A fragment of the 16x16x128 operand is 32 B per lane: 16-B chunks g and 4 + g of its
+// 128-B row (g = lane >> 4); A and B use the same k assignment, so the sum over k is exact.
+#include "common.h"
+
+using namespace lta;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 256, BN = 256, BKB = 128, NTHR = 256;
+constexpr int OP_BYTES = BM * BKB;    // 32 KiB per operand per stage
+constexpr int STAGE = 2 * OP_BYTES;   // 64 KiB
+
+__device__ __forceinline__ int xcd_tile(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), bytes, 0x00020000};
+}
+
+// K-major operand rows of 128 B per K-tile: instruction i (0..7) of wave w fills LDS bytes
+// [(4i + w) KiB, +1 KiB) = rows 8(4i + w) .. +7; lane -> row + (lane >> 3), stored chunk lane & 7
+// holding logical chunk (lane & 7) ^ (row & 7).
+struct StagerB {
+  i32x4 rsrc;
+  int voff, istride;
+  __device__ __forceinline__ void init(const char* X, int ld, int r0, int K, int wave, int lane) {
+    const char* base = X + (int64_t)r0 * ld;
+    rsrc = make_rsrc(base, (BM - 1) * ld + K);
+    const int r = lane >> 3, c = (lane & 7) ^ r;
+    voff = (wave * 8 + r) * ld + c * 16;
+    istride = 32 * ld;
+  }
+  __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(dst), "v"(voff), "s"(rsrc), "s"(i * istride + kt * BKB)
+                 : "memory", "m0");
+  }
+};
+
+__device__ __forceinline__ v8i read_frag8(const char* img, int row, int g) {
+  const uint4 lo = *reinterpret_cast<const uint4*>(img + row * 128 + ((g ^ (row & 7)) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(img + row * 128 + (((4 + g) ^ (row & 7)) << 4));
+  return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+template <int FA, int FB>
+__device__ __forceinline__ void mfma8(f32x4& acc, const v8i& a, const v8i& b) {
+  if constexpr (FA == 0 && FB == 0)
+    asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else if constexpr (FA == 1 && FB == 0)
+    asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0 cbsz:1" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0 blgp:1" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+#define LTA_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+template <int FA, int FB, bool BIAS>
+__global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                           __hip_bfloat16* __restrict__ C,
+                                                           const __hip_bfloat16* __restrict__ bias, int M, int N,
+                                                           int K, int lda, int ldb, int ldc,
+                                                           const float* __restrict__ sa,
+                                                           const float* __restrict__ sb) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  StagerB st_a, st_b;
+  st_a.init(A, lda, m0, K, wave, lane);
+  st_b.init(B, ldb, n0, K, wave, lane);
+  auto glds = [&](int j, int kt, char* stage) {
+    if (j < 8)
+      st_a.issue(j, kt, stage, wave);
+    else
+      st_b.issue(j - 8, kt, stage + OP_BYTES, wave);
+  };
+  const int arow = wm * 128 + fr, brow = wn * 128 + fr;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  v8i fa[8], fb[8];
+
+  const int nk = K / BKB;
+  // ---- prologue: tiles 0 and 1 in flight, tile 0's fragments into registers ----
+#pragma unroll
+  for (int j = 0; j < 16; ++j) glds(j, 0, smem);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) glds(j, 1, smem + STAGE);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int m = 0; m < 8; ++m) fa[m] = read_frag8(smem, arow + m * 16, fg);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) fb[n] = read_frag8(smem + OP_BYTES, brow + n * 16, fg);
+
+  auto body = [&](int t, auto cur_c) {
+    constexpr int CUR = decltype(cur_c)::value;
+    char* const bc = smem + CUR * STAGE;
+    char* const bn = smem + (CUR ^ 1) * STAGE;
+    const int t2 = min(t + 2, nk - 1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    LTA_FENCE();
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const int m = i >> 3, n = i & 7;
+      mfma8<FA, FB>(acc[m][n], fa[m], fb[n]);
+      if (i < 32 && (i & 1) == 0) glds(i >> 1, t2, bc);
+      if (m >= 1 && n == 0) fa[m - 1] = read_frag8(bn, arow + (m - 1) * 16, fg);
+      if (m == 7) fb[n] = read_frag8(bn + OP_BYTES, brow + n * 16, fg);
+      if (i == 63) fa[7] = read_frag8(bn, arow + 7 * 16, fg);
+      LTA_FENCE();
+    }
+  };
+  // nk is even (K % 256 == 0, checked by the host)
+  for (int t = 0; t < nk; t += 2) {
+    body(t, std::integral_constant<int, 0>{});
+    body(t + 1, std::integral_constant<int, 1>{});
+  }
+
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue: alpha = 1 / (sa * sb), + bias, -> swizzled bf16 image per wave -> 16-B stores ----
+  const float alpha = 1.f / (*sa * *sb);
+  char* wbuf = smem + wave * (128 * 256);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int col = n * 16 + fr;
+    float bv = 0.f;
+    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 128 + col]);
+    const int ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + fg * 4 + j;
+        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4) + co) =
+            __float2bfloat16(acc[m][n][j] * alpha + bv);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int id = it * 64 + lane;
+    const int row = id >> 4, ch = id & 15;
+    const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+    *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * ldc + n0 + wn * 128 + ch * 8) = v;
+  }
+}
+
+#undef LTA_FENCE
+
+}  // namespace
+
+// C[M,N] bf16 = (A . B^T) / (*sa * *sb) (+ bias); A [M,K], B [N,K] fp8 as bytes (row pitches lda /
+// ldb in bytes), fmt 0 = e4m3fn, 1 = e5m2 (e5m2 on one operand at most).  M, N % 256 == 0,
+// K % 256 == 0, 16-B aligned rows, operands under 2 GiB.
+LTA_EXPORT int lta_gemm4_fp8(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                             int ldb, int ldc, int fmt_a, int fmt_b, const void* sa, const void* sb,
+                             hipStream_t stream) {
+  if (M % BM || N % BN || K % (2 * BKB) || M <= 0 || N <= 0 || lda % 16 || ldb % 16 || ldc % 8) return -2;
+  if ((int64_t)M * lda >= (1ll << 31) || (int64_t)N * ldb >= (1ll << 31)) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_G8(FA, FB, BI)                                                                                       \
+  hipLaunchKernelGGL((gemm4_fp8_kernel<FA, FB, BI>), grid, block, 0, stream, (const char*)A, (const char*)B,      \
+                     (__hip_bfloat16*)C, (const __hip_bfloat16*)bias, M, N, K, lda, ldb, ldc, (const float*)sa, \
+                     (const float*)sb)
+  const bool bi = bias != nullptr;
+  if (fmt_a == 0 && fmt_b == 0) { if (bi) LTA_G8(0, 0, true); else LTA_G8(0, 0, false); }
+  else if (fmt_a == 1 && fmt_b == 0) { if (bi) LTA_G8(1, 0, true); else LTA_G8(1, 0, false); }
+  else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_G8(0, 1, true); else LTA_G8(0, 1, false); }
+  else return -1;
+#undef LTA_G8
+  return (int)hipGetLastError();
+}

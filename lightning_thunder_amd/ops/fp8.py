@@ -57,16 +57,32 @@ def cast_transpose(x2d: torch.Tensor, amax: torch.Tensor, fmax: float, scale_out
     return y, yt
 
 
+register_signature("lta_gemm4_fp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, c_int, c_int, c_void_p, c_void_p, c_void_p])
+
+
+def gemm4_fp8_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """The 4-wave fp8 kernel (csrc/gemm4_fp8.hip): M, N % 256, K % 256, 16-B aligned rows."""
+    M, K = a.shape
+    N = b.shape[0]
+    return (M % 256 == 0 and N % 256 == 0 and K % 256 == 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.stride(0) % 16 == 0 and b.stride(0) % 16 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and M * a.stride(0) < 2**31 and N * b.stride(0) < 2**31)
+
+
 def gemm_nt_fp8(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int = 0, fmt_b: int = 0,
                 bias: torch.Tensor | None = None) -> torch.Tensor:
-    """bf16 [M, N] = (a [M,K] . b[N,K]^T) / (sa * sb) (+ bias); a/b fp8 as uint8, sa/sb device scalars."""
+    """bf16 [M, N] = (a [M,K] . b[N,K]^T) / (sa * sb) (+ bias); a/b fp8 as uint8, sa/sb device scalars.
+    The 4-wave pipelined kernel (gemm4_fp8) when the shape tiles, else the 8-wave one (gemm.hip)."""
     lib = require()
     M, K = a.shape
     N = b.shape[0]
     out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    check(lib.lta_gemm_nt_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), None if bias is None else bias.data_ptr(), M,
-                              N, K, a.stride(0), b.stride(0), out.stride(0), fmt_a, fmt_b, sa.data_ptr(), sb.data_ptr(),
-                              stream_ptr(a.device)), "lta_gemm_nt_fp8")
+    fn, name = ((lib.lta_gemm4_fp8, "lta_gemm4_fp8") if gemm4_fp8_supported(a, b)
+                else (lib.lta_gemm_nt_fp8, "lta_gemm_nt_fp8"))
+    check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), None if bias is None else bias.data_ptr(), M, N, K,
+             a.stride(0), b.stride(0), out.stride(0), fmt_a, fmt_b, sa.data_ptr(), sb.data_ptr(), stream_ptr(a.device)),
+          name)
     return out
 
 

@@ -337,15 +337,18 @@ def test_gemm_bf16_layouts(layout, shape, residual):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fmts", [(0, 0), (1, 0)])
-def test_gemm_nt_fp8(fmts):
+@pytest.mark.parametrize("fmts", [(0, 0), (1, 0), (0, 1)])
+@pytest.mark.parametrize("shape", [(512, 768, 1024), (512, 768, 1152), (1024, 512, 4096)])
+def test_gemm_nt_fp8(fmts, shape):
+    """fp8 NT GEMM: K % 256 shapes on the 4-wave kernel (gemm4_fp8), K = 1152 on the 8-wave one."""
     from lightning_thunder_amd.ops.fp8 import gemm_nt_fp8
 
     torch.manual_seed(0)
-    M, N, K = 512, 768, 1024
+    M, N, K = shape
     da = torch.float8_e5m2 if fmts[0] else torch.float8_e4m3fn
+    db = torch.float8_e5m2 if fmts[1] else torch.float8_e4m3fn
     a8 = torch.randn(M, K, device="cuda").to(da)
-    b8 = torch.randn(N, K, device="cuda").to(torch.float8_e4m3fn)
+    b8 = torch.randn(N, K, device="cuda").to(db)
     sa, sb = torch.tensor(2.0, device="cuda"), torch.tensor(4.0, device="cuda")
     bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
     out = gemm_nt_fp8(a8.view(torch.uint8), b8.view(torch.uint8), sa, sb, fmts[0], fmts[1], bias)
