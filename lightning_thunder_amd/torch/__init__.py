@@ -1784,3 +1784,4 @@ def checkpoint(function, *args, **kwargs):
 
 from . import default_torch_ops  # noqa: E402,F401  (auto-registration of the long tail)
 from . import nn_ops  # noqa: E402,F401  (conv / pooling / normalization / activation decompositions)
+from . import more_ops  # noqa: E402,F401  (losses, special functions, products, scans, shape utilities)
