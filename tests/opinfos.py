@@ -652,3 +652,155 @@ OPS += [
 ]
 
 OPS_BY_NAME = {o.name: o for o in OPS}
+
+
+# =========================================================================================
+# torch/more_ops.py: losses, special functions, products, scans and shape utilities
+# =========================================================================================
+def _pair(shape_a, shape_b, low=-2.0, high=2.0, lb=None, hb=None):
+    def gen(device, dtype, requires_grad):
+        yield SampleInput((_t(shape_a, device, dtype, requires_grad, low, high),
+                           _t(shape_b, device, dtype, requires_grad, low if lb is None else lb,
+                              high if hb is None else hb)))
+
+    return gen
+
+
+def _loss_samples(target="normal", extra=({},)):
+    def gen(device, dtype, requires_grad):
+        x = _t((3, 5), device, dtype, requires_grad)
+        if target == "sign":
+            y = torch.where(torch.rand(3, 5, device=device) > 0.5, 1.0, -1.0).to(dtype)
+        elif target == "prob":
+            y = _t((3, 5), device, dtype, False, 0.05, 0.95)
+        elif target == "binary":
+            y = (torch.rand(3, 5, device=device) > 0.5).to(dtype)
+        else:
+            y = _t((3, 5), device, dtype, requires_grad)
+        for kw in extra:
+            yield SampleInput((x, y), dict(kw))
+
+    return gen
+
+
+def _prob_input_loss(device, dtype, requires_grad):
+    p = _t((3, 5), device, dtype, requires_grad, 0.05, 0.95)
+    y = (torch.rand(3, 5, device=device) > 0.5).to(dtype)
+    yield SampleInput((p, y))
+    yield SampleInput((p, y), {"reduction": "sum"})
+
+
+def _three(shapes, low=-2.0, high=2.0):
+    def gen(device, dtype, requires_grad):
+        yield SampleInput(tuple(_t(s, device, dtype, requires_grad, low, high) for s in shapes))
+
+    return gen
+
+
+def _cosemb_samples(device, dtype, requires_grad):
+    a, b = _t((4, 6), device, dtype, requires_grad), _t((4, 6), device, dtype, requires_grad)
+    yield SampleInput((a, b, torch.tensor([1.0, -1.0, 1.0, -1.0], device=device, dtype=dtype)), {"margin": 0.1})
+
+
+def _mrank_samples(device, dtype, requires_grad):
+    a, b = _t((6,), device, dtype, requires_grad), _t((6,), device, dtype, requires_grad)
+    yield SampleInput((a, b, torch.tensor([1.0, -1.0, 1.0, -1.0, 1.0, 1.0], device=device, dtype=dtype)))
+
+
+def _gnll_samples(device, dtype, requires_grad):
+    x, y = _t((3, 5), device, dtype, requires_grad), _t((3, 5), device, dtype, requires_grad)
+    yield SampleInput((x, y, _t((3, 5), device, dtype, requires_grad, 0.2, 2.0)))
+    yield SampleInput((x, y, _t((3, 1), device, dtype, requires_grad, 0.2, 2.0)), {"full": True})
+
+
+def _list_samples(shapes):
+    def gen(device, dtype, requires_grad):
+        yield SampleInput(([_t(s, device, dtype, requires_grad) for s in shapes],))
+
+    return gen
+
+
+OPS += [
+    # losses / distances
+    OpInfo("smooth_l1_loss", F.smooth_l1_loss, _loss_samples(extra=({}, {"beta": 0.5}, {"reduction": "none"}))),
+    OpInfo("huber_loss", F.huber_loss, _loss_samples(extra=({}, {"delta": 0.3}, {"reduction": "sum"}))),
+    OpInfo("binary_cross_entropy", lambda p, y, **kw: F.binary_cross_entropy(p, (y > 0.5).to(p.dtype), **kw),
+           _prob_input_loss, atol=3e-2, rtol=3e-2),
+    OpInfo("kl_div", lambda x, y: F.kl_div(x.log_softmax(-1), y, reduction="batchmean"), _loss_samples("prob")),
+    OpInfo("kl_div_log_target", lambda x, y: F.kl_div(x, y, reduction="sum", log_target=True), _loss_samples()),
+    OpInfo("poisson_nll_loss", F.poisson_nll_loss, _loss_samples("prob", ({}, {"full": True}))),
+    OpInfo("soft_margin_loss", lambda x, y: F.soft_margin_loss(x, y.sign().detach()), _loss_samples("sign")),
+    OpInfo("hinge_embedding_loss", lambda x, y: F.hinge_embedding_loss(x, y.sign()), _loss_samples("sign")),
+    OpInfo("multilabel_soft_margin_loss", F.multilabel_soft_margin_loss, _loss_samples("binary")),
+    OpInfo("margin_ranking_loss", lambda a, b, t: F.margin_ranking_loss(a, b, t.sign()), _mrank_samples),
+    OpInfo("cosine_embedding_loss", lambda a, b, t, **kw: F.cosine_embedding_loss(a, b, t.sign(), **kw), _cosemb_samples, atol=3e-2, rtol=3e-2),
+    OpInfo("gaussian_nll_loss", F.gaussian_nll_loss, _gnll_samples, atol=3e-2, rtol=3e-2),
+    OpInfo("cosine_similarity", F.cosine_similarity, _pair((4, 6), (4, 6))),
+    OpInfo("pairwise_distance", F.pairwise_distance, _pair((4, 6), (4, 6)), atol=3e-2, rtol=3e-2),
+    OpInfo("triplet_margin_loss", F.triplet_margin_loss, _three([(4, 6)] * 3), atol=3e-2, rtol=3e-2),
+    # elementwise special functions
+    elementwise_binary("logaddexp", torch.logaddexp, samples=_pair((3, 4), (3, 4))),
+    elementwise_binary("logaddexp2", torch.logaddexp2, samples=_pair((3, 4), (4,))),
+    elementwise_binary("xlogy", torch.xlogy, samples=_pair((3, 4), (3, 4), lb=0.1, hb=3.0)),
+    elementwise_binary("xlog1py", torch.special.xlog1py, samples=_pair((3, 4), (3, 4), lb=0.1, hb=3.0)),
+    elementwise_binary("hypot", torch.hypot, samples=_pair((3, 4), (3, 4))),
+    elementwise_binary("fmax", torch.fmax, samples=_pair((3, 4), (3, 4))),
+    elementwise_binary("fmin", torch.fmin, samples=_pair((3, 4), (3, 4))),
+    elementwise_unary("logit", lambda x: torch.logit(x, 1e-3), 0.05, 0.95),
+    elementwise_unary("sinc", torch.sinc),
+    elementwise_unary("deg2rad", torch.deg2rad),
+    elementwise_unary("rad2deg", torch.rad2deg),
+    elementwise_unary("frac", torch.frac),
+    elementwise_unary("positive", torch.positive),
+    elementwise_unary("erfcx", torch.special.erfcx, 0.0, 2.0, dtypes=FLOAT32),
+    elementwise_unary("float_power", lambda x: torch.float_power(x, 2.5), 0.1, 2.0, dtypes=FLOAT32),
+    elementwise_unary("isposinf", lambda x: torch.isposinf(1.0 / x.round()), differentiable=False),
+    elementwise_unary("isneginf", lambda x: torch.isneginf(1.0 / x.round()), differentiable=False),
+    elementwise_binary("isclose", lambda a, b: torch.isclose(a, a + b * 1e-9), samples=_pair((3, 4), (3, 4)),
+                       differentiable=False),
+    elementwise_binary("heaviside", torch.heaviside, samples=_pair((3, 4), (3, 4)), dtypes=FLOAT32,
+                       differentiable=False),
+    # reductions / scans
+    OpInfo("nansum", torch.nansum, reduction_samples(dims=(None, 1))),
+    OpInfo("nanmean", torch.nanmean, reduction_samples(dims=(None, 0)), dtypes=FLOAT32),
+    OpInfo("count_nonzero", lambda x: torch.count_nonzero(x.round(), 1), unary_samples(shapes=[(3, 4)]),
+           differentiable=False),
+    OpInfo("cumprod", lambda x: torch.cumprod(x, 1), unary_samples(shapes=[(3, 5)]), dtypes=FLOAT32),
+    OpInfo("logcumsumexp", lambda x: torch.logcumsumexp(x, -1), unary_samples(shapes=[(3, 5), (6,)])),
+    OpInfo("diff", lambda x: torch.diff(x, n=2), unary_samples(shapes=[(3, 6)])),
+    OpInfo("diff_prepend", lambda x: torch.diff(x, dim=0, prepend=x[:1] * 2), unary_samples(shapes=[(3, 4)])),
+    OpInfo("trace", torch.trace, unary_samples(shapes=[(4, 4), (3, 5)]), dtypes=FLOAT32),
+    # products
+    OpInfo("dot", torch.dot, _pair((6,), (6,))),
+    OpInfo("vdot", torch.vdot, _pair((6,), (6,))),
+    OpInfo("inner", torch.inner, _pair((3, 4), (5, 4))),
+    OpInfo("mv", torch.mv, _pair((3, 4), (4,))),
+    OpInfo("addmv", lambda a, m, v: torch.addmv(a, m, v, beta=0.5, alpha=2.0), _three([(3,), (3, 4), (4,)])),
+    OpInfo("addr", lambda a, u, v: torch.addr(a, u, v, alpha=0.5), _three([(3, 4), (3,), (4,)])),
+    OpInfo("addbmm", torch.addbmm, _three([(3, 5), (2, 3, 4), (2, 4, 5)])),
+    OpInfo("kron", torch.kron, _pair((2, 3), (3, 2))),
+    OpInfo("tensordot", lambda a, b: torch.tensordot(a, b, dims=([1, 2], [0, 1])), _pair((2, 3, 4), (3, 4, 5))),
+    OpInfo("bilinear", F.bilinear, _three([(3, 4), (3, 5), (2, 4, 5)]), atol=3e-2, rtol=3e-2),
+    # shape utilities
+    OpInfo("column_stack", torch.column_stack, _list_samples([(4,), (4, 2)])),
+    OpInfo("row_stack", torch.row_stack, _list_samples([(4,), (2, 4)])),
+    OpInfo("dstack", torch.dstack, _list_samples([(3, 4), (3, 4)])),
+    OpInfo("hsplit", lambda x: torch.hsplit(x, 2), unary_samples(shapes=[(3, 4)])),
+    OpInfo("vsplit", lambda x: torch.vsplit(x, [1, 3]), unary_samples(shapes=[(4, 3)])),
+    OpInfo("dsplit", lambda x: torch.dsplit(x, 2), unary_samples(shapes=[(2, 3, 4)])),
+    OpInfo("broadcast_tensors", torch.broadcast_tensors, _pair((1, 4), (3, 1))),
+    OpInfo("pixel_shuffle", lambda x: F.pixel_shuffle(x, 2), unary_samples(shapes=[(1, 8, 2, 3)])),
+    OpInfo("pixel_unshuffle", lambda x: F.pixel_unshuffle(x, 2), unary_samples(shapes=[(1, 2, 4, 6)])),
+    OpInfo("rot90", lambda x: torch.rot90(x, 1, (0, 2)), unary_samples(shapes=[(2, 3, 4)])),
+    OpInfo("rot90_neg", lambda x: torch.rot90(x, -1), unary_samples(shapes=[(3, 4)])),
+    OpInfo("tile", lambda x: torch.tile(x, (2, 1, 2)), unary_samples(shapes=[(3, 4)])),
+    OpInfo("block_diag", torch.block_diag, _pair((2, 3), (3, 2))),
+    OpInfo("cartesian_prod", torch.cartesian_prod, _pair((3,), (2,))),
+    OpInfo("meshgrid", lambda a, b: torch.meshgrid(a, b, indexing="ij"), _pair((3,), (2,))),
+    OpInfo("meshgrid_xy", lambda a, b: torch.meshgrid(a, b, indexing="xy"), _pair((3,), (2,))),
+    OpInfo("vander", lambda x: torch.vander(x, 4, increasing=True), unary_samples(shapes=[(5,)]),
+           differentiable=False),
+    OpInfo("eye_mul", lambda x: torch.eye(3, 4, dtype=x.dtype, device=x.device) * x, unary_samples(shapes=[(3, 4)])),
+]
+
+OPS_BY_NAME = {o.name: o for o in OPS}
