@@ -1223,7 +1223,7 @@ def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=Fa
     if query.dtype not in (torch.bfloat16, torch.float16) or key.dtype != query.dtype or value.dtype != query.dtype:
         return False
     D = query.shape[-1]
-    if D not in (64, 128) or key.shape[-1] != D or value.shape[-1] != D:
+    if D not in (64, 96, 128) or key.shape[-1] != D or value.shape[-1] != D:
         return False
     if key.shape[1] != value.shape[1] or query.shape[1] % key.shape[1] != 0:
         return False

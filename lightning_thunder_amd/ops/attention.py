@@ -27,7 +27,7 @@ register_signature("lta_attn_bwd_ex", [c_int, c_void_p, c_void_p, c_void_p, c_vo
                                        c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                        ctypes.c_uint64, c_void_p])
 
-SUPPORTED_HEAD_DIMS = (64, 128)
+SUPPORTED_HEAD_DIMS = (64, 96, 128)
 
 
 def prepare_mask(mask: torch.Tensor, B: int, Hq: int, Tq: int, Sk: int):

@@ -797,6 +797,173 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// dQ, D = 128, no mask / dropout (v2): the forward v2 structure (attention_fwd.hip) applied to the
+// dQ sweep — 8 waves x 32 query rows = 256 queries per workgroup, one workgroup per CU, so each
+// staged K/V tile feeds twice the queries of v1; {K rows, V rows, K transposed-read image}
+// double-buffered in LDS, register-staged one tile ahead (T14), one barrier per tile; the scale and
+// LSE fold into one FMA per score; the causal / key-edge mask runs only on a wave's last tile.
+// ---------------------------------------------------------------------------------------------
+constexpr int kBM2 = 256;
+constexpr int kThreads2 = 512;
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                      const T* __restrict__ V, const T* __restrict__ dO,
+                                                                      const float* __restrict__ LSE,
+                                                                      const float* __restrict__ DELTA, T* __restrict__ dQ,
+                                                                      int Hq, int Hkv, int Tq, int Sk, float scale,
+                                                                      float scale_log2, RowStrides sdo) {
+  constexpr int D = 128;
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  constexpr int ST = 2 * kBN * C::RSTR + kBN * C::TSTR;  // elements per stage: K rows, V rows, K image
+  __shared__ __attribute__((aligned(16))) short smem[2 * ST];
+
+  const int n_qt = (Tq + kBM2 - 1) / kBM2;
+  const int qt = n_qt - 1 - (int)blockIdx.y;
+  const int bh = blockIdx.x;
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hk = hq / (Hq / Hkv);
+  const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* dOb = dO + b * sdo.b + hq * sdo.h;
+  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  const int q0 = qt * kBM2 + wave * 32;
+  const int qi = q0 + r;
+  const int qrow = min(qi, Tq - 1);
+
+  int n_tiles = (Sk + kBN - 1) / kBN;
+  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM2 + kBM2, Tq) + kBN - 1) / kBN);
+  int nw = n_tiles;  // this wave's tiles; only tile nw-1 can need the mask
+  if (CAUSAL) nw = min(n_tiles, min(q0 + 31, Tq - 1) / kBN + 1);
+  const bool last_masked = (nw * kBN > Sk) || (CAUSAL && (nw - 1) * kBN + kBN - 1 > q0);
+
+  F qf[C::KS], of[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+    of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
+  }
+  const float nlse2 = -LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
+  const float dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
+
+  f32x16 dqacc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
+
+  uint4 pk[2], pv[2];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int id = c * kThreads2 + tid, row = id >> 4, ch = id & 15;
+      const int kc = min(t * kBN + row, Sk - 1);  // clamped rows are real keys; dS = 0 there
+      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
+      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+    }
+  };
+  auto lstore = [&](int st) {
+    short* Kr = smem + st * ST;
+    short* Vr = Kr + kBN * C::RSTR;
+    short* Kt = Vr + kBN * C::RSTR;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int id = c * kThreads2 + tid, row = id >> 4, ch = id & 15;
+      *reinterpret_cast<uint4*>(Kr + row * C::RSTR + ch * 8) = pk[c];
+      *reinterpret_cast<uint4*>(Vr + row * C::RSTR + ch * 8) = pv[c];
+      *reinterpret_cast<uint4*>(Kt + row * C::TSTR + ch * 8) = pk[c];
+    }
+  };
+
+  const int last = n_tiles - 1;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < n_tiles; ++t) {
+    gload(min(t + 1, last));  // tile t+1 in flight over tile t's math
+    if (t < nw) {
+      const short* Kr = smem + (t & 1) * ST;
+      const short* Vr = Kr + kBN * C::RSTR;
+      const __attribute__((address_space(3))) short* Kt3 =
+          (const __attribute__((address_space(3))) short*)(Vr + kBN * C::RSTR);
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sacc[kt][i] = 0.f;
+          pacc[kt][i] = 0.f;
+        }
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          sacc[kt] = mfma(load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h), qf[s], sacc[kt]);  // S^T
+          pacc[kt] = mfma(load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h), of[s], pacc[kt]);  // dP^T
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kt][i], scale_log2, nlse2));
+          pacc[kt][i] = p * (pacc[kt][i] - dlt);  // dS^T
+        }
+      if (t == nw - 1 && last_masked) {  // wave-uniform
+        const int kbase = t * kBN;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kk = kbase + kt * 32 + acc_row(i, h);
+            if (kk >= Sk || (CAUSAL && kk > qi)) pacc[kt][i] = 0.f;
+          }
+      }
+      F df[2][2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        pack_frag(df[kt][0], pacc[kt], 0);
+        pack_frag(df[kt][1], pacc[kt], 1);
+      }
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const int col0 = dt * 32 + 16 * (g & 1);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            dqacc[dt] = mfma(tr_frag<F>(Kt3, kt * 32 + 16 * s + 4 * h, col0, C::TSTR, l16), df[kt][s], dqacc[dt]);
+      }
+    }
+    lstore((t + 1) & 1);  // over tile t-1 (read before the last barrier)
+    __syncthreads();
+  }
+
+  if (qi < Tq) {
+    T* drow = dQ + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        union {
+          T v[4];
+          uint2 u;
+        } pk2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk2.v[e] = from_f32<T>(dqacc[dt][4 * a + e] * scale);
+        *reinterpret_cast<uint2*>(drow + d) = pk2.u;
+      }
+    }
+  }
+}
+
 template <typename T, int D, int EX>
 void launch_masked(const void* dO, const void* Q, const void* K, const void* V, const void* LSE, void* DELTA, void* dQ,
                    void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, float sl2, int causal,
@@ -820,6 +987,8 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DKDV
 #undef LTA_DQ
 }
+
+int g_dq_v2 = 0;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -861,14 +1030,22 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
                        sdo, ex);
   }
-  if (causal) {
+  if (!causal && !(D == 128 && dkdv_v2))
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                       sl2, sdo, ex);
+  if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
+    dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, false>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+  } else if (causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
   } else {
-    if (!(D == 128 && dkdv_v2))
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo, ex);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
   }
@@ -922,9 +1099,11 @@ LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const v
   if (dtype == kBF16) {
     if (D == 128) LTA_B(__hip_bfloat16, 128);
     if (D == 64) LTA_B(__hip_bfloat16, 64);
+    if (D == 96) LTA_B(__hip_bfloat16, 96);
   } else if (dtype == kF16) {
     if (D == 128) LTA_B(__half, 128);
     if (D == 64) LTA_B(__half, 64);
+    if (D == 96) LTA_B(__half, 96);
   }
 #undef LTA_B
   return -1;
@@ -943,4 +1122,11 @@ LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void
                             int Hkv, int Tq, int Sk, int D, float scale, int causal, hipStream_t stream) {
   return lta_attn_bwd_s(dtype, dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, workspace, B, Hq, Hkv, Tq, Sk, D, scale, causal,
                         nullptr, stream);
+}
+
+// dQ kernel selection (A/B measurement hook): 1 = v2, 0 = v1; returns the previous choice
+LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
+  const int old = g_dq_v2;
+  if (impl == 0 || impl == 1) g_dq_v2 = impl;
+  return old;
 }

@@ -74,7 +74,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("kind", ["bool_padding", "float_bias", "bool_full"])
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 96, 128])
 def test_masked_attention_fwd_bwd(kind, D):
     from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
 

@@ -147,7 +147,7 @@ def _sdpa_ref(q, k, v, causal, scale=None):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Hq,Hkv,T,S,D", [
     (2, 4, 4, 64, 64, 128), (1, 4, 2, 200, 200, 128), (2, 2, 2, 256, 256, 64), (1, 8, 1, 129, 129, 64),
-    (1, 2, 2, 96, 333, 128), (1, 32, 32, 1024, 1024, 128),
+    (1, 2, 2, 96, 333, 128), (1, 32, 32, 1024, 1024, 128), (2, 4, 2, 300, 300, 96), (1, 4, 4, 256, 256, 96),
 ])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
