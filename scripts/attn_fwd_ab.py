@@ -84,8 +84,9 @@ for (B, Hq, Hkv, T) in [(1, 4, 4, 1024), (2, 8, 2, 1000), (1, 2, 1, 77)]:
         rdq, rdk, rdv = torch.autograd.grad(ro, (q, k, v), do.float())
         lib.lta_attn_fwd_set_impl(0)
         o, lse = attn_fwd(q.detach(), k.detach(), v.detach(), causal)
-        for impl in (0, 1):
-            lib.lta_attn_bwd_set_dq_impl(impl)
+        for impl in (0, 1, 2):
+            lib.lta_attn_bwd_set_dq_impl(min(impl, 1))
+            lib.lta_attn_bwd_set_dkdv_impl(1 if impl == 2 else 0)
             dq, dk, dv = attn_bwd(do, q.detach(), k.detach(), v.detach(), o, lse, causal)
             torch.cuda.synchronize()
             key = f"B{B}_H{Hq}/{Hkv}_T{T}_{'causal' if causal else 'full'}_dq{impl}"
@@ -99,8 +100,9 @@ k, v = torch.randn_like(q), torch.randn_like(q)
 do = torch.randn(B, T, H, D, device="cuda", dtype=torch.bfloat16).transpose(1, 2)
 lib.lta_attn_fwd_set_impl(0)
 o, lse = attn_fwd(q, k, v, True)
-for impl in (0, 1, 0, 1):
-    lib.lta_attn_bwd_set_dq_impl(impl)
+for impl in (0, 1, 2, 0, 1, 2):
+    lib.lta_attn_bwd_set_dq_impl(min(impl, 1))
+    lib.lta_attn_bwd_set_dkdv_impl(1 if impl == 2 else 0)
     for _ in range(3):
         attn_bwd(do, q, k, v, o, lse, True)
     torch.cuda.synchronize()
@@ -115,5 +117,6 @@ for impl in (0, 1, 0, 1):
     out["bwd_perf"][f"causal_dq{impl}"] = {"us": round(ms * 1000, 1), "tflops_nominal": round(fl / ms / 1e9, 1),
                                            "dq_abs_sum": float(dq.float().abs().sum())}
     print("bwd", impl, out["bwd_perf"][f"causal_dq{impl}"], flush=True)
-lib.lta_attn_bwd_set_dq_impl(1)
+lib.lta_attn_bwd_set_dq_impl(0)
+lib.lta_attn_bwd_set_dkdv_impl(0)
 json.dump(out, open("gpurun_out/attn_fwd_ab.json", "w"), indent=1)
