@@ -99,11 +99,42 @@ def _is_dynamic(gm: torch.fx.GraphModule) -> bool:
     return False
 
 
+def _is_checkpoint_hop(node) -> bool:
+    return node.op == "call_function" and _target_name(node) == "tag_activation_checkpoint"
+
+
+def _checkpoint_hop_call(body, *args, **kwargs):
+    """What a ``tag_activation_checkpoint`` node becomes inside a compiled submodule: the region
+    through ``torch.utils.checkpoint`` (the framework's checkpoint symbol recomputes it in the
+    backward; reference ``thunder/dynamo/utils.py:741-792`` checkpoint_converter)."""
+    from .. import torch as ltorch
+
+    return ltorch.checkpoint(body, *args)
+
+
+def _convert_checkpoints(gm: torch.fx.GraphModule) -> None:
+    for n in gm.graph.nodes:
+        if _is_checkpoint_hop(n):
+            n.target = _checkpoint_hop_call
+            n.kwargs = {}
+    gm.recompile()
+
+
 def is_node_supported(node: torch.fx.Node) -> tuple[bool, SplitReason | None]:
     """Symbolically runs ``node`` through the framework's torch-function dispatch on proxies."""
     if node.op in ("placeholder", "output", "get_attr"):
         return True, None
     name = _target_name(node)
+    if _is_checkpoint_hop(node):
+        # an activation-checkpointed region is supported when every node of its body is
+        body = getattr(node.graph.owning_module, node.args[0].target, None)
+        if not isinstance(body, torch.fx.GraphModule):
+            return False, SplitReason(SplitReasonType.UNSUPPORTED_NODE, "checkpoint body is not a GraphModule")
+        for bn in body.graph.nodes:
+            ok, why = is_node_supported(bn)
+            if not ok:
+                return False, why
+        return True, None
     if name in _ALWAYS_EAGER:
         return False, SplitReason(SplitReasonType.UNSUPPORTED_NODE, f"{name} needs host values / side effects")
     if node.op == "call_module":
@@ -185,6 +216,8 @@ class ThunderCompiler:
         part, reasons = _split(gm)
         if not part:
             return gm
+        if any(_is_checkpoint_hop(n) and part[n][1] for n in gm.graph.nodes):
+            _convert_checkpoints(gm)
         compiled = []
         mapping = {}
         if all(ok for _, ok in part.values()):

@@ -92,3 +92,34 @@ def test_thunderfx_static_graph_extraction_only_prologue():
     assert any(isinstance(t, ExtractionOnlyPrologueTransform) for t in fn._lc_cd.transforms)
     pro = str(thunder.last_prologue_traces(fn)[-1])
     assert "check_tensor_shape_and_metadata" not in pro, pro
+
+
+def test_thunderfx_activation_checkpoint_region():
+    """A torch.utils.checkpoint region (dynamo's tag_activation_checkpoint higher-order op) compiles
+    into the thunder submodule and its intermediates are recomputed in the backward (reference
+    thunder/dynamo/utils.py checkpoint_converter)."""
+    from lightning_thunder_amd.dynamo import thunderfx
+
+    def f(x, w):
+        y = torch.utils.checkpoint.checkpoint(lambda a: torch.sin(a @ w).relu(), x, use_reentrant=False)
+        return (y * 2).sum()
+
+    x = torch.randn(8, 8, requires_grad=True)
+    w = torch.randn(8, 8, requires_grad=True)
+    cf = thunderfx(f)
+    out = cf(x, w)
+    out.backward()
+    x2, w2 = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_()
+    ref = f(x2, w2)
+    ref.backward()
+    torch.testing.assert_close(out, ref)
+    torch.testing.assert_close(x.grad, x2.grad)
+    torch.testing.assert_close(w.grad, w2.grad)
+    infos = cf.subgraph_infos
+    assert len(infos) == 1 and infos[0].split_graph_module is None  # no eager split
+    fwd = str(cf.last_traces[0][-1])
+    # only the two inputs are saved for the backward: the region's intermediates are recomputed
+    import re
+
+    saved = re.search(r"return \(\(.*?\), \((.*?)\), \(\)\)", fwd).group(1)
+    assert len([s for s in saved.split(",") if s.strip()]) == 2, fwd
