@@ -408,6 +408,53 @@ def _is_tensor_lookaside(interp, obj):
     return isinstance(obj, (torch.Tensor, TensorProxy))
 
 
+def _autocast_enter(interp, mgr):
+    """``with torch.autocast(...)`` inside traced code sets the trace's autocast dtype (the symbols'
+    autocast rules then apply) instead of toggling the tracing process's eager autocast state
+    (reference ``thunder/core/jit_ext.py`` autocast enter/exit lookasides)."""
+    from .trace import get_tracectx
+
+    trc = get_tracectx()
+    if trc is None:
+        return _AUTOCAST.__enter__(mgr)
+    mgr.__dict__.setdefault("_lta_prev_autocast", []).append(trc.autocast_dtype)
+    trc.autocast_dtype = mgr.fast_dtype if getattr(mgr, "_enabled", True) else None
+    return mgr
+
+
+def _autocast_exit(interp, mgr, *exc):
+    from .trace import get_tracectx
+
+    trc = get_tracectx()
+    prev = mgr.__dict__.get("_lta_prev_autocast")
+    if trc is None or not prev:
+        return _AUTOCAST.__exit__(mgr, *exc)
+    trc.autocast_dtype = prev.pop()
+    return False
+
+
+_AUTOCAST = torch.amp.autocast_mode.autocast
+_autocast_classes = [_AUTOCAST]
+for _mod, _cls in (("torch.cpu.amp", "autocast"), ("torch.cuda.amp", "autocast")):
+    try:
+        _c = getattr(__import__(_mod, fromlist=[_cls]), _cls)
+        _autocast_classes.append(_c)
+    except (ImportError, AttributeError):
+        pass
+for _c in _autocast_classes:
+    register_lookaside(_c.__enter__)(_autocast_enter)
+    register_lookaside(_c.__exit__)(_autocast_exit)
+if hasattr(torch.amp.autocast_mode, "_enter_autocast"):  # dynamo's graph-level form of the same region
+
+    @register_lookaside(torch.amp.autocast_mode._enter_autocast)
+    def _fx_enter_autocast(interp, *vals):
+        return _autocast_enter(interp, _AUTOCAST(*vals))
+
+    @register_lookaside(torch.amp.autocast_mode._exit_autocast)
+    def _fx_exit_autocast(interp, mode):
+        return _autocast_exit(interp, mode, None, None, None)
+
+
 @register_lookaside(torch.compile)
 def _torch_compile_lookaside(interp, *args, **kwargs):
     raise NotImplementedError("Using torch.compile within a function to be JIT-compiled by Thunder is not supported.")

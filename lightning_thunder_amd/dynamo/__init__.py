@@ -51,8 +51,11 @@ class SubgraphInfo:
 
 _ALWAYS_EAGER = {
     "_local_scalar_dense", "item", "tolist", "nonzero", "unique", "masked_select", "manual_seed", "set_grad_enabled",
-    "_enter_autocast", "_exit_autocast", "print",
+    "print",
 }
+# context-manager nodes: supported as a whole region (the interpreter applies the autocast inside the
+# compiled program), or the whole region runs eagerly (reference get_nodes_in_unsupported_ctx_regions)
+_CTX_ENTER, _CTX_EXIT = "_enter_autocast", "_exit_autocast"
 
 
 def _target_name(node) -> str:
@@ -112,11 +115,32 @@ def _checkpoint_hop_call(body, *args, **kwargs):
     return ltorch.checkpoint(body, *args)
 
 
-def _convert_checkpoints(gm: torch.fx.GraphModule) -> None:
+def _fx_enter_autocast(*vals):
+    """A compiled region's ``_enter_autocast`` node: sets the trace's autocast dtype."""
+    from ..core.interpreter import _AUTOCAST, _autocast_enter
+
+    return _autocast_enter(None, _AUTOCAST(*vals))
+
+
+def _fx_exit_autocast(mode):
+    from ..core.interpreter import _autocast_exit
+
+    return _autocast_exit(None, mode, None, None, None)
+
+
+def _convert_checkpoints(gm: torch.fx.GraphModule, part: dict) -> None:
+    """Rewrite the nodes a compiled submodule cannot run natively: checkpoint regions and autocast
+    enter / exit (inside a thunder submodule they set the program's autocast state)."""
     for n in gm.graph.nodes:
+        if n not in part or not part[n][1]:
+            continue  # nodes of eager partitions keep their torch targets
         if _is_checkpoint_hop(n):
             n.target = _checkpoint_hop_call
             n.kwargs = {}
+        elif n.op == "call_function" and _target_name(n) == _CTX_ENTER:
+            n.target = _fx_enter_autocast
+        elif n.op == "call_function" and _target_name(n) == _CTX_EXIT:
+            n.target = _fx_exit_autocast
     gm.recompile()
 
 
@@ -125,6 +149,8 @@ def is_node_supported(node: torch.fx.Node) -> tuple[bool, SplitReason | None]:
     if node.op in ("placeholder", "output", "get_attr"):
         return True, None
     name = _target_name(node)
+    if name in (_CTX_ENTER, _CTX_EXIT):
+        return True, None  # decided per region in _split
     if _is_checkpoint_hop(node):
         # an activation-checkpointed region is supported when every node of its body is
         body = getattr(node.graph.owning_module, node.args[0].target, None)
@@ -172,12 +198,29 @@ def _split(gm: torch.fx.GraphModule):
     part = {}
     cur = 0
     prev_supported = None
-    for node in gm.graph.nodes:
-        if node.op in ("placeholder", "output"):
-            continue
+    nodes = [n for n in gm.graph.nodes if n.op not in ("placeholder", "output")]
+    support = {}
+    for node in nodes:
         ok, why = is_node_supported(node)
         if why is not None:
             reasons.append(why)
+        support[node] = ok
+    # an autocast region with any unsupported node runs eagerly as a whole
+    stack = []
+    for i, node in enumerate(nodes):
+        name = _target_name(node)
+        if name == _CTX_ENTER:
+            stack.append(i)
+        elif name == _CTX_EXIT and stack:
+            j = stack.pop()
+            region = nodes[j:i + 1]
+            if not all(support[n] for n in region):
+                for n in region:
+                    support[n] = False
+                reasons.append(SplitReason(SplitReasonType.UNSUPPORTED_NODE,
+                                           "autocast region with an unsupported node runs eagerly"))
+    for node in nodes:
+        ok = support[node]
         if prev_supported is None or ok != prev_supported:
             cur += 1
         part[node] = (cur, ok)
@@ -216,8 +259,9 @@ class ThunderCompiler:
         part, reasons = _split(gm)
         if not part:
             return gm
-        if any(_is_checkpoint_hop(n) and part[n][1] for n in gm.graph.nodes):
-            _convert_checkpoints(gm)
+        if any((_is_checkpoint_hop(n) or _target_name(n) in (_CTX_ENTER, _CTX_EXIT)) and part[n][1]
+               for n in gm.graph.nodes if n in part):
+            _convert_checkpoints(gm, part)
         compiled = []
         mapping = {}
         if all(ok for _, ok in part.values()):

@@ -361,3 +361,28 @@ def test_fp8_training_recipes_parse():
     x = torch.randn(256, 256)
     torch.testing.assert_close(jm(x), m(x))
     assert t.n_converted == 0
+
+
+def test_jit_inner_autocast_context():
+    """``with torch.autocast(...)`` inside jitted code applies the autocast rules to the region only."""
+    import lightning_thunder_amd as lta
+
+    def f(x, w):
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            y = x @ w
+        return y, x @ w
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 8, requires_grad=True)
+    w = torch.randn(8, 8, requires_grad=True)
+    jf = lta.jit(f)
+    y, z = jf(x, w)
+    ry, rz = f(x, w)
+    assert y.dtype == torch.bfloat16 and z.dtype == torch.float32
+    torch.testing.assert_close(y, ry)
+    torch.testing.assert_close(z, rz)
+    (y.float().sum() + z.sum()).backward()
+    gx = x.grad.clone()
+    x.grad = None
+    (ry.float().sum() + rz.sum()).backward()
+    torch.testing.assert_close(gx, x.grad, atol=5e-2, rtol=2e-2)
