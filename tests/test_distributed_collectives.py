@@ -75,6 +75,7 @@ def _collectives_worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def _model():
@@ -106,6 +107,7 @@ def _nosync_worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def _fsdp_nosync_worker(rank, port, out_dir):
@@ -130,6 +132,7 @@ def _fsdp_nosync_worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def _run(worker):

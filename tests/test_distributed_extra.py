@@ -58,6 +58,7 @@ def _ckpt_worker(rank, world, port, d, make=None):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def test_fsdp_dcp_roundtrip():
@@ -106,6 +107,7 @@ def _hybrid_worker(rank, world, port, d, coalesced=False):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 import pytest
@@ -166,6 +168,7 @@ def _sd_worker(rank, world, port, d):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def test_thunder_module_state_dict_hooks_fsdp():

@@ -72,6 +72,7 @@ def _worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 @pytest.mark.gpu

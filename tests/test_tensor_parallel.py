@@ -81,6 +81,7 @@ def _worker(rank, port, mode, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def _run(mode):
@@ -159,6 +160,7 @@ def _litgpt_worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def test_litgpt_tensor_parallel_train_step_like_bench():
@@ -239,6 +241,7 @@ def _megatron_llama_worker(rank, port, out_dir):
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
         torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
 
 
 def test_megatron_llama_head_parallel_vocab_parallel():
