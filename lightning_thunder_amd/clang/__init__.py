@@ -257,6 +257,8 @@ digamma = _u(prims.digamma, K.INT_TO_FLOAT)
 erf = _u(prims.erf, K.INT_TO_FLOAT)
 erfc = _u(prims.erfc, K.INT_TO_FLOAT)
 erfinv = _u(prims.erfinv, K.INT_TO_FLOAT)
+erfcinv = _u(prims.erfcinv, K.INT_TO_FLOAT)
+ndtri = _u(prims.ndtri, K.INT_TO_FLOAT)
 exp = _u(prims.exp, K.INT_TO_FLOAT)
 exp2 = _u(prims.exp2, K.INT_TO_FLOAT)
 expm1 = _u(prims.expm1, K.INT_TO_FLOAT)

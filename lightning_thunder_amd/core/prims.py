@@ -88,6 +88,8 @@ class PrimIDs(Enum):
     ERF = auto()
     ERFC = auto()
     ERFINV = auto()
+    ERFCINV = auto()
+    NDTRI = auto()
     EXP = auto()
     EXP2 = auto()
     EXPM1 = auto()
@@ -377,6 +379,8 @@ digamma = _make_unary(PrimIDs.DIGAMMA, "digamma")
 erf = _make_unary(PrimIDs.ERF, "erf")
 erfc = _make_unary(PrimIDs.ERFC, "erfc")
 erfinv = _make_unary(PrimIDs.ERFINV, "erfinv")
+erfcinv = _make_unary(PrimIDs.ERFCINV, "erfcinv")
+ndtri = _make_unary(PrimIDs.NDTRI, "ndtri")
 exp = _make_unary(PrimIDs.EXP, "exp")
 exp2 = _make_unary(PrimIDs.EXP2, "exp2")
 expm1 = _make_unary(PrimIDs.EXPM1, "expm1")
@@ -905,7 +909,7 @@ def is_elementwise(sym) -> bool:
 ALL_ELEMENTWISE_UNARY = {
     PrimIDs.ABS, PrimIDs.ACOS, PrimIDs.ACOSH, PrimIDs.ASIN, PrimIDs.ASINH, PrimIDs.ATAN, PrimIDs.ATANH,
     PrimIDs.BITWISE_NOT, PrimIDs.CEIL, PrimIDs.COS, PrimIDs.COSH, PrimIDs.DIGAMMA, PrimIDs.ERF, PrimIDs.ERFC,
-    PrimIDs.ERFINV, PrimIDs.EXP, PrimIDs.EXP2, PrimIDs.EXPM1, PrimIDs.FLOOR, PrimIDs.ISFINITE, PrimIDs.LGAMMA,
+    PrimIDs.ERFINV, PrimIDs.ERFCINV, PrimIDs.NDTRI, PrimIDs.EXP, PrimIDs.EXP2, PrimIDs.EXPM1, PrimIDs.FLOOR, PrimIDs.ISFINITE, PrimIDs.LGAMMA,
     PrimIDs.LOG, PrimIDs.LOG10, PrimIDs.LOG1P, PrimIDs.LOG2, PrimIDs.NEG, PrimIDs.RECIPROCAL, PrimIDs.ROUND,
     PrimIDs.RSQRT, PrimIDs.SIGN, PrimIDs.SIGNBIT, PrimIDs.SIN, PrimIDs.SINH, PrimIDs.SQRT, PrimIDs.TAN,
     PrimIDs.TANH, PrimIDs.TRUNC, PrimIDs.REAL, PrimIDs.IMAG,

@@ -143,6 +143,13 @@ register_vjp(PrimIDs.ERFINV)(
     _unary_rule(P.erfinv, lambda a, o, g: P.mul(g, P.mul(P.exp(P.mul(o, o)), math.sqrt(math.pi) / 2.0)))
 )
 
+register_vjp(PrimIDs.ERFCINV)(
+    _unary_rule(P.erfcinv, lambda a, o, g: P.mul(g, P.mul(P.exp(P.mul(o, o)), -math.sqrt(math.pi) / 2.0)))
+)
+register_vjp(PrimIDs.NDTRI)(
+    _unary_rule(P.ndtri, lambda a, o, g: P.mul(g, P.mul(P.exp(P.mul(P.mul(o, o), 0.5)), math.sqrt(2.0 * math.pi))))
+)
+
 
 def _trigamma(x):
     """psi_1(x) = sum_{k<6} 1/(x+k)^2 + asymptotic series at x+6 (accurate to ~1e-10 for x > 0)."""

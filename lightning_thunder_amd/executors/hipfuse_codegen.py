@@ -92,7 +92,8 @@ _UNARY_FLOAT = {
     PrimIDs.LOG2: "log2", PrimIDs.LOG10: "log10", PrimIDs.SQRT: "sqrt", PrimIDs.RSQRT: "rsqrt", PrimIDs.SIN: "sin",
     PrimIDs.COS: "cos", PrimIDs.TAN: "tan", PrimIDs.SINH: "sinh", PrimIDs.COSH: "cosh", PrimIDs.TANH: "tanh",
     PrimIDs.ASIN: "asin", PrimIDs.ACOS: "acos", PrimIDs.ATAN: "atan", PrimIDs.ASINH: "asinh", PrimIDs.ACOSH: "acosh",
-    PrimIDs.ATANH: "atanh", PrimIDs.ERF: "erf", PrimIDs.ERFC: "erfc", PrimIDs.ERFINV: "erfinv", PrimIDs.LGAMMA: "lgamma",
+    PrimIDs.ATANH: "atanh", PrimIDs.ERF: "erf", PrimIDs.ERFC: "erfc", PrimIDs.ERFINV: "erfinv", PrimIDs.ERFCINV: "erfcinv",
+    PrimIDs.NDTRI: "normcdfinv", PrimIDs.LGAMMA: "lgamma",
     PrimIDs.FLOOR: "floor", PrimIDs.CEIL: "ceil", PrimIDs.TRUNC: "trunc", PrimIDs.ROUND: "rint",
 }
 _UNARY_ANY = {PrimIDs.NEG, PrimIDs.ABS, PrimIDs.RECIPROCAL, PrimIDs.SIGN, PrimIDs.BITWISE_NOT, PrimIDs.ISFINITE,

@@ -160,7 +160,8 @@ _unary_map = {
     prims.abs: torch.abs, prims.acos: torch.acos, prims.acosh: torch.acosh, prims.asin: torch.asin,
     prims.asinh: torch.asinh, prims.atan: torch.atan, prims.atanh: torch.atanh, prims.bitwise_not: torch.bitwise_not,
     prims.ceil: torch.ceil, prims.cos: torch.cos, prims.cosh: torch.cosh, prims.digamma: torch.digamma,
-    prims.erf: torch.erf, prims.erfc: torch.erfc, prims.erfinv: torch.erfinv, prims.exp: torch.exp,
+    prims.erf: torch.erf, prims.erfc: torch.erfc, prims.erfinv: torch.erfinv, prims.erfcinv: lambda a: torch.erfinv(1 - a),
+    prims.ndtri: torch.special.ndtri, prims.exp: torch.exp,
     prims.exp2: torch.exp2, prims.expm1: torch.expm1, prims.floor: torch.floor, prims.isfinite: torch.isfinite,
     prims.lgamma: torch.lgamma, prims.log: torch.log, prims.log10: torch.log10, prims.log1p: torch.log1p,
     prims.log2: torch.log2, prims.neg: torch.neg, prims.reciprocal: torch.reciprocal, prims.round: torch.round,

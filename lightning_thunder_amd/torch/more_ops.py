@@ -767,3 +767,72 @@ def random_(a, from_=0, to=None, *, generator=None):
     u = prims.uniform(a.shape, 0.0, 1.0, device=a.device, dtype=torch.float64)
     v = _f("floor")(_f("add")(_f("mul")(u, float(pyval(to) - pyval(from_))), float(pyval(from_))))
     return _fill(a, v)
+
+
+# =========================================================================================
+# torch.special: normal-distribution functions and friends
+# =========================================================================================
+@_export
+@torchsymbol(*_tfn("special.ndtri"), id="torch.special.ndtri")
+def ndtri(a):
+    from .. import clang
+
+    return clang.ndtri(a)
+
+
+@_export
+@torchsymbol(*_tfn("special.ndtr"), id="torch.special.ndtr")
+def ndtr(a):
+    a = _f("to")(a, torch.get_default_dtype()) if not a.dtype.is_floating_point else a
+    return _f("mul")(_f("erfc")(_f("mul")(a, -1.0 / math.sqrt(2.0))), 0.5)
+
+
+@_export
+@torchsymbol(*_tfn("special.log_ndtr"), id="torch.special.log_ndtr")
+def log_ndtr(a):
+    # log(0.5 erfc(-x/sqrt2)); for x < -5 the erfc underflows in fp32: use log(erfcx(t)) - t^2 there
+    a = _f("to")(a, torch.get_default_dtype()) if not a.dtype.is_floating_point else a
+    t = _f("mul")(a, -1.0 / math.sqrt(2.0))
+    direct = _f("log")(_f("mul")(_f("erfc")(t), 0.5))
+    tail = _f("sub")(_f("log")(_f("mul")(_erfcx_impl(t), 0.5)), _f("mul")(t, t))
+    return _f("where")(_f("lt")(a, -5.0), tail, direct)
+
+
+def _erfcx_impl(a):
+    return _f("mul")(_f("exp")(_f("mul")(a, a)), _f("erfc")(a))
+
+
+@_export
+@torchsymbol(*_tfn("special.entr"), id="torch.special.entr")
+def entr(a):
+    r = _f("neg")(_f("mul")(a, _f("log")(a)))
+    r = _f("where")(_f("eq")(a, 0), _f("zeros_like")(r), r)
+    return _f("where")(_f("lt")(a, 0), _f("full_like")(r, float("-inf")), r)
+
+
+@_export
+@torchsymbol(*_tfn("special.gammaln"), id="torch.special.gammaln")
+def gammaln(a):
+    return _f("lgamma")(a)
+
+
+@_export
+@torchsymbol(*_tfn("special.multigammaln", "mvlgamma", "Tensor.mvlgamma"), id="torch.special.multigammaln")
+def multigammaln(a, p: int):
+    p = pyval(p)
+    acc = _f("lgamma")(a)
+    for j in range(1, p):
+        acc = _f("add")(acc, _f("lgamma")(_f("sub")(a, j / 2.0)))
+    return _f("add")(acc, p * (p - 1) / 4.0 * math.log(math.pi))
+
+
+@_export
+@torchsymbol(*_tfn("special.expm1"), id="torch.special.expm1")
+def special_expm1(a):
+    return _f("expm1")(a)
+
+
+@_export
+@torchsymbol(*_tfn("special.log1p"), id="torch.special.log1p")
+def special_log1p(a):
+    return _f("log1p")(a)

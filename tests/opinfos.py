@@ -804,3 +804,13 @@ OPS += [
 ]
 
 OPS_BY_NAME = {o.name: o for o in OPS}
+
+OPS += [
+    elementwise_unary("special_ndtri", torch.special.ndtri, 0.02, 0.98, dtypes=FLOAT32),
+    elementwise_unary("special_ndtr", torch.special.ndtr, dtypes=FLOAT32),
+    elementwise_unary("special_log_ndtr", torch.special.log_ndtr, -3.0, 3.0, dtypes=FLOAT32),
+    elementwise_unary("special_entr", torch.special.entr, 0.05, 2.0, dtypes=FLOAT32),
+    elementwise_unary("special_gammaln", torch.special.gammaln, 0.5, 4.0, dtypes=FLOAT32),
+    elementwise_unary("special_multigammaln", lambda x: torch.special.multigammaln(x, 3), 1.5, 4.0, dtypes=FLOAT32),
+]
+OPS_BY_NAME = {o.name: o for o in OPS}
