@@ -106,7 +106,7 @@ _BINARY_SPECIAL = {PrimIDs.MAXIMUM, PrimIDs.MINIMUM}
 REDUCTIONS = {PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD, PrimIDs.VAR_MEAN}
 ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY | _BINARY_SPECIAL | {
     PrimIDs.WHERE, PrimIDs.CONVERT_ELEMENT_TYPE}
-VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE}
+VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE}
 SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
 
 
@@ -242,6 +242,8 @@ class Plan:
             self._add_broadcast(bsym, am)
         elif sid in (PrimIDs.RESHAPE, PrimIDs.SQUEEZE):
             self._add_unit_reshape(bsym, am)
+        elif sid == PrimIDs.TRANSPOSE:
+            self._add_transpose(bsym, am)
         elif sid in REDUCTIONS:
             self._add_reduction(bsym, am)
         elif sid == PrimIDs.UNIFORM_PHILOX:
@@ -345,6 +347,29 @@ class Plan:
         if om is None:
             raise NotFusible("broadcast of external to non-domain shape")
         am[0] = tuple(om[bdims[i]] if a.shape[i] != 1 else None for i in range(len(a.shape)))
+        self.maps[out.name] = om
+
+    def _add_transpose(self, bsym, am):
+        """A permutation only relabels which domain dim each dim of the value walks: the output's
+        map is the input's map permuted (an external input is then read through permuted strides)."""
+        a, out = bsym.args[0], bsym.output
+        perm = tuple(int(p) for p in bsym.args[1])
+        if self._internal(a):
+            amap = self.maps[a.name]
+            if amap is None:
+                raise NotFusible("transpose of a value whose index map is not known yet")
+            self.maps[out.name] = tuple(amap[perm[i]] for i in range(len(perm)))
+            return
+        om = self._map_for_shape(out.shape)
+        if om == "new":
+            self._set_domain(out.shape)
+            om = self._identity(out.shape)
+        if om is None:
+            raise NotFusible("transpose of external to non-domain shape")
+        amap = [None] * len(perm)
+        for i, p in enumerate(perm):
+            amap[p] = om[i]
+        am[0] = tuple(amap)
         self.maps[out.name] = om
 
     def _add_unit_reshape(self, bsym, am):
@@ -715,7 +740,7 @@ class _Gen:
         if sid == PrimIDs.WHERE:
             cond = R(0, "bool")
             return [(out.name, f"({cond} ? {R(1)} : {R(2)})")]
-        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE):
+        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE):
             return [(out.name, R(0))]
         if sid == PrimIDs.FULL:
             return [(out.name, self._scalar_ref(b.args[1], ct))]

@@ -61,6 +61,12 @@ def _full_and_col(a, b):
     return y, y.sum(0)
 
 
+def _transpose_mix(x, y):
+    # a transposed input and a transposed intermediate inside one region
+    z = torch.tanh(x.t()) * 2.0 + y
+    return z, (z * z).t() + x
+
+
 CASES = {
     "ln_gelu_softmax": (_layer_norm_gelu_softmax, lambda dt, d: (torch.randn(4, 8, 256, device=d, dtype=dt),
                                                                   torch.randn(256, device=d, dtype=dt),
@@ -81,6 +87,8 @@ CASES = {
     "full_and_col": (_full_and_col, lambda dt, d: (torch.randn(300, 200, device=d, dtype=dt),
                                                     torch.randn(300, 200, device=d, dtype=dt))),
 }
+CASES["transpose_mix"] = (_transpose_mix, lambda dt, d: (torch.randn(96, 160, device=d, dtype=dt),
+                                                          torch.randn(160, 96, device=d, dtype=dt)))
 _COLUMN_CASES = ("bias_grad", "ln_dgamma_dbeta", "col_amax_epilogue", "full_and_col")
 
 
