@@ -1264,8 +1264,8 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DQ
 }
 
-int g_dkdv_v3 = 0;  // dK/dV kernel for D = 128 without mask / dropout: 1 = v3 (64 keys per wave), 0 = v2
-int g_dq_v2 = 0;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
+int g_dkdv_v3 = 1;  // dK/dV kernel for D = 128 without mask / dropout: 1 = v3 (64 keys per wave), 0 = v2
+int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,

@@ -277,25 +277,25 @@ __device__ __forceinline__ float row_max32(const f32x16 (&s)[2]) {
   }
   float v = max3f(m[0], m[1], m[2]);
   v = max3f(v, m[3], m[3]);
+  // swap(v, v): element 0 carries lanes 32..63 into lanes 0..31, element 1 lanes 0..31 into 32..63
+  // (each lane's own value in the other element), so max / sum over both elements pairs lane l with l^32
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return max3f(v, __uint_as_float(sw[0]), __uint_as_float(sw[0]));
+  return max3f(v, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
 }
 
 __device__ __forceinline__ float lane_pair_sum(float v) {
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return v + __uint_as_float(sw[0]);
+  return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // own + partner in every lane
 }
 
-constexpr int kBM2 = 256;
-constexpr int kThreads2 = 512;
-
-template <typename T, bool CAUSAL, int THR, bool PIPE>
-__global__ __launch_bounds__(kThreads2, 1) void attn_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+template <typename T, bool CAUSAL, int THR, bool PIPE, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                    const T* __restrict__ V, T* __restrict__ O,
                                                                    float* __restrict__ LSE, int Hq, int Hkv, int Tq,
                                                                    int Sk, float c, int64_t so_b, int64_t so_h,
                                                                    int64_t so_t) {
   constexpr int D = 128;
+  constexpr int kBM2 = 32 * NW, kThreads2 = 64 * NW, NLD = kBN * 16 / kThreads2;  // 16-B chunks / thread / tile
   using C = Cfg<D>;
   using F = typename Frag<T>::type;
   constexpr int KT = kBN * C::KSTR, VT = kBN * C::VSTR;  // elements per K / V tile image
@@ -343,11 +343,11 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_fwd_v2_kernel(const T* __re
     }
   }
 
-  // ---- register staging (512 threads: 2 x 16-B chunks of K and of V per thread per tile) -------
-  uint4 kreg[2], vreg[2];
+  // ---- register staging (NLD 16-B chunks of K and of V per thread per tile) --------------------
+  uint4 kreg[NLD], vreg[NLD];
   auto gload_k = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
       const int kc = min(t * kBN + row, Sk - 1);  // clamped rows are real keys; the mask drops them
       kreg[i] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_fwd_v2_kernel(const T* __re
   };
   auto gload_v = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
       const int kc = min(t * kBN + row, Sk - 1);
       vreg[i] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
@@ -363,14 +363,14 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_fwd_v2_kernel(const T* __re
   };
   auto lstore_k = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
       *reinterpret_cast<uint4*>(smem + buf * KT + row * C::KSTR + ch * 8) = kreg[i];
     }
   };
   auto lstore_v = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
       *reinterpret_cast<uint4*>(smem + 2 * KT + buf * VT + row * C::VSTR + ch * 8) = vreg[i];
     }
@@ -578,14 +578,20 @@ int launch_v2(const void* q, const void* k, const void* v, void* o, void* lse, i
               float scale, int causal, const int64_t* so, int impl, hipStream_t s) {
   constexpr int D = 128;
   const float c = scale * 1.44269504088896340736f;
-  dim3 grid(B * Hq, (Tq + kBM2 - 1) / kBM2), block(kThreads2);
+  const int nw = impl >= 5 ? 4 : 8;  // 5, 6: 4 waves x 2 workgroups per CU
+  dim3 grid(B * Hq, (Tq + 32 * nw - 1) / (32 * nw)), block(64 * nw);
   const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * D, sh = so ? so[1] : (int64_t)Tq * D, st = so ? so[2] : D;
-#define LTA_V2(CA, TH, PI)                                                                                           \
-  hipLaunchKernelGGL((attn_fwd_v2_kernel<T, CA, TH, PI>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, \
-                     (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st)
+#define LTA_V2(CA, TH, PI)                                                                                         \
+  if (nw == 4)                                                                                                     \
+    hipLaunchKernelGGL((attn_fwd_v2_kernel<T, CA, TH, false, 4>), grid, block, 0, s, (const T*)q, (const T*)k,     \
+                       (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st);                           \
+  else                                                                                                             \
+    hipLaunchKernelGGL((attn_fwd_v2_kernel<T, CA, TH, PI, 8>), grid, block, 0, s, (const T*)q, (const T*)k,        \
+                       (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st)
   // impl: 1 = one S tile, exact rescale; 2 = one S tile, deferred rescale (THR 8);
-  //       3 = att[2] pipeline, exact; 4 = att[2] pipeline, deferred
-  const bool defer = impl == 2 || impl == 4, pipe = impl >= 3;
+  //       3 = att[2] pipeline, exact; 4 = att[2] pipeline, deferred (all 8 waves, 1 workgroup / CU);
+  //       5 = one S tile, exact; 6 = one S tile, deferred (4 waves, 2 workgroups / CU)
+  const bool defer = impl == 2 || impl == 4 || impl == 6, pipe = impl == 3 || impl == 4;
   if (causal) {
     if (pipe) { if (defer) LTA_V2(true, 8, true); else LTA_V2(true, 0, true); }
     else { if (defer) LTA_V2(true, 8, false); else LTA_V2(true, 0, false); }
@@ -687,6 +693,6 @@ LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void*
 // forward kernel selection for D = 128 without mask / dropout (A/B measurement hook)
 LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
   const int old = g_fwd_impl;
-  if (impl >= 0 && impl <= 4) g_fwd_impl = impl;
+  if (impl >= 0 && impl <= 6) g_fwd_impl = impl;
   return old;
 }
