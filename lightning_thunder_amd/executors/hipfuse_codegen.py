@@ -33,6 +33,7 @@ The design is CDNA4-first rather than a translation:
 from __future__ import annotations
 
 import hashlib
+import re
 import math
 from dataclasses import dataclass, field
 
@@ -565,11 +566,28 @@ def _contig_strides(shape):
     return tuple(reversed(st))
 
 
+_VALUE_ID = re.compile(r"\b([vr])_([A-Za-z_]\w*)")
+
+
+def _canonical_names(body: str) -> str:
+    """Renames the per-value identifiers (``v_<proxy>`` / ``r_<proxy>``) by order of first use, so
+    structurally identical regions (e.g. the same fusion in every transformer layer) produce the
+    same source, hash to one kernel name and compile once."""
+    ids: dict[str, str] = {}
+
+    def sub(m):
+        k = ids.setdefault(m.group(2), f"n{len(ids)}")
+        return f"{m.group(1)}_{k}"
+
+    return _VALUE_ID.sub(sub, body)
+
+
 def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix: str = "lta_fused") -> KernelSource:
     """``inputs``: region inputs (TensorProxy/NumberProxy), ``outputs``: TensorProxies,
     ``targs``: input name -> TensorArg for the tensor inputs at this call signature."""
     g = _Gen(plan, inputs, outputs, targs)
     body, grid, block, vec, mode = g.build()
+    body = _canonical_names(body)
     from ..core.rng import PHILOX_HIP
 
     src = _PREAMBLE + (PHILOX_HIP if "philox_uniform(" in body else "") + body
