@@ -123,7 +123,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   const int qt_begin = CAUSAL ? min((kb * kKB) / kQT, n_qt) : 0;
   const int nq = n_qt - qt_begin;
   const int total = group * nq;
-  constexpr int LOADS = kQT * C::CH / kThreads;  // 16-B chunks per thread per tile
+  // 16-B chunks per thread per tile, rounded up (D = 96: 384 chunks over 256 threads); the tail is
+  // guarded by NCH
+  constexpr int NCH = kQT * C::CH, LOADS = (NCH + kThreads - 1) / kThreads;
 
   uint4 pq[LOADS], po[LOADS];
   float plse = 0.f, pdel = 0.f;
@@ -135,6 +137,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
 #pragma unroll
     for (int c = 0; c < LOADS; ++c) {
       const int id = c * kThreads + tid;
+      if (NCH % kThreads != 0 && id >= NCH) break;
       const int row = id / C::CH, ch = id % C::CH;
       const int qc = min(qbase + row, Tq - 1);
       pq[c] = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
 #pragma unroll
     for (int c = 0; c < LOADS; ++c) {
       const int id = c * kThreads + tid;
+      if (NCH % kThreads != 0 && id >= NCH) break;
       const int row = id / C::CH, ch = id % C::CH;
       uint4 xq = pq[c], xo = po[c];
       if (qbase + row >= Tq) {
@@ -956,6 +960,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   int n_tiles = (Sk + kBN - 1) / kBN;
   if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
   constexpr int LOADS = kBN * C::CH / kThreads;
+  static_assert(kBN * C::CH % kThreads == 0, "K/V staging must cover the tile");
 
   // K/V tiles are prefetched into registers one tile ahead (latency hides behind the MFMAs).
   uint4 pk[LOADS], pv[LOADS];
