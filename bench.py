@@ -242,9 +242,9 @@ def main():
             # a high-priority RCCL stream gets a hardware queue of its own: on the normal-priority
             # pool the collectives' stream can share the compute stream's queue (GPU_MAX_HW_QUEUES)
             # and then never run concurrently with compute (measured: one queue, zero overlap)
-            opts = torch.distributed.ProcessGroupNCCL.Options()
-            opts.is_high_priority_stream = os.environ.get("LTA_NCCL_HIGH_PRIORITY", "1") == "1"
-            torch.distributed.init_process_group("nccl", device_id=device, pg_options=opts)
+            from lightning_thunder_amd.distributed import high_priority_pg_options
+
+            torch.distributed.init_process_group("nccl", device_id=device, pg_options=high_priority_pg_options())
         else:
             torch.distributed.init_process_group(backend)
 

@@ -38,9 +38,25 @@ def _sync_grads(module) -> None:
         hook()
 
 
+def high_priority_pg_options():
+    """RCCL process-group options with a high-priority internal stream.  On ROCm a high-priority
+    stream is placed on a hardware queue of its own; a normal-priority collective stream can land on
+    the compute stream's queue (``GPU_MAX_HW_QUEUES`` queues are shared round-robin) and then never
+    overlaps compute (``profiles/llama2_7b_world1_rccl_fsdp_step_breakdown.txt``: 0.02 ms of overlap
+    on a shared queue, 68 ms on separate ones).  ``LTA_NCCL_HIGH_PRIORITY=0`` turns it off."""
+    if not hasattr(tdist, "ProcessGroupNCCL"):
+        return None
+    opts = tdist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = os.environ.get("LTA_NCCL_HIGH_PRIORITY", "1") == "1"
+    return opts
+
+
 def copy_default_process_group():
-    """A copy of the default group (reference :39-75): separate RCCL communicator for compiled collectives."""
+    """A copy of the default group (reference :39-75): separate RCCL communicator for compiled
+    collectives, on a high-priority stream (:func:`high_priority_pg_options`) when the backend is RCCL."""
     os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+    if tdist.get_backend() == "nccl":
+        return tdist.new_group(pg_options=high_priority_pg_options())
     return tdist.new_group()
 
 
