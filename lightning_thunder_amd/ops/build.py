@@ -43,7 +43,8 @@ def _sources():
 # Per-file device flags.  attention_bwd: MFMAs written as intrinsics take VGPR destinations, so the
 # S / dP tiles stay where their softmax reads them while the dK / dV accumulators (inline-asm MFMAs)
 # own the AGPR file (without it hipcc swaps them through AGPRs every tile).
-FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+              "attention_fwd3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:

@@ -633,6 +633,10 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 
 }  // namespace
 
+LTA_EXPORT int lta_attn_fwd_v3(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
+                               int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
+                               const int64_t* o_strides, int defer, hipStream_t stream);
+
 // o_strides: optional int64[3] (batch, head, token) element strides of O (head dim contiguous);
 // null = contiguous [B,H,T,D].  [B,T,H,D] storage lets the output projection read O without a copy.
 // mask: optional fp32 additive mask [Bm][Hm][Tq][Skp] (Bm in {1,B}, Hm in {1,Hq}, Skp = Sk rounded up
@@ -660,6 +664,9 @@ LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const vo
     ex.offset = (unsigned)offset;
     exf |= kExDrop;
   }
+  if (D == 128 && exf == 0 && g_fwd_impl >= 7 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
+    return lta_attn_fwd_v3(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, g_fwd_impl == 8,
+                           stream);
   if (D == 128 && exf == 0 && g_fwd_impl != 0 && Tq > 0 && Sk > 0) {
     if (dtype == kBF16)
       return launch_v2<__hip_bfloat16>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, g_fwd_impl, stream);
@@ -693,6 +700,6 @@ LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void*
 // forward kernel selection for D = 128 without mask / dropout (A/B measurement hook)
 LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
   const int old = g_fwd_impl;
-  if (impl >= 0 && impl <= 6) g_fwd_impl = impl;
+  if (impl >= 0 && impl <= 8) g_fwd_impl = impl;
   return old;
 }

@@ -72,6 +72,10 @@ json.dump(out, open("gpurun_out/attn_fwd_ab.json", "w"), indent=1)
 # ---- backward: dQ kernel v1 vs v2 ---------------------------------------------------------------
 from lightning_thunder_amd.ops.attention import attn_bwd  # noqa: E402
 
+if "fwd" in sys.argv[2:]:
+    json.dump(out, open("gpurun_out/attn_fwd_ab.json", "w"), indent=1)
+    sys.exit(0)
+
 out["bwd_numerics"], out["bwd_perf"] = {}, {}
 torch.manual_seed(1)
 for (B, Hq, Hkv, T) in [(1, 4, 4, 1024), (2, 8, 2, 1000), (1, 2, 1, 77)]:
