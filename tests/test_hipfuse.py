@@ -355,3 +355,24 @@ def test_moe_model_cpu():
     gr = torch.autograd.grad(m(x), list(m.parameters()), g)
     for a, b in zip(gj, gr):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
+def test_repeated_fusions_share_one_kernel(cpu_fusion):
+    """Structurally identical regions (the same block in every layer) generate the same source
+    (value names are canonicalised), so they hash to one kernel and compile once."""
+    from lightning_thunder_amd.models.nanogpt import NanoGPT, NanoGPTConfig
+
+    torch.manual_seed(0)
+    m = NanoGPT(NanoGPTConfig(n_layer=3, n_head=2, n_embd=64, block_size=32, vocab_size=128))
+    jm = thunder.jit(m, executors=["hipfuse", "torch"])
+    x = torch.randint(0, 128, (2, 32))
+    jm(x, x)
+    names = []
+    for fb in hipfuse.fusions(thunder.last_traces(jm)[-1]):
+        fu = fb._call_ctx[fb.sym.name]
+        targs = {p.name: cg.TensorArg(tuple(p.shape), tuple(torch.empty(tuple(p.shape)).stride()), p.dtype, True)
+                 for p in fu.inputs if isinstance(p, TensorProxy)}
+        names.append(cg.generate(fu.plan, fu.inputs, fu.outputs, targs).name)
+    assert len(names) >= 6 and len(set(names)) < len(names), names  # per-layer regions dedupe
+    src = cg._canonical_names("float v_t12[8]; v_t12[j] = r_t3 + v_t12[j]; v8_float q; r_t3 = 1;")
+    assert src == "float v_n0[8]; v_n0[j] = r_n1 + v_n0[j]; v8_float q; r_n1 = 1;"
