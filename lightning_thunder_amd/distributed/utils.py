@@ -103,12 +103,20 @@ def schedule_allgathers(trace: TraceCtx, prefetch: int = 2) -> TraceCtx:
     order = sorted(range(len(gathers)), key=lambda gi: first_wait[gi])
     gather_ids = {id(g) for g in gathers}
     after: dict[int, list] = {}  # position of a wait -> gathers to issue right after it
+    before: dict[int, list] = {}  # position of a wait -> gathers to issue right before it
     head = []
     for k, gi in enumerate(order):
         if k < prefetch:
             head.append(gathers[gi])
+            continue
+        p = last_wait[order[k - prefetch]]
+        if p < first_wait[gi]:
+            after.setdefault(p, []).append(gathers[gi])
         else:
-            after.setdefault(last_wait[order[k - prefetch]], []).append(gathers[gi])
+            # the earlier bucket stays in use past this one's first wait (e.g. the parameters outside
+            # the transformer blocks: embedding at the start, LM head at the end): issue right before
+            # the first wait instead, never after it
+            before.setdefault(first_wait[gi], []).append(gathers[gi])
     # a gather must also come after whatever produces its inputs (normally trace inputs)
     out = []
     ret = bsyms[-1] if bsyms and bsyms[-1].sym.id == PrimIDs.RETURN else None
@@ -128,6 +136,7 @@ def schedule_allgathers(trace: TraceCtx, prefetch: int = 2) -> TraceCtx:
             continue
         if b is ret:
             break
+        out.extend(before.get(pos, ()))
         out.append(b)
         if pending_late:
             ready = [g for g in pending_late

@@ -181,3 +181,50 @@ def test_thunder_module_state_dict_hooks_fsdp():
     for r in res:
         assert r["full_err"] == 0.0 and r["shapes_ok"], r
         assert r["changed"] > 0 and r["restored"] < 1e-12 and r["bad_shape"], r
+
+
+def _zero3_window_worker(rank, world, port, d):
+    """ZeRO-3 + block bucketing with coalesced gathers and the prefetch window (the RCCL program's
+    schedule, on gloo): the bucket of parameters outside the blocks is waited on at the start (the
+    embedding) and at the end (the LM head), so the window must not place a block's gather after
+    that bucket's last wait (it did: the forward read a future before its gather)."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import fsdp
+    from lightning_thunder_amd.distributed.transforms import FSDPType
+    from lightning_thunder_amd.models.litgpt import GPT
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LTA_COALESCED_GRAD_SYNC="1")
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        for strategy in ("none", "block"):
+            torch.manual_seed(0)
+            m = GPT.from_name("llama2-like")
+            m.set_rope_cache(64, device="cpu")
+            jm = fsdp(thunder.jit(m), bucketing_strategy=strategy, sharding_strategy=FSDPType.ZERO3)
+            x = torch.randint(0, m.config.vocab_size, (2, 64), generator=torch.Generator().manual_seed(1))
+            out = jm(x)
+            out.float().pow(2).mean().backward()
+            res[strategy] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                             str(thunder.last_traces(jm)[-1]).count("all_gather_coalesced("))
+        torch.save(res, os.path.join(d, f"r{rank}.pt"))
+    finally:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    os._exit(0)  # skip interpreter teardown: gloo worker threads can abort it (rare SIGABRT)
+
+
+def test_zero3_block_bucketing_window_order():
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_zero3_window_worker, args=(1, _free_port(), d), nprocs=1, join=True, start_method="spawn")
+        res = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+    out0, g0, _ = res["none"]
+    out1, g1, n_coalesced = res["block"]
+    assert n_coalesced >= 3
+    torch.testing.assert_close(out1, out0)
+    for n in g0:
+        torch.testing.assert_close(g1[n], g0[n])
