@@ -107,7 +107,7 @@ _BINARY_SPECIAL = {PrimIDs.MAXIMUM, PrimIDs.MINIMUM}
 REDUCTIONS = {PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD, PrimIDs.VAR_MEAN}
 ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY | _BINARY_SPECIAL | {
     PrimIDs.WHERE, PrimIDs.CONVERT_ELEMENT_TYPE}
-VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE}
+VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD}
 SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
 
 
@@ -128,14 +128,15 @@ class Plan:
     red: int = 0  # number of trailing reduced domain dims
     colred: int = 0  # number of LEADING reduced domain dims (column mode; exclusive with red)
     has_reduction: bool = False
+    has_pad: bool = False  # pads (conditional loads) are admitted in pointwise regions only
     nodes: list = field(default_factory=list)
     maps: dict = field(default_factory=dict)  # internal value name -> map tuple
     arg_maps: list = field(default_factory=list)  # per node: {arg position: map} for tensor args
     post: set = field(default_factory=set)  # column mode: values computed from a column reduction
 
     def copy(self) -> "Plan":
-        return Plan(self.domain, self.red, self.colred, self.has_reduction, list(self.nodes), dict(self.maps),
-                    [dict(m) for m in self.arg_maps], set(self.post))
+        return Plan(self.domain, self.red, self.colred, self.has_reduction, self.has_pad, list(self.nodes),
+                    dict(self.maps), [dict(m) for m in self.arg_maps], set(self.post))
 
     # --- maps ----------------------------------------------------------------------------
     def _identity(self, shape):
@@ -245,6 +246,8 @@ class Plan:
             self._add_unit_reshape(bsym, am)
         elif sid == PrimIDs.TRANSPOSE:
             self._add_transpose(bsym, am)
+        elif sid == PrimIDs.PAD:
+            self._add_pad(bsym, am)
         elif sid in REDUCTIONS:
             self._add_reduction(bsym, am)
         elif sid == PrimIDs.UNIFORM_PHILOX:
@@ -373,6 +376,30 @@ class Plan:
         am[0] = tuple(amap)
         self.maps[out.name] = om
 
+    def _add_pad(self, bsym, am):
+        """Pad of an external input (e.g. the backward of a slice: the gradient of q / k / v placed
+        into the fused qkv gradient): a conditional load — the input where the domain index falls
+        inside it, the pad value elsewhere.  Pointwise regions only; no interior (dilation) padding."""
+        a, pv, cfg = bsym.args[0], bsym.args[1], bsym.args[2]
+        out = bsym.output
+        if self._internal(a) or not isinstance(a, TensorProxy):
+            raise NotFusible("pad of an internal value")
+        if isinstance(pv, TensorProxy) or self.red or self.colred or self.has_reduction:
+            raise NotFusible("pad in a reduction region / tensor pad value")
+        cfg = tuple((int(pyval(lo)), int(pyval(hi)), int(pyval(it))) for lo, hi, it in cfg)
+        if any(it != 0 or lo < 0 or hi < 0 for lo, hi, it in cfg):
+            raise NotFusible("interior or negative padding")
+        om = self._map_for_shape(out.shape)
+        if om == "new":
+            self._set_domain(out.shape)
+            om = self._identity(out.shape)
+        if om is None:
+            raise NotFusible("pad to non-domain shape")
+        # the input's dim i walks domain dim om[i] offset by -lo_i; a[i] of size 1 with lo == hi == 0 broadcasts
+        am[0] = ("pad", tuple(om), tuple(lo for lo, _, _ in cfg), float(pyval(pv)))
+        self.has_pad = True
+        self.maps[out.name] = om
+
     def _add_unit_reshape(self, bsym, am):
         a, out = bsym.args[0], bsym.output
         if _sq(a.shape) != _sq(out.shape):
@@ -408,6 +435,8 @@ class Plan:
         self.maps[out.name] = om
 
     def _add_reduction(self, bsym, am):
+        if self.has_pad:
+            raise NotFusible("reduction in a region with pads")
         a = bsym.args[0]
         dims = tuple(sorted(bsym.args[1]))
         if not isinstance(a, TensorProxy) or a.ndim == 0 or not dims:
@@ -673,6 +702,8 @@ class _Gen:
 
     def _dstrides(self, arg: TensorArg, amap) -> list:
         """Per-domain-dim element strides of an external tensor read through ``amap``."""
+        if amap and amap[0] == "pad":
+            amap = amap[1]
         st = [0] * self.nd
         for i, d in enumerate(amap):
             if d is not None and arg.shape[i] != 1:
@@ -758,8 +789,8 @@ class _Gen:
         if sid == PrimIDs.WHERE:
             cond = R(0, "bool")
             return [(out.name, f"({cond} ? {R(1)} : {R(2)})")]
-        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE):
-            return [(out.name, R(0))]
+        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD):
+            return [(out.name, R(0))]  # index remapping only: the arg map / conditional load does the work
         if sid == PrimIDs.FULL:
             return [(out.name, self._scalar_ref(b.args[1], ct))]
         if sid == PrimIDs.UNIFORM_PHILOX:
@@ -909,7 +940,34 @@ class _Gen:
                 self.loaded.add((nm, "row"))
                 self._emit_load(a, amap, nm, False, out, indent)
 
+    def _emit_pad_load(self, a, amap, nm, out, indent):
+        """Element-wise conditional load of a padded input (see ``Plan._add_pad``)."""
+        _, base, lo, pv = amap
+        ta = self.targs[a.name]
+        ct = _CTYPE[a.dtype]
+        ptr = self._ptr(a, False)
+        V, last = self.vec, self.nd - 1
+        conds, terms = [], []
+        for i, d in enumerate(base):
+            if d is None or a.shape[i] == 1:
+                continue
+            if f"i{d}" not in self.idx_avail:
+                raise NotFusible(f"codegen: index i{d} not available for pad load of {a.name}")
+            idx = f"((long long)i{d}{' + j' if d == last else ''} - {lo[i]}ll)"
+            if lo[i] != 0 or a.shape[i] != self.D[d]:  # unpadded dims are always in range
+                conds.append(f"{idx} >= 0ll && {idx} < {a.shape[i]}ll")
+            terms.append(f"{idx} * {ta.strides[i]}ll")
+        cond = " && ".join(conds) or "true"
+        off = " + ".join(terms) or "0ll"
+        out.append(f"{indent}{ct} {nm}[{V}];")
+        out.append(f"{indent}#pragma unroll")
+        out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = ({cond}) ? "
+                   f"{_load_conv(a.dtype, f'{ptr}[{off}]')} : {_lit(pv, ct)};")
+
     def _emit_load(self, a, amap, nm, vec_scope, out, indent):
+        if amap and amap[0] == "pad":
+            assert vec_scope, "pad loads exist in pointwise regions only"
+            return self._emit_pad_load(a, amap, nm, out, indent)
         ta = self.targs[a.name]
         st = self._dstrides(ta, amap)
         ct, sty = _CTYPE[a.dtype], _STYPE[a.dtype]

@@ -61,6 +61,13 @@ def _full_and_col(a, b):
     return y, y.sum(0)
 
 
+def _split_grad_pad(dq, dk, dv):
+    # the backward of a qkv split: the q / k / v gradients padded into d(qkv) and summed (one kernel)
+    n = dq.shape[-1]
+    g = torch.nn.functional.pad(dq, (0, 2 * n)) + torch.nn.functional.pad(dk, (n, n))
+    return (g + torch.nn.functional.pad(dv, (2 * n, 0))) * 0.5
+
+
 def _transpose_mix(x, y):
     # a transposed input and a transposed intermediate inside one region
     z = torch.tanh(x.t()) * 2.0 + y
@@ -87,6 +94,7 @@ CASES = {
     "full_and_col": (_full_and_col, lambda dt, d: (torch.randn(300, 200, device=d, dtype=dt),
                                                     torch.randn(300, 200, device=d, dtype=dt))),
 }
+CASES["pad_sum"] = (_split_grad_pad, lambda dt, d: tuple(torch.randn(4, 16, 64, device=d, dtype=dt) for _ in range(3)))
 CASES["transpose_mix"] = (_transpose_mix, lambda dt, d: (torch.randn(96, 160, device=d, dtype=dt),
                                                           torch.randn(160, 96, device=d, dtype=dt)))
 _COLUMN_CASES = ("bias_grad", "ln_dgamma_dbeta", "col_amax_epilogue", "full_and_col")
