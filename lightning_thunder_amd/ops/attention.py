@@ -27,6 +27,14 @@ register_signature("lta_attn_bwd_ex", [c_int, c_void_p, c_void_p, c_void_p, c_vo
                                        c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                        ctypes.c_uint64, c_void_p])
 
+register_signature("lta_attn_fwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p, c_int, c_int, c_float,
+                                        ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p])
+register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                        c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
+                                        ctypes.c_uint64, c_void_p, c_void_p])
+
 SUPPORTED_HEAD_DIMS = (64, 96, 128)
 
 
@@ -71,6 +79,15 @@ def _strides3(t):
     return (ctypes.c_int64 * 3)(*t.stride()[:3])
 
 
+def _qkv_in_place(q, k, v):
+    """q / k / v as the kernels read them: any [B, H, T] strides with the head dim contiguous and
+    16-byte aligned rows in place (e.g. views into a fused qkv projection), else a contiguous copy;
+    plus their (batch, head, token) strides for the kernels."""
+    q, k, v = (t if _rows_ok(t) else t.contiguous() for t in (q, k, v))
+    st = (ctypes.c_int64 * 9)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3])
+    return q, k, v, st
+
+
 def _rows_ok(t) -> bool:
     """Head dim contiguous, 16-byte aligned rows: any [B, H, T] strides are read in place."""
     return t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
@@ -84,23 +101,20 @@ def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str 
     transposed view: the usual ``o.transpose(1, 2).reshape(B, T, Hq * D)`` before the output
     projection is then a view instead of a copy, and the backward reads it (and dO) in place."""
     lib = require()
-    q, k, v = _c(q), _c(k), _c(v)
+    q, k, v, qkv_st = _qkv_in_place(q, k, v)
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
     if out_layout == "bshd":
         o = torch.empty((B, T, Hq, D), device=q.device, dtype=q.dtype).transpose(1, 2)
     else:
-        o = torch.empty_like(q)
+        o = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)
     lse = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
-    if mask is None and not dropout_p:
-        rc = lib.lta_attn_fwd_s(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
-                                int(causal), ctypes.cast(_strides3(o), c_void_p), stream_ptr(q.device))
-    else:
-        mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
-        rc = lib.lta_attn_fwd_ex(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
-                                 int(causal), ctypes.cast(_strides3(o), c_void_p), ptr(mimg), mb, mh, float(dropout_p),
-                                 int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), stream_ptr(q.device))
+    mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
+    rc = lib.lta_attn_fwd_ex2(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
+                              int(causal), ctypes.cast(_strides3(o), c_void_p), ptr(mimg), mb, mh, float(dropout_p),
+                              int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), ctypes.cast(qkv_st, c_void_p),
+                              stream_ptr(q.device))
     check(rc, "lta_attn_fwd")
     return o, lse
 
@@ -110,32 +124,27 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     """Returns (dq, dk, dv) with dk/dv summed over the query heads of each kv group; with
     ``mask_grad`` (a float mask) a 4th result: the mask's gradient, reduced to its shape."""
     lib = require()
-    q, k, v = _c(q), _c(k), _c(v)
+    q, k, v, qkv_st = _qkv_in_place(q, k, v)
     do = do if _rows_ok(do) else do.contiguous()
     o = o if _rows_ok(o) else o.contiguous()
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
-    dq = torch.empty_like(q)
-    dk = torch.empty_like(k)
-    dv = torch.empty_like(v)
+    # gradients are written dense [B, H, T, D] whatever the strides of q / k / v
+    dq = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)
+    dk = torch.empty((B, Hkv, S, D), device=q.device, dtype=q.dtype)
+    dv = torch.empty((B, Hkv, S, D), device=q.device, dtype=q.dtype)
     delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
     st = (ctypes.c_int64 * 6)(*do.stride()[:3], *o.stride()[:3])
-    if mask is None and not dropout_p:
-        rc = lib.lta_attn_bwd_s(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq),
-                                ptr(dk), ptr(dv), None, B, Hq, Hkv, T, S, D, float(sc), int(causal),
-                                ctypes.cast(st, c_void_p), stream_ptr(q.device))
-        check(rc, "lta_attn_bwd")
-        return dq, dk, dv
     mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
     dmask = None
     if mask_grad:
         assert mask is not None and mask.dtype != torch.bool
         dmask = torch.empty((B, Hq, T, S), device=q.device, dtype=torch.float32)
-    rc = lib.lta_attn_bwd_ex(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
-                             ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
-                             mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),
-                             int(offset) & (2 ** 64 - 1), stream_ptr(q.device))
+    rc = lib.lta_attn_bwd_ex2(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
+                              ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
+                              mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),
+                              int(offset) & (2 ** 64 - 1), ctypes.cast(qkv_st, c_void_p), stream_ptr(q.device))
     check(rc, "lta_attn_bwd")
     if not mask_grad:
         return dq, dk, dv

@@ -73,7 +73,26 @@ __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >
 // EX bit flags of a kernel instantiation (compile-time: the plain causal path carries no cost):
 enum : int { kExMask = 1, kExDrop = 2, kExMaskGrad = 4 };
 
+// Element strides (batch, head, token) of Q, K and V (head dim contiguous, rows 16-byte aligned):
+// views into a fused qkv projection are read in place.  contiguous(): dense [B, H, T, D].
+struct QKVStrides {
+  int64_t qb, qh, qt, kb, kh, kt, vb, vh, vt;
+  static QKVStrides contiguous(int Hq, int Hkv, int Tq, int Sk, int D) {
+    return {(int64_t)Hq * Tq * D, (int64_t)Tq * D, D, (int64_t)Hkv * Sk * D, (int64_t)Sk * D, D,
+            (int64_t)Hkv * Sk * D, (int64_t)Sk * D, D};
+  }
+  static QKVStrides from(const int64_t* s, int Hq, int Hkv, int Tq, int Sk, int D) {
+    return s ? QKVStrides{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]} : contiguous(Hq, Hkv, Tq, Sk, D);
+  }
+  bool is_contiguous(int Hq, int Hkv, int Tq, int Sk, int D) const {
+    const QKVStrides c = contiguous(Hq, Hkv, Tq, Sk, D);
+    return qb == c.qb && qh == c.qh && qt == c.qt && kb == c.kb && kh == c.kh && kt == c.kt && vb == c.vb &&
+           vh == c.vh && vt == c.vt;
+  }
+};
+
 struct AttnExtra {
+  QKVStrides sx;          // Q / K / V strides (every kernel reads its operands through them)
   const float* mask;      // additive mask (natural-log domain), fp32 [Bm][Hm][Tq][Skp], key dim padded to 64
   int64_t mb, mh, mq;     // element strides (0 for a broadcast batch / head)
   float* dmask;           // kExMaskGrad: dS written as fp32 [B][Hq][Tq][Sk] (reduced over broadcast dims by the host)

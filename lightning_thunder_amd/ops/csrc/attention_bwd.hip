@@ -98,16 +98,16 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int kw = kb * kKB + wave * 32;  // this wave's first key
   const int key = kw + r;               // this lane's key
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Kb = K + b * ex.sx.kb + hk * ex.sx.kh;
+  const T* Vb = V + b * ex.sx.vb + hk * ex.sx.vh;
 
   F kf[C::KS], vf[C::KS];
   {
     const int krow = min(key, Sk - 1);
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) {
-      kf[s] = load_frag<F>(Kb + (int64_t)krow * D + 16 * s + 8 * h);
-      vf[s] = load_frag<F>(Vb + (int64_t)krow * D + 16 * s + 8 * h);
+      kf[s] = load_frag<F>(Kb + (int64_t)krow * ex.sx.kt + 16 * s + 8 * h);
+      vf[s] = load_frag<F>(Vb + (int64_t)krow * ex.sx.vt + 16 * s + 8 * h);
     }
   }
   f32x16 dkacc[C::DT], dvacc[C::DT];
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   auto issue = [&](int it) {
     const int hq = hk * group + it / nq;
     const int qbase = (qt_begin + it % nq) * kQT;
-    const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* Qb = Q + b * ex.sx.qb + hq * ex.sx.qh;
     const T* dOb = dO + b * sdo.b + hq * sdo.h;
 #pragma unroll
     for (int c = 0; c < LOADS; ++c) {
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       if (NCH % kThreads != 0 && id >= NCH) break;
       const int row = id / C::CH, ch = id % C::CH;
       const int qc = min(qbase + row, Tq - 1);
-      pq[c] = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * D + ch * 8);
+      pq[c] = *reinterpret_cast<const uint4*>(Qb + (int64_t)qc * ex.sx.qt + ch * 8);
       po[c] = *reinterpret_cast<const uint4*>(dOb + qc * sdo.t + ch * 8);
     }
     if (tid < kQT) {
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
                                                                        const float* __restrict__ LSE,
                                                                        const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                       float scale, float scale_log2, RowStrides sdo) {
+                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -392,8 +392,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
   const int kw = kb * kKB + wave * 32;
   const int key = kw + r;
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
 
   // K and V rows of this workgroup's 128 keys -> LDS (padded rows: conflict-free B-operand reads);
   // held there rather than in registers so the loop carries nothing but the AGPR accumulators
@@ -402,8 +402,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
     const int id = c * kThreads + tid;
     const int row = id / C::CH, ch = id % C::CH;
     const int vr = min(kb * kKB + row, Sk - 1);
-    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * D + ch * 8);
-    *reinterpret_cast<uint4*>(Ks + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Kb + (int64_t)vr * D + ch * 8);
+    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * sx.vt + ch * 8);
+    *reinterpret_cast<uint4*>(Ks + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Kb + (int64_t)vr * sx.kt + ch * 8);
   }
 
   f32x16 dkacc[C::DT], dvacc[C::DT];
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
   auto issue = [&](int hi, int ti, int st) {
     const int hq = hk * group + hi;
     const int qbase = (qt_begin + ti) * kQT;
-    const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* Qb = Q + b * sx.qb + hq * sx.qh;
     const T* dOb = dO + b * sdo.b + hq * sdo.h;
     char* qimg = smem + st * STAGE;
     if (wave == 0) {
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
       const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
       const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
       const int qc = min(qbase + row, Tq - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * D + ch * 8),
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * sx.qt + ch * 8),
                                        (lds_void*)(qimg + k * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
                                        (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
                                                                        const float* __restrict__ LSE,
                                                                        const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                       float scale, float scale_log2, RowStrides sdo) {
+                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -658,8 +658,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int kw = kb * kKB3 + wave * 64;  // this wave's first key; half j: keys kw + 32 j + r
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
 
   // V rows of the workgroup's 256 keys -> LDS; K rows of this wave's 64 keys -> registers
 #pragma unroll
@@ -667,14 +667,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
     const int id = c * kThreads + tid;
     const int row = id / C::CH, ch = id % C::CH;
     const int vr = min(kb * kKB3 + row, Sk - 1);
-    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * D + ch * 8);
+    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * sx.vt + ch * 8);
   }
   F kf[2][C::KS];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int kr = min(kw + 32 * j + r, Sk - 1);
 #pragma unroll
-    for (int s = 0; s < C::KS; ++s) kf[j][s] = load_frag<F>(Kb + (int64_t)kr * D + 16 * s + 8 * h);
+    for (int s = 0; s < C::KS; ++s) kf[j][s] = load_frag<F>(Kb + (int64_t)kr * sx.kt + 16 * s + 8 * h);
   }
 
   f32x16 dkacc[2][C::DT], dvacc[2][C::DT];
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
   auto issue = [&](int hi, int ti, int st) {
     const int hq = hk * group + hi;
     const int qbase = (qt_begin + ti) * kQT;
-    const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+    const T* Qb = Q + b * sx.qb + hq * sx.qh;
     const T* dOb = dO + b * sdo.b + hq * sdo.h;
     char* qimg = smem + st * STAGE;
     if (wave == 0) {
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
       const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
       const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
       const int qc = min(qbase + row, Tq - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * D + ch * 8),
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * sx.qt + ch * 8),
                                        (lds_void*)(qimg + k * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
                                        (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
@@ -926,10 +926,10 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   const int bh = blockIdx.x;
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
-  const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* Qb = Q + b * ex.sx.qb + hq * ex.sx.qh;
   const T* dOb = dO + b * sdo.b + hq * sdo.h;
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Kb = K + b * ex.sx.kb + hk * ex.sx.kh;
+  const T* Vb = V + b * ex.sx.vb + hk * ex.sx.vh;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   F qf[C::KS], of[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+    qf[s] = load_frag<F>(Qb + (int64_t)qrow * ex.sx.qt + 16 * s + 8 * h);
     of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
   }
   const float lse2 = LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
@@ -970,8 +970,8 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
       const int kc = min(t * kBN + row, Sk - 1);
-      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
-      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * ex.sx.kt + ch * 8);
+      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * ex.sx.vt + ch * 8);
     }
   };
   if (n_tiles > 0) issue(0);
@@ -1094,7 +1094,7 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
                                                                       const float* __restrict__ LSE,
                                                                       const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                       int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                      float scale_log2, RowStrides sdo) {
+                                                                      float scale_log2, RowStrides sdo, QKVStrides sx) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -1106,10 +1106,10 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
   const int bh = blockIdx.x;
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
-  const T* Qb = Q + ((int64_t)b * Hq + hq) * (int64_t)Tq * D;
+  const T* Qb = Q + b * sx.qb + hq * sx.qh;
   const T* dOb = dO + b * sdo.b + hq * sdo.h;
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
   F qf[C::KS], of[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+    qf[s] = load_frag<F>(Qb + (int64_t)qrow * sx.qt + 16 * s + 8 * h);
     of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
   }
   const float nlse2 = -LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
@@ -1145,8 +1145,8 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
     for (int c = 0; c < 2; ++c) {
       const int id = c * kThreads2 + tid, row = id >> 4, ch = id & 15;
       const int kc = min(t * kBN + row, Sk - 1);  // clamped rows are real keys; dS = 0 there
-      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
-      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * sx.kt + ch * 8);
+      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * sx.vt + ch * 8);
     }
   };
   auto lstore = [&](int st) {
@@ -1303,20 +1303,20 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dkdv_v3_kernel<T, true>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo);
+                         sl2, sdo, ex.sx);
     else
       hipLaunchKernelGGL((attn_bwd_dkdv_v3_kernel<T, false>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo);
+                         sl2, sdo, ex.sx);
   } else if (D == 128 && dkdv_v2) {
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo);
+                         sl2, sdo, ex.sx);
     else
       hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo);
+                         sl2, sdo, ex.sx);
   } else if (causal) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
@@ -1330,10 +1330,10 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
     else
       hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, false>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo);
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
   } else if (causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
@@ -1350,11 +1350,12 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
 // (head dim contiguous); null = contiguous [B,H,T,D] for both.  mask / dropout as lta_attn_fwd_ex;
 // dmask (optional, needs mask): fp32 [B][Hq][Tq][Sk] receives dS, the additive mask's gradient
 // before the reduction over its broadcast dims.
-LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
-                               const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
-                               int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
-                               int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
-                               hipStream_t stream) {
+// qkv_strides: optional int64[9] = (batch, head, token) strides of Q, K, V (as lta_attn_fwd_ex2)
+LTA_EXPORT int lta_attn_bwd_ex2(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                                const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
+                                int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
+                                int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
+                                const int64_t* qkv_strides, hipStream_t stream) {
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f || (dmask && !mask)) return -2;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
@@ -1364,6 +1365,7 @@ LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const v
     return (e && e[0] == '1') ? 0 : 1;
   }();
   AttnExtra ex{};
+  ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
   int exf = 0;
   if (mask) {
     const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
@@ -1399,6 +1401,15 @@ LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const v
   }
 #undef LTA_B
   return -1;
+}
+
+LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                               const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
+                               int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
+                               int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
+                               hipStream_t stream) {
+  return lta_attn_bwd_ex2(dtype, dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, D, scale, causal, strides,
+                          mask, mask_b, mask_h, dmask, dropout_p, seed, offset, nullptr, stream);
 }
 
 LTA_EXPORT int lta_attn_bwd_s(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,

@@ -55,9 +55,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   const int bh = blockIdx.x;
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
-  const T* Qb = Q + ((int64_t)b * Hq + hq) * Tq * D;
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
+  const T* Qb = Q + b * ex.sx.qb + hq * ex.sx.qh;
+  const T* Kb = K + b * ex.sx.kb + hk * ex.sx.kh;
+  const T* Vb = V + b * ex.sx.vb + hk * ex.sx.vh;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   {
     const int qrow = min(qi, Tq - 1);
 #pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
+    for (int s = 0; s < C::KS; ++s) qf[s] = load_frag<F>(Qb + (int64_t)qrow * ex.sx.qt + 16 * s + 8 * h);
   }
 
   f32x16 oacc[C::DT];
@@ -97,8 +97,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
       const int row = id / C::CH, ch = id % C::CH;
       const int key = t * kBN + row;
       const int kc = min(key, Sk - 1);  // branch-free: clamp the address, zero the data
-      uint4 kx = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
-      uint4 vx = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
+      uint4 kx = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * ex.sx.kt + ch * 8);
+      uint4 vx = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * ex.sx.vt + ch * 8);
       const bool ok = key < Sk;
       kreg[c] = ok ? kx : make_uint4(0, 0, 0, 0);
       vreg[c] = ok ? vx : make_uint4(0, 0, 0, 0);
@@ -641,12 +641,16 @@ LTA_EXPORT int lta_attn_fwd_v3(int dtype, const void* q, const void* k, const vo
 // null = contiguous [B,H,T,D].  [B,T,H,D] storage lets the output projection read O without a copy.
 // mask: optional fp32 additive mask [Bm][Hm][Tq][Skp] (Bm in {1,B}, Hm in {1,Hq}, Skp = Sk rounded up
 // to 64, padding -inf); dropout_p > 0: counter-based dropout of P (seed, offset: the generator state).
-LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
-                               int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
-                               const void* mask, int mask_b, int mask_h, float dropout_p, uint64_t seed,
-                               uint64_t offset, hipStream_t stream) {
+// qkv_strides: optional int64[9] = (batch, head, token) element strides of Q, K, V (head dim
+// contiguous, 16-byte aligned rows); null = contiguous [B,H,T,D].
+LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
+                                int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
+                                const int64_t* o_strides, const void* mask, int mask_b, int mask_h, float dropout_p,
+                                uint64_t seed, uint64_t offset, const int64_t* qkv_strides, hipStream_t stream) {
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f) return -2;
   AttnExtra ex{};
+  ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
+  const bool dense = ex.sx.is_contiguous(Hq, Hkv, Tq, Sk, D);  // the experimental v2 / v3 kernels read dense only
   int exf = 0;
   if (mask) {
     const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
@@ -664,10 +668,10 @@ LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const vo
     ex.offset = (unsigned)offset;
     exf |= kExDrop;
   }
-  if (D == 128 && exf == 0 && g_fwd_impl >= 7 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
+  if (dense && D == 128 && exf == 0 && g_fwd_impl >= 7 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
     return lta_attn_fwd_v3(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, g_fwd_impl == 8,
                            stream);
-  if (D == 128 && exf == 0 && g_fwd_impl != 0 && Tq > 0 && Sk > 0) {
+  if (dense && D == 128 && exf == 0 && g_fwd_impl != 0 && Tq > 0 && Sk > 0) {
     if (dtype == kBF16)
       return launch_v2<__hip_bfloat16>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, g_fwd_impl, stream);
     if (dtype == kF16)
@@ -683,6 +687,14 @@ LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const vo
     if (D == 96) return launch<__half, 96>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
   }
   return -1;
+}
+
+LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                               int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
+                               const void* mask, int mask_b, int mask_h, float dropout_p, uint64_t seed,
+                               uint64_t offset, hipStream_t stream) {
+  return lta_attn_fwd_ex2(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, mask, mask_b, mask_h,
+                          dropout_p, seed, offset, nullptr, stream);
 }
 
 LTA_EXPORT int lta_attn_fwd_s(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,

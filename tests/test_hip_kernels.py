@@ -844,3 +844,32 @@ def test_gemv_group_matches_separate_projections(M, norm, ns):
         xf = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()).bfloat16().float()
     for o, w in zip(outs, ws):
         torch.testing.assert_close(o.float(), xf @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("Hkv", [4, 2])
+@pytest.mark.parametrize("masked", [False, True])
+def test_flash_attention_strided_qkv_views(D, Hkv, masked):
+    """q / k / v as views into one fused projection output [B, T, (Hq + 2 Hkv) * D] (head dim
+    contiguous, token stride (Hq + 2 Hkv) * D) are read in place: results equal the contiguous call."""
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+    torch.manual_seed(0)
+    B, Hq, T = 2, 4, 256
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    q = qkv[..., : Hq * D].view(B, T, Hq, D).transpose(1, 2)
+    k = qkv[..., Hq * D: (Hq + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
+    v = qkv[..., (Hq + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)
+    assert not q.is_contiguous()
+    do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    kw = dict(dropout_p=0.1, seed=7, offset=3) if masked else {}
+    o1, l1 = attn_fwd(q, k, v, True, **kw)
+    o2, l2 = attn_fwd(q.contiguous(), k.contiguous(), v.contiguous(), True, **kw)
+    torch.testing.assert_close(o1, o2, atol=0, rtol=0)
+    torch.testing.assert_close(l1, l2, atol=0, rtol=0)
+    g1 = attn_bwd(do, q, k, v, o1, l1, True, **kw)
+    g2 = attn_bwd(do, q.contiguous(), k.contiguous(), v.contiguous(), o2, l2, True, **kw)
+    for a, b in zip(g1, g2):
+        assert a.is_contiguous()
+        torch.testing.assert_close(a, b, atol=0, rtol=0)
