@@ -812,9 +812,180 @@ def _fuse_rms_bwd_residual(trace):
     return new
 
 
+# ---- fused SwiGLU GEMMs (csrc/gemm4.hip EPI 1 / 2) ---------------------------------------
+def _gate_up_meta(x, w1, w2):
+    shp = tuple(x.shape[:-1]) + (w1.shape[0],)
+    return TensorProxy(like=x, shape=shp), TensorProxy(like=x, shape=shp), TensorProxy(like=x, shape=shp)
+
+
+def _gate_up_impl(x, w1, w2):
+    from ..ops.gemm import gate_up_swiglu
+
+    return gate_up_swiglu(x, w1, w2, need_ab=True)
+
+
+def _gate_up_y_impl(x, w1, w2):
+    from ..ops.gemm import gate_up_swiglu
+
+    return gate_up_swiglu(x, w1, w2, need_ab=False)[2]
+
+
+hip_gate_up = ex.register_operator("hip_gate_up", meta=_gate_up_meta, fn=_gate_up_impl)
+hip_gate_up_y = ex.register_operator("hip_gate_up_y", meta=lambda x, w1, w2: _gate_up_meta(x, w1, w2)[2],
+                                     fn=_gate_up_y_impl)
+
+
+def _mm_swiglu_bwd_impl(dy, w, a, b):
+    from ..ops.gemm import matmul_swiglu_bwd
+
+    return matmul_swiglu_bwd(dy, w, a, b)
+
+
+hip_matmul_swiglu_bwd = ex.register_operator(
+    "hip_matmul_swiglu_bwd", meta=lambda dy, w, a, b: (TensorProxy(like=a), TensorProxy(like=b)), fn=_mm_swiglu_bwd_impl)
+
+
+def _fuse_swiglu_gemms(trace):
+    """LLaMA-MLP SwiGLU chains onto the GEMM epilogues (prefill / training shapes; decode rows go to
+    the gated GEMV of :func:`_fuse_decode_gemv`):
+
+    * forward: ``a = hip_linear(x, w1); b = hip_linear(x, w2); y = hip_swiglu(a, b)`` ->
+      ``a, b, y = hip_gate_up(x, w1, w2)`` (one launch; ``hip_gate_up_y`` when nothing else reads
+      a / b, e.g. inference);
+    * backward: ``g = hip_matmul(dy, w); da, db = hip_swiglu_bwd(g, a, b)`` (g read nowhere else) ->
+      ``da, db = hip_matmul_swiglu_bwd(dy, w, a, b)``.
+    Reference counterpart: nvFuser fusing the pointwise SwiGLU into its matmul segments
+    (thunder/executors/nvfuserex_impl.py:2437-2488)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+    uses: dict[str, list] = {}
+    for k, b in enumerate(bsyms):
+        for a in b.flat_proxy_args:
+            uses.setdefault(a.name, []).append(k)
+    outs = {o.name for o in tree_flatten(trace.output)[0] if isinstance(o, TensorProxy)} if trace.output is not None else set()
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    n_fwd = n_bwd = 0
+    for i, b in enumerate(bsyms):
+        if b.sym is hip_swiglu and len(b.args) == 2:
+            a, g = b.args
+            ja, jg = producer.get(a.name), producer.get(g.name)
+            if ja is None or jg is None or ja == jg or {ja, jg} & (drop | set(replace)):
+                continue
+            la, lg = bsyms[ja], bsyms[jg]
+            if la.sym is not hip_linear or lg.sym is not hip_linear:
+                continue
+            pa, pg = _linear_parts(la), _linear_parts(lg)
+            if pa["x"].name != pg["x"].name or any(p.get(k) is not None for p in (pa, pg) for k in ("bias", "residual", "act")):
+                continue
+            x, w1, w2 = pa["x"], pa["w"], pg["w"]
+            if tuple(w1.shape) != tuple(w2.shape) or _rows(x) <= _GEMV_MAX_ROWS or x.dtype != torch.bfloat16:
+                continue
+            at = max(ja, jg)
+            # every other reader of a / b must come after the fused op's position
+            others = [k for k in uses.get(a.name, []) + uses.get(g.name, []) if k != i]
+            if any(k <= at for k in others):
+                continue
+            if others or a.name in outs or g.name in outs:
+                nb = ex.bind_call_ctx(hip_gate_up.bind(x, w1, w2, output=(a, g, b.output)))
+            else:
+                nb = ex.bind_call_ctx(hip_gate_up_y.bind(x, w1, w2, output=b.output))
+            replace[at] = nb
+            drop.update((min(ja, jg), i))
+            n_fwd += 1
+        elif b.sym is hip_swiglu_bwd and len(b.args) == 3:
+            g, a, bb = b.args
+            j = producer.get(g.name)
+            if j is None or j in drop or j in replace or bsyms[j].sym is not hip_matmul:
+                continue
+            mb = bsyms[j]
+            if (len(mb.args) > 2 and mb.args[2] is not None) or uses.get(g.name, []) != [i] or g.name in outs:
+                continue
+            dy, w = mb.args[0], mb.args[1]
+            if w.ndim != 2 or tuple(a.shape) != tuple(g.shape) or tuple(bb.shape) != tuple(g.shape):
+                continue
+            replace[i] = ex.bind_call_ctx(hip_matmul_swiglu_bwd.bind(dy, w, a, bb, output=b.output))
+            drop.add(j)
+            n_bwd += 1
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {n_fwd} gate-up SwiGLU GEMM(s), {n_bwd} SwiGLU-backward GEMM epilogue(s)"))
+    return new
+
+
+def _linear_qkv_rope_impl(x, w, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    from ..ops.gemm import linear_qkv_rope
+
+    return linear_qkv_rope(x, w, cos, sin, n_head, n_query_groups, head_size, rope_n)
+
+
+def _linear_qkv_rope_meta(x, w, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    B, T = x.shape[0], x.shape[1]
+    return (TensorProxy(like=x, shape=(B, n_head, T, head_size)),
+            TensorProxy(like=x, shape=(B, n_query_groups, T, head_size)),
+            TensorProxy(like=x, shape=(B, n_query_groups, T, head_size)))
+
+
+hip_linear_qkv_rope = ex.register_operator("hip_linear_qkv_rope", meta=_linear_qkv_rope_meta, fn=_linear_qkv_rope_impl)
+
+
+def _fuse_qkv_rope_gemm(trace):
+    """``qkv = hip_linear(x, w); q, k, v = hip_qkv_rope(qkv, cos, sin, ...)`` (qkv read nowhere else,
+    prefill / training rows) -> ``q, k, v = hip_linear_qkv_rope(x, w, cos, sin, ...)``: the attention
+    input projection stores the RoPE'd head layouts from its epilogue (csrc/gemm4.hip EPI 3), so the
+    [B, T, (nh + 2 ng) D] projection output never goes to HBM.  Reference counterpart: the
+    torch.compile / nvFuser cat+RoPE fusion of thunder/executors/torch_compile.py (rope) — here it
+    lands in the GEMM itself."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+    uses: dict[str, list] = {}
+    for k, b in enumerate(bsyms):
+        for a in b.flat_proxy_args:
+            uses.setdefault(a.name, []).append(k)
+    outs = {o.name for o in tree_flatten(trace.output)[0] if isinstance(o, TensorProxy)} if trace.output is not None else set()
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_qkv_rope or len(b.args) != 7:
+            continue
+        qkv, cos, sin, nh, ng, hs, rn = b.args
+        j = producer.get(getattr(qkv, "name", None))
+        if j is None or j in drop or bsyms[j].sym is not hip_linear or uses.get(qkv.name, []) != [i] or qkv.name in outs:
+            continue
+        p = _linear_parts(bsyms[j])
+        if any(p.get(k) is not None for k in ("bias", "residual", "act")) or p["x"].ndim != 3 or _rows(p["x"]) <= _GEMV_MAX_ROWS:
+            continue
+        if not all(isinstance(v, int) for v in (nh, ng, hs, rn)):
+            continue
+        if producer.get(getattr(cos, "name", None), -1) > j or producer.get(getattr(sin, "name", None), -1) > j:
+            continue  # cos / sin must exist where the GEMM runs
+        replace[j] = ex.bind_call_ctx(hip_linear_qkv_rope.bind(p["x"], p["w"], cos, sin, nh, ng, hs, rn, output=b.output))
+        drop.add(i)
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} qkv projection(s) with the RoPE split in the GEMM epilogue"))
+    return new
+
+
 def _post_claim(trace):
-    return _group_decode_projections(
-        _fuse_kv_cache_writes(_fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace)))))
+    return _fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
+        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace)))))))
 
 
 ex.post_claim_pass = _post_claim

@@ -33,6 +33,21 @@
 //   * blockIdx -> tile: bijective XCD remap, then groups of 8 tile-rows (L2 reuse of A and B panels).
 //   * Epilogue: fp32 alpha / bias / activation in registers -> bf16 in a per-wave swizzled LDS image
 //     -> 16-B row-contiguous stores (+ residual, same rounding points as ATen's linear then add).
+//   * SwiGLU epilogues (EPI, lta_gemm4_swiglu): the LLaMA MLP's gate/up pair and its backward never
+//     round-trip through HBM between the GEMM and the gating:
+//       EPI 1 (forward, "gate-up"): every 256-column output tile is 128 columns of W1 and the same 128
+//         columns of W2 (B staged from two weight tensors: LDS-DMA instructions 0-3 read W1 rows, 4-7 W2
+//         rows), so one workgroup holds a = x W1^T and b = x W2^T for the same 128 columns in its two
+//         wave columns; after the images meet in LDS it stores a, b (saved for the backward) and
+//         y = silu(a) * b — the separate swiglu pass (read a, b; write y) disappears.
+//       EPI 2 (backward, dgrad layout): g = dY . W_proj never leaves the chip; the store pass reads a, b
+//         and writes da = g b silu'(a), db = g silu(a) (the swiglu backward pass and g's round trip
+//         disappear).  Both round exactly where the unfused ops round (a, b, g in bf16).
+//   * EPI 3 (attention input projection, lta_gemm4_qkv_rope): the [q heads | k heads | v heads] x 128
+//     output columns are stored straight into q [B, nh, T, 128], k / v [B, ng, T, 128] with the
+//     rotate-half RoPE applied to q and k from the bf16 image (a dimension's partner d +- 64 is the
+//     chunk ch ^ 8 of the same image row): the qkv tensor is never written, the split/RoPE pass
+//     (read qkv, write q, k, v) disappears; same rounding points as csrc/rope.hip.
 #include "common.h"
 
 using namespace lta;
@@ -90,14 +105,24 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
   return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), bytes, 0x00020000};
 }
 
-template <bool MN>
+template <bool MN, bool DUAL = false>
 struct Stager {
-  i32x4 rsrc;
+  i32x4 rsrc, rsrc2;     // DUAL (K-major only): rows 0..127 from rsrc, rows 128..255 from rsrc2
   int voff0, voff1;      // K-major: voff0 for every i; MN-major: even / odd i
   int istride, kstride;  // bytes between consecutive i / consecutive K-tiles
   // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length
-  __device__ __forceinline__ void init(const __hip_bfloat16* X, int ld, int r0, int K, int wave, int lane) {
-    if constexpr (!MN) {
+  __device__ __forceinline__ void init(const __hip_bfloat16* X, int ld, int r0, int K, int wave, int lane,
+                                       const __hip_bfloat16* X2 = nullptr) {
+    if constexpr (DUAL) {
+      // r0 = the row of BOTH sources this tile starts at; each source contributes 128 rows
+      rsrc = make_rsrc(X + (int64_t)r0 * ld, (BM / 2 - 1) * ld * 2 + K * 2);
+      rsrc2 = make_rsrc(X2 + (int64_t)r0 * ld, (BM / 2 - 1) * ld * 2 + K * 2);
+      const int r = lane >> 3, c = (lane & 7) ^ r;
+      voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
+      voff1 = voff0;
+      istride = 32 * ld * 2;
+      kstride = BK * 2;
+    } else if constexpr (!MN) {
       // 8 rows of 128 B per instruction: lane -> row 8(4i + w) + (lane >> 3), stored chunk lane & 7,
       // which holds logical chunk (lane & 7) ^ row & 7
       const __hip_bfloat16* base = X + (int64_t)r0 * ld;
@@ -123,9 +148,11 @@ struct Stager {
   }
   __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
     const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    const bool second = DUAL && i >= 4;
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :
-                 : "s"(dst), "v"((MN && (i & 1)) ? voff1 : voff0), "s"(rsrc), "s"(i * istride + kt * kstride)
+                 : "s"(dst), "v"((MN && (i & 1)) ? voff1 : voff0), "s"(second ? rsrc2 : rsrc),
+                   "s"((second ? i - 4 : i) * istride + kt * kstride)
                  : "memory", "m0");
   }
 };
@@ -167,13 +194,37 @@ __device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& a, const bf16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR>
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// Extra operands of the fused epilogues.
+struct EpiArgs {
+  const __hip_bfloat16* B2;  // EPI 1: W2
+  __hip_bfloat16* C2;        // EPI 1: b; EPI 2: db; EPI 3: k
+  __hip_bfloat16* C3;        // EPI 1: y; EPI 3: v
+  const __hip_bfloat16* R2;  // EPI 2: b
+  const float* cos_;         // EPI 3: [T][128] fp32
+  const float* sin_;
+  int T, nh, ng;             // EPI 3: tokens per sequence, q heads, kv heads
+};
+
+// EPI 0: plain (bias / act / residual); 1: gate-up forward (B2 = W2; C = a, C2 = b, C3 = y, each
+// [M][N/2] with pitch ldc; C / C2 may be null); 2: swiglu backward (R = a, R2 = b, C = da, C2 = db,
+// all [M][N] with pitch ldc); 3: qkv + RoPE (C = q, C2 = k, C3 = v).  See the header.
+template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat16* __restrict__ A,
                                                             const __hip_bfloat16* __restrict__ B,
                                                             __hip_bfloat16* __restrict__ C,
                                                             const __hip_bfloat16* __restrict__ bias,
                                                             const __hip_bfloat16* __restrict__ R, int M, int N, int K,
-                                                            int lda, int ldb, int ldc, int ldr, float alpha) {
+                                                            int lda, int ldb, int ldc, int ldr, float alpha,
+                                                            EpiArgs ep = {}) {
+  const __hip_bfloat16* const B2 = ep.B2;
+  __hip_bfloat16* const C2 = ep.C2;
+  __hip_bfloat16* const C3 = ep.C3;
+  const __hip_bfloat16* const R2 = ep.R2;
+  static_assert(EPI != 1 || (!AT && !BT && !BIAS && !RES && ACT == 0), "gate-up: forward layout, no other epilogue");
+  static_assert(EPI != 3 || (!AT && !BT && !BIAS && !RES && ACT == 0), "qkv rope: forward layout, no other epilogue");
+  static_assert(EPI != 2 || (!AT && BT && !BIAS && !RES && ACT == 0), "swiglu backward: dgrad layout only");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];  // the ONLY LDS object (rule 4a)
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -193,9 +244,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   const int m0 = tm * BM, n0 = tn * BN;
 
   Stager<AT> sa;
-  Stager<BT> sb;
+  Stager<BT, EPI == 1> sb;
   sa.init(A, lda, m0, K, wave, lane);
-  sb.init(B, ldb, n0, K, wave, lane);
+  if constexpr (EPI == 1)
+    sb.init(B, ldb, n0 / 2, K, wave, lane, B2);
+  else
+    sb.init(B, ldb, n0, K, wave, lane);
   // glds j (0..15) of a K-tile: j < 8 -> A instruction j, else B instruction j - 8
   auto glds = [&](int j, int kt, char* stage) {
     if (j < 8)
@@ -316,7 +370,84 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     __builtin_amdgcn_sched_barrier(0);  // one accumulator column block at a time: bounded VGPR use
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
-  __builtin_amdgcn_wave_barrier();
+  if constexpr (EPI == 1) {
+    __syncthreads();  // the partner wave's image (b for a, a for b) is read below
+  } else {
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (EPI == 1) {
+    // a (wn = 0) / b (wn = 1) quadrant of this wave -> its own output at column n0/2 + ...
+    __hip_bfloat16* const dst = wn ? C2 : C;
+    if (dst != nullptr) {
+#pragma unroll
+      for (int it = 0; it < 32; ++it) {
+        const int id = it * 64 + lane;
+        const int row = id >> 4, ch = id & 15;
+        const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+        *reinterpret_cast<uint4*>(dst + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = v;
+      }
+    }
+    // y = silu(a) * b: wave (wm, wn) takes rows wn*64 .. +63 of the wm row half
+    const char* ia = smem + (wm * 2) * (128 * 256);
+    const char* ib = smem + (wm * 2 + 1) * (128 * 256);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int id = it * 64 + lane;
+      const int row = wn * 64 + (id >> 4), ch = id & 15;
+      const int off = row * 256 + ((ch ^ (row & 15)) << 4);
+      const uint4 va = *reinterpret_cast<const uint4*>(ia + off), vb = *reinterpret_cast<const uint4*>(ib + off);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&va);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&vb);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = __bfloat162float(a[e]);
+        o.h[e] = __float2bfloat16(x * sigmoid_f(x) * __bfloat162float(b[e]));
+      }
+      *reinterpret_cast<uint4*>(C3 + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = o.u;
+    }
+    return;
+  }
+  if constexpr (EPI == 3) {
+    // this wave's 128 columns are one head: q head cb, k head cb - nh or v head cb - nh - ng
+    const int cb = (n0 + wn * 128) >> 7;
+    const bool is_q = cb < ep.nh, is_k = !is_q && cb < ep.nh + ep.ng;
+    __hip_bfloat16* const dst = is_q ? C : (is_k ? C2 : C3);
+    const int hh = is_q ? cb : (is_k ? cb - ep.nh : cb - ep.nh - ep.ng);
+    const int nheads = is_q ? ep.nh : ep.ng;
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int id = it * 64 + lane;
+      const int row = id >> 4, ch = id & 15;
+      uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+      const int grow = m0 + wm * 128 + row;
+      const int bi = grow / ep.T, t = grow - bi * ep.T;
+      if (is_q || is_k) {
+        const uint4 pv = *reinterpret_cast<const uint4*>(wbuf + row * 256 + (((ch ^ 8) ^ (row & 15)) << 4));
+        const float4* cp = reinterpret_cast<const float4*>(ep.cos_ + (int64_t)t * 128 + ch * 8);
+        const float4* sp = reinterpret_cast<const float4*>(ep.sin_ + (int64_t)t * 128 + ch * 8);
+        const float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+        const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const __hip_bfloat16* x = reinterpret_cast<const __hip_bfloat16*>(&v);
+        const __hip_bfloat16* p = reinterpret_cast<const __hip_bfloat16*>(&pv);
+        const float sgn = ch < 8 ? -1.f : 1.f;
+        union {
+          uint4 u;
+          __hip_bfloat16 h[8];
+        } o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          o.h[e] = __float2bfloat16(__bfloat162float(x[e]) * cs[e] + sgn * __bfloat162float(p[e]) * sn[e]);
+        v = o.u;
+      }
+      *reinterpret_cast<uint4*>(dst + (((int64_t)bi * nheads + hh) * ep.T + t) * 128 + ch * 8) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < 32; ++it) {
     const int id = it * 64 + lane;
@@ -324,6 +455,28 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
     const int64_t grow = m0 + wm * 128 + row;
     const int gcol = n0 + wn * 128 + ch * 8;
+    if constexpr (EPI == 2) {
+      // v = g (bf16, as the unfused dgrad stores it); a, b at the same element
+      const uint4 va = *reinterpret_cast<const uint4*>(R + grow * ldc + gcol);
+      const uint4 vb = *reinterpret_cast<const uint4*>(R2 + grow * ldc + gcol);
+      const __hip_bfloat16* g = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&va);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&vb);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } oa, ob;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = __bfloat162float(a[e]), gg = __bfloat162float(g[e]), bb = __bfloat162float(b[e]);
+        const float sg = sigmoid_f(x);
+        oa.h[e] = __float2bfloat16(gg * bb * (sg * (1.f + x * (1.f - sg))));
+        ob.h[e] = __float2bfloat16(gg * (x * sg));
+      }
+      *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = oa.u;
+      *reinterpret_cast<uint4*>(C2 + grow * ldc + gcol) = ob.u;
+      continue;
+    }
     if constexpr (RES) {
       const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
       const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
@@ -405,4 +558,56 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   if (variant == 2) { LTA_G4V(2) }
 #undef LTA_G4V
   return -1;
+}
+
+// Fused SwiGLU GEMMs (see the header), bf16, variant-1 pipeline:
+//   mode 1 (gate-up forward): A = x [M][K] (lda), B = W1, B2 = W2, each [Nh][K] (pitch ldb);
+//     C = a, C2 = b (either may be null: not needed), C3 = y = silu(a) * b, each [M][Nh] (pitch ldc).
+//     Requires Nh % 128 == 0.
+//   mode 2 (swiglu backward): A = dY [M][K] (lda), B = W stored [K][Nh] (pitch ldb); R = a, R2 = b,
+//     C = da, C2 = db, each [M][Nh] (pitch ldc).  Requires Nh % 256 == 0.
+// Requires M % 256 == 0, K % 128 == 0, 16-B aligned rows, operands under 2 GiB.
+LTA_EXPORT int lta_gemm4_swiglu(const void* A, const void* B, const void* B2, void* C, void* C2, void* C3,
+                                const void* R, const void* R2, int M, int Nh, int K, int lda, int ldb, int ldc,
+                                int mode, hipStream_t s) {
+  if (M % BM || K % (2 * BK) || M <= 0 || Nh <= 0 || K <= 0) return -2;
+  if ((int64_t)M * lda * 2 >= (1ll << 31)) return -2;
+  const dim3 block(NTHR);
+  if (mode == 1) {
+    if (Nh % (BN / 2) || !B2 || !C3 || (int64_t)Nh * ldb * 2 >= (1ll << 31)) return -2;
+    const int N = 2 * Nh;
+    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 1>), dim3((M / BM) * (N / BN)), block,
+                       0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr,
+                       M, N, K, lda, ldb, ldc, 0, 1.f,
+                       EpiArgs{(const __hip_bfloat16*)B2, (__hip_bfloat16*)C2, (__hip_bfloat16*)C3, nullptr, nullptr,
+                               nullptr, 0, 0, 0});
+    return (int)hipGetLastError();
+  }
+  if (mode == 2) {
+    if (Nh % BN || !R || !R2 || !C || !C2 || (int64_t)K * ldb * 2 >= (1ll << 31)) return -2;
+    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, true, 1, 2>), dim3((M / BM) * (Nh / BN)), block,
+                       0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr,
+                       (const __hip_bfloat16*)R, M, Nh, K, lda, ldb, ldc, ldc, 1.f,
+                       EpiArgs{nullptr, (__hip_bfloat16*)C2, nullptr, (const __hip_bfloat16*)R2, nullptr, nullptr, 0, 0,
+                               0});
+    return (int)hipGetLastError();
+  }
+  return -1;
+}
+
+// q, k, v = RoPE-split(x . W^T) (EPI 3): A = x [M = B*T][K] (lda), B = W [(nh + 2 ng) * 128][K]
+// (ldb, rows = q heads, then k heads, then v heads); cos / sin fp32 [T][128] (rotate-half, full
+// width); q [B][nh][T][128], k / v [B][ng][T][128] contiguous.  Requires head size 128,
+// (nh + 2 ng) even, M % 256 == 0, K % 128 == 0.
+LTA_EXPORT int lta_gemm4_qkv_rope(const void* A, const void* B, const float* cos_, const float* sin_, void* q, void* k,
+                                  void* v, int M, int K, int lda, int ldb, int T, int nh, int ng, hipStream_t s) {
+  const int N = (nh + 2 * ng) * 128;
+  if (M % BM || K % (2 * BK) || N % BN || M <= 0 || K <= 0 || T <= 0 || M % T || nh <= 0 || ng <= 0) return -2;
+  if ((int64_t)M * lda * 2 >= (1ll << 31) || (int64_t)N * ldb * 2 >= (1ll << 31)) return -2;
+  if (!q || !k || !v || !cos_ || !sin_) return -2;
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 3>), dim3((M / BM) * (N / BN)),
+                     dim3(NTHR), 0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)q, nullptr,
+                     nullptr, M, N, K, lda, ldb, 0, 0, 1.f,
+                     EpiArgs{nullptr, (__hip_bfloat16*)k, (__hip_bfloat16*)v, nullptr, cos_, sin_, T, nh, ng});
+  return (int)hipGetLastError();
 }

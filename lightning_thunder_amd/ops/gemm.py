@@ -447,3 +447,114 @@ def grouped_mm(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> torch.Te
     check(lib.lta_gemm_grouped_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
                                        b.stride(0), stream_ptr(a.device)), "lta_gemm_grouped_nt_bf16")
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# fused SwiGLU GEMMs (csrc/gemm4.hip lta_gemm4_swiglu): the LLaMA MLP gate/up pair and its backward
+# ---------------------------------------------------------------------------------------------
+register_signature("lta_gemm4_swiglu", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+
+
+def _plain_2d(t: torch.Tensor) -> bool:
+    return (t.dim() == 2 and t.dtype == torch.bfloat16 and t.is_cuda and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
+def gate_up_supported(x2: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> bool:
+    if _os.environ.get("LTA_GEMM", "auto") == "torch" or _os.environ.get("LTA_FUSED_SWIGLU", "1") == "0":
+        return False
+    if not (_plain_2d(x2) and _plain_2d(w1) and _plain_2d(w2)) or w1.shape != w2.shape or w1.stride() != w2.stride():
+        return False
+    M, K = x2.shape
+    Nh = w1.shape[0]
+    return (w1.shape[1] == K and M % 256 == 0 and Nh % 128 == 0 and K % 128 == 0 and M > 0 and Nh > 0
+            and M * x2.stride(0) * 2 < 2 ** 31 and Nh * w1.stride(0) * 2 < 2 ** 31)
+
+
+def gate_up_swiglu(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, need_ab: bool = True):
+    """``a = x W1^T, b = x W2^T, y = silu(a) * b`` -> ``(a, b, y)`` (``a``/``b`` None when not
+    ``need_ab``).  One launch of the gate-up GEMM when supported, else linear + linear + swiglu with
+    the same rounding points."""
+    K = x.shape[-1]
+    Nh = w1.shape[0]
+    x2 = x.reshape(-1, K)
+    lead = x.shape[:-1]
+    if gate_up_supported(x2, w1, w2):
+        M = x2.shape[0]
+        y = torch.empty((M, Nh), dtype=torch.bfloat16, device=x.device)
+        a = torch.empty_like(y) if need_ab else None
+        b = torch.empty_like(y) if need_ab else None
+        _count("gemm4")
+        rc = require().lta_gemm4_swiglu(x2.data_ptr(), w1.data_ptr(), w2.data_ptr(),
+                                        None if a is None else a.data_ptr(), None if b is None else b.data_ptr(),
+                                        y.data_ptr(), None, None, M, Nh, K, x2.stride(0), w1.stride(0), Nh, 1,
+                                        stream_ptr(x.device))
+        check(rc, "lta_gemm4_swiglu")
+        r = (lambda t: None if t is None else t.reshape(*lead, Nh))
+        return r(a), r(b), r(y)
+    from .fused import swiglu_fwd
+
+    a = linear(x, w1)
+    b = linear(x, w2)
+    return a, b, swiglu_fwd(a, b)
+
+
+def matmul_swiglu_bwd(dy: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """``g = dy @ w`` (the dgrad of the MLP down-projection, ``w`` = its weight viewed [K, N]) then the
+    SwiGLU backward ``(da, db)`` of ``y = silu(a) * b``, with ``g`` kept on chip when supported."""
+    N = w.shape[1]
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    a2, b2 = a.reshape(-1, N), b.reshape(-1, N)
+    lay = gemm4_layout(dy2, w) if _os.environ.get("LTA_GEMM", "auto") != "torch" else None
+    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _os.environ.get("LTA_FUSED_SWIGLU", "1") != "0"
+            and a2.is_contiguous() and b2.is_contiguous() and a2.data_ptr() % 16 == 0 and b2.data_ptr() % 16 == 0
+            and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.shape[0] == dy2.shape[0]):
+        M, K = dy2.shape
+        da = torch.empty((M, N), dtype=torch.bfloat16, device=dy.device)
+        db = torch.empty_like(da)
+        _count("gemm4")
+        rc = require().lta_gemm4_swiglu(dy2.data_ptr(), w.data_ptr(), None, da.data_ptr(), db.data_ptr(), None,
+                                        a2.data_ptr(), b2.data_ptr(), M, N, K, lay[2], lay[3], N, 2,
+                                        stream_ptr(dy.device))
+        check(rc, "lta_gemm4_swiglu")
+        return da.reshape(a.shape), db.reshape(b.shape)
+    from .fused import swiglu_bwd
+
+    g = matmul(dy, w)
+    return swiglu_bwd(g.reshape(a.shape), a, b)
+
+
+register_signature("lta_gemm4_qkv_rope", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+
+
+def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_head: int,
+                    n_query_groups: int, head_size: int, rope_n: int):
+    """``q, k, v = qkv_split_rope(x @ w.T)`` for a ``[q heads | k heads | v heads]`` projection: one
+    launch of the GEMM whose epilogue applies the rotate-half RoPE and stores the [B, H, T, D]
+    head layouts (csrc/gemm4.hip EPI 3) when supported, else the GEMM then csrc/rope.hip."""
+    B, T, K = x.shape
+    x2 = x.reshape(-1, K)
+    nq = n_head + 2 * n_query_groups
+    ok = (_os.environ.get("LTA_GEMM", "auto") != "torch" and _os.environ.get("LTA_FUSED_QKV_ROPE", "1") != "0"
+          and head_size == 128 and rope_n == 128 and nq % 2 == 0 and tuple(w.shape) == (nq * 128, K)
+          and _plain_2d(x2) and _plain_2d(w) and x2.shape[0] % 256 == 0 and K % 128 == 0
+          and cos.dtype == torch.float32 and sin.dtype == torch.float32 and cos.shape[-1] == 128
+          and sin.shape[-1] == 128 and cos.shape[0] >= T and sin.shape[0] >= T
+          and x2.shape[0] * x2.stride(0) * 2 < 2 ** 31 and w.shape[0] * w.stride(0) * 2 < 2 ** 31)
+    if ok:
+        c = cos[:T].contiguous()
+        s = sin[:T].contiguous()
+        q = torch.empty((B, n_head, T, 128), dtype=torch.bfloat16, device=x.device)
+        k = torch.empty((B, n_query_groups, T, 128), dtype=torch.bfloat16, device=x.device)
+        v = torch.empty_like(k)
+        _count("gemm4")
+        rc = require().lta_gemm4_qkv_rope(x2.data_ptr(), w.data_ptr(), c.data_ptr(), s.data_ptr(), q.data_ptr(),
+                                          k.data_ptr(), v.data_ptr(), x2.shape[0], K, x2.stride(0), w.stride(0), T,
+                                          n_head, n_query_groups, stream_ptr(x.device))
+        check(rc, "lta_gemm4_qkv_rope")
+        return q, k, v
+    from .fused import qkv_rope_fwd
+
+    return qkv_rope_fwd(linear(x, w), cos, sin, n_head, n_query_groups, head_size, rope_n)

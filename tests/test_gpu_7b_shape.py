@@ -73,6 +73,10 @@ def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
     bw = str(thunder.last_backward_traces(tm)[-1])
     assert "hip_linear" in fw and "hip_flash_attn_fwd" in fw and "hip_cross_entropy_fwd" in fw, fw
     assert "hip_matmul" in bw and "hip_flash_attn_bwd" in bw, bw
+    # the MLP's SwiGLU runs in the GEMM epilogues (gate-up forward, down-projection dgrad backward)
+    assert "hip_gate_up" in fw and "hip_swiglu(" not in fw, fw
+    assert "hip_linear_qkv_rope" in fw and "hip_qkv_rope(" not in fw, fw
+    assert "hip_matmul_swiglu_bwd" in bw and "hip_swiglu_bwd(" not in bw, bw
     from lightning_thunder_amd.ops import gemm as G
 
     # every GEMM of the step ran on the hand-written kernel (no library fallback)
