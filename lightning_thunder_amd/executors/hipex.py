@@ -857,7 +857,10 @@ def _fuse_swiglu_gemms(trace):
     Reference counterpart: nvFuser fusing the pointwise SwiGLU into its matmul segments
     (thunder/executors/nvfuserex_impl.py:2437-2488)."""
     from ..core.trace import from_trace, TraceProvenance
+    from ..ops.gemm import _fused_swiglu_on
 
+    if not _fused_swiglu_on():
+        return trace
     bsyms = list(trace.bound_symbols)
     uses: dict[str, list] = {}
     for k, b in enumerate(bsyms):

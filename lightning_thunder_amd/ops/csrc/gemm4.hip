@@ -418,33 +418,40 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     __hip_bfloat16* const dst = is_q ? C : (is_k ? C2 : C3);
     const int hh = is_q ? cb : (is_k ? cb - ep.nh : cb - ep.nh - ep.ng);
     const int nheads = is_q ? ep.nh : ep.ng;
+    // one lane = one row's chunk pair (ch, ch + 8): a dimension d < 64 and its partner d + 64 share
+    // cos / sin (rotate-half duplicates them), so each pair loads them once
 #pragma unroll 4
-    for (int it = 0; it < 32; ++it) {
+    for (int it = 0; it < 16; ++it) {
       const int id = it * 64 + lane;
-      const int row = id >> 4, ch = id & 15;
-      uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+      const int row = id >> 3, ch = id & 7;
+      uint4 v0 = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+      uint4 v1 = *reinterpret_cast<const uint4*>(wbuf + row * 256 + (((ch + 8) ^ (row & 15)) << 4));
       const int grow = m0 + wm * 128 + row;
       const int bi = grow / ep.T, t = grow - bi * ep.T;
+      __hip_bfloat16* const o = dst + (((int64_t)bi * nheads + hh) * ep.T + t) * 128 + ch * 8;
       if (is_q || is_k) {
-        const uint4 pv = *reinterpret_cast<const uint4*>(wbuf + row * 256 + (((ch ^ 8) ^ (row & 15)) << 4));
         const float4* cp = reinterpret_cast<const float4*>(ep.cos_ + (int64_t)t * 128 + ch * 8);
         const float4* sp = reinterpret_cast<const float4*>(ep.sin_ + (int64_t)t * 128 + ch * 8);
         const float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
         const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
         const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const __hip_bfloat16* x = reinterpret_cast<const __hip_bfloat16*>(&v);
-        const __hip_bfloat16* p = reinterpret_cast<const __hip_bfloat16*>(&pv);
-        const float sgn = ch < 8 ? -1.f : 1.f;
+        const __hip_bfloat16* x1 = reinterpret_cast<const __hip_bfloat16*>(&v0);
+        const __hip_bfloat16* x2 = reinterpret_cast<const __hip_bfloat16*>(&v1);
         union {
           uint4 u;
           __hip_bfloat16 h[8];
-        } o;
+        } o1, o2;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          o.h[e] = __float2bfloat16(__bfloat162float(x[e]) * cs[e] + sgn * __bfloat162float(p[e]) * sn[e]);
-        v = o.u;
+        for (int e = 0; e < 8; ++e) {
+          const float a = __bfloat162float(x1[e]), bb = __bfloat162float(x2[e]);
+          o1.h[e] = __float2bfloat16(a * cs[e] - bb * sn[e]);
+          o2.h[e] = __float2bfloat16(bb * cs[e] + a * sn[e]);
+        }
+        v0 = o1.u;
+        v1 = o2.u;
       }
-      *reinterpret_cast<uint4*>(dst + (((int64_t)bi * nheads + hh) * ep.T + t) * 128 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(o) = v0;
+      *reinterpret_cast<uint4*>(o + 64) = v1;
     }
     return;
   }

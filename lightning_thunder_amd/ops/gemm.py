@@ -456,13 +456,22 @@ register_signature("lta_gemm4_swiglu", [c_void_p, c_void_p, c_void_p, c_void_p, 
                                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
 
 
+def _fused_swiglu_on() -> bool:
+    """SwiGLU in the GEMM epilogues is OPT-IN (``LTA_FUSED_SWIGLU=1``): measured on the Llama-2-7B
+    step (profiles/fused_epilogue_ab.txt: 169.3 ms fused vs 168.4 ms unfused) the
+    one-workgroup-per-CU kernel exposes its epilogue, and the third output (gate-up: 581 us per layer)
+    or the per-tile a / b loads (down-projection dgrad + swiglu backward: 382 us per layer) cost about
+    what the separate streaming passes they remove cost."""
+    return _os.environ.get("LTA_FUSED_SWIGLU", "0") == "1"
+
+
 def _plain_2d(t: torch.Tensor) -> bool:
     return (t.dim() == 2 and t.dtype == torch.bfloat16 and t.is_cuda and t.stride(1) == 1 and t.stride(0) % 8 == 0
             and t.data_ptr() % 16 == 0)
 
 
 def gate_up_supported(x2: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> bool:
-    if _os.environ.get("LTA_GEMM", "auto") == "torch" or _os.environ.get("LTA_FUSED_SWIGLU", "1") == "0":
+    if _os.environ.get("LTA_GEMM", "auto") == "torch" or not _fused_swiglu_on():
         return False
     if not (_plain_2d(x2) and _plain_2d(w1) and _plain_2d(w2)) or w1.shape != w2.shape or w1.stride() != w2.stride():
         return False
@@ -507,7 +516,7 @@ def matmul_swiglu_bwd(dy: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: tor
     dy2 = dy.reshape(-1, dy.shape[-1])
     a2, b2 = a.reshape(-1, N), b.reshape(-1, N)
     lay = gemm4_layout(dy2, w) if _os.environ.get("LTA_GEMM", "auto") != "torch" else None
-    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _os.environ.get("LTA_FUSED_SWIGLU", "1") != "0"
+    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _fused_swiglu_on()
             and a2.is_contiguous() and b2.is_contiguous() and a2.data_ptr() % 16 == 0 and b2.data_ptr() % 16 == 0
             and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.shape[0] == dy2.shape[0]):
         M, K = dy2.shape
@@ -529,6 +538,28 @@ register_signature("lta_gemm4_qkv_rope", [c_void_p, c_void_p, c_void_p, c_void_p
                                           c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
 
 
+_HALVES_EQUAL: dict = {}
+
+
+def _rope_halves_equal(cos: torch.Tensor, sin: torch.Tensor, T: int) -> bool:
+    """The fused epilogue reads cos / sin once per (d, d + 64) pair: true for rotate-half caches
+    built as cat(freqs, freqs) (LitGPT / HF).  Checked once per cache buffer (not per call)."""
+    try:
+        key = (cos.data_ptr(), sin.data_ptr(), tuple(cos.shape), tuple(sin.shape), cos._version, sin._version, T)
+    except RuntimeError:  # inference tensors carry no version counter
+        key = (cos.data_ptr(), sin.data_ptr(), tuple(cos.shape), tuple(sin.shape), T)
+    hit = _HALVES_EQUAL.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        c, s_ = cos[:T], sin[:T]
+        hit = bool(torch.equal(c[:, :64], c[:, 64:]) and torch.equal(s_[:, :64], s_[:, 64:]))
+        if len(_HALVES_EQUAL) > 64:
+            _HALVES_EQUAL.clear()
+        _HALVES_EQUAL[key] = hit
+    return hit
+
+
 def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_head: int,
                     n_query_groups: int, head_size: int, rope_n: int):
     """``q, k, v = qkv_split_rope(x @ w.T)`` for a ``[q heads | k heads | v heads]`` projection: one
@@ -542,8 +573,9 @@ def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, cos: torch.Tensor, sin: to
           and _plain_2d(x2) and _plain_2d(w) and x2.shape[0] % 256 == 0 and K % 128 == 0
           and cos.dtype == torch.float32 and sin.dtype == torch.float32 and cos.shape[-1] == 128
           and sin.shape[-1] == 128 and cos.shape[0] >= T and sin.shape[0] >= T
+          and cos.dim() == 2 and sin.dim() == 2
           and x2.shape[0] * x2.stride(0) * 2 < 2 ** 31 and w.shape[0] * w.stride(0) * 2 < 2 ** 31)
-    if ok:
+    if ok and _rope_halves_equal(cos, sin, T):
         c = cos[:T].contiguous()
         s = sin[:T].contiguous()
         q = torch.empty((B, n_head, T, 128), dtype=torch.bfloat16, device=x.device)

@@ -22,10 +22,12 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("gemm_mode", ["default", "hip"])
+@pytest.mark.parametrize("gemm_mode", ["default", "hip", "fused_swiglu"])
 def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
     if gemm_mode == "hip":
         monkeypatch.setenv("LTA_GEMM", "hip")
+    if gemm_mode == "fused_swiglu":
+        monkeypatch.setenv("LTA_FUSED_SWIGLU", "1")
     torch.manual_seed(0)
     dev = torch.device("cuda")
     m32 = GPT.from_name("llama2-7b-shape-2l").to(device=dev)
@@ -74,9 +76,10 @@ def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
     assert "hip_linear" in fw and "hip_flash_attn_fwd" in fw and "hip_cross_entropy_fwd" in fw, fw
     assert "hip_matmul" in bw and "hip_flash_attn_bwd" in bw, bw
     # the MLP's SwiGLU runs in the GEMM epilogues (gate-up forward, down-projection dgrad backward)
-    assert "hip_gate_up" in fw and "hip_swiglu(" not in fw, fw
+    if gemm_mode == "fused_swiglu":
+        assert "hip_gate_up" in fw and "hip_swiglu(" not in fw, fw
+        assert "hip_matmul_swiglu_bwd" in bw and "hip_swiglu_bwd(" not in bw, bw
     assert "hip_linear_qkv_rope" in fw and "hip_qkv_rope(" not in fw, fw
-    assert "hip_matmul_swiglu_bwd" in bw and "hip_swiglu_bwd(" not in bw, bw
     from lightning_thunder_amd.ops import gemm as G
 
     # every GEMM of the step ran on the hand-written kernel (no library fallback)

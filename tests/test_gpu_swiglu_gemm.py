@@ -9,6 +9,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _fused_on(monkeypatch):
+    monkeypatch.setenv("LTA_FUSED_SWIGLU", "1")  # opt-in epilogues (ops/gemm.py _fused_swiglu_on)
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
