@@ -281,11 +281,12 @@ def test_gemm_nt_bf16(shape, epi):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("e5m2", [False, True])
-def test_fp8_cast_and_transpose(e5m2):
+@pytest.mark.parametrize("shape", [(128, 192), (256, 384), (384, 1280)])  # 64x64 tiles / 128x128 tiles
+def test_fp8_cast_and_transpose(e5m2, shape):
     from lightning_thunder_amd.ops.fp8 import cast, cast_transpose, amax_into, E4M3_MAX, E5M2_MAX
 
     torch.manual_seed(0)
-    x = torch.randn(128, 192, device="cuda", dtype=torch.bfloat16) * 3
+    x = torch.randn(*shape, device="cuda", dtype=torch.bfloat16) * 3
     fmax = E5M2_MAX if e5m2 else E4M3_MAX
     amax = torch.zeros((), device="cuda")
     amax_into(x, amax)
@@ -297,8 +298,12 @@ def test_fp8_cast_and_transpose(e5m2):
     dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
     ref = (x.float() * scale).clamp(-fmax, fmax).to(dt).view(torch.uint8)
     assert (y != ref).sum().item() <= 2  # fp32 rounding of x*s at a tie at most
-    y2, yt = cast_transpose(x, amax, fmax, None, e5m2)
+    amax2 = torch.zeros((), device="cuda")
+    y2, yt = cast_transpose(x, amax, fmax, None, e5m2, amax_out=amax2)
     assert torch.equal(y2, y) and torch.equal(yt, y.t().contiguous())
+    torch.testing.assert_close(amax2, x.float().abs().amax())
+    _, yt2 = cast_transpose(x, amax, fmax, None, e5m2, rowmajor=False)
+    assert torch.equal(yt2, yt)
 
 
 @pytest.mark.parametrize("layout", ["nn", "tn", "tt", "nt"])
