@@ -132,14 +132,14 @@ def _fp8_quant_impl(t, e5m2):
     return quantize(t, e5m2)
 
 
-def _fp8_gemm_meta(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape):
+def _fp8_gemm_meta(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape, residual=None):
     return TensorProxy(like=qa, shape=tuple(out_shape), dtype=torch.bfloat16)
 
 
-def _fp8_gemm_impl(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape):
+def _fp8_gemm_impl(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape, residual=None):
     from ..ops.fp8 import gemm
 
-    return gemm(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape)
+    return gemm(qa, qb, sa, sb, fmt_a, fmt_b, bias, out_shape, residual)
 
 
 # quantize = amax + cast(+transpose) (pure: CSE shares one quantisation of x between the sibling
@@ -359,11 +359,21 @@ def _fuse_linear_epilogues(trace):
         for pos in (0, 1):
             y, r = b.args[pos], b.args[1 - pos]
             j = producer.get(y.name)
-            if j is None or j in drop or bsyms[j].sym not in (hip_linear, hip_matmul) or uses.get(y.name, 0) != 1:
+            if j is None or j in drop or bsyms[j].sym not in (hip_linear, hip_matmul, hip_fp8_gemm) or uses.get(y.name, 0) != 1:
                 continue
             lb = bsyms[j]
             if tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype or tuple(b.output.shape) != tuple(y.shape):
                 continue
+            if lb.sym is hip_fp8_gemm:
+                if len(lb.args) > 8 and lb.args[8] is not None or "residual" in lb.kwargs:
+                    continue
+                if producer.get(r.name, -1) > i or j in replace:
+                    continue
+                # computed where the add was (every input of the GEMM exists there)
+                nb = ex.bind_call_ctx(hip_fp8_gemm.bind(*lb.args[:8], r, output=b.output))
+                replace[i] = nb
+                drop.add(j)
+                break
             if producer.get(r.name, -1) > j:
                 continue  # the residual is produced after the GEMM: the fused op could not see it
             if lb.sym is hip_matmul:

@@ -81,13 +81,18 @@ __device__ __forceinline__ void mfma8(f32x4& acc, const v8i& a, const v8i& b) {
 
 #define LTA_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-template <int FA, int FB, bool BIAS>
+// RES: C = bf16(bf16(A.B^T / (sa sb) + bias) + R) — the residual add of the unfused pair, with the
+// same two rounding points (the FP8 transformer block's residual stream and the dgrad sum of the
+// gate / up projections never take a separate elementwise pass).
+template <int FA, int FB, bool BIAS, bool RES = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                            __hip_bfloat16* __restrict__ C,
                                                            const __hip_bfloat16* __restrict__ bias, int M, int N,
                                                            int K, int lda, int ldb, int ldc,
                                                            const float* __restrict__ sa,
-                                                           const float* __restrict__ sb) {
+                                                           const float* __restrict__ sb,
+                                                           const __hip_bfloat16* __restrict__ R = nullptr,
+                                                           int ldr = 0) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -196,7 +201,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
   for (int it = 0; it < 32; ++it) {
     const int id = it * 64 + lane;
     const int row = id >> 4, ch = id & 15;
-    const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+    uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+    if constexpr (RES) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(R + (int64_t)(m0 + wm * 128 + row) * ldr + n0 + wn * 128 + ch * 8);
+      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
+      union {
+        uint4 u;
+        __hip_bfloat16 h[8];
+      } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
+      v = o.u;
+    }
     *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * ldc + n0 + wn * 128 + ch * 8) = v;
   }
 }
@@ -224,5 +241,26 @@ LTA_EXPORT int lta_gemm4_fp8(const void* A, const void* B, void* C, const void* 
   else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_G8(0, 1, true); else LTA_G8(0, 1, false); }
   else return -1;
 #undef LTA_G8
+  return (int)hipGetLastError();
+}
+
+// lta_gemm4_fp8 + residual: C = bf16(bf16((A . B^T) / (sa sb) (+ bias)) + R), R [M, N] bf16 (pitch ldr).
+LTA_EXPORT int lta_gemm4_fp8_res(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                                 int K, int lda, int ldb, int ldc, int ldr, int fmt_a, int fmt_b, const void* sa,
+                                 const void* sb, hipStream_t stream) {
+  if (!R) return lta_gemm4_fp8(A, B, C, bias, M, N, K, lda, ldb, ldc, fmt_a, fmt_b, sa, sb, stream);
+  if (M % BM || N % BN || K % (2 * BKB) || M <= 0 || N <= 0 || lda % 16 || ldb % 16 || ldc % 8 || ldr % 8) return -2;
+  if ((int64_t)M * lda >= (1ll << 31) || (int64_t)N * ldb >= (1ll << 31)) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_G8R(FA, FB, BI)                                                                                      \
+  hipLaunchKernelGGL((gemm4_fp8_kernel<FA, FB, BI, true>), grid, block, 0, stream, (const char*)A, (const char*)B, \
+                     (__hip_bfloat16*)C, (const __hip_bfloat16*)bias, M, N, K, lda, ldb, ldc, (const float*)sa,  \
+                     (const float*)sb, (const __hip_bfloat16*)R, ldr)
+  const bool bi = bias != nullptr;
+  if (fmt_a == 0 && fmt_b == 0) { if (bi) LTA_G8R(0, 0, true); else LTA_G8R(0, 0, false); }
+  else if (fmt_a == 1 && fmt_b == 0) { if (bi) LTA_G8R(1, 0, true); else LTA_G8R(1, 0, false); }
+  else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_G8R(0, 1, true); else LTA_G8R(0, 1, false); }
+  else return -1;
+#undef LTA_G8R
   return (int)hipGetLastError();
 }

@@ -70,14 +70,28 @@ def gemm4_fp8_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
             and M * a.stride(0) < 2**31 and N * b.stride(0) < 2**31)
 
 
+register_signature("lta_gemm4_fp8_res", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                          c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p])
+
+
 def gemm_nt_fp8(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int = 0, fmt_b: int = 0,
-                bias: torch.Tensor | None = None) -> torch.Tensor:
+                bias: torch.Tensor | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
     """bf16 [M, N] = (a [M,K] . b[N,K]^T) / (sa * sb) (+ bias); a/b fp8 as uint8, sa/sb device scalars.
     The 4-wave pipelined kernel (gemm4_fp8) when the shape tiles, else the 8-wave one (gemm.hip)."""
     lib = require()
     M, K = a.shape
     N = b.shape[0]
     out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if residual is not None:
+        r2 = residual.reshape(M, N)
+        if (gemm4_fp8_supported(a, b) and r2.dtype == torch.bfloat16 and r2.stride(1) == 1 and r2.stride(0) % 8 == 0
+                and r2.data_ptr() % 16 == 0):
+            check(lib.lta_gemm4_fp8_res(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                        None if bias is None else bias.data_ptr(), r2.data_ptr(), M, N, K, a.stride(0),
+                                        b.stride(0), out.stride(0), r2.stride(0), fmt_a, fmt_b, sa.data_ptr(),
+                                        sb.data_ptr(), stream_ptr(a.device)), "lta_gemm4_fp8_res")
+            return out
+        return gemm_nt_fp8(a, b, sa, sb, fmt_a, fmt_b, bias) + r2
     fn, name = ((lib.lta_gemm4_fp8, "lta_gemm4_fp8") if gemm4_fp8_supported(a, b)
                 else (lib.lta_gemm_nt_fp8, "lta_gemm_nt_fp8"))
     check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), None if bias is None else bias.data_ptr(), M, N, K,
@@ -148,8 +162,8 @@ def quantize(t: torch.Tensor, e5m2: bool = False):
 
 
 def gemm(qa: torch.Tensor, qb: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int, fmt_b: int,
-         bias: torch.Tensor | None, out_shape) -> torch.Tensor:
-    return gemm_nt_fp8(qa, qb, sa, sb, fmt_a, fmt_b, bias).reshape(out_shape)
+         bias: torch.Tensor | None, out_shape, residual: torch.Tensor | None = None) -> torch.Tensor:
+    return gemm_nt_fp8(qa, qb, sa, sb, fmt_a, fmt_b, bias, residual).reshape(out_shape)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -359,6 +359,10 @@ def test_gemm_nt_fp8(fmts, shape):
     out = gemm_nt_fp8(a8.view(torch.uint8), b8.view(torch.uint8), sa, sb, fmts[0], fmts[1], bias)
     ref = (a8.float() @ b8.float().t()) / 8.0 + bias.float()
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=5e-2)
+    # residual epilogue: the unfused pair's rounding points (GEMM output in bf16, then the add)
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out_r = gemm_nt_fp8(a8.view(torch.uint8), b8.view(torch.uint8), sa, sb, fmts[0], fmts[1], bias, r)
+    assert torch.equal(out_r, out + r)
 
 
 @pytest.mark.gpu
