@@ -404,7 +404,10 @@ static void launch_cast(const void* x, void* y, int64_t n, const void* amax_in, 
 template <typename T, bool E5>
 static void launch_cast_t(const void* x, void* y, void* yt, int R, int C, const void* amax_in, float fmax,
                           void* scale_out, void* amax, hipStream_t s) {
-  if (R % 128 == 0 && C % 128 == 0 && std::getenv("LTA_CAST_T64") == nullptr) {
+  // 128 x 128 tiles only where they measured faster (profiles/fp8_cast_transpose_ab.json, round 3:
+  // 4096x12288 46 -> 38 us, 4096x22016 98 -> 80, 32000x4096 130 -> 113; but 4096x4096 12.8 -> 17.7 and
+  // 4096x11008 30 -> 35: fewer, larger tiles leave too few loads in flight on the smaller shapes)
+  if (R % 128 == 0 && C % 128 == 0 && (C >= 12288 || R >= 16384) && std::getenv("LTA_CAST_T64") == nullptr) {
     dim3 grid((unsigned)std::min<int64_t>((int64_t)(C / 128) * (R / 128), 1024)), block(256);
     hipLaunchKernelGGL((cast_transpose128_kernel<T, E5>), grid, block, 0, s, (const T*)x, (uint8_t*)y, (uint8_t*)yt,
                        R, C, (const float*)amax_in, fmax, (float*)scale_out, (float*)amax);
