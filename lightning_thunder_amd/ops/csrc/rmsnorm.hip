@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
   for (int64_t row = r0; row < r1; row += 2) {
     const bool two = row + 1 < r1;
     const float ra = rstd[row], rb = two ? rstd[row + 1] : 0.f;
-    Vec16<T> xv[2][CHUNKS], gv[2][CHUNKS];
+    Vec16<T> xv[2][CHUNKS], gv[2][CHUNKS], rv[2][CHUNKS];
 #pragma unroll
     for (int c = 0; c < CHUNKS; ++c) {
       const int idx = (c * kThreads + threadIdx.x) * V;
@@ -124,6 +124,12 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
         if (two) {
           xv[1][c] = load16(x + (row + 1) * cols + idx);
           gv[1][c] = load16(dy + (row + 1) * cols + idx);
+        }
+        // the residual-stream gradient is only added at the store, but is loaded here with the row
+        // operands so its latency hides under the block reduction instead of following it
+        if (res != nullptr) {
+          rv[0][c] = load16(res + row * cols + idx);
+          if (two) rv[1][c] = load16(res + (row + 1) * cols + idx);
         }
       }
     }
@@ -175,13 +181,12 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
       for (int c = 0; c < CHUNKS; ++c) {
         const int idx = (c * kThreads + threadIdx.x) * V;
         if (idx < cols) {
-          Vec16<T> o, rv;
-          if (res != nullptr) rv = load16(res + rr * cols + idx);  // gradient arriving through the residual
+          Vec16<T> o;
 #pragma unroll
           for (int j = 0; j < V; ++j) {
             const float xh = to_f32(xv[h][c].v[j]) * r;
             const float gw = to_f32(gv[h][c].v[j]) * to_f32(wv[c].v[j]);
-            const float add = res != nullptr ? to_f32(rv.v[j]) : 0.f;
+            const float add = res != nullptr ? to_f32(rv[h][c].v[j]) : 0.f;  // gradient through the residual
             o.v[j] = from_f32<T>(r * (gw - xh * dot) + add);
           }
           store16(dx + rr * cols + idx, o);

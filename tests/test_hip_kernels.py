@@ -33,6 +33,11 @@ def test_rmsnorm_fwd_bwd(dtype, shape):
     dx, dw = rms_norm_bwd(dy, x, w, rstd)
     torch.testing.assert_close(dx.float(), xf.grad, atol=TOL[dtype] * 4, rtol=TOL[dtype] * 2)
     torch.testing.assert_close(dw.float(), wf.grad, atol=TOL[dtype] * shape[0] * 4, rtol=TOL[dtype] * 4)
+    # residual-gradient form (the add of the pre-norm block's skip path in the store pass)
+    r = torch.randn(shape, device="cuda", dtype=dtype)
+    dx2, dw2 = rms_norm_bwd(dy, x, w, rstd, r)
+    torch.testing.assert_close(dx2.float(), xf.grad + r.float(), atol=TOL[dtype] * 8, rtol=TOL[dtype] * 2)
+    torch.testing.assert_close(dw2, dw)
 
 
 @pytest.mark.parametrize("dtype", DT)
