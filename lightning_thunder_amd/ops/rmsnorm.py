@@ -29,8 +29,11 @@ def rms_norm_fwd(x: torch.Tensor, weight: torch.Tensor | None, eps: float):
 
 
 def _bwd_blocks(rows: int) -> int:
-    # ~2 workgroups per CU on MI355X (256 CUs), at least one row each
-    return max(1, min(rows, 512))
+    # workgroups per launch: LTA_RMS_BWD_BLOCKS (A/B knob), default ~2 per CU on MI355X (256 CUs),
+    # at least one row each
+    import os
+
+    return max(1, min(rows, int(os.environ.get("LTA_RMS_BWD_BLOCKS", "512"))))
 
 
 def rms_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor | None, rstd: torch.Tensor,
