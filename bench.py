@@ -37,7 +37,9 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--model", default="Llama-2-7b-hf")
     p.add_argument("--seq", type=int, default=4096)
-    p.add_argument("--mbs", type=int, default=1)
+    p.add_argument("--mbs", type=int, default=None,
+                   help="micro-batch per GPU; default 1 on one GPU (BASELINE config 1: MBS 1) and 2 for data-parallel "
+                        "N>1 (the reference's ZeRO-2 chart is at batch 2 per GPU, BASELINE.md)")
     p.add_argument("--mode", default="thunder", choices=["thunder", "eager"])
     p.add_argument("--parallel", default="auto", choices=["auto", "fsdp", "ddp", "tp", "none"],
                    help="auto: fsdp for N>1; tp: Megatron tensor parallel over all ranks (BASELINE config 4, "
@@ -224,6 +226,8 @@ def run(args, rank, world, device, mode):
 def main():
     args = parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.mbs is None:
+        args.mbs = 2 if world > 1 and args.parallel in ("auto", "fsdp", "ddp") else 1
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -237,16 +241,23 @@ def main():
     # rehearsal of the RCCL program: bucketed / coalesced collectives at full model size)
     force = os.environ.get("LTA_BENCH_FORCE_DIST") == "1"
     if world > 1 or force:
+        from datetime import timedelta
+
+        # as the reference's benchmark_litgpt.py:64-69: no record_stream allocator thrash, async
+        # error handling, and a bounded rendezvous / collective timeout instead of an endless hang
         os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        timeout = timedelta(minutes=int(os.environ.get("LTA_DIST_TIMEOUT_MIN", "10")))
         if backend == "nccl":
             # a high-priority RCCL stream gets a hardware queue of its own: on the normal-priority
             # pool the collectives' stream can share the compute stream's queue (GPU_MAX_HW_QUEUES)
             # and then never run concurrently with compute (measured: one queue, zero overlap)
             from lightning_thunder_amd.distributed import high_priority_pg_options
 
-            torch.distributed.init_process_group("nccl", device_id=device, pg_options=high_priority_pg_options())
+            torch.distributed.init_process_group("nccl", device_id=device, pg_options=high_priority_pg_options(),
+                                                 timeout=timeout)
         else:
-            torch.distributed.init_process_group(backend)
+            torch.distributed.init_process_group(backend, timeout=timeout)
 
     dt, cfg, mem, parallel = run(args, rank, world, device, args.mode)
     data_parallel = parallel != "tp"

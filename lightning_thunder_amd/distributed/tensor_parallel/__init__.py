@@ -34,6 +34,8 @@ Design (MI355X, RCCL over xGMI):
 """
 from __future__ import annotations
 
+import dataclasses
+
 from typing import Sequence
 
 import torch
@@ -90,6 +92,8 @@ class TensorParallelTransform(Transform):
                 continue
             if not all(hasattr(cfg, a) for a in ("n_head", "n_query_groups", "head_size")):
                 continue
+            if not dataclasses.is_dataclass(cfg) or isinstance(cfg, type):
+                continue  # the localized copy is made with dataclasses.replace
             if not isinstance(mods.get(name), torch.nn.Linear) or not isinstance(mods.get(proj), torch.nn.Linear):
                 continue
             out.append((parent, name, proj))
@@ -156,6 +160,11 @@ class TensorParallelTransform(Transform):
                     prm._parameters["weight"] = newp
                     # the attention code now sees this rank's heads only
                     pm.config = replace(cfg, n_head=nh // world, n_query_groups=ng // world)
+                    kv = getattr(pm, "kv_cache", None)
+                    if kv is not None and hasattr(kv, "k") and kv.k.shape[1] == ng:
+                        # a cache allocated before sharding holds every kv group: keep this rank's
+                        kv.k = kv.k[:, rank * (ng // world):(rank + 1) * (ng // world)].contiguous()
+                        kv.v = kv.v[:, rank * (ng // world):(rank + 1) * (ng // world)].contiguous()
                     head_done.update((qkv_name, proj_name))
             for name, kind in self.targets.items():
                 if name in head_done:
@@ -448,6 +457,10 @@ def vocab_parallel_loss(trace, group):
         ignore_index = args[4] if len(args) > 4 else kw.get("ignore_index", -100)
         reduction = args[6] if len(args) > 6 else kw.get("reduction", "mean")
         smoothing = args[7] if len(args) > 7 else kw.get("label_smoothing", 0.0)
+        size_average = args[3] if len(args) > 3 else kw.get("size_average")
+        reduce_ = args[5] if len(args) > 5 else kw.get("reduce")
+        if size_average is not None or reduce_ is not None:
+            continue  # legacy reduction flags (reduce=False means 'none'): leave the call alone
         if weight is not None or smoothing or reduction not in ("mean", "sum") or not isinstance(inp, TensorProxy):
             continue
         if inp.ndim != 2 or target is None:

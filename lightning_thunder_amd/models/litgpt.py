@@ -344,8 +344,11 @@ class GPT(nn.Module):
         max_seq_length = max_seq_length or c.block_size
         dtype = dtype or self.lm_head.weight.dtype
         device = device or self.lm_head.weight.device
-        shape = (batch_size, c.n_query_groups, max_seq_length, c.head_size)
         for block in self.transformer.h:
+            # sized from the attention module's own config: under head-parallel TP it holds only
+            # this rank's kv groups (distributed/tensor_parallel swaps in a localized config)
+            ac = getattr(block.attn, "config", c)
+            shape = (batch_size, ac.n_query_groups, max_seq_length, ac.head_size)
             block.attn.kv_cache = KVCache(shape, shape, device=device, dtype=dtype)
         if self.cos.numel() == 0 or self.cos.shape[0] < max_seq_length:
             self.set_rope_cache(max_seq_length, device=device)

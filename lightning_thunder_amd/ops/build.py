@@ -40,11 +40,13 @@ def _sources():
     return hip, cpp
 
 
-# Per-file device flags.  attention_bwd: MFMAs written as intrinsics take VGPR destinations, so the
+# Per-file device flags.  attention_fwd4: no SLP vectorisation (it packs the softmax row-sum chain
+# into v_pk_add_f32, an anti-lever beside MFMAs: MI355X_MICROARCH.md constants table).  attention_bwd: MFMAs written as intrinsics take VGPR destinations, so the
 # S / dP tiles stay where their softmax reads them while the dK / dV accumulators (inline-asm MFMAs)
 # own the AGPR file (without it hipcc swaps them through AGPRs every tile).
 FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-              "attention_fwd3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+              "attention_fwd3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+              "attention_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:

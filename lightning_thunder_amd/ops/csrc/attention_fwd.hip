@@ -633,6 +633,9 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 
 }  // namespace
 
+LTA_EXPORT int lta_attn_fwd_v4(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
+                               int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
+                               const int64_t* o_strides, const int64_t* qkv_strides, int defer, hipStream_t stream);
 LTA_EXPORT int lta_attn_fwd_v3(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
                                int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
                                const int64_t* o_strides, int defer, hipStream_t stream);
@@ -668,7 +671,13 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
     ex.offset = (unsigned)offset;
     exf |= kExDrop;
   }
-  if (dense && D == 128 && exf == 0 && g_fwd_impl >= 7 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
+  if (D == 128 && exf == 0 && g_fwd_impl >= 9 && Tq > 0 && Sk > 0) {  // v4 (attention_fwd4.hip)
+    const int rc = lta_attn_fwd_v4(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides,
+                                   qkv_strides, g_fwd_impl == 9 ? 0 : (g_fwd_impl == 10 ? 1 : 1 | ((g_fwd_impl - 10) << 1)),
+                                   stream);
+    if (rc != -1) return rc;
+  }
+  if (dense && D == 128 && exf == 0 && g_fwd_impl >= 7 && g_fwd_impl <= 8 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
     return lta_attn_fwd_v3(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, g_fwd_impl == 8,
                            stream);
   if (dense && D == 128 && exf == 0 && g_fwd_impl != 0 && Tq > 0 && Sk > 0) {
@@ -712,6 +721,6 @@ LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void*
 // forward kernel selection for D = 128 without mask / dropout (A/B measurement hook)
 LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
   const int old = g_fwd_impl;
-  if (impl >= 0 && impl <= 8) g_fwd_impl = impl;
+  if (impl >= 0 && impl <= 14) g_fwd_impl = impl;
   return old;
 }

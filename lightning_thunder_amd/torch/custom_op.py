@@ -21,7 +21,6 @@ executor ``thunder/executors/custom_op_ex.py:15``.
 from __future__ import annotations
 
 import inspect
-import itertools
 
 import torch
 
@@ -35,8 +34,6 @@ except ImportError:  # pragma: no cover
     _co = None
 
 _symbols: dict = {}
-_bwd_state: dict[int, tuple] = {}
-_ids = itertools.count()
 
 
 def opdef_of(func):
@@ -119,39 +116,60 @@ class _RuntimeCtx:
             setattr(self, k, v)
 
 
+class _BwdState:
+    """What the backward symbol of one traced call needs besides its tensor operands.  It travels as
+    the symbol's ``_state`` keyword, so the trace that calls the backward owns it (printed into the
+    program's object context) and it is freed with that trace — no process-global registry."""
+
+    __slots__ = ("n_saved", "tnames", "static", "needs", "input_likes")
+
+    def __init__(self, n_saved, tnames, static, needs, input_likes):
+        self.n_saved, self.tnames, self.static, self.needs = n_saved, tnames, static, needs
+        self.input_likes = input_likes  # (shape, device, dtype) of each differentiable input, else None
+
+
 def _bwd_impl(opdef):
-    def impl(*flat, _key):
-        n_saved, tnames, n_grads, static, needs = _bwd_state[_key]
-        saved = flat[:n_saved]
-        tvals = flat[n_saved:n_saved + len(tnames)]
-        grads = flat[n_saved + len(tnames):]
-        attrs = dict(static)
-        attrs.update(zip(tnames, tvals))
-        res = opdef._backward_fn(_RuntimeCtx(saved, attrs, needs), *grads)
+    def impl(*flat, _state):
+        st = _state
+        saved = flat[:st.n_saved]
+        tvals = flat[st.n_saved:st.n_saved + len(st.tnames)]
+        grads = flat[st.n_saved + len(st.tnames):]
+        attrs = dict(st.static)
+        attrs.update(zip(st.tnames, tvals))
+        res = opdef._backward_fn(_RuntimeCtx(saved, attrs, st.needs), *grads)
         return tuple(res) if isinstance(res, (tuple, list)) else (res,)
 
     return impl
 
 
-def _bwd_meta(opdef, inputs):
+def _bwd_meta(opdef):
     impl = _bwd_impl(opdef)
 
-    def meta(*flat, _key):
+    def meta(*flat, _state):
         device = _device_of(flat)
         mflat = [_meta_tensor(x) for x in flat]
         try:
             with torch.no_grad():
-                out = impl(*mflat, _key=_key)
+                out = impl(*mflat, _state=_state)
             return tuple(_proxy_like(o, device) for o in out)
         except Exception:
             # the backward does not run on meta tensors: assume one gradient per tensor input
-            return tuple(TensorProxy(like=x) if isinstance(x, TensorProxy) and x.dtype.is_floating_point else None
-                         for x in inputs[_key])
+            return tuple(None if lk is None else TensorProxy(shape=lk[0], device=lk[1], dtype=lk[2])
+                         for lk in _state.input_likes)
 
     return meta
 
 
-_bwd_inputs: dict[int, tuple] = {}
+def check_supported(opdef) -> None:
+    """Refuse custom ops that mutate their arguments, as the reference does
+    (``thunder/torch/custom_op.py:347-350``): a pure symbol would let DCE drop the write (e.g. a
+    mutator returning None) and CSE merge two calls, losing the mutation without an error."""
+    schema = opdef._opoverload._schema
+    if schema.is_mutable:
+        mutated = [a.name for a in schema.arguments if a.alias_info is not None and a.alias_info.is_write]
+        raise NotImplementedError(
+            f"custom op {opdef._namespace}::{opdef._name} mutates one or more of its arguments "
+            f"({', '.join(mutated) or 'see its schema'}), which is not supported")
 
 
 def custom_op_symbol(opdef) -> Symbol:
@@ -160,6 +178,7 @@ def custom_op_symbol(opdef) -> Symbol:
     sym = _symbols.get(op)
     if sym is not None:
         return sym
+    check_supported(opdef)
     qual = f"{opdef._namespace}::{opdef._name}"
     pname = "custom_op_" + "".join(c if c.isalnum() else "_" for c in f"{opdef._namespace}_{opdef._name}")
     from ..core.prims import OpTags
@@ -173,7 +192,7 @@ def custom_op_symbol(opdef) -> Symbol:
 
     custom_opex.register(sym, op)
     if opdef._backward_fn is not None and opdef._setup_context_fn is not None:
-        bsym = Symbol(pname.replace("custom_op_", "custom_op_bwd_", 1), _bwd_meta(opdef, _bwd_inputs),
+        bsym = Symbol(pname.replace("custom_op_", "custom_op_bwd_", 1), _bwd_meta(opdef),
                       id=f"custom_op_bwd.{qual}", is_prim=True)
         register_symbol(bsym)
         custom_opex.register(bsym, _bwd_impl(opdef))
@@ -212,16 +231,16 @@ def _make_rule(sym, bsym, opdef):
             return None
         needs = tuple(isinstance(x, TensorProxy) and x.dtype.is_floating_point for x in inputs)
         outs = tuple(out) if isinstance(out, (tuple, list)) else (out,)
-        key = next(_ids)
-        _bwd_state[key] = (len(saved), tuple(tnames), len(outs), static, needs)
-        _bwd_inputs[key] = inputs
+        likes = tuple((tuple(x.shape), x.device, x.dtype) if isinstance(x, TensorProxy) and x.dtype.is_floating_point
+                      else None for x in inputs)
+        state = _BwdState(len(saved), tuple(tnames), static, needs, likes)
 
         def bwd(*gs):
             if any(g is None for g in gs):
                 from .. import torch as ltorch
 
                 gs = tuple(ltorch.zeros_like(o) if g is None else g for g, o in zip(gs, outs))
-            grads = bsym(*saved, *tvals, *gs, _key=key)
+            grads = bsym(*saved, *tvals, *gs, _state=state)
             grads = tuple(grads) if isinstance(grads, (tuple, list)) else (grads,)
             # one entry per positional argument of the call
             return tuple(grads[i] if i < len(grads) else None for i in range(len(args)))

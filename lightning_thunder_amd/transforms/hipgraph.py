@@ -30,6 +30,7 @@ next replay of the same region (same contract as the reference's runner).  Pass
 from __future__ import annotations
 
 import threading
+import weakref
 
 import torch
 
@@ -149,7 +150,10 @@ class HipGraphRunner:
             # which invalidates any other signature's "already written back" record for it
             epochs = self.owner._bump_epochs([t.data_ptr() for t in dst])
             if private and not any(t.is_inference() for t in dst):
-                self._written_back[sig] = tuple((t.data_ptr(), t._version, ep) for t, ep in zip(dst, epochs))
+                # the storage itself is remembered (weakly): an address the caching allocator hands
+                # to a NEW tensor whose version counter happens to match must not pass as written back
+                self._written_back[sig] = tuple((t.data_ptr(), t._version, ep, weakref.ref(t.untyped_storage()))
+                                                for t, ep in zip(dst, epochs))
             else:
                 self._written_back.pop(sig, None)
         self.replays += 1
@@ -165,7 +169,9 @@ class HipGraphRunner:
         rec = self._written_back.get(sig)
         if rec is not None and not any(t.is_inference() for t in src):
             cur = tuple((t.data_ptr(), t._version, self.owner._epoch(t.data_ptr())) for t in src)
-            if cur == rec:
+            same_storage = all(r[3]() is not None and _same_storage(r[3](), t.untyped_storage())
+                               for r, t in zip(rec, src))
+            if same_storage and cur == tuple(r[:3] for r in rec):
                 return
         torch._foreach_copy_([ins[i] for i in self._bound], src)
 
@@ -191,6 +197,12 @@ class HipGraphRunner:
         self.entries[key] = e
         self.captures += 1
         return e
+
+
+def _same_storage(a, b) -> bool:
+    """Whether two untyped-storage handles are the same allocation object (storage handles are fresh
+    Python wrappers on each access; compare the underlying StorageImpl)."""
+    return a._cdata == b._cdata
 
 
 class HipGraphTransform(Transform):

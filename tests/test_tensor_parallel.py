@@ -258,3 +258,50 @@ def test_megatron_llama_head_parallel_vocab_parallel():
             assert res["embed_allreduce"] == 1 and res["vocab_ce"] == 1, res
             if res["sdpa_heads"]:
                 assert res["sdpa_heads"][0][1] == 4 // WORLD, res  # local query heads
+
+
+def _tp_kv_cache_worker(rank, port, out_dir):
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed import column_parallel, row_parallel
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.manual_seed(0)
+        ref = GPT.from_name("llama3-like").double()
+        init_weights(ref)
+        m = GPT.from_name("llama3-like").double()
+        m.load_state_dict(ref.state_dict())
+        n = m.config.n_layer
+        tm = thunder.jit(m)
+        tm = column_parallel(tm, [f"transformer.h.{i}.{s}" for i in range(n) for s in ("attn.attn", "mlp.fc_1", "mlp.fc_2")])
+        tm = row_parallel(tm, [f"transformer.h.{i}.{s}" for i in range(n) for s in ("attn.proj", "mlp.proj")])
+        for mm in (ref, m):
+            mm.set_rope_cache(16)
+            mm.set_kv_cache(batch_size=1, max_seq_length=16, device="cpu", dtype=torch.float64)
+        res = {"cache_groups": tuple(m.transformer.h[0].attn.kv_cache.k.shape)}
+        x = torch.randint(0, 320, (1, 6))
+        pos = torch.arange(6)
+        err = (tm(x, pos) - ref(x, pos)).abs().max().item()
+        nxt = torch.randint(0, 320, (1, 1))
+        p1 = torch.tensor([6])
+        err = max(err, (tm(nxt, p1) - ref(nxt, p1)).abs().max().item())
+        res["err"] = err
+        torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    os._exit(0)
+
+
+def test_head_parallel_kv_cache_decode():
+    """Head-parallel TP sizes each block's KV cache from the attention module's localized config
+    (this rank's kv groups), so prefill + a decode step against the cache match the unsharded model."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_tp_kv_cache_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        for r in range(WORLD):
+            res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
+            assert res["cache_groups"][1] == 2 // WORLD, res  # llama3-like: 2 kv groups
+            assert res["err"] < 1e-9, res

@@ -230,6 +230,66 @@ def test_custom_op_saves_output_and_computed_attrs():
     torch.testing.assert_close(g, x.grad)
 
 
+def test_custom_op_mutating_args_is_refused():
+    """A custom op with non-empty ``mutates_args`` is refused (reference
+    thunder/torch/custom_op.py:347-350), never traced as a pure symbol whose write DCE could drop."""
+    @torch.library.custom_op("lta_test::add_into", mutates_args=("out",))
+    def add_into(x: torch.Tensor, out: torch.Tensor) -> None:
+        out.add_(x)
+
+    @add_into.register_fake
+    def _(x, out):
+        return None
+
+    def f(x, out):
+        add_into(x, out)
+        return x * 2
+
+    x, buf = torch.randn(4), torch.zeros(4)
+    with pytest.raises(NotImplementedError, match="mutates"):
+        thunder.jit(f)(x, buf)
+    # eager still works, and the write is observable
+    f(x, buf)
+    torch.testing.assert_close(buf, x)
+
+
+def test_custom_op_backward_state_is_trace_owned():
+    """The backward symbol's per-call state rides in the bound symbol (freed with the trace), not
+    in a process-global dict that grows with every retrace."""
+    import lightning_thunder_amd.torch.custom_op as co
+
+    assert not hasattr(co, "_bwd_state") and not hasattr(co, "_bwd_inputs")
+
+    @torch.library.custom_op("lta_test::cube", mutates_args=())
+    def cube(x: torch.Tensor) -> torch.Tensor:
+        return x * x * x
+
+    @cube.register_fake
+    def _(x):
+        return torch.empty_like(x)
+
+    def setup(ctx, inputs, output):
+        ctx.save_for_backward(inputs[0])
+
+    def bwd(ctx, g):
+        (x,) = ctx.saved_tensors
+        return 3 * g * x * x
+
+    cube.register_autograd(bwd, setup_context=setup)
+    jf = thunder.jit(lambda x: cube(x).sum())
+    x = torch.randn(6, requires_grad=True)
+    jf(x).backward()
+    torch.testing.assert_close(x.grad, 3 * x.detach() ** 2)
+    bw = thunder.last_backward_traces(jf)[-1]
+    def walk(bsyms):
+        for b in bsyms:
+            yield b
+            yield from walk(b.subsymbols)
+
+    states = [v for b in walk(bw.bound_symbols) for v in b.kwargs.values() if isinstance(v, co._BwdState)]
+    assert len(states) == 1, str(bw)
+
+
 def test_examine_patterns_and_memory(capsys):
     from lightning_thunder_amd.examine import examine, make_trace_dot, get_alloc_memory
     from lightning_thunder_amd.core.patterns import Pattern
