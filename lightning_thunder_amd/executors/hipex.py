@@ -62,7 +62,15 @@ def _linear_checker(a, w, bias=None):
         return False
     if M <= 8:  # decode: the weight-streaming GEMV (csrc/gemv.hip)
         return K % 8 == 0
-    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+    return _hand_gemm_shape(M, N, K)
+
+
+def _hand_gemm_shape(M: int, N: int, K: int) -> bool:
+    """A shape some hand GEMM tiles: gemm4 (any M >= 64 and N % 8 with edge tiles, K % 128) or the
+    8-wave kernel (M, N % 256, K % 64)."""
+    from ..ops.gemm import GEMM4_MIN_M
+
+    return (M >= GEMM4_MIN_M and N % 8 == 0 and K % 128 == 0) or (M % 256 == 0 and N % 256 == 0 and K % 64 == 0)
 
 
 def _linear_exec(a, w, bias=None):
@@ -93,7 +101,7 @@ def _mm_checker(a, b):
     for s in a.shape[:-1]:
         M *= s
     K, N = b.shape
-    return a.shape[-1] == K and M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+    return a.shape[-1] == K and _hand_gemm_shape(M, N, K)
 
 
 def _mm_meta(a, b, residual=None):
@@ -1407,7 +1415,9 @@ def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=Fa
     if query.dtype not in (torch.bfloat16, torch.float16) or key.dtype != query.dtype or value.dtype != query.dtype:
         return False
     D = query.shape[-1]
-    if D not in (64, 96, 128) or key.shape[-1] != D or value.shape[-1] != D:
+    from ..ops.attention import padded_head_dim
+
+    if padded_head_dim(D) is None or key.shape[-1] != D or value.shape[-1] != D:
         return False
     if key.shape[1] != value.shape[1] or query.shape[1] % key.shape[1] != 0:
         return False

@@ -116,9 +116,8 @@ class HipFusion:
         self.number_pos = [i for i, a in enumerate(inputs) if not isinstance(a, TensorProxy)]
         self._variants: dict = {}
         self._lock = threading.Lock()
-        nwords = len(self.tensor_pos) + max(len(outputs), 1) + len(self.number_pos)
-        self._argbuf_t = ctypes.c_uint64 * nwords
-        self._argbuf_ws_t = ctypes.c_uint64 * (nwords + 1)  # + the workspace pointer (column mode)
+        # + the workspace pointer (column mode) in the second type
+        self._argbuf_t, self._argbuf_ws_t = arg_buffer_types(len(self.tensor_pos), len(outputs), len(self.number_pos))
 
     def __repr__(self):
         return f"HipFusion({self.name}, {len(self.nodes)} prims)"
@@ -155,8 +154,7 @@ class HipFusion:
             for p, t in zip((self.inputs[i] for i in self.tensor_pos), tensors):
                 targs[p.name] = cg.TensorArg(tuple(t.shape), tuple(t.stride()), t.dtype, t.data_ptr() % 16 == 0)
             ks = cg.generate(self.plan, self.inputs, self.outputs, targs)
-            fns = [load_kernel(ks)] + [load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.extra]
-            v = (fns, ks)
+            v = (load_kernels(ks), ks)
             self._variants[key] = v
             return v
 
@@ -175,33 +173,55 @@ class HipFusion:
         if any(o.numel() == 0 for o in outs) or any(t.numel() == 0 for t in tensors):
             return tuple(outs)
         (fns, ks) = self._variant(tensors)
-        buf = self._argbuf_ws_t() if ks.ws_bytes else self._argbuf_t()
-        k = 0
-        for t in tensors:
-            buf[k] = t.data_ptr()
-            k += 1
-        for o in outs:
-            buf[k] = o.data_ptr()
-            k += 1
-        if not outs:
-            k += 1
-        for i in self.number_pos:
-            buf[k] = _double_bits(args[i])
-            k += 1
-        ws = None
-        if ks.ws_bytes:
-            ws = torch.empty(ks.ws_bytes, dtype=torch.uint8, device=dev)  # stream-ordered by the allocator
-            buf[k] = ws.data_ptr()
-        from ..ops._lib import stream_ptr
-
-        launches = [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
-        for fn, (grid, block) in zip(fns, launches):
-            rc = _lib().lta_rtc_launch(fn, grid[0], grid[1], grid[2], block[0], block[1], block[2], 0, stream_ptr(dev),
-                                       ctypes.cast(buf, ctypes.c_void_p), ctypes.sizeof(buf))
-            if rc != 0:
-                raise RuntimeError(f"{self.name}: hipModuleLaunchKernel failed with {rc}")
-        del ws
+        launch(ks, fns, tensors, outs, [args[i] for i in self.number_pos], self._argbuf_t, self._argbuf_ws_t,
+               self.name)
         return tuple(outs)
+
+
+def arg_buffer_types(n_tensors: int, n_outputs: int, n_numbers: int):
+    nwords = n_tensors + max(n_outputs, 1) + n_numbers
+    return ctypes.c_uint64 * nwords, ctypes.c_uint64 * (nwords + 1)
+
+
+def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: list, argbuf_t=None, argbuf_ws_t=None,
+           name: str = "hipFusion") -> None:
+    """Launches a generated kernel source (and its extra kernels) with the fusion calling convention:
+    one argument block of 64-bit words = input tensor pointers, output pointers (one dummy word when
+    there are none), numbers as double bits, then the workspace pointer when ``ks.ws_bytes``."""
+    if argbuf_t is None:
+        argbuf_t, argbuf_ws_t = arg_buffer_types(len(tensors), len(outs), len(numbers))
+    dev = (tensors or outs)[0].device
+    buf = argbuf_ws_t() if ks.ws_bytes else argbuf_t()
+    k = 0
+    for t in tensors:
+        buf[k] = t.data_ptr()
+        k += 1
+    for o in outs:
+        buf[k] = o.data_ptr()
+        k += 1
+    if not outs:
+        k += 1
+    for x in numbers:
+        buf[k] = _double_bits(x)
+        k += 1
+    ws = None
+    if ks.ws_bytes:
+        ws = torch.empty(ks.ws_bytes, dtype=torch.uint8, device=dev)  # stream-ordered by the allocator
+        buf[k] = ws.data_ptr()
+    from ..ops._lib import stream_ptr
+
+    launches = [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
+    for fn, (grid, block) in zip(fns, launches):
+        rc = _lib().lta_rtc_launch(fn, grid[0], grid[1], grid[2], block[0], block[1], block[2], 0, stream_ptr(dev),
+                                   ctypes.cast(buf, ctypes.c_void_p), ctypes.sizeof(buf))
+        if rc != 0:
+            raise RuntimeError(f"{name}: hipModuleLaunchKernel failed with {rc}")
+    del ws
+
+
+def load_kernels(ks: cg.KernelSource) -> list:
+    """Function handles of a kernel source's main kernel and its extra kernels."""
+    return [load_kernel(ks)] + [load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.extra]
 
 
 def _double_bits(x) -> int:

@@ -35,7 +35,24 @@ register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_v
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                         ctypes.c_uint64, c_void_p, c_void_p])
 
-SUPPORTED_HEAD_DIMS = (64, 96, 128)
+SUPPORTED_HEAD_DIMS = (64, 96, 128)  # the kernels' compile-time head dims
+# Other head dims up to 128 (multiples of 8) run zero-padded to the next kernel head dim, as the
+# reference pads for aten flash (thunder/executors/sdpaex.py:45-59): zero columns of Q / K leave
+# Q K^T unchanged, zero columns of V give zero columns of O (sliced off), the scale stays the
+# caller's (1 / sqrt(D) of the real D), and the padded gradient columns are exactly zero.
+MAX_PADDED_HEAD_DIM = 128
+
+
+def padded_head_dim(D: int) -> int | None:
+    if D in SUPPORTED_HEAD_DIMS:
+        return D
+    if D % 8 or D <= 0 or D > MAX_PADDED_HEAD_DIM:
+        return None
+    return next(d for d in SUPPORTED_HEAD_DIMS if d >= D)
+
+
+def _pad_d(t: torch.Tensor, Dp: int) -> torch.Tensor:
+    return t if t.shape[-1] == Dp else torch.nn.functional.pad(t, (0, Dp - t.shape[-1]))
 
 
 def prepare_mask(mask: torch.Tensor, B: int, Hq: int, Tq: int, Sk: int):
@@ -63,7 +80,7 @@ def supported(q, k, v) -> bool:
         and k.dtype == q.dtype
         and v.dtype == q.dtype
         and q.ndim == 4
-        and q.shape[-1] in SUPPORTED_HEAD_DIMS
+        and padded_head_dim(q.shape[-1]) is not None
         and k.shape[-1] == q.shape[-1]
         and v.shape[-1] == q.shape[-1]
         and q.shape[1] % k.shape[1] == 0
@@ -101,6 +118,13 @@ def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str 
     transposed view: the usual ``o.transpose(1, 2).reshape(B, T, Hq * D)`` before the output
     projection is then a view instead of a copy, and the backward reads it (and dO) in place."""
     lib = require()
+    D0 = q.shape[-1]
+    Dp = padded_head_dim(D0)
+    if Dp is not None and Dp != D0:
+        sc = scale if scale is not None else 1.0 / math.sqrt(D0)
+        o, lse = attn_fwd(_pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), causal, sc, out_layout, mask, dropout_p, seed,
+                          offset)
+        return o[..., :D0], lse
     q, k, v, qkv_st = _qkv_in_place(q, k, v)
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
@@ -124,6 +148,13 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     """Returns (dq, dk, dv) with dk/dv summed over the query heads of each kv group; with
     ``mask_grad`` (a float mask) a 4th result: the mask's gradient, reduced to its shape."""
     lib = require()
+    D0 = q.shape[-1]
+    Dp = padded_head_dim(D0)
+    if Dp is not None and Dp != D0:
+        sc = scale if scale is not None else 1.0 / math.sqrt(D0)
+        res = attn_bwd(_pad_d(do, Dp), _pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), _pad_d(o, Dp), lse, causal, sc, mask,
+                       dropout_p, seed, offset, mask_grad)
+        return (res[0][..., :D0], res[1][..., :D0], res[2][..., :D0]) + tuple(res[3:])
     q, k, v, qkv_st = _qkv_in_place(q, k, v)
     do = do if _rows_ok(do) else do.contiguous()
     o = o if _rows_ok(o) else o.contiguous()

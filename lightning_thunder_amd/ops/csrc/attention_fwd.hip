@@ -570,8 +570,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd_v2_kernel(c
   }
 }
 
-// 0 = v1 (4 waves x 2 workgroups per CU), 1..4 = v2 variants (launch_v2)
-int g_fwd_impl = 0;
+// 0 = v1 (4 waves x 2 workgroups per CU), 1..6 = v2 variants (launch_v2), 7 / 8 = v3, 9 / 10 = v4
+// exact / deferred rescale (attention_fwd4.hip), 11..14 = v4 ablation builds.  Default: v4 deferred
+// for D = 128 without mask / dropout (profiles/attn_v4_*), v1 for everything else.
+int g_fwd_impl = 10;
 
 template <typename T>
 int launch_v2(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
@@ -721,6 +723,6 @@ LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void*
 // forward kernel selection for D = 128 without mask / dropout (A/B measurement hook)
 LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
   const int old = g_fwd_impl;
-  if (impl >= 0 && impl <= 14) g_fwd_impl = impl;
+  if (impl >= 0 && impl <= 15) g_fwd_impl = impl;
   return old;
 }

@@ -132,12 +132,20 @@ __device__ __forceinline__ void scale_acc(f32x16& acc, float a) {
 }
 
 #define LTA_FENCE() __builtin_amdgcn_sched_barrier(0)
+// LDS fragment-read lookahead (MFMAs) of the QK (K rows) and PV (V^T transposed) phases
+#ifndef LTA_KLA
+#define LTA_KLA 5
+#endif
+#ifndef LTA_VLA
+#define LTA_VLA 3
+#endif
 
 template <int N>
 using IC = std::integral_constant<int, N>;
 
-// ABL (measurement builds only, impl 11..14): 1 no LDS-DMA in the loop, 2 no softmax-finish VALU,
-// 3 no per-tile barrier, 4 no softmax start (results are wrong; timing only)
+// ABL (measurement builds only, impl 11..15): 1 no LDS-DMA in the loop, 2 no softmax-finish VALU,
+// 3 no per-tile barrier, 4 no softmax start (results are wrong; timing only), 5 s_memtime stamps of
+// workgroup (0, 0) at every phase boundary of its first 64 tiles, written over LSE (diagnostic)
 template <typename T, bool CAUSAL, int THR, int ABL = 0>
 __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                   const T* __restrict__ V, T* __restrict__ O,
@@ -145,10 +153,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
                                                                   int Sk, float c, int64_t so_b, int64_t so_h,
                                                                   int64_t so_t, QKVStrides sx) {
   using F = typename Frag<T>::type;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * kNBuf * kTileB];  // the only LDS object
+  constexpr int kStampBase = 2 * kNBuf * kTileB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kNBuf * kTileB + (ABL == 5 ? 4 * 64 * 6 * 8 : 0)];  // the only LDS object
 
   const int n_qt = (Tq + kBM - 1) / kBM;
-  const int qt = n_qt - 1 - (int)blockIdx.y;  // heaviest causal blocks first
+  // causal: workgroup y runs query tile n_qt-1-y (heavy) then tile y (light), so every workgroup
+  // carries the same number of key tiles and the grid is one balanced wave of workgroups
+  const int qt_heavy = n_qt - 1 - (int)blockIdx.y, qt_light = (int)blockIdx.y;
+  const int npass = (CAUSAL && qt_light < qt_heavy) ? 2 : 1;
   const int bh = blockIdx.x;                  // x-fastest: all query blocks of a head share an XCD
   const int b = bh / Hq, hq = bh % Hq;
   const int hk = hq / (Hq / Hkv);
@@ -161,6 +173,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int qt = pass == 0 ? qt_heavy : qt_light;
   const int q0 = qt * kBM + wave * kRows;  // block X: queries q0 + 32 X + r
 
   int n_tiles = (Sk + kBN - 1) / kBN;
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
   // QK of block X on a K image; slot i = MFMA (s = i >> 1, kt = i & 1); filler(i) after the MFMA
   auto qk_phase = [&](auto xc, int kimg, auto&& filler) {
     constexpr int X = decltype(xc)::value;
-    constexpr int L = 3;  // fragment reads run L MFMAs ahead
+    constexpr int L = LTA_KLA;  // fragment reads run L MFMAs ahead
     F kf[L + 1];
 #pragma unroll
     for (int i = 0; i < L; ++i) kf[i] = kfrag(kimg, i >> 1, i & 1);
@@ -373,7 +387,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
   // PV of block X on a V image; slot i = MFMA (dt = i >> 2, kt = (i >> 1) & 1, s = i & 1)
   auto pv_phase = [&](auto xc, int vimg, auto&& filler) {
     constexpr int X = decltype(xc)::value;
-    constexpr int L = 2;
+    constexpr int L = LTA_VLA;
     F vf[L + 1];
 #pragma unroll
     for (int i = 0; i < L; ++i) vf[i] = vfrag(vimg, i >> 2, (i >> 1) & 1, i & 1);
@@ -409,7 +423,16 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
 
   // one barrier per tile for every wave: its unmasked tiles, its masked last tile (peeled, so the
   // mask code cannot be hoisted into the main loop), then staging-only tiles for the later waves
+  auto stamp = [&](int t, int k) {
+    if constexpr (ABL == 5) {
+      if (blockIdx.x == 0 && blockIdx.y == 0 && pass == 0 && t < 64) {
+        const uint64_t ts = __builtin_amdgcn_s_memtime();
+        if (lane == 0) *reinterpret_cast<uint64_t*>(smem + kStampBase + ((wave * 64 + t) * 6 + k) * 8) = ts;
+      }
+    }
+  };
   auto tile = [&](int t, auto mc) {
+    stamp(t, 0);
     const int t1 = min(t + 2, last);  // two tiles ahead; past the end: re-stage the last tile into a free slot
     const int kimg = (t % kNBuf) * kTileB;
     const int vimg = kVBase + (t % kNBuf) * kTileB;
@@ -419,6 +442,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
       fin(IC<1>{}, 1, IC<1>{}, 0, i, none);
       if ((i & 3) == 0) dma(i >> 2, t1);
     });
+    stamp(t, 1);
     pv_phase(IC<1>{}, vprev, [&](int i) {
       fin(IC<0>{}, 0, IC<1>{}, 1, i, [&]() {
         pin2(sacc[0][0], sacc[0][1]);
@@ -426,17 +450,21 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
       });
       if ((i & 3) == 2) dma(4 + (i >> 2), t1);
     });
+    stamp(t, 2);
     qk_phase(IC<1>{}, kimg, [&](int i) { fin(IC<0>{}, 1, IC<0>{}, 0, i, none); });
+    stamp(t, 3);
     pv_phase(IC<0>{}, vimg, [&](int i) {
       fin(IC<1>{}, 0, IC<0>{}, 1, i, [&]() {
         pin2(sacc[1][0], sacc[1][1]);
         start(IC<1>{}, mc, t);
       });
     });
+    stamp(t, 4);
     if constexpr (ABL != 3) {
       asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");  // tile t+1 landed (this wave's part)
       __builtin_amdgcn_s_barrier();                                 // ... and everyone's; tile t-2 free
     }
+    stamp(t, 5);
   };
   const int nplain = last_masked ? nw - 1 : nw;
   int t = 0;
@@ -497,13 +525,23 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
     if (h == 0 && LSE != nullptr)
       LSE[((int64_t)b * Hq + hq) * Tq + qi] = (l > 0.f) ? (m[x] + log2f(l)) * 0.69314718055994530942f : -INFINITY;
   }
+  __builtin_amdgcn_s_barrier();  // every wave's LDS reads of this pass precede the next pass's DMA
+  }  // pass
+  if constexpr (ABL == 5) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      uint64_t* dst = reinterpret_cast<uint64_t*>(LSE) + wave * 64 * 6;
+      for (int i = lane; i < 64 * 6; i += 64)
+        dst[i] = *reinterpret_cast<const uint64_t*>(smem + kStampBase + (wave * 64 * 6 + i) * 8);
+    }
+  }
 }
 
 template <typename T>
 int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
            float scale, int causal, const int64_t* so, const QKVStrides& sx, int thr, int abl, hipStream_t s) {
   const float c = scale * 1.44269504088896340736f;
-  dim3 grid(B * Hq, (Tq + kBM - 1) / kBM), block(kThreads);
+  const int n_qt = (Tq + kBM - 1) / kBM;
+  dim3 grid(B * Hq, causal ? (n_qt + 1) / 2 : n_qt), block(kThreads);
   const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * kD, sh = so ? so[1] : (int64_t)Tq * kD, st = so ? so[2] : kD;
 #ifdef LTA_V4_ONE
 #define LTA_V4(CA, TH) if (CA && TH) hipLaunchKernelGGL((attn_fwd_v4_kernel<T, true, 8>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st, sx)
@@ -524,6 +562,7 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
     if (abl == 2) LTA_V4A(2);
     if (abl == 3) LTA_V4A(3);
     if (abl == 4) LTA_V4A(4);
+    if (abl == 5) LTA_V4A(5);
 #undef LTA_V4A
     return (int)hipGetLastError();
   }

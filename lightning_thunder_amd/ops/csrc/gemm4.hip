@@ -108,18 +108,21 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
 template <bool MN, bool DUAL = false>
 struct Stager {
   i32x4 rsrc, rsrc2;     // DUAL (K-major only): rows 0..127 from rsrc, rows 128..255 from rsrc2
-  int voff0, voff1;      // K-major: voff0 for every i; MN-major: even / odd i
-  int istride, kstride;  // bytes between consecutive i / consecutive K-tiles
-  // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length
+  int voff[8];           // K-major: per instruction i (edge rows clamped); MN-major: [0] even, [1] odd i
+  int istride, kstride;  // bytes between consecutive i (MN-major, DUAL) / consecutive K-tiles
+  // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length;
+  // valid = rows (K-major) / columns (MN-major) of the tile inside the operand (< BM on an edge
+  // tile: the sources of the rest are clamped to the last valid one, whose copies only feed
+  // output rows / columns that are never stored — no out-of-bounds read, no reliance on the
+  // buffer range check)
   __device__ __forceinline__ void init(const __hip_bfloat16* X, int ld, int r0, int K, int wave, int lane,
-                                       const __hip_bfloat16* X2 = nullptr) {
+                                       const __hip_bfloat16* X2 = nullptr, int valid = BM) {
     if constexpr (DUAL) {
       // r0 = the row of BOTH sources this tile starts at; each source contributes 128 rows
       rsrc = make_rsrc(X + (int64_t)r0 * ld, (BM / 2 - 1) * ld * 2 + K * 2);
       rsrc2 = make_rsrc(X2 + (int64_t)r0 * ld, (BM / 2 - 1) * ld * 2 + K * 2);
       const int r = lane >> 3, c = (lane & 7) ^ r;
-      voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
-      voff1 = voff0;
+      voff[0] = ((wave * 8 + r) * ld + c * 8) * 2;
       istride = 32 * ld * 2;
       kstride = BK * 2;
     } else if constexpr (!MN) {
@@ -128,9 +131,9 @@ struct Stager {
       const __hip_bfloat16* base = X + (int64_t)r0 * ld;
       rsrc = make_rsrc(base, (BM - 1) * ld * 2 + K * 2);
       const int r = lane >> 3, c = (lane & 7) ^ r;
-      voff0 = ((wave * 8 + r) * ld + c * 8) * 2;
-      voff1 = voff0;
-      istride = 32 * ld * 2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) voff[i] = (min(32 * i + wave * 8 + r, valid - 1) * ld + c * 8) * 2;
+      istride = 0;
       kstride = BK * 2;
     } else {
       // 2 k-rows of 512 B per instruction: lane -> k-row 2(4i + w) + (lane >> 5), stored chunk
@@ -139,9 +142,9 @@ struct Stager {
       rsrc = make_rsrc(base, (K - 1) * ld * 2 + BM * 2);
       const int half = lane >> 5, slot = lane & 31;
       const int kr = 2 * wave + half;  // k-row for i = 0
-      const int c0 = slot ^ tr_swz(kr);
-      voff0 = (kr * ld + c0 * 8) * 2;
-      voff1 = (kr * ld + (c0 ^ 8) * 8) * 2;
+      const int c0 = slot ^ tr_swz(kr), cmax = (valid >> 3) - 1;  // valid % 8 == 0 (16-B rows)
+      voff[0] = (kr * ld + min(c0, cmax) * 8) * 2;
+      voff[1] = (kr * ld + min(c0 ^ 8, cmax) * 8) * 2;
       istride = 8 * ld * 2;
       kstride = BK * ld * 2;
     }
@@ -149,10 +152,11 @@ struct Stager {
   __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
     const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
     const bool second = DUAL && i >= 4;
+    const int vo = DUAL ? voff[0] : (MN ? voff[i & 1] : voff[i]);
+    const int so = (DUAL || MN) ? (second ? i - 4 : i) * istride + kt * kstride : kt * kstride;
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :
-                 : "s"(dst), "v"((MN && (i & 1)) ? voff1 : voff0), "s"(second ? rsrc2 : rsrc),
-                   "s"((second ? i - 4 : i) * istride + kt * kstride)
+                 : "s"(dst), "v"(vo), "s"(second ? rsrc2 : rsrc), "s"(so)
                  : "memory", "m0");
   }
 };
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fq = lane >> 4;
 
-  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int nTm = (M + BM - 1) / BM, nTn = (N + BN - 1) / BN, nwg = nTm * nTn;
   const int wg = xcd_tile((int)blockIdx.x, nwg);
   constexpr int G = 8;
   const int per_group = G * nTn;
@@ -245,11 +249,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
 
   Stager<AT> sa;
   Stager<BT, EPI == 1> sb;
-  sa.init(A, lda, m0, K, wave, lane);
+  sa.init(A, lda, m0, K, wave, lane, nullptr, min(BM, M - m0));
   if constexpr (EPI == 1)
     sb.init(B, ldb, n0 / 2, K, wave, lane, B2);
   else
-    sb.init(B, ldb, n0, K, wave, lane);
+    sb.init(B, ldb, n0, K, wave, lane, nullptr, min(BN, N - n0));
   // glds j (0..15) of a K-tile: j < 8 -> A instruction j, else B instruction j - 8
   auto glds = [&](int j, int kt, char* stage) {
     if (j < 8)
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   for (int n = 0; n < 8; ++n) {
     const int col = n * 16 + fr;
     float bv = 0.f;
-    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 128 + col]);
+    if constexpr (BIAS) bv = (n0 + wn * 128 + col < N) ? to_f32(bias[n0 + wn * 128 + col]) : 0.f;
     const int ch = col >> 3, co = (col & 7) * 2;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -384,7 +388,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
         const int id = it * 64 + lane;
         const int row = id >> 4, ch = id & 15;
         const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
-        *reinterpret_cast<uint4*>(dst + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = v;
+        if (m0 + wm * 128 + row < M)
+          *reinterpret_cast<uint4*>(dst + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = v;
       }
     }
     // y = silu(a) * b: wave (wm, wn) takes rows wn*64 .. +63 of the wm row half
@@ -407,7 +412,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
         const float x = __bfloat162float(a[e]);
         o.h[e] = __float2bfloat16(x * sigmoid_f(x) * __bfloat162float(b[e]));
       }
-      *reinterpret_cast<uint4*>(C3 + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = o.u;
+      if (m0 + wm * 128 + row < M)
+        *reinterpret_cast<uint4*>(C3 + (int64_t)(m0 + wm * 128 + row) * ldc + n0 / 2 + ch * 8) = o.u;
     }
     return;
   }
@@ -427,6 +433,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
       uint4 v0 = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
       uint4 v1 = *reinterpret_cast<const uint4*>(wbuf + row * 256 + (((ch + 8) ^ (row & 15)) << 4));
       const int grow = m0 + wm * 128 + row;
+      if (grow >= M) continue;  // edge tile (prefill with T*B % 256 != 0)
       const int bi = grow / ep.T, t = grow - bi * ep.T;
       __hip_bfloat16* const o = dst + (((int64_t)bi * nheads + hh) * ep.T + t) * 128 + ch * 8;
       if (is_q || is_k) {
@@ -462,6 +469,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
     const int64_t grow = m0 + wm * 128 + row;
     const int gcol = n0 + wn * 128 + ch * 8;
+    if (grow >= M || gcol >= N) continue;  // edge tile: N % 8 == 0, so a chunk is all in or all out
     if constexpr (EPI == 2) {
       // v = g (bf16, as the unfused dgrad stores it); a, b at the same element
       const uint4 va = *reinterpret_cast<const uint4*>(R + grow * ldc + gcol);
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
 template <int ACT, bool AT, bool BT, int VAR>
 int launch4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
             int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
-  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+  dim3 grid(((M + BM - 1) / BM) * ((N + BN - 1) / BN)), block(NTHR);
 #define LTA_G4(BI, RE)                                                                                            \
   hipLaunchKernelGGL((gemm4_bf16_kernel<ACT, BI, RE, AT, BT, VAR>), grid, block, 0, s, (const __hip_bfloat16*)A,  \
                      (const __hip_bfloat16*)B, (__hip_bfloat16*)C, (const __hip_bfloat16*)bias,                  \
@@ -542,14 +550,15 @@ int dispatch_layout(const void* A, const void* B, void* C, const void* bias, con
 // C[M,N] = act(alpha * opA . opB + bias) (+ R), bf16 in / fp32 accumulate / bf16 out.
 //   at = 0: A [M][K] (lda = row pitch)        at = 1: A stored [K][M] (lda = its row pitch)
 //   bt = 0: B [N][K] (nn.Linear weight)       bt = 1: B stored [K][N]
-// act/bias only with at = bt = 0.  Requires M, N % 256 == 0, K % 128 == 0, 16-B aligned rows and
-// operands under 2 GiB (32-bit buffer offsets).
+// act/bias only with at = bt = 0.  Any M, N with N % 8 == 0 (edge tiles: clamped operand sources,
+// masked stores), K % 128 == 0, 16-B aligned rows, operands under 2 GiB (32-bit buffer offsets).
 // variant: glds split (0: all in the barrier phase, 1: half, 2: a quarter; see the header).  Variant 1
 // is the production kernel (every epilogue); 0 and 2 are plain products kept for A/B measurement.
 LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
                               int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
                               int variant, hipStream_t s) {
-  if (M % BM || N % BN || K % (2 * BK) || M <= 0 || N <= 0 || K <= 0) return -2;
+  if (N % 8 || K % (2 * BK) || M <= 0 || N <= 0 || K <= 0) return -2;
+  if (at && M % 8) return -2;  // MN-major A: 16-B rows
   // buffer-resource byte offsets are 32-bit
   const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
   if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
@@ -573,17 +582,18 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
 //     Requires Nh % 128 == 0.
 //   mode 2 (swiglu backward): A = dY [M][K] (lda), B = W stored [K][Nh] (pitch ldb); R = a, R2 = b,
 //     C = da, C2 = db, each [M][Nh] (pitch ldc).  Requires Nh % 256 == 0.
-// Requires M % 256 == 0, K % 128 == 0, 16-B aligned rows, operands under 2 GiB.
+// Any M (edge row tiles), K % 128 == 0, 16-B aligned rows, operands under 2 GiB.
 LTA_EXPORT int lta_gemm4_swiglu(const void* A, const void* B, const void* B2, void* C, void* C2, void* C3,
                                 const void* R, const void* R2, int M, int Nh, int K, int lda, int ldb, int ldc,
                                 int mode, hipStream_t s) {
-  if (M % BM || K % (2 * BK) || M <= 0 || Nh <= 0 || K <= 0) return -2;
+  if (K % (2 * BK) || M <= 0 || Nh <= 0 || K <= 0) return -2;
   if ((int64_t)M * lda * 2 >= (1ll << 31)) return -2;
   const dim3 block(NTHR);
+  const int nTm = (M + BM - 1) / BM;
   if (mode == 1) {
     if (Nh % (BN / 2) || !B2 || !C3 || (int64_t)Nh * ldb * 2 >= (1ll << 31)) return -2;
     const int N = 2 * Nh;
-    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 1>), dim3((M / BM) * (N / BN)), block,
+    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 1>), dim3(nTm * (N / BN)), block,
                        0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr,
                        M, N, K, lda, ldb, ldc, 0, 1.f,
                        EpiArgs{(const __hip_bfloat16*)B2, (__hip_bfloat16*)C2, (__hip_bfloat16*)C3, nullptr, nullptr,
@@ -592,7 +602,7 @@ LTA_EXPORT int lta_gemm4_swiglu(const void* A, const void* B, const void* B2, vo
   }
   if (mode == 2) {
     if (Nh % BN || !R || !R2 || !C || !C2 || (int64_t)K * ldb * 2 >= (1ll << 31)) return -2;
-    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, true, 1, 2>), dim3((M / BM) * (Nh / BN)), block,
+    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, true, 1, 2>), dim3(nTm * (Nh / BN)), block,
                        0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr,
                        (const __hip_bfloat16*)R, M, Nh, K, lda, ldb, ldc, ldc, 1.f,
                        EpiArgs{nullptr, (__hip_bfloat16*)C2, nullptr, (const __hip_bfloat16*)R2, nullptr, nullptr, 0, 0,
@@ -605,14 +615,14 @@ LTA_EXPORT int lta_gemm4_swiglu(const void* A, const void* B, const void* B2, vo
 // q, k, v = RoPE-split(x . W^T) (EPI 3): A = x [M = B*T][K] (lda), B = W [(nh + 2 ng) * 128][K]
 // (ldb, rows = q heads, then k heads, then v heads); cos / sin fp32 [T][128] (rotate-half, full
 // width); q [B][nh][T][128], k / v [B][ng][T][128] contiguous.  Requires head size 128,
-// (nh + 2 ng) even, M % 256 == 0, K % 128 == 0.
+// (nh + 2 ng) even, K % 128 == 0 (any M = B * T: edge row tiles).
 LTA_EXPORT int lta_gemm4_qkv_rope(const void* A, const void* B, const float* cos_, const float* sin_, void* q, void* k,
                                   void* v, int M, int K, int lda, int ldb, int T, int nh, int ng, hipStream_t s) {
   const int N = (nh + 2 * ng) * 128;
-  if (M % BM || K % (2 * BK) || N % BN || M <= 0 || K <= 0 || T <= 0 || M % T || nh <= 0 || ng <= 0) return -2;
+  if (K % (2 * BK) || N % BN || M <= 0 || K <= 0 || T <= 0 || M % T || nh <= 0 || ng <= 0) return -2;
   if ((int64_t)M * lda * 2 >= (1ll << 31) || (int64_t)N * ldb * 2 >= (1ll << 31)) return -2;
   if (!q || !k || !v || !cos_ || !sin_) return -2;
-  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 3>), dim3((M / BM) * (N / BN)),
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 3>), dim3(((M + BM - 1) / BM) * (N / BN)),
                      dim3(NTHR), 0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)q, nullptr,
                      nullptr, M, N, K, lda, ldb, 0, 0, 1.f,
                      EpiArgs{nullptr, (__hip_bfloat16*)k, (__hip_bfloat16*)v, nullptr, cos_, sin_, T, nh, ng});

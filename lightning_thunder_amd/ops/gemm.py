@@ -23,14 +23,23 @@ def _rowmajor_2d(t: torch.Tensor) -> bool:
 
 
 def gemm_nt_supported(a: torch.Tensor, b: torch.Tensor, bias=None, residual=None) -> bool:
-    """a [M,K] and b [N,K] bf16 on the GPU with tile-divisible shapes."""
+    """a [M,K] and b [N,K] bf16 on the GPU with tile-divisible shapes (the 8-wave kernel)."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda:
         return False
+    M, K = a.shape
+    N = b.shape[0]
+    if M % TILE_M or N % TILE_N or K % TILE_K:
+        return False
+    return nt_epilogue_ok(a, b, bias, residual)
+
+
+def nt_epilogue_ok(a: torch.Tensor, b: torch.Tensor, bias=None, residual=None) -> bool:
+    """Row-major a [M,K], b [N,K] and a bias / residual the NT epilogues read (bf16, contiguous)."""
     if not (_rowmajor_2d(a) and _rowmajor_2d(b)):
         return False
     M, K = a.shape
     N = b.shape[0]
-    if M % TILE_M or N % TILE_N or K % TILE_K or b.shape[1] != K:
+    if b.shape[1] != K:
         return False
     if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()):
         return False
@@ -69,15 +78,20 @@ register_signature("lta_gemm4_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_
                                       c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p])
 
 
+GEMM4_MIN_M = 64
+
+
 def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
     """(at, bt, lda, ldb) of ``a [M,K] @ b [K,N]`` for ``lta_gemm4_bf16``, or None when the operands
-    are not bf16 2-D GPU tensors with one unit-stride dim, 16-B aligned rows and tile-divisible
-    shapes (M, N % 256, K % 128)."""
+    are not bf16 2-D GPU tensors with one unit-stride dim and 16-B aligned rows, or K % 128 != 0.
+    M and N need not divide the 256 x 256 tile (edge tiles clamp their operand rows and mask their
+    stores; N % 8 == 0 for whole 16-B output chunks); M < GEMM4_MIN_M goes elsewhere (a 256-row
+    tile would be mostly idle)."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda or a.dim() != 2 or b.dim() != 2:
         return None
     M, K = a.shape
     N = b.shape[1]
-    if b.shape[0] != K or M % 256 or N % 256 or K % 128 or M == 0 or N == 0 or K == 0:
+    if b.shape[0] != K or M < GEMM4_MIN_M or N % 8 or K % 128 or N == 0 or K == 0:
         return None
     la, lb = _operand_layout(a, M, K), _operand_layout(b, K, N)
     if la is None or lb is None:
@@ -296,9 +310,9 @@ _GEMM4_VARIANTS: dict = {}
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` on the hand-written kernels, chosen by a static rule:
-    the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip) when M, N % 256
-    and K % 128, the 8-wave kernel (csrc/gemm.hip) when K % 64, else torch (``LTA_GEMM=torch``
-    forces torch)."""
+    the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip, any M >= 64,
+    N % 8, K % 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
+    else torch (``LTA_GEMM=torch`` forces torch)."""
     K = x.shape[-1]
     N = w.shape[0]
     x2 = x.reshape(-1, K)
@@ -310,7 +324,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
             return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
         wt = w.t()
         lay = gemm4_layout(x2, wt)
-        if lay is not None and gemm_nt_supported(x2, w, bias, r2):
+        if lay is not None and nt_epilogue_ok(x2, w, bias, r2):
             _count("gemm4")
             y = matmul4(x2, wt, bias=bias, residual=r2, act=act, variant=gemm4_variant(0, 0, x2.shape[0], N, K))
             return y.reshape(*x.shape[:-1], N)
@@ -407,16 +421,6 @@ def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = Non
     return _torch_mm(a, b, residual)
 
 
-def matmul_selection_table() -> dict:
-    """Kept for API compatibility: the selection is a static rule now (see :func:`matmul`)."""
-    return {}
-
-
-def selection_table() -> dict:
-    """Kept for API compatibility: the selection is a static rule now (see :func:`linear`)."""
-    return {}
-
-
 # ---------------------------------------------------------------------------------------------
 # K10 grouped GEMM (mixture of experts)
 # ---------------------------------------------------------------------------------------------
@@ -477,7 +481,7 @@ def gate_up_supported(x2: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> b
         return False
     M, K = x2.shape
     Nh = w1.shape[0]
-    return (w1.shape[1] == K and M % 256 == 0 and Nh % 128 == 0 and K % 128 == 0 and M > 0 and Nh > 0
+    return (w1.shape[1] == K and M >= GEMM4_MIN_M and Nh % 128 == 0 and K % 128 == 0 and Nh > 0
             and M * x2.stride(0) * 2 < 2 ** 31 and Nh * w1.stride(0) * 2 < 2 ** 31)
 
 
@@ -516,7 +520,7 @@ def matmul_swiglu_bwd(dy: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: tor
     dy2 = dy.reshape(-1, dy.shape[-1])
     a2, b2 = a.reshape(-1, N), b.reshape(-1, N)
     lay = gemm4_layout(dy2, w) if _os.environ.get("LTA_GEMM", "auto") != "torch" else None
-    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _fused_swiglu_on()
+    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _fused_swiglu_on() and N % 256 == 0
             and a2.is_contiguous() and b2.is_contiguous() and a2.data_ptr() % 16 == 0 and b2.data_ptr() % 16 == 0
             and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.shape[0] == dy2.shape[0]):
         M, K = dy2.shape
@@ -570,7 +574,7 @@ def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, cos: torch.Tensor, sin: to
     nq = n_head + 2 * n_query_groups
     ok = (_os.environ.get("LTA_GEMM", "auto") != "torch" and _os.environ.get("LTA_FUSED_QKV_ROPE", "1") != "0"
           and head_size == 128 and rope_n == 128 and nq % 2 == 0 and tuple(w.shape) == (nq * 128, K)
-          and _plain_2d(x2) and _plain_2d(w) and x2.shape[0] % 256 == 0 and K % 128 == 0
+          and _plain_2d(x2) and _plain_2d(w) and x2.shape[0] >= GEMM4_MIN_M and K % 128 == 0
           and cos.dtype == torch.float32 and sin.dtype == torch.float32 and cos.shape[-1] == 128
           and sin.shape[-1] == 128 and cos.shape[0] >= T and sin.shape[0] >= T
           and cos.dim() == 2 and sin.dim() == 2

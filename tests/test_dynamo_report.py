@@ -4,6 +4,7 @@ import os
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from lightning_thunder_amd.dynamo.report import fx_report, thunder_optimize, thunder_profile
@@ -43,3 +44,71 @@ def test_thunder_optimize_selects_a_backend():
     torch._dynamo.reset()
     o2 = thunder_optimize(lambda a: torch.tanh(a) * 2, trials=1)
     torch.testing.assert_close(o2(x), torch.tanh(x) * 2)
+
+
+def _fusing_fn(x, w):
+    y = torch.nn.functional.gelu(x @ w) * 2 + 1
+    z = torch.sin(y).sum(-1)
+    return (y.exp() * z.unsqueeze(-1)).tanh()
+
+
+@pytest.fixture
+def cpu_fusion():
+    from lightning_thunder_amd.executors import hipfuse
+
+    old = hipfuse.ex.allow_cpu
+    hipfuse.ex.allow_cpu = True
+    yield
+    hipfuse.ex.allow_cpu = old
+
+
+def test_fusion_level_reports_cpu(tmp_path, cpu_fusion):
+    """ThunderFX split subgraphs -> their hipfuse regions: each re-runs against its prims, is timed
+    alone, and dumps a standalone repro script (generated HIP source + data file)."""
+    import py_compile
+
+    from lightning_thunder_amd.dynamo.report import (analyze_thunder_splits, get_thunder_split_reports,
+                                                     save_failing_repros)
+
+    x = torch.randn(8, 16, requires_grad=True)
+    w = torch.randn(16, 32, requires_grad=True)
+    reps = get_thunder_split_reports(_fusing_fn, x, w)
+    assert reps
+    fus = reps[0].create_fusion_reports()
+    assert any("_fwd_" in f.name for f in fus) and any("_bwd_" in f.name for f in fus), [str(f) for f in fus]
+    for f in fus:
+        assert f.run_repro()["ok"]
+        bench = f.run_benchmark(2)
+        assert bench["fusion_ms"] > 0 and bench["bytes"] > 0
+        path = f.write_repro(str(tmp_path))
+        py_compile.compile(path, doraise=True)
+        src = open(path).read()
+        assert "__global__" in src and "hipfuse.launch" in src
+        data = torch.load(path.replace("_repro.py", "_data.pt"), weights_only=True)
+        assert "in0" in data and "out0" in data
+    summary = analyze_thunder_splits(_fusing_fn, x, w)
+    assert summary["subgraphs"] and summary["subgraphs"][0]["fusions"]
+    assert save_failing_repros(reps, str(tmp_path / "failing")) == []  # nothing fails
+
+
+@pytest.mark.gpu
+def test_fusion_repro_runs_standalone_gpu(tmp_path):
+    """The dumped repro of a generated kernel compiles, launches and matches on the GPU by itself, and
+    the benchmark report times every fusion region (bytes / GB/s)."""
+    import subprocess
+    import sys
+
+    from lightning_thunder_amd.dynamo.report import get_thunder_split_reports, thunderfx_benchmark_report
+
+    x = torch.randn(256, 512, device="cuda", requires_grad=True)
+    w = torch.randn(512, 1024, device="cuda", requires_grad=True)
+    reps = get_thunder_split_reports(_fusing_fn, x, w)
+    fus = reps[0].create_fusion_reports()
+    assert fus
+    path = fus[0].write_repro(str(tmp_path))
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, path], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "matches" in r.stdout, r.stderr[-2000:]
+    assert "GB/s" in r.stdout
+    rows = thunderfx_benchmark_report(_fusing_fn, x, w, folder=str(tmp_path / "bench"))
+    assert rows and all("fusion_ms" in row and row["fusion_gbps"] > 0 for row in rows), rows

@@ -153,6 +153,8 @@ def _sdpa_ref(q, k, v, causal, scale=None):
 @pytest.mark.parametrize("B,Hq,Hkv,T,S,D", [
     (2, 4, 4, 64, 64, 128), (1, 4, 2, 200, 200, 128), (2, 2, 2, 256, 256, 64), (1, 8, 1, 129, 129, 64),
     (1, 2, 2, 96, 333, 128), (1, 32, 32, 1024, 1024, 128), (2, 4, 2, 300, 300, 96), (1, 4, 4, 256, 256, 96),
+    # head dims without a kernel instantiation run zero-padded to the next one (ops/attention.py)
+    (2, 4, 2, 200, 200, 32), (1, 4, 4, 256, 256, 80), (1, 2, 2, 100, 100, 48), (1, 2, 1, 77, 77, 112),
 ])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
@@ -168,7 +170,8 @@ def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
     do = torch.randn(B, T, Hq, D, device="cuda", dtype=dtype).transpose(1, 2) if T % 2 else \
         torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
     o, lse = attn_fwd(q, k, v, causal)
-    assert o.transpose(1, 2).is_contiguous()  # O stored [B, T, H, D]
+    if D in (64, 96, 128):
+        assert o.transpose(1, 2).is_contiguous()  # O stored [B, T, H, D]
     qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
     ref = _sdpa_ref(qf, kf, vf, causal)
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
@@ -320,6 +323,8 @@ def test_gemm_bf16_layouts(layout, shape, residual):
 
     torch.manual_seed(0)
     M, N, K = shape
+    if layout[0] == "t":
+        M -= M % 8  # an MN-major operand needs 16-byte rows
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16) / K ** 0.5
     if layout[0] == "t":  # a stored [K][M] (column-major view), padded pitch
@@ -887,3 +892,53 @@ def test_flash_attention_strided_qkv_views(D, Hkv, masked):
     for a, b in zip(g1, g2):
         assert a.is_contiguous()
         torch.testing.assert_close(a, b, atol=0, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+@pytest.mark.parametrize("shape", [(1000, 16032, 256), (300, 50304, 128), (777, 1000, 384), (4096, 264, 512)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_gemm4_edge_tiles(layout, shape, residual):
+    """gemm4 on shapes that do not divide its 256 x 256 tile (a T=1000 prefill, the GPT-2 LM head
+    N=50304, the Llama-3-8B TP=8 vocab shard 128256/8 = 16032) in all four operand layouts, against
+    fp32; the hand kernel serves them (no library GEMM)."""
+    from lightning_thunder_amd.ops.gemm import matmul, last_gemm_backend_counts
+
+    torch.manual_seed(0)
+    M, N, K = shape
+    if layout[0] == "t":
+        M -= M % 8  # an MN-major operand needs 16-byte rows
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    if layout[0] == "t":  # a stored [K][M]
+        a = a.t().contiguous().t()
+    if layout[1] == "t":  # b stored [N][K] (nn.Linear weight viewed as w.t())
+        b = b.t().contiguous().t()
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if residual else None
+    last_gemm_backend_counts(reset=True)
+    out = matmul(a, b, res)
+    counts = last_gemm_backend_counts(reset=True)
+    assert counts.get("gemm4", 0) == 1 and counts.get("torch", 0) == 0, counts
+    ref = a.float() @ b.float()
+    if res is not None:
+        ref = ref.bfloat16().float() + res.float()
+    err = (out.float() - ref).abs().max().item()
+    assert err < 3e-2 + 1e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(1000, 16032), (300, 50304)])
+def test_linear_edge_tiles_bias_act(M, N):
+    """The forward linear epilogue (bias + GELU) on edge tiles: the bias of columns past N is never read."""
+    from lightning_thunder_amd.ops.gemm import linear, last_gemm_backend_counts
+
+    torch.manual_seed(1)
+    K = 512
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    last_gemm_backend_counts(reset=True)
+    y = linear(x, w, bias, act="gelu_tanh")
+    assert last_gemm_backend_counts(reset=True).get("gemm4", 0) == 1
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t() + bias.float(), approximate="tanh")
+    assert (y.float() - ref).abs().max().item() < 5e-2
