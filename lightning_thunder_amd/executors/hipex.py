@@ -1075,6 +1075,8 @@ def _rms_grad(a, normalized_shape, weight=None, eps=None):
 # K10 grouped GEMM (MoE experts)
 # =========================================================================================
 def _gmm_meta(a, b, offs):
+    if a.ndim == 2 and b.ndim == 2:  # the wgrad form: [G, K, N]
+        return TensorProxy(like=a, shape=(offs.shape[0], a.shape[0], b.shape[1]))
     return TensorProxy(like=a, shape=(a.shape[0], b.shape[2]))
 
 
@@ -1088,8 +1090,11 @@ hip_grouped_mm = ex.register_operator("hip_grouped_mm", meta=_gmm_meta, fn=_gmm_
 
 
 def _gmm_checker(a, b, offs=None, bias=None, out_dtype=None):
-    return (_gpu(a, b, offs) and offs is not None and bias is None and out_dtype is None and a.ndim == 2 and b.ndim == 3
-            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16)
+    """Forward / dgrad (2-D x 3-D) and wgrad (2-D x 2-D, reduction over each group's rows) forms:
+    the VJP of _grouped_mm (transforms/autodiff.py) emits all three, so MoE training runs every
+    expert GEMM on the hand kernels (csrc/gemm4.hip grouped modes)."""
+    return (_gpu(a, b, offs) and offs is not None and bias is None and out_dtype is None and a.ndim == 2
+            and b.ndim in (2, 3) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16)
 
 
 def _gmm_exec(a, b, offs=None, bias=None, out_dtype=None):

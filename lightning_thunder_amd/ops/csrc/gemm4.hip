@@ -105,9 +105,15 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
   return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), bytes, 0x00020000};
 }
 
-template <bool MN, bool DUAL = false>
+template <bool MN, bool DUAL = false, bool KEDGE = false>
 struct Stager {
   i32x4 rsrc, rsrc2;     // DUAL (K-major only): rows 0..127 from rsrc, rows 128..255 from rsrc2
+  // KEDGE (MN-major, grouped wgrad): the reduction length `kred` need not divide the K-tile.  Every
+  // K-tile gets its own buffer resource ending at the last valid k-row, and the k-row offsets live
+  // in the per-lane voffset (the range check covers voffset, not soffset), so k-rows past the end
+  // arrive in LDS as zeros (verified: tests/test_hip_kernels.py::test_lds_dma_out_of_range_lanes_write_zero)
+  const char* kbase;
+  int kred, ldb2;
   int voff[8];           // K-major: per instruction i (edge rows clamped); MN-major: [0] even, [1] odd i
   int istride, kstride;  // bytes between consecutive i (MN-major, DUAL) / consecutive K-tiles
   // X + r0 (rows / columns of this tile); ld = row pitch in elements; K = reduction length;
@@ -143,14 +149,36 @@ struct Stager {
       const int half = lane >> 5, slot = lane & 31;
       const int kr = 2 * wave + half;  // k-row for i = 0
       const int c0 = slot ^ tr_swz(kr), cmax = (valid >> 3) - 1;  // valid % 8 == 0 (16-B rows)
-      voff[0] = (kr * ld + min(c0, cmax) * 8) * 2;
-      voff[1] = (kr * ld + min(c0 ^ 8, cmax) * 8) * 2;
+      if constexpr (KEDGE) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) voff[i] = ((8 * i + kr) * ld + min((i & 1) ? c0 ^ 8 : c0, cmax) * 8) * 2;
+        kbase = reinterpret_cast<const char*>(base);
+        kred = K;
+        ldb2 = ld * 2;
+      } else {
+        voff[0] = (kr * ld + min(c0, cmax) * 8) * 2;
+        voff[1] = (kr * ld + min(c0 ^ 8, cmax) * 8) * 2;
+      }
       istride = 8 * ld * 2;
       kstride = BK * ld * 2;
     }
   }
   __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
     const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    if constexpr (KEDGE) {
+      // the group bounds come from device memory: readfirstlane makes the (uniform) descriptor provably
+      // scalar (cdna_hip_programming.md T20)
+      const int rows = max(0, min(BK, kred - kt * BK));
+      const uint64_t a = (uint64_t)(uintptr_t)(kbase + (int64_t)kt * BK * ldb2);
+      const i32x4 rk = i32x4{__builtin_amdgcn_readfirstlane((int)(uint32_t)a),
+                             __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu)),
+                             __builtin_amdgcn_readfirstlane(rows * ldb2), 0x00020000};
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                   :
+                   : "s"(dst), "v"(voff[i]), "s"(rk)
+                   : "memory", "m0");
+      return;
+    }
     const bool second = DUAL && i >= 4;
     const int vo = DUAL ? voff[0] : (MN ? voff[i & 1] : voff[i]);
     const int so = (DUAL || MN) ? (second ? i - 4 : i) * istride + kt * kstride : kt * kstride;
@@ -209,12 +237,20 @@ struct EpiArgs {
   const float* cos_;         // EPI 3: [T][128] fp32
   const float* sin_;
   int T, nh, ng;             // EPI 3: tokens per sequence, q heads, kv heads
+  const int* offs;           // GRP 1 / 2: int32 cumulative group ends (device)
+  int G;                     // GRP: number of groups
+  int64_t bstride, cstride;  // GRP 1: elements between groups' B; GRP 2: between groups' C
 };
 
 // EPI 0: plain (bias / act / residual); 1: gate-up forward (B2 = W2; C = a, C2 = b, C3 = y, each
 // [M][N/2] with pitch ldc; C / C2 may be null); 2: swiglu backward (R = a, R2 = b, C = da, C2 = db,
 // all [M][N] with pitch ldc); 3: qkv + RoPE (C = q, C2 = k, C3 = v).  See the header.
-template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0>
+// GRP 0: one GEMM.  GRP 1 (MoE forward / dgrad): rows [offs[g-1], offs[g]) of A times group g's B
+// (B + g * bstride); a row tile never spans two groups (grid: ceil(M / 256) + G row slots per
+// column tile, each workgroup scans the device offsets for its (group, row tile); no host sync).
+// GRP 2 (MoE wgrad): C[g] (C + g * cstride) = A_g^T . B_g, A / B stored [rows][.] (AT = BT = 1)
+// with group g's rows as the reduction; the reduction tail is zero-filled (Stager KEDGE).
+template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0, int GRP = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat16* __restrict__ A,
                                                             const __hip_bfloat16* __restrict__ B,
                                                             __hip_bfloat16* __restrict__ C,
@@ -229,6 +265,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   static_assert(EPI != 1 || (!AT && !BT && !BIAS && !RES && ACT == 0), "gate-up: forward layout, no other epilogue");
   static_assert(EPI != 3 || (!AT && !BT && !BIAS && !RES && ACT == 0), "qkv rope: forward layout, no other epilogue");
   static_assert(EPI != 2 || (!AT && BT && !BIAS && !RES && ACT == 0), "swiglu backward: dgrad layout only");
+  static_assert(GRP == 0 || (EPI == 0 && !BIAS && !RES && ACT == 0), "grouped: plain products");
+  static_assert(GRP != 1 || !AT, "grouped rows: A row-major");
+  static_assert(GRP != 2 || (AT && BT), "grouped reduction: A and B stored [rows][.]");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];  // the ONLY LDS object (rule 4a)
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -237,23 +276,58 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   const int fr = lane & 15, fq = lane >> 4;
 
   const int nTm = (M + BM - 1) / BM, nTn = (N + BN - 1) / BN, nwg = nTm * nTn;
-  const int wg = xcd_tile((int)blockIdx.x, nwg);
-  constexpr int G = 8;
-  const int per_group = G * nTn;
-  const int group = wg / per_group;
-  const int first_m = group * G;
-  const int gm = min(nTm - first_m, G);
-  const int in_group = wg % per_group;
-  const int tm = first_m + in_group % gm, tn = in_group / gm;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const __hip_bfloat16* Ag = A;
+  const __hip_bfloat16* Bg = B;
+  __hip_bfloat16* Cg = C;
+  int Mlim = M, Kr = K, m0, n0;
+  if constexpr (GRP == 0) {
+    const int wg = xcd_tile((int)blockIdx.x, nwg);
+    constexpr int G = 8;
+    const int per_group = G * nTn;
+    const int group = wg / per_group;
+    const int first_m = group * G;
+    const int gm = min(nTm - first_m, G);
+    const int in_group = wg % per_group;
+    const int tm = first_m + in_group % gm, tn = in_group / gm;
+    m0 = tm * BM;
+    n0 = tn * BN;
+  } else if constexpr (GRP == 1) {
+    const int bid = (int)blockIdx.x, tn = bid % nTn;
+    int slot = bid / nTn, g = 0, start = 0, end = 0;
+    bool found = false;
+    for (; g < ep.G; ++g) {
+      end = ep.offs[g];
+      const int tiles = (end - start + BM - 1) / BM;
+      if (slot < tiles) {
+        found = true;
+        break;
+      }
+      slot -= tiles;
+      start = end;
+    }
+    if (!found) return;  // uniform over the workgroup (scalar offsets): no barrier is skipped by part of it
+    m0 = start + slot * BM;
+    n0 = tn * BN;
+    Mlim = end;
+    Bg = B + (int64_t)g * ep.bstride;
+  } else {
+    const int g = (int)blockIdx.x / nwg, t = (int)blockIdx.x % nwg;
+    const int start = g ? ep.offs[g - 1] : 0, end = ep.offs[g];
+    m0 = (t / nTn) * BM;
+    n0 = (t % nTn) * BN;
+    Ag = A + (int64_t)start * lda;
+    Bg = B + (int64_t)start * ldb;
+    Cg = C + (int64_t)g * ep.cstride;
+    Kr = max(0, end - start);
+  }
 
-  Stager<AT> sa;
-  Stager<BT, EPI == 1> sb;
-  sa.init(A, lda, m0, K, wave, lane, nullptr, min(BM, M - m0));
+  Stager<AT, false, GRP == 2> sa;
+  Stager<BT, EPI == 1, GRP == 2> sb;
+  sa.init(Ag, lda, m0, Kr, wave, lane, nullptr, min(BM, Mlim - m0));
   if constexpr (EPI == 1)
-    sb.init(B, ldb, n0 / 2, K, wave, lane, B2);
+    sb.init(Bg, ldb, n0 / 2, Kr, wave, lane, B2);
   else
-    sb.init(B, ldb, n0, K, wave, lane, nullptr, min(BN, N - n0));
+    sb.init(Bg, ldb, n0, Kr, wave, lane, nullptr, min(BN, N - n0));
   // glds j (0..15) of a K-tile: j < 8 -> A instruction j, else B instruction j - 8
   auto glds = [&](int j, int kt, char* stage) {
     if (j < 8)
@@ -286,7 +360,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   constexpr int NB2 = VAR == 0 ? 16 : (VAR == 1 ? 8 : 4);
   constexpr int NA = 16 - NB2;
 
-  const int nk = K / BK;
+  // GRP 2: ceil to an even K-tile count (the zero-filled tail tiles add nothing)
+  const int nk = GRP == 2 ? (Kr + 2 * BK - 1) / (2 * BK) * 2 : K / BK;
   // ---- prologue: tile 0 whole, tile 1's phase-B2 share; wait for tile 0 ----
 #pragma unroll
   for (int j = 0; j < 16; ++j) glds(j, 0, smem);
@@ -469,7 +544,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
     const int64_t grow = m0 + wm * 128 + row;
     const int gcol = n0 + wn * 128 + ch * 8;
-    if (grow >= M || gcol >= N) continue;  // edge tile: N % 8 == 0, so a chunk is all in or all out
+    if (grow >= Mlim || gcol >= N) continue;  // edge tile (or group end): N % 8 == 0, a chunk is all in or out
     if constexpr (EPI == 2) {
       // v = g (bf16, as the unfused dgrad stores it); a, b at the same element
       const uint4 va = *reinterpret_cast<const uint4*>(R + grow * ldc + gcol);
@@ -504,7 +579,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
       for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
       v = o.u;
     }
-    *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = v;
+    *reinterpret_cast<uint4*>(Cg + grow * ldc + gcol) = v;
   }
 }
 
@@ -573,6 +648,49 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   if (variant == 0) { LTA_G4V(0) }
   if (variant == 2) { LTA_G4V(2) }
 #undef LTA_G4V
+  return -1;
+}
+
+// Grouped GEMMs for mixture-of-experts training (K10; reference nvFuser _grouped_mm forward and
+// backward, thunder/executors/nvfuserex_impl.py:3226-3252), bf16, variant-1 pipeline.
+//   mode 1: C[M][N] rows of group g = A[rows of g][K] . op(B_g), B_g = B + g * bstride:
+//           bt = 0: B_g stored [N][K] (the expert weight: MoE forward), bt = 1: stored [K][N] (dgrad:
+//           dY . W_g with W_g [N_out = K-of-forward][...]); K % 128 == 0, N % 8 == 0.
+//   mode 2: C[g][M][N] (C + g * cstride) = A_g^T . B_g with A stored [rows][M] (lda), B stored
+//           [rows][N] (ldb) and group g's rows the reduction (wgrad); any group sizes (zero-filled
+//           reduction tails, empty groups give zeros); M, N % 8 == 0.
+// offs: int32 [G] cumulative group ends on the device (no host synchronisation).
+LTA_EXPORT int lta_gemm4_grouped(int mode, const void* A, const void* B, void* C, const void* offs, int G, int M, int N,
+                                 int K, int lda, int ldb, int ldc, int64_t bstride, int64_t cstride, int bt,
+                                 hipStream_t s) {
+  if (G <= 0 || M <= 0 || N <= 0 || N % 8 || !offs) return -2;
+  EpiArgs ep{};
+  ep.offs = (const int*)offs;
+  ep.G = G;
+  ep.bstride = bstride;
+  ep.cstride = cstride;
+  const int nTn = (N + BN - 1) / BN;
+  if (mode == 1) {
+    if (K % (2 * BK) || K <= 0) return -2;
+    const dim3 grid(((M + BM - 1) / BM + G) * nTn);
+    if (bt)
+      hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, true, 1, 0, 1>), grid, dim3(NTHR), 0, s,
+                         (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M,
+                         N, K, lda, ldb, ldc, 0, 1.f, ep);
+    else
+      hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, false, false, 1, 0, 1>), grid, dim3(NTHR), 0, s,
+                         (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M,
+                         N, K, lda, ldb, ldc, 0, 1.f, ep);
+    return (int)hipGetLastError();
+  }
+  if (mode == 2) {
+    if (M % 8) return -2;
+    const dim3 grid(G * ((M + BM - 1) / BM) * nTn);
+    hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, true, true, 1, 0, 2>), grid, dim3(NTHR), 0, s,
+                       (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N,
+                       K, lda, ldb, ldc, 0, 1.f, ep);
+    return (int)hipGetLastError();
+  }
   return -1;
 }
 

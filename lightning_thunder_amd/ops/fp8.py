@@ -195,13 +195,16 @@ class _DelayedState:
         self.recipe = recipe
         self.n = n_slots
         self.hist = self.cur = self.hmax = None
+        self.step_amax = None  # amax each slot was scaled from in the current step
         self.seen = [False] * n_slots
+        self.step_seen = [-1] * n_slots  # the step (``updates``) a slot was last quantised in
         self.updates = 0
 
     def ensure(self, device):
         if self.hist is None:
             z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=device)  # noqa: E731
             self.hist, self.cur, self.hmax = z(self.recipe.amax_history_len, self.n), z(self.n), z(self.n)
+            self.step_amax = z(self.n)
 
     def group(self):
         import torch.distributed as tdist
@@ -244,18 +247,28 @@ def delayed_update(key: int) -> None:
 
 def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
     """As :func:`quantize`, scaled from the slot's amax history; the tensor's own amax goes to the
-    slot's current-step entry.  Returns (q, q^T, scale) with a private scale scalar."""
+    slot's current-step entry.  Returns (q, q^T, scale) with a private scale scalar.
+
+    Every later quantisation of the slot within the same step — a sibling linear reading the same
+    input, or the backward's recompute of an activation-checkpointed region — is scaled from the
+    very amax the first one used, so the recompute reproduces the forward's fp8 values bit for bit
+    (also on a slot's first step, where the forward fell back to current scaling and the history is
+    still empty); its amax contribution is the same max again (reference: TE's recompute-phase
+    handling, thunder/executors/transformer_engineex_impl.py:459-515)."""
     st = _DELAYED[key]
     st.ensure(t.device)
     t2 = t.reshape(-1, t.shape[-1])
     fmax = (E5M2_MAX if e5m2 else E4M3_MAX) * 2.0 ** -st.recipe.margin
     scale = torch.empty((), dtype=torch.float32, device=t.device)
-    if st.seen[slot]:
-        amax_in = st.hmax[slot]
-    else:  # first use of the slot: no history yet -> current scaling for this call
-        st.seen[slot] = True
-        amax_in = torch.zeros((), dtype=torch.float32, device=t.device)
-        amax_into(t2, amax_in)
+    amax_in = st.step_amax[slot]
+    if st.step_seen[slot] != st.updates:  # first quantisation of the slot in this step
+        st.step_seen[slot] = st.updates
+        if st.seen[slot]:
+            amax_in.copy_(st.hmax[slot])
+        else:  # first use of the slot: no history yet -> current scaling for this step
+            st.seen[slot] = True
+            amax_in.zero_()
+            amax_into(t2, amax_in)
     q, qT = cast_transpose(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=st.cur[slot])
     return q, qT, scale
 

@@ -430,6 +430,10 @@ register_signature("lta_gemm_grouped_nt_bf16", [c_void_p, c_void_p, c_void_p, c_
                                                 c_int64, c_void_p])
 
 
+register_signature("lta_gemm4_grouped", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                         c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_void_p])
+
+
 def grouped_nt_supported(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> bool:
     """a [M, K]; b [G, K, N] given as the transpose of a K-contiguous [G, N, K] weight."""
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 3):
@@ -440,17 +444,96 @@ def grouped_nt_supported(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -
     return a.is_contiguous() and b.stride(1) == 1 and b.stride(2) == K and a.data_ptr() % 16 == 0
 
 
-def grouped_mm(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
-    """out[M, N] = a[rows of group g] @ b[g] (offs: int32 cumulative row ends)."""
-    if not grouped_nt_supported(a, b, offs):
-        return torch._grouped_mm(a, b, offs)
-    lib = require()
+def _grouped_b_layout(b: torch.Tensor):
+    """(bt, ldb) of a [G, K, N] grouped operand read per group as [K][N]: bt = 0 when each group is
+    stored [N][K] (K contiguous: an nn.Linear-style expert weight viewed transposed), 1 when stored
+    [K][N] (N contiguous: the dgrad's W_g); None otherwise."""
     G, K, N = b.shape
-    M = a.shape[0]
-    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    check(lib.lta_gemm_grouped_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
-                                       b.stride(0), stream_ptr(a.device)), "lta_gemm_grouped_nt_bf16")
-    return out
+    if b.data_ptr() % 16:
+        return None
+    if b.stride(1) == 1 and b.stride(2) % 8 == 0 and b.stride(2) >= K:
+        return 0, b.stride(2)
+    if b.stride(2) == 1 and b.stride(1) % 8 == 0 and b.stride(1) >= N:
+        return 1, b.stride(1)
+    return None
+
+
+def grouped_rows_supported(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> bool:
+    """The 2-D x 3-D grouped form on the 4-wave kernel (mode 1): a [M, K] row-major, b [G, K, N] in
+    either per-group layout, K % 128, N % 8."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 3):
+        return False
+    G, K, N = b.shape
+    if a.shape[1] != K or K % 128 or N % 8 or offs is None or offs.dtype != torch.int32 or offs.numel() != G:
+        return False
+    if not (a.stride(1) == 1 and a.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0):
+        return False
+    return _grouped_b_layout(b) is not None and b.stride(0) * G * 2 < 2 ** 62
+
+
+def grouped_mm(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """MoE grouped GEMM (``torch._grouped_mm`` semantics), on hand kernels when the layout allows:
+      * a [M, K] @ b [G, K, N] -> [M, N]: rows [offs[g-1], offs[g]) of ``a`` times ``b[g]`` (forward,
+        and the dgrad ``dY @ W_g`` whose b is the expert weight itself);
+      * a [K, M] @ b [M, N] -> [G, K, N]: per group the product over its rows (the wgrad
+        ``x_g^T dY_g``), written straight in the expert weight's [G, N, K] layout and returned as
+        its transposed view;
+    ``offs``: int32 cumulative row ends."""
+    if a.dim() == 2 and b.dim() == 2:
+        return grouped_mm_wgrad(a, b, offs)
+    if grouped_rows_supported(a, b, offs):
+        G, K, N = b.shape
+        M = a.shape[0]
+        bt, ldb = _grouped_b_layout(b)
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+        _count("gemm4")
+        check(require().lta_gemm4_grouped(1, a.data_ptr(), b.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
+                                          a.stride(0), ldb, N, b.stride(0), 0, bt, stream_ptr(a.device)),
+              "lta_gemm4_grouped")
+        return out
+    if grouped_nt_supported(a, b, offs):
+        lib = require()
+        G, K, N = b.shape
+        M = a.shape[0]
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+        _count("gemm")
+        check(lib.lta_gemm_grouped_nt_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), offs.data_ptr(), G, M, N, K,
+                                           b.stride(0), stream_ptr(a.device)), "lta_gemm_grouped_nt_bf16")
+        return out
+    _count("torch")
+    return torch._grouped_mm(a, b, offs)
+
+
+def grouped_wgrad_supported(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> bool:
+    """a [K, M] viewed from a row-major [M, K] (token rows), b [M, N] row-major."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2):
+        return False
+    K, M = a.shape
+    N = b.shape[1]
+    if b.shape[0] != M or K % 8 or N % 8 or offs is None or offs.dtype != torch.int32:
+        return False
+    return (a.stride(0) == 1 and a.stride(1) % 8 == 0 and b.stride(1) == 1 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def grouped_mm_wgrad(a: torch.Tensor, b: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """[G, K, N] = per group g: a[:, rows of g] @ b[rows of g] — the MoE wgrad.  Computed as
+    C'[g] = b_g^T a_g^T, i.e. [G][N][K] (the expert weight's own layout, so its gradient needs no
+    transposing copy) on the 4-wave kernel's grouped-reduction mode, returned transposed."""
+    if not grouped_wgrad_supported(a, b, offs):
+        _count("torch")
+        return torch._grouped_mm(a, b, offs)
+    K, M = a.shape
+    N = b.shape[1]
+    G = offs.numel()
+    out = torch.empty((G, N, K), dtype=torch.bfloat16, device=a.device)
+    _count("gemm4")
+    # C'[g] [N][K] = b_g^T . a_g^T: A operand = b stored [rows][N] (at = 1), B operand = a's storage
+    # [rows][K] (bt = 1)
+    check(require().lta_gemm4_grouped(2, b.data_ptr(), a.data_ptr(), out.data_ptr(), offs.data_ptr(), G, N, K, M,
+                                      b.stride(0), a.stride(1), K, 0, N * K, 1, stream_ptr(a.device)),
+          "lta_gemm4_grouped")
+    return out.transpose(1, 2)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -90,40 +90,64 @@ class FP8LinearTransform(Transform):
             "mxfp4" if isinstance(self.recipe, MXFP4BlockScaling) else None)
         delayed = self.recipe != "current" and not mx
         slots: dict = {}  # ("x"|"w", proxy name) / ("dy", site) -> history slot; siblings reading one x share it
+        key = None
+        if delayed:
+            from ..ops.fp8 import new_delayed_state
+
+            key = new_delayed_state(self.recipe, 0)  # slot count set once the program is scanned
 
         def slot(k):
             return slots.setdefault(k, len(slots))
 
-        sites = []
+        def convert(nb):
+            """fp8_linear bound to the linear's own output proxy, or None when not eligible."""
+            nonlocal n
+            if nb.sym.name != "linear" or len(nb.args) < 2:
+                return None
+            x, w = nb.args[0], nb.args[1]
+            bias = nb.args[2] if len(nb.args) > 2 else nb.kwargs.get("bias")
+            if not eligible(x, w, bias) or any(s in w.name for s in self.skip):
+                return None
+            if delayed:
+                args = (x, w, bias, key, (slot(("x", x.name)), slot(("w", w.name)), slot(("dy", n))))
+            elif mx:
+                args = (x, w, bias, mx)
+            else:
+                args = (x, w, bias)
+            n += 1
+            return fp8_linear.bind(*args, output=nb.output)
+
+        def rewrite_region(b):
+            """Activation-checkpointed regions keep their linears as subsymbols of the checkpoint
+            call: convert those too (the backward's recompute then replays fp8_linear)."""
+            subs = []
+            changed = False
+            for sb in b.subsymbols:
+                cv = convert(sb)
+                if cv is None and sb.sym.name == "checkpoint":
+                    cv = rewrite_region(sb)
+                subs.append(cv if cv is not None else sb)
+                changed |= cv is not None
+            return b.from_bsym(subsymbols=subs) if changed else None
+
         with tracectx(new):
             for b in computation_trace.bound_symbols:
                 nb = b.swap_proxies(swap, skip_output=True)
-                if b.sym.name == "linear" and len(nb.args) >= 2:
-                    x, w = nb.args[0], nb.args[1]
-                    bias = nb.args[2] if len(nb.args) > 2 else nb.kwargs.get("bias")
-                    if eligible(x, w, bias) and not any(s in w.name for s in self.skip):
-                        if delayed:
-                            sl = (slot(("x", x.name)), slot(("w", w.name)), slot(("dy", n)))
-                            sites.append(len(new.bound_symbols))
-                            y = fp8_linear(x, w, bias, -1, sl)  # key patched below (slot count known last)
-                        elif mx:
-                            y = fp8_linear(x, w, bias, mx)
-                        else:
-                            y = fp8_linear(x, w, bias)
-                        swap[b.output.name] = y
-                        n += 1
-                        continue
-                new.bound_symbols.append(nb)
+                cv = convert(nb)
+                if cv is None and nb.sym.name == "checkpoint":
+                    cv = rewrite_region(nb)
+                new.bound_symbols.append(cv if cv is not None else nb)
         self.n_converted = n
         if not n:
             return prologue_trace, computation_trace, epilogue_trace
         if delayed:
-            from ..ops.fp8 import new_delayed_state
+            from ..ops.fp8 import delayed_state
 
-            self.state_key = key = new_delayed_state(self.recipe, len(slots))
-            for i in sites:
-                b = new.bound_symbols[i]
-                new.bound_symbols[i] = b.from_bsym(args=b.args[:3] + (key,) + b.args[4:])
+            st = delayed_state(key)
+            st.n = len(slots)
+            st.seen = [False] * st.n
+            st.step_seen = [-1] * st.n
+            self.state_key = key
             upd = fp8_delayed_update.bind(key, output=None)
             new.bound_symbols.insert(0, upd)
         what = "current scaling" if self.recipe == "current" else f"{self.recipe!r}"

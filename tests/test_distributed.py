@@ -74,6 +74,10 @@ def _worker(rank, port, mode, out_dir):
         jm = thunder.jit(m)
         if mode == "blocks_zero3":
             jm = fsdp(jm, sharding_strategy=FSDPType.ZERO3, bucketing_strategy=FSDPBucketingStrategy.BLOCK)
+        elif mode == "blocks_zero2":
+            # ~one block's gradients per bucket (8x8 weight + bias, fp64 = 576 B)
+            jm = fsdp(jm, sharding_strategy=FSDPType.ZERO2, bucketing_strategy=FSDPBucketingStrategy.BLOCK,
+                      bucket_size_in_mb=500 / 2 ** 20)
         elif mode == "ddp":
             jm = ddp(jm, bucket_size_in_mb=0.0005)
         elif mode == "ddp_nobucket":
@@ -170,3 +174,28 @@ def test_fsdp_zero3_allgather_window():
         assert len(gathers) >= 4, res[0][key]
         # gather of block 2 comes after the first wait: at most two blocks in flight
         assert gathers[2] > waits[0], (key, gathers, waits)
+
+
+def test_fsdp_zero2_reduce_scatter_overlaps_backward():
+    """ZeRO-2 with one bucket per block: each block's gradient reduce-scatter is issued as soon as the
+    block's gradients exist — before the next (earlier) block's backward matmuls — and every wait
+    comes after all of them, so the collectives overlap the rest of the backward; grads match."""
+    import re
+
+    from lightning_thunder_amd.distributed.transforms import shard_tensor
+
+    ref, _ = _reference_grads(_Blocks)
+    res = _run("blocks_zero2_coalesced")
+    for rank, r in enumerate(res):
+        for n, g in ref.items():
+            expected, _ = shard_tensor(g, rank, WORLD)
+            torch.testing.assert_close(r["grads"][n], expected)
+    lines = [l for l in res[0]["bw"].splitlines() if "=" in l and not l.strip().startswith("#")]
+    mm = [i for i, l in enumerate(lines) if re.search(r"\bmatmul\(", l)]
+    rs = [i for i, l in enumerate(lines) if "reduce_scatter" in l]
+    waits = [i for i, l in enumerate(lines) if re.search(r"\bdist_wait\(|\bwait\(", l)]
+    assert len(rs) == 5, res[0]["bw"]  # one coalesced reduce-scatter per block
+    for k, i in enumerate(rs[:-1]):
+        # compute of an earlier block runs between this block's issue and the next issue
+        assert any(i < j < rs[k + 1] for j in mm), (k, res[0]["bw"])
+    assert rs[0] < mm[-1] and min(waits) > mm[-1], res[0]["bw"]

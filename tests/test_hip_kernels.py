@@ -942,3 +942,137 @@ def test_linear_edge_tiles_bias_act(M, N):
     assert last_gemm_backend_counts(reset=True).get("gemm4", 0) == 1
     ref = torch.nn.functional.gelu(x.float() @ w.float().t() + bias.float(), approximate="tanh")
     assert (y.float() - ref).abs().max().item() < 5e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe", ["delayed", "current"])
+def test_fp8_activation_checkpointing_matches_plain(recipe):
+    """FP8 linears inside an activation-checkpointed block: the transform converts them (they are
+    subsymbols of the checkpoint call), and the backward's recompute reproduces the forward's fp8
+    values, so over several delayed-scaling steps (the first one on current scaling, later ones on
+    the amax history) every loss and gradient equals the un-checkpointed run's."""
+    from torch.utils.checkpoint import checkpoint
+
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    class Block(torch.nn.Module):
+        def __init__(self, ckpt):
+            super().__init__()
+            self.ckpt = ckpt
+            self.a = torch.nn.Linear(512, 1024, bias=False)
+            self.b = torch.nn.Linear(1024, 512, bias=False)
+
+        def inner(self, x):
+            return self.b(torch.nn.functional.gelu(self.a(x)))
+
+        def forward(self, x):
+            h = checkpoint(self.inner, x, use_reentrant=False) if self.ckpt else self.inner(x)
+            return (h.float() ** 2).mean()
+
+    torch.manual_seed(0)
+    plain = Block(False).cuda().bfloat16()
+    ck = Block(True).cuda().bfloat16()
+    ck.load_state_dict(plain.state_dict())
+    ta, tb = FP8LinearTransform(recipe=recipe), FP8LinearTransform(recipe=recipe)
+    jp, jc = thunder.jit(plain, transforms=[ta]), thunder.jit(ck, transforms=[tb])
+    for step in range(3):
+        x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16, generator=torch.Generator("cuda").manual_seed(step))
+        lp, lc = jp(x), jc(x)
+        lp.backward()
+        lc.backward()
+        assert ta.n_converted == 2 and tb.n_converted == 2
+        torch.testing.assert_close(lc, lp, rtol=0, atol=0)
+        for (n, p), (_, q) in zip(plain.named_parameters(), ck.named_parameters()):
+            torch.testing.assert_close(q.grad, p.grad, rtol=0, atol=0, msg=f"step {step} {n}")
+            p.grad = None
+            q.grad = None
+    bw = str(thunder.last_backward_traces(jc)[-1])
+    assert "fp8" in bw  # the checkpointed region recomputes its fp8 forward in the backward
+
+
+@pytest.mark.gpu
+def test_lds_dma_out_of_range_lanes_write_zero():
+    """Out-of-range lanes of an LDS-DMA buffer load deposit zeros in LDS (not stale bytes): the
+    grouped wgrad GEMM's reduction tail depends on it."""
+    import ctypes
+
+    from lightning_thunder_amd.ops._lib import require, stream_ptr
+
+    lib = require()
+    src = torch.arange(256, device="cuda", dtype=torch.int32).view(torch.uint8)[:1024].contiguous()
+    out = torch.empty(1024, device="cuda", dtype=torch.uint8)
+    valid = 16 * 20  # lanes 0..19 in range
+    rc = lib.lta_probe_lds_dma_oob(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(out.data_ptr()), valid,
+                                   ctypes.c_void_p(stream_ptr(src.device)))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out[:valid], src[:valid])
+    assert (out[valid:] == 0).all(), out[valid:valid + 32]
+
+
+def _ragged_offsets(M, G, device):
+    # uneven groups incl. an empty one and sizes that divide neither 64 nor 256
+    sizes = torch.tensor([300, 0, 77, 513, 1, 129, 600, 0][:G])
+    sizes[-1] = M - sizes[:-1].sum()
+    assert (sizes >= 0).all()
+    return torch.cumsum(sizes, 0).to(torch.int32).to(device), sizes
+
+
+@pytest.mark.gpu
+def test_grouped_gemm_forward_dgrad_wgrad():
+    """The three MoE grouped GEMMs on the 4-wave kernel's grouped modes, against fp32 per group:
+    forward a @ W_g^T, dgrad dY @ W_g and wgrad dY_g^T x_g (written in W's [G, N, K] layout)."""
+    from lightning_thunder_amd.ops.gemm import grouped_mm, last_gemm_backend_counts
+
+    torch.manual_seed(0)
+    G, M, K, N = 8, 2048, 256, 384
+    offs, sizes = _ragged_offsets(M, G, "cuda")
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(G, N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5  # nn.Linear-style experts
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    last_gemm_backend_counts(reset=True)
+    y = grouped_mm(x, w.transpose(-1, -2), offs)     # forward  [M, N]
+    dx = grouped_mm(dy, w, offs)                      # dgrad    [M, K]  (b = W_g [N][K] read as [K-red][N-out])
+    dwT = grouped_mm(x.t(), dy, offs)                 # wgrad    [G, K, N]
+    counts = last_gemm_backend_counts(reset=True)
+    assert counts.get("gemm4", 0) == 3 and counts.get("torch", 0) == 0, counts
+    assert dwT.transpose(1, 2).is_contiguous()        # the weight's own [G, N, K] layout
+    start = 0
+    for g in range(G):
+        end = start + int(sizes[g])
+        xs, ds = x[start:end].float(), dy[start:end].float()
+        ry = xs @ w[g].float().t()
+        rdx = ds @ w[g].float()
+        rdw = xs.t() @ ds
+        for got, ref in ((y[start:end], ry), (dx[start:end], rdx), (dwT[g], rdw)):
+            err = (got.float() - ref).abs().max().item() if ref.numel() else 0.0
+            assert err < 2e-2 * max(1.0, ref.abs().max().item()), (g, err)
+        start = end
+
+
+@pytest.mark.gpu
+def test_moe_training_backward_on_hand_grouped_kernels():
+    """A Llama-4-style MoE block training step: forward AND backward expert GEMMs run on the hand
+    grouped kernels (hip_grouped_mm in both traces, no library _grouped_mm), grads match eager."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.llama4_moe import Llama4MoE, MoEConfig
+    from lightning_thunder_amd.ops.gemm import last_gemm_backend_counts
+
+    torch.manual_seed(0)
+    m = Llama4MoE(MoEConfig()).cuda().bfloat16()
+    x = torch.randn(1, 2048, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    jm = thunder.jit(m)
+    last_gemm_backend_counts(reset=True)
+    out = jm(x)
+    ref = m(x)
+    g = torch.randn_like(out)
+    ins = [x] + list(m.parameters())
+    ga = torch.autograd.grad(out, ins, g)
+    gr = torch.autograd.grad(ref, ins, g)
+    for a, b in zip(ga, gr):
+        rel = ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-6)).item()
+        assert rel < 3e-2, (tuple(a.shape), rel)
+    fw, bw = str(thunder.last_traces(jm)[-1]), str(thunder.last_backward_traces(jm)[-1])
+    assert "hip_grouped_mm" in fw and "hip_grouped_mm" in bw
+    assert "_grouped_mm(" not in bw.replace("hip_grouped_mm(", ""), bw
