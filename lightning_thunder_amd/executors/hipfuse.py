@@ -317,8 +317,10 @@ def _connected(plan_names: set, group_inputs: set, b: BoundSymbol) -> bool:
 
 
 def _external_view(names: set, b: BoundSymbol) -> bool:
-    """Broadcasts/unit reshapes of values produced outside the open region are free to join it."""
-    return b.sym.id in cg.VIEWS and not any(a.name in names for a in b.flat_proxy_args)
+    """Views (broadcasts, reshapes, slices, ...) and gathers / concatenations of values produced
+    outside the open region are free to join it (e.g. a position-embedding lookup joins the region
+    that adds it to the token embeddings)."""
+    return (b.sym.id in cg.VIEWS or b.sym.id in cg.GATHERS) and not any(a.name in names for a in b.flat_proxy_args)
 
 
 _LAZY: set = set()  # names of lazily re-materialised casts of the trace being partitioned

@@ -107,12 +107,55 @@ _BINARY_SPECIAL = {PrimIDs.MAXIMUM, PrimIDs.MINIMUM}
 REDUCTIONS = {PrimIDs.SUM, PrimIDs.AMAX, PrimIDs.AMIN, PrimIDs.PROD, PrimIDs.VAR_MEAN}
 ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY | _BINARY_SPECIAL | {
     PrimIDs.WHERE, PrimIDs.CONVERT_ELEMENT_TYPE}
-VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD}
-SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
+VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD, PrimIDs.SLICE}
+# data movement with indirect / piecewise loads of external inputs (pointwise regions only)
+GATHERS = {PrimIDs.CAT, PrimIDs.TAKE, PrimIDs.TAKE_ALONG_AXIS, PrimIDs.EMBEDDING}
+SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | GATHERS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
 
 
 def is_compute(bsym) -> bool:
-    return bsym.sym.id in ELEMENTWISE or bsym.sym.id in REDUCTIONS or bsym.sym.id == PrimIDs.UNIFORM_PHILOX
+    sid = bsym.sym.id
+    return sid in ELEMENTWISE or sid in REDUCTIONS or sid in GATHERS or sid == PrimIDs.UNIFORM_PHILOX
+
+
+def tensor_args(b):
+    """(key, proxy) of every tensor operand of ``b``: the argument position, or (0, j) for the
+    j-th tensor of a ``cat`` list.  Arg maps (``Plan.arg_maps``) are keyed the same way."""
+    if b.sym.id == PrimIDs.CAT:
+        return [((0, j), t) for j, t in enumerate(b.args[0]) if isinstance(t, TensorProxy)]
+    return [(i, a) for i, a in enumerate(b.args) if isinstance(a, TensorProxy)]
+
+
+def base_map(amap):
+    """The domain-dim map inside an arg map: plain maps are tuples of domain dims (or None);
+    conditional / affine / indirect loads are tagged tuples ``(kind, base, ...)``:
+
+    * ``("pad", base, lo, value)``: input dim i walks domain dim base[i] shifted by -lo[i]; out of range -> value
+    * ``("slice", base, start, step)``: input index start[i] + step[i] * i_{base[i]} (an affine load)
+    * ``("gather", base, dim, idx_name, idx_map, size)``: input dim ``dim`` is indexed by the value of
+      the index tensor ``idx_name`` read through ``idx_map``; the other dims through ``base``
+    * ``("cat", base, dim, lo)``: one piece of a concatenation; dim ``dim`` offset by ``lo``
+    * ``("reshape", base, shape)``: the input read as if reshaped to ``shape`` (row-major), whose
+      dims walk ``base``
+    """
+    if amap and isinstance(amap[0], str):
+        return amap[1]
+    return amap
+
+
+def _kind(amap):
+    return amap[0] if amap and isinstance(amap[0], str) else None
+
+
+def _remap_amap(amap, f):
+    if amap is None:
+        return None
+    rm = lambda mp: tuple(None if x is None else f(x) for x in mp)  # noqa: E731
+    if amap and isinstance(amap[0], str):
+        if amap[0] == "gather":
+            return (amap[0], rm(amap[1]), amap[2], amap[3], rm(amap[4]), amap[5])
+        return (amap[0], rm(amap[1])) + tuple(amap[2:])
+    return rm(amap)
 
 
 def _sq(shape):
@@ -128,7 +171,7 @@ class Plan:
     red: int = 0  # number of trailing reduced domain dims
     colred: int = 0  # number of LEADING reduced domain dims (column mode; exclusive with red)
     has_reduction: bool = False
-    has_pad: bool = False  # pads (conditional loads) are admitted in pointwise regions only
+    has_pad: bool = False  # pads / cats / gathers (conditional or indirect loads): pointwise regions only
     nodes: list = field(default_factory=list)
     maps: dict = field(default_factory=dict)  # internal value name -> map tuple
     arg_maps: list = field(default_factory=list)  # per node: {arg position: map} for tensor args
@@ -202,11 +245,10 @@ class Plan:
         self.maps[name] = m
         for k, b in enumerate(self.nodes):
             if any(o.name == name for o in b.flat_outs):
-                for pos, a in enumerate(b.args):
-                    if isinstance(a, TensorProxy):
-                        self.arg_maps[k][pos] = m
-                        if a.name in self.maps:
-                            self._resolve(a.name, m)
+                for pos, a in tensor_args(b):
+                    self.arg_maps[k][pos] = m
+                    if a.name in self.maps:
+                        self._resolve(a.name, m)
 
     def _check_dtype(self, *ts):
         for t in ts:
@@ -248,6 +290,12 @@ class Plan:
             self._add_transpose(bsym, am)
         elif sid == PrimIDs.PAD:
             self._add_pad(bsym, am)
+        elif sid == PrimIDs.SLICE:
+            self._add_slice(bsym, am)
+        elif sid == PrimIDs.CAT:
+            self._add_cat(bsym, am)
+        elif sid in (PrimIDs.TAKE, PrimIDs.TAKE_ALONG_AXIS, PrimIDs.EMBEDDING):
+            self._add_gather(bsym, am)
         elif sid in REDUCTIONS:
             self._add_reduction(bsym, am)
         elif sid == PrimIDs.UNIFORM_PHILOX:
@@ -329,7 +377,7 @@ class Plan:
                     if s != 1 and shape[bdims[d]] != s:
                         raise NotFusible("bad upgrade")
                 def remap(mp):
-                    return tuple(None if x is None else bdims[x] for x in mp)
+                    return _remap_amap(mp, lambda x: bdims[x])
                 self.maps = {k: remap(v) for k, v in self.maps.items()}
                 self.arg_maps = [{k: remap(v) for k, v in d.items()} for d in self.arg_maps]
                 self._set_domain(shape)
@@ -400,9 +448,120 @@ class Plan:
         self.has_pad = True
         self.maps[out.name] = om
 
+    def _ext_out_map(self, out, what):
+        """Map of the output of an op on external inputs: it must span the domain (or open it)."""
+        om = self._map_for_shape(out.shape)
+        if om == "new":
+            self._set_domain(out.shape)
+            om = self._identity(out.shape)
+        if om is None and not (self.red or self.colred or self.has_reduction):
+            # a pointwise region: a smaller value right-aligned with the domain (what a later
+            # broadcast makes of it, e.g. a position embedding added to token embeddings) is
+            # evaluated per domain element
+            shape, D = tuple(out.shape), self.domain
+            k = len(D) - len(shape)
+            if k >= 0 and all(s == 1 or s == D[k + i] for i, s in enumerate(shape)):
+                om = tuple(None if s == 1 else k + i for i, s in enumerate(shape))
+        if om is None:
+            raise NotFusible(f"{what} to non-domain shape")
+        return tuple(om)
+
+    def _add_slice(self, bsym, am):
+        """Slice of an external input (e.g. q / k / v split from a fused projection, a strided
+        subsample): an affine load — base offset sum(start_i * stride_i), stride_i * step_i per dim.
+        Admitted in every mode (it is a plain strided read)."""
+        a, out = bsym.args[0], bsym.output
+        if self._internal(a):
+            raise NotFusible("slice of an internal value")
+        starts = tuple(int(pyval(x)) for x in bsym.args[1])
+        steps = tuple(int(pyval(x)) for x in bsym.args[3]) if len(bsym.args) > 3 and bsym.args[3] is not None \
+            else (1,) * a.ndim
+        om = self._ext_out_map(out, "slice")
+        am[0] = ("slice", om, starts, steps)
+        self.maps[out.name] = om
+
+    def _add_cat(self, bsym, am):
+        """Concatenation of external inputs: each piece is a load offset along the cat dim; per
+        vector the piece is selected by the domain index (pointwise regions only)."""
+        tensors, dim = list(bsym.args[0]), int(pyval(bsym.args[1]))
+        out = bsym.output
+        if any(self._internal(t) for t in tensors) or not all(isinstance(t, TensorProxy) for t in tensors):
+            raise NotFusible("cat of an internal value")
+        if self.red or self.colred or self.has_reduction:
+            raise NotFusible("cat in a reduction region")
+        om = self._ext_out_map(out, "cat")
+        lo = 0
+        for j, t in enumerate(tensors):
+            am[(0, j)] = ("cat", om, dim, lo)
+            lo += int(t.shape[dim])
+        self.has_pad = True
+        self.maps[out.name] = om
+
+    def _add_gather(self, bsym, am):
+        """Indirect loads: ``take`` (index_select), ``take_along_axis`` (gather) and ``embedding`` of
+        external inputs.  The index tensor is read through its own map; out-of-range indices are
+        clamped into the source (never an out-of-bounds read).  Pointwise regions only."""
+        sid, out = bsym.sym.id, bsym.output
+        if sid == PrimIDs.EMBEDDING:
+            idx, a, dim = bsym.args[0], bsym.args[1], 0
+            if bsym.kwargs.get("max_norm") is not None:
+                raise NotFusible("embedding max_norm")
+            apos, ipos = 1, 0
+        else:
+            a, idx, dim = bsym.args[0], bsym.args[1], int(pyval(bsym.args[2]))
+            apos, ipos = 0, 1
+        if not isinstance(a, TensorProxy) or not isinstance(idx, TensorProxy) or self._internal(a):
+            raise NotFusible("gather of an internal value")
+        if idx.dtype not in _INTS:
+            raise NotFusible("gather index dtype")
+        if self.red or self.colred or self.has_reduction:
+            raise NotFusible("gather in a reduction region")
+        ni = idx.ndim
+        ipos_out = tuple(range(ni)) if sid in (PrimIDs.EMBEDDING, PrimIDs.TAKE_ALONG_AXIS) else \
+            tuple(range(dim, dim + ni))
+        if self._internal(idx) and self.domain is not None and tuple(idx.shape) == self.domain and \
+                tuple(out.shape) != self.domain:
+            # domain upgrade: the region so far computed the index; it continues over the gathered
+            # value, each index dim walking its output dim
+            def remap(mp):
+                return _remap_amap(mp, lambda x: ipos_out[x])
+            self.maps = {k: remap(v) for k, v in self.maps.items()}
+            self.arg_maps = [{k: remap(v) for k, v in d.items()} for d in self.arg_maps]
+            self._set_domain(out.shape)
+        om = self._ext_out_map(out, "gather")
+        if sid == PrimIDs.TAKE_ALONG_AXIS:
+            imap = om
+            base = tuple(None if i == dim else om[i] for i in range(a.ndim))
+        else:
+            if sid == PrimIDs.EMBEDDING:
+                imap = om[:ni]
+                base = (None, om[ni])
+            else:
+                imap = om[dim:dim + ni]
+                base = om[:dim] + (None,) + om[dim + ni:]
+        imap = tuple(None if idx.shape[i] == 1 else imap[i] for i in range(idx.ndim))
+        if self._internal(idx):
+            # an index computed in the region (e.g. positions from arithmetic on an iota)
+            if self.maps[idx.name] is None:
+                self._resolve(idx.name, imap)
+            elif self.maps[idx.name] != imap:
+                raise NotFusible("gather index with a different map")
+        else:
+            am[ipos] = imap
+        am[apos] = ("gather", base, dim, idx.name, imap, int(a.shape[dim]))
+        self.has_pad = True
+        self.maps[out.name] = om
+
     def _add_unit_reshape(self, bsym, am):
         a, out = bsym.args[0], bsym.output
         if _sq(a.shape) != _sq(out.shape):
+            if bsym.sym.id == PrimIDs.RESHAPE and not self._internal(a):
+                # a general reshape of an external input: read it as the reshaped tensor (a view
+                # when its strides allow, else an index decomposition)
+                om = self._ext_out_map(out, "reshape")
+                am[0] = ("reshape", om, tuple(int(x) for x in out.shape))
+                self.maps[out.name] = om
+                return
             raise NotFusible("non-unit reshape")
         if self._internal(a):
             if self.maps[a.name] is None:
@@ -598,6 +757,47 @@ def _contig_strides(shape):
 _VALUE_ID = re.compile(r"\b([vr])_([A-Za-z_]\w*)")
 
 
+def _view_strides(shape, strides, new_shape):
+    """Strides of ``new_shape`` as a view of a tensor (``shape``, ``strides``), or None when the
+    reshape needs a copy (the rule of ``torch.Tensor.view``: each run of merged / split dims must
+    be contiguous within itself)."""
+    shape, strides, new_shape = list(shape), list(strides), list(new_shape)
+    if math.prod(shape) != math.prod(new_shape):
+        return None
+    if math.prod(shape) == 0:
+        return _contig_strides(tuple(new_shape))
+    res = [0] * len(new_shape)
+    # drop size-1 input dims; chunk the rest into contiguous runs
+    dims = [(n, s) for n, s in zip(shape, strides) if n != 1]
+    vi = len(new_shape) - 1
+    ci = len(dims) - 1
+    while vi >= 0 or ci >= 0:
+        # one chunk: input dims [cj, ci] contiguous among themselves
+        if ci < 0:
+            while vi >= 0:
+                if new_shape[vi] != 1:
+                    return None
+                res[vi] = 1
+                vi -= 1
+            break
+        cj = ci
+        while cj > 0 and dims[cj - 1][1] == dims[cj][1] * dims[cj][0]:
+            cj -= 1
+        chunk = math.prod(n for n, _ in dims[cj:ci + 1])
+        stride = dims[ci][1]
+        acc = 1
+        while vi >= 0 and (acc < chunk or new_shape[vi] == 1):
+            res[vi] = stride * acc
+            acc *= new_shape[vi]
+            vi -= 1
+            if acc == chunk and (vi < 0 or new_shape[vi] != 1):
+                break
+        if acc != chunk:
+            return None
+        ci = cj - 1
+    return res
+
+
 def _canonical_names(body: str) -> str:
     """Renames the per-value identifiers (``v_<proxy>`` / ``r_<proxy>``) by order of first use, so
     structurally identical regions (e.g. the same fusion in every transformer layer) produce the
@@ -664,14 +864,12 @@ class _Gen:
         for k, b in enumerate(self.p.nodes):
             am = self.p.arg_maps[k]
             dep, lvl = False, 0
-            for i, a in enumerate(b.args):
-                if not isinstance(a, TensorProxy):
-                    continue
+            for i, a in tensor_args(b):
                 if a.name in self.dep:
                     dep |= self.dep[a.name]
                     lvl = max(lvl, self.level[a.name])
                 else:
-                    m = am.get(i)
+                    m = base_map(am.get(i))
                     d = self.red == 0 or any(x in red for x in m if x is not None)
                     dep |= d
             if b.sym.id in REDUCTIONS:
@@ -702,12 +900,12 @@ class _Gen:
 
     def _dstrides(self, arg: TensorArg, amap) -> list:
         """Per-domain-dim element strides of an external tensor read through ``amap``."""
-        if amap and amap[0] == "pad":
-            amap = amap[1]
+        steps = amap[3] if amap and amap[0] == "slice" else None
+        amap = base_map(amap)
         st = [0] * self.nd
         for i, d in enumerate(amap):
             if d is not None and arg.shape[i] != 1:
-                st[d] += arg.strides[i]
+                st[d] += arg.strides[i] * (steps[i] if steps else 1)
         return st
 
     def build(self):
@@ -789,8 +987,21 @@ class _Gen:
         if sid == PrimIDs.WHERE:
             cond = R(0, "bool")
             return [(out.name, f"({cond} ? {R(1)} : {R(2)})")]
-        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD):
+        if sid in (PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD,
+                   PrimIDs.SLICE, PrimIDs.TAKE, PrimIDs.TAKE_ALONG_AXIS):
             return [(out.name, R(0))]  # index remapping only: the arg map / conditional load does the work
+        if sid == PrimIDs.EMBEDDING:
+            return [(out.name, R(1))]
+        if sid == PrimIDs.CAT:
+            # select the piece that owns this domain index along the cat dim
+            pieces = tensor_args(b)
+            d = base_map(self.p.arg_maps[k][pieces[0][0]])[int(pyval(b.args[1]))]
+            idx = f"(i{d}{' + j' if (lane and d == self.nd - 1) else ''})"
+            e = self.ref(pieces[-1][1], k, pieces[-1][0], lane)
+            for key, t in reversed(pieces[:-1]):
+                hi = self.p.arg_maps[k][key][3] + int(t.shape[int(pyval(b.args[1]))])
+                e = f"({idx} < {hi}u ? {self.ref(t, k, key, lane)} : {e})"
+            return [(out.name, e)]
         if sid == PrimIDs.FULL:
             return [(out.name, self._scalar_ref(b.args[1], ct))]
         if sid == PrimIDs.UNIFORM_PHILOX:
@@ -802,7 +1013,7 @@ class _Gen:
                 u = f"({u} * {_lit(hi - lo, 'float')} + {_lit(lo, 'float')})"
             return [(out.name, _rnd(out.dtype, f"({ct})({u})"))]
         # operand compute type: that of the first tensor operand (prims enforce equal dtypes)
-        tin = [a for a in b.args if isinstance(a, TensorProxy)]
+        tin = [a for _, a in tensor_args(b)]
         ict = _CTYPE[tin[0].dtype] if tin else ct
         if sid in _UNARY_FLOAT:
             return [(out.name, _rnd(out.dtype, f"{_f(_UNARY_FLOAT[sid], ict)}({R(0)})"))]
@@ -865,7 +1076,7 @@ class _Gen:
             nm = f"L{len(self.load_names)}"
             self.load_names[key] = nm
         red = self._reduced_dims()
-        dep = self.red == 0 or any(x in red for x in amap if x is not None)
+        dep = self.red == 0 or any(x in red for x in base_map(amap) if x is not None)
         if lane and dep:
             return f"{nm}[{lane}]"
         return nm
@@ -880,11 +1091,10 @@ class _Gen:
                 return
             k = self.producer[name]
             b = self.p.nodes[k]
-            for a in b.args:
-                if isinstance(a, TensorProxy):
-                    if a.name in self.producer:
-                        if scope == "row" or self.dep.get(a.name, True):
-                            want(a.name)
+            for _, a in tensor_args(b):
+                if a.name in self.producer:
+                    if scope == "row" or self.dep.get(a.name, True):
+                        want(a.name)
                     # external loads are materialised when referenced
             if k not in order:
                 order.append(k)
@@ -913,12 +1123,14 @@ class _Gen:
         if self.force_scalar:
             return False
         red = self._reduced_dims()
-        return self.red == 0 or any(x in red for x in amap if x is not None)
+        return self.red == 0 or any(x in red for x in base_map(amap) if x is not None)
 
     def _materialize_loads(self, b, k, vec_scope, out, indent):
         """Emit the external loads node ``k`` references, once per scope."""
-        for i, a in enumerate(b.args):
-            if not isinstance(a, TensorProxy) or a.name in self.producer:
+        # indirect (gather) loads last: they read the index loads of the same node
+        items = sorted(tensor_args(b), key=lambda it: _kind(self.p.arg_maps[k].get(it[0])) == "gather")
+        for i, a in items:
+            if a.name in self.producer:
                 continue
             amap = self.p.arg_maps[k][i]
             nm = self.load_names[(a.name, amap)]
@@ -949,7 +1161,7 @@ class _Gen:
         V, last = self.vec, self.nd - 1
         conds, terms = [], []
         for i, d in enumerate(base):
-            if d is None or a.shape[i] == 1:
+            if d is None:  # a size-1 output dim: index 0, in range
                 continue
             if f"i{d}" not in self.idx_avail:
                 raise NotFusible(f"codegen: index i{d} not available for pad load of {a.name}")
@@ -965,40 +1177,160 @@ class _Gen:
                    f"{_load_conv(a.dtype, f'{ptr}[{off}]')} : {_lit(pv, ct)};")
 
     def _emit_load(self, a, amap, nm, vec_scope, out, indent):
-        if amap and amap[0] == "pad":
-            assert vec_scope, "pad loads exist in pointwise regions only"
+        kind = _kind(amap)
+        if kind in ("pad", "cat", "gather"):
+            assert vec_scope, f"{kind} loads exist in pointwise regions only"
+        if kind == "pad":
             return self._emit_pad_load(a, amap, nm, out, indent)
+        if kind == "cat":
+            return self._emit_cat_load(a, amap, nm, out, indent)
+        if kind == "gather":
+            return self._emit_gather_load(a, amap, nm, out, indent)
         ta = self.targs[a.name]
-        st = self._dstrides(ta, amap)
+        if kind == "reshape":
+            vs = _view_strides(ta.shape, ta.strides, amap[2])
+            if vs is None:
+                return self._emit_reshape_load(a, amap, nm, vec_scope, out, indent)
+            ta = TensorArg(tuple(amap[2]), tuple(vs), ta.dtype, ta.align16)
+            amap = amap[1]
+        c0 = 0
+        if kind == "slice":
+            c0 = sum(int(b) * int(st) for b, st in zip(amap[2], ta.strides))
+        self._emit_affine_load(a, ta, self._dstrides(ta, amap), c0, None, nm, vec_scope, out, indent)
+
+    def _emit_affine_load(self, a, ta, st, c0, guard, nm, vec_scope, out, indent):
+        """Load ``a`` at element offset sum(i_d * st[d]) + c0 (c0 may be negative: wrap-around
+        index arithmetic, only evaluated where the true offset is in range); with ``guard`` (a
+        per-vector condition) the load is skipped and 0 is used where it is false."""
         ct, sty = _CTYPE[a.dtype], _STYPE[a.dtype]
         ptr = self._ptr(a, False)
         for d in range(self.nd):
             if st[d] and f"i{d}" not in self.idx_avail:
                 raise NotFusible(f"codegen: index i{d} not available for load of {a.name}")
-        off = " + ".join(f"(({self.IT})i{d} * {st[d]}u)" for d in range(self.nd) if st[d]) or "0"
+        terms = [f"(({self.IT})i{d} * {st[d]}u)" for d in range(self.nd) if st[d]]
+        if c0:
+            terms.append(f"({self.IT})({c0}ll)")
+        off = " + ".join(terms) or "0"
         if not vec_scope:
+            assert guard is None
             out.append(f"{indent}const {ct} {nm} = {_load_conv(a.dtype, f'{ptr}[{off}]')};")
             return
         V = self.vec
         last = self.nd - 1
         sl = st[last] if self.nd else 0
+        zero = _lit(0, ct)
         if sl == 0:
-            out.append(f"{indent}const {ct} {nm}_s = {_load_conv(a.dtype, f'{ptr}[{off}]')};")
+            ld = _load_conv(a.dtype, f'{ptr}[{off}]')
+            out.append(f"{indent}const {ct} {nm}_s = {f'({guard}) ? {ld} : {zero}' if guard else ld};")
             out.append(f"{indent}{ct} {nm}[{V}];")
             out.append(f"{indent}#pragma unroll")
             out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {nm}_s;")
             return
-        vec_ok = V > 1 and sl == 1 and ta.align16 and all(st[d] % V == 0 for d in range(last)) and \
-            (a.dtype.itemsize * V <= 16 or ta.align16)
+        vec_ok = V > 1 and sl == 1 and ta.align16 and all(st[d] % V == 0 for d in range(last)) and c0 % V == 0
         out.append(f"{indent}{ct} {nm}[{V}];")
+        if guard:
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {zero};")
+            out.append(f"{indent}if ({guard})")
         if vec_ok:
             vt = self._vtype(sty, V)
             out.append(f"{indent}{{ const {vt} t = *(const {vt}*)({ptr} + ({off}));")
             out.append(f"{indent}#pragma unroll")
             out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, 't[j]')}; }}")
         else:
+            out.append(f"{indent}{{")
             out.append(f"{indent}#pragma unroll")
-            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, f'{ptr}[({off}) + ({self.IT})j * {sl}u]')};")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, f'{ptr}[({off}) + ({self.IT})j * {sl}u]')}; }}")
+
+    def _emit_cat_load(self, a, amap, nm, out, indent):
+        """One piece of a concatenation.  When every vector lies inside one piece (the cat dim is
+        not the innermost, or the piece bounds are multiples of VEC) the piece is read with the
+        usual vector load under a per-vector range guard; otherwise an element-wise conditional load."""
+        _, base, dim, lo = amap
+        ta = self.targs[a.name]
+        d, n = base[dim], int(a.shape[dim])
+        last = self.nd - 1
+        if d is None:
+            raise NotFusible("codegen: cat dim not in the domain")
+        if d == last and (lo % self.vec or n % self.vec):
+            los = tuple(lo if i == dim else 0 for i in range(a.ndim))
+            return self._emit_pad_load(a, ("pad", base, los, 0.0), nm, out, indent)
+        if f"i{d}" not in self.idx_avail:
+            raise NotFusible(f"codegen: index i{d} not available for cat load of {a.name}")
+        guard = (f"i{d} >= {lo}u && " if lo else "") + f"i{d} < {lo + n}u"
+        st = self._dstrides(ta, base)
+        c0 = -lo * int(ta.strides[dim]) if a.shape[dim] != 1 else 0
+        if a.shape[dim] == 1:  # a one-wide piece: its stride along the cat dim never applies
+            st[d] = 0
+        self._emit_affine_load(a, ta, st, c0, guard, nm, True, out, indent)
+
+    def _emit_gather_load(self, a, amap, nm, out, indent):
+        """Indirect load (``take`` / ``take_along_axis`` / ``embedding``): the gathered dim's index
+        comes from the index tensor's load of the same node (clamped into [0, size), negative
+        indices wrap once as in Python)."""
+        _, base, dim, idx_name, imap, size = amap
+        ta = self.targs[a.name]
+        inm = f"v_{idx_name}" if idx_name in self.producer else self.load_names[(idx_name, imap)]
+        st = self._dstrides(ta, base)
+        sg = int(ta.strides[dim])
+        ct = _CTYPE[a.dtype]
+        ptr = self._ptr(a, False)
+        V, last = self.vec, self.nd - 1
+        for dd in range(self.nd):
+            if st[dd] and f"i{dd}" not in self.idx_avail:
+                raise NotFusible(f"codegen: index i{dd} not available for gather of {a.name}")
+        off = " + ".join(f"((long long)i{dd} * {st[dd]}ll)" for dd in range(self.nd) if st[dd]) or "0ll"
+        clamp = (f"long long x = (long long){inm}[{{l}}]; x = x < 0 ? x + {size}ll : x; "
+                 f"x = x < 0 ? 0 : (x >= {size}ll ? {size - 1}ll : x);")
+        uniform = last not in [x for x in imap if x is not None]
+        sl = st[last] if self.nd else 0
+        vec_ok = uniform and V > 1 and sl == 1 and ta.align16 and sg % V == 0 and \
+            all(st[dd] % V == 0 for dd in range(last))
+        out.append(f"{indent}{ct} {nm}[{V}];")
+        if vec_ok:
+            vt = self._vtype(_STYPE[a.dtype], V)
+            out.append(f"{indent}{{ {clamp.format(l='0')}")
+            out.append(f"{indent}const {vt} t = *(const {vt}*)({ptr} + ({off}) + x * {sg}ll);")
+            out.append(f"{indent}#pragma unroll")
+            out.append(f"{indent}for (int j = 0; j < {V}; ++j) {nm}[j] = {_load_conv(a.dtype, 't[j]')}; }}")
+            return
+        out.append(f"{indent}#pragma unroll")
+        out.append(f"{indent}for (int j = 0; j < {V}; ++j) {{ {clamp.format(l='j')}")
+        out.append(f"{indent}  {nm}[j] = {_load_conv(a.dtype, f'{ptr}[({off}) + (long long)j * {sl}ll + x * {sg}ll]')}; }}")
+
+    def _emit_reshape_load(self, a, amap, nm, vec_scope, out, indent):
+        """Reshape of an input whose strides do not allow a view: per element, the row-major flat
+        index of the reshaped value is decomposed over the input's shape (constant divisors)."""
+        _, base, shape = amap
+        ta = self.targs[a.name]
+        ct = _CTYPE[a.dtype]
+        ptr = self._ptr(a, False)
+        V, last = self.vec, self.nd - 1
+        cst = _contig_strides(tuple(shape))
+        terms = []
+        for i, d in enumerate(base):
+            if d is None or shape[i] == 1:
+                continue
+            if f"i{d}" not in self.idx_avail:
+                raise NotFusible(f"codegen: index i{d} not available for reshape load of {a.name}")
+            lane = " + j" if (vec_scope and d == last) else ""
+            terms.append(f"((long long)i{d}{lane}) * {cst[i]}ll")
+        flat = " + ".join(terms) or "0ll"
+        acst = _contig_strides(tuple(ta.shape))
+        parts = []
+        for i, (n, sa) in enumerate(zip(ta.shape, ta.strides)):
+            if n == 1:
+                continue
+            parts.append(f"((f / {acst[i]}ll) % {n}ll) * {sa}ll")
+        offx = " + ".join(parts) or "0ll"
+        if not vec_scope:
+            out.append(f"{indent}const {ct} {nm} = [&] {{ const long long f = {flat}; "
+                       f"return {_load_conv(a.dtype, f'{ptr}[{offx}]')}; }}();")
+            return
+        out.append(f"{indent}{ct} {nm}[{V}];")
+        out.append(f"{indent}#pragma unroll")
+        out.append(f"{indent}for (int j = 0; j < {V}; ++j) {{ const long long f = {flat}; "
+                   f"{nm}[j] = {_load_conv(a.dtype, f'{ptr}[{offx}]')}; }}")
 
     def _out_strides(self, o):
         """Per-domain-dim strides of a (contiguous) output plus its guard dims."""
@@ -1080,8 +1412,8 @@ class _Gen:
         emitted: set = set()
         # referencing builds the load-name table lazily; pre-populate by a dry run over all nodes
         for k, b in enumerate(self.p.nodes):
-            for i, a in enumerate(b.args):
-                if isinstance(a, TensorProxy) and a.name not in self.producer:
+            for i, a in tensor_args(b):
+                if a.name not in self.producer:
                     self.ref(a, k, i, "j")
         self._emit_nodes({o.name for o in self.outputs}, "vec", emitted, body, ind)
         for o in self.outputs:
@@ -1111,8 +1443,8 @@ class _Gen:
         self.idx_avail = set()
         self.flat_index = f"((unsigned long long)rowc * {R}ull + (unsigned long long)c + (unsigned long long)j)"
         for k, b in enumerate(self.p.nodes):
-            for i, a in enumerate(b.args):
-                if isinstance(a, TensorProxy) and a.name not in self.producer:
+            for i, a in tensor_args(b):
+                if a.name not in self.producer:
                     self.ref(a, k, i, "j")
         body: list[str] = []
         body.append(f"  const unsigned lane = threadIdx.x % {T}u;")
@@ -1294,8 +1626,8 @@ class _Gen:
         col_outs = [o for o in self.outputs if o.name not in full_names]
         self.load_names, self.loaded, self.idx_avail = {}, set(), set()
         for kk, b in enumerate(self.p.nodes):
-            for i, a in enumerate(b.args):
-                if isinstance(a, TensorProxy) and a.name not in self.producer:
+            for i, a in tensor_args(b):
+                if a.name not in self.producer:
                     self.ref(a, kk, i, "j")
         accs = []
         for n, kk in enumerate(red_nodes):
@@ -1407,9 +1739,8 @@ class _Gen:
                 res.add(n)
                 return
             b = self.p.nodes[self.producer[n]]
-            for a in b.args:
-                if isinstance(a, TensorProxy):
-                    walk(a.name)
+            for _, a in tensor_args(b):
+                walk(a.name)
 
         walk(name)
         return res

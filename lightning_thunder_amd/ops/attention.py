@@ -34,6 +34,10 @@ register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_v
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                         ctypes.c_uint64, c_void_p, c_void_p])
+register_signature("lta_attn_bwd_ex3", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                        c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
+                                        ctypes.c_uint64, c_void_p, c_void_p, c_void_p])
 
 SUPPORTED_HEAD_DIMS = (64, 96, 128)  # the kernels' compile-time head dims
 # Other head dims up to 128 (multiples of 8) run zero-padded to the next kernel head dim, as the
@@ -105,6 +109,15 @@ def _qkv_in_place(q, k, v):
     return q, k, v, st
 
 
+def _grad_like(t):
+    """An empty [B, H, T, D] gradient for ``t``: [B, T, H, D] memory (transposed view) when ``t`` is a
+    head split of a token-major tensor (token stride > head stride), dense [B, H, T, D] otherwise."""
+    B, H, T, D = t.shape
+    if H > 1 and T > 1 and t.stride(2) > t.stride(1):
+        return torch.empty((B, T, H, D), device=t.device, dtype=t.dtype).transpose(1, 2)
+    return torch.empty((B, H, T, D), device=t.device, dtype=t.dtype)
+
+
 def _rows_ok(t) -> bool:
     """Head dim contiguous, 16-byte aligned rows: any [B, H, T] strides are read in place."""
     return t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
@@ -161,10 +174,10 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     B, Hq, T, D = q.shape
     Hkv, S = k.shape[1], k.shape[2]
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
-    # gradients are written dense [B, H, T, D] whatever the strides of q / k / v
-    dq = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)
-    dk = torch.empty((B, Hkv, S, D), device=q.device, dtype=q.dtype)
-    dv = torch.empty((B, Hkv, S, D), device=q.device, dtype=q.dtype)
+    # gradients take their operand's (head, token) order: heads split from a [B, T, H*D] projection
+    # get [B, T, H, D] gradients, so the transpose + reshape back to [B, T, H*D] is a view
+    dq, dk, dv = _grad_like(q), _grad_like(k), _grad_like(v)
+    gst = (ctypes.c_int64 * 9)(*dq.stride()[:3], *dk.stride()[:3], *dv.stride()[:3])
     delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
     st = (ctypes.c_int64 * 6)(*do.stride()[:3], *o.stride()[:3])
     mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
@@ -172,10 +185,11 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     if mask_grad:
         assert mask is not None and mask.dtype != torch.bool
         dmask = torch.empty((B, Hq, T, S), device=q.device, dtype=torch.float32)
-    rc = lib.lta_attn_bwd_ex2(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
+    rc = lib.lta_attn_bwd_ex3(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
                               ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
                               mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),
-                              int(offset) & (2 ** 64 - 1), ctypes.cast(qkv_st, c_void_p), stream_ptr(q.device))
+                              int(offset) & (2 ** 64 - 1), ctypes.cast(qkv_st, c_void_p), ctypes.cast(gst, c_void_p),
+                              stream_ptr(q.device))
     check(rc, "lta_attn_bwd")
     if not mask_grad:
         return dq, dk, dv

@@ -77,12 +77,23 @@ enum : int { kExMask = 1, kExDrop = 2, kExMaskGrad = 4 };
 // views into a fused qkv projection are read in place.  contiguous(): dense [B, H, T, D].
 struct QKVStrides {
   int64_t qb, qh, qt, kb, kh, kt, vb, vh, vt;
+  // backward only: dQ / dK / dV (batch, head, token) strides; the host lays the gradients out like
+  // their operands (e.g. [B, T, H, D] for heads split from a fused projection), so the usual
+  // transpose + reshape back to [B, T, H*D] that follows is a view instead of a copy
+  int64_t dqb, dqh, dqt, dkb, dkh, dkt, dvb, dvh, dvt;
   static QKVStrides contiguous(int Hq, int Hkv, int Tq, int Sk, int D) {
-    return {(int64_t)Hq * Tq * D, (int64_t)Tq * D, D, (int64_t)Hkv * Sk * D, (int64_t)Sk * D, D,
-            (int64_t)Hkv * Sk * D, (int64_t)Sk * D, D};
+    const int64_t q[3] = {(int64_t)Hq * Tq * D, (int64_t)Tq * D, D}, k[3] = {(int64_t)Hkv * Sk * D, (int64_t)Sk * D, D};
+    return {q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2], q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2]};
   }
   static QKVStrides from(const int64_t* s, int Hq, int Hkv, int Tq, int Sk, int D) {
-    return s ? QKVStrides{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]} : contiguous(Hq, Hkv, Tq, Sk, D);
+    QKVStrides r = contiguous(Hq, Hkv, Tq, Sk, D);
+    if (s) r = QKVStrides{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], r.dqb, r.dqh, r.dqt,
+                          r.dkb, r.dkh, r.dkt, r.dvb, r.dvh, r.dvt};
+    return r;
+  }
+  void set_grad(const int64_t* g) {  // optional int64[9]: dQ, dK, dV (batch, head, token) strides
+    if (!g) return;
+    dqb = g[0], dqh = g[1], dqt = g[2], dkb = g[3], dkh = g[4], dkt = g[5], dvb = g[6], dvh = g[7], dvt = g[8];
   }
   bool is_contiguous(int Hq, int Hkv, int Tq, int Sk, int D) const {
     const QKVStrides c = contiguous(Hq, Hkv, Tq, Sk, D);

@@ -262,8 +262,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
 
   // dK^T / dV^T: element i of tile dt is d = dt*32 + acc_row(i,h), key = this lane's key
   if (key < Sk) {
-    T* dkrow = dK + (((int64_t)b * Hkv + hk) * Sk + key) * D;
-    T* dvrow = dV + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+    T* dkrow = dK + (int64_t)b * ex.sx.dkb + (int64_t)hk * ex.sx.dkh + (int64_t)key * ex.sx.dkt;
+    T* dvrow = dV + (int64_t)b * ex.sx.dvb + (int64_t)hk * ex.sx.dvh + (int64_t)key * ex.sx.dvt;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -600,8 +600,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* 
   for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[dt]), "+a"(dvacc[dt]));
 
   if (key < Sk) {
-    T* dkrow = dK + (((int64_t)b * Hkv + hk) * Sk + key) * D;
-    T* dvrow = dV + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+    T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
+    T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -875,8 +875,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 32 * j + r;
     if (key < Sk) {
-      T* dkrow = dK + (((int64_t)b * Hkv + hk) * Sk + key) * D;
-      T* dvrow = dV + (((int64_t)b * Hkv + hk) * Sk + key) * D;
+      T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
+      T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   }
 
   if (qi < Tq) {
-    T* drow = dQ + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+    T* drow = dQ + (int64_t)b * ex.sx.dqb + (int64_t)hq * ex.sx.dqh + (int64_t)qi * ex.sx.dqt;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -1227,7 +1227,7 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
   }
 
   if (qi < Tq) {
-    T* drow = dQ + (((int64_t)b * Hq + hq) * Tq + qi) * D;
+    T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
 #pragma unroll
@@ -1351,11 +1351,13 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
 // dmask (optional, needs mask): fp32 [B][Hq][Tq][Sk] receives dS, the additive mask's gradient
 // before the reduction over its broadcast dims.
 // qkv_strides: optional int64[9] = (batch, head, token) strides of Q, K, V (as lta_attn_fwd_ex2)
-LTA_EXPORT int lta_attn_bwd_ex2(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+// grad_strides: optional int64[9] = dQ, dK, dV (batch, head, token) element strides (head dim
+// contiguous, rows 16-byte aligned); null = dense [B, H, T, D] gradients.
+LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
                                 const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
                                 int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
                                 int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
-                                const int64_t* qkv_strides, hipStream_t stream) {
+                                const int64_t* qkv_strides, const int64_t* grad_strides, hipStream_t stream) {
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f || (dmask && !mask)) return -2;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
@@ -1366,6 +1368,7 @@ LTA_EXPORT int lta_attn_bwd_ex2(int dtype, const void* dO, const void* Q, const 
   }();
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
+  ex.sx.set_grad(grad_strides);
   int exf = 0;
   if (mask) {
     const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
@@ -1401,6 +1404,15 @@ LTA_EXPORT int lta_attn_bwd_ex2(int dtype, const void* dO, const void* Q, const 
   }
 #undef LTA_B
   return -1;
+}
+
+LTA_EXPORT int lta_attn_bwd_ex2(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                                const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
+                                int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
+                                int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
+                                const int64_t* qkv_strides, hipStream_t stream) {
+  return lta_attn_bwd_ex3(dtype, dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, D, scale, causal, strides,
+                          mask, mask_b, mask_h, dmask, dropout_p, seed, offset, qkv_strides, nullptr, stream);
 }
 
 LTA_EXPORT int lta_attn_bwd_ex(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,

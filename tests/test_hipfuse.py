@@ -97,7 +97,61 @@ CASES = {
 CASES["pad_sum"] = (_split_grad_pad, lambda dt, d: tuple(torch.randn(4, 16, 64, device=d, dtype=dt) for _ in range(3)))
 CASES["transpose_mix"] = (_transpose_mix, lambda dt, d: (torch.randn(96, 160, device=d, dtype=dt),
                                                           torch.randn(160, 96, device=d, dtype=dt)))
+
+
+# shape / index ops on region inputs: affine (slice, viewable reshape), piecewise (cat) and
+# indirect (index_select / gather / embedding) loads
+def _slice_mix(x):
+    n = x.shape[-1] // 3
+    q, k, v = x[..., :n], x[..., n:2 * n], x[..., 2 * n:]
+    return q * torch.sigmoid(k) + v[..., ::1] * x[..., ::3]
+
+
+def _cat_mix(a, b, c):
+    # last-dim cat with VEC-aligned pieces, a misaligned (5 + 11) last-dim cat, a leading-dim cat
+    y = torch.cat([a, b], dim=-1) * 2.0 + c
+    z = torch.cat([c[..., :5], c[..., 5:16]], -1)
+    w = torch.cat([a, b, a], dim=0)
+    return y, z.tanh() + 1.0, w * 3.0
+
+
+def _gather_mix(w, idx, x, gidx):
+    e = torch.index_select(w, 0, idx) + 1.0
+    g = torch.gather(x, 1, gidx) * 2.0
+    h = torch.index_select(w, 0, torch.minimum(idx + 1, torch.full_like(idx, 99))) * 0.5  # an in-region index
+    return e.sin(), g.exp(), h.cos()
+
+
+def _embed_add(ids, wte, wpe):
+    pos = torch.arange(ids.shape[1], device=ids.device)
+    return (torch.nn.functional.embedding(ids, wte) + torch.nn.functional.embedding(pos, wpe)) * 0.5
+
+
+def _reshape_ext(x, yt):
+    # a viewable (contiguous) reshape and a copy-requiring one (``yt`` is a transposed input) of inputs
+    return x.reshape(8, 4, 24) * yt.reshape(8, 4, 24) + 1.0, (x.reshape(16, 48) - yt.reshape(16, 48)).abs()
+
+
+def _cat_inputs(dt, d):
+    return (torch.randn(6, 32, 64, device=d, dtype=dt), torch.randn(6, 32, 64, device=d, dtype=dt),
+            torch.randn(6, 32, 128, device=d, dtype=dt))
+
+
+def _gather_inputs(dt, d):
+    return (torch.randn(100, 48, device=d, dtype=dt), torch.randint(0, 100, (37,), device=d),
+            torch.randn(16, 40, device=d, dtype=dt), torch.randint(0, 40, (16, 24), device=d))
+
+
+CASES["slice_mix"] = (_slice_mix, lambda dt, d: (torch.randn(4, 32, 3 * 96, device=d, dtype=dt),))
+CASES["cat_mix"] = (_cat_mix, _cat_inputs)
+CASES["gather_mix"] = (_gather_mix, _gather_inputs)
+CASES["embed_add"] = (_embed_add, lambda dt, d: (torch.randint(0, 500, (4, 64), device=d),
+                                                 torch.randn(500, 128, device=d, dtype=dt),
+                                                 torch.randn(64, 128, device=d, dtype=dt)))
+CASES["reshape_ext"] = (_reshape_ext, lambda dt, d: (torch.randn(32, 24, device=d, dtype=dt),
+                                                      torch.randn(24, 32, device=d, dtype=dt).t()))
 _COLUMN_CASES = ("bias_grad", "ln_dgamma_dbeta", "col_amax_epilogue", "full_and_col")
+_SHAPE_CASES = ("slice_mix", "cat_mix", "gather_mix", "embed_add", "reshape_ext")
 
 
 @pytest.fixture
@@ -138,6 +192,30 @@ def test_column_reductions_fused_cpu(case, cpu_fusion):
         p.name: cg.TensorArg(tuple(p.shape), tuple(torch.empty(tuple(p.shape)).stride()), p.dtype, True)
         for p in f.inputs if isinstance(p, TensorProxy)})
     assert ks.extra and ks.ws_bytes > 0 and ks.mode.startswith("col")
+
+
+@pytest.mark.parametrize("case", _SHAPE_CASES)
+def test_shape_ops_fused_cpu(case, cpu_fusion):
+    """Slices, concatenations, index_select / gather / embedding lookups and reshapes of region
+    inputs are index maps of the fused kernel (affine, piecewise or indirect loads): none of them
+    is left to ATen as a separate gather / copy kernel."""
+    fn, mk = CASES[case]
+    jf = thunder.jit(fn, executors=["hipfuse", "torch"])
+    jf(*mk(torch.float32, "cpu"))
+    tr = thunder.last_traces(jf)[-1]
+    fus = hipfuse.fusions(tr)
+    assert fus
+    left = [b.sym.name for b in tr.bound_symbols if not b.sym.is_fusion]
+    for name in ("cat", "take", "take_along_axis", "embedding", "embedding_prim", "reshape"):
+        assert name not in left and name + "_prim" not in left, (case, left)
+    kinds = set()
+    for fb in fus:
+        f = fb._call_ctx[fb.sym.name]
+        for am in f.plan.arg_maps:
+            kinds |= {cg._kind(m) for m in am.values()}
+    want = {"slice_mix": "slice", "cat_mix": "cat", "gather_mix": "gather", "embed_add": "gather",
+            "reshape_ext": "reshape"}[case]
+    assert want in kinds, kinds
 
 
 def test_single_region_for_norm_chain(cpu_fusion):
