@@ -53,6 +53,9 @@ def parse_args():
                    help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling), MXFP8 blocks, "
                         "or mxfp4 (MXFP4 forward GEMMs, MXFP8 backward)")
     p.add_argument("--hipgraph", action="store_true")
+    p.add_argument("--optim-overlap", default="auto", choices=["auto", "on", "off"],
+                   help="issue the fused AdamW update of each parameter bucket on a side stream inside the "
+                        "backward (auto: on for 1-process thunder runs without hipGraphs)")
     p.add_argument("--lora", type=int, default=0, metavar="R",
                    help="LoRA fine-tuning of every transformer linear at rank R (base weights frozen; reference "
                         "benchmark_peft.py); not the pretraining headline")
@@ -169,6 +172,11 @@ def run(args, rank, world, device, mode):
             fwd = DistributedDataParallel(model, device_ids=[device.index])
         params = list(model.parameters())
     opt = make_optimizer(params, mode)
+    overlap = args.optim_overlap == "on" or (args.optim_overlap == "auto" and world == 1 and not _force_dist())
+    if mode == "thunder" and overlap and not args.hipgraph and hasattr(opt, "overlap_with_backward"):
+        # the update still runs inside the timed step: in the backward's shadow, joined by opt.step()
+        opt.overlap_with_backward(fwd)
+        args.overlap_used = True
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
 
@@ -297,7 +305,8 @@ def main():
                 "seq_len": args.seq,
                 "parallelism": f"{parallel}{world}" if world > 1 else "single",
                 "mode": args.mode + (f"+lora-r{args.lora}" if args.lora else ""),
-                "optimizer": "AdamW",
+                "optimizer": "AdamW" + (" (fused, update issued inside the backward on a side stream)"
+                                        if getattr(args, "overlap_used", False) else ""),
             },
             "tokens_per_sec_per_gpu": round(per_gpu, 2),
             "model_tflops_per_gpu": round(tflops, 1),

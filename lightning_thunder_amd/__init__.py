@@ -87,6 +87,7 @@ class CacheEntry:
         self.computation_fn = None
         self.forward_fn = None
         self.backward_fn = None
+        self.overlap_optimizer = None  # transforms/optimizer_overlap.py
         self.epilogue_writes = []
         self.param_accessors = []
         self.constants = []
@@ -147,6 +148,17 @@ def _check_traces(traces, cd):
 
 
 from .core.functionalization import storage_alias_pattern  # noqa: E402
+
+
+def _overlap_allowed(cd: CompileData) -> bool:
+    """Optimizer-in-backward hooks: single process only, and not inside captured hipGraphs."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return False
+    from .transforms.hipgraph import HipGraphTransform
+
+    return not any(isinstance(t, HipGraphTransform) for t in cd.transforms)
 
 
 def _post_transforms(cd: CompileData) -> list:
@@ -263,6 +275,14 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
 
                 fw = schedule_allgathers(fw, int(window))
                 bw = schedule_allgathers(bw, int(window))
+            opt = getattr(cd, "overlap_optimizer", None)
+            if opt is not None and _overlap_allowed(cd):
+                from .transforms.optimizer_overlap import insert_grad_ready_hooks
+
+                names = [comp.args[i].name if isinstance(comp.args[i], TensorProxy) else None
+                         for i in fb.grad_input_indices]
+                bw = insert_grad_ready_hooks(bw, names, getattr(cd, "overlap_bucket_bytes", 128 << 20), fw=fw)
+                entry.overlap_optimizer = opt
             fw = del_last_used(fw)
             bw = del_last_used(bw)
             bw.unpack_list_arg = True

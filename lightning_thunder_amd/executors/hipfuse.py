@@ -426,12 +426,33 @@ def _schedule_segment(seg: list, used_outside: set | None = None) -> list:
         raise ValueError(f"fusion_type must be 'dataflow' or 'consecutive', got {fusion_type!r}")
     consecutive = fusion_type == "consecutive"
 
+    def feeds_region(i, depth=6) -> bool:
+        """A source (no tensor inputs: an RNG draw, a ``full``) joins the open region when a fusible
+        consumer within a few hops also reads the region's values (e.g. the dropout mask of a
+        dropout backward whose gradient the region produces)."""
+        if any(isinstance(a, TensorProxy) for a in seg[i].flat_proxy_args):
+            return False
+        frontier, seen = [i], {i}
+        for _ in range(depth):
+            nxt = []
+            for j in frontier:
+                for u in users[j]:
+                    if u in seen or not fusible[u]:
+                        continue
+                    seen.add(u)
+                    if any(a.name in names for a in seg[u].flat_proxy_args):
+                        return True
+                    nxt.append(u)
+            frontier = nxt
+        return False
+
     while ready:
         pick = None
         if plan is not None:
             for i in (sorted(ready)[:1] if consecutive else sorted(ready)):
                 if fusible[i] and (_connected(names, ins, seg[i]) or _external_view(names, seg[i]) or
-                                   any(d in in_group or _connected(names, ins, seg[d]) for d in lazy_deps[i])) \
+                                   any(d in in_group or _connected(names, ins, seg[d]) for d in lazy_deps[i]) or
+                                   (not consecutive and feeds_region(i))) \
                         and try_admit(i):
                     pick = i
                     break

@@ -819,7 +819,7 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
     body = _canonical_names(body)
     from ..core.rng import PHILOX_HIP
 
-    src = _PREAMBLE + (PHILOX_HIP if "philox_uniform(" in body else "") + body
+    src = _PREAMBLE + (PHILOX_HIP if ("philox_uniform(" in body or "philox4(" in body) else "") + body
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
     name = f"{kernel_prefix}_{h}"
     src = src.replace("__KERNEL_NAME__", name)
@@ -850,6 +850,7 @@ class _Gen:
                 self.producer[o.name] = k
         self.lines: list[str] = []
         self.typedefs: dict[str, str] = {}
+        self.flat_base4 = None  # flat index of vector lane 0 when it is a multiple of 4 (pointwise mode)
 
     # --- analysis ---------------------------------------------------------------------------
     def _reduced_dims(self):
@@ -1108,6 +1109,9 @@ class _Gen:
             if b.sym.id in REDUCTIONS:
                 continue
             vec_scope = scope == "vec" and self.dep.get(b.flat_outs[0].name, True)
+            if vec_scope and b.sym.id == PrimIDs.UNIFORM_PHILOX and self.flat_base4 and self.vec % 4 == 0:
+                self._emit_philox_vec(b, out, indent)
+                continue
             self._materialize_loads(b, k, vec_scope, out, indent)
             exprs = self._expr(b, k, "j" if vec_scope else "")
             for name, e in exprs:
@@ -1118,6 +1122,26 @@ class _Gen:
                     out.append(f"{indent}for (int j = 0; j < {self.vec}; ++j) v_{name}[j] = {e};")
                 else:
                     out.append(f"{indent}const {ct} r_{name} = {e};")
+
+    def _emit_philox_vec(self, b, out, indent):
+        """A vector of uniforms from whole Philox blocks: the lane group's flat index is a multiple
+        of 4 (``flat_base4``), so lanes 4q..4q+3 take the 4 words of one block (core/rng.py)."""
+        o = b.output
+        ct = _CTYPE[o.dtype]
+        seed = self._scalar_ref(b.kwargs["seed"], "double")
+        off = self._scalar_ref(b.kwargs["offset"], "double")
+        lo, hi = float(pyval(b.args[1])), float(pyval(b.args[2]))
+        V = self.vec
+        out.append(f"{indent}{ct} v_{o.name}[{V}];")
+        out.append(f"{indent}#pragma unroll")
+        out.append(f"{indent}for (int q = 0; q < {V // 4}; ++q) {{ unsigned w[4];")
+        out.append(f"{indent}  philox4((unsigned)(unsigned long long)({seed}), (unsigned long long)({off}), "
+                   f"((unsigned long long)({self.flat_base4}) >> 2) + (unsigned long long)q, w);")
+        u = "philox_u24(w[i])"
+        if lo != 0.0 or hi != 1.0:
+            u = f"({u} * {_lit(hi - lo, 'float')} + {_lit(lo, 'float')})"
+        out.append(f"{indent}  #pragma unroll")
+        out.append(f"{indent}  for (int i = 0; i < 4; ++i) v_{o.name}[4 * q + i] = {_rnd(o.dtype, f'({ct})({u})')}; }}")
 
     def _load_dep(self, amap) -> bool:
         if self.force_scalar:
@@ -1408,6 +1432,7 @@ class _Gen:
         body.append(f"  for ({IT} v = ({IT})blockIdx.x * {block}u + threadIdx.x; v < {nvec}u; v += ({IT})gridDim.x * {block}u) {{")
         body.append(f"{ind}const {IT} e = v * {V}u;")
         self.flat_index = "((unsigned long long)e + (unsigned long long)j)"
+        self.flat_base4 = "e" if V % 4 == 0 else None
         self._decompose("e", list(range(self.nd)), body, ind)
         emitted: set = set()
         # referencing builds the load-name table lazily; pre-populate by a dry run over all nodes

@@ -19,6 +19,7 @@ class ThunderFunction(torch.autograd.Function):
 
         flat_out, out_spec = tree_flatten(out)
         ctx.entry = entry
+        ctx.overlap_params = getattr(entry, "_overlap_params", None)
         ctx.saved = list(saved_tensors) + list(saved_other)
         ctx.n_inputs = n_inputs
         tensor_outs = []
@@ -67,15 +68,30 @@ class ThunderFunction(torch.autograd.Function):
                 shape, dtype, device = outs_meta[i]
                 cts[i] = torch.zeros(shape, dtype=dtype, device=device)
         args.extend(cts)
-        in_grads = entry.backward_fn(args)
+        handled: set = set()
+        if ctx.overlap_params:
+            # the optimizer updates these parameters inside the backward (optimizer_overlap.py)
+            from ..transforms.optimizer_overlap import active
+
+            with active(entry.overlap_optimizer, ctx.overlap_params, handled):
+                in_grads = entry.backward_fn(args)
+        else:
+            in_grads = entry.backward_fn(args)
         result = [None] * ctx.n_inputs
-        for idx, g in zip(entry.grad_input_indices, in_grads):
-            result[idx] = g
+        for k, (idx, g) in enumerate(zip(entry.grad_input_indices, in_grads)):
+            result[idx] = None if k in handled else g
         return (None, None, *result)
 
 
 def connect_to_autograd(entry, flat_inputs):
+    entry._overlap_params = None
+    opt = entry.overlap_optimizer
+    if opt is not None:
+        # backward output k -> the parameter tensor the attached optimizer updates in the backward
+        entry._overlap_params = {k: flat_inputs[i] for k, i in enumerate(entry.grad_input_indices)
+                                 if opt.manages(flat_inputs[i])} or None
     outs = ThunderFunction.apply(entry, len(flat_inputs), *flat_inputs)
+    entry._overlap_params = None
     from ..core.pytree import tree_unflatten
 
     flat_out = list(entry._last_flat_out)

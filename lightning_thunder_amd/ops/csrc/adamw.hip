@@ -31,10 +31,14 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
   p = p - (lr / bc1) * (m / denom);
 }
 
-template <typename TP, typename TS>
-__global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
-                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
-                                                    float bc2_sqrt, float grad_scale) {
+// U = 16-byte vectors per lane in flight per operand.  The default (U = 4) streams at full HBM
+// rate on an idle GPU.  The lean variant (U = 1, <= 80 VGPRs, 6 waves/SIMD) is for the update
+// issued on a side stream during the backward: its waves fit next to a 4-wave gemm4 workgroup
+// (168 VGPR + 256 AGPR per wave), so the optimizer streams HBM while the GEMM keeps the MFMAs busy.
+template <typename TP, typename TS, int U>
+__device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
+                                           float lr, float b1, float b2, float eps, float wd, float bc1,
+                                           float bc2_sqrt, float grad_scale) {
   const int2 ck = chunks[blockIdx.x];
   const TensorMeta mt = metas[ck.x];
   const int64_t start = (int64_t)ck.y * kChunk;
@@ -48,7 +52,6 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
                    (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0);
   if (vec) {
     // U vectors per lane per trip, all loads issued before any math: 4U 16-B loads in flight per lane
-    constexpr int U = 4;
     for (int64_t i0 = start + (int64_t)threadIdx.x * VP; i0 < end; i0 += 256 * VP * U) {
       Vec16<TP> pv[U], gv[U];
       Vec16<TS> mv[U], vv[U];
@@ -91,17 +94,39 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
   }
 }
 
+template <typename TP, typename TS>
+__global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
+                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                    float bc2_sqrt, float grad_scale) {
+  adamw_body<TP, TS, 4>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+}
+
+template <typename TP, typename TS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void adamw_lean_kernel(
+    const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks, float lr, float b1, float b2, float eps,
+    float wd, float bc1, float bc2_sqrt, float grad_scale) {
+  adamw_body<TP, TS, 1>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+}
+
 }  // namespace
 
 LTA_EXPORT int lta_adamw_chunk_size() { return kChunk; }
 
 // metas: device array of TensorMeta; chunks: device int2 array {tensor, chunk index}
-LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr, float b1,
-                         float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, hipStream_t stream) {
+// lean = 1: the register-capped variant (see adamw_body) for updates overlapped with compute
+LTA_EXPORT int lta_adamw_ex(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr,
+                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, int lean,
+                            hipStream_t stream) {
   dim3 grid(n_chunks), block(256);
-#define LTA_L(TPt, TSt)                                                                                           \
-  hipLaunchKernelGGL((adamw_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas, (const int2*)chunks, \
-                     lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale)
+#define LTA_L(TPt, TSt)                                                                                              \
+  do {                                                                                                               \
+    if (lean)                                                                                                        \
+      hipLaunchKernelGGL((adamw_lean_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,            \
+                         (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
+    else                                                                                                             \
+      hipLaunchKernelGGL((adamw_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,                 \
+                         (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
+  } while (0)
   if (pdtype == kBF16 && sdtype == kBF16) LTA_L(__hip_bfloat16, __hip_bfloat16);
   else if (pdtype == kBF16 && sdtype == kF32) LTA_L(__hip_bfloat16, float);
   else if (pdtype == kF16 && sdtype == kF16) LTA_L(__half, __half);
@@ -110,4 +135,10 @@ LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* 
   else return -1;
 #undef LTA_L
   return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr, float b1,
+                         float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, hipStream_t stream) {
+  return lta_adamw_ex(pdtype, sdtype, metas, chunks, n_chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale, 0,
+                      stream);
 }

@@ -5,6 +5,11 @@
 match ``torch.optim.AdamW`` (decoupled weight decay, bias correction); moments are kept
 in the parameter dtype by default (like torch's fused AdamW) or in fp32 with
 ``state_dtype=torch.float32``.  Falls back to torch's implementation for CPU tensors.
+
+``overlap_with_backward(jitted_model)`` moves the update into the compiled backward: each bucket
+of parameters is updated on a side stream as soon as its gradients are final and the backward no
+longer reads the parameters (``transforms/optimizer_overlap.py``); ``step()`` then joins that
+stream and updates only what the backward did not.
 """
 from __future__ import annotations
 
@@ -19,6 +24,52 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self.state_dtype = state_dtype
         self._chunk_cache: dict = {}
+        self._managed: dict = {}  # id(param) -> param group (overlap mode)
+        self._side: dict = {}  # device -> side stream of the overlapped updates
+        self._inflight: list = []  # metadata tensors read by queued side-stream launches
+
+    # --- update overlapped with the backward (transforms/optimizer_overlap.py) ----------------------
+    def overlap_with_backward(self, jitted, bucket_mb: int = 128) -> None:
+        """Update parameters inside ``jitted``'s compiled backward (call before its first forward).
+        Every backward must then be followed by ``step()`` (no gradient accumulation / clipping)."""
+        from .transforms.optimizer_overlap import overlap_with_backward
+
+        self._managed = {id(p): g for g in self.param_groups for p in g["params"]}
+        overlap_with_backward(jitted, self, bucket_mb)
+
+    def manages(self, t) -> bool:
+        return isinstance(t, torch.Tensor) and t.is_cuda and id(t) in self._managed
+
+    @torch.no_grad()
+    def overlapped_update(self, params, grads) -> None:
+        """Called from the backward: update ``params`` with ``grads`` on the side stream, ordered
+        after everything the compute stream has queued so far."""
+        dev = params[0].device
+        side = self._side.get(dev)
+        if side is None:
+            # high priority: a stream of its own priority class gets its own hardware queue (a
+            # normal-priority side stream can share the compute stream's queue and never overlap)
+            side = self._side[dev] = torch.cuda.Stream(device=dev, priority=-1)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        buckets: dict = {}
+        with torch.cuda.stream(side):
+            for p, g in zip(params, grads):
+                group = self._managed[id(p)]
+                st = self._state(p)
+                st["step"] += 1
+                key = (id(group), p.dtype, st["exp_avg"].dtype, st["step"])
+                buckets.setdefault(key, (group, []))[1].append((p, g))
+            for (_, pdt, sdt, step), (group, pg) in buckets.items():
+                lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+                self._fused([p for p, _ in pg], pdt, sdt, dev, step, lr, b1, b2, eps, wd,
+                            grads=[g for _, g in pg], lean=True)
+        for g in grads:
+            g.record_stream(side)  # the compute stream may free the gradient before the update ran
+
+    def _join(self):
+        for dev, side in self._side.items():
+            torch.cuda.current_stream(dev).wait_stream(side)
+        self._inflight.clear()
 
     def _state(self, p):
         st = self.state[p]
@@ -35,6 +86,7 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._join()
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             buckets: dict = {}
@@ -62,18 +114,21 @@ class AdamW(torch.optim.Optimizer):
         denom = (st["exp_avg_sq"].sqrt() / math.sqrt(bc2)).add_(eps)
         p.addcdiv_(st["exp_avg"].to(p.dtype), denom.to(p.dtype), value=-lr / bc1)
 
-    def _fused(self, ps, pdt, sdt, dev, step, lr, b1, b2, eps, wd):
+    def _fused(self, ps, pdt, sdt, dev, step, lr, b1, b2, eps, wd, grads=None, lean=False):
         from .ops._lib import require, DTYPE_CODE, stream_ptr, check, register_signature, c_int, c_void_p, c_float
 
         lib = require()
-        register_signature("lta_adamw", [c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
-                                         c_float, c_float, c_float, c_float, c_void_p])
+        register_signature("lta_adamw_ex", [c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
+                                            c_float, c_float, c_float, c_float, c_int, c_void_p])
         metas = []
-        for p in ps:
+        keep = []
+        for i, p in enumerate(ps):
             st = self.state[p]
-            g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+            g = p.grad if grads is None else grads[i]
+            g = g if g.is_contiguous() else g.contiguous()
             if g.dtype != p.dtype:
                 g = g.to(p.dtype)
+            keep.append(g)
             metas += [p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()]
         meta_t = torch.tensor(metas, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         key = (dev, tuple(p.numel() for p in ps))
@@ -91,8 +146,10 @@ class AdamW(torch.optim.Optimizer):
             self._chunk_cache[key] = chunks
         bc1 = 1 - b1 ** step
         bc2_sqrt = math.sqrt(1 - b2 ** step)
-        rc = lib.lta_adamw(DTYPE_CODE[pdt], DTYPE_CODE[sdt], meta_t.data_ptr(), chunks.data_ptr(), chunks.shape[0], lr, b1,
-                           b2, eps, wd, bc1, bc2_sqrt, 1.0, stream_ptr(dev))
+        rc = lib.lta_adamw_ex(DTYPE_CODE[pdt], DTYPE_CODE[sdt], meta_t.data_ptr(), chunks.data_ptr(), chunks.shape[0], lr,
+                              b1, b2, eps, wd, bc1, bc2_sqrt, 1.0, int(lean), stream_ptr(dev))
         check(rc, "lta_adamw")
-        # keep the metadata alive until the kernel has consumed it
+        # keep the metadata (and converted gradients) alive until the kernel has consumed them
         self._last_meta = meta_t
+        if lean:
+            self._inflight.append((meta_t, keep))

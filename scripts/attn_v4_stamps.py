@@ -16,7 +16,7 @@ for causal in (False, True):
     for _ in range(3):
         o, lse = attn_fwd(q, k, v, causal)
     torch.cuda.synchronize()
-    st = lse.view(torch.int64)[:4 * 64 * 6].view(4, 64, 6).cpu()
+    st = lse.reshape(-1).view(torch.int64)[:4 * 64 * 6].view(4, 64, 6).cpu()
     names = ["Ph1 QK_A", "Ph2 PV_B", "Ph3 QK_B", "Ph4 PV_A", "wait+bar"]
     print("causal" if causal else "full")
     for w in range(4):

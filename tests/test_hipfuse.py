@@ -119,7 +119,7 @@ def _gather_mix(w, idx, x, gidx):
     e = torch.index_select(w, 0, idx) + 1.0
     g = torch.gather(x, 1, gidx) * 2.0
     h = torch.index_select(w, 0, torch.minimum(idx + 1, torch.full_like(idx, 99))) * 0.5  # an in-region index
-    return e.sin(), g.exp(), h.cos()
+    return e.sin(), g.tanh(), h.cos()
 
 
 def _embed_add(ids, wte, wpe):
@@ -392,7 +392,22 @@ def test_philox_dropout_mask_recomputed(cpu_fusion):
 
 
 def test_philox_torch_matches_reference_vectors():
-    from lightning_thunder_amd.core.rng import philox_uniform_torch
+    from lightning_thunder_amd.core.rng import philox_uniform_torch, philox4x32
+
+    # Random123 known-answer vectors for philox4x32_R(10)
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = philox4x32(*[torch.tensor([c], dtype=torch.int64) for c in ctr], *key)
+        assert tuple(int(g) for g in got) == want
+    # element e = word e % 4 of block e // 4
+    u4 = philox_uniform_torch((8,), 77, 5, "cpu")
+    for blk in range(2):
+        words = philox4x32(torch.tensor([blk]), torch.tensor([0]), torch.tensor([5]), torch.tensor([0]), 77, 0)
+        for i, w in enumerate(words):
+            assert u4[4 * blk + i].item() == (int(w) >> 8) / 16777216.0
 
     u = philox_uniform_torch((8,), 1234, 0, "cpu")
     assert ((u >= 0) & (u < 1)).all()
@@ -403,14 +418,15 @@ def test_philox_torch_matches_reference_vectors():
 
 
 @pytest.mark.gpu
-def test_philox_dropout_gpu_matches_torch_philox():
+@pytest.mark.parametrize("shape", [(256, 384), (33, 7)])  # whole-block vector draws / per-element draws
+def test_philox_dropout_gpu_matches_torch_philox(shape):
     from lightning_thunder_amd.core import rng
     from lightning_thunder_amd.core.rng import philox_uniform_torch
 
     def f(x):
         return torch.nn.functional.dropout(torch.tanh(x), p=0.25, training=True)
 
-    x = torch.randn(256, 384, device="cuda", requires_grad=True)
+    x = torch.randn(*shape, device="cuda", requires_grad=True)
     jf = thunder.jit(f)
     torch.manual_seed(123)
     rng._state["seed"] = None  # restart the counter for this seed
