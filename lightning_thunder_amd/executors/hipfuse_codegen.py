@@ -1183,6 +1183,22 @@ class _Gen:
         ct = _CTYPE[a.dtype]
         ptr = self._ptr(a, False)
         V, last = self.vec, self.nd - 1
+        if V > 1 and all(lo[i] % V == 0 and a.shape[i] % V == 0 for i, d in enumerate(base) if d == last):
+            # every vector lies wholly inside or outside the input: one range test per vector and
+            # the usual (16-byte when aligned) load at a shifted offset
+            conds, st, c0 = [], [0] * self.nd, 0
+            for i, d in enumerate(base):
+                if d is None:
+                    continue
+                if f"i{d}" not in self.idx_avail:
+                    raise NotFusible(f"codegen: index i{d} not available for pad load of {a.name}")
+                n = int(a.shape[i])
+                if lo[i] != 0 or n != self.D[d]:
+                    conds.append((f"i{d} >= {lo[i]}u && " if lo[i] else "") + f"i{d} < {lo[i] + n}u")
+                if n != 1:
+                    st[d] += ta.strides[i]
+                    c0 -= lo[i] * ta.strides[i]
+            return self._emit_affine_load(a, ta, st, c0, " && ".join(conds) or None, nm, True, out, indent, fill=pv)
         conds, terms = [], []
         for i, d in enumerate(base):
             if d is None:  # a size-1 output dim: index 0, in range
@@ -1222,7 +1238,7 @@ class _Gen:
             c0 = sum(int(b) * int(st) for b, st in zip(amap[2], ta.strides))
         self._emit_affine_load(a, ta, self._dstrides(ta, amap), c0, None, nm, vec_scope, out, indent)
 
-    def _emit_affine_load(self, a, ta, st, c0, guard, nm, vec_scope, out, indent):
+    def _emit_affine_load(self, a, ta, st, c0, guard, nm, vec_scope, out, indent, fill=0):
         """Load ``a`` at element offset sum(i_d * st[d]) + c0 (c0 may be negative: wrap-around
         index arithmetic, only evaluated where the true offset is in range); with ``guard`` (a
         per-vector condition) the load is skipped and 0 is used where it is false."""
@@ -1242,7 +1258,7 @@ class _Gen:
         V = self.vec
         last = self.nd - 1
         sl = st[last] if self.nd else 0
-        zero = _lit(0, ct)
+        zero = _lit(fill, ct)
         if sl == 0:
             ld = _load_conv(a.dtype, f'{ptr}[{off}]')
             out.append(f"{indent}const {ct} {nm}_s = {f'({guard}) ? {ld} : {zero}' if guard else ld};")
@@ -1727,16 +1743,29 @@ class _Gen:
         self._scope_id = "fin"
         self.idx_avail = set()
         fin: list[str] = []
-        fin.append(f"  const {IT} e = ({IT})blockIdx.x * 256u + threadIdx.x;")
-        fin.append(f"  if (e >= {C}u) return;")
+        # 4 waves per 64 columns: wave w sums splits w, w+4, ... (a 4x shorter serial chain), then
+        # the 4 partial sums are combined in a fixed order (deterministic)
+        fin.append(f"  const unsigned part = threadIdx.x >> 6, cl = threadIdx.x & 63u;")
+        fin.append(f"  const {IT} e0 = ({IT})blockIdx.x * 64u + cl;")
+        fin.append(f"  const bool ok = e0 < {C}u;")
+        fin.append(f"  const {IT} e = ok ? e0 : 0u;")
+        for (n, kk, act, init, comb), off in zip(accs, offs):
+            fin.append(f"  const {act}* ws{n} = (const {act}*)((const char*)A.ws + {off}ull);")
+            fin.append(f"  {act} t{n} = {init};")
+            fin.append(f"  for (unsigned s = part; s < {S}u; s += 4u) t{n} = {cf(comb, act, f't{n}', f'ws{n}[({IT})s * {C}u + e]')};")
+            fin.append(f"  __shared__ {act} sf{n}[4][64];")
+            fin.append(f"  sf{n}[part][cl] = t{n};")
+        fin.append("  __syncthreads();")
+        fin.append("  if (part != 0u || !ok) return;")
         self._decompose("e", list(range(k, nd)), fin, "  ")
         done: set = set()
         for (n, kk, act, init, comb), off in zip(accs, offs):
             b = self.p.nodes[kk]
             o = b.output
-            fin.append(f"  const {act}* ws{n} = (const {act}*)((const char*)A.ws + {off}ull);")
-            fin.append(f"  {act} t{n} = ws{n}[e];")
-            fin.append(f"  for (unsigned s = 1; s < {S}u; ++s) t{n} = {cf(comb, act, f't{n}', f'ws{n}[({IT})s * {C}u + e]')};")
+            tot = f"sf{n}[0][cl]"
+            for w in range(1, 4):
+                tot = cf(comb, act, tot, f"sf{n}[{w}][cl]")
+            fin.append(f"  t{n} = {tot};")
             out_ct = _CTYPE[o.dtype]
             fin.append(f"  const {out_ct} r_{o.name} = {_rnd(o.dtype, f'({out_ct})(t{n})')};")
             done.add(o.name)
@@ -1748,7 +1777,7 @@ class _Gen:
         self.force_scalar = False
         fin_src = "\n".join([f'extern "C" __global__ void __launch_bounds__(256) __KERNEL_NAME___fin(Args A) {{'] + fin
                             + ["}"]) + "\n"
-        self.extra = [("_fin", ((C + 255) // 256, 1, 1), (256, 1, 1))]
+        self.extra = [("_fin", ((C + 63) // 64, 1, 1), (256, 1, 1))]
         self.ws_bytes = ws_off
         return main + fin_src, (ncs, S, 1), (256, 1, 1), V, f"col(S={S})"
 
