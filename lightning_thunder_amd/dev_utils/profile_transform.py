@@ -20,35 +20,7 @@ from ..core.transform_common import Transform
 from ._insert import host_call, SKIP
 
 
-def _range_push(name):
-    if torch.cuda.is_available():
-        torch.cuda.nvtx.range_push(name)
-
-
-def _range_pop():
-    if torch.cuda.is_available():
-        torch.cuda.nvtx.range_pop()
-
-
-class RoctxProfileTransform(Transform):
-    def transform_trace_post_optimization(self, trace, **kwargs):
-        new = from_trace(trace)
-        out = []
-        for b in trace.bound_symbols:
-            if b.sym.name in SKIP:
-                out.append(b)
-                continue
-            label = b.sym.name
-            out.append(host_call("roctx_push", lambda _l=label: _range_push(_l)))
-            out.append(b)
-            out.append(host_call("roctx_pop", _range_pop))
-        new.bound_symbols = out
-        new.scopes = [new.bound_symbols]
-        new.set_provenance(TraceProvenance("roctx ranges"))
-        return new
-
-
-NvtxProfileTransform = RoctxProfileTransform
+from .nvtx_profile_transform import RoctxProfileTransform, NvtxProfileTransform, _range_push, _range_pop  # noqa: F401
 
 
 class ProfileTransform(Transform):

@@ -114,23 +114,4 @@ def make_trace_dot(trace: TraceCtx, show_metadata: bool = False) -> str:
     return "\n".join(lines)
 
 
-def get_alloc_memory(trace: TraceCtx) -> tuple[int, dict[str, int]]:
-    """Peak bytes of live tensors while executing ``trace`` (reference memory_calculation.py):
-    walks the bound symbols, adding outputs and releasing tensors at their ``del``."""
-    from ..core.proxies import TensorProxy
-
-    live: dict[str, int] = {}
-    for a in trace.args:
-        if isinstance(a, TensorProxy):
-            live[a.name] = a.numel * a.dtype.itemsize if isinstance(a.numel, int) else 0
-    peak = sum(live.values())
-    for b in trace.bound_symbols:
-        if b.sym.name == "python_del":
-            for p in b.flat_proxy_args:
-                live.pop(p.name, None)
-            continue
-        for o in b.flat_proxy_outs:
-            if isinstance(o, TensorProxy) and o.name not in live:
-                live[o.name] = int(o.numel) * o.dtype.itemsize
-        peak = max(peak, sum(live.values()))
-    return peak, live
+from .memory_calculation import get_alloc_memory  # noqa: E402

@@ -33,19 +33,7 @@ from ..core.trace import from_trace, TraceProvenance
 
 _tls = threading.local()
 
-# bound symbols whose output may alias their first input (a parameter read through a view must
-# count as a read of the parameter)
-_VIEW_IDS = {PrimIDs.TRANSPOSE, PrimIDs.RESHAPE, PrimIDs.BROADCAST_IN_DIM, PrimIDs.SQUEEZE, PrimIDs.SLICE}
-_VIEW_NAMES = ("transpose", "reshape", "view", "expand", "broadcast", "squeeze", "unsqueeze", "slice", "permute",
-               "t", "getitem", "split", "chunk", "as_strided", "narrow", "flatten")
-
-
-def _is_view(b) -> bool:
-    if b.sym.id in _VIEW_IDS or OpTags.SHAPE_OP in (b.sym.tags or ()):
-        return True
-    nm = str(b.sym.name)
-    base = nm[:-5] if nm.endswith("_prim") else nm
-    return base in _VIEW_NAMES
+from ..examine.memory_calculation import is_view_bsym as _is_view  # noqa: E402
 
 
 def view_aliases(trace, alias_of: dict | None = None) -> dict:

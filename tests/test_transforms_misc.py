@@ -396,10 +396,16 @@ def test_reference_module_paths():
     from lightning_thunder_amd.dev_utils.nvtx_profile_transform import NvtxProfileTransform
     from lightning_thunder_amd.examine.memory_calculation import get_alloc_memory
 
-    jf = thunder.jit(lambda x: (x * 2).sin(), transforms=[NvtxProfileTransform()])
+    jf = thunder.jit(lambda x: (x * 2).sin(), transforms=[NvtxProfileTransform(include_shapes=True)])
     jf(torch.ones(4))
     peak, _ = get_alloc_memory(thunder.last_traces(jf)[-1])
     assert peak > 0
+    # views share their source's storage; a freed intermediate is not counted twice
+    jg = thunder.jit(lambda x: x.reshape(-1).t().sin(), executors=["torch"])
+    jg(torch.ones(64, 32))
+    peak, live, tl = get_alloc_memory(thunder.last_traces(jg)[-1], timeline=True)
+    assert peak == 2 * 64 * 32 * 4, (peak, tl)
+    assert tl and all(isinstance(n, str) and m >= 0 for n, m in tl)
 
 
 def test_fp8_training_recipes_parse():
