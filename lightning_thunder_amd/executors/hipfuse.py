@@ -515,14 +515,23 @@ def _fusion_pass(trace):
                 outside |= u
         items.extend(_schedule_segment(s_, outside))
 
+    from ..common import get_compile_option
+
+    remat_names = {}
+    if get_compile_option("fusion_type", "hipfuse partitioner mode", "dataflow") != "consecutive" and \
+            get_compile_option("hipfuse_rematerialize", "recompute cheap producer cones of values passed between "
+                               "hipfuse regions instead of materialising them (default True)", True):
+        remat_names = _rematerialize_between_regions(items)
     lazy_names = set(_LAZY)
     # consumers outside each group decide region outputs
     use_count: dict[str, list] = {}
     for idx, it in enumerate(items):
         bs = it[1] if isinstance(it, tuple) else [it]
+        inside = remat_names.get(idx, ())  # recomputed here: these reads are internal to the region
         for b in bs:
             for a in b.flat_proxy_args:
-                use_count.setdefault(a.name, []).append(idx)
+                if a.name not in inside:
+                    use_count.setdefault(a.name, []).append(idx)
     new_bsyms: list = []
     for idx, it in enumerate(items):
         if not isinstance(it, tuple):
@@ -547,7 +556,7 @@ def _fusion_pass(trace):
         for b in group:
             if is_ext_view(b):
                 o = b.flat_proxy_outs[0].name
-                if any(u != idx for u in use_count.get(o, [])):
+                if any(u != idx for u in use_count.get(o, [])) and o not in remat_names.get(idx, ()):
                     need.add(o)
         for b in reversed(group):
             if is_ext_view(b) and b.flat_proxy_outs[0].name in need:
@@ -575,6 +584,7 @@ def _fusion_pass(trace):
                 produced.append(o)
                 pset.add(o.name)
         outputs = [o for o in produced if o.name not in pre_names and o.name not in lazy_names
+                   and o.name not in remat_names.get(idx, ())
                    and any(u != idx for u in use_count.get(o.name, []))]
         seen = set()
         inputs = []
@@ -596,6 +606,87 @@ def _fusion_pass(trace):
     new.scopes = [new.bound_symbols]
     new.set_provenance(TraceProvenance("Fusion (hipfuse)"))
     return new
+
+
+def _tensor_bytes(p) -> int:
+    n = p.numel
+    return int(n) * p.dtype.itemsize if isinstance(n, int) else 0
+
+
+def _rematerialize_between_regions(items: list) -> dict:
+    """Fusion-region rematerialisation (reference: ``thunder/core/rematerialization.py:239-407``,
+    the min-cut between adjacent nvFuser regions).  When a region reads a value X that an earlier
+    region produces only for it, and X's producer cone inside the earlier region (elementwise /
+    view / gather prims, no reduction) reads fewer bytes than X's HBM round trip (write + read),
+    the cone is recomputed inside the consumer and X is never materialised.  Returns, per item
+    index, the names the consumer recomputes (they must not become its outputs: their original
+    region still defines them for any other user)."""
+    remat: dict[int, set] = {}
+    group_pos = [i for i, it in enumerate(items) if isinstance(it, tuple)]
+    if len(group_pos) < 2:
+        return remat
+    producer_item: dict[str, int] = {}
+    uses: dict[str, set] = {}
+    for idx, it in enumerate(items):
+        bs = it[1] if isinstance(it, tuple) else [it]
+        for b in bs:
+            for a in b.flat_proxy_args:
+                uses.setdefault(a.name, set()).add(idx)
+            for o in b.flat_proxy_outs:
+                producer_item.setdefault(o.name, idx)
+    cheap = cg.ELEMENTWISE | cg.VIEWS | cg.GATHERS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
+    for j in group_pos:
+        for _ in range(8):  # a few rounds: a recomputed cone can expose the next candidate
+            plan2, g2 = items[j]
+            made = {o.name for b in g2 for o in b.flat_proxy_outs}
+            ext, ext_names = [], set()
+            for b in g2:
+                for a in b.flat_proxy_args:
+                    if isinstance(a, TensorProxy) and a.name not in made and a.name not in ext_names:
+                        ext.append(a)
+                        ext_names.add(a.name)
+            done = False
+            for x in ext:
+                i = producer_item.get(x.name)
+                if i is None or i >= j or not isinstance(items[i], tuple) or uses.get(x.name, set()) - {i, j}:
+                    continue
+                g1 = items[i][1]
+                prod = {o.name: b for b in g1 for o in b.flat_proxy_outs}
+                cone, stack, seen = [], [x.name], set()
+                ok = True
+                while stack and ok:
+                    n = stack.pop()
+                    b = prod.get(n)
+                    if b is None or id(b) in seen:
+                        continue
+                    seen.add(id(b))
+                    if b.sym.id not in cheap:
+                        ok = False
+                        break
+                    cone.append(b)
+                    stack.extend(a.name for a in b.flat_proxy_args if isinstance(a, TensorProxy))
+                if not ok or not cone:
+                    continue
+                cone = [b for b in g1 if id(b) in seen]  # program order
+                cone_made = {o.name for b in cone for o in b.flat_proxy_outs}
+                reads = {a.name: a for b in cone for a in b.flat_proxy_args
+                         if isinstance(a, TensorProxy) and a.name not in cone_made}
+                extra = sum(_tensor_bytes(a) for n, a in reads.items() if n not in ext_names)
+                if extra >= 2 * _tensor_bytes(x):
+                    continue
+                trial = cg.Plan()
+                if not all(trial.try_add(b) for b in cone + list(g2)) or trial.has_pending():
+                    continue
+                items[j] = (trial, cone + list(g2))
+                remat.setdefault(j, set()).update(cone_made)
+                uses[x.name].discard(j)
+                for n in reads:
+                    uses.setdefault(n, set()).add(j)
+                done = True
+                break
+            if not done:
+                break
+    return remat
 
 
 def _replan(group):

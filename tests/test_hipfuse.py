@@ -142,6 +142,14 @@ def _gather_inputs(dt, d):
             torch.randn(16, 40, device=d, dtype=dt), torch.randint(0, 40, (16, 24), device=d))
 
 
+def _two_reductions(x):
+    # a column reduction and a row softmax-sum of the same elementwise value: two regions; the
+    # second recomputes tanh(x) * 3 from x instead of reading a materialised copy
+    a = torch.tanh(x) * 3.0
+    return a.sum(0), (a - a.amax(1, keepdim=True)).exp().sum(1)
+
+
+CASES["remat_regions"] = (_two_reductions, lambda dt, d: (torch.randn(256, 512, device=d, dtype=dt),))
 CASES["slice_mix"] = (_slice_mix, lambda dt, d: (torch.randn(4, 32, 3 * 96, device=d, dtype=dt),))
 CASES["cat_mix"] = (_cat_mix, _cat_inputs)
 CASES["gather_mix"] = (_gather_mix, _gather_inputs)
@@ -216,6 +224,21 @@ def test_shape_ops_fused_cpu(case, cpu_fusion):
     want = {"slice_mix": "slice", "cat_mix": "cat", "gather_mix": "gather", "embed_add": "gather",
             "reshape_ext": "reshape"}[case]
     assert want in kinds, kinds
+
+
+def test_region_rematerialization_cpu(cpu_fusion):
+    """Fusion-region rematerialisation (reference core/rematerialization.py:239-407): the value two
+    regions share is recomputed by the consumer from the cheaper producer input, never written."""
+    fn, mk = CASES["remat_regions"]
+    (x,) = mk(torch.float32, "cpu")
+    jf = thunder.jit(fn, executors=["hipfuse", "torch"])
+    for o, r in zip(jf(x), fn(x)):
+        torch.testing.assert_close(o, r)
+    fus = hipfuse.fusions(thunder.last_traces(jf)[-1])
+    assert len(fus) == 2
+    for fb in fus:
+        assert [a.name for a in fb.args] == [fus[0].args[0].name]  # both read only x
+        assert len(fb.output) == 1  # nothing intermediate is materialised
 
 
 def test_single_region_for_norm_chain(cpu_fusion):
