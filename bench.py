@@ -53,9 +53,10 @@ def parse_args():
                    help="FP8 scaling: per-tensor current, delayed (amax history, TE DelayedScaling), MXFP8 blocks, "
                         "or mxfp4 (MXFP4 forward GEMMs, MXFP8 backward)")
     p.add_argument("--hipgraph", action="store_true")
-    p.add_argument("--optim-overlap", default="auto", choices=["auto", "on", "off"],
+    p.add_argument("--optim-overlap", default="off", choices=["auto", "on", "off"],
                    help="issue the fused AdamW update of each parameter bucket on a side stream inside the "
-                        "backward (auto: on for 1-process thunder runs without hipGraphs)")
+                        "backward (auto: on for 1-process thunder runs without hipGraphs).  Off by default: "
+                        "measured no faster on 1x MI355X (profiles/optim_overlap_ab.txt)")
     p.add_argument("--lora", type=int, default=0, metavar="R",
                    help="LoRA fine-tuning of every transformer linear at rank R (base weights frozen; reference "
                         "benchmark_peft.py); not the pretraining headline")

@@ -900,6 +900,286 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* 
 }
 
 // ---------------------------------------------------------------------------------------------
+// dK / dV, D = 128 (v4): v3's data flow with the tile's VALU work moved into the MFMA shadows.
+// v3 runs S -> exp -> dP -> dS -> dV -> dK as dependent blocks, so at one wave per SIMD the
+// exponentials and dS (about 200 VALU per lane and tile) serialise against the MFMA pipe.  Here
+// the tile is four phases, each an MFMA chain with independent VALU interleaved (pinned with
+// sched_barrier, since hipcc otherwise gathers the VALU in front of or behind the chain):
+//   A: S = Q K^T (16 MFMA)      B: dP = dO V^T (16) | P = exp2(S c - LSE)
+//   C: dV^T += dO^T P (16) | dS = P (dP - delta), pack    D: dK^T += Q^T dS (16)
+// ---------------------------------------------------------------------------------------------
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                       const T* __restrict__ V, const T* __restrict__ dO,
+                                                                       const float* __restrict__ LSE,
+                                                                       const float* __restrict__ DELTA, T* __restrict__ dK,
+                                                                       T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
+                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
+  constexpr int D = 128;
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  constexpr int NST = 3;
+  constexpr int IMG = kQT * 256;
+  constexpr int STAGE = 2 * IMG + 256;
+  constexpr int VOFF = NST * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[VOFF + kKB3 * C::RSTR * 2];
+  short* Vs = reinterpret_cast<short*>(smem + VOFF);
+
+  const int kb = (int)blockIdx.y;
+  const int bh = blockIdx.x;
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int group = Hq / Hkv;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int kw = kb * kKB3 + wave * 64;  // this wave's first key; half j: keys kw + 32 j + r
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
+
+  // V rows of the workgroup's 256 keys -> LDS; K rows of this wave's 64 keys -> registers
+#pragma unroll
+  for (int c = 0; c < kKB3 * C::CH / kThreads; ++c) {
+    const int id = c * kThreads + tid;
+    const int row = id / C::CH, ch = id % C::CH;
+    const int vr = min(kb * kKB3 + row, Sk - 1);
+    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * sx.vt + ch * 8);
+  }
+  F kf[2][C::KS];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kr = min(kw + 32 * j + r, Sk - 1);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) kf[j][s] = load_frag<F>(Kb + (int64_t)kr * sx.kt + 16 * s + 8 * h);
+  }
+
+  f32x16 dkacc[2][C::DT], dvacc[2][C::DT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dkacc[j][dt][i] = 0.f;
+        dvacc[j][dt][i] = 0.f;
+      }
+
+  const int n_qt = (Tq + kQT - 1) / kQT;
+  const int qt_begin = CAUSAL ? min((kb * kKB3) / kQT, n_qt) : 0;
+  const int nq = n_qt - qt_begin;
+  const int total = group * nq;
+
+  float plse = 0.f, pdel = 0.f;
+  auto stash_stats = [&](int st) {
+    if (wave == 0 && lane < kQT) {
+      float* sp = reinterpret_cast<float*>(smem + st * STAGE + 2 * IMG);
+      sp[lane] = plse;
+      sp[kQT + lane] = pdel;
+    }
+  };
+  auto issue = [&](int hi, int ti, int st) {
+    const int hq = hk * group + hi;
+    const int qbase = (qt_begin + ti) * kQT;
+    const T* Qb = Q + b * sx.qb + hq * sx.qh;
+    const T* dOb = dO + b * sdo.b + hq * sdo.h;
+    char* qimg = smem + st * STAGE;
+    if (wave == 0) {
+      const int64_t srow = ((int64_t)b * Hq + hq) * Tq + min(qbase + (lane & 31), Tq - 1);
+      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off"
+                   : "=&v"(plse), "=&v"(pdel)
+                   : "v"(LSE + srow), "v"(DELTA + srow)
+                   : "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = wave * 2 + i;
+      const int u = 64 * k + lane;
+      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
+      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
+      const int qc = min(qbase + row, Tq - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * sx.qt + ch * 8),
+                                       (lds_void*)(qimg + k * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
+                                       (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
+    }
+  };
+  auto wait_all_but_newest = [&]() { asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory"); };
+
+  int nhi = 0, nti = 0;
+  auto advance = [&]() {
+    if (++nti == nq) {
+      nti = 0;
+      ++nhi;
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V staging loads
+  if (total > 0) {
+    issue(nhi, nti, 0);
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(plse), "+v"(pdel)::"memory");
+    stash_stats(0);
+  }
+  if (total > 1) {
+    issue(nhi, nti, 1);
+    advance();
+    wait_all_but_newest();
+    stash_stats(1);
+  }
+  __syncthreads();
+
+  unsigned tr_a, tr_b;
+  {
+    const int l16 = lane & 15, g = lane >> 4;
+    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
+    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
+  }
+  constexpr float kLog2e = 1.44269504088896340736f;
+  int ti = 0, st = 0;
+  for (int it = 0; it < total; ++it) {
+    const bool issue_next = it + 2 < total;
+    const int st2 = st >= 1 ? st - 1 : 2;
+    if (issue_next) issue(nhi, nti, st2);
+    const int qt_abs = qt_begin + ti;
+    const int qbase = qt_abs * kQT;
+    {
+      const char* qimg = smem + st * STAGE;
+      const char* oimg = qimg + IMG;
+      const float* sl = reinterpret_cast<const float*>(qimg + 2 * IMG);
+      // row statistics of this query tile (LSE, delta): plain LDS loads, waited on at first use
+      f32x4v L[4], Dl[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        L[a] = *reinterpret_cast<const f32x4v*>(sl + 4 * h + 8 * a);
+        Dl[a] = *reinterpret_cast<const f32x4v*>(sl + kQT + 4 * h + 8 * a);
+      }
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sacc[j][i] = 0.f;
+          pacc[j][i] = 0.f;
+        }
+      // phase A: S = Q K^T for both halves (nothing of this tile is ready to overlap yet)
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const F qa = load_frag<F>(qimg + du_off(r, 2 * s + h));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sacc[j] = mfma(qa, kf[j][s], sacc[j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // phase B: dP = dO V^T, with P = exp2(S c - LSE log2 e) in the MFMAs' shadow: slice s of the
+      // exponentials (4 of the 32 per lane) follows the two MFMAs of k-step s
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const F oa = load_frag<F>(oimg + du_off(r, 2 * s + h));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          pacc[j] = mfma(oa, load_frag<F>(Vs + (wave * 64 + 32 * j + r) * C::RSTR + 16 * s + 8 * h), pacc[j]);
+        const int j = s >> 2, i0 = 4 * (s & 3);
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i)
+          sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, -L[i >> 2][i & 3] * kLog2e));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int key = kw + 32 * j + r;
+        const bool masked = (CAUSAL && kw + 32 * j + 31 > qbase) || kw + 32 * j + 32 > Sk || qbase + kQT > Tq;
+        if (masked) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qq = qbase + acc_row(i, h);
+            if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) sacc[j][i] = 0.f;
+          }
+        }
+      }
+      F pf[2][2], df[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        pack_frag(pf[j][0], sacc[j], 0);
+        pack_frag(pf[j][1], sacc[j], 1);
+      }
+      {
+        F xt[8];
+        tr_frags8(xt, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T
+        // phase C: dV^T += dO^T P, with dS = P (dP - delta) and its packing in the MFMAs' shadow
+#pragma unroll
+        for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            mfma_acc_agpr(dvacc[j][dt], xt[2 * dt], pf[j][0]);
+            mfma_acc_agpr(dvacc[j][dt], xt[2 * dt + 1], pf[j][1]);
+            const int jj = dt >> 1, i0 = 8 * (dt & 1) + 4 * j;
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) pacc[jj][i] = sacc[jj][i] * (pacc[jj][i] - Dl[i >> 2][i & 3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (dt & 1) {  // half dt>>1 of dS complete: pack it
+            pack_frag(df[dt >> 1][0], pacc[dt >> 1], 0);
+            pack_frag(df[dt >> 1][1], pacc[dt >> 1], 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // Q^T
+        // phase D: dK^T += Q^T dS
+#pragma unroll
+        for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            mfma_acc_agpr(dkacc[j][dt], xt[2 * dt], df[j][0]);
+            mfma_acc_agpr(dkacc[j][dt], xt[2 * dt + 1], df[j][1]);
+          }
+      }
+    }
+    if (issue_next) {
+      advance();
+      wait_all_but_newest();
+      stash_stats(st2);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    ti = ti + 1 == nq ? 0 : ti + 1;
+    st = st == 2 ? 0 : st + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[j][dt]), "+a"(dvacc[j][dt]));
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 32 * j + r;
+    if (key < Sk) {
+      T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
+      T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int d = dt * 32 + 8 * a + 4 * h;
+          union {
+            T v[4];
+            uint2 u;
+          } pk, pv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            pk.v[e] = from_f32<T>(dkacc[j][dt][4 * a + e] * scale);
+            pv.v[e] = from_f32<T>(dvacc[j][dt][4 * a + e]);
+          }
+          *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
+          *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // dQ
 // ---------------------------------------------------------------------------------------------
 constexpr int kBM = 128;
@@ -1269,7 +1549,7 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DQ
 }
 
-int g_dkdv_v3 = 1;  // dK/dV kernel for D = 128 without mask / dropout: 1 = v3 (64 keys per wave), 0 = v2
+int g_dkdv_v3 = 1;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
 int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
@@ -1300,14 +1580,17 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
   if (D == 128 && dkdv_v2 && g_dkdv_v3 && Tq > 0 && Sk > 0) {
     dim3 g4(B * Hkv, (Sk + kKB3 - 1) / kKB3);
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dkdv_v3_kernel<T, true>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo, ex.sx);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_v3_kernel<T, false>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo, ex.sx);
+#define LTA_DKDV3(KERN, CA)                                                                                          \
+  hipLaunchKernelGGL((KERN<T, CA>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V, (const T*)dO,              \
+                     (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx)
+    if (g_dkdv_v3 == 2) {
+      if (causal) LTA_DKDV3(attn_bwd_dkdv_v4_kernel, true);
+      else LTA_DKDV3(attn_bwd_dkdv_v4_kernel, false);
+    } else {
+      if (causal) LTA_DKDV3(attn_bwd_dkdv_v3_kernel, true);
+      else LTA_DKDV3(attn_bwd_dkdv_v3_kernel, false);
+    }
+#undef LTA_DKDV3
   } else if (D == 128 && dkdv_v2) {
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
@@ -1446,9 +1729,9 @@ LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
   return old;
 }
 
-// dK/dV kernel selection (A/B measurement hook): 1 = v3, 0 = v2; returns the previous choice
+// dK/dV kernel selection (A/B measurement hook): 2 = v4, 1 = v3, 0 = v2; returns the previous choice
 LTA_EXPORT int lta_attn_bwd_set_dkdv_impl(int impl) {
   const int old = g_dkdv_v3;
-  if (impl == 0 || impl == 1) g_dkdv_v3 = impl;
+  if (impl >= 0 && impl <= 2) g_dkdv_v3 = impl;
   return old;
 }
