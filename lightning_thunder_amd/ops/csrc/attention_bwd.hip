@@ -1046,13 +1046,11 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
       const char* qimg = smem + st * STAGE;
       const char* oimg = qimg + IMG;
       const float* sl = reinterpret_cast<const float*>(qimg + 2 * IMG);
-      // row statistics of this query tile (LSE, delta): plain LDS loads, waited on at first use
+      // row statistics of this query tile: LSE now (phase B), delta after phase B (phase C), so the
+      // two are never live together; plain LDS loads, waited on at first use
       f32x4v L[4], Dl[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        L[a] = *reinterpret_cast<const f32x4v*>(sl + 4 * h + 8 * a);
-        Dl[a] = *reinterpret_cast<const f32x4v*>(sl + kQT + 4 * h + 8 * a);
-      }
+      for (int a = 0; a < 4; ++a) L[a] = *reinterpret_cast<const f32x4v*>(sl + 4 * h + 8 * a);
       f32x16 sacc[2], pacc[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -1061,28 +1059,47 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           sacc[j][i] = 0.f;
           pacc[j][i] = 0.f;
         }
-      // phase A: S = Q K^T for both halves (nothing of this tile is ready to overlap yet)
+      // phase A: S = Q K^T for both halves (nothing of this tile is ready to overlap yet); all 8 Q
+      // fragments are read up front so the MFMA chain never waits on one LDS read at a time
+      {
+        F qa[C::KS];
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F qa = load_frag<F>(qimg + du_off(r, 2 * s + h));
+        for (int s = 0; s < C::KS; ++s) qa[s] = load_frag<F>(qimg + du_off(r, 2 * s + h));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) sacc[j] = mfma(qa, kf[j][s], sacc[j]);
+        for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) sacc[j] = mfma(qa[s], kf[j][s], sacc[j]);
       }
       __builtin_amdgcn_sched_barrier(0);
       // phase B: dP = dO V^T, with P = exp2(S c - LSE log2 e) in the MFMAs' shadow: slice s of the
-      // exponentials (4 of the 32 per lane) follows the two MFMAs of k-step s
+      // exponentials (4 of the 32 per lane) follows the two MFMAs of k-step s, whose operands were
+      // read one slice earlier
+      {
+        F oa = load_frag<F>(oimg + du_off(r, h));
+        F va0 = load_frag<F>(Vs + (wave * 64 + r) * C::RSTR + 8 * h);
+        F va1 = load_frag<F>(Vs + (wave * 64 + 32 + r) * C::RSTR + 8 * h);
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F oa = load_frag<F>(oimg + du_off(r, 2 * s + h));
+        for (int s = 0; s < C::KS; ++s) {
+          F ob = oa, vb0 = va0, vb1 = va1;
+          if (s + 1 < C::KS) {
+            ob = load_frag<F>(oimg + du_off(r, 2 * (s + 1) + h));
+            vb0 = load_frag<F>(Vs + (wave * 64 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
+            vb1 = load_frag<F>(Vs + (wave * 64 + 32 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
+          }
+          pacc[0] = mfma(oa, va0, pacc[0]);
+          pacc[1] = mfma(oa, va1, pacc[1]);
+          const int j = s >> 2, i0 = 4 * (s & 3);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          pacc[j] = mfma(oa, load_frag<F>(Vs + (wave * 64 + 32 * j + r) * C::RSTR + 16 * s + 8 * h), pacc[j]);
-        const int j = s >> 2, i0 = 4 * (s & 3);
-#pragma unroll
-        for (int i = i0; i < i0 + 4; ++i)
-          sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, -L[i >> 2][i & 3] * kLog2e));
-        __builtin_amdgcn_sched_barrier(0);
+          for (int i = i0; i < i0 + 4; ++i)
+            sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, -L[i >> 2][i & 3] * kLog2e));
+          __builtin_amdgcn_sched_barrier(0);
+          oa = ob;
+          va0 = vb0;
+          va1 = vb1;
+        }
       }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) Dl[a] = *reinterpret_cast<const f32x4v*>(sl + kQT + 4 * h + 8 * a);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int key = kw + 32 * j + r;
@@ -1549,7 +1566,7 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DQ
 }
 
-int g_dkdv_v3 = 1;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
+int g_dkdv_v3 = 2;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
 int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
