@@ -346,6 +346,44 @@ __device__ __forceinline__ void tr_frags8(f16x8 (&f)[8], unsigned ba, unsigned b
   for (int i = 0; i < 8; ++i) f[i] = __builtin_bit_cast(f16x8, t[i]);
 }
 
+// tr_frags8 in two halves: issue the 16 transposed reads (no wait) and, later, wait and assemble.
+// Between the two, LDS reads the compiler issues are still waited for correctly (LDS returns in
+// order, so a compiler lgkmcnt(N) only gets stricter); nothing may read `x` before tr_wait16.
+typedef short s16x4t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void tr_issue16(s16x4t (&x)[16], unsigned ba, unsigned bb) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
+      "ds_read_b64_tr_b16 %2, %16 offset:4096\n\tds_read_b64_tr_b16 %3, %17 offset:4096\n\t"
+      "ds_read_b64_tr_b16 %4, %16 offset:512\n\tds_read_b64_tr_b16 %5, %17 offset:512\n\t"
+      "ds_read_b64_tr_b16 %6, %16 offset:4608\n\tds_read_b64_tr_b16 %7, %17 offset:4608\n\t"
+      "ds_read_b64_tr_b16 %8, %16 offset:1024\n\tds_read_b64_tr_b16 %9, %17 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %10, %16 offset:5120\n\tds_read_b64_tr_b16 %11, %17 offset:5120\n\t"
+      "ds_read_b64_tr_b16 %12, %16 offset:1536\n\tds_read_b64_tr_b16 %13, %17 offset:1536\n\t"
+      "ds_read_b64_tr_b16 %14, %16 offset:5632\n\tds_read_b64_tr_b16 %15, %17 offset:5632"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7]),
+        "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11]), "=&v"(x[12]), "=&v"(x[13]), "=&v"(x[14]), "=&v"(x[15])
+      : "v"(ba), "v"(bb)
+      : "memory");
+}
+template <typename F>
+__device__ __forceinline__ void tr_wait16(F (&f)[8], s16x4t (&x)[16]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                 "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+               :
+               : "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    union {
+      struct { s16x4t a, b; } s;
+      F f;
+    } u;
+    u.s.a = x[2 * i];
+    u.s.b = x[2 * i + 1];
+    f[i] = u.f;
+  }
+}
+
 // dK^T / dV^T accumulate in the accumulator (AGPR) file through inline-asm MFMAs: they are only
 // ever MFMA C/D operands, and pinning them there leaves the 256 architectural VGPRs to K, the S / dP
 // tiles and their softmax (hipcc otherwise parks S / dP in AGPRs and copies them out every tile).
@@ -972,7 +1010,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   auto stash_stats = [&](int st) {
     if (wave == 0 && lane < kQT) {
       float* sp = reinterpret_cast<float*>(smem + st * STAGE + 2 * IMG);
-      sp[lane] = plse;
+      sp[lane] = -plse * 1.44269504088896340736f;  // stored as -LSE log2 e: exp2(S c + this) = P
       sp[kQT + lane] = pdel;
     }
   };
@@ -1052,6 +1090,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
 #pragma unroll
       for (int a = 0; a < 4; ++a) L[a] = *reinterpret_cast<const f32x4v*>(sl + 4 * h + 8 * a);
       f32x16 sacc[2], pacc[2];
+      F pf[2][2], df[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1091,7 +1130,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           const int j = s >> 2, i0 = 4 * (s & 3);
 #pragma unroll
           for (int i = i0; i < i0 + 4; ++i)
-            sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, -L[i >> 2][i & 3] * kLog2e));
+            sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, L[i >> 2][i & 3]));
+          if (s == 4 || s == 5) pack_frag(pf[0][s - 4], sacc[0], s - 4);  // half 0 is complete (unmasked form)
           __builtin_amdgcn_sched_barrier(0);
           oa = ob;
           va0 = vb0;
@@ -1100,6 +1140,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
       }
 #pragma unroll
       for (int a = 0; a < 4; ++a) Dl[a] = *reinterpret_cast<const f32x4v*>(sl + kQT + 4 * h + 8 * a);
+      s16x4t xr[16];
+      tr_issue16(xr, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T, waited below
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int key = kw + 32 * j + r;
@@ -1110,17 +1152,17 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
             const int qq = qbase + acc_row(i, h);
             if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) sacc[j][i] = 0.f;
           }
+          if (j == 0) {  // re-pack the masked half 0
+            pack_frag(pf[0][0], sacc[0], 0);
+            pack_frag(pf[0][1], sacc[0], 1);
+          }
         }
       }
-      F pf[2][2], df[2][2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        pack_frag(pf[j][0], sacc[j], 0);
-        pack_frag(pf[j][1], sacc[j], 1);
-      }
+      pack_frag(pf[1][0], sacc[1], 0);
+      pack_frag(pf[1][1], sacc[1], 1);
       {
         F xt[8];
-        tr_frags8(xt, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T
+        tr_wait16(xt, xr);
         // phase C: dV^T += dO^T P, with dS = P (dP - delta) and its packing in the MFMAs' shadow
 #pragma unroll
         for (int dt = 0; dt < C::DT; ++dt) {
@@ -1131,15 +1173,19 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
             const int jj = dt >> 1, i0 = 8 * (dt & 1) + 4 * j;
 #pragma unroll
             for (int i = i0; i < i0 + 4; ++i) pacc[jj][i] = sacc[jj][i] * (pacc[jj][i] - Dl[i >> 2][i & 3]);
+            // sched_barrier does not hold IR-level sinking: pin the slice here, not at the pack below
+            asm volatile("" : "+v"(pacc[jj]));
             __builtin_amdgcn_sched_barrier(0);
           }
           if (dt & 1) {  // half dt>>1 of dS complete: pack it
             pack_frag(df[dt >> 1][0], pacc[dt >> 1], 0);
             pack_frag(df[dt >> 1][1], pacc[dt >> 1], 1);
+            // half 0's S / dP registers are free now: Q^T's transposed reads (phase D) go out here
+            if (dt == 1) tr_issue16(xr, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // Q^T
+        tr_wait16(xt, xr);  // Q^T
         // phase D: dK^T += Q^T dS
 #pragma unroll
         for (int dt = 0; dt < C::DT; ++dt)
@@ -1478,12 +1524,34 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
           sacc[kt][i] = 0.f;
           pacc[kt][i] = 0.f;
         }
+      // the 4 K / V fragments of k-step s+1 are read while k-step s's MFMAs run (one LDS latency
+      // per tile instead of one per MFMA pair)
+      F kc[2], vc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        kc[kt] = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 8 * h);
+        vc[kt] = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 8 * h);
+      }
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) {
+        F kn[2] = {kc[0], kc[1]}, vn[2] = {vc[0], vc[1]};
+        if (s + 1 < C::KS) {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            kn[kt] = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
+            vn[kt] = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
+          }
+        }
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          sacc[kt] = mfma(load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h), qf[s], sacc[kt]);  // S^T
-          pacc[kt] = mfma(load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h), of[s], pacc[kt]);  // dP^T
+          sacc[kt] = mfma(kc[kt], qf[s], sacc[kt]);  // S^T
+          pacc[kt] = mfma(vc[kt], of[s], pacc[kt]);  // dP^T
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          kc[kt] = kn[kt];
+          vc[kt] = vn[kt];
         }
       }
 #pragma unroll
