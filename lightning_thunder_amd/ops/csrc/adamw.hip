@@ -35,7 +35,7 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 // rate on an idle GPU.  The lean variant (U = 1, <= 80 VGPRs, 6 waves/SIMD) is for the update
 // issued on a side stream during the backward: its waves fit next to a 4-wave gemm4 workgroup
 // (168 VGPR + 256 AGPR per wave), so the optimizer streams HBM while the GEMM keeps the MFMAs busy.
-template <typename TP, typename TS, int U>
+template <typename TP, typename TS, int U, bool NT = false>
 __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
                                            float lr, float b1, float b2, float eps, float wd, float bc1,
                                            float bc2_sqrt, float grad_scale) {
@@ -59,10 +59,17 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * 256 * VP;
         if (i < end) {
-          pv[u] = load16(P + i);
-          gv[u] = load16(G + i);
-          mv[u] = load16(M + i);
-          vv[u] = load16(V + i);
+          if constexpr (NT) {
+            pv[u] = load16_nt(P + i);
+            gv[u] = load16_nt(G + i);
+            mv[u] = load16_nt(M + i);
+            vv[u] = load16_nt(V + i);
+          } else {
+            pv[u] = load16(P + i);
+            gv[u] = load16(G + i);
+            mv[u] = load16(M + i);
+            vv[u] = load16(V + i);
+          }
         }
       }
 #pragma unroll
@@ -77,9 +84,15 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
             mv[u].v[j] = from_f32<TS>(m);
             vv[u].v[j] = from_f32<TS>(v);
           }
-          store16(P + i, pv[u]);
-          store16(M + i, mv[u]);
-          store16(V + i, vv[u]);
+          if constexpr (NT) {
+            store16_nt(P + i, pv[u]);
+            store16_nt(M + i, mv[u]);
+            store16_nt(V + i, vv[u]);
+          } else {
+            store16(P + i, pv[u]);
+            store16(M + i, mv[u]);
+            store16(V + i, vv[u]);
+          }
         }
       }
     }
@@ -94,12 +107,14 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
   }
 }
 
-template <typename TP, typename TS>
+template <typename TP, typename TS, bool NT = false>
 __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
                                                     float lr, float b1, float b2, float eps, float wd, float bc1,
                                                     float bc2_sqrt, float grad_scale) {
-  adamw_body<TP, TS, 4>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+  adamw_body<TP, TS, 4, NT>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
 }
+
+int g_adamw_nt = 0;  // A/B: non-temporal loads / stores in the post-backward kernel
 
 template <typename TP, typename TS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void adamw_lean_kernel(
@@ -112,6 +127,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void a
 
 LTA_EXPORT int lta_adamw_chunk_size() { return kChunk; }
 
+// A/B switch for the post-backward kernel's non-temporal streaming; returns the previous setting
+LTA_EXPORT int lta_adamw_set_nt(int nt) {
+  const int old = g_adamw_nt;
+  g_adamw_nt = nt ? 1 : 0;
+  return old;
+}
+
 // metas: device array of TensorMeta; chunks: device int2 array {tensor, chunk index}
 // lean = 1: the register-capped variant (see adamw_body) for updates overlapped with compute
 LTA_EXPORT int lta_adamw_ex(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr,
@@ -122,6 +144,9 @@ LTA_EXPORT int lta_adamw_ex(int pdtype, int sdtype, const void* metas, const voi
   do {                                                                                                               \
     if (lean)                                                                                                        \
       hipLaunchKernelGGL((adamw_lean_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,            \
+                         (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
+    else if (g_adamw_nt)                                                                                             \
+      hipLaunchKernelGGL((adamw_kernel<TPt, TSt, true>), grid, block, 0, stream, (const TensorMeta*)metas,           \
                          (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
     else                                                                                                             \
       hipLaunchKernelGGL((adamw_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,                 \

@@ -46,6 +46,21 @@ __device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
   *reinterpret_cast<uint4*>(p) = r.raw;
 }
 
+// non-temporal forms for pure streams (read once / written once): no L2 / MALL residency
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ Vec16<T> load16_nt(const T* p) {
+  Vec16<T> r;
+  r.raw = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p)));
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void store16_nt(T* p, const Vec16<T>& r) {
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4v, r.raw), reinterpret_cast<u32x4v*>(p));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
