@@ -210,7 +210,7 @@ def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: l
         buf[k] = ws.data_ptr()
     from ..ops._lib import stream_ptr
 
-    launches = [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
+    launches = [(g, b) for _, g, b in ks.pre] + [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
     for fn, (grid, block) in zip(fns, launches):
         rc = _lib().lta_rtc_launch(fn, grid[0], grid[1], grid[2], block[0], block[1], block[2], 0, stream_ptr(dev),
                                    ctypes.cast(buf, ctypes.c_void_p), ctypes.sizeof(buf))
@@ -221,7 +221,8 @@ def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: l
 
 def load_kernels(ks: cg.KernelSource) -> list:
     """Function handles of a kernel source's main kernel and its extra kernels."""
-    return [load_kernel(ks)] + [load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.extra]
+    return ([load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.pre] + [load_kernel(ks)] +
+            [load_kernel(ks, ks.name + suffix) for suffix, _, _ in ks.extra])
 
 
 def _double_bits(x) -> int:

@@ -110,12 +110,15 @@ ELEMENTWISE = set(_UNARY_FLOAT) | _UNARY_ANY | set(_BINARY) | _BINARY_FLOAT_ONLY
 VIEWS = {PrimIDs.BROADCAST_IN_DIM, PrimIDs.RESHAPE, PrimIDs.SQUEEZE, PrimIDs.TRANSPOSE, PrimIDs.PAD, PrimIDs.SLICE}
 # data movement with indirect / piecewise loads of external inputs (pointwise regions only)
 GATHERS = {PrimIDs.CAT, PrimIDs.TAKE, PrimIDs.TAKE_ALONG_AXIS, PrimIDs.EMBEDDING}
-SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | GATHERS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
+# indirect stores: the region ends in one of these (a copy kernel, then the region kernel storing
+# each value at its indexed position)
+SCATTERS = {PrimIDs.SCATTER, PrimIDs.INDEX_PUT}
+SUPPORTED = ELEMENTWISE | REDUCTIONS | VIEWS | GATHERS | SCATTERS | {PrimIDs.FULL, PrimIDs.UNIFORM_PHILOX}
 
 
 def is_compute(bsym) -> bool:
     sid = bsym.sym.id
-    return sid in ELEMENTWISE or sid in REDUCTIONS or sid in GATHERS or sid == PrimIDs.UNIFORM_PHILOX
+    return sid in ELEMENTWISE or sid in REDUCTIONS or sid in GATHERS or sid in SCATTERS or sid == PrimIDs.UNIFORM_PHILOX
 
 
 def tensor_args(b):
@@ -139,7 +142,7 @@ def base_map(amap):
       dims walk ``base``
     """
     if amap and isinstance(amap[0], str):
-        return amap[1]
+        return amap[1] if len(amap) > 1 else ()
     return amap
 
 
@@ -151,6 +154,8 @@ def _remap_amap(amap, f):
     if amap is None:
         return None
     rm = lambda mp: tuple(None if x is None else f(x) for x in mp)  # noqa: E731
+    if amap and isinstance(amap[0], str) and len(amap) == 1:
+        return amap
     if amap and isinstance(amap[0], str):
         if amap[0] == "gather":
             return (amap[0], rm(amap[1]), amap[2], amap[3], rm(amap[4]), amap[5])
@@ -176,10 +181,14 @@ class Plan:
     maps: dict = field(default_factory=dict)  # internal value name -> map tuple
     arg_maps: list = field(default_factory=list)  # per node: {arg position: map} for tensor args
     post: set = field(default_factory=set)  # column mode: values computed from a column reduction
+    # the region's closing scatter / index_put: {"node", "out", "a", "dim", "idx", "src"} (the region
+    # takes no node after it)
+    scatter: dict | None = None
 
     def copy(self) -> "Plan":
         return Plan(self.domain, self.red, self.colred, self.has_reduction, self.has_pad, list(self.nodes),
-                    dict(self.maps), [dict(m) for m in self.arg_maps], set(self.post))
+                    dict(self.maps), [dict(m) for m in self.arg_maps], set(self.post),
+                    dict(self.scatter) if self.scatter else None)
 
     # --- maps ----------------------------------------------------------------------------
     def _identity(self, shape):
@@ -272,6 +281,8 @@ class Plan:
         sid = bsym.sym.id
         if sid not in SUPPORTED:
             raise NotFusible(str(sid))
+        if self.scatter is not None:
+            raise NotFusible("region closed by a scatter")
         outs = [o for o in bsym.flat_outs]
         if not outs or not all(isinstance(o, TensorProxy) for o in outs):
             raise NotFusible("non-tensor output")
@@ -296,6 +307,8 @@ class Plan:
             self._add_cat(bsym, am)
         elif sid in (PrimIDs.TAKE, PrimIDs.TAKE_ALONG_AXIS, PrimIDs.EMBEDDING):
             self._add_gather(bsym, am)
+        elif sid in SCATTERS:
+            self._add_scatter(bsym, am)
         elif sid in REDUCTIONS:
             self._add_reduction(bsym, am)
         elif sid == PrimIDs.UNIFORM_PHILOX:
@@ -552,6 +565,57 @@ class Plan:
         self.has_pad = True
         self.maps[out.name] = om
 
+    def _add_scatter(self, bsym, am):
+        """``scatter(a, index, src, dim)`` / ``index_put(a, (index,), values)`` (one 1-D index on dim 0,
+        no accumulation) closing a pointwise region: the region runs over the index / values domain
+        (src / values may be computed in it), a copy kernel first writes ``a`` into the output and the
+        region kernel then stores each value at its indexed position (indices clamped into range)."""
+        sid, out = bsym.sym.id, bsym.output
+        if self.red or self.colred or self.has_reduction:
+            raise NotFusible("scatter in a reduction region")
+        if sid == PrimIDs.SCATTER:
+            a, idx, src, dim = bsym.args[0], bsym.args[1], bsym.args[2], int(pyval(bsym.args[3]))
+            ipos, spos = 1, 2
+            dom = tuple(int(x) for x in idx.shape)
+        else:
+            a, indices, src, acc = bsym.args[0], bsym.args[1], bsym.args[2], bsym.args[3]
+            if pyval(acc) or len(indices) != 1 or not isinstance(indices[0], TensorProxy) or indices[0].ndim != 1:
+                raise NotFusible("index_put form")
+            idx, dim, ipos, spos = indices[0], 0, None, 2
+            if not isinstance(src, TensorProxy) or tuple(src.shape) != (int(idx.shape[0]),) + tuple(a.shape[1:]):
+                raise NotFusible("index_put values shape")
+            dom = tuple(int(x) for x in src.shape)
+        if not isinstance(a, TensorProxy) or self._internal(a) or not isinstance(idx, TensorProxy) or \
+                self._internal(idx) or idx.dtype not in _INTS:
+            raise NotFusible("scatter operands")
+        if any(d == 0 for d in dom) or out.dtype != a.dtype:
+            raise NotFusible("scatter shape / dtype")
+        if self.domain is None:
+            self._set_domain(dom)
+        if self.domain != dom:
+            raise NotFusible("scatter domain")
+        om = self._identity(dom)
+        imap = om if sid == PrimIDs.SCATTER else om[:1]
+        if isinstance(src, TensorProxy):
+            if self._internal(src):
+                if self.maps[src.name] is None:
+                    self._resolve(src.name, om)
+                elif self.maps[src.name] != om:
+                    raise NotFusible("scatter source map")
+            else:
+                if src.ndim != len(dom) or any(src.shape[i] < dom[i] for i in range(len(dom))):
+                    raise NotFusible("scatter source shape")
+                am[spos] = tuple(None if src.shape[i] == 1 else i for i in range(len(dom)))
+        if ipos is not None:
+            am[ipos] = imap
+        else:  # index_put's index rides in the indices tuple: read through the scatter record
+            am[("idx",)] = imap
+        am[0] = ("scatter_dst",)
+        self.has_pad = True
+        self.maps[out.name] = ("scatter_out",)
+        self.scatter = dict(node=len(self.nodes), out=out.name, a=a.name, dim=dim, idx=idx.name, imap=imap,
+                            src=src.name if isinstance(src, TensorProxy) else None)
+
     def _add_unit_reshape(self, bsym, am):
         a, out = bsym.args[0], bsym.output
         if _sq(a.shape) != _sq(out.shape):
@@ -738,10 +802,12 @@ class TensorArg:
 
 
 class KernelSource:
-    def __init__(self, name, src, grid, block, vec, mode, extra=(), ws_bytes=0):
+    def __init__(self, name, src, grid, block, vec, mode, extra=(), ws_bytes=0, pre=()):
         self.name, self.src, self.grid, self.block, self.vec, self.mode = name, src, grid, block, vec, mode
         # further kernels launched after the main one with the same arguments: (name suffix, grid, block)
         self.extra = list(extra)
+        # kernels launched BEFORE the main one (a scatter region's copy of its base tensor)
+        self.pre = list(pre)
         # bytes of scratch the kernels share (passed as the last Args field), 0 = none
         self.ws_bytes = ws_bytes
 
@@ -823,7 +889,7 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
     name = f"{kernel_prefix}_{h}"
     src = src.replace("__KERNEL_NAME__", name)
-    return KernelSource(name, src, grid, block, vec, mode, extra=g.extra, ws_bytes=g.ws_bytes)
+    return KernelSource(name, src, grid, block, vec, mode, extra=g.extra, ws_bytes=g.ws_bytes, pre=g.pre)
 
 
 class _Gen:
@@ -838,6 +904,7 @@ class _Gen:
         self.colred = plan.colred
         self.force_scalar = False  # column epilogue kernel: every load is one element
         self.extra: list = []
+        self.pre: list = []
         self.ws_bytes = 0
         self.tensor_inputs = [a for a in inputs if isinstance(a, TensorProxy)]
         self.number_inputs = [a for a in inputs if not isinstance(a, TensorProxy)]
@@ -1109,6 +1176,9 @@ class _Gen:
             if b.sym.id in REDUCTIONS:
                 continue
             vec_scope = scope == "vec" and self.dep.get(b.flat_outs[0].name, True)
+            if b.sym.id in SCATTERS:
+                self._emit_scatter(b, k, out, indent)
+                continue
             if vec_scope and b.sym.id == PrimIDs.UNIFORM_PHILOX and self.flat_base4 and self.vec % 4 == 0:
                 self._emit_philox_vec(b, out, indent)
                 continue
@@ -1154,7 +1224,7 @@ class _Gen:
         # indirect (gather) loads last: they read the index loads of the same node
         items = sorted(tensor_args(b), key=lambda it: _kind(self.p.arg_maps[k].get(it[0])) == "gather")
         for i, a in items:
-            if a.name in self.producer:
+            if a.name in self.producer or _kind(self.p.arg_maps[k].get(i)) == "scatter_dst":
                 continue
             amap = self.p.arg_maps[k][i]
             nm = self.load_names[(a.name, amap)]
@@ -1454,13 +1524,88 @@ class _Gen:
         # referencing builds the load-name table lazily; pre-populate by a dry run over all nodes
         for k, b in enumerate(self.p.nodes):
             for i, a in tensor_args(b):
-                if a.name not in self.producer:
+                if a.name not in self.producer and _kind(self.p.arg_maps[k].get(i)) != "scatter_dst":
                     self.ref(a, k, i, "j")
         self._emit_nodes({o.name for o in self.outputs}, "vec", emitted, body, ind)
+        sc = self.p.scatter
         for o in self.outputs:
-            self._emit_store(o, True, body, ind)
+            if sc is None or o.name != sc["out"]:
+                self._emit_store(o, True, body, ind)
         body.append("  }")
-        return self._wrap(body, block), (grid, 1, 1), (block, 1, 1), V, "pointwise"
+        src = self._wrap(body, block)
+        if sc is not None:
+            src += self._scatter_copy_kernel()
+        return src, (grid, 1, 1), (block, 1, 1), V, "pointwise" if sc is None else "scatter"
+
+    # --- scatter regions -------------------------------------------------------------------------
+    def _scatter_copy_kernel(self) -> str:
+        """The pre-kernel of a scatter region: the base tensor copied into the (contiguous) output."""
+        sc = self.p.scatter
+        a = next(t for t in self.tensor_inputs if t.name == sc["a"])
+        o = next(t for t in self.outputs if t.name == sc["out"])
+        ta = self.targs[a.name]
+        n = math.prod(ta.shape)
+        IT = self.IT
+        contig = tuple(ta.strides) == tuple(_contig_strides(tuple(ta.shape))) or n == 1
+        nbytes = n * a.dtype.itemsize
+        lines = [f'extern "C" __global__ void __launch_bounds__(256) __KERNEL_NAME___pre(Args A) {{']
+        if contig and ta.align16 and nbytes % 16 == 0:
+            items = nbytes // 16
+            lines += [f"  const uint4* s = (const uint4*)A.in[{self.in_index[a.name]}];",
+                      f"  uint4* d = (uint4*)A.out[{self.out_index[o.name]}];",
+                      f"  for ({IT} v = ({IT})blockIdx.x * 256u + threadIdx.x; v < {items}u; v += ({IT})gridDim.x * 256u) d[v] = s[v];"]
+        else:
+            items = n
+            cst = _contig_strides(tuple(ta.shape))
+            terms = " + ".join(f"((e / {cst[i]}ull) % {ta.shape[i]}ull) * {ta.strides[i]}ull"
+                               for i in range(len(ta.shape)) if ta.shape[i] != 1) or "0ull"
+            sty = _STYPE[a.dtype]
+            lines += [f"  const {sty}* s = (const {sty}*)A.in[{self.in_index[a.name]}];",
+                      f"  {sty}* d = ({sty}*)A.out[{self.out_index[o.name]}];",
+                      f"  for (unsigned long long e = (unsigned long long)blockIdx.x * 256ull + threadIdx.x; e < {n}ull; "
+                      f"e += (unsigned long long)gridDim.x * 256ull) d[e] = s[{terms}];"]
+        lines.append("}")
+        self.pre = [("_pre", (max(1, min((items + 255) // 256, 8192)), 1, 1), (256, 1, 1))]
+        return "\n".join(lines) + "\n"
+
+    def _emit_scatter(self, b, k, out, indent):
+        """Store the node's source values at their indexed positions of the output (clamped indices)."""
+        sc = self.p.scatter
+        V, last = self.vec, self.nd - 1
+        o = b.output
+        a = next(t for t in self.tensor_inputs if t.name == sc["a"])
+        ta = self.targs[a.name]
+        ct = _CTYPE[o.dtype]
+        self._materialize_loads(b, k, True, out, indent)
+        if b.sym.id == PrimIDs.INDEX_PUT:
+            ip = next(t for t in self.tensor_inputs if t.name == sc["idx"])
+            inm = "LIX"
+            self._emit_load(ip, sc["imap"], inm, True, out, indent)
+        else:
+            inm = self.load_names[(sc["idx"], sc["imap"])]
+        src = b.args[2]
+        if isinstance(src, TensorProxy):
+            if src.name in self.producer:
+                val = f"v_{src.name}[j]"
+            else:
+                val = self.ref(src, k, 2, "j")
+        else:
+            val = self._scalar_ref(src, ct)
+        shape = tuple(int(x) for x in ta.shape)
+        cst = _contig_strides(shape)
+        d, size = int(sc["dim"]), shape[int(sc["dim"])]
+        terms = []
+        for i in range(self.nd):
+            if i == d:
+                continue
+            if self.D[i] != 1:
+                terms.append(f"((long long)i{i}{' + j' if i == last else ''}) * {cst[i]}ll")
+        terms.append(f"x * {cst[d]}ll")
+        optr = self._ptr(o, True)
+        out.append(f"{indent}#pragma unroll")
+        out.append(f"{indent}for (int j = 0; j < {V}; ++j) {{ long long x = (long long){inm}[j]; "
+                   f"x = x < 0 ? x + {size}ll : x; x = x < 0 ? 0 : (x >= {size}ll ? {size - 1}ll : x);")
+        out.append(f"{indent}  {optr}[{' + '.join(terms)}] = {_store_conv(o.dtype, f'({ct})({val})')}; }}")
 
     # --- row kernel ---------------------------------------------------------------------------
     def _build_row(self, numel):
@@ -1485,7 +1630,7 @@ class _Gen:
         self.flat_index = f"((unsigned long long)rowc * {R}ull + (unsigned long long)c + (unsigned long long)j)"
         for k, b in enumerate(self.p.nodes):
             for i, a in tensor_args(b):
-                if a.name not in self.producer:
+                if a.name not in self.producer and _kind(self.p.arg_maps[k].get(i)) != "scatter_dst":
                     self.ref(a, k, i, "j")
         body: list[str] = []
         body.append(f"  const unsigned lane = threadIdx.x % {T}u;")

@@ -149,6 +149,22 @@ def _two_reductions(x):
     return a.sum(0), (a - a.amax(1, keepdim=True)).exp().sum(1)
 
 
+def _scatter_region(a, idx, src, b, pidx, vals):
+    # a region closed by scatter (source computed in it) and one closed by index_put
+    s = torch.scatter(a, 1, idx, torch.tanh(src) * 2.0)
+    t = b.index_put((pidx,), vals.sin() + 1.0)
+    return s, t
+
+
+def _scatter_inputs(dt, d):
+    g = torch.Generator(device="cpu").manual_seed(3)
+    idx = torch.stack([torch.randperm(96, generator=g)[:40] for _ in range(24)]).to(d)  # unique per row
+    pidx = torch.randperm(300, generator=g)[:77].to(d)
+    return (torch.randn(24, 96, device=d, dtype=dt), idx, torch.randn(24, 40, device=d, dtype=dt),
+            torch.randn(300, 64, device=d, dtype=dt), pidx, torch.randn(77, 64, device=d, dtype=dt))
+
+
+CASES["scatter_region"] = (_scatter_region, _scatter_inputs)
 CASES["remat_regions"] = (_two_reductions, lambda dt, d: (torch.randn(256, 512, device=d, dtype=dt),))
 CASES["slice_mix"] = (_slice_mix, lambda dt, d: (torch.randn(4, 32, 3 * 96, device=d, dtype=dt),))
 CASES["cat_mix"] = (_cat_mix, _cat_inputs)
@@ -159,7 +175,7 @@ CASES["embed_add"] = (_embed_add, lambda dt, d: (torch.randint(0, 500, (4, 64), 
 CASES["reshape_ext"] = (_reshape_ext, lambda dt, d: (torch.randn(32, 24, device=d, dtype=dt),
                                                       torch.randn(24, 32, device=d, dtype=dt).t()))
 _COLUMN_CASES = ("bias_grad", "ln_dgamma_dbeta", "col_amax_epilogue", "full_and_col")
-_SHAPE_CASES = ("slice_mix", "cat_mix", "gather_mix", "embed_add", "reshape_ext")
+_SHAPE_CASES = ("slice_mix", "cat_mix", "gather_mix", "embed_add", "reshape_ext", "scatter_region")
 
 
 @pytest.fixture
@@ -214,7 +230,7 @@ def test_shape_ops_fused_cpu(case, cpu_fusion):
     fus = hipfuse.fusions(tr)
     assert fus
     left = [b.sym.name for b in tr.bound_symbols if not b.sym.is_fusion]
-    for name in ("cat", "take", "take_along_axis", "embedding", "embedding_prim", "reshape"):
+    for name in ("cat", "take", "take_along_axis", "embedding", "embedding_prim", "reshape", "scatter", "index_put"):
         assert name not in left and name + "_prim" not in left, (case, left)
     kinds = set()
     for fb in fus:
@@ -222,7 +238,7 @@ def test_shape_ops_fused_cpu(case, cpu_fusion):
         for am in f.plan.arg_maps:
             kinds |= {cg._kind(m) for m in am.values()}
     want = {"slice_mix": "slice", "cat_mix": "cat", "gather_mix": "gather", "embed_add": "gather",
-            "reshape_ext": "reshape"}[case]
+            "reshape_ext": "reshape", "scatter_region": "scatter_dst"}[case]
     assert want in kinds, kinds
 
 
