@@ -87,6 +87,10 @@ def dtensor_symbol(fn: Callable, name: str | None = None) -> Symbol:
     from ..executors import torchex
 
     impl = fn
+    if fn in (torch.nn.functional.linear, torch._grouped_mm):
+        def impl(*a, _fn=fn, **k):
+            out = _local_product(_fn, a, k)
+            return _fn(*a, **k) if out is None else out
     if getattr(fn, "__name__", "") == "redistribute":
         # the trace orders every consumer after the collective: run it synchronously on the stream
         def impl(*a, _fn=fn, **k):
@@ -95,6 +99,75 @@ def dtensor_symbol(fn: Callable, name: str | None = None) -> Symbol:
 
     torchex.register_opaque(sym, impl)
     return sym
+
+
+def _local_product(fn, args, kwargs):
+    """Column-parallel products whose placements need no communication, run on the local shards
+    with the hand-written GEMM kernels (``ops/gemm.py``) and re-wrapped as DTensors:
+
+    * ``linear(x, w, b)``: x replicated, w (and b) sharded on the output features (``Shard(0)``) or
+      replicated on each mesh dim -> y sharded on its last dim where w is sharded;
+    * ``torch._grouped_mm(x, w, offs)`` (MoE experts): x and offs replicated, w ``[G, K, N]`` sharded
+      on N (``Shard(2)``) or replicated -> y sharded on its last dim.
+
+    Returns None when the pattern does not apply (the DTensor op then runs as is).  Only the forward
+    uses this path: the backward re-runs the DTensor op under torch autograd."""
+    try:
+        from torch.distributed.tensor import DTensor, Replicate, Shard
+    except ImportError:  # pragma: no cover
+        return None
+    if fn is torch.nn.functional.linear:
+        x, w = args[0], args[1]
+        b = args[2] if len(args) > 2 else kwargs.get("bias")
+        wdim = 0
+    else:
+        if len(args) < 3 or kwargs:
+            return None
+        x, w, b = args[0], args[1], None
+        offs = args[2]
+        if isinstance(offs, DTensor):
+            if any(not p.is_replicate() for p in offs.placements):
+                return None
+            offs = offs.to_local()
+        wdim = 2
+    if not (isinstance(x, DTensor) and isinstance(w, DTensor)) or x.device_mesh != w.device_mesh:
+        return None
+    if not x.to_local().is_cuda or any(not p.is_replicate() for p in x.placements):
+        return None
+    out_pl = []
+    for p in w.placements:
+        if p.is_replicate():
+            out_pl.append(Replicate())
+        elif p.is_shard() and p.dim % w.ndim == wdim:
+            out_pl.append(Shard(x.ndim - 1))
+        else:
+            return None
+    bl = None
+    if b is not None:
+        if not isinstance(b, DTensor) or len(b.placements) != len(w.placements):
+            return None
+        for pb, pw in zip(b.placements, w.placements):
+            if not ((pb.is_replicate() and pw.is_replicate()) or (pb.is_shard() and pw.is_shard() and pb.dim % b.ndim == 0)):
+                return None
+        bl = b.to_local()
+    from ..ops import gemm
+
+    xl, wl = x.to_local(), w.to_local()
+    if fn is torch.nn.functional.linear:
+        yl = gemm.linear(xl, wl, bl)
+        shape = tuple(x.shape[:-1]) + (w.shape[0],)
+    else:
+        if xl.ndim != 2 or wl.ndim != 3:
+            return None
+        yl = gemm.grouped_mm(xl, wl, offs)
+        shape = (x.shape[0], w.shape[2])
+    stride = []
+    acc = 1
+    for n in reversed(shape):
+        stride.append(acc)
+        acc *= n
+    return DTensor.from_local(yl, x.device_mesh, out_pl, run_check=False, shape=torch.Size(shape),
+                              stride=tuple(reversed(stride)))
 
 
 def has_dtensor(flat) -> bool:

@@ -83,3 +83,51 @@ def test_dtensor_ops_and_tensor_parallel():
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             bad = {k: v for k, v in res.items() if v is not True}
             assert not bad, bad
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_dtensor_column_parallel_products_on_hand_kernels_gpu():
+    """Column-parallel DTensor products (replicated input, weight sharded on the output features)
+    need no communication: their forward runs the hand-written GEMMs on the local shards
+    (distributed/dtensor.py ``_local_product``) and the result keeps DTensor's placement."""
+    import torch.nn.functional as F
+    from torch.distributed.device_mesh import DeviceMesh
+    from torch.distributed.tensor import DTensor, Replicate, Shard
+
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.ops.gemm import last_gemm_backend_counts
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    torch.distributed.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        mesh = DeviceMesh("cuda", [0])
+        torch.manual_seed(0)
+        W = torch.randn(512, 256, device="cuda", dtype=torch.bfloat16) / 16
+        X = torch.randn(128, 256, device="cuda", dtype=torch.bfloat16)
+        w = DTensor.from_local(W, mesh, [Shard(0)], run_check=False)
+        x = DTensor.from_local(X, mesh, [Replicate()], run_check=False)
+        last_gemm_backend_counts(reset=True)
+        y = thunder.jit(lambda x, w: F.linear(x, w))(x, w)
+        assert last_gemm_backend_counts(reset=True).get("gemm4", 0) >= 1
+        assert isinstance(y, DTensor) and tuple(y.placements) == (Shard(1),)
+        ref = X.float() @ W.float().t()
+        assert (y.to_local().float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+        G, K, N = 4, 256, 384
+        offs = torch.tensor([100, 160, 300, 512], device="cuda", dtype=torch.int32)
+        WG = torch.randn(G, K, N, device="cuda", dtype=torch.bfloat16) / 16
+        XG = torch.randn(512, K, device="cuda", dtype=torch.bfloat16)
+        wg = DTensor.from_local(WG, mesh, [Shard(2)], run_check=False)
+        xg = DTensor.from_local(XG, mesh, [Replicate()], run_check=False)
+        og = DTensor.from_local(offs, mesh, [Replicate()], run_check=False)
+        last_gemm_backend_counts(reset=True)
+        yg = thunder.jit(lambda x, w, o: torch._grouped_mm(x, w, o))(xg, wg, og)
+        assert last_gemm_backend_counts(reset=True).get("gemm4", 0) >= 1
+        assert tuple(yg.placements) == (Shard(1),)
+        refg = torch._grouped_mm(XG, WG, offs).float()
+        assert (yg.to_local().float() - refg).abs().max().item() < 2e-2 * refg.abs().max().item()
+    finally:
+        torch.distributed.destroy_process_group()
