@@ -1420,9 +1420,11 @@ def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=Fa
     if query.dtype not in (torch.bfloat16, torch.float16) or key.dtype != query.dtype or value.dtype != query.dtype:
         return False
     D = query.shape[-1]
-    from ..ops.attention import padded_head_dim
+    from ..ops.attention import padded_head_dim, PLAIN_ONLY_HEAD_DIM
 
     if padded_head_dim(D) is None or key.shape[-1] != D or value.shape[-1] != D:
+        return False
+    if D > PLAIN_ONLY_HEAD_DIM and (attn_mask is not None or p > 0.0):
         return False
     if key.shape[1] != value.shape[1] or query.shape[1] % key.shape[1] != 0:
         return False

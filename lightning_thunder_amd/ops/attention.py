@@ -39,12 +39,15 @@ register_signature("lta_attn_bwd_ex3", [c_int, c_void_p, c_void_p, c_void_p, c_v
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                         ctypes.c_uint64, c_void_p, c_void_p, c_void_p])
 
-SUPPORTED_HEAD_DIMS = (64, 96, 128)  # the kernels' compile-time head dims
-# Other head dims up to 128 (multiples of 8) run zero-padded to the next kernel head dim, as the
+SUPPORTED_HEAD_DIMS = (64, 96, 128, 256)  # the kernels' compile-time head dims
+# Other head dims up to 256 (multiples of 8) run zero-padded to the next kernel head dim, as the
 # reference pads for aten flash (thunder/executors/sdpaex.py:45-59): zero columns of Q / K leave
 # Q K^T unchanged, zero columns of V give zero columns of O (sliced off), the scale stays the
 # caller's (1 / sqrt(D) of the real D), and the padded gradient columns are exactly zero.
-MAX_PADDED_HEAD_DIM = 128
+# D = 256 (Gemma; cuDNN's limit, thunder/executors/cudnn_sdpa.py:339-363) runs 32-key tiles at one
+# workgroup per CU with the accumulators in the AGPR file, without masks or dropout.
+MAX_PADDED_HEAD_DIM = 256
+PLAIN_ONLY_HEAD_DIM = 128  # above this head dim the kernels take no additive mask / dropout
 
 
 def padded_head_dim(D: int) -> int | None:

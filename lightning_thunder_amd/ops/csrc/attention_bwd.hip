@@ -23,6 +23,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 template <int D> struct BCfg {
+  static constexpr int BN = D > 128 ? 32 : 64;  // dQ kernel: keys per tile (D = 256: registers)
+  static constexpr int NKT = BN / 32;
   static constexpr int RSTR = D + 8;    // row-read image stride (ds_read_b128 conflict-free)
   static constexpr int TSTR = D + 32;   // transposed-read image stride (ds_read_b64_tr_b16 conflict-free)
   static constexpr int CH = D / 8;
@@ -60,6 +62,17 @@ __global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
   if (row < rows && sub == 0) delta[row] = acc;
+}
+
+// dK^T / dV^T accumulate in the accumulator (AGPR) file through inline-asm MFMAs: they are only
+// ever MFMA C/D operands, and pinning them there leaves the 256 architectural VGPRs to K, the S / dP
+// tiles and their softmax (hipcc otherwise parks S / dP in AGPRs and copies them out every tile).
+// `s_nop 1` covers the VALU (cvt_pk) write -> MFMA operand read; an accumulate chain needs none.
+__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const f16x8& a, const f16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -249,17 +262,28 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       const int col0 = dt * 32 + 16 * (g & 1);
       const F oa0 = tr_frag<F>(dOt3, 4 * h, col0, C::TSTR, l16);
       const F oa1 = tr_frag<F>(dOt3, 16 + 4 * h, col0, C::TSTR, l16);
-      dvacc[dt] = mfma(oa0, pf0, dvacc[dt]);
-      dvacc[dt] = mfma(oa1, pf1, dvacc[dt]);
       const F qa0 = tr_frag<F>(Qt3, 4 * h, col0, C::TSTR, l16);
       const F qa1 = tr_frag<F>(Qt3, 16 + 4 * h, col0, C::TSTR, l16);
-      dkacc[dt] = mfma(qa0, df0, dkacc[dt]);
-      dkacc[dt] = mfma(qa1, df1, dkacc[dt]);
+      if constexpr (D > 128) {  // 2 x 128 accumulators: pinned to the AGPR file (K, V fill the VGPRs)
+        mfma_acc_agpr(dvacc[dt], oa0, pf0);
+        mfma_acc_agpr(dvacc[dt], oa1, pf1);
+        mfma_acc_agpr(dkacc[dt], qa0, df0);
+        mfma_acc_agpr(dkacc[dt], qa1, df1);
+      } else {
+        dvacc[dt] = mfma(oa0, pf0, dvacc[dt]);
+        dvacc[dt] = mfma(oa1, pf1, dvacc[dt]);
+        dkacc[dt] = mfma(qa0, df0, dkacc[dt]);
+        dkacc[dt] = mfma(qa1, df1, dkacc[dt]);
+      }
     }
     if (more) stash(it + 1, buf ^ 1);
     __syncthreads();
   }
 
+  if constexpr (D > 128) {  // the last asm MFMAs' results must be complete before they are read
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[dt]), "+a"(dvacc[dt]));
+  }
   // dK^T / dV^T: element i of tile dt is d = dt*32 + acc_row(i,h), key = this lane's key
   if (key < Sk) {
     T* dkrow = dK + (int64_t)b * ex.sx.dkb + (int64_t)hk * ex.sx.dkh + (int64_t)key * ex.sx.dkt;
@@ -382,17 +406,6 @@ __device__ __forceinline__ void tr_wait16(F (&f)[8], s16x4t (&x)[16]) {
     u.s.b = x[2 * i + 1];
     f[i] = u.f;
   }
-}
-
-// dK^T / dV^T accumulate in the accumulator (AGPR) file through inline-asm MFMAs: they are only
-// ever MFMA C/D operands, and pinning them there leaves the 256 architectural VGPRs to K, the S / dP
-// tiles and their softmax (hipcc otherwise parks S / dP in AGPRs and copies them out every tile).
-// `s_nop 1` covers the VALU (cvt_pk) write -> MFMA operand read; an accumulate chain needs none.
-__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const f16x8& a, const f16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 template <typename T, bool CAUSAL>
@@ -1249,7 +1262,7 @@ constexpr int kBM = 128;
 constexpr int kBN = 64;
 
 template <typename T, int D, bool CAUSAL, int EX = 0>
-__global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+__global__ __launch_bounds__(kThreads, (EX || D > 128) ? 1 : 2) void attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                   const T* __restrict__ V, const T* __restrict__ dO,
                                                                   const float* __restrict__ LSE,
                                                                   const float* __restrict__ DELTA, T* __restrict__ dQ,
@@ -1258,10 +1271,10 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
   constexpr bool MASK = EX & kExMask, DROP = EX & kExDrop;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
-  __shared__ __attribute__((aligned(16))) short smem[2 * kBN * C::RSTR + kBN * C::TSTR];
+  __shared__ __attribute__((aligned(16))) short smem[2 * C::BN * C::RSTR + C::BN * C::TSTR];
   short* Kr = smem;                    // [64][RSTR]  K rows (A operand of S^T)
-  short* Vr = Kr + kBN * C::RSTR;      // [64][RSTR]  V rows (A operand of dP^T)
-  short* Kt = Vr + kBN * C::RSTR;      // [64][TSTR]  K image for transposed reads (A of dQ^T)
+  short* Vr = Kr + C::BN * C::RSTR;      // [64][RSTR]  V rows (A operand of dP^T)
+  short* Kt = Vr + C::BN * C::RSTR;      // [64][TSTR]  K image for transposed reads (A of dQ^T)
   const __attribute__((address_space(3))) short* Kt3 = (const __attribute__((address_space(3))) short*)Kt;
 
   const int n_qt = (Tq + kBM - 1) / kBM;
@@ -1300,10 +1313,10 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
 
-  int n_tiles = (Sk + kBN - 1) / kBN;
-  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
-  constexpr int LOADS = kBN * C::CH / kThreads;
-  static_assert(kBN * C::CH % kThreads == 0, "K/V staging must cover the tile");
+  int n_tiles = (Sk + C::BN - 1) / C::BN;
+  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + C::BN - 1) / C::BN);
+  constexpr int LOADS = C::BN * C::CH / kThreads;
+  static_assert(C::BN * C::CH % kThreads == 0, "K/V staging must cover the tile");
 
   // K/V tiles are prefetched into registers one tile ahead (latency hides behind the MFMAs).
   uint4 pk[LOADS], pv[LOADS];
@@ -1312,7 +1325,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
     for (int c = 0; c < LOADS; ++c) {
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
-      const int kc = min(t * kBN + row, Sk - 1);
+      const int kc = min(t * C::BN + row, Sk - 1);
       pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * ex.sx.kt + ch * 8);
       pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * ex.sx.vt + ch * 8);
     }
@@ -1325,7 +1338,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
       uint4 xk = pk[c], xv = pv[c];
-      if (t * kBN + row >= Sk) {
+      if (t * C::BN + row >= Sk) {
         xk = make_uint4(0, 0, 0, 0);
         xv = make_uint4(0, 0, 0, 0);
       }
@@ -1336,9 +1349,9 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
     __syncthreads();
     if (t + 1 < n_tiles) issue(t + 1);
 
-    f32x16 sacc[2], pacc[2];
+    f32x16 sacc[C::NKT], pacc[C::NKT];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         sacc[kt][i] = 0.f;
@@ -1347,17 +1360,17 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < C::NKT; ++kt) {
         const F ka = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h);
         const F va = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * s + 8 * h);
         sacc[kt] = mfma(ka, qf[s], sacc[kt]);  // S^T = K Q^T
         pacc[kt] = mfma(va, of[s], pacc[kt]);  // dP^T = V dO^T
       }
     }
-    const int kbase = t * kBN;
+    const int kbase = t * C::BN;
     if constexpr (MASK) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float4 mv = *reinterpret_cast<const float4*>(mrow + kbase + kt * 32 + 8 * j + 4 * h);
@@ -1368,7 +1381,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
         }
     }
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < C::NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kbase + kt * 32 + acc_row(i, h);
@@ -1382,9 +1395,9 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
         pacc[kt][i] = p * (dp - dlt);  // dS^T
       }
     }
-    F df[2][2];
+    F df[C::NKT][2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < C::NKT; ++kt) {
       pack_frag(df[kt][0], pacc[kt], 0);
       pack_frag(df[kt][1], pacc[kt], 1);
     }
@@ -1392,7 +1405,7 @@ __global__ __launch_bounds__(kThreads, EX ? 1 : 2) void attn_bwd_dq_kernel(const
     for (int dt = 0; dt < C::DT; ++dt) {
       const int col0 = dt * 32 + 16 * (g & 1);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < C::NKT; ++kt) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const F ka = tr_frag<F>(Kt3, kt * 32 + 16 * s + 4 * h, col0, C::TSTR, l16);
@@ -1610,6 +1623,218 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// dQ, D = 128 (v3): the dK/dV v3 data flow mirrored onto the query side.  One workgroup per 256
+// queries, 64 per wave in two 32-row halves: Q rows in registers (B operand of S^T = K Q^T), the
+// workgroup's dO rows in LDS (B operand of dP^T = V dO^T), 32-key K / V tiles streamed by
+// global_load_lds into a 3-stage ring of layout-(a) images that serve the row reads of S^T / dP^T
+// and the transposed reads of dQ^T += K^T dS^T; dQ^T accumulates in the AGPR file.  Against v2
+// (32 queries per wave, register-staged K / V) every staged fragment feeds twice the MFMAs and the
+// staging needs no VGPRs.
+// ---------------------------------------------------------------------------------------------
+constexpr int kQB3 = 256;  // queries per workgroup
+constexpr int kKT3 = 32;   // keys per streamed tile
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                     const T* __restrict__ V, const T* __restrict__ dO,
+                                                                     const float* __restrict__ LSE,
+                                                                     const float* __restrict__ DELTA, T* __restrict__ dQ,
+                                                                     int Hq, int Hkv, int Tq, int Sk, float scale,
+                                                                     float scale_log2, RowStrides sdo, QKVStrides sx) {
+  constexpr int D = 128;
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  constexpr int NST = 3;
+  constexpr int IMG = kKT3 * 256;  // 32 rows x 128 x 16-bit
+  constexpr int STAGE = 2 * IMG;   // K image, V image
+  constexpr int OOFF = NST * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[OOFF + kQB3 * C::RSTR * 2];
+  short* Os = reinterpret_cast<short*>(smem + OOFF);
+
+  const int n_qb = (Tq + kQB3 - 1) / kQB3;
+  const int qb = n_qb - 1 - (int)blockIdx.y;  // heaviest causal blocks first
+  const int bh = blockIdx.x;
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hk = hq / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qw = qb * kQB3 + wave * 64;  // this wave's first query; half j: queries qw + 32 j + r
+  const T* Qb = Q + b * sx.qb + hq * sx.qh;
+  const T* dOb = dO + b * sdo.b + hq * sdo.h;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
+
+  // dO rows of the workgroup's 256 queries -> LDS; Q rows and row statistics of this wave's 64
+  // queries -> registers (rows past Tq are clamped copies; their dQ is not stored)
+#pragma unroll
+  for (int c = 0; c < kQB3 * C::CH / kThreads; ++c) {
+    const int id = c * kThreads + tid;
+    const int row = id / C::CH, ch = id % C::CH;
+    const int orow = min(qb * kQB3 + row, Tq - 1);
+    *reinterpret_cast<uint4*>(Os + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(dOb + (int64_t)orow * sdo.t + ch * 8);
+  }
+  constexpr float kLog2e = 1.44269504088896340736f;
+  F qf[2][C::KS];
+  float nl2[2], dl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qr = min(qw + 32 * j + r, Tq - 1);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[j][s] = load_frag<F>(Qb + (int64_t)qr * sx.qt + 16 * s + 8 * h);
+    nl2[j] = -LSE[((int64_t)b * Hq + hq) * Tq + qr] * kLog2e;
+    dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+  }
+
+  f32x16 dqacc[2][C::DT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dqacc[j][dt][i] = 0.f;
+
+  int n_kt = (Sk + kKT3 - 1) / kKT3;
+  if (CAUSAL) n_kt = min(n_kt, (min(qb * kQB3 + kQB3, Tq) + kKT3 - 1) / kKT3);
+
+  // one 32-key tile: 8 x 1 KiB of K and of V per workgroup, lane-linear DMA into layout (a)
+  // (the swizzle is applied to the source row / chunk; see dK/dV v3)
+  auto issue = [&](int t, int st) {
+    char* kimg = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = wave * 2 + i;
+      const int u = 64 * k + lane;
+      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
+      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
+      const int kc = min(t * kKT3 + row, Sk - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)kc * sx.kt + ch * 8), (lds_void*)(kimg + k * 1024), 16,
+                                       0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)kc * sx.vt + ch * 8),
+                                       (lds_void*)(kimg + IMG + k * 1024), 16, 0, 0);
+    }
+  };
+  if (n_kt > 0) issue(0, 0);
+  if (n_kt > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed (tile 1 may be in flight)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  unsigned tr_a, tr_b;
+  {
+    const int l16 = lane & 15, g = lane >> 4;
+    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
+    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
+  }
+  int st = 0;
+  for (int t = 0; t < n_kt; ++t) {
+    const bool issue_next = t + 2 < n_kt;
+    const int st2 = st >= 1 ? st - 1 : 2;
+    if (issue_next) issue(t + 2, st2);
+    const char* kimg = smem + st * STAGE;
+    const char* vimg = kimg + IMG;
+    f32x16 sacc[2], pacc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        sacc[j][i] = 0.f;
+        pacc[j][i] = 0.f;
+      }
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F ka = load_frag<F>(kimg + du_off(r, 2 * s + h));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) sacc[j] = mfma(ka, qf[j][s], sacc[j]);  // S^T = K Q^T
+    }
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F va = load_frag<F>(vimg + du_off(r, 2 * s + h));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)  // dP^T = V dO^T
+        pacc[j] = mfma(va, load_frag<F>(Os + (wave * 64 + 32 * j + r) * C::RSTR + 16 * s + 8 * h), pacc[j]);
+    }
+    const int kbase = t * kKT3;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, nl2[j]));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int qi = qw + 32 * j + r;
+      const bool masked = kbase + kKT3 > Sk || (CAUSAL && kbase + kKT3 - 1 > qw + 32 * j);  // wave-uniform
+      if (masked) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kbase + acc_row(i, h);
+          if (key >= Sk || (CAUSAL && key > qi)) sacc[j][i] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pacc[j][i] = sacc[j][i] * (pacc[j][i] - dl[j]);  // dS^T
+    F df[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pack_frag(df[j][0], pacc[j], 0);
+      pack_frag(df[j][1], pacc[j], 1);
+    }
+    {
+      F xt[8];
+      tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // K^T
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          mfma_acc_agpr(dqacc[j][dt], xt[2 * dt], df[j][0]);
+          mfma_acc_agpr(dqacc[j][dt], xt[2 * dt + 1], df[j][1]);
+        }
+    }
+    if (issue_next)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile t+1 landed; t+2 may be in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    st = st == 2 ? 0 : st + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dqacc[j][dt]));
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qi = qw + 32 * j + r;
+    if (qi < Tq) {
+      T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int d = dt * 32 + 8 * a + 4 * h;
+          union {
+            T v[4];
+            uint2 u;
+          } pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(dqacc[j][dt][4 * a + e] * scale);
+          *reinterpret_cast<uint2*>(drow + d) = pk.u;
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int D, int EX>
 void launch_masked(const void* dO, const void* Q, const void* K, const void* V, const void* LSE, void* DELTA, void* dQ,
                    void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, float sl2, int causal,
@@ -1635,7 +1860,7 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 }
 
 int g_dkdv_v3 = 2;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
-int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 1 = v2 (8 waves), 0 = v1
+int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 2 = v3, 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -1646,6 +1871,9 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
   if (exf) {  // masks / dropout: the plain-HIP dK/dV kernel with the extra terms compiled in
+    if constexpr (D > 128) {
+      return -1;  // D = 256: plain (causal / full) attention only
+    } else {
     switch (exf) {
 #define LTA_M(F)                                                                                                  \
   case F:                                                                                                         \
@@ -1661,6 +1889,7 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
         return -1;
     }
     return (int)hipGetLastError();
+    }
   }
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
   if (D == 128 && dkdv_v2 && g_dkdv_v3 && Tq > 0 && Sk > 0) {
@@ -1694,7 +1923,15 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
                        sl2, sdo, ex);
-  if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
+  if (D == 128 && g_dq_v2 == 2 && Tq > 0 && Sk > 0) {
+    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
+  } else if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
     dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
@@ -1765,10 +2002,12 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
     if (D == 128) LTA_B(__hip_bfloat16, 128);
     if (D == 64) LTA_B(__hip_bfloat16, 64);
     if (D == 96) LTA_B(__hip_bfloat16, 96);
+    if (D == 256) LTA_B(__hip_bfloat16, 256);
   } else if (dtype == kF16) {
     if (D == 128) LTA_B(__half, 128);
     if (D == 64) LTA_B(__half, 64);
     if (D == 96) LTA_B(__half, 96);
+    if (D == 256) LTA_B(__half, 256);
   }
 #undef LTA_B
   return -1;
@@ -1810,7 +2049,7 @@ LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void
 // dQ kernel selection (A/B measurement hook): 1 = v2, 0 = v1; returns the previous choice
 LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
   const int old = g_dq_v2;
-  if (impl == 0 || impl == 1) g_dq_v2 = impl;
+  if (impl >= 0 && impl <= 2) g_dq_v2 = impl;
   return old;
 }
 

@@ -26,16 +26,21 @@ constexpr int kBN = 64;   // keys per tile
 constexpr int kThreads = 256;
 
 template <int D> struct Cfg {
+  // D = 256 (Gemma): 32-key tiles and one workgroup per CU, so Q (64 VGPRs), O (128 accumulators)
+  // and the staged K / V tile fit the 512-entry VGPR + AGPR file of a lone wave without spilling
+  static constexpr int BN = D > 128 ? 32 : kBN;    // keys per tile
+  static constexpr int NKT = BN / 32;              // 32-key sub-tiles
+  static constexpr int OCC = D > 128 ? 1 : 2;      // workgroups per CU (launch bound)
   static constexpr int KSTR = D + 8;               // K tile row stride (elements)
-  static constexpr int VSTR = D + (D == 128 ? 32 : 32);  // V tile row stride
+  static constexpr int VSTR = D + 32;              // V tile row stride
   static constexpr int CH = D / 8;                 // 16-byte chunks per row
-  static constexpr int LOADS = kBN * CH / kThreads;  // chunks per thread per tile
+  static constexpr int LOADS = BN * CH / kThreads;  // chunks per thread per tile
   static constexpr int KS = D / 16;                // MFMA k-steps over D
   static constexpr int DT = D / 32;                // 32-wide d tiles
 };
 
 template <typename T, int D, bool CAUSAL, int EX = 0>
-__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+__global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                const T* __restrict__ V, T* __restrict__ O,
                                                                float* __restrict__ LSE, int Hq, int Hkv, int Tq,
                                                                int Sk, float scale_log2, int64_t so_b, int64_t so_h,
@@ -43,9 +48,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
   constexpr bool MASK = EX & kExMask, DROP = EX & kExDrop;
   using C = Cfg<D>;
   using F = typename Frag<T>::type;
-  __shared__ __attribute__((aligned(16))) short smem[kBN * C::KSTR + kBN * C::VSTR];
+  __shared__ __attribute__((aligned(16))) short smem[C::BN * C::KSTR + C::BN * C::VSTR];
   short* Ks = smem;
-  short* Vs = smem + kBN * C::KSTR;
+  short* Vs = smem + C::BN * C::KSTR;
   const __attribute__((address_space(3))) short* Vs3 = (const __attribute__((address_space(3))) short*)Vs;
 
   const int n_qt = (Tq + kBM - 1) / kBM;
@@ -85,8 +90,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
 
-  int n_tiles = (Sk + kBN - 1) / kBN;
-  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + kBN - 1) / kBN);
+  int n_tiles = (Sk + C::BN - 1) / C::BN;
+  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM + kBM, Tq) + C::BN - 1) / C::BN);
 
   // register staging of one K/V tile
   uint4 kreg[C::LOADS], vreg[C::LOADS];
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     for (int c = 0; c < C::LOADS; ++c) {
       const int id = c * kThreads + tid;
       const int row = id / C::CH, ch = id % C::CH;
-      const int key = t * kBN + row;
+      const int key = t * C::BN + row;
       const int kc = min(key, Sk - 1);  // branch-free: clamp the address, zero the data
       uint4 kx = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * ex.sx.kt + ch * 8);
       uint4 vx = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * ex.sx.vt + ch * 8);
@@ -122,27 +127,27 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     if (t + 1 < n_tiles) gload(t + 1);  // next tile's HBM traffic overlaps this tile's math
 
     // ---- S^T = K Q^T : two 32-key sub-tiles -------------------------------------------------
-    f32x16 sacc[2];
+    f32x16 sacc[C::NKT];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < C::NKT; ++kt) {
         const F ka = load_frag<F>(Ks + (kt * 32 + r) * C::KSTR + 16 * s + 8 * h);
         sacc[kt] = mfma(ka, qf[s], sacc[kt]);
       }
     }
 
     // ---- scale, mask, online softmax (lane-local row = query qi) --------------------------------
-    const int kbase = t * kBN;
-    const bool need_mask = (kbase + kBN > Sk) || (CAUSAL && kbase + kBN - 1 > q0);
+    const int kbase = t * C::BN;
+    const bool need_mask = (kbase + C::BN > Sk) || (CAUSAL && kbase + C::BN - 1 > q0);
     float mx = -INFINITY;
     if constexpr (MASK) {  // additive mask, 4 consecutive keys per 16-B load (key dim padded to 64)
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float4 mv = *reinterpret_cast<const float4*>(mrow + kbase + kt * 32 + 8 * j + 4 * h);
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
         }
     }
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < C::NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float v = MASK ? sacc[kt][i] : sacc[kt][i] * scale_log2;
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     const float alpha = __builtin_amdgcn_exp2f(m - m_use);
     float rs = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < C::NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(sacc[kt][i] - m_use);
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     m = m_new;
     if constexpr (DROP) {  // the normalizer keeps every probability; only P.V sees the dropped ones
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const bool keep = rng_keep(ex, qterm, rng_k(kbase + kt * 32 + acc_row(i, h)));
@@ -197,9 +202,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
 
     // ---- O^T += V^T P^T ----------------------------------------------------------------------
-    F pf[2][2];
+    F pf[C::NKT][2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < C::NKT; ++kt) {
       pack_frag(pf[kt][0], sacc[kt], 0);
       pack_frag(pf[kt][1], sacc[kt], 1);
     }
@@ -207,7 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const T* __restri
     for (int dt = 0; dt < C::DT; ++dt) {
       const int col0 = dt * 32 + 16 * (g & 1);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < C::NKT; ++kt) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const F va = tr_frag<F>(Vs3, kt * 32 + 16 * s + 4 * h, col0, C::VSTR, l16);
@@ -692,10 +697,14 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
     if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 96) return launch<__hip_bfloat16, 96>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+    if (D == 256 && exf == 0)  // D = 256: plain (causal / full) attention only
+      return launch_ex<__hip_bfloat16, 256, 0>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, stream);
   } else if (dtype == kF16) {
     if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 96) return launch<__half, 96>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
+    if (D == 256 && exf == 0)
+      return launch_ex<__half, 256, 0>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, stream);
   }
   return -1;
 }

@@ -165,3 +165,37 @@ def test_sdpa_with_mask_and_dropout_claimed_by_hipex():
     y.float().pow(2).mean().backward()
     assert torch.isfinite(y).all()
     assert "hip_flash_attn_fwd_ex" in str(thunder.last_traces(jg)[-1])
+
+
+def test_sdpa_head_dim_256_claimed_by_hipex():
+    """Gemma's head dim: plain causal SDPA at D=256 runs on the hand kernels (forward and backward),
+    matching fp32; with an additive mask it is declined (the D=256 kernels take no mask / dropout)."""
+    import lightning_thunder_amd as thunder
+
+    B, Hq, Hkv, T, D = 1, 4, 2, 192, 256
+    q, k, v = (t.requires_grad_(True) for t in _qkv(B, Hq, Hkv, T, T, D))
+
+    def f(q, k, v):
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
+
+    jf = thunder.jit(f)
+    out = jf(q, k, v)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = f(qr, kr, vr)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    do = torch.randn_like(out)
+    out.backward(do)
+    ref.backward(do.float())
+    for got, want in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        assert _rel(got, want) < 2e-2, _rel(got, want)
+    assert "hip_flash_attn_fwd" in str(thunder.last_traces(jf)[-1])
+    assert "hip_flash_attn_bwd" in str(thunder.last_backward_traces(jf)[-1])
+
+    mask = torch.zeros(T, T, device="cuda", dtype=torch.bfloat16)
+
+    def g(q, k, v):
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
+
+    jg = thunder.jit(g)
+    jg(q.detach(), k.detach(), v.detach())
+    assert "hip_flash_attn" not in str(thunder.last_traces(jg)[-1])

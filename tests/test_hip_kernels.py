@@ -155,6 +155,8 @@ def _sdpa_ref(q, k, v, causal, scale=None):
     (1, 2, 2, 96, 333, 128), (1, 32, 32, 1024, 1024, 128), (2, 4, 2, 300, 300, 96), (1, 4, 4, 256, 256, 96),
     # head dims without a kernel instantiation run zero-padded to the next one (ops/attention.py)
     (2, 4, 2, 200, 200, 32), (1, 4, 4, 256, 256, 80), (1, 2, 2, 100, 100, 48), (1, 2, 1, 77, 77, 112),
+    # D = 256 (Gemma): 32-key tiles, AGPR accumulators; 192 runs padded to 256
+    (1, 4, 2, 200, 200, 256), (2, 2, 2, 256, 256, 256), (1, 2, 2, 96, 333, 256), (1, 4, 4, 130, 130, 192),
 ])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
@@ -170,7 +172,7 @@ def test_flash_attention_fwd_bwd(dtype, B, Hq, Hkv, T, S, D, causal):
     do = torch.randn(B, T, Hq, D, device="cuda", dtype=dtype).transpose(1, 2) if T % 2 else \
         torch.randn(B, Hq, T, D, device="cuda", dtype=dtype)
     o, lse = attn_fwd(q, k, v, causal)
-    if D in (64, 96, 128):
+    if D in (64, 96, 128, 256):
         assert o.transpose(1, 2).is_contiguous()  # O stored [B, T, H, D]
     qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
     ref = _sdpa_ref(qf, kf, vf, causal)
