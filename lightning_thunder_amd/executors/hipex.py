@@ -1393,7 +1393,9 @@ def _is_decode(query, key, attn_mask) -> bool:
 
     if attn_mask is None or not isinstance(attn_mask, TensorProxy) or attn_mask.dtype != torch.bool:
         return False
-    B, Hq, T, _ = query.shape
+    B, Hq, T, D = query.shape
+    if D not in (64, 128):  # the decode kernel's head dims (others take the padded flash path)
+        return False
     return T <= DECODE_MAX_QUERIES and _broadcastable(tuple(attn_mask.shape), (B, Hq, T, key.shape[2]))
 
 

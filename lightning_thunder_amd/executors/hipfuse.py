@@ -293,6 +293,23 @@ def compile_source(ks: cg.KernelSource) -> bytes:
     return data
 
 
+def precompile(trace) -> int:
+    """Generates and compiles (hiprtc, no GPU needed) the kernel of every hipfuse region of an
+    execution trace for dense, 16-byte aligned inputs: an ahead-of-time build check (and disk-cache
+    warm-up) that surfaces codegen errors before a GPU run.  Returns the number of regions."""
+    from ..core import dtypes as _dt
+
+    fus = fusions(trace)
+    for fb in fus:
+        f = fb._call_ctx[fb.sym.name]
+        targs = {}
+        for p in (f.inputs[i] for i in f.tensor_pos):
+            shape = tuple(int(x) for x in p.shape)
+            targs[p.name] = cg.TensorArg(shape, cg._contig_strides(shape), _dt.to_torch_dtype(p.dtype), True)
+        compile_source(cg.generate(f.plan, f.inputs, f.outputs, targs))  # one source: main + pre / extra kernels
+    return len(fus)
+
+
 def load_kernel(ks: cg.KernelSource, name: str | None = None):
     data = compile_source(ks)
     lib = _lib()
@@ -657,6 +674,8 @@ def _rematerialize_between_regions(items: list) -> dict:
                 ok = True
                 while stack and ok:
                     n = stack.pop()
+                    if n in made:  # already computed inside the consumer (an earlier recomputed cone)
+                        continue
                     b = prod.get(n)
                     if b is None or id(b) in seen:
                         continue
@@ -675,10 +694,11 @@ def _rematerialize_between_regions(items: list) -> dict:
                 extra = sum(_tensor_bytes(a) for n, a in reads.items() if n not in ext_names)
                 if extra >= 2 * _tensor_bytes(x):
                     continue
+                merged = _topo_order(cone + list(g2))
                 trial = cg.Plan()
-                if not all(trial.try_add(b) for b in cone + list(g2)) or trial.has_pending():
+                if not all(trial.try_add(b) for b in merged) or trial.has_pending():
                     continue
-                items[j] = (trial, cone + list(g2))
+                items[j] = (trial, merged)
                 remat.setdefault(j, set()).update(cone_made)
                 uses[x.name].discard(j)
                 for n in reads:
@@ -688,6 +708,30 @@ def _rematerialize_between_regions(items: list) -> dict:
             if not done:
                 break
     return remat
+
+
+def _topo_order(bsyms: list) -> list:
+    """``bsyms`` in a dependency-respecting order, as close to the given order as possible (a
+    recomputed cone may read values an earlier recomputed cone defines inside the consumer)."""
+    prod = {}
+    for k, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            prod.setdefault(o.name, k)
+    out, placed = [], set()
+
+    def place(k, stack=()):
+        if k in placed:
+            return
+        for a in bsyms[k].flat_proxy_args:
+            d = prod.get(a.name)
+            if d is not None and d != k and d not in stack:
+                place(d, stack + (k,))
+        placed.add(k)
+        out.append(bsyms[k])
+
+    for k in range(len(bsyms)):
+        place(k)
+    return out
 
 
 def _replan(group):

@@ -1835,6 +1835,253 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __
   }
 }
 
+// dQ v4: v3's data flow with the VALU work of a tile in the MFMA shadows (as dK/dV v4):
+//   A: S^T half 0 (8 MFMA), S^T half 1 (8) | P half 0      B0: dP^T half 0 (8) | P half 1
+//   B1: dP^T half 1 (8) | dS^T half 0, pack                 C0: dQ^T half 0 (8) | dS^T half 1, pack
+//   C1: dQ^T half 1 (8)
+// The dP^T chains start at -delta (row constant as the initial accumulator), so dS^T = P * acc.
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                                     const T* __restrict__ V, const T* __restrict__ dO,
+                                                                     const float* __restrict__ LSE,
+                                                                     const float* __restrict__ DELTA, T* __restrict__ dQ,
+                                                                     int Hq, int Hkv, int Tq, int Sk, float scale,
+                                                                     float scale_log2, RowStrides sdo, QKVStrides sx) {
+  constexpr int D = 128;
+  using C = BCfg<D>;
+  using F = typename Frag<T>::type;
+  constexpr int NST = 3;
+  constexpr int IMG = kKT3 * 256;  // 32 rows x 128 x 16-bit
+  constexpr int STAGE = 2 * IMG;   // K image, V image
+  constexpr int OOFF = NST * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[OOFF + kQB3 * C::RSTR * 2];
+  short* Os = reinterpret_cast<short*>(smem + OOFF);
+
+  const int n_qb = (Tq + kQB3 - 1) / kQB3;
+  const int qb = n_qb - 1 - (int)blockIdx.y;  // heaviest causal blocks first
+  const int bh = blockIdx.x;
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hk = hq / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qw = qb * kQB3 + wave * 64;  // this wave's first query; half j: queries qw + 32 j + r
+  const T* Qb = Q + b * sx.qb + hq * sx.qh;
+  const T* dOb = dO + b * sdo.b + hq * sdo.h;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Vb = V + b * sx.vb + hk * sx.vh;
+
+  // dO rows of the workgroup's 256 queries -> LDS; Q rows and row statistics of this wave's 64
+  // queries -> registers (rows past Tq are clamped copies; their dQ is not stored)
+#pragma unroll
+  for (int c = 0; c < kQB3 * C::CH / kThreads; ++c) {
+    const int id = c * kThreads + tid;
+    const int row = id / C::CH, ch = id % C::CH;
+    const int orow = min(qb * kQB3 + row, Tq - 1);
+    *reinterpret_cast<uint4*>(Os + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(dOb + (int64_t)orow * sdo.t + ch * 8);
+  }
+  constexpr float kLog2e = 1.44269504088896340736f;
+  F qf[2][C::KS];
+  float nl2[2], dl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qr = min(qw + 32 * j + r, Tq - 1);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[j][s] = load_frag<F>(Qb + (int64_t)qr * sx.qt + 16 * s + 8 * h);
+    nl2[j] = -LSE[((int64_t)b * Hq + hq) * Tq + qr] * kLog2e;
+    dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+  }
+
+  f32x16 dqacc[2][C::DT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dqacc[j][dt][i] = 0.f;
+
+  int n_kt = (Sk + kKT3 - 1) / kKT3;
+  if (CAUSAL) n_kt = min(n_kt, (min(qb * kQB3 + kQB3, Tq) + kKT3 - 1) / kKT3);
+
+  // one 32-key tile: 8 x 1 KiB of K and of V per workgroup, lane-linear DMA into layout (a)
+  // (the swizzle is applied to the source row / chunk; see dK/dV v3)
+  auto issue = [&](int t, int st) {
+    char* kimg = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = wave * 2 + i;
+      const int u = 64 * k + lane;
+      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
+      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
+      const int kc = min(t * kKT3 + row, Sk - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)kc * sx.kt + ch * 8), (lds_void*)(kimg + k * 1024), 16,
+                                       0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)kc * sx.vt + ch * 8),
+                                       (lds_void*)(kimg + IMG + k * 1024), 16, 0, 0);
+    }
+  };
+  if (n_kt > 0) issue(0, 0);
+  if (n_kt > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed (tile 1 may be in flight)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  unsigned tr_a, tr_b;
+  {
+    const int l16 = lane & 15, g = lane >> 4;
+    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
+    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
+  }
+  int st = 0;
+  for (int t = 0; t < n_kt; ++t) {
+    const bool issue_next = t + 2 < n_kt;
+    const int st2 = st >= 1 ? st - 1 : 2;
+    if (issue_next) issue(t + 2, st2);
+    const char* kimg = smem + st * STAGE;
+    const char* vimg = kimg + IMG;
+    const short* o0 = Os + (wave * 64 + r) * C::RSTR + 8 * h;  // dO rows of half 0 (half 1: + 32 rows)
+    const int kbase = t * kKT3;
+    f32x16 sacc[2], pacc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        sacc[j][i] = 0.f;
+        pacc[j][i] = -dl[j];  // the dP^T chain starts at -delta: it ends as dP - delta
+      }
+    auto exp_slice = [&](int j, int i0, int n) {
+#pragma unroll
+      for (int i = i0; i < i0 + n; ++i)
+        sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, nl2[j]));
+    };
+    auto mask_half = [&](int j) {  // wave-uniform: only tiles on the diagonal or the key edge
+      const int qi = qw + 32 * j + r;
+      if (kbase + kKT3 > Sk || (CAUSAL && kbase + kKT3 - 1 > qw + 32 * j)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kbase + acc_row(i, h);
+          if (key >= Sk || (CAUSAL && key > qi)) sacc[j][i] = 0.f;
+        }
+      }
+    };
+    // phase A: S^T = K Q^T, half 0 then half 1; P of half 0 in the second chain's shadow
+    F fa[C::KS];
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) fa[s] = load_frag<F>(kimg + du_off(r, 2 * s + h));
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) sacc[0] = mfma(fa[s], qf[0][s], sacc[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      sacc[1] = mfma(fa[s], qf[1][s], sacc[1]);
+      exp_slice(0, 2 * s, 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mask_half(0);
+    // V fragments (A operand of both dP^T chains) replace the K fragments
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) fa[s] = load_frag<F>(vimg + du_off(r, 2 * s + h));
+    // phase B0: dP^T of half 0 | P of half 1
+    {
+      F oa = load_frag<F>(o0);
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        F ob = oa;
+        if (s + 1 < C::KS) ob = load_frag<F>(o0 + 16 * (s + 1));
+        pacc[0] = mfma(fa[s], oa, pacc[0]);
+        exp_slice(1, 2 * s, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        oa = ob;
+      }
+    }
+    mask_half(1);
+    // K^T transposed reads for the dQ chains go out now (waited before phase C)
+    s16x4t xr[16];
+    tr_issue16(xr, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));
+    // phase B1: dP^T of half 1 | dS^T = P (dP - delta) of half 0 (its chain is complete), packed
+    F df[2][2];
+    {
+      F oa = load_frag<F>(o0 + 32 * C::RSTR);
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        F ob = oa;
+        if (s + 1 < C::KS) ob = load_frag<F>(o0 + 32 * C::RSTR + 16 * (s + 1));
+        pacc[1] = mfma(fa[s], oa, pacc[1]);
+#pragma unroll
+        for (int i = 2 * s; i < 2 * s + 2; ++i) pacc[0][i] *= sacc[0][i];
+        asm volatile("" : "+v"(pacc[0]));  // keep the slice here (sched_barrier does not stop IR sinking)
+        if (s == 7) {
+          pack_frag(df[0][0], pacc[0], 0);
+          pack_frag(df[0][1], pacc[0], 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        oa = ob;
+      }
+    }
+    {
+      F xt[8];
+      tr_wait16(xt, xr);
+      // phase C0: dQ^T += K^T dS^T of half 0 | dS^T of half 1, packed
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        mfma_acc_agpr(dqacc[0][dt], xt[2 * dt], df[0][0]);
+        mfma_acc_agpr(dqacc[0][dt], xt[2 * dt + 1], df[0][1]);
+#pragma unroll
+        for (int i = 4 * dt; i < 4 * dt + 4; ++i) pacc[1][i] *= sacc[1][i];
+        asm volatile("" : "+v"(pacc[1]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pack_frag(df[1][0], pacc[1], 0);
+      pack_frag(df[1][1], pacc[1], 1);
+      // phase C1: dQ^T of half 1
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        mfma_acc_agpr(dqacc[1][dt], xt[2 * dt], df[1][0]);
+        mfma_acc_agpr(dqacc[1][dt], xt[2 * dt + 1], df[1][1]);
+      }
+    }
+    if (issue_next)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile t+1 landed; t+2 may be in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    st = st == 2 ? 0 : st + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dqacc[j][dt]));
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qi = qw + 32 * j + r;
+    if (qi < Tq) {
+      T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int d = dt * 32 + 8 * a + 4 * h;
+          union {
+            T v[4];
+            uint2 u;
+          } pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(dqacc[j][dt][4 * a + e] * scale);
+          *reinterpret_cast<uint2*>(drow + d) = pk.u;
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int D, int EX>
 void launch_masked(const void* dO, const void* Q, const void* K, const void* V, const void* LSE, void* DELTA, void* dQ,
                    void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, float sl2, int causal,
@@ -1860,7 +2107,7 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 }
 
 int g_dkdv_v3 = 2;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
-int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 2 = v3, 1 = v2 (8 waves), 0 = v1
+int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 3 = v4, 2 = v3, 1 = v2 (8 waves), 0 = v1
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -1923,7 +2170,15 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
                        sl2, sdo, ex);
-  if (D == 128 && g_dq_v2 == 2 && Tq > 0 && Sk > 0) {
+  if (D == 128 && g_dq_v2 == 3 && Tq > 0 && Sk > 0) {
+    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
+  } else if (D == 128 && g_dq_v2 == 2 && Tq > 0 && Sk > 0) {
     dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
@@ -2049,7 +2304,7 @@ LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void
 // dQ kernel selection (A/B measurement hook): 1 = v2, 0 = v1; returns the previous choice
 LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
   const int old = g_dq_v2;
-  if (impl >= 0 && impl <= 2) g_dq_v2 = impl;
+  if (impl >= 0 && impl <= 3) g_dq_v2 = impl;
   return old;
 }
 

@@ -1,10 +1,10 @@
-"""dQ v3 (256 queries per workgroup, LDS-DMA K/V ring) vs v2: numerics on odd shapes and timing
-at the Llama-2-7B shape.
+"""dQ v3 / v4 (256 queries per workgroup, LDS-DMA K/V ring; v4 with the VALU in the MFMA shadows)
+vs v2: numerics on odd shapes and timing at the Llama-2-7B shape.
 
     python scripts/attn_dq_v3_check.py
-Prints per case the max |v3 - v2| of dQ/dK/dV (same arithmetic in the same key order, so this
-should be ~0) and the fp32-reference error of v3 for small shapes; then the backward time
-(preprocess + dK/dV + dQ) per implementation, median of interleaved rounds.
+Prints per case the max |vN - v2| of dQ/dK/dV (v3: same arithmetic in the same key order, ~0;
+v4 starts the dP chain at -delta, so it differs by rounding) and the fp32-reference error; then
+the backward time (preprocess + dK/dV + dQ) per implementation, median of interleaved rounds.
 """
 import ctypes
 import math
@@ -48,24 +48,25 @@ for (B, Hq, Hkv, T, causal) in [(1, 4, 4, 1024, True), (2, 8, 2, 1000, True), (1
     v = torch.randn_like(k)
     do = torch.randn_like(q)
     o, lse = attn_fwd(q, k, v, causal)
-    g3 = run(1, do, q, k, v, o, lse, causal)  # v2
-    g4 = run(2, do, q, k, v, o, lse, causal)  # v3
-    d = [(a.float() - b.float()).abs().max().item() for a, b in zip(g3, g4)]
+    g2 = run(1, do, q, k, v, o, lse, causal)  # v2
     r = ref_bwd(do, q, k, v, causal)
-    e = [((a.float() - b).abs().max() / b.abs().max()).item() for a, b in zip(g4, r)]
-    ok = max(d) < 1e-2 and max(e) < 2e-2 and all(torch.isfinite(t).all() for t in g4)
-    bad |= not ok
-    print(f"B{B} H{Hq}/{Hkv} T{T} {'causal' if causal else 'full'}: |v3-v2| {['%.2e' % x for x in d]} "
-          f"rel err vs fp32 {['%.2e' % x for x in e]} {'ok' if ok else 'BAD'}", flush=True)
+    for impl in (2, 3):
+        gn = run(impl, do, q, k, v, o, lse, causal)
+        d = [(a.float() - b.float()).abs().max().item() for a, b in zip(g2, gn)]
+        e = [((a.float() - b).abs().max() / b.abs().max()).item() for a, b in zip(gn, r)]
+        ok = max(d) < 2e-2 and max(e) < 2e-2 and all(torch.isfinite(t).all() for t in gn)
+        bad |= not ok
+        print(f"B{B} H{Hq}/{Hkv} T{T} {'causal' if causal else 'full'}: |v{impl + 1}-v2| {['%.2e' % x for x in d]} "
+              f"rel err vs fp32 {['%.2e' % x for x in e]} {'ok' if ok else 'BAD'}", flush=True)
 
 q = torch.randn(1, 32, 4096, 128, device="cuda", dtype=torch.bfloat16)
 k, v = torch.randn_like(q), torch.randn_like(q)
 do = torch.randn(1, 4096, 32, 128, device="cuda", dtype=torch.bfloat16).transpose(1, 2)
 for causal in (True, False):
     o, lse = attn_fwd(q, k, v, causal)
-    times = {1: [], 2: []}
+    times = {1: [], 2: [], 3: []}
     for _ in range(3):
-        for impl in (1, 2):
+        for impl in (1, 2, 3):
             for _ in range(3):
                 run(impl, do, q, k, v, o, lse, causal)
             torch.cuda.synchronize()
@@ -77,7 +78,7 @@ for causal in (True, False):
             e.synchronize()
             times[impl].append(s.elapsed_time(e) / 10 * 1000)
     fl = 2.5 * 4 * 4096 * 4096 * 128 * 32 / (2 if causal else 1)
-    for impl in (1, 2):
+    for impl in (1, 2, 3):
         us = sorted(times[impl])[1]
         print(f"{'causal' if causal else 'full'} dq v{impl + 1}: bwd {us:.1f} us  {fl / us / 1e6:.0f} TF/s nominal", flush=True)
 lib.lta_attn_bwd_set_dq_impl(1)

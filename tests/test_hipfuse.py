@@ -517,3 +517,39 @@ def test_repeated_fusions_share_one_kernel(cpu_fusion):
     assert len(names) >= 6 and len(set(names)) < len(names), names  # per-layer regions dedupe
     src = cg._canonical_names("float v_t12[8]; v_t12[j] = r_t3 + v_t12[j]; v8_float q; r_t3 = 1;")
     assert src == "float v_n0[8]; v_n0[j] = r_n1 + v_n0[j]; v8_float q; r_n1 = 1;"
+
+
+def _compile_fusions_of(jf):
+    """Every region's kernel source, compiled with hiprtc on the CPU (hipfuse.precompile)."""
+    return hipfuse.precompile(thunder.last_traces(jf)[-1])
+
+
+_SOURCE_CASES = {
+    # ops whose decompositions put a constant (full) into several regions: the consumer region
+    # recomputes the producer cones (fusion-region rematerialisation) without defining a value twice
+    "heaviside": (lambda a, b: torch.heaviside(a, b), lambda: (torch.randn(2, 3, 8, 8), torch.randn(2, 3, 8, 8))),
+    "bce": (lambda a, b: torch.nn.functional.binary_cross_entropy(torch.sigmoid(a), torch.sigmoid(b)),
+            lambda: (torch.randn(4, 33), torch.randn(4, 33))),
+    "gaussian_nll": (lambda a, b, v: torch.nn.functional.gaussian_nll_loss(a, b, v.abs() + 0.1),
+                     lambda: (torch.randn(8, 12), torch.randn(8, 12), torch.randn(8, 12))),
+    "interp": (lambda a: torch.nn.functional.interpolate(a, scale_factor=1.6, mode="linear"),
+               lambda: (torch.randn(2, 3, 5),)),
+}
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs ROCm hiprtc")
+@pytest.mark.parametrize("case", sorted(_SOURCE_CASES) + ["slice_mix", "cat_mix", "gather_mix", "remat_regions",
+                                                          "pad_sum", "ln_gelu_softmax"])
+def test_generated_sources_compile_cpu(case, cpu_fusion):
+    if case in _SOURCE_CASES:
+        fn, mk = _SOURCE_CASES[case]
+        args = mk()
+    else:
+        fn, mk = CASES[case]
+        args = mk(torch.float32, "cpu")
+    jf = thunder.jit(fn, executors=["hipfuse", "torch"])
+    out = jf(*args)
+    ref = fn(*args)
+    for o, r in zip(out if isinstance(out, tuple) else (out,), ref if isinstance(ref, tuple) else (ref,)):
+        torch.testing.assert_close(o, r, rtol=1e-5, atol=1e-5)
+    assert _compile_fusions_of(jf) >= 1

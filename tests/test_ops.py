@@ -149,3 +149,25 @@ def test_hipfuse_partition_consistency(opinfo, dtype, hipfuse_on_cpu):
             expected = opinfo.op(*sample.args, **sample.kwargs)
             got = jfn(*sample.args, **sample.kwargs)
             _compare(got, expected, opinfo, dtype)
+
+
+@pytest.mark.skipif(not __import__("os").path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs ROCm hiprtc")
+@pytest.mark.parametrize("opinfo", [pytest.param(o, id=o.name) for o in OPS if torch.float32 in o.dtypes])
+def test_hipfuse_codegen_cpu(opinfo):
+    """Every op through the hipfuse partitioner on CPU (regions run by the reference path, checked
+    against eager) with each region's generated HIP kernel compiled by hiprtc for gfx950 — the
+    GPU-side codegen checked without a GPU."""
+    from lightning_thunder_amd.executors import hipfuse
+
+    old = hipfuse.ex.allow_cpu
+    hipfuse.ex.allow_cpu = True
+    try:
+        torch.manual_seed(1234)
+        jfn = thunder.jit(opinfo.op, executors=["hipfuse", "torch"])
+        for sample in opinfo.samples("cpu", torch.float32, False):
+            expected = opinfo.op(*sample.args, **sample.kwargs)
+            got = jfn(*sample.args, **sample.kwargs)
+            _compare(got, expected, opinfo, torch.float32)
+            hipfuse.precompile(thunder.last_traces(jfn)[-1])
+    finally:
+        hipfuse.ex.allow_cpu = old
