@@ -239,7 +239,13 @@ def _hf_arch(name):
 @pytest.mark.parametrize("name", ["gpt2", "mistral", "qwen2", "phi", "gemma", "t5", "vit", "roberta", "mixtral", "falcon"])
 def test_hf_architectures_fwd_bwd(name):
     """HF transformers architectures through the interpreter: outputs and parameter gradients
-    match eager (reference analogue: thunder/tests/test_networks.py HF model tests)."""
+    match eager (reference analogue: thunder/tests/test_networks.py HF model tests).  hipfuse
+    partitions the CPU program too (its regions run the reference path) and every generated
+    kernel is compiled for gfx950 with hiprtc."""
+    import os
+
+    from lightning_thunder_amd.executors import hipfuse
+
     torch.manual_seed(0)
     model, inputs = _hf_arch(name)
     model.eval()
@@ -248,12 +254,21 @@ def test_hf_architectures_fwd_bwd(name):
     ref.float().pow(2).mean().backward()
     ref_grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
     model.zero_grad()
-    out = getattr(thunder.jit(model)(**inputs), key)
-    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
-    out.float().pow(2).mean().backward()
+    old = hipfuse.ex.allow_cpu
+    hipfuse.ex.allow_cpu = True
+    try:
+        jm = thunder.jit(model)
+        out = getattr(jm(**inputs), key)
+        torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+        out.float().pow(2).mean().backward()
+    finally:
+        hipfuse.ex.allow_cpu = old
     for n, g in ref_grads.items():
         p = dict(model.named_parameters())[n]
         torch.testing.assert_close(p.grad, g, atol=1e-4, rtol=1e-3, msg=n)
+    if os.path.exists("/opt/rocm/lib/libhiprtc.so"):
+        for tr in (thunder.last_traces(jm)[-1], thunder.last_backward_traces(jm)[-1]):
+            hipfuse.precompile(tr)
 
 
 @pytest.mark.gpu
