@@ -1004,9 +1004,71 @@ def _fuse_qkv_rope_gemm(trace):
     return new
 
 
+def _attn_bwd_rope_meta(g, q, k, v, o, lse, causal, scale, cos, sin, n_head, n_query_groups):
+    B, _, T, D = q.shape
+    return TensorProxy(like=g, shape=(B, T, (n_head + 2 * n_query_groups) * D))
+
+
+def _attn_bwd_rope_impl(g, q, k, v, o, lse, causal, scale, cos, sin, n_head, n_query_groups):
+    from ..ops.attention import attn_bwd_rope
+
+    return attn_bwd_rope(g, q, k, v, o, lse, causal, scale, cos, sin, n_head, n_query_groups)
+
+
+hip_attn_bwd_rope = ex.register_operator("hip_flash_attn_bwd_rope", meta=_attn_bwd_rope_meta, fn=_attn_bwd_rope_impl)
+
+
+def _fuse_attn_bwd_rope(trace):
+    """``dq, dk, dv = hip_flash_attn_bwd(...); dqkv = hip_qkv_rope_bwd(dq, dk, dv, cos, sin, ...)``
+    (dq / dk / dv read nowhere else, full-width rotate-half RoPE on 128-wide heads) ->
+    ``dqkv = hip_flash_attn_bwd_rope(..., cos, sin, n_head, n_query_groups)``: the RoPE backward
+    runs in the attention backward's dQ / dK epilogues and the three gradients are stored straight
+    into the fused projection's gradient (the mirror of the qkv-RoPE GEMM epilogue of the forward)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = trace.bound_symbols
+    uses: dict[str, int] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            uses[a.name] = uses.get(a.name, 0) + 1
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_qkv_rope_bwd or len(b.args) != 9:
+            continue
+        gq, gk, gv, cos, sin, nh, ng, hs, rn = b.args
+        if not all(isinstance(t, TensorProxy) for t in (gq, gk, gv, cos, sin)) or hs != 128 or rn != hs:
+            continue
+        j = producer.get(gq.name)
+        if j is None or j in drop or bsyms[j].sym is not hip_attn_bwd:
+            continue
+        ab = bsyms[j]
+        if tuple(o.name for o in ab.flat_proxy_outs) != (gq.name, gk.name, gv.name):
+            continue
+        if any(uses.get(t.name, 0) != 1 for t in (gq, gk, gv)):
+            continue
+        g, q, k, v, o, lse, causal, scale = ab.args
+        if q.shape[1] != nh or k.shape[1] != ng or q.shape[2] != k.shape[2]:
+            continue
+        replace[i] = ex.bind_call_ctx(hip_attn_bwd_rope.bind(g, q, k, v, o, lse, causal, scale, cos, sin, nh, ng,
+                                                             output=b.output))
+        drop.add(j)
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} RoPE backward(s) fused into the attention backward"))
+    return new
+
+
 def _post_claim(trace):
-    return _fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
-        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace)))))))
+    return _fuse_attn_bwd_rope(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
+        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace))))))))
 
 
 ex.post_claim_pass = _post_claim

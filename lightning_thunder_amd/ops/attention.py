@@ -34,6 +34,9 @@ register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_v
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
                                         ctypes.c_uint64, c_void_p, c_void_p])
+register_signature("lta_attn_bwd_rope", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
 register_signature("lta_attn_bwd_ex3", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
@@ -205,6 +208,41 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     if dims:
         g = g.sum(dims, keepdim=True)
     return dq, dk, dv, g.to(mask.dtype)
+
+
+def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):
+    """The attention backward and the backward of the rotate-half RoPE + qkv split in one pass:
+    returns d(qkv) [B, T, (n_head + 2 n_query_groups) * 128], with dQ / dK rotated back in the
+    dK/dV and dQ kernels' epilogues and stored (like dV) straight into their columns of the fused
+    projection's gradient (no dq / dk / dv tensors, no separate RoPE-backward pass).  Falls back to
+    ``attn_bwd`` + ``ops.fused.qkv_rope_bwd`` when the kernels do not cover the case."""
+    lib = require()
+    B, Hq, T, D = q.shape
+    Hkv, S = k.shape[1], k.shape[2]
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    if D == 128 and S == T and Hq == n_head and Hkv == n_query_groups:
+        qq, kk, vv, qkv_st = _qkv_in_place(q, k, v)
+        dd = do if _rows_ok(do) else do.contiguous()
+        oo = o if _rows_ok(o) else o.contiguous()
+        cs = cos[:T].float().contiguous()
+        sn = sin[:T].float().contiguous()
+        W = (Hq + 2 * Hkv) * D
+        dqkv = torch.empty((B, T, W), device=q.device, dtype=q.dtype)
+        gst = (ctypes.c_int64 * 9)(T * W, D, W, T * W, D, W, T * W, D, W)
+        delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
+        st = (ctypes.c_int64 * 6)(*dd.stride()[:3], *oo.stride()[:3])
+        esz = dqkv.element_size()
+        rc = lib.lta_attn_bwd_rope(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
+                                   ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq, Hkv, T,
+                                   S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ctypes.cast(qkv_st, c_void_p),
+                                   ctypes.cast(gst, c_void_p), ptr(cs), ptr(sn), stream_ptr(q.device))
+        if rc != -1:
+            check(rc, "lta_attn_bwd_rope")
+            return dqkv
+    from .fused import qkv_rope_bwd
+
+    dq, dk, dv = attn_bwd(do, q, k, v, o, lse, causal, sc)
+    return qkv_rope_bwd(dq, dk, dv, cos, sin, n_head, n_query_groups, D, D)
 
 
 # ------------------------------------------------------------------------------------------------

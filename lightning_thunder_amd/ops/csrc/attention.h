@@ -81,14 +81,20 @@ struct QKVStrides {
   // their operands (e.g. [B, T, H, D] for heads split from a fused projection), so the usual
   // transpose + reshape back to [B, T, H*D] that follows is a view instead of a copy
   int64_t dqb, dqh, dqt, dkb, dkh, dkt, dvb, dvh, dvt;
+  // backward only, optional: fp32 [T][D] cos / sin of a rotate-half RoPE applied to q and k in the
+  // forward; dQ and dK are then stored with the rotation's transpose applied (the RoPE backward
+  // fused into the attention backward's epilogue)
+  const float* rope_cos;
+  const float* rope_sin;
   static QKVStrides contiguous(int Hq, int Hkv, int Tq, int Sk, int D) {
     const int64_t q[3] = {(int64_t)Hq * Tq * D, (int64_t)Tq * D, D}, k[3] = {(int64_t)Hkv * Sk * D, (int64_t)Sk * D, D};
-    return {q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2], q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2]};
+    return {q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2], q[0], q[1], q[2], k[0], k[1], k[2], k[0], k[1], k[2],
+            nullptr, nullptr};
   }
   static QKVStrides from(const int64_t* s, int Hq, int Hkv, int Tq, int Sk, int D) {
     QKVStrides r = contiguous(Hq, Hkv, Tq, Sk, D);
     if (s) r = QKVStrides{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], r.dqb, r.dqh, r.dqt,
-                          r.dkb, r.dkh, r.dkt, r.dvb, r.dvh, r.dvt};
+                          r.dkb, r.dkh, r.dkt, r.dvb, r.dvh, r.dvt, nullptr, nullptr};
     return r;
   }
   void set_grad(const int64_t* g) {  // optional int64[9]: dQ, dK, dV (batch, head, token) strides

@@ -75,6 +75,52 @@ __device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const f16x8& a, const
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// One lane's 128-wide row of a dQ^T / dK^T / dV^T accumulator set (d-tile dt, element i: d = dt*32 +
+// acc_row(i, h)) times `mul` -> the T row at `row` (4 consecutive d per 8-byte store).  With `cs` / `sn`
+// (this token's fp32 cos / sin rows) the transpose of the rotate-half RoPE is applied on the fp32
+// values first — d and its partner d + 64 are tiles dt and dt + 2 of the same lane:
+//   o[d] = x[d] cos[d] + x[d+64] sin[d+64],  o[d+64] = x[d+64] cos[d+64] - x[d] sin[d]
+// (the rotation the forward applied to q / k, transposed: csrc/rope.hip's backward, one rounding).
+template <typename T, typename ACC>
+__device__ __forceinline__ void store_row_d128(T* row, const ACC& acc, float mul, int h, const float* cs,
+                                               const float* sn) {
+  union P4 {
+    T v[4];
+    uint2 u;
+  };
+  if (cs == nullptr) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        P4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(acc[dt][4 * a + e] * mul);
+        *reinterpret_cast<uint2*>(row + dt * 32 + 8 * a + 4 * h) = pk.u;
+      }
+    return;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int d = dt * 32 + 8 * a + 4 * h;
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + d), s1 = *reinterpret_cast<const float4*>(sn + d);
+      const float4 c2 = *reinterpret_cast<const float4*>(cs + d + 64), s2 = *reinterpret_cast<const float4*>(sn + d + 64);
+      const float cl[4] = {c1.x, c1.y, c1.z, c1.w}, sl[4] = {s1.x, s1.y, s1.z, s1.w};
+      const float ch[4] = {c2.x, c2.y, c2.z, c2.w}, sh[4] = {s2.x, s2.y, s2.z, s2.w};
+      P4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = acc[dt][4 * a + e] * mul, x2 = acc[dt + 2][4 * a + e] * mul;
+        lo.v[e] = from_f32<T>(x1 * cl[e] + x2 * sh[e]);
+        hi.v[e] = from_f32<T>(x2 * ch[e] - x1 * sl[e]);
+      }
+      *reinterpret_cast<uint2*>(row + d) = lo.u;
+      *reinterpret_cast<uint2*>(row + d + 64) = hi.u;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // dK / dV
 // ---------------------------------------------------------------------------------------------
@@ -1233,24 +1279,10 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
     if (key < Sk) {
       T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
       T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int d = dt * 32 + 8 * a + 4 * h;
-          union {
-            T v[4];
-            uint2 u;
-          } pk, pv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            pk.v[e] = from_f32<T>(dkacc[j][dt][4 * a + e] * scale);
-            pv.v[e] = from_f32<T>(dvacc[j][dt][4 * a + e]);
-          }
-          *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
-          *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
-        }
-      }
+      const bool rope = sx.rope_cos != nullptr;
+      store_row_d128(dkrow, dkacc[j], scale, h, rope ? sx.rope_cos + (int64_t)key * 128 : nullptr,
+                     rope ? sx.rope_sin + (int64_t)key * 128 : nullptr);
+      store_row_d128(dvrow, dvacc[j], 1.f, h, nullptr, nullptr);
     }
   }
 }
@@ -1606,20 +1638,9 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
 
   if (qi < Tq) {
     T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int d = dt * 32 + 8 * a + 4 * h;
-        union {
-          T v[4];
-          uint2 u;
-        } pk2;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pk2.v[e] = from_f32<T>(dqacc[dt][4 * a + e] * scale);
-        *reinterpret_cast<uint2*>(drow + d) = pk2.u;
-      }
-    }
+    const bool rope = sx.rope_cos != nullptr;
+    store_row_d128(drow, dqacc, scale, h, rope ? sx.rope_cos + (int64_t)qi * 128 : nullptr,
+                   rope ? sx.rope_sin + (int64_t)qi * 128 : nullptr);
   }
 }
 
@@ -1817,20 +1838,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __
     const int qi = qw + 32 * j + r;
     if (qi < Tq) {
       T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int d = dt * 32 + 8 * a + 4 * h;
-          union {
-            T v[4];
-            uint2 u;
-          } pk;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(dqacc[j][dt][4 * a + e] * scale);
-          *reinterpret_cast<uint2*>(drow + d) = pk.u;
-        }
-      }
+      const bool rope = sx.rope_cos != nullptr;
+      store_row_d128(drow, dqacc[j], scale, h, rope ? sx.rope_cos + (int64_t)qi * 128 : nullptr,
+                     rope ? sx.rope_sin + (int64_t)qi * 128 : nullptr);
     }
   }
 }
@@ -2064,20 +2074,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v4_kernel(const T* __
     const int qi = qw + 32 * j + r;
     if (qi < Tq) {
       T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int d = dt * 32 + 8 * a + 4 * h;
-          union {
-            T v[4];
-            uint2 u;
-          } pk;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(dqacc[j][dt][4 * a + e] * scale);
-          *reinterpret_cast<uint2*>(drow + d) = pk.u;
-        }
-      }
+      const bool rope = sx.rope_cos != nullptr;
+      store_row_d128(drow, dqacc[j], scale, h, rope ? sx.rope_cos + (int64_t)qi * 128 : nullptr,
+                     rope ? sx.rope_sin + (int64_t)qi * 128 : nullptr);
     }
   }
 }
@@ -2206,6 +2205,44 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
 
 }  // namespace
 
+static int dkdv_v2_enabled() {
+  static const int v2 = [] {
+    const char* e = getenv("LTA_ATTN_BWD_V1");  // A/B switch: the v1 dK/dV kernel
+    return (e && e[0] == '1') ? 0 : 1;
+  }();
+  return v2;
+}
+
+// Attention backward with the RoPE backward fused into the dQ / dK epilogues (self-attention,
+// D = 128, no mask / dropout, dK/dV v4 + dQ v2..v4): rope_cos / rope_sin are fp32 [Tq][128] (the
+// forward rotated q and k with them), dQ / dK / dV may point into one [B, T, (Hq + 2 Hkv) * 128]
+// buffer through grad_strides, so the attention input projection's gradient is written in place.
+// Returns -1 when the configuration is not covered (the caller runs the two passes instead).
+LTA_EXPORT int lta_attn_bwd_rope(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
+                                 const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
+                                 int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
+                                 const int64_t* qkv_strides, const int64_t* grad_strides, const float* rope_cos,
+                                 const float* rope_sin, hipStream_t stream) {
+  if (D != 128 || Tq != Sk || Tq <= 0 || Hq % Hkv != 0 || !rope_cos || !rope_sin || g_dkdv_v3 != 2 || g_dq_v2 < 1 ||
+      !dkdv_v2_enabled())
+    return -1;
+  const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
+  const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
+  const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
+  AttnExtra ex{};
+  ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
+  ex.sx.set_grad(grad_strides);
+  ex.sx.rope_cos = rope_cos;
+  ex.sx.rope_sin = rope_sin;
+  if (dtype == kBF16)
+    return launch_bwd<__hip_bfloat16, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo,
+                                           so, 1, ex, 0, stream);
+  if (dtype == kF16)
+    return launch_bwd<__half, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo, so, 1,
+                                   ex, 0, stream);
+  return -1;
+}
+
 // strides: optional int64[6] = dO (batch, head, token), O (batch, head, token) element strides
 // (head dim contiguous); null = contiguous [B,H,T,D] for both.  mask / dropout as lta_attn_fwd_ex;
 // dmask (optional, needs mask): fp32 [B][Hq][Tq][Sk] receives dS, the additive mask's gradient
@@ -2222,10 +2259,7 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
   const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
-  static const int v2 = [] {
-    const char* e = getenv("LTA_ATTN_BWD_V1");  // A/B switch: the v1 dK/dV kernel
-    return (e && e[0] == '1') ? 0 : 1;
-  }();
+  const int v2 = dkdv_v2_enabled();
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
   ex.sx.set_grad(grad_strides);

@@ -80,6 +80,8 @@ def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
         assert "hip_gate_up" in fw and "hip_swiglu(" not in fw, fw
         assert "hip_matmul_swiglu_bwd" in bw and "hip_swiglu_bwd(" not in bw, bw
     assert "hip_linear_qkv_rope" in fw and "hip_qkv_rope(" not in fw, fw
+    # ... and its backward in the attention backward's dQ / dK epilogues
+    assert "hip_flash_attn_bwd_rope" in bw and "hip_qkv_rope_bwd(" not in bw, bw
     from lightning_thunder_amd.ops import gemm as G
 
     # every GEMM of the step ran on the hand-written kernel (no library fallback)

@@ -1081,3 +1081,36 @@ def test_moe_training_backward_on_hand_grouped_kernels():
     fw, bw = str(thunder.last_traces(jm)[-1]), str(thunder.last_backward_traces(jm)[-1])
     assert "hip_grouped_mm" in fw and "hip_grouped_mm" in bw
     assert "_grouped_mm(" not in bw.replace("hip_grouped_mm(", ""), bw
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,causal", [(1, 4, 2, 300, True), (2, 4, 4, 256, False), (1, 8, 1, 1000, True)])
+def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
+    """attn_bwd_rope (RoPE backward in the dQ / dK epilogues, gradients stored into d(qkv)) against
+    the two-pass path (attention backward, then the qkv RoPE backward) and an fp32 reference."""
+    from lightning_thunder_amd.models.litgpt import build_rope_cache
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd, attn_bwd_rope
+    from lightning_thunder_amd.ops.fused import qkv_rope_bwd
+
+    torch.manual_seed(0)
+    D = 128
+    cos, sin = build_rope_cache(T, D, device="cuda")
+    q = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    o, lse = attn_fwd(q, k, v, causal)
+    fused = attn_bwd_rope(do, q, k, v, o, lse, causal, None, cos, sin, Hq, Hkv)
+    dq, dk, dv = attn_bwd(do, q, k, v, o, lse, causal)
+    two = qkv_rope_bwd(dq, dk, dv, cos, sin, Hq, Hkv, D, D)
+    assert fused.shape == (B, T, (Hq + 2 * Hkv) * D)
+    # fp32 reference of the same composite: rotate-half RoPE transposed of the fp32 gradients
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    rep = Hq // Hkv
+    s = qf @ kf.repeat_interleave(rep, 1).transpose(-1, -2) / D ** 0.5
+    if causal:
+        s = s.masked_fill(torch.ones(T, T, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
+    (torch.softmax(s, -1) @ vf.repeat_interleave(rep, 1)).backward(do.float())
+    ref = qkv_rope_bwd(qf.grad, kf.grad, vf.grad, cos, sin, Hq, Hkv, D, D)
+    e_fused = ((fused.float() - ref).norm() / ref.norm()).item()
+    e_two = ((two.float() - ref).norm() / ref.norm()).item()
+    assert e_fused < 1e-2 and e_fused <= 1.5 * e_two + 1e-4, (e_fused, e_two)
