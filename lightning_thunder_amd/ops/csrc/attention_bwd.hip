@@ -1482,7 +1482,9 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
                                                                       const float* __restrict__ LSE,
                                                                       const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                       int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                      float scale_log2, RowStrides sdo, QKVStrides sx) {
+                                                                      float scale_log2, RowStrides sdo, QKVStrides sx,
+                                                                      const T* __restrict__ O = nullptr,
+                                                                      RowStrides so = {}) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -1519,7 +1521,23 @@ __global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* _
     of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
   }
   const float nlse2 = -LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
-  const float dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
+  float dlt;
+  if (O != nullptr) {
+    // delta = rowsum(dO * O) here instead of a preprocess launch: the lane pair (r, r + 32) holds the
+    // row's dO in its fragments; the dK/dV kernel, launched after this one, reads what is stored
+    const T* Orow = O + (int64_t)b * so.b + (int64_t)hq * so.h + (int64_t)qrow * so.t;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const F ov = load_frag<F>(Orow + 16 * s + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += (float)of[s][e] * (float)ov[e];
+    }
+    dlt = acc + __shfl_xor(acc, 32, 64);
+    if (h == 0 && qi < Tq) const_cast<float*>(DELTA)[((int64_t)b * Hq + hq) * Tq + qi] = dlt;
+  } else {
+    dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
+  }
 
   f32x16 dqacc[C::DT];
 #pragma unroll
@@ -2114,8 +2132,11 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
                RowStrides sdo, RowStrides so, int dkdv_v2, const AttnExtra& ex, int exf, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
-  hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                     (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
+  // dQ v2 computes delta itself and runs first (the dK/dV kernel reads it): no preprocess launch
+  const bool dq_delta = exf == 0 && D == 128 && g_dq_v2 == 1 && Tq > 0 && Sk > 0;
+  if (!dq_delta)
+    hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                       (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
   if (exf) {  // masks / dropout: the plain-HIP dK/dV kernel with the extra terms compiled in
     if constexpr (D > 128) {
       return -1;  // D = 256: plain (causal / full) attention only
@@ -2138,6 +2159,17 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     }
   }
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
+  if (dq_delta) {
+    dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,
+                         ex.sx, (const T*)O, so);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, false>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,
+                         ex.sx, (const T*)O, so);
+  }
   if (D == 128 && dkdv_v2 && g_dkdv_v3 && Tq > 0 && Sk > 0) {
     dim3 g4(B * Hkv, (Sk + kKB3 - 1) / kKB3);
 #define LTA_DKDV3(KERN, CA)                                                                                          \
@@ -2185,6 +2217,8 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     else
       hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
+  } else if (dq_delta) {
+    // launched before the dK/dV kernel (above)
   } else if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
     dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
     if (causal)
