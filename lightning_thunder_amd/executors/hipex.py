@@ -1449,6 +1449,15 @@ def _broadcastable(shape, target) -> bool:
     return True
 
 
+def _is_decode_shape(query, key, attn_mask) -> bool:
+    from ..ops.attention import DECODE_MAX_QUERIES
+
+    if attn_mask is None or not isinstance(attn_mask, TensorProxy) or attn_mask.dtype != torch.bool:
+        return False
+    B, Hq, T, _ = query.shape
+    return T <= DECODE_MAX_QUERIES and _broadcastable(tuple(attn_mask.shape), (B, Hq, T, key.shape[2]))
+
+
 def _is_decode(query, key, attn_mask) -> bool:
     """Few query rows against a KV cache with a boolean mask: the K3d decode kernel."""
     from ..ops.attention import DECODE_MAX_QUERIES
@@ -1490,6 +1499,8 @@ def _sdpa_checker(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=Fa
         return False
     if D > PLAIN_ONLY_HEAD_DIM and (attn_mask is not None or p > 0.0):
         return False
+    if D not in (64, 128) and _is_decode_shape(query, key, attn_mask):
+        return False  # decode steps at head dims without a decode kernel stay on ATen (padding buys nothing there)
     if key.shape[1] != value.shape[1] or query.shape[1] % key.shape[1] != 0:
         return False
     if key.shape[1] != query.shape[1] and not enable_gqa:

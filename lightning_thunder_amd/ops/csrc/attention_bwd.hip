@@ -1011,7 +1011,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
                                                                        const float* __restrict__ LSE,
                                                                        const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
+                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx,
+                                                                       int qrev = 0) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -1075,7 +1076,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   };
   auto issue = [&](int hi, int ti, int st) {
     const int hq = hk * group + hi;
-    const int qbase = (qt_begin + ti) * kQT;
+    // qrev: every key block sweeps the query tiles from the last one down, so the workgroups of one
+    // head (one XCD: grid x = head) read the same Q / dO tile at about the same time (L2 reuse)
+    const int qbase = (qt_begin + (qrev ? nq - 1 - ti : ti)) * kQT;
     const T* Qb = Q + b * sx.qb + hq * sx.qh;
     const T* dOb = dO + b * sdo.b + hq * sdo.h;
     char* qimg = smem + st * STAGE;
@@ -1137,7 +1140,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
     const bool issue_next = it + 2 < total;
     const int st2 = st >= 1 ? st - 1 : 2;
     if (issue_next) issue(nhi, nti, st2);
-    const int qt_abs = qt_begin + ti;
+    const int qt_abs = qt_begin + (qrev ? nq - 1 - ti : ti);
     const int qbase = qt_abs * kQT;
     {
       const char* qimg = smem + st * STAGE;
@@ -1680,7 +1683,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __
                                                                      const float* __restrict__ LSE,
                                                                      const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                      int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                     float scale_log2, RowStrides sdo, QKVStrides sx) {
+                                                                     float scale_log2, RowStrides sdo, QKVStrides sx,
+                                                                     const T* __restrict__ O = nullptr, RowStrides so = {}) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -1723,7 +1727,21 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) qf[j][s] = load_frag<F>(Qb + (int64_t)qr * sx.qt + 16 * s + 8 * h);
     nl2[j] = -LSE[((int64_t)b * Hq + hq) * Tq + qr] * kLog2e;
-    dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+    if (O != nullptr) {  // delta = rowsum(dO * O) here (no preprocess launch; dK/dV runs after this kernel)
+      const T* Orow = O + (int64_t)b * so.b + (int64_t)hq * so.h + (int64_t)qr * so.t;
+      const T* Drow = dOb + (int64_t)qr * sdo.t;
+      float acc = 0.f;
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const F ov = load_frag<F>(Orow + 16 * s + 8 * h), dv = load_frag<F>(Drow + 16 * s + 8 * h);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += (float)dv[e] * (float)ov[e];
+      }
+      dl[j] = acc + __shfl_xor(acc, 32, 64);
+      if (h == 0 && qw + 32 * j + r < Tq) const_cast<float*>(DELTA)[((int64_t)b * Hq + hq) * Tq + qw + 32 * j + r] = dl[j];
+    } else {
+      dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+    }
   }
 
   f32x16 dqacc[2][C::DT];
@@ -1874,7 +1892,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v4_kernel(const T* __
                                                                      const float* __restrict__ LSE,
                                                                      const float* __restrict__ DELTA, T* __restrict__ dQ,
                                                                      int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                     float scale_log2, RowStrides sdo, QKVStrides sx) {
+                                                                     float scale_log2, RowStrides sdo, QKVStrides sx,
+                                                                     const T* __restrict__ O = nullptr, RowStrides so = {}) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -1917,7 +1936,21 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v4_kernel(const T* __
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) qf[j][s] = load_frag<F>(Qb + (int64_t)qr * sx.qt + 16 * s + 8 * h);
     nl2[j] = -LSE[((int64_t)b * Hq + hq) * Tq + qr] * kLog2e;
-    dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+    if (O != nullptr) {  // delta = rowsum(dO * O) here (no preprocess launch; dK/dV runs after this kernel)
+      const T* Orow = O + (int64_t)b * so.b + (int64_t)hq * so.h + (int64_t)qr * so.t;
+      const T* Drow = dOb + (int64_t)qr * sdo.t;
+      float acc = 0.f;
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const F ov = load_frag<F>(Orow + 16 * s + 8 * h), dv = load_frag<F>(Drow + 16 * s + 8 * h);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += (float)dv[e] * (float)ov[e];
+      }
+      dl[j] = acc + __shfl_xor(acc, 32, 64);
+      if (h == 0 && qw + 32 * j + r < Tq) const_cast<float*>(DELTA)[((int64_t)b * Hq + hq) * Tq + qw + 32 * j + r] = dl[j];
+    } else {
+      dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
+    }
   }
 
   f32x16 dqacc[2][C::DT];
@@ -2124,7 +2157,16 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 }
 
 int g_dkdv_v3 = 2;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
-int g_dq_v2 = 1;  // dQ kernel for D = 128 without mask / dropout: 3 = v4, 2 = v3, 1 = v2 (8 waves), 0 = v1
+int g_dkdv_qrev = [] {  // dK/dV v4 sweeps the query tiles last-to-first (A/B: LTA_DKDV_QREV=0 / lta_attn_bwd_set_dkdv_qrev)
+  const char* e = getenv("LTA_DKDV_QREV");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+// dQ kernel for D = 128 without mask / dropout: 3 = v4 (default: 534 vs 546 us causal backward per
+// layer, profiles/attn_dq_v3_ab.txt), 2 = v3, 1 = v2 (8 waves), 0 = v1; LTA_DQ_IMPL overrides
+int g_dq_v2 = [] {
+  const char* e = getenv("LTA_DQ_IMPL");
+  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
+}();
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -2133,7 +2175,7 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
   // dQ v2 computes delta itself and runs first (the dK/dV kernel reads it): no preprocess launch
-  const bool dq_delta = exf == 0 && D == 128 && g_dq_v2 == 1 && Tq > 0 && Sk > 0;
+  const bool dq_delta = exf == 0 && D == 128 && g_dq_v2 >= 1 && Tq > 0 && Sk > 0;
   if (!dq_delta)
     hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
@@ -2159,7 +2201,20 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     }
   }
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
-  if (dq_delta) {
+  if (dq_delta && g_dq_v2 >= 2) {
+    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
+#define LTA_DQ34(KERN, CA)                                                                                         \
+  hipLaunchKernelGGL((KERN<T, CA>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V, (const T*)dO,             \
+                     (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx, (const T*)O, so)
+    if (g_dq_v2 == 3) {
+      if (causal) LTA_DQ34(attn_bwd_dq_v4_kernel, true);
+      else LTA_DQ34(attn_bwd_dq_v4_kernel, false);
+    } else {
+      if (causal) LTA_DQ34(attn_bwd_dq_v3_kernel, true);
+      else LTA_DQ34(attn_bwd_dq_v3_kernel, false);
+    }
+#undef LTA_DQ34
+  } else if (dq_delta) {
     dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
@@ -2176,8 +2231,14 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   hipLaunchKernelGGL((KERN<T, CA>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V, (const T*)dO,              \
                      (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx)
     if (g_dkdv_v3 == 2) {
-      if (causal) LTA_DKDV3(attn_bwd_dkdv_v4_kernel, true);
-      else LTA_DKDV3(attn_bwd_dkdv_v4_kernel, false);
+      if (causal)
+        hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, true>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                           (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                           sl2, sdo, ex.sx, g_dkdv_qrev);
+      else
+        hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, false>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
+                           (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
+                           sl2, sdo, ex.sx, g_dkdv_qrev);
     } else {
       if (causal) LTA_DKDV3(attn_bwd_dkdv_v3_kernel, true);
       else LTA_DKDV3(attn_bwd_dkdv_v3_kernel, false);
@@ -2201,7 +2262,9 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                        (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
                        sl2, sdo, ex);
-  if (D == 128 && g_dq_v2 == 3 && Tq > 0 && Sk > 0) {
+  if (dq_delta) {
+    // launched before the dK/dV kernel (above)
+  } else if (D == 128 && g_dq_v2 == 3 && Tq > 0 && Sk > 0) {
     dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
     if (causal)
       hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
@@ -2217,8 +2280,6 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     else
       hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
                          (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-  } else if (dq_delta) {
-    // launched before the dK/dV kernel (above)
   } else if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
     dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
     if (causal)
@@ -2380,5 +2441,12 @@ LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
 LTA_EXPORT int lta_attn_bwd_set_dkdv_impl(int impl) {
   const int old = g_dkdv_v3;
   if (impl >= 0 && impl <= 2) g_dkdv_v3 = impl;
+  return old;
+}
+
+// dK/dV v4 query-tile order (A/B measurement hook): 1 = last tile first, 0 = first tile first
+LTA_EXPORT int lta_attn_bwd_set_dkdv_qrev(int rev) {
+  const int old = g_dkdv_qrev;
+  g_dkdv_qrev = rev ? 1 : 0;
   return old;
 }
