@@ -1838,6 +1838,8 @@ class _Gen:
             body.append(f"  for (int j = 0; j < {V}; ++j) acc{n}[j] = {init};")
         body.append(f"  const {IT} r0 = ({IT})blockIdx.y * {RPS}u;")
         body.append(f"  const {IT} r1 = r0 + {RPS}u < {R}u ? r0 + {RPS}u : {R}u;")
+        # unrolled: each wave keeps 4 rows' loads in flight (the adds keep their serial order)
+        body.append("  #pragma unroll 4")
         body.append(f"  for ({IT} r = r0 + wv; r < (cvalid ? r1 : 0u); r += 4u) {{")
         ind = "    "
         self._decompose("r", list(range(k)), body, ind)
@@ -1897,6 +1899,8 @@ class _Gen:
         for (n, kk, act, init, comb), off in zip(accs, offs):
             fin.append(f"  const {act}* ws{n} = (const {act}*)((const char*)A.ws + {off}ull);")
             fin.append(f"  {act} t{n} = {init};")
+            # unrolled: 8 partial loads in flight per thread (same serial combine order, deterministic)
+            fin.append("  #pragma unroll 8")
             fin.append(f"  for (unsigned s = part; s < {S}u; s += 4u) t{n} = {cf(comb, act, f't{n}', f'ws{n}[({IT})s * {C}u + e]')};")
             fin.append(f"  __shared__ {act} sf{n}[4][64];")
             fin.append(f"  sf{n}[part][cl] = t{n};")

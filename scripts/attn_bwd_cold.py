@@ -1,0 +1,46 @@
+"""Attention backward at the Llama-2-7B shape with cache-resident vs cold inputs.
+
+    python scripts/attn_bwd_cold.py
+'warm' repeats the backward on one input set (q, k, v, o, dO stay in L2 / the 256 MB MALL);
+'cold' cycles through 8 input sets (1.6 GB), so each backward starts from HBM as in a training
+step, where the inputs were written long before.  Per-kernel times from rocprofv3 separate the
+dK/dV and dQ kernels; this script reports the whole backward (median of rounds).
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
+
+
+def make():
+    q = torch.randn(1, 32, 4096, 128, device="cuda", dtype=torch.bfloat16)
+    k, v = torch.randn_like(q), torch.randn_like(q)
+    do = torch.randn(1, 4096, 32, 128, device="cuda", dtype=torch.bfloat16).transpose(1, 2)
+    o, lse = attn_fwd(q, k, v, True)
+    return do, q, k, v, o, lse
+
+
+sets = [make() for _ in range(8)]
+torch.cuda.synchronize()
+
+
+def timed(seq):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for a in seq:
+        attn_bwd(*a, True)
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / len(seq) * 1000
+
+
+for _ in range(3):
+    timed(sets)
+warm, cold = [], []
+for _ in range(5):
+    warm.append(timed([sets[0]] * 8))
+    cold.append(timed(sets))
+print(f"causal backward per layer: warm {sorted(warm)[2]:.1f} us, cold {sorted(cold)[2]:.1f} us", flush=True)
