@@ -785,7 +785,8 @@ def _fuse_kv_cache_writes(trace):
 def _fuse_rms_bwd_residual(trace):
     """``(dx, dw) = hip_rms_norm_bwd(g, x, w, rstd); z = dx + r`` (dx used nowhere else) ->
     ``(z, dw) = hip_rms_norm_bwd(g, x, w, rstd, r)``: the residual stream's gradient is added in the
-    normalisation backward's store pass instead of a separate elementwise launch."""
+    normalisation backward's store pass instead of a separate elementwise launch.  The same for
+    ``hip_layer_norm_bwd`` (GPT-2 / NeoX blocks)."""
     from ..core.trace import from_trace, TraceProvenance
 
     bsyms = trace.bound_symbols
@@ -807,17 +808,23 @@ def _fuse_rms_bwd_residual(trace):
         for pos in (0, 1):
             y, r = b.args[pos], b.args[1 - pos]
             j = producer.get(y.name)
-            if j is None or j in drop or j in replace or bsyms[j].sym is not hip_rms_norm_bwd or uses.get(y.name, 0) != 1:
+            if j is None or j in drop or j in replace or uses.get(y.name, 0) != 1:
                 continue
             rb = bsyms[j]
-            if len(rb.args) > 4 and rb.args[4] is not None:
+            if rb.sym is hip_rms_norm_bwd:
+                nargs = 4  # (dy, x, weight, rstd[, residual])
+            elif rb.sym is hip_layer_norm_bwd:
+                nargs = 6  # (dy, x, weight, mean, rstd, has_bias[, residual])
+            else:
+                continue
+            if len(rb.args) > nargs and rb.args[nargs] is not None:
                 continue
             outs = rb.output
             if outs[0] is not y or tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype:
                 continue
             if tuple(b.output.shape) != tuple(y.shape) or b.output.dtype != y.dtype or producer.get(r.name, -1) > j:
                 continue
-            nb = ex.bind_call_ctx(hip_rms_norm_bwd.bind(*rb.args[:4], r, output=(b.output, outs[1])))
+            nb = ex.bind_call_ctx(rb.sym.bind(*rb.args[:nargs], r, output=(b.output, *outs[1:])))
             replace[j] = nb
             drop.add(i)
             break
@@ -826,7 +833,7 @@ def _fuse_rms_bwd_residual(trace):
     new = from_trace(trace)
     new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
     new.scopes = [new.bound_symbols]
-    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} residual-gradient add(s) fused into RMSNorm backward"))
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} residual-gradient add(s) fused into a normalisation backward"))
     return new
 
 
@@ -1180,15 +1187,15 @@ def _ln_fwd_impl(x, weight, bias, eps):
     return layer_norm_fwd(x, weight, bias, eps)
 
 
-def _ln_bwd_meta(dy, x, weight, mean, rstd, has_bias):
+def _ln_bwd_meta(dy, x, weight, mean, rstd, has_bias, residual=None):
     return (TensorProxy(like=x), None if weight is None else TensorProxy(like=weight),
             TensorProxy(like=x, shape=(x.shape[-1],)) if has_bias else None)
 
 
-def _ln_bwd_impl(dy, x, weight, mean, rstd, has_bias):
+def _ln_bwd_impl(dy, x, weight, mean, rstd, has_bias, residual=None):
     from ..ops.rmsnorm import layer_norm_bwd
 
-    return layer_norm_bwd(dy, x, weight, mean, rstd, has_bias)
+    return layer_norm_bwd(dy, x, weight, mean, rstd, has_bias, residual)
 
 
 hip_layer_norm_fwd = ex.register_operator("hip_layer_norm_fwd", meta=_ln_fwd_meta, fn=_ln_fwd_impl)

@@ -8,6 +8,7 @@
 // the per-column dW partial sums in registers, writing one fp32 partial row per workgroup;
 // a second kernel reduces the partials (no float atomics: deterministic).
 #include "common.h"
+#include "colreduce.h"
 
 using namespace lta;
 
@@ -257,50 +258,6 @@ __global__ __launch_bounds__(kThreads) void column_reduce_kernel(const float* __
 #pragma unroll
     for (int i = 0; i < kWaves; ++i) t += sm[i][lane];
     out[col] = from_f32<T>(t);
-  }
-}
-
-// Same reduction, latency-friendly: a 256-thread block owns 32 columns, 8 lanes x float4 per row
-// and 32 row groups, each thread keeping 8 independent loads in flight; 4x the blocks of the
-// kernel above (cols / 32), one LDS pass to combine the row groups.  Needs cols % 4 == 0.
-template <typename T>
-__global__ __launch_bounds__(kThreads) void column_reduce_v4_kernel(const float* __restrict__ partial,
-                                                                    T* __restrict__ out, int nblocks, int cols) {
-  __shared__ float4 sm[32][8];
-  const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3;
-  const int col = blockIdx.x * 32 + cl * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col < cols) {
-    int b = rg;
-    for (; b + 7 * 32 < nblocks; b += 8 * 32) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(partial + (int64_t)(b + u * 32) * cols + col);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        acc.x += v[u].x;
-        acc.y += v[u].y;
-        acc.z += v[u].z;
-        acc.w += v[u].w;
-      }
-    }
-    for (; b < nblocks; b += 32) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + (int64_t)b * cols + col);
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
-    }
-  }
-  sm[rg][cl] = acc;
-  __syncthreads();
-  if (threadIdx.x < 32) {
-    const int c = threadIdx.x >> 2, e = threadIdx.x & 3;
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) t += reinterpret_cast<const float*>(&sm[i][c])[e];
-    const int oc = blockIdx.x * 32 + threadIdx.x;
-    if (oc < cols) out[oc] = from_f32<T>(t);
   }
 }
 

@@ -63,6 +63,8 @@ register_signature("lta_layernorm_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_
                                          c_int64, c_float, c_void_p])
 register_signature("lta_layernorm_bwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p])
+register_signature("lta_layernorm_bwd_res", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p])
 
 
 def layer_norm_fwd(x: torch.Tensor, weight, bias, eps: float):
@@ -78,16 +80,20 @@ def layer_norm_fwd(x: torch.Tensor, weight, bias, eps: float):
     return y.view(x.shape), mean, rstd
 
 
-def layer_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight, mean, rstd, has_bias: bool):
+def layer_norm_bwd(dy: torch.Tensor, x: torch.Tensor, weight, mean, rstd, has_bias: bool,
+                   residual: torch.Tensor | None = None):
+    """(dx, dw, db); ``residual`` (same shape as x) is added to dx in the same pass."""
     lib = require()
     x2, rows, cols = _as_2d(x)
     dy2, _, _ = _as_2d(dy)
+    r2 = None if residual is None else _as_2d(residual)[0]
     w = None if weight is None else weight.contiguous()
     dx = torch.empty_like(x2)
     nblocks = _bwd_blocks(rows)
     dw = None if weight is None else torch.empty_like(w)
     db = torch.empty(cols, device=x.device, dtype=x.dtype) if has_bias else None
     ws = torch.empty((nblocks, 2, cols), device=x.device, dtype=torch.float32) if (dw is not None or has_bias) else None
-    check(lib.lta_layernorm_bwd(dcode(x2), ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dx), ptr(dw), ptr(db),
-                                ptr(ws), rows, cols, nblocks, stream_ptr(x.device)), "lta_layernorm_bwd")
+    check(lib.lta_layernorm_bwd_res(dcode(x2), ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dx), ptr(dw),
+                                    ptr(db), ptr(ws), rows, cols, nblocks, ptr(r2), stream_ptr(x.device)),
+          "lta_layernorm_bwd")
     return dx.view(x.shape), dw, db

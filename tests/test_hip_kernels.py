@@ -1114,3 +1114,34 @@ def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
     e_fused = ((fused.float() - ref).norm() / ref.norm()).item()
     e_two = ((two.float() - ref).norm() / ref.norm()).item()
     assert e_fused < 1e-2 and e_fused <= 1.5 * e_two + 1e-4, (e_fused, e_two)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols", [1024, 1000, 3000])
+def test_layer_norm_backward_residual_fused(cols):
+    """A pre-norm residual block's backward: the residual stream's gradient is added in the
+    LayerNorm backward's store pass (no separate add), gradients vs fp64 within 3x eager's error."""
+    import lightning_thunder_amd as thunder
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 300, cols, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = torch.randn(cols, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(cols, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+
+    def f(x, w, b):
+        return x + torch.nn.functional.layer_norm(x, (cols,), w, b, 1e-5).tanh()
+
+    jf = thunder.jit(f)
+    y = jf(x, w, b)
+    g = torch.randn_like(y)
+    grads = torch.autograd.grad(y, (x, w, b), g)
+    bw = thunder.last_backward_traces(jf)[-1]
+    lnb = [bb for bb in bw.bound_symbols if bb.sym.name == "hip_layer_norm_bwd"]
+    assert lnb and len(lnb[0].args) == 7 and lnb[0].args[6] is not None, str(bw)
+    xr, wr, br = (t.detach().double().requires_grad_() for t in (x, w, b))
+    gr = torch.autograd.grad(f(xr, wr, br), (xr, wr, br), g.double())
+    ge = torch.autograd.grad(f(x, w, b), (x, w, b), g)
+    for o, r, e in zip(grads, gr, ge):
+        err = (o.double() - r).abs().max().item()
+        err_e = (e.double() - r).abs().max().item()
+        assert err <= 3 * err_e + 1e-3, (err, err_e)
