@@ -738,6 +738,15 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 __device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
+// tanh for regions whose every output is a 16-bit float: odd Taylor series to x^9 for |x| < 0.4
+// (truncation < 4e-7 absolute), 1 - 2 / (e^2|x| + 1) above (fast exp / divide, ~1e-7 absolute);
+// ~1e-6 relative worst case, far inside bf16 / fp16 rounding, at a third of ocml tanhf's instructions
+__device__ __forceinline__ float fast_tanhf(float x) {
+  const float ax = fabsf(x), x2 = x * x;
+  const float p = x + x * x2 * (-0.33333333f + x2 * (0.13333333f + x2 * (-0.053968254f + x2 * 0.021869488f)));
+  const float t = 1.f - __fdividef(2.f, __expf(2.f * ax) + 1.f);
+  return ax < 0.4f ? p : copysignf(t, x);
+}
 __device__ __forceinline__ float hfr(float f) { return (float)(_Float16)f; }
 template <class T> __device__ __forceinline__ T nmax(T a, T b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
 template <class T> __device__ __forceinline__ T nmin(T a, T b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
@@ -903,6 +912,8 @@ class _Gen:
         self.red = plan.red
         self.colred = plan.colred
         self.force_scalar = False  # column epilogue kernel: every load is one element
+        # every value leaving the kernel is rounded to bf16 / fp16: cheaper transcendental forms apply
+        self.half_outputs = bool(outputs) and all(o.dtype in (torch.bfloat16, torch.float16) for o in outputs)
         self.extra: list = []
         self.pre: list = []
         self.ws_bytes = 0
@@ -1084,6 +1095,8 @@ class _Gen:
         tin = [a for _, a in tensor_args(b)]
         ict = _CTYPE[tin[0].dtype] if tin else ct
         if sid in _UNARY_FLOAT:
+            if sid == PrimIDs.TANH and ict == "float" and self.half_outputs:
+                return [(out.name, _rnd(out.dtype, f"fast_tanhf({R(0)})"))]
             return [(out.name, _rnd(out.dtype, f"{_f(_UNARY_FLOAT[sid], ict)}({R(0)})"))]
         if sid in _UNARY_ANY:
             x = R(0, ict)
