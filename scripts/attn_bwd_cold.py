@@ -44,3 +44,20 @@ for _ in range(5):
     warm.append(timed([sets[0]] * 8))
     cold.append(timed(sets))
 print(f"causal backward per layer: warm {sorted(warm)[2]:.1f} us, cold {sorted(cold)[2]:.1f} us", flush=True)
+
+# the same backward between large GEMMs (as in the training step, where the chip's clock is set by
+# the GEMM-heavy load around the attention kernels)
+a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+b = torch.randn(11008, 4096, device="cuda", dtype=torch.bfloat16)
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(8)]
+mixed = []
+for _ in range(5):
+    for i, (s, e) in enumerate(ev):
+        for _ in range(6):
+            torch.nn.functional.linear(a, b)
+        s.record()
+        attn_bwd(*sets[i], True)
+        e.record()
+    torch.cuda.synchronize()
+    mixed.append(sorted(s.elapsed_time(e) * 1000 for s, e in ev)[4])
+print(f"causal backward per layer between GEMMs: {sorted(mixed)[2]:.1f} us", flush=True)
