@@ -6,6 +6,7 @@
 // described by a device table {tensor index, element offset}; every lane moves 16-byte
 // vectors.  Math in fp32.
 #include "common.h"
+#include <cstdlib>
 
 using namespace lta;
 
@@ -114,7 +115,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
   adamw_body<TP, TS, 4, NT>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
 }
 
-int g_adamw_nt = 1;  // non-temporal loads / stores in the post-backward kernel (5.99 vs 5.73 TB/s measured, scripts/adamw_nt_ab.py)
+// non-temporal loads / stores in the post-backward kernel: opt-in (LTA_ADAMW_NT=1).  Measured 5.99 vs
+// 5.73 TB/s (scripts/adamw_nt_ab.py), but its results were not bitwise equal to the plain kernel's in
+// tests/test_optim_overlap.py (profiles/adamw_nt_ab.txt), so the plain kernel stays the default
+int g_adamw_nt = [] {
+  const char* e = getenv("LTA_ADAMW_NT");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
 
 template <typename TP, typename TS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void adamw_lean_kernel(

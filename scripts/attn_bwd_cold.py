@@ -61,3 +61,14 @@ for _ in range(5):
     torch.cuda.synchronize()
     mixed.append(sorted(s.elapsed_time(e) * 1000 for s, e in ev)[4])
 print(f"causal backward per layer between GEMMs: {sorted(mixed)[2]:.1f} us", flush=True)
+
+# training-step-like magnitudes: tiny upstream gradients (dO ~ 1e-6) and small scores
+small = []
+for do, q, k, v, o, lse in sets[:2]:
+    qs, ks = q * 0.1, k * 0.1
+    os_, ls = attn_fwd(qs, ks, v, True)
+    small.append((do * 1e-6, qs, ks, v, os_, ls))
+ts = []
+for _ in range(5):
+    ts.append(timed(small * 4))
+print(f"causal backward per layer, small dO / scores: {sorted(ts)[2]:.1f} us", flush=True)
