@@ -999,13 +999,6 @@ class _Gen:
             if inner % v == 0:
                 vec = v
                 break
-        # plain elementwise regions over 16-bit tensors only: 32 bytes per lane (two 16-B loads issued
-        # together per operand), so a wave keeps twice the bytes in flight of the 16-B form (these
-        # streaming kernels are latency-bound at 8 waves / SIMD otherwise)
-        if (vec == 8 and max_item == 2 and inner % 16 == 0 and not self.red and not self.colred
-                and not self.p.has_pad and self.p.scatter is None
-                and not any(b.sym.id == PrimIDs.UNIFORM_PHILOX for b in self.p.nodes)):
-            vec = 16
         # every vector-loaded operand must keep 16B-compatible alignment; otherwise it gathers
         self.vec = vec
         big = numel >= 2**31 or any(
