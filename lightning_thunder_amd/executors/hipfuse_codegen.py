@@ -731,13 +731,10 @@ class Plan:
 # -----------------------------------------------------------------------------------------
 _PREAMBLE = r"""
 __device__ __forceinline__ float bf2f(unsigned short x) { return __builtin_bit_cast(float, ((unsigned)x) << 16); }
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  unsigned u = __builtin_bit_cast(unsigned, f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
-}
-__device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
+// f32 -> bf16 with round-to-nearest-even on the gfx950 conversion instruction (v_cvt_pk_bf16_f32:
+// half the VALU of the bit-twiddling form, two values per instruction when paired)
+__device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+__device__ __forceinline__ float bfr(float f) { return (float)(__bf16)f; }
 // tanh for regions whose every output is a 16-bit float: odd Taylor series to x^9 for |x| < 0.4
 // (truncation < 4e-7 absolute), 1 - 2 / (e^2|x| + 1) above (fast exp / divide, ~1e-7 absolute);
 // ~1e-6 relative worst case, far inside bf16 / fp16 rounding, at a third of ocml tanhf's instructions
