@@ -240,7 +240,25 @@ struct EpiArgs {
   const int* offs;           // GRP 1 / 2: int32 cumulative group ends (device)
   int G;                     // GRP: number of groups
   int64_t bstride, cstride;  // GRP 1: elements between groups' B; GRP 2: between groups' C
+  // GRP 0 tail split (lta_gemm4_bf16_ws): this launch covers the linear tiles [tile_base, tile_base +
+  // tile_count) (tile_count 0: all); ksplit == 2: workgroup b computes K half b & 1 of tile
+  // tile_base + b / 2 and stores the fp32 partial [2][tile_count][256][256] (plain products)
+  int tile_base, tile_count, ksplit;
+  float* partial;
 };
+
+// linear tile index -> (tile row, tile column): groups of 8 tile-rows walked column-major (the A and B
+// panels of a group stay in L2)
+__device__ __forceinline__ void tile_coords(int wg, int nTm, int nTn, int& tm, int& tn) {
+  constexpr int G = 8;
+  const int per_group = G * nTn;
+  const int group = wg / per_group;
+  const int first_m = group * G;
+  const int gm = min(nTm - first_m, G);
+  const int in_group = wg % per_group;
+  tm = first_m + in_group % gm;
+  tn = in_group / gm;
+}
 
 // EPI 0: plain (bias / act / residual); 1: gate-up forward (B2 = W2; C = a, C2 = b, C3 = y, each
 // [M][N/2] with pitch ldc; C / C2 may be null); 2: swiglu backward (R = a, R2 = b, C = da, C2 = db,
@@ -250,7 +268,7 @@ struct EpiArgs {
 // column tile, each workgroup scans the device offsets for its (group, row tile); no host sync).
 // GRP 2 (MoE wgrad): C[g] (C + g * cstride) = A_g^T . B_g, A / B stored [rows][.] (AT = BT = 1)
 // with group g's rows as the reduction; the reduction tail is zero-filled (Stager KEDGE).
-template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0, int GRP = 0>
+template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0, int GRP = 0, bool SPLIT = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat16* __restrict__ A,
                                                             const __hip_bfloat16* __restrict__ B,
                                                             __hip_bfloat16* __restrict__ C,
@@ -280,17 +298,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   const __hip_bfloat16* Bg = B;
   __hip_bfloat16* Cg = C;
   int Mlim = M, Kr = K, m0, n0;
+  [[maybe_unused]] int wg_lin = 0;
   if constexpr (GRP == 0) {
-    const int wg = xcd_tile((int)blockIdx.x, nwg);
-    constexpr int G = 8;
-    const int per_group = G * nTn;
-    const int group = wg / per_group;
-    const int first_m = group * G;
-    const int gm = min(nTm - first_m, G);
-    const int in_group = wg % per_group;
-    const int tm = first_m + in_group % gm, tn = in_group / gm;
+    int wg;
+    if constexpr (SPLIT)  // ksplit == 2 (the host's only split): shifts keep the index scalar
+      wg = ep.tile_base + ((int)blockIdx.x >> 1);
+    else if (ep.tile_count == 0)
+      wg = xcd_tile((int)blockIdx.x, nwg);
+    else
+      wg = ep.tile_base + xcd_tile((int)blockIdx.x, ep.tile_count);
+    wg_lin = wg;
+    int tm, tn;
+    tile_coords(wg, nTm, nTn, tm, tn);
     m0 = tm * BM;
     n0 = tn * BN;
+    if constexpr (SPLIT) {  // this workgroup's K half (K % (4 BK) == 0, checked by the host)
+      const int kp = (int)blockIdx.x & 1;
+      Kr = K >> 1;
+      Ag = A + (AT ? (int64_t)kp * Kr * lda : (int64_t)kp * Kr);
+      Bg = B + (BT ? (int64_t)kp * Kr * ldb : (int64_t)kp * Kr);
+    }
   } else if constexpr (GRP == 1) {
     const int bid = (int)blockIdx.x, tn = bid % nTn;
     int slot = bid / nTn, g = 0, start = 0, end = 0;
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   constexpr int NA = 16 - NB2;
 
   // GRP 2: ceil to an even K-tile count (the zero-filled tail tiles add nothing)
-  const int nk = GRP == 2 ? (Kr + 2 * BK - 1) / (2 * BK) * 2 : K / BK;
+  const int nk = GRP == 2 ? (Kr + 2 * BK - 1) / (2 * BK) * 2 : Kr / BK;
   // ---- prologue: tile 0 whole, tile 1's phase-B2 share; wait for tile 0 ----
 #pragma unroll
   for (int j = 0; j < 16; ++j) glds(j, 0, smem);
@@ -427,6 +454,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
+  if constexpr (SPLIT) {  // tail split: the fp32 partial of this K half (summed by gemm4_tail_fixup)
+    float* P = ep.partial + ((int64_t)((int)blockIdx.x & 1) * ep.tile_count + (wg_lin - ep.tile_base)) * (BM * BN);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) P[(wm * 128 + m * 16 + fq * 4 + j) * BN + wn * 128 + n * 16 + fr] = acc[m][n][j];
+        __builtin_amdgcn_sched_barrier(0);  // one accumulator block at a time: bounded VGPR use
+      }
+    return;
+  }
   // ---- epilogue: every wave has passed the last barrier after its final LDS read, so the stage
   // buffers are free: registers -> swizzled bf16 image (per wave 128 x 128, 256-B rows) -> stores
   char* wbuf = smem + wave * (128 * 256);
@@ -585,6 +624,62 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
 
 #undef LTA_FENCE
 
+// C tiles of a tail split: sum the K-slice partials (fixed order), scale, round, store (edges masked).
+// One thread per 8 consecutive columns of a tile row.
+__global__ __launch_bounds__(256) void gemm4_tail_fixup(const float* __restrict__ partial, __hip_bfloat16* __restrict__ C,
+                                                        int ksplit, int tile_base, int tile_count, int M, int N,
+                                                        int ldc, float alpha) {
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int t = (int)(id / (BM * BN / 8));
+  if (t >= tile_count) return;
+  const int rem = (int)(id % (BM * BN / 8)), row = rem / (BN / 8), ch = rem % (BN / 8);
+  int tm, tn;
+  tile_coords(tile_base + t, (M + BM - 1) / BM, (N + BN - 1) / BN, tm, tn);
+  const int64_t grow = (int64_t)tm * BM + row;
+  const int gcol = tn * BN + ch * 8;
+  if (grow >= M || gcol >= N) return;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < ksplit; ++k) {
+    const float* p = partial + ((int64_t)k * tile_count + t) * (BM * BN) + row * BN + ch * 8;
+    const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+    a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w; a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
+  }
+  union {
+    uint4 u;
+    __hip_bfloat16 h[8];
+  } o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(a[e] * alpha);
+  *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = o.u;
+}
+
+// Plain product with a wave-quantisation tail: the last partial wave of tiles (tail <= 128 tiles of
+// 256 CUs) runs as 2 K-slices per tile (so it takes half a tile time instead of a whole one), then a
+// fixup sums the two fp32 partials.  Returns -1 when the shape does not qualify.
+template <bool AT, bool BT>
+int launch4_tail(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                 void* ws, int64_t ws_bytes, hipStream_t s) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN), tail = nwg % 256;
+  if (nwg <= 256 || tail == 0 || tail > 128 || K % (2 * BK * 2) || !ws || ws_bytes < (int64_t)2 * tail * BM * BN * 4)
+    return -1;
+  EpiArgs ep{};
+  ep.tile_base = 0;
+  ep.tile_count = nwg - tail;
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1>), dim3(nwg - tail), dim3(NTHR), 0, s,
+                     (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N, K,
+                     lda, ldb, ldc, 0, alpha, ep);
+  ep.tile_base = nwg - tail;
+  ep.tile_count = tail;
+  ep.ksplit = 2;
+  ep.partial = (float*)ws;
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1, 0, 0, true>), dim3(2 * tail), dim3(NTHR), 0, s,
+                     (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N, K,
+                     lda, ldb, ldc, 0, 1.f, ep);
+  hipLaunchKernelGGL(gemm4_tail_fixup, dim3((unsigned)((int64_t)tail * (BM * BN / 8) / 256)), dim3(256), 0, s,
+                     (const float*)ws, (__hip_bfloat16*)C, 2, nwg - tail, tail, M, N, ldc, alpha);
+  return (int)hipGetLastError();
+}
+
 template <int ACT, bool AT, bool BT, int VAR>
 int launch4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
             int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
@@ -649,6 +744,26 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   if (variant == 2) { LTA_G4V(2) }
 #undef LTA_G4V
   return -1;
+}
+
+// lta_gemm4_bf16 with a workspace: a plain product (no act / bias / residual, variant 1) whose tile
+// grid ends in a partial wave of <= 128 tiles runs that tail split over K (launch4_tail); ws: fp32,
+// >= 2 * tail * 256 * 256 elements.  Everything else is lta_gemm4_bf16.
+LTA_EXPORT int lta_gemm4_bf16_ws(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
+                                 int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
+                                 int variant, void* ws, int64_t ws_bytes, hipStream_t s) {
+  if (ws && variant == 1 && act == kNone && !bias && !R && N % 8 == 0 && M > 0 && N > 0 && K > 0 && !(at && M % 8)) {
+    const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
+    if (ea * 2 < (1ll << 31) && eb * 2 < (1ll << 31)) {
+      int rc = -1;
+      if (!at && !bt) rc = launch4_tail<false, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ws, ws_bytes, s);
+      else if (!at && bt) rc = launch4_tail<false, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ws, ws_bytes, s);
+      else if (at && !bt) rc = launch4_tail<true, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ws, ws_bytes, s);
+      else rc = launch4_tail<true, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ws, ws_bytes, s);
+      if (rc != -1) return rc;
+    }
+  }
+  return lta_gemm4_bf16(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, variant, s);
 }
 
 // Grouped GEMMs for mixture-of-experts training (K10; reference nvFuser _grouped_mm forward and

@@ -195,7 +195,8 @@ class _DelayedState:
         self.recipe = recipe
         self.n = n_slots
         self.hist = self.cur = self.hmax = None
-        self.step_amax = None  # amax each slot was scaled from in the current step
+        self.step_amax = None  # first-step amax of a slot (current scaling: no history yet)
+        self.step_src = [None] * n_slots  # the amax tensor each slot is scaled from in this step
         self.seen = [False] * n_slots
         self.step_seen = [-1] * n_slots  # the step (``updates``) a slot was last quantised in
         self.updates = 0
@@ -260,15 +261,19 @@ def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
     t2 = t.reshape(-1, t.shape[-1])
     fmax = (E5M2_MAX if e5m2 else E4M3_MAX) * 2.0 ** -st.recipe.margin
     scale = torch.empty((), dtype=torch.float32, device=t.device)
-    amax_in = st.step_amax[slot]
     if st.step_seen[slot] != st.updates:  # first quantisation of the slot in this step
         st.step_seen[slot] = st.updates
         if st.seen[slot]:
-            amax_in.copy_(st.hmax[slot])
+            # the history max itself (a view: hmax only changes in delayed_update, after the step's
+            # last quantisation), not a per-slot device copy of it (a 4-byte memcpy launch each)
+            st.step_src[slot] = st.hmax[slot]
         else:  # first use of the slot: no history yet -> current scaling for this step
             st.seen[slot] = True
+            amax_in = st.step_amax[slot]
             amax_in.zero_()
             amax_into(t2, amax_in)
+            st.step_src[slot] = amax_in
+    amax_in = st.step_src[slot]
     q, qT = cast_transpose(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=st.cur[slot])
     return q, qT, scale
 

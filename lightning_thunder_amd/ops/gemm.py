@@ -7,7 +7,7 @@ import torch
 
 import ctypes
 
-from ._lib import require, stream_ptr, check, register_signature, dcode, c_int, c_void_p, c_float
+from ._lib import require, stream_ptr, check, register_signature, dcode, c_int, c_void_p, c_float, c_int64
 
 ACT = {None: 0, "none": 0, "gelu_tanh": 1, "gelu": 2, "gelu_erf": 2, "silu": 3, "relu": 4}
 TILE_M, TILE_N, TILE_K = 256, 256, 64
@@ -76,6 +76,24 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
 # ---------------------------------------------------------------------------------------------
 register_signature("lta_gemm4_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p])
+register_signature("lta_gemm4_bf16_ws", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                         c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p, c_int64,
+                                         c_void_p])
+
+# wave-quantisation tail of plain products: the last partial wave (<= 128 of 256 CUs' tiles, e.g. the
+# 1376-tile Llama-2-7B gate/up forward and wgrad) runs as two K halves per tile + an fp32 fixup
+# (csrc/gemm4.hip launch4_tail); LTA_GEMM_TAIL_SPLIT=0 turns it off
+_TAIL_SPLIT = _os.environ.get("LTA_GEMM_TAIL_SPLIT", "1") != "0"
+
+
+def _tail_workspace(M: int, N: int, K: int, device):
+    if not _TAIL_SPLIT or K % 256:
+        return None
+    nwg = -(-M // 256) * -(-N // 256)
+    tail = nwg % 256
+    if nwg <= 256 or tail == 0 or tail > 128:
+        return None
+    return torch.empty(2 * tail * 256 * 256, dtype=torch.float32, device=device)
 
 
 GEMM4_MIN_M = 64
@@ -121,6 +139,13 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
         assert residual.shape == (M, N) and residual.stride(1) == 1 and residual.dtype == torch.bfloat16
     if bias is not None:
         assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
+    ws = _tail_workspace(M, N, K, a.device) if (bias is None and residual is None and act is None and variant == 1) else None
+    if ws is not None:
+        rc = require().lta_gemm4_bf16_ws(a.data_ptr(), b.data_ptr(), out.data_ptr(), None, None, M, N, K, lda, ldb,
+                                         out.stride(0), 0, alpha, ACT[act], at, bt, variant, ws.data_ptr(),
+                                         ws.numel() * 4, stream_ptr(a.device))
+        check(rc, "lta_gemm4_bf16_ws")
+        return out
     rc = require().lta_gemm4_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(),
                                   None if bias is None else bias.data_ptr(),
                                   None if residual is None else residual.data_ptr(), M, N, K, lda, ldb, out.stride(0),

@@ -1145,3 +1145,28 @@ def test_layer_norm_backward_residual_fused(cols):
         err = (o.double() - r).abs().max().item()
         err_e = (e.double() - r).abs().max().item()
         assert err <= 3 * err_e + 1e-3, (err, err_e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,layout", [(1280, 13312, 512, "nt"), (1000, 17000, 256, "nt"), (4096, 22016, 4096, "nt"),
+                                          (22016, 4096, 1024, "tn"), (4352, 4096, 768, "nn"), (4352, 4096, 512, "tt")])
+def test_gemm4_wave_tail_split(M, N, K, layout):
+    """Plain products whose tile grid ends in a partial wave (<= 128 tiles) run that tail as two K
+    halves + an fp32 fixup (csrc/gemm4.hip launch4_tail): vs an fp32 reference in every layout."""
+    from lightning_thunder_amd.ops.gemm import matmul4, _tail_workspace
+
+    assert _tail_workspace(M, N, K, "cuda") is not None  # the shape takes the split path
+    torch.manual_seed(0)
+    if layout[0] == "n":
+        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    else:  # a stored [K][M]
+        a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16).t()
+    if layout[1] == "t":  # b = W^T, W [N][K]
+        b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16).t()
+    else:
+        b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+    out = matmul4(a, b)
+    ref = a.float() @ b.float()
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 5e-3, err
+    assert torch.isfinite(out).all()
