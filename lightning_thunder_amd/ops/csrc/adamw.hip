@@ -25,11 +25,14 @@ constexpr int kChunk = 16384;  // elements per workgroup-chunk
 template <typename TP, typename TS>
 __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float lr, float b1, float b2,
                                            float eps, float wd, float bc1, float bc2_sqrt) {
+  // explicit FMAs and no compiler contraction: every instantiation (plain, non-temporal, lean) rounds
+  // identically, so updates issued from different kernels are bitwise interchangeable
+#pragma clang fp contract(off)
   p = p * (1.f - lr * wd);
-  m = b1 * m + (1.f - b1) * g;
-  v = b2 * v + (1.f - b2) * g * g;
+  m = __builtin_fmaf(b1, m, (1.f - b1) * g);
+  v = __builtin_fmaf(b2, v, ((1.f - b2) * g) * g);
   const float denom = sqrtf(v) / bc2_sqrt + eps;
-  p = p - (lr / bc1) * (m / denom);
+  p = __builtin_fmaf(-(lr / bc1), m / denom, p);
 }
 
 // U = 16-byte vectors per lane in flight per operand.  The default (U = 4) streams at full HBM
@@ -115,12 +118,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict
   adamw_body<TP, TS, 4, NT>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
 }
 
-// non-temporal loads / stores in the post-backward kernel: opt-in (LTA_ADAMW_NT=1).  Measured 5.99 vs
-// 5.73 TB/s (scripts/adamw_nt_ab.py), but its results were not bitwise equal to the plain kernel's in
-// tests/test_optim_overlap.py (profiles/adamw_nt_ab.txt), so the plain kernel stays the default
+// non-temporal loads / stores in the post-backward kernel (LTA_ADAMW_NT=0 turns them off): 5.99 vs
+// 5.73 TB/s (scripts/adamw_nt_ab.py).  Before adamw_elem pinned its rounding, the compiler contracted
+// this variant differently and it was not bitwise equal to the lean kernel (profiles/adamw_nt_ab.txt)
 int g_adamw_nt = [] {
   const char* e = getenv("LTA_ADAMW_NT");
-  return (e && e[0] == '1') ? 1 : 0;
+  return (e && e[0] == '0') ? 0 : 1;
 }();
 
 template <typename TP, typename TS>

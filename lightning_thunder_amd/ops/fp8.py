@@ -193,13 +193,18 @@ class DelayedScaling:
 class _DelayedState:
     def __init__(self, recipe: DelayedScaling, n_slots: int):
         self.recipe = recipe
-        self.n = n_slots
         self.hist = self.cur = self.hmax = None
         self.step_amax = None  # first-step amax of a slot (current scaling: no history yet)
+        self.updates = 0
+        self.resize(n_slots)
+
+    def resize(self, n_slots: int) -> None:
+        """Set the slot count (before the first quantisation; the transform knows it only after it
+        has rewritten the trace)."""
+        self.n = n_slots
         self.step_src = [None] * n_slots  # the amax tensor each slot is scaled from in this step
         self.seen = [False] * n_slots
         self.step_seen = [-1] * n_slots  # the step (``updates``) a slot was last quantised in
-        self.updates = 0
 
     def ensure(self, device):
         if self.hist is None:

@@ -144,9 +144,7 @@ class FP8LinearTransform(Transform):
             from ..ops.fp8 import delayed_state
 
             st = delayed_state(key)
-            st.n = len(slots)
-            st.seen = [False] * st.n
-            st.step_seen = [-1] * st.n
+            st.resize(len(slots))
             self.state_key = key
             upd = fp8_delayed_update.bind(key, output=None)
             new.bound_symbols.insert(0, upd)

@@ -452,3 +452,13 @@ def test_jit_inner_autocast_context():
     x.grad = None
     (ry.float().sum() + rz.sum()).backward()
     torch.testing.assert_close(gx, x.grad, atol=5e-2, rtol=2e-2)
+
+
+def test_fp8_delayed_state_resize_sizes_every_per_slot_list():
+    """The FP8 transform sizes the delayed-scaling state after rewriting the trace: every per-slot
+    list (scaling source, first-use and per-step flags) must follow the new slot count."""
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling, new_delayed_state, delayed_state
+
+    st = delayed_state(new_delayed_state(DelayedScaling(), 0))
+    st.resize(7)
+    assert st.n == 7 and len(st.step_src) == len(st.seen) == len(st.step_seen) == 7
