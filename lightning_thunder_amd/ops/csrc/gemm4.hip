@@ -241,7 +241,7 @@ struct EpiArgs {
   int G;                     // GRP: number of groups
   int64_t bstride, cstride;  // GRP 1: elements between groups' B; GRP 2: between groups' C
   // GRP 0 tail split (lta_gemm4_bf16_ws): this launch covers the linear tiles [tile_base, tile_base +
-  // tile_count) (tile_count 0: all); ksplit == 2: workgroup b computes K half b & 1 of tile
+  // tile_count) (kernel TAIL = 1 and 2); ksplit == 2: workgroup b computes K half b & 1 of tile
   // tile_base + b / 2 and stores the fp32 partial [2][tile_count][256][256] (plain products)
   int tile_base, tile_count, ksplit;
   float* partial;
@@ -268,7 +268,7 @@ __device__ __forceinline__ void tile_coords(int wg, int nTm, int nTn, int& tm, i
 // column tile, each workgroup scans the device offsets for its (group, row tile); no host sync).
 // GRP 2 (MoE wgrad): C[g] (C + g * cstride) = A_g^T . B_g, A / B stored [rows][.] (AT = BT = 1)
 // with group g's rows as the reduction; the reduction tail is zero-filled (Stager KEDGE).
-template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0, int GRP = 0, bool SPLIT = false>
+template <int ACT, bool BIAS, bool RES, bool AT, bool BT, int VAR, int EPI = 0, int GRP = 0, int TAIL = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat16* __restrict__ A,
                                                             const __hip_bfloat16* __restrict__ B,
                                                             __hip_bfloat16* __restrict__ C,
@@ -300,19 +300,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   int Mlim = M, Kr = K, m0, n0;
   [[maybe_unused]] int wg_lin = 0;
   if constexpr (GRP == 0) {
+    // TAIL 0: every tile (the production instantiations keep exactly this code: a run-time tile
+    // range here changed hipcc's schedule of the GELU + bias epilogue into wrong results);
+    // 1: tiles [tile_base, tile_base + tile_count); 2: the K-split tail (ksplit == 2, the host's only
+    // split: shifts keep the index scalar)
     int wg;
-    if constexpr (SPLIT)  // ksplit == 2 (the host's only split): shifts keep the index scalar
+    if constexpr (TAIL == 2)
       wg = ep.tile_base + ((int)blockIdx.x >> 1);
-    else if (ep.tile_count == 0)
-      wg = xcd_tile((int)blockIdx.x, nwg);
-    else
+    else if constexpr (TAIL == 1)
       wg = ep.tile_base + xcd_tile((int)blockIdx.x, ep.tile_count);
+    else
+      wg = xcd_tile((int)blockIdx.x, nwg);
     wg_lin = wg;
     int tm, tn;
     tile_coords(wg, nTm, nTn, tm, tn);
     m0 = tm * BM;
     n0 = tn * BN;
-    if constexpr (SPLIT) {  // this workgroup's K half (K % (4 BK) == 0, checked by the host)
+    if constexpr (TAIL == 2) {  // this workgroup's K half (K % (4 BK) == 0, checked by the host)
       const int kp = (int)blockIdx.x & 1;
       Kr = K >> 1;
       Ag = A + (AT ? (int64_t)kp * Kr * lda : (int64_t)kp * Kr);
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  if constexpr (SPLIT) {  // tail split: the fp32 partial of this K half (summed by gemm4_tail_fixup)
+  if constexpr (TAIL == 2) {  // tail split: the fp32 partial of this K half (summed by gemm4_tail_fixup)
     float* P = ep.partial + ((int64_t)((int)blockIdx.x & 1) * ep.tile_count + (wg_lin - ep.tile_base)) * (BM * BN);
 #pragma unroll
     for (int m = 0; m < 8; ++m)
@@ -665,14 +669,14 @@ int launch4_tail(const void* A, const void* B, void* C, int M, int N, int K, int
   EpiArgs ep{};
   ep.tile_base = 0;
   ep.tile_count = nwg - tail;
-  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1>), dim3(nwg - tail), dim3(NTHR), 0, s,
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1, 0, 0, 1>), dim3(nwg - tail), dim3(NTHR), 0, s,
                      (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N, K,
                      lda, ldb, ldc, 0, alpha, ep);
   ep.tile_base = nwg - tail;
   ep.tile_count = tail;
   ep.ksplit = 2;
   ep.partial = (float*)ws;
-  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1, 0, 0, true>), dim3(2 * tail), dim3(NTHR), 0, s,
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1, 0, 0, 2>), dim3(2 * tail), dim3(NTHR), 0, s,
                      (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N, K,
                      lda, ldb, ldc, 0, 1.f, ep);
   hipLaunchKernelGGL(gemm4_tail_fixup, dim3((unsigned)((int64_t)tail * (BM * BN / 8) / 256)), dim3(256), 0, s,
