@@ -63,7 +63,12 @@ def parse_args():
     p.add_argument("--checkpoint-activations", action="store_true",
                    help="recompute every transformer block in the backward (memory for longer sequences)")
     p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
-    p.add_argument("--eager-baseline", action="store_true", help="also time PyTorch eager (1 GPU) for speedup")
+    p.add_argument("--eager-baseline", default="auto", choices=["auto", "on", "off"],
+                   help="also time PyTorch eager on the same config for speedup_vs_eager (auto: on for the 1-GPU "
+                        "thunder run; a short segment of --eager-steps after --eager-warmup, outside thunder's "
+                        "timed region)")
+    p.add_argument("--eager-steps", type=int, default=5)
+    p.add_argument("--eager-warmup", type=int, default=2)
     p.add_argument("--profile-dir", default=None)
     return p.parse_args()
 
@@ -105,8 +110,11 @@ def _force_dist() -> bool:
     return os.environ.get("LTA_BENCH_FORCE_DIST") == "1"
 
 
-def run(args, rank, world, device, mode):
+def run(args, rank, world, device, mode, steps=None, warmup=None):
     import lightning_thunder_amd as thunder
+
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
 
     model, cfg = build_model(args, device)
     parallel = args.parallel
@@ -201,7 +209,7 @@ def run(args, rank, world, device, mode):
 
     data = [batch() for _ in range(4)]
     t_first = time.perf_counter()
-    for i in range(args.warmup):
+    for i in range(warmup):
         loss = step(*data[i % 4])
         if i == 0:
             torch.cuda.synchronize()
@@ -211,7 +219,7 @@ def run(args, rank, world, device, mode):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         loss = step(*data[i % 4])
     if world > 1:
         torch.distributed.barrier()
@@ -222,7 +230,7 @@ def run(args, rank, world, device, mode):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = t.item()
     mem = torch.cuda.max_memory_allocated(device) / 1e9
-    log(rank, f"[{mode}] {args.steps} steps in {dt:.3f}s, loss={loss.item():.4f}, peak mem {mem:.1f} GB")
+    log(rank, f"[{mode}] {steps} steps in {dt:.3f}s, loss={loss.item():.4f}, peak mem {mem:.1f} GB")
     if mode == "thunder":
         from lightning_thunder_amd.ops import gemm as _g
 
@@ -276,12 +284,17 @@ def main():
     from lightning_thunder_amd.models.litgpt import flops_per_token
 
     tflops = flops_per_token(cfg, args.seq) * per_gpu / 1e12
-    speedup = None
-    if args.eager_baseline and world == 1 and args.mode == "thunder":
+    speedup = eager_ms = None
+    want_eager = args.eager_baseline == "on" or (args.eager_baseline == "auto" and world == 1 and not _force_dist()
+                                                 and not args.lora)
+    if want_eager and args.mode == "thunder":
+        # PyTorch eager on the same model / batch / optimizer semantics (torch fused AdamW), after
+        # thunder's timed region; thunder's model and optimizer state are freed first
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
-        dte, _, _, _ = run(args, rank, world, device, "eager")
-        speedup = dte / dt
+        dte, _, _, _ = run(args, rank, world, device, "eager", steps=args.eager_steps, warmup=args.eager_warmup)
+        eager_ms = dte / args.eager_steps * 1000
+        speedup = eager_ms / (dt / args.steps * 1000)
     base = BASELINE_TOKENS_PER_SEC_PER_GPU_1 if world == 1 else BASELINE_TOKENS_PER_SEC_PER_GPU_FSDP
     if rank == 0:
         out = {
@@ -313,6 +326,7 @@ def main():
             "model_tflops_per_gpu": round(tflops, 1),
             "peak_mem_gb": round(mem, 2),
             "speedup_vs_eager": None if speedup is None else round(speedup, 3),
+            "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 3),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -454,547 +454,14 @@ __device__ __forceinline__ void tr_wait16(F (&f)[8], s16x4t (&x)[16]) {
   }
 }
 
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                                       const T* __restrict__ V, const T* __restrict__ dO,
-                                                                       const float* __restrict__ LSE,
-                                                                       const float* __restrict__ DELTA, T* __restrict__ dK,
-                                                                       T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
-  constexpr int D = 128;
-  using C = BCfg<D>;
-  using F = typename Frag<T>::type;
-  // Three-stage DMA ring: tile it+2 is issued while tile it is multiplied, and the end-of-tile wait
-  // only retires tile it+1 (counted vmcnt, raw barrier), so a DMA has two tiles of compute to land.
-  // Stage = {Q image 8 KB, dO image 8 KB, LSE 128 B, delta 128 B}; the statistics come through
-  // registers of wave 0 (loaded before its DMAs, so retiring them never waits on a DMA) and are
-  // written into their stage at the end of the tile before.
-  constexpr int NST = 3;
-  constexpr int IMG = kQT * 256;           // one 32-row image (bytes)
-  constexpr int STAGE = 2 * IMG + 256;
-  constexpr int VOFF = NST * STAGE;        // V rows after the stages
-  constexpr int VBYTES = kKB * C::RSTR * 2;
-  constexpr int KOFF = VOFF + VBYTES;      // K rows
-  // ONE __shared__ object: a second one can make hipcc drain the DMA queue before every ds_read
-  __shared__ __attribute__((aligned(1024))) char smem[KOFF + VBYTES];
-  short* Vs = reinterpret_cast<short*>(smem + VOFF);
-  short* Ks = reinterpret_cast<short*>(smem + KOFF);
-
-  const int kb = (int)blockIdx.y;
-  const int bh = blockIdx.x;
-  const int b = bh / Hkv, hk = bh % Hkv;
-  const int group = Hq / Hkv;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
-  const int kw = kb * kKB + wave * 32;
-  const int key = kw + r;
-  const T* Kb = K + b * sx.kb + hk * sx.kh;
-  const T* Vb = V + b * sx.vb + hk * sx.vh;
-
-  // K and V rows of this workgroup's 128 keys -> LDS (padded rows: conflict-free B-operand reads);
-  // held there rather than in registers so the loop carries nothing but the AGPR accumulators
-#pragma unroll
-  for (int c = 0; c < kKB * C::CH / kThreads; ++c) {
-    const int id = c * kThreads + tid;
-    const int row = id / C::CH, ch = id % C::CH;
-    const int vr = min(kb * kKB + row, Sk - 1);
-    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * sx.vt + ch * 8);
-    *reinterpret_cast<uint4*>(Ks + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Kb + (int64_t)vr * sx.kt + ch * 8);
-  }
-
-  f32x16 dkacc[C::DT], dvacc[C::DT];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      dkacc[dt][i] = 0.f;
-      dvacc[dt][i] = 0.f;
-    }
-
-  const int n_qt = (Tq + kQT - 1) / kQT;
-  const int qt_begin = CAUSAL ? min((kb * kKB) / kQT, n_qt) : 0;
-  const int nq = n_qt - qt_begin;
-  const int total = group * nq;
-
-  float plse = 0.f, pdel = 0.f;
-  auto stash_stats = [&](int st) {
-    if (wave == 0 && lane < kQT) {
-      float* sp = reinterpret_cast<float*>(smem + st * STAGE + 2 * IMG);
-      sp[lane] = plse;
-      sp[kQT + lane] = pdel;
-    }
-  };
-  // DMA tile (query head hk*group + hi, query tile qt_begin + ti) into stage `st`: wave w stages
-  // rows 8w .. 8w+7 of the Q and dO images (4 loads), wave 0 also the LSE / delta rows (2 loads)
-  auto issue = [&](int hi, int ti, int st) {
-    const int hq = hk * group + hi;
-    const int qbase = (qt_begin + ti) * kQT;
-    const T* Qb = Q + b * sx.qb + hq * sx.qh;
-    const T* dOb = dO + b * sdo.b + hq * sdo.h;
-    char* qimg = smem + st * STAGE;
-    if (wave == 0) {
-      // asm loads: hipcc would otherwise wait for them with vmcnt(0), i.e. behind this tile's DMAs;
-      // they are issued first, so the vmcnt(4) that retires the tile before covers them
-      const int64_t srow = ((int64_t)b * Hq + hq) * Tq + min(qbase + (lane & 31), Tq - 1);
-      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off"
-                   : "=&v"(plse), "=&v"(pdel)
-                   : "v"(LSE + srow), "v"(DELTA + srow)
-                   : "memory");
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // wave-instruction k = 2*wave + i fills 16-B units u = 64k + lane of the image (lane-linear);
-      // invert layout (a): u = 128 (row>>3) + 32 (ch>>2) + 4 (row&7) + ((ch&3) ^ ((row>>2)&3))
-      const int k = wave * 2 + i;
-      const int u = 64 * k + lane;
-      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
-      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
-      const int qc = min(qbase + row, Tq - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * sx.qt + ch * 8),
-                                       (lds_void*)(qimg + k * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
-                                       (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
-    }
-  };
-  // wait for every load of this wave except the newest tile's 4 DMAs (the statistics loads of
-  // the newest tile, issued before them, land too)
-  auto wait_all_but_newest = [&]() { asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory"); };
-
-  // prologue: tiles 0 and 1 in flight, tile 0 landed
-  int nhi = 0, nti = 0;  // next tile to issue
-  auto advance = [&]() {
-    if (++nti == nq) {
-      nti = 0;
-      ++nhi;
-    }
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V staging loads
-  if (total > 0) {
-    issue(nhi, nti, 0);
-    advance();
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(plse), "+v"(pdel)::"memory");
-    stash_stats(0);
-  }
-  if (total > 1) {
-    issue(nhi, nti, 1);
-    advance();
-    wait_all_but_newest();
-    stash_stats(1);
-  }
-  __syncthreads();
-
-  // transposed-read base addresses of this lane (layout (a)): group lane 4q+p reads row 4h+q (ba)
-  // or 8+4h+q (bb), columns 16(g&1) + 4p .. +3 of d-tile 0
-  unsigned tr_a, tr_b;
-  {
-    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
-    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
-    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
-  }
-  int ti = 0;  // current tile's query-tile index
-  int st = 0;  // current stage
-  for (int it = 0; it < total; ++it) {
-    const bool issue_next = it + 2 < total;
-    const int st2 = st >= 1 ? st - 1 : 2;  // (st + 2) % 3: the stage tile it-1 used
-    if (issue_next) issue(nhi, nti, st2);
-    const int qbase = (qt_begin + ti) * kQT;
-    const char* qimg = smem + st * STAGE;
-    const char* oimg = qimg + IMG;
-    const float* sl = reinterpret_cast<const float*>(qimg + 2 * IMG);
-
-    // S = Q K^T (rows: this tile's queries, columns: this wave's keys)
-    f32x16 sacc, pacc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      sacc[i] = 0.f;
-      pacc[i] = 0.f;
-    }
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F kb_ = load_frag<F>(Ks + (wave * 32 + r) * C::RSTR + 16 * s + 8 * h);
-      sacc = mfma(load_frag<F>(qimg + du_off(r, 2 * s + h)), kb_, sacc);
-    }
-    // dP = dO V^T, overlapping the exponentials of P
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F vb = load_frag<F>(Vs + (wave * 32 + r) * C::RSTR + 16 * s + 8 * h);
-      pacc = mfma(load_frag<F>(oimg + du_off(r, 2 * s + h)), vb, pacc);
-    }
-    // statistics rows 8a + 4h .. +3 (a = 0..3) of LSE and delta.  Read in ONE asm statement with
-    // its own wait: as plain loads hipcc cannot tell them from the stage the DMA in flight is
-    // writing and would drain the DMA queue (vmcnt(0)) in front of them.
-    f32x4v L[4], Dl[4];
-    {
-      const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(sl + 4 * h);
-      asm volatile(
-          "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
-          "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
-          "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(Dl[0]), "=&v"(Dl[1]), "=&v"(Dl[2]), "=&v"(Dl[3])
-          : "v"(addr)
-          : "memory");
-    }
-    constexpr float kLog2e = 1.44269504088896340736f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float li = L[i >> 2][i & 3];
-      sacc[i] = __builtin_amdgcn_exp2f(sacc[i] * scale_log2 - li * kLog2e);
-    }
-    // wave-uniform: only tiles that straddle the causal diagonal or an edge need the mask (rows
-    // past Tq are clamped copies: P = 0 there also zeroes their dS)
-    const bool masked = (CAUSAL && kw + 31 > qbase) || kw + 32 > Sk || qbase + kQT > Tq;
-    if (masked) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qq = qbase + acc_row(i, h);
-        if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) sacc[i] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float di = Dl[i >> 2][i & 3];
-      pacc[i] = sacc[i] * (pacc[i] - di);  // dS
-    }
-    F pf0, pf1, df0, df1;
-    pack_frag(pf0, sacc, 0);
-    pack_frag(pf1, sacc, 1);
-    pack_frag(df0, pacc, 0);
-    pack_frag(df1, pacc, 1);
-    {
-      F xt[8];
-      tr_frags8(xt, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        mfma_acc_agpr(dvacc[dt], xt[2 * dt], pf0);
-        mfma_acc_agpr(dvacc[dt], xt[2 * dt + 1], pf1);
-      }
-      tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // Q^T
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        mfma_acc_agpr(dkacc[dt], xt[2 * dt], df0);
-        mfma_acc_agpr(dkacc[dt], xt[2 * dt + 1], df1);
-      }
-    }
-    // tile it+1 must have landed (tile it+2 may stay in flight); every wave's reads of stage st are
-    // done before the barrier, after which tile it+3 may be DMA'd into it
-    if (issue_next) {
-      advance();
-      wait_all_but_newest();
-      stash_stats(st2);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    ti = ti + 1 == nq ? 0 : ti + 1;
-    st = st == 2 ? 0 : st + 1;
-  }
-  // the last asm MFMAs' results must be complete before any other instruction reads them
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[dt]), "+a"(dvacc[dt]));
-
-  if (key < Sk) {
-    T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
-    T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int d = dt * 32 + 8 * a + 4 * h;
-        union {
-          T v[4];
-          uint2 u;
-        } pk, pv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pk.v[e] = from_f32<T>(dkacc[dt][4 * a + e] * scale);
-          pv.v[e] = from_f32<T>(dvacc[dt][4 * a + e]);
-        }
-        *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
-        *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// dK / dV, D = 128 (v3): v2 with 64 keys per wave (256 per workgroup) in two 32-key halves.
-// Every Q / dO image read (row reads for S and dP, transposed reads for dV^T and dK^T) now feeds
-// two halves' MFMAs: 64 MFMAs per 32-query tile per wave against v2's 32, for 8 more LDS row
-// reads (V of the second half).  K of the wave's 64 keys stays in registers (B operand of S),
-// V lives in LDS, the dK^T / dV^T accumulators fill the 256 AGPRs (cdna_hip_programming.md,
-// Appendix B 'Attention backward': one wave per SIMD owning 64 keys).
+// dK / dV, D = 128: one workgroup per 256 keys, 64 per wave in two 32-key halves.  Every Q / dO
+// image read (row reads for S and dP, transposed reads for dV^T and dK^T) feeds both halves' MFMAs;
+// K of the wave's 64 keys stays in registers (B operand of S), V lives in LDS, the dK^T / dV^T
+// accumulators fill the 256 AGPRs (cdna_hip_programming.md, Appendix B 'Attention backward').
+// (The retired v2 / v3 dK/dV kernels: profiles/attn_bwd_v1_v2_ab.txt, profiles/attn_bwd_dkdv_v4_ab.txt.)
 // ---------------------------------------------------------------------------------------------
 constexpr int kKB3 = 256;
-
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v3_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                                       const T* __restrict__ V, const T* __restrict__ dO,
-                                                                       const float* __restrict__ LSE,
-                                                                       const float* __restrict__ DELTA, T* __restrict__ dK,
-                                                                       T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
-                                                                       float scale, float scale_log2, RowStrides sdo, QKVStrides sx) {
-  constexpr int D = 128;
-  using C = BCfg<D>;
-  using F = typename Frag<T>::type;
-  constexpr int NST = 3;
-  constexpr int IMG = kQT * 256;
-  constexpr int STAGE = 2 * IMG + 256;
-  constexpr int VOFF = NST * STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[VOFF + kKB3 * C::RSTR * 2];
-  short* Vs = reinterpret_cast<short*>(smem + VOFF);
-
-  const int kb = (int)blockIdx.y;
-  const int bh = blockIdx.x;
-  const int b = bh / Hkv, hk = bh % Hkv;
-  const int group = Hq / Hkv;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int kw = kb * kKB3 + wave * 64;  // this wave's first key; half j: keys kw + 32 j + r
-  const T* Kb = K + b * sx.kb + hk * sx.kh;
-  const T* Vb = V + b * sx.vb + hk * sx.vh;
-
-  // V rows of the workgroup's 256 keys -> LDS; K rows of this wave's 64 keys -> registers
-#pragma unroll
-  for (int c = 0; c < kKB3 * C::CH / kThreads; ++c) {
-    const int id = c * kThreads + tid;
-    const int row = id / C::CH, ch = id % C::CH;
-    const int vr = min(kb * kKB3 + row, Sk - 1);
-    *reinterpret_cast<uint4*>(Vs + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(Vb + (int64_t)vr * sx.vt + ch * 8);
-  }
-  F kf[2][C::KS];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int kr = min(kw + 32 * j + r, Sk - 1);
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) kf[j][s] = load_frag<F>(Kb + (int64_t)kr * sx.kt + 16 * s + 8 * h);
-  }
-
-  f32x16 dkacc[2][C::DT], dvacc[2][C::DT];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        dkacc[j][dt][i] = 0.f;
-        dvacc[j][dt][i] = 0.f;
-      }
-
-  const int n_qt = (Tq + kQT - 1) / kQT;
-  const int qt_begin = CAUSAL ? min((kb * kKB3) / kQT, n_qt) : 0;
-  const int nq = n_qt - qt_begin;
-  const int total = group * nq;
-
-  float plse = 0.f, pdel = 0.f;
-  auto stash_stats = [&](int st) {
-    if (wave == 0 && lane < kQT) {
-      float* sp = reinterpret_cast<float*>(smem + st * STAGE + 2 * IMG);
-      sp[lane] = plse;
-      sp[kQT + lane] = pdel;
-    }
-  };
-  auto issue = [&](int hi, int ti, int st) {
-    const int hq = hk * group + hi;
-    const int qbase = (qt_begin + ti) * kQT;
-    const T* Qb = Q + b * sx.qb + hq * sx.qh;
-    const T* dOb = dO + b * sdo.b + hq * sdo.h;
-    char* qimg = smem + st * STAGE;
-    if (wave == 0) {
-      const int64_t srow = ((int64_t)b * Hq + hq) * Tq + min(qbase + (lane & 31), Tq - 1);
-      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off"
-                   : "=&v"(plse), "=&v"(pdel)
-                   : "v"(LSE + srow), "v"(DELTA + srow)
-                   : "memory");
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = wave * 2 + i;
-      const int u = 64 * k + lane;
-      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
-      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
-      const int qc = min(qbase + row, Tq - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)qc * sx.qt + ch * 8),
-                                       (lds_void*)(qimg + k * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(dOb + qc * sdo.t + ch * 8),
-                                       (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
-    }
-  };
-  auto wait_all_but_newest = [&]() { asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory"); };
-
-  int nhi = 0, nti = 0;
-  auto advance = [&]() {
-    if (++nti == nq) {
-      nti = 0;
-      ++nhi;
-    }
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V staging loads
-  if (total > 0) {
-    issue(nhi, nti, 0);
-    advance();
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(plse), "+v"(pdel)::"memory");
-    stash_stats(0);
-  }
-  if (total > 1) {
-    issue(nhi, nti, 1);
-    advance();
-    wait_all_but_newest();
-    stash_stats(1);
-  }
-  __syncthreads();
-
-  unsigned tr_a, tr_b;
-  {
-    const int l16 = lane & 15, g = lane >> 4;
-    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
-    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
-    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
-  }
-  constexpr float kLog2e = 1.44269504088896340736f;
-  int ti = 0, st = 0;
-  for (int it = 0; it < total; ++it) {
-    const bool issue_next = it + 2 < total;
-    const int st2 = st >= 1 ? st - 1 : 2;
-    if (issue_next) issue(nhi, nti, st2);
-    const int qt_abs = qt_begin + ti;
-    const int qbase = qt_abs * kQT;
-    {  // (a wave-uniform skip of the tiles wholly above the wave's keys costs 110 spilled VGPRs: the
-       // masked P of those tiles is zero instead, ~4 % of the causal sweep)
-      const char* qimg = smem + st * STAGE;
-      const char* oimg = qimg + IMG;
-      const float* sl = reinterpret_cast<const float*>(qimg + 2 * IMG);
-      f32x16 sacc[2], pacc[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          sacc[j][i] = 0.f;
-          pacc[j][i] = 0.f;
-        }
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F qa = load_frag<F>(qimg + du_off(r, 2 * s + h));
-#pragma unroll
-        for (int j = 0; j < 2; ++j) sacc[j] = mfma(qa, kf[j][s], sacc[j]);  // S = Q K^T
-      }
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F oa = load_frag<F>(oimg + du_off(r, 2 * s + h));
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          pacc[j] = mfma(oa, load_frag<F>(Vs + (wave * 64 + 32 * j + r) * C::RSTR + 16 * s + 8 * h), pacc[j]);
-      }
-      f32x4v L[4], Dl[4];
-      {
-        const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(sl + 4 * h);
-        asm volatile(
-            "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
-            "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
-            "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
-            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(Dl[0]), "=&v"(Dl[1]), "=&v"(Dl[2]), "=&v"(Dl[3])
-            : "v"(addr)
-            : "memory");
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, -L[i >> 2][i & 3] * kLog2e));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int key = kw + 32 * j + r;
-        const bool masked = (CAUSAL && kw + 32 * j + 31 > qbase) || kw + 32 * j + 32 > Sk || qbase + kQT > Tq;
-        if (masked) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qq = qbase + acc_row(i, h);
-            if (key >= Sk || qq >= Tq || (CAUSAL && key > qq)) sacc[j][i] = 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) pacc[j][i] = sacc[j][i] * (pacc[j][i] - Dl[i >> 2][i & 3]);  // dS
-      F pf[2][2], df[2][2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        pack_frag(pf[j][0], sacc[j], 0);
-        pack_frag(pf[j][1], sacc[j], 1);
-        pack_frag(df[j][0], pacc[j], 0);
-        pack_frag(df[j][1], pacc[j], 1);
-      }
-      {
-        F xt[8];
-        tr_frags8(xt, tr_a + (unsigned)(st * STAGE + IMG), tr_b + (unsigned)(st * STAGE + IMG));  // dO^T
-#pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            mfma_acc_agpr(dvacc[j][dt], xt[2 * dt], pf[j][0]);
-            mfma_acc_agpr(dvacc[j][dt], xt[2 * dt + 1], pf[j][1]);
-          }
-        tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // Q^T
-#pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            mfma_acc_agpr(dkacc[j][dt], xt[2 * dt], df[j][0]);
-            mfma_acc_agpr(dkacc[j][dt], xt[2 * dt + 1], df[j][1]);
-          }
-      }
-    }
-    if (issue_next) {
-      advance();
-      wait_all_but_newest();
-      stash_stats(st2);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    ti = ti + 1 == nq ? 0 : ti + 1;
-    st = st == 2 ? 0 : st + 1;
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[j][dt]), "+a"(dvacc[j][dt]));
-
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int key = kw + 32 * j + r;
-    if (key < Sk) {
-      T* dkrow = dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
-      T* dvrow = dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int d = dt * 32 + 8 * a + 4 * h;
-          union {
-            T v[4];
-            uint2 u;
-          } pk, pv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            pk.v[e] = from_f32<T>(dkacc[j][dt][4 * a + e] * scale);
-            pv.v[e] = from_f32<T>(dvacc[j][dt][4 * a + e]);
-          }
-          *reinterpret_cast<uint2*>(dkrow + d) = pk.u;
-          *reinterpret_cast<uint2*>(dvrow + d) = pv.u;
-        }
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // dK / dV, D = 128 (v4): v3's data flow with the tile's VALU work moved into the MFMA shadows.
@@ -1470,416 +937,14 @@ __global__ __launch_bounds__(kThreads, (EX || D > 128) ? 1 : 2) void attn_bwd_dq
 }
 
 // ---------------------------------------------------------------------------------------------
-// dQ, D = 128, no mask / dropout (v2): the forward v2 structure (attention_fwd.hip) applied to the
-// dQ sweep — 8 waves x 32 query rows = 256 queries per workgroup, one workgroup per CU, so each
-// staged K/V tile feeds twice the queries of v1; {K rows, V rows, K transposed-read image}
-// double-buffered in LDS, register-staged one tile ahead (T14), one barrier per tile; the scale and
-// LSE fold into one FMA per score; the causal / key-edge mask runs only on a wave's last tile.
-// ---------------------------------------------------------------------------------------------
-constexpr int kBM2 = 256;
-constexpr int kThreads2 = 512;
-
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(kThreads2, 1) void attn_bwd_dq_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                                      const T* __restrict__ V, const T* __restrict__ dO,
-                                                                      const float* __restrict__ LSE,
-                                                                      const float* __restrict__ DELTA, T* __restrict__ dQ,
-                                                                      int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                      float scale_log2, RowStrides sdo, QKVStrides sx,
-                                                                      const T* __restrict__ O = nullptr,
-                                                                      RowStrides so = {}) {
-  constexpr int D = 128;
-  using C = BCfg<D>;
-  using F = typename Frag<T>::type;
-  constexpr int ST = 2 * kBN * C::RSTR + kBN * C::TSTR;  // elements per stage: K rows, V rows, K image
-  __shared__ __attribute__((aligned(16))) short smem[2 * ST];
-
-  const int n_qt = (Tq + kBM2 - 1) / kBM2;
-  const int qt = n_qt - 1 - (int)blockIdx.y;
-  const int bh = blockIdx.x;
-  const int b = bh / Hq, hq = bh % Hq;
-  const int hk = hq / (Hq / Hkv);
-  const T* Qb = Q + b * sx.qb + hq * sx.qh;
-  const T* dOb = dO + b * sdo.b + hq * sdo.h;
-  const T* Kb = K + b * sx.kb + hk * sx.kh;
-  const T* Vb = V + b * sx.vb + hk * sx.vh;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
-  const int q0 = qt * kBM2 + wave * 32;
-  const int qi = q0 + r;
-  const int qrow = min(qi, Tq - 1);
-
-  int n_tiles = (Sk + kBN - 1) / kBN;
-  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM2 + kBM2, Tq) + kBN - 1) / kBN);
-  int nw = n_tiles;  // this wave's tiles; only tile nw-1 can need the mask
-  if (CAUSAL) nw = min(n_tiles, min(q0 + 31, Tq - 1) / kBN + 1);
-  const bool last_masked = (nw * kBN > Sk) || (CAUSAL && (nw - 1) * kBN + kBN - 1 > q0);
-
-  F qf[C::KS], of[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    qf[s] = load_frag<F>(Qb + (int64_t)qrow * sx.qt + 16 * s + 8 * h);
-    of[s] = load_frag<F>(dOb + qrow * sdo.t + 16 * s + 8 * h);
-  }
-  const float nlse2 = -LSE[((int64_t)b * Hq + hq) * Tq + qrow] * 1.44269504088896340736f;
-  float dlt;
-  if (O != nullptr) {
-    // delta = rowsum(dO * O) here instead of a preprocess launch: the lane pair (r, r + 32) holds the
-    // row's dO in its fragments; the dK/dV kernel, launched after this one, reads what is stored
-    const T* Orow = O + (int64_t)b * so.b + (int64_t)hq * so.h + (int64_t)qrow * so.t;
-    float acc = 0.f;
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F ov = load_frag<F>(Orow + 16 * s + 8 * h);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc += (float)of[s][e] * (float)ov[e];
-    }
-    dlt = acc + __shfl_xor(acc, 32, 64);
-    if (h == 0 && qi < Tq) const_cast<float*>(DELTA)[((int64_t)b * Hq + hq) * Tq + qi] = dlt;
-  } else {
-    dlt = DELTA[((int64_t)b * Hq + hq) * Tq + qrow];
-  }
-
-  f32x16 dqacc[C::DT];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
-
-  uint4 pk[2], pv[2];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int id = c * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      const int kc = min(t * kBN + row, Sk - 1);  // clamped rows are real keys; dS = 0 there
-      pk[c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * sx.kt + ch * 8);
-      pv[c] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * sx.vt + ch * 8);
-    }
-  };
-  auto lstore = [&](int st) {
-    short* Kr = smem + st * ST;
-    short* Vr = Kr + kBN * C::RSTR;
-    short* Kt = Vr + kBN * C::RSTR;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int id = c * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      *reinterpret_cast<uint4*>(Kr + row * C::RSTR + ch * 8) = pk[c];
-      *reinterpret_cast<uint4*>(Vr + row * C::RSTR + ch * 8) = pv[c];
-      *reinterpret_cast<uint4*>(Kt + row * C::TSTR + ch * 8) = pk[c];
-    }
-  };
-
-  const int last = n_tiles - 1;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int t = 0; t < n_tiles; ++t) {
-    gload(min(t + 1, last));  // tile t+1 in flight over tile t's math
-    if (t < nw) {
-      const short* Kr = smem + (t & 1) * ST;
-      const short* Vr = Kr + kBN * C::RSTR;
-      const __attribute__((address_space(3))) short* Kt3 =
-          (const __attribute__((address_space(3))) short*)(Vr + kBN * C::RSTR);
-      f32x16 sacc[2], pacc[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          sacc[kt][i] = 0.f;
-          pacc[kt][i] = 0.f;
-        }
-      // the 4 K / V fragments of k-step s+1 are read while k-step s's MFMAs run (one LDS latency
-      // per tile instead of one per MFMA pair)
-      F kc[2], vc[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        kc[kt] = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 8 * h);
-        vc[kt] = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 8 * h);
-      }
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        F kn[2] = {kc[0], kc[1]}, vn[2] = {vc[0], vc[1]};
-        if (s + 1 < C::KS) {
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            kn[kt] = load_frag<F>(Kr + (kt * 32 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
-            vn[kt] = load_frag<F>(Vr + (kt * 32 + r) * C::RSTR + 16 * (s + 1) + 8 * h);
-          }
-        }
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          sacc[kt] = mfma(kc[kt], qf[s], sacc[kt]);  // S^T
-          pacc[kt] = mfma(vc[kt], of[s], pacc[kt]);  // dP^T
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          kc[kt] = kn[kt];
-          vc[kt] = vn[kt];
-        }
-      }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kt][i], scale_log2, nlse2));
-          pacc[kt][i] = p * (pacc[kt][i] - dlt);  // dS^T
-        }
-      if (t == nw - 1 && last_masked) {  // wave-uniform
-        const int kbase = t * kBN;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int kk = kbase + kt * 32 + acc_row(i, h);
-            if (kk >= Sk || (CAUSAL && kk > qi)) pacc[kt][i] = 0.f;
-          }
-      }
-      F df[2][2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        pack_frag(df[kt][0], pacc[kt], 0);
-        pack_frag(df[kt][1], pacc[kt], 1);
-      }
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        const int col0 = dt * 32 + 16 * (g & 1);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            dqacc[dt] = mfma(tr_frag<F>(Kt3, kt * 32 + 16 * s + 4 * h, col0, C::TSTR, l16), df[kt][s], dqacc[dt]);
-      }
-    }
-    lstore((t + 1) & 1);  // over tile t-1 (read before the last barrier)
-    __syncthreads();
-  }
-
-  if (qi < Tq) {
-    T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
-    const bool rope = sx.rope_cos != nullptr;
-    store_row_d128(drow, dqacc, scale, h, rope ? sx.rope_cos + (int64_t)qi * 128 : nullptr,
-                   rope ? sx.rope_sin + (int64_t)qi * 128 : nullptr);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// dQ, D = 128 (v3): the dK/dV v3 data flow mirrored onto the query side.  One workgroup per 256
-// queries, 64 per wave in two 32-row halves: Q rows in registers (B operand of S^T = K Q^T), the
-// workgroup's dO rows in LDS (B operand of dP^T = V dO^T), 32-key K / V tiles streamed by
-// global_load_lds into a 3-stage ring of layout-(a) images that serve the row reads of S^T / dP^T
-// and the transposed reads of dQ^T += K^T dS^T; dQ^T accumulates in the AGPR file.  Against v2
-// (32 queries per wave, register-staged K / V) every staged fragment feeds twice the MFMAs and the
-// staging needs no VGPRs.
+// dQ, D = 128: one workgroup per 256 queries, 64 per wave in two 32-row halves: Q rows in registers
+// (B operand of S^T = K Q^T), the workgroup's dO rows in LDS (B operand of dP^T = V dO^T), 32-key
+// K / V tiles streamed by global_load_lds into a 3-stage ring of images that serve the row reads
+// of S^T / dP^T and the transposed reads of dQ^T += K^T dS^T; dQ^T accumulates in the AGPR file.
+// (The retired v2 / v3 dQ kernels: profiles/attn_dq_v3_ab.txt.)
 // ---------------------------------------------------------------------------------------------
 constexpr int kQB3 = 256;  // queries per workgroup
 constexpr int kKT3 = 32;   // keys per streamed tile
-
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v3_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                                     const T* __restrict__ V, const T* __restrict__ dO,
-                                                                     const float* __restrict__ LSE,
-                                                                     const float* __restrict__ DELTA, T* __restrict__ dQ,
-                                                                     int Hq, int Hkv, int Tq, int Sk, float scale,
-                                                                     float scale_log2, RowStrides sdo, QKVStrides sx,
-                                                                     const T* __restrict__ O = nullptr, RowStrides so = {}) {
-  constexpr int D = 128;
-  using C = BCfg<D>;
-  using F = typename Frag<T>::type;
-  constexpr int NST = 3;
-  constexpr int IMG = kKT3 * 256;  // 32 rows x 128 x 16-bit
-  constexpr int STAGE = 2 * IMG;   // K image, V image
-  constexpr int OOFF = NST * STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[OOFF + kQB3 * C::RSTR * 2];
-  short* Os = reinterpret_cast<short*>(smem + OOFF);
-
-  const int n_qb = (Tq + kQB3 - 1) / kQB3;
-  const int qb = n_qb - 1 - (int)blockIdx.y;  // heaviest causal blocks first
-  const int bh = blockIdx.x;
-  const int b = bh / Hq, hq = bh % Hq;
-  const int hk = hq / (Hq / Hkv);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int qw = qb * kQB3 + wave * 64;  // this wave's first query; half j: queries qw + 32 j + r
-  const T* Qb = Q + b * sx.qb + hq * sx.qh;
-  const T* dOb = dO + b * sdo.b + hq * sdo.h;
-  const T* Kb = K + b * sx.kb + hk * sx.kh;
-  const T* Vb = V + b * sx.vb + hk * sx.vh;
-
-  // dO rows of the workgroup's 256 queries -> LDS; Q rows and row statistics of this wave's 64
-  // queries -> registers (rows past Tq are clamped copies; their dQ is not stored)
-#pragma unroll
-  for (int c = 0; c < kQB3 * C::CH / kThreads; ++c) {
-    const int id = c * kThreads + tid;
-    const int row = id / C::CH, ch = id % C::CH;
-    const int orow = min(qb * kQB3 + row, Tq - 1);
-    *reinterpret_cast<uint4*>(Os + row * C::RSTR + ch * 8) = *reinterpret_cast<const uint4*>(dOb + (int64_t)orow * sdo.t + ch * 8);
-  }
-  constexpr float kLog2e = 1.44269504088896340736f;
-  F qf[2][C::KS];
-  float nl2[2], dl[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qr = min(qw + 32 * j + r, Tq - 1);
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[j][s] = load_frag<F>(Qb + (int64_t)qr * sx.qt + 16 * s + 8 * h);
-    nl2[j] = -LSE[((int64_t)b * Hq + hq) * Tq + qr] * kLog2e;
-    if (O != nullptr) {  // delta = rowsum(dO * O) here (no preprocess launch; dK/dV runs after this kernel)
-      const T* Orow = O + (int64_t)b * so.b + (int64_t)hq * so.h + (int64_t)qr * so.t;
-      const T* Drow = dOb + (int64_t)qr * sdo.t;
-      float acc = 0.f;
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const F ov = load_frag<F>(Orow + 16 * s + 8 * h), dv = load_frag<F>(Drow + 16 * s + 8 * h);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc += (float)dv[e] * (float)ov[e];
-      }
-      dl[j] = acc + __shfl_xor(acc, 32, 64);
-      if (h == 0 && qw + 32 * j + r < Tq) const_cast<float*>(DELTA)[((int64_t)b * Hq + hq) * Tq + qw + 32 * j + r] = dl[j];
-    } else {
-      dl[j] = DELTA[((int64_t)b * Hq + hq) * Tq + qr];
-    }
-  }
-
-  f32x16 dqacc[2][C::DT];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dqacc[j][dt][i] = 0.f;
-
-  int n_kt = (Sk + kKT3 - 1) / kKT3;
-  if (CAUSAL) n_kt = min(n_kt, (min(qb * kQB3 + kQB3, Tq) + kKT3 - 1) / kKT3);
-
-  // one 32-key tile: 8 x 1 KiB of K and of V per workgroup, lane-linear DMA into layout (a)
-  // (the swizzle is applied to the source row / chunk; see dK/dV v3)
-  auto issue = [&](int t, int st) {
-    char* kimg = smem + st * STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = wave * 2 + i;
-      const int u = 64 * k + lane;
-      const int row = ((u >> 7) << 3) | ((u >> 2) & 7);
-      const int ch = (((u >> 5) & 3) << 2) | ((u & 3) ^ ((row >> 2) & 3));
-      const int kc = min(t * kKT3 + row, Sk - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)kc * sx.kt + ch * 8), (lds_void*)(kimg + k * 1024), 16,
-                                       0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)kc * sx.vt + ch * 8),
-                                       (lds_void*)(kimg + IMG + k * 1024), 16, 0, 0);
-    }
-  };
-  if (n_kt > 0) issue(0, 0);
-  if (n_kt > 1) {
-    issue(1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed (tile 1 may be in flight)
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-
-  unsigned tr_a, tr_b;
-  {
-    const int l16 = lane & 15, g = lane >> 4;
-    const int q = l16 >> 2, p = l16 & 3, cl = 2 * (g & 1) + (p >> 1);
-    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    tr_a = base + 64 * (4 * h + q) + 16 * (cl ^ h) + 8 * (p & 1);
-    tr_b = base + 2048 + 64 * (4 * h + q) + 16 * (cl ^ (2 + h)) + 8 * (p & 1);
-  }
-  int st = 0;
-  for (int t = 0; t < n_kt; ++t) {
-    const bool issue_next = t + 2 < n_kt;
-    const int st2 = st >= 1 ? st - 1 : 2;
-    if (issue_next) issue(t + 2, st2);
-    const char* kimg = smem + st * STAGE;
-    const char* vimg = kimg + IMG;
-    f32x16 sacc[2], pacc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        sacc[j][i] = 0.f;
-        pacc[j][i] = 0.f;
-      }
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F ka = load_frag<F>(kimg + du_off(r, 2 * s + h));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) sacc[j] = mfma(ka, qf[j][s], sacc[j]);  // S^T = K Q^T
-    }
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F va = load_frag<F>(vimg + du_off(r, 2 * s + h));
-#pragma unroll
-      for (int j = 0; j < 2; ++j)  // dP^T = V dO^T
-        pacc[j] = mfma(va, load_frag<F>(Os + (wave * 64 + 32 * j + r) * C::RSTR + 16 * s + 8 * h), pacc[j]);
-    }
-    const int kbase = t * kKT3;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][i], scale_log2, nl2[j]));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int qi = qw + 32 * j + r;
-      const bool masked = kbase + kKT3 > Sk || (CAUSAL && kbase + kKT3 - 1 > qw + 32 * j);  // wave-uniform
-      if (masked) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kbase + acc_row(i, h);
-          if (key >= Sk || (CAUSAL && key > qi)) sacc[j][i] = 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) pacc[j][i] = sacc[j][i] * (pacc[j][i] - dl[j]);  // dS^T
-    F df[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      pack_frag(df[j][0], pacc[j], 0);
-      pack_frag(df[j][1], pacc[j], 1);
-    }
-    {
-      F xt[8];
-      tr_frags8(xt, tr_a + (unsigned)(st * STAGE), tr_b + (unsigned)(st * STAGE));  // K^T
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          mfma_acc_agpr(dqacc[j][dt], xt[2 * dt], df[j][0]);
-          mfma_acc_agpr(dqacc[j][dt], xt[2 * dt + 1], df[j][1]);
-        }
-    }
-    if (issue_next)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile t+1 landed; t+2 may be in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    st = st == 2 ? 0 : st + 1;
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dqacc[j][dt]));
-
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qi = qw + 32 * j + r;
-    if (qi < Tq) {
-      T* drow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)qi * sx.dqt;
-      const bool rope = sx.rope_cos != nullptr;
-      store_row_d128(drow, dqacc[j], scale, h, rope ? sx.rope_cos + (int64_t)qi * 128 : nullptr,
-                     rope ? sx.rope_sin + (int64_t)qi * 128 : nullptr);
-    }
-  }
-}
 
 // dQ v4: v3's data flow with the VALU work of a tile in the MFMA shadows (as dK/dV v4):
 //   A: S^T half 0 (8 MFMA), S^T half 1 (8) | P half 0      B0: dP^T half 0 (8) | P half 1
@@ -2156,30 +1221,38 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DQ
 }
 
-int g_dkdv_v3 = 2;  // dK/dV kernel for D = 128 without mask / dropout: 2 = v4 (pipelined), 1 = v3, 0 = v2
-int g_dkdv_qrev = [] {  // dK/dV v4 sweeps the query tiles last-to-first (A/B: LTA_DKDV_QREV=0 / lta_attn_bwd_set_dkdv_qrev)
+// dK/dV sweep order of the D = 128 kernel: query tiles last-to-first (A/B: LTA_DKDV_QREV=0)
+int g_dkdv_qrev = [] {
   const char* e = getenv("LTA_DKDV_QREV");
   return (e && e[0] == '0') ? 0 : 1;
-}();
-// dQ kernel for D = 128 without mask / dropout: 3 = v4 (default: 534 vs 546 us causal backward per
-// layer, profiles/attn_dq_v3_ab.txt), 2 = v3, 1 = v2 (8 waves), 0 = v1; LTA_DQ_IMPL overrides
-int g_dq_v2 = [] {
-  const char* e = getenv("LTA_DQ_IMPL");
-  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
 }();
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
                void* dQ, void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, int causal,
-               RowStrides sdo, RowStrides so, int dkdv_v2, const AttnExtra& ex, int exf, hipStream_t s) {
+               RowStrides sdo, RowStrides so, int fast, const AttnExtra& ex, int exf, hipStream_t s) {
   const float sl2 = scale * 1.44269504088896340736f;
   const int64_t rows = (int64_t)B * Hq * Tq;
-  // dQ v2 computes delta itself and runs first (the dK/dV kernel reads it): no preprocess launch
-  const bool dq_delta = exf == 0 && D == 128 && g_dq_v2 >= 1 && Tq > 0 && Sk > 0;
-  if (!dq_delta)
-    hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                       (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
-  if (exf) {  // masks / dropout: the plain-HIP dK/dV kernel with the extra terms compiled in
+  dim3 blk(kThreads);
+  if (exf == 0 && D == 128 && fast && Tq > 0 && Sk > 0) {
+    // production path: the dQ kernel computes delta = rowsum(dO O) itself and runs first (the dK/dV
+    // kernel reads it), so there is no preprocess launch
+    dim3 gq(B * Hq, (Tq + kQB3 - 1) / kQB3), gk(B * Hkv, (Sk + kKB3 - 1) / kKB3);
+#define LTA_FAST(CA)                                                                                                 \
+  hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, CA>), gq, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,            \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,   \
+                     ex.sx, (const T*)O, so);                                                                          \
+  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,          \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
+                     sdo, ex.sx, g_dkdv_qrev)
+    if (causal) { LTA_FAST(true); }
+    else { LTA_FAST(false); }
+#undef LTA_FAST
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                     (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
+  if (exf) {  // masks / dropout: the plain-HIP kernels with the extra terms compiled in
     if constexpr (D > 128) {
       return -1;  // D = 256: plain (causal / full) attention only
     } else {
@@ -2200,112 +1273,28 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     return (int)hipGetLastError();
     }
   }
-  dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM), blk(kThreads);
-  if (dq_delta && g_dq_v2 >= 2) {
-    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
-#define LTA_DQ34(KERN, CA)                                                                                         \
-  hipLaunchKernelGGL((KERN<T, CA>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V, (const T*)dO,             \
-                     (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx, (const T*)O, so)
-    if (g_dq_v2 == 3) {
-      if (causal) LTA_DQ34(attn_bwd_dq_v4_kernel, true);
-      else LTA_DQ34(attn_bwd_dq_v4_kernel, false);
-    } else {
-      if (causal) LTA_DQ34(attn_bwd_dq_v3_kernel, true);
-      else LTA_DQ34(attn_bwd_dq_v3_kernel, false);
-    }
-#undef LTA_DQ34
-  } else if (dq_delta) {
-    dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,
-                         ex.sx, (const T*)O, so);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, false>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,
-                         ex.sx, (const T*)O, so);
-  }
-  if (D == 128 && dkdv_v2 && g_dkdv_v3 && Tq > 0 && Sk > 0) {
-    dim3 g4(B * Hkv, (Sk + kKB3 - 1) / kKB3);
-#define LTA_DKDV3(KERN, CA)                                                                                          \
-  hipLaunchKernelGGL((KERN<T, CA>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V, (const T*)dO,              \
-                     (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx)
-    if (g_dkdv_v3 == 2) {
-      if (causal)
-        hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, true>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                           (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                           sl2, sdo, ex.sx, g_dkdv_qrev);
-      else
-        hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, false>), g4, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                           (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                           sl2, sdo, ex.sx, g_dkdv_qrev);
-    } else {
-      if (causal) LTA_DKDV3(attn_bwd_dkdv_v3_kernel, true);
-      else LTA_DKDV3(attn_bwd_dkdv_v3_kernel, false);
-    }
-#undef LTA_DKDV3
-  } else if (D == 128 && dkdv_v2) {
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo, ex.sx);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_v2_kernel<T, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                         sl2, sdo, ex.sx);
-  } else if (causal) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, true>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2,
-                       sdo, ex);
-  }
-  if (!causal && !(D == 128 && dkdv_v2))
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, false>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,
-                       sl2, sdo, ex);
-  if (dq_delta) {
-    // launched before the dK/dV kernel (above)
-  } else if (D == 128 && g_dq_v2 == 3 && Tq > 0 && Sk > 0) {
-    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-  } else if (D == 128 && g_dq_v2 == 2 && Tq > 0 && Sk > 0) {
-    dim3 g5(B * Hq, (Tq + kQB3 - 1) / kQB3);
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, true>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<T, false>), g5, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-  } else if (D == 128 && g_dq_v2 && Tq > 0 && Sk > 0) {
-    dim3 g3(B * Hq, (Tq + kBM2 - 1) / kBM2), blk3(kThreads2);
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, true>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<T, false>), g3, blk3, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex.sx);
-  } else if (causal) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, true>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, false>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,
-                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex);
-  }
+  dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM);
+#define LTA_V1(CA)                                                                                                   \
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, CA>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,          \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
+                     sdo, ex);                                                                                         \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, CA>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,            \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex)
+  if (causal) { LTA_V1(true); }
+  else { LTA_V1(false); }
+#undef LTA_V1
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-static int dkdv_v2_enabled() {
-  static const int v2 = [] {
-    const char* e = getenv("LTA_ATTN_BWD_V1");  // A/B switch: the v1 dK/dV kernel
+// LTA_ATTN_BWD_V1=1: the plain-HIP (v1) kernels for D = 128 too (A/B and bisection switch)
+static int fast_enabled() {
+  static const int fast = [] {
+    const char* e = getenv("LTA_ATTN_BWD_V1");
     return (e && e[0] == '1') ? 0 : 1;
   }();
-  return v2;
+  return fast;
 }
 
 // Attention backward with the RoPE backward fused into the dQ / dK epilogues (self-attention,
@@ -2318,8 +1307,7 @@ LTA_EXPORT int lta_attn_bwd_rope(int dtype, const void* dO, const void* Q, const
                                  int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
                                  const int64_t* qkv_strides, const int64_t* grad_strides, const float* rope_cos,
                                  const float* rope_sin, hipStream_t stream) {
-  if (D != 128 || Tq != Sk || Tq <= 0 || Hq % Hkv != 0 || !rope_cos || !rope_sin || g_dkdv_v3 != 2 || g_dq_v2 < 1 ||
-      !dkdv_v2_enabled())
+  if (D != 128 || Tq != Sk || Tq <= 0 || Hq % Hkv != 0 || !rope_cos || !rope_sin || !fast_enabled())
     return -1;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
@@ -2354,7 +1342,7 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
   const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
-  const int v2 = dkdv_v2_enabled();
+  const int v2 = fast_enabled();
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
   ex.sx.set_grad(grad_strides);
@@ -2430,21 +1418,8 @@ LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void
                         nullptr, stream);
 }
 
-// dQ kernel selection (A/B measurement hook): 1 = v2, 0 = v1; returns the previous choice
-LTA_EXPORT int lta_attn_bwd_set_dq_impl(int impl) {
-  const int old = g_dq_v2;
-  if (impl >= 0 && impl <= 3) g_dq_v2 = impl;
-  return old;
-}
-
-// dK/dV kernel selection (A/B measurement hook): 2 = v4, 1 = v3, 0 = v2; returns the previous choice
-LTA_EXPORT int lta_attn_bwd_set_dkdv_impl(int impl) {
-  const int old = g_dkdv_v3;
-  if (impl >= 0 && impl <= 2) g_dkdv_v3 = impl;
-  return old;
-}
-
-// dK/dV v4 query-tile order (A/B measurement hook): 1 = last tile first, 0 = first tile first
+// dK/dV query-tile order of the D = 128 kernel (A/B measurement hook): 1 = last tile first, 0 = first
+// tile first; returns the previous choice
 LTA_EXPORT int lta_attn_bwd_set_dkdv_qrev(int rev) {
   const int old = g_dkdv_qrev;
   g_dkdv_qrev = rev ? 1 : 0;

@@ -247,368 +247,11 @@ __global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// v2 (D = 128, no mask / dropout): 8 waves x 32 query rows = 256 queries per workgroup and one
-// workgroup per CU (two waves per SIMD), so a K/V tile staged in LDS feeds twice the queries of v1.
-//  * K and V tiles are register-staged (T14: global loads issued at the top of a tile, LDS writes
-//    at its end) into double-buffered LDS, one barrier per tile;
-//  * K runs one tile ahead of V: phase A of tile t computes S(t+1) = K(t+1) Q^T while the VALU
-//    finishes the softmax of tile t (exp2, row sum, bf16 pack); phase B computes O += V(t)^T P(t)
-//    while the VALU starts the softmax of tile t+1 (row max, rescale decision) (att[2], T15);
-//  * the scale is folded into the exponent (p = exp2(s*c - m), one FMA per score), the row max is
-//    a max3 tree on the raw scores plus one permlane32 swap;
-//  * the O rescale is skipped while no row max of the wave grows by more than THR (log2 units; T13;
-//    THR = 0 skips only exact no-growth tiles, bit-identical to always rescaling);
-//  * under causal masking only a wave's last tile straddles the diagonal (32-row waves, 64-key
-//    tiles), so the mask is one wave-uniform branch per wave; waves past their diagonal keep
-//    staging tiles for the rest of the workgroup without computing.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-__device__ __forceinline__ float row_max32(const f32x16 (&s)[2]) {
-  float m[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f32x16& x = s[c >> 1];
-    const int o = 8 * (c & 1);
-    float v = max3f(x[o], x[o + 1], x[o + 2]);
-    v = max3f(v, x[o + 3], x[o + 4]);
-    v = max3f(v, x[o + 5], x[o + 6]);
-    m[c] = max3f(v, x[o + 7], x[o + 7]);
-  }
-  float v = max3f(m[0], m[1], m[2]);
-  v = max3f(v, m[3], m[3]);
-  // swap(v, v): element 0 carries lanes 32..63 into lanes 0..31, element 1 lanes 0..31 into 32..63
-  // (each lane's own value in the other element), so max / sum over both elements pairs lane l with l^32
-  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return max3f(v, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
-}
-
-__device__ __forceinline__ float lane_pair_sum(float v) {
-  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // own + partner in every lane
-}
-
-template <typename T, bool CAUSAL, int THR, bool PIPE, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                                   const T* __restrict__ V, T* __restrict__ O,
-                                                                   float* __restrict__ LSE, int Hq, int Hkv, int Tq,
-                                                                   int Sk, float c, int64_t so_b, int64_t so_h,
-                                                                   int64_t so_t) {
-  constexpr int D = 128;
-  constexpr int kBM2 = 32 * NW, kThreads2 = 64 * NW, NLD = kBN * 16 / kThreads2;  // 16-B chunks / thread / tile
-  using C = Cfg<D>;
-  using F = typename Frag<T>::type;
-  constexpr int KT = kBN * C::KSTR, VT = kBN * C::VSTR;  // elements per K / V tile image
-  // PIPE: Q lives in LDS (the att[2] loop does not fit 256 registers with Q fragments held)
-  constexpr int QT = PIPE ? kBM2 * C::KSTR : 0;
-  __shared__ __attribute__((aligned(16))) short smem[2 * KT + 2 * VT + QT];
-
-  const int n_qt = (Tq + kBM2 - 1) / kBM2;
-  const int qt = n_qt - 1 - (int)blockIdx.y;  // heaviest causal blocks first
-  const int bh = blockIdx.x;                  // x-fastest: a head's blocks share one XCD's L2
-  const int b = bh / Hq, hq = bh % Hq;
-  const int hk = hq / (Hq / Hkv);
-  const T* Qb = Q + ((int64_t)b * Hq + hq) * Tq * D;
-  const T* Kb = K + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-  const T* Vb = V + ((int64_t)b * Hkv + hk) * (int64_t)Sk * D;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  short* Qs = smem + 2 * KT + 2 * VT + wave * 32 * C::KSTR;  // PIPE only
-  const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
-  const int q0 = qt * kBM2 + wave * 32;
-  const int qi = q0 + r;
-
-  int n_tiles = (Sk + kBN - 1) / kBN;
-  if (CAUSAL) n_tiles = min(n_tiles, (min(qt * kBM2 + kBM2, Tq) + kBN - 1) / kBN);
-  // this wave's tiles: [0, nw); only tile nw-1 can need the causal / key-edge mask
-  int nw = n_tiles;
-  if (CAUSAL) nw = min(n_tiles, min(q0 + 31, Tq - 1) / kBN + 1);
-  const bool last_masked = (nw * kBN > Sk) || (CAUSAL && (nw - 1) * kBN + kBN - 1 > q0);
-
-  F qf[PIPE ? 1 : C::KS];
-  if constexpr (!PIPE) {
-    const int qrow = min(qi, Tq - 1);
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[s] = load_frag<F>(Qb + (int64_t)qrow * D + 16 * s + 8 * h);
-  } else {
-    // this wave's 32 query rows -> its own LDS rows (visible after the prologue barrier)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = (i * 64 + lane) >> 4, ch = lane & 15;
-      const int qrow = min(q0 + row, Tq - 1);
-      *reinterpret_cast<uint4*>(Qs + row * C::KSTR + ch * 8) =
-          *reinterpret_cast<const uint4*>(Qb + (int64_t)qrow * D + ch * 8);
-    }
-  }
-
-  // ---- register staging (NLD 16-B chunks of K and of V per thread per tile) --------------------
-  uint4 kreg[NLD], vreg[NLD];
-  auto gload_k = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      const int kc = min(t * kBN + row, Sk - 1);  // clamped rows are real keys; the mask drops them
-      kreg[i] = *reinterpret_cast<const uint4*>(Kb + (int64_t)kc * D + ch * 8);
-    }
-  };
-  auto gload_v = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      const int kc = min(t * kBN + row, Sk - 1);
-      vreg[i] = *reinterpret_cast<const uint4*>(Vb + (int64_t)kc * D + ch * 8);
-    }
-  };
-  auto lstore_k = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      *reinterpret_cast<uint4*>(smem + buf * KT + row * C::KSTR + ch * 8) = kreg[i];
-    }
-  };
-  auto lstore_v = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int id = i * kThreads2 + tid, row = id >> 4, ch = id & 15;
-      *reinterpret_cast<uint4*>(smem + 2 * KT + buf * VT + row * C::VSTR + ch * 8) = vreg[i];
-    }
-  };
-
-  // ---- math pieces --------------------------------------------------------------------------------
-  f32x16 oacc[C::DT];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
-  float m_use = -INFINITY, l = 0.f, alpha = 1.f;
-  bool resc = false;
-
-  auto qk = [&](int buf, f32x16(&sacc)[2]) {
-    const short* Ks = smem + buf * KT;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const F qs = PIPE ? load_frag<F>(Qs + r * C::KSTR + 16 * s + 8 * h) : qf[PIPE ? 0 : s];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-        sacc[kt] = mfma(load_frag<F>(Ks + (kt * 32 + r) * C::KSTR + 16 * s + 8 * h), qs, sacc[kt]);
-    }
-  };
-  auto apply_mask = [&](int t, f32x16(&sacc)[2]) {
-    const int kbase = t * kBN;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kbase + kt * 32 + acc_row(i, h);
-        if (key >= Sk || (CAUSAL && key > qi)) sacc[kt][i] = -INFINITY;
-      }
-  };
-  // row max and the rescale decision for a freshly computed tile
-  auto start = [&](const f32x16(&sacc)[2]) {
-    const float mx = row_max32(sacc) * c;  // c > 0: the max commutes with the scale
-    const bool grow = !(mx - m_use <= (float)THR);  // true at m_use = -inf
-    resc = __builtin_amdgcn_ballot_w64(grow) != 0;  // wave-uniform
-    if (resc) {
-      const float mn = fmaxf(m_use, mx);
-      const float mu = (mn == -INFINITY) ? 0.f : mn;
-      alpha = __builtin_amdgcn_exp2f(m_use - mu);
-      m_use = mu;
-    }
-  };
-  // exponentials, row sum, l update and the bf16 P fragments of a started tile
-  auto finish = [&](f32x16(&sacc)[2], F(&pf)[2][2]) {
-    const float nm = -m_use;
-    float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kt][i], c, nm));
-        sacc[kt][i] = p;
-        if (i & 1) rs1 += p; else rs0 += p;
-      }
-    const float rs = lane_pair_sum(rs0 + rs1);
-    l = resc ? l * alpha + rs : l + rs;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      pack_frag(pf[kt][0], sacc[kt], 0);
-      pack_frag(pf[kt][1], sacc[kt], 1);
-    }
-  };
-  auto rescale_o = [&]() {
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-  };
-  auto pv = [&](int buf, const F(&pf)[2][2]) {
-    const __attribute__((address_space(3))) short* Vs3 =
-        (const __attribute__((address_space(3))) short*)(smem + 2 * KT + buf * VT);
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) {
-      const int col0 = dt * 32 + 16 * (g & 1);
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          oacc[dt] = mfma(tr_frag<F>(Vs3, kt * 32 + 16 * s + 4 * h, col0, C::VSTR, l16), pf[kt][s], oacc[dt]);
-    }
-  };
-
-  const int last = n_tiles - 1;
-  if constexpr (PIPE) {
-    // ---- prologue: K(0) -> LDS; K(1), V(0) -> LDS; S(0) and its softmax start ----------------------
-    gload_k(0);
-    lstore_k(0);
-    gload_k(min(1, last));
-    gload_v(0);
-    lstore_k(1);
-    lstore_v(0);
-    __syncthreads();
-    f32x16 sA[2], sB[2];
-    F pf[2][2];
-    qk(0, sA);
-    if (nw == 1 && last_masked) apply_mask(0, sA);
-    start(sA);
-    __syncthreads();  // every wave's reads of K(0) precede tile 0's overwrite of its buffer
-
-    // tile t: loads of K(t+2), V(t+1) in flight over the math; X = S(t) (started), Y <- S(t+1)
-    auto tile = [&](int t, f32x16(&X)[2], f32x16(&Y)[2]) {
-      gload_k(min(t + 2, last));
-      gload_v(min(t + 1, last));
-      if (t < nw) {
-        if (resc) rescale_o();  // PV(t-1) is complete in O; P(t) is at the new max
-        if (t + 1 < nw) {
-          __builtin_amdgcn_sched_barrier(0);
-          qk((t + 1) & 1, Y);  // phase A: S(t+1) || finish(t)
-          finish(X, pf);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // Q + K fragment reads
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // softmax-finish VALU
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // K fragment read
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 == nw - 1 && last_masked) apply_mask(t + 1, Y);
-          pv(t & 1, pf);  // phase B: PV(t) || start(t+1)
-          start(Y);
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // two V^T transposed reads
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 1);  // softmax-start VALU
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        } else {
-          finish(X, pf);
-          pv(t & 1, pf);
-        }
-      }
-      lstore_k(t & 1);        // K(t+2) over K(t) (read in tile t-1)
-      lstore_v((t + 1) & 1);  // V(t+1) over V(t-1) (read in tile t-1)
-      __syncthreads();
-    };
-    for (int t = 0; t < n_tiles; t += 2) {
-      tile(t, sA, sB);
-      if (t + 1 < n_tiles) tile(t + 1, sB, sA);
-    }
-  } else {
-    // ---- one S tile per wave; the two waves of a SIMD overlap each other's softmax and MFMAs -------
-    gload_k(0);
-    gload_v(0);
-    lstore_k(0);
-    lstore_v(0);
-    __syncthreads();
-    f32x16 S[2];
-    F pf[2][2];
-    for (int t = 0; t < n_tiles; ++t) {
-      gload_k(min(t + 1, last));  // tile t+1 in flight over tile t's math
-      gload_v(min(t + 1, last));
-      if (t < nw) {
-        qk(t & 1, S);
-        if (t == nw - 1 && last_masked) apply_mask(t, S);
-        start(S);
-        if (resc) rescale_o();
-        finish(S, pf);
-        pv(t & 1, pf);
-      }
-      lstore_k((t + 1) & 1);  // over tile t-1 (read before the last barrier)
-      lstore_v((t + 1) & 1);
-      __syncthreads();
-    }
-  }
-
-  // ---- epilogue: O = O^T / l ; LSE ------------------------------------------------------------------
-  if (qi < Tq) {
-    const float inv = (l > 0.f) ? 1.f / l : 0.f;
-    T* orow = O + b * so_b + hq * so_h + qi * so_t;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int d = dt * 32 + 8 * a + 4 * h;
-        union {
-          T v[4];
-          uint2 u;
-        } pk;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(oacc[dt][4 * a + e] * inv);
-        *reinterpret_cast<uint2*>(orow + d) = pk.u;
-      }
-    }
-    if (h == 0 && LSE != nullptr)
-      LSE[((int64_t)b * Hq + hq) * Tq + qi] = (l > 0.f) ? (m_use + log2f(l)) * 0.69314718055994530942f : -INFINITY;
-  }
-}
-
-// 0 = v1 (4 waves x 2 workgroups per CU), 1..6 = v2 variants (launch_v2), 7 / 8 = v3, 9 / 10 = v4
-// exact / deferred rescale (attention_fwd4.hip), 11..14 = v4 ablation builds.  Default: v4 deferred
-// for D = 128 without mask / dropout (profiles/attn_v4_*), v1 for everything else.
+// D = 128 without mask / dropout: 10 = v4 with the deferred O rescale (default), 9 = v4 exact online
+// softmax, 0 = v1 (the plain-HIP kernel every other configuration runs; profiles/attn_v4_*, retired
+// v2 / v3 kernels: profiles/attn_v2_ab.json, profiles/attn_fwd_pmc.json).  11..15 select the v4
+// measurement builds, compiled only with -DLTA_ATTN_DIAG.
 int g_fwd_impl = 10;
-
-template <typename T>
-int launch_v2(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
-              float scale, int causal, const int64_t* so, int impl, hipStream_t s) {
-  constexpr int D = 128;
-  const float c = scale * 1.44269504088896340736f;
-  const int nw = impl >= 5 ? 4 : 8;  // 5, 6: 4 waves x 2 workgroups per CU
-  dim3 grid(B * Hq, (Tq + 32 * nw - 1) / (32 * nw)), block(64 * nw);
-  const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * D, sh = so ? so[1] : (int64_t)Tq * D, st = so ? so[2] : D;
-#define LTA_V2(CA, TH, PI)                                                                                         \
-  if (nw == 4)                                                                                                     \
-    hipLaunchKernelGGL((attn_fwd_v2_kernel<T, CA, TH, false, 4>), grid, block, 0, s, (const T*)q, (const T*)k,     \
-                       (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st);                           \
-  else                                                                                                             \
-    hipLaunchKernelGGL((attn_fwd_v2_kernel<T, CA, TH, PI, 8>), grid, block, 0, s, (const T*)q, (const T*)k,        \
-                       (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st)
-  // impl: 1 = one S tile, exact rescale; 2 = one S tile, deferred rescale (THR 8);
-  //       3 = att[2] pipeline, exact; 4 = att[2] pipeline, deferred (all 8 waves, 1 workgroup / CU);
-  //       5 = one S tile, exact; 6 = one S tile, deferred (4 waves, 2 workgroups / CU)
-  const bool defer = impl == 2 || impl == 4 || impl == 6, pipe = impl == 3 || impl == 4;
-  if (causal) {
-    if (pipe) { if (defer) LTA_V2(true, 8, true); else LTA_V2(true, 0, true); }
-    else { if (defer) LTA_V2(true, 8, false); else LTA_V2(true, 0, false); }
-  } else {
-    if (pipe) { if (defer) LTA_V2(false, 8, true); else LTA_V2(false, 0, true); }
-    else { if (defer) LTA_V2(false, 8, false); else LTA_V2(false, 0, false); }
-  }
-#undef LTA_V2
-  return (int)hipGetLastError();
-}
 
 template <typename T, int D, int EX>
 int launch_ex(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
@@ -643,9 +286,6 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 LTA_EXPORT int lta_attn_fwd_v4(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
                                int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
                                const int64_t* o_strides, const int64_t* qkv_strides, int defer, hipStream_t stream);
-LTA_EXPORT int lta_attn_fwd_v3(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
-                               int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
-                               const int64_t* o_strides, int defer, hipStream_t stream);
 
 // o_strides: optional int64[3] (batch, head, token) element strides of O (head dim contiguous);
 // null = contiguous [B,H,T,D].  [B,T,H,D] storage lets the output projection read O without a copy.
@@ -660,7 +300,6 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f) return -2;
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
-  const bool dense = ex.sx.is_contiguous(Hq, Hkv, Tq, Sk, D);  // the experimental v2 / v3 kernels read dense only
   int exf = 0;
   if (mask) {
     const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;
@@ -683,15 +322,6 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
                                    qkv_strides, g_fwd_impl == 9 ? 0 : (g_fwd_impl == 10 ? 1 : 1 | ((g_fwd_impl - 10) << 1)),
                                    stream);
     if (rc != -1) return rc;
-  }
-  if (dense && D == 128 && exf == 0 && g_fwd_impl >= 7 && g_fwd_impl <= 8 && Tq > 0 && Sk > 0)  // v3: 64 rows per wave (attention_fwd3.hip)
-    return lta_attn_fwd_v3(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides, g_fwd_impl == 8,
-                           stream);
-  if (dense && D == 128 && exf == 0 && g_fwd_impl != 0 && Tq > 0 && Sk > 0) {
-    if (dtype == kBF16)
-      return launch_v2<__hip_bfloat16>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, g_fwd_impl, stream);
-    if (dtype == kF16)
-      return launch_v2<__half>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, g_fwd_impl, stream);
   }
   if (dtype == kBF16) {
     if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);

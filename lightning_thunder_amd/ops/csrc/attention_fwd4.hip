@@ -550,6 +550,7 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
   hipLaunchKernelGGL((attn_fwd_v4_kernel<T, CA, TH>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, \
                      (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st, sx)
 #endif
+#ifdef LTA_ATTN_DIAG  // measurement builds (scripts/attn_v4_ablate.py, attn_v4_stamps.py)
   if (abl) {
 #define LTA_V4A(A)                                                                                                   \
   if (causal)                                                                                                        \
@@ -566,6 +567,9 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 #undef LTA_V4A
     return (int)hipGetLastError();
   }
+#else
+  if (abl) return -1;
+#endif
   if (causal) {
     if (thr) LTA_V4(true, 8); else LTA_V4(true, 0);
   } else {

@@ -657,14 +657,23 @@ __global__ __launch_bounds__(256) void gemm4_tail_fixup(const float* __restrict_
   *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = o.u;
 }
 
-// Plain product with a wave-quantisation tail: the last partial wave of tiles (tail <= 128 tiles of
-// 256 CUs) runs as 2 K-slices per tile (so it takes half a tile time instead of a whole one), then a
+// Plain product with a wave-quantisation tail: the last partial wave of tiles (at most half as many
+// tiles as CUs) runs as 2 K-slices per tile (so it takes half a tile time instead of a whole one), then a
 // fixup sums the two fp32 partials.  Returns -1 when the shape does not qualify.
+// Compute units of the current device (one resident workgroup each): the wave size of the tile grid.
+int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return n > 0 ? n : 256;
+}
+
 template <bool AT, bool BT>
 int launch4_tail(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                  void* ws, int64_t ws_bytes, hipStream_t s) {
-  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN), tail = nwg % 256;
-  if (nwg <= 256 || tail == 0 || tail > 128 || K % (2 * BK * 2) || !ws || ws_bytes < (int64_t)2 * tail * BM * BN * 4)
+  const int cus = device_cus();
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN), tail = nwg % cus;
+  if (nwg <= cus || tail == 0 || 2 * tail > cus || K % (2 * BK * 2) || !ws || ws_bytes < (int64_t)2 * tail * BM * BN * 4)
     return -1;
   EpiArgs ep{};
   ep.tile_base = 0;
@@ -726,8 +735,7 @@ int dispatch_layout(const void* A, const void* B, void* C, const void* bias, con
 //   bt = 0: B [N][K] (nn.Linear weight)       bt = 1: B stored [K][N]
 // act/bias only with at = bt = 0.  Any M, N with N % 8 == 0 (edge tiles: clamped operand sources,
 // masked stores), K % 128 == 0, 16-B aligned rows, operands under 2 GiB (32-bit buffer offsets).
-// variant: glds split (0: all in the barrier phase, 1: half, 2: a quarter; see the header).  Variant 1
-// is the production kernel (every epilogue); 0 and 2 are plain products kept for A/B measurement.
+// variant: glds split; 1 (half of a K-tile's LDS-DMA loads in the barrier phase) is the only one built.
 LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
                               int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
                               int variant, hipStream_t s) {
@@ -736,18 +744,11 @@ LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void*
   // buffer-resource byte offsets are 32-bit
   const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
   if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
-  if (variant == 1) return dispatch_layout<1>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, s);
-  // the other glds splits exist for A/B measurement: plain products only
-  if (act != kNone || bias || R) return -1;
-#define LTA_G4V(V)                                                                                              \
-  if (!at && !bt) return launch4<kNone, false, false, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s); \
-  if (!at && bt) return launch4<kNone, false, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
-  if (at && !bt) return launch4<kNone, true, false, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);   \
-  return launch4<kNone, true, true, V>(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, alpha, s);
-  if (variant == 0) { LTA_G4V(0) }
-  if (variant == 2) { LTA_G4V(2) }
-#undef LTA_G4V
-  return -1;
+  // variant: the LDS-DMA split (1 = 8 of a K-tile's 16 LDS-DMA loads in the previous tile's second
+  // half).  The measured alternatives (0: all 16, 2: 4; profiles/gemm4_microbench.json g4v0 / g4v2)
+  // are retired from the library; the argument stays in the ABI.
+  if (variant != 1) return -1;
+  return dispatch_layout<1>(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, s);
 }
 
 // lta_gemm4_bf16 with a workspace: a plain product (no act / bias / residual, variant 1) whose tile

@@ -222,12 +222,18 @@ class _DelayedState:
 
 
 _DELAYED: dict[int, _DelayedState] = {}
+_DELAYED_KEYS = iter(range(1 << 62))
 
 
 def new_delayed_state(recipe: DelayedScaling, n_slots: int) -> int:
-    key = len(_DELAYED)
+    key = next(_DELAYED_KEYS)
     _DELAYED[key] = _DelayedState(recipe, n_slots)
     return key
+
+
+def release_delayed_state(key: int) -> None:
+    """Drop a state no program uses (the transform registered it, then converted no linear)."""
+    _DELAYED.pop(key, None)
 
 
 def delayed_state(key: int) -> _DelayedState:
@@ -260,7 +266,13 @@ def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
     very amax the first one used, so the recompute reproduces the forward's fp8 values bit for bit
     (also on a slot's first step, where the forward fell back to current scaling and the history is
     still empty); its amax contribution is the same max again (reference: TE's recompute-phase
-    handling, thunder/executors/transformer_engineex_impl.py:459-515)."""
+    handling, thunder/executors/transformer_engineex_impl.py:459-515).
+
+    Requirement: each forward is followed by its own backward before the next forward (f1 b1 f2 b2).
+    The scaling source is the live history max, which ``delayed_update`` advances at the start of
+    every forward; with interleaved schedules (f1 f2 b2 b1: pipelining, or accumulation that runs
+    several forwards first) the recompute of f1's checkpointed region inside b1 would read f2's
+    scaling source and no longer reproduce f1's fp8 values bit for bit."""
     st = _DELAYED[key]
     st.ensure(t.device)
     t2 = t.reshape(-1, t.shape[-1])

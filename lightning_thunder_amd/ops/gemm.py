@@ -86,14 +86,39 @@ register_signature("lta_gemm4_bf16_ws", [c_void_p, c_void_p, c_void_p, c_void_p,
 _TAIL_SPLIT = _os.environ.get("LTA_GEMM_TAIL_SPLIT", "1") != "0"
 
 
+_CUS: dict = {}
+_WS: dict = {}
+
+
+def _device_cus(device) -> int:
+    """Compute units of ``device`` (the kernel reads the same attribute: hipDeviceAttributeMultiprocessorCount)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _CUS:
+        _CUS[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count)
+    return _CUS[idx]
+
+
 def _tail_workspace(M: int, N: int, K: int, device):
     if not _TAIL_SPLIT or K % 256:
         return None
+    cus = _device_cus(device)
     nwg = -(-M // 256) * -(-N // 256)
-    tail = nwg % 256
-    if nwg <= 256 or tail == 0 or tail > 128:
+    tail = nwg % cus
+    if nwg <= cus or tail == 0 or 2 * tail > cus:
         return None
-    return torch.empty(2 * tail * 256 * 256, dtype=torch.float32, device=device)
+    # one cached fp32 workspace per (device, stream), grown to the largest tail seen: the partials are
+    # consumed by the fixup launched right behind the split on the same stream, so reuse is ordered
+    need = 2 * tail * 256 * 256
+    if torch.cuda.is_current_stream_capturing():
+        # a captured graph keeps the pointer: give it its own allocation (from the graph's pool), never
+        # one a later, larger tail could replace
+        return torch.empty(need, dtype=torch.float32, device=device)
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
 
 
 GEMM4_MIN_M = 64
@@ -116,6 +141,8 @@ def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
         return None
     at = 0 if la[0] == 1 else 1
     bt = 1 if lb[0] == 1 else 0
+    if at and M % 8:  # an MN-major A is staged in 16-B row pieces (the kernel returns -2 otherwise)
+        return None
     # 32-bit buffer offsets
     if (K if at else M) * la[1] * 2 >= 2 ** 31 or (K if bt else N) * lb[1] * 2 >= 2 ** 31:
         return None

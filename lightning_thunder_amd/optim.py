@@ -27,6 +27,7 @@ class AdamW(torch.optim.Optimizer):
         self._managed: dict = {}  # id(param) -> param group (overlap mode)
         self._side: dict = {}  # device -> side stream of the overlapped updates
         self._inflight: list = []  # metadata tensors read by queued side-stream launches
+        self._handled: set = set()  # id(param) updated inside a backward since the last step()
 
     # --- update overlapped with the backward (transforms/optimizer_overlap.py) ----------------------
     def overlap_with_backward(self, jitted, bucket_mb: int = 128) -> None:
@@ -40,10 +41,23 @@ class AdamW(torch.optim.Optimizer):
     def manages(self, t) -> bool:
         return isinstance(t, torch.Tensor) and t.is_cuda and id(t) in self._managed
 
+    def _mark_handled(self, params) -> None:
+        """Records that ``params`` were updated inside a backward of this iteration; a second update
+        before ``step()`` is an error.  It would come from a second backward node (the jitted function
+        called twice before one backward, or a weight shared between jitted calls), each holding only
+        a partial gradient, and would apply a second AdamW step."""
+        for p in params:
+            if id(p) in self._handled:
+                raise RuntimeError("overlapped optimizer: parameter of shape "
+                                   f"{tuple(p.shape)} updated twice in one iteration; call step() after every "
+                                   "backward, or do not use overlap_with_backward for this model")
+        self._handled.update(id(p) for p in params)
+
     @torch.no_grad()
     def overlapped_update(self, params, grads) -> None:
         """Called from the backward: update ``params`` with ``grads`` on the side stream, ordered
         after everything the compute stream has queued so far."""
+        self._mark_handled(params)
         dev = params[0].device
         side = self._side.get(dev)
         if side is None:
@@ -87,12 +101,18 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._join()
+        handled, self._handled = self._handled, set()
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             buckets: dict = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
+                if id(p) in handled:
+                    # p was already updated inside the backward; a gradient accumulated into p.grad by
+                    # another autograd path would otherwise get a second step this iteration
+                    raise RuntimeError(f"overlapped optimizer: parameter of shape {tuple(p.shape)} was updated "
+                                       "in the backward and also has p.grad set")
                 st = self._state(p)
                 st["step"] += 1
                 if p.device.type != "cuda":

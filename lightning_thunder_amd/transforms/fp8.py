@@ -139,6 +139,10 @@ class FP8LinearTransform(Transform):
                 new.bound_symbols.append(cv if cv is not None else nb)
         self.n_converted = n
         if not n:
+            if key is not None:
+                from ..ops.fp8 import release_delayed_state
+
+                release_delayed_state(key)
             return prologue_trace, computation_trace, epilogue_trace
         if delayed:
             from ..ops.fp8 import delayed_state

@@ -35,12 +35,42 @@ _tls = threading.local()
 
 from ..examine.memory_calculation import is_view_bsym as _is_view  # noqa: E402
 
+# ops that may hand back their input tensor itself at run time (no fresh allocation): torch returns
+# ``a`` from contiguous() of a contiguous tensor, from detach()/alias() (new view of the same
+# storage), and from to()/type_as()/float()... when nothing changes; in-place ops return ``self``
+_MAY_RETURN_INPUT = {"contiguous", "detach", "alias", "shallow_copy", "to", "type_as", "type", "convert_element_type",
+                     "float", "double", "half", "bfloat16", "int", "long", "short", "bool", "byte", "char", "cpu",
+                     "cuda", "requires_grad_", "data", "clone_if_needed", "view_as_real", "view_as_complex",
+                     "resolve_conj", "resolve_neg", "conj", "real", "lift_fresh", "copy_with_setitem", "copy_"}
+
+
+def may_alias_bsym(b) -> bool:
+    """True when an output of ``b`` may share storage with its first tensor input at run time: views,
+    the identity-returning conversions above (same dtype / shape out as in), in-place ops (trailing
+    ``_``), and composite bound symbols containing any of these."""
+    if _is_view(b):
+        return True
+    nm = str(getattr(b.sym, "name", ""))
+    base = nm[:-5] if nm.endswith("_prim") else nm
+    base = base.rsplit(".", 1)[-1]
+    ins = [a for a in b.flat_proxy_args if isinstance(a, TensorProxy)]
+    outs = [o for o in b.flat_proxy_outs if isinstance(o, TensorProxy)]
+    if not ins or not outs:
+        return False
+    if base.endswith("_") and not base.endswith("__"):
+        return True
+    if base in _MAY_RETURN_INPUT:
+        a = ins[0]
+        return any(o.dtype == a.dtype and tuple(o.shape) == tuple(a.shape) for o in outs)
+    return any(may_alias_bsym(s) for s in (getattr(b, "subsymbols", None) or ()))
+
 
 def view_aliases(trace, alias_of: dict | None = None) -> dict:
-    """name -> root name for every value of ``trace`` that may be a view of another value."""
+    """name -> root name for every value of ``trace`` that may share storage with another value (views
+    and ops that may return their input: :func:`may_alias_bsym`)."""
     alias_of = dict(alias_of or {})
     for b in trace.bound_symbols:
-        if not _is_view(b):
+        if not may_alias_bsym(b):
             continue
         srcs = [a.name for a in b.flat_proxy_args if isinstance(a, TensorProxy)]
         if not srcs:

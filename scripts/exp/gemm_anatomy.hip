@@ -1,0 +1,192 @@
+// GEMM anatomy builds (measurement only, never part of the library): the production gemm4 NT main
+// loop (csrc/gemm4.hip, variant 1) with parts removed, to price each part of a K-tile on random data.
+//   ABL bit 0: no LDS-DMA in the main loop      bit 1: no fragment ds_reads in the main loop
+//   ABL bit 2: no per-tile wait + barrier        bit 3: no epilogue (accumulators kept live, no stores)
+// Every workgroup's wave 0 stamps s_memtime / s_memrealtime around its whole life into `st`
+// (4 x u64 per workgroup), from which the in-kernel clock is read (MI355X_MICROARCH.md give-back 6).
+#include "common.h"
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
+constexpr int OP_BYTES = BM * BK * 2, STAGE = 2 * OP_BYTES;
+
+__device__ __forceinline__ int xcd_tile(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), bytes, 0x00020000};
+}
+struct Stager {
+  i32x4 rsrc;
+  int voff[8];
+  __device__ __forceinline__ void init(const __hip_bfloat16* X, int ld, int r0, int K, int wave, int lane) {
+    rsrc = make_rsrc(X + (int64_t)r0 * ld, (BM - 1) * ld * 2 + K * 2);
+    const int r = lane >> 3, c = (lane & 7) ^ r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) voff[i] = ((32 * i + wave * 8 + r) * ld + c * 8) * 2;
+  }
+  __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(dst), "v"(voff[i]), "s"(rsrc), "s"(kt * BK * 2)
+                 : "memory", "m0");
+  }
+};
+__device__ __forceinline__ bf16x8 read_frag(const char* img, int rc, int kk, int fr, int fq) {
+  const int row = rc + fr;
+  return *reinterpret_cast<const bf16x8*>(img + row * 128 + (((kk * 4 + fq) ^ (fr & 7)) << 4));
+}
+__device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+#define FENCE() __builtin_amdgcn_sched_barrier(0)
+
+template <int ABL>
+__global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __restrict__ A, const __hip_bfloat16* __restrict__ B,
+                                                      __hip_bfloat16* __restrict__ C, int M, int N, int K, uint64_t* st) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
+  uint64_t t0 = 0, r0 = 0;
+  if (wave == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  const int nTm = M / BM, nTn = N / BN, nwg = nTm * nTn;
+  const int wg = xcd_tile((int)blockIdx.x, nwg);
+  constexpr int G = 8;
+  const int per_group = G * nTn, group = wg / per_group, first_m = group * G, gm = min(nTm - first_m, G);
+  const int tm = first_m + (wg % per_group) % gm, tn = (wg % per_group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  Stager sa, sb;
+  sa.init(A, K, m0, K, wave, lane);
+  sb.init(B, K, n0, K, wave, lane);
+  auto glds = [&](int j, int kt, char* stage) {
+    if (j < 8) sa.issue(j, kt, stage, wave); else sb.issue(j - 8, kt, stage + OP_BYTES, wave);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  auto read_one = [&](const char* stage, int kk, int r, bf16x8* fa, bf16x8* fb) {
+    if (r == 0) fa[0] = read_frag(stage, wm * 128, kk, fr, fq);
+    else if (r <= 8) fb[r - 1] = read_frag(stage + OP_BYTES, wn * 128 + (r - 1) * 16, kk, fr, fq);
+    else fa[r - 8] = read_frag(stage, wm * 128 + (r - 8) * 16, kk, fr, fq);
+  };
+  constexpr int NB2 = 8, NA = 8;
+  constexpr bool G_ON = !(ABL & 1), R_ON = !(ABL & 2), B_ON = !(ABL & 4);
+  const int nk = K / BK;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) glds(j, 0, smem);
+#pragma unroll
+  for (int j = 0; j < NB2; ++j) glds(j, 1, smem + STAGE);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB2) : "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) read_one(smem, 0, r, fa0, fb0);
+  if constexpr (!R_ON) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) read_one(smem, 1, r, fa1, fb1);
+  }
+  auto body = [&](int t, auto cur_c) {
+    constexpr int CUR = decltype(cur_c)::value;
+    char* const bc = smem + CUR * STAGE;
+    char* const bn = smem + (CUR ^ 1) * STAGE;
+    const int t1 = min(t + 1, nk - 1), t2 = min(t + 2, nk - 1);
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
+      if (R_ON && (i & 3) == 0) read_one(bc, 1, i >> 2, fa1, fb1);
+      if (G_ON && (i & 3) == 2 && (i >> 2) < NA) glds(NB2 + (i >> 2), t1, bn);
+      FENCE();
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      FENCE();
+    }
+    if constexpr (B_ON) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    FENCE();
+#pragma unroll
+    for (int i = 32; i < 64; ++i) {
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      const int s = i - 32;
+      if (R_ON && (s & 1) == 0) read_one(bn, 0, s >> 1, fa0, fb0);
+      else if (G_ON && (s & 3) == 1 && (s >> 2) < NB2) glds(s >> 2, t2, bc);
+      FENCE();
+    }
+  };
+  for (int t = 0; t < nk; t += 2) {
+    body(t, std::integral_constant<int, 0>{});
+    body(t + 1, std::integral_constant<int, 1>{});
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (!(ABL & 8)) {
+    char* wbuf = smem + wave * (128 * 256);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int col = n * 16 + fr, ch = col >> 3, co = (col & 7) * 2;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = m * 16 + fq * 4 + j;
+          *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4) + co) = __float2bfloat16(acc[m][n][j]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 32; ++it) {
+      const int id = it * 64 + lane, row = id >> 4, ch = id & 15;
+      const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * N + n0 + wn * 128 + ch * 8) = v;
+    }
+  } else {
+    // keep the accumulators live without storing them
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n) s += acc[m][n][0];
+    if (s == 1234.5f) C[tid] = __float2bfloat16(s);
+  }
+  if (wave == 0 && lane == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    st[blockIdx.x * 4 + 0] = t0;
+    st[blockIdx.x * 4 + 1] = t1;
+    st[blockIdx.x * 4 + 2] = r0;
+    st[blockIdx.x * 4 + 3] = r1;
+  }
+}
+}  // namespace
+
+LTA_EXPORT int anat_gemm(int abl, const void* A, const void* B, void* C, int M, int N, int K, void* st, hipStream_t s) {
+  if (M % BM || N % BN || K % (2 * BK)) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define L(X) case X: hipLaunchKernelGGL(anat_kernel<X>, grid, block, 0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, M, N, K, (uint64_t*)st); break;
+  switch (abl) {
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(15)
+    default: return -1;
+  }
+#undef L
+  return (int)hipGetLastError();
+}

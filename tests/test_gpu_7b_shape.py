@@ -28,6 +28,9 @@ def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
         monkeypatch.setenv("LTA_GEMM", "hip")
     if gemm_mode == "fused_swiglu":
         monkeypatch.setenv("LTA_FUSED_SWIGLU", "1")
+    from lightning_thunder_amd.ops import gemm as G
+
+    G.last_gemm_backend_counts(reset=True)  # counts are per process: earlier tests may have used torch
     torch.manual_seed(0)
     dev = torch.device("cuda")
     m32 = GPT.from_name("llama2-7b-shape-2l").to(device=dev)

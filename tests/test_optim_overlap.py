@@ -9,7 +9,7 @@ import torch
 
 import lightning_thunder_amd as thunder
 from lightning_thunder_amd.optim import AdamW
-from lightning_thunder_amd.transforms.optimizer_overlap import _is_view
+from lightning_thunder_amd.transforms.optimizer_overlap import _is_view, may_alias_bsym
 
 
 class _CPUOverlapAdamW(AdamW):
@@ -20,6 +20,7 @@ class _CPUOverlapAdamW(AdamW):
 
     @torch.no_grad()
     def overlapped_update(self, params, grads):
+        self._mark_handled(params)
         self.calls = getattr(self, "calls", 0) + 1
         for p, g in zip(params, grads):
             group = self._managed[id(p)]
@@ -101,6 +102,105 @@ def test_hooks_wait_for_the_last_parameter_read():
             if j > i and any(a.name in alias for a in b.flat_proxy_args) and not str(b.sym.name).startswith("optim_"):
                 if b.sym.name not in ("python_return", "python_del"):
                     raise AssertionError(f"{pname} read by {b.sym.name} after its update hook")
+
+
+def test_second_backward_update_in_one_iteration_raises():
+    """Two calls of the jitted model before one backward: two backward nodes would each hand over a
+    partial gradient and the parameter would get two AdamW steps; the optimizer refuses."""
+    m = _mlp()
+    opt = _CPUOverlapAdamW(m.parameters(), lr=1e-2)
+    jm = thunder.jit(m)
+    opt.overlap_with_backward(jm, bucket_mb=0)
+    x1, x2 = torch.randn(8, 32), torch.randn(8, 32)
+    with pytest.raises(RuntimeError, match="updated twice"):
+        (jm(x1).sum() + jm(x2).sum()).backward()
+    # one call per backward keeps working after a step() clears the iteration's record
+    opt._handled.clear()
+    opt.zero_grad(set_to_none=True)
+    jm(x1).sum().backward()
+    opt.step()
+    jm(x2).sum().backward()
+    opt.step()
+
+
+def test_updated_param_with_grad_from_another_path_raises():
+    m = _mlp()
+    opt = _CPUOverlapAdamW(m.parameters(), lr=1e-2)
+    jm = thunder.jit(m)
+    opt.overlap_with_backward(jm, bucket_mb=0)
+    w = m[0].weight
+    (jm(torch.randn(8, 32)).sum() + w.square().sum()).backward()  # eager use of w outside the program
+    assert w.grad is not None
+    with pytest.raises(RuntimeError, match="also has p.grad"):
+        opt.step()
+
+
+class _ContiguousWeight(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.w = torch.nn.Parameter(torch.randn(32, 32))
+        self.v = torch.nn.Parameter(torch.randn(32, 32))
+
+    def forward(self, x):
+        wc = self.w.contiguous()  # may return w itself at run time: an alias saved for the backward
+        h = torch.tanh(x @ wc.t())
+        h = torch.tanh(h @ self.v.t())
+        return (h @ wc).sum()  # wc read again late in the backward (dgrad of the last product)
+
+
+def test_hook_waits_for_reads_through_identity_ops():
+    """``contiguous(w)`` saved in the forward is read late in the backward: the update hook of w must
+    follow that read (an early hook would let the side-stream AdamW write w while it is still read)."""
+    from lightning_thunder_amd.transforms.optimizer_overlap import insert_grad_ready_hooks
+
+    m = _ContiguousWeight()
+    jm = thunder.jit(m)
+    jm(torch.randn(8, 32)).backward()
+    bw = thunder.last_backward_traces(jm)[0]
+    fw = thunder.last_traces(jm)[0]
+    comp = thunder.last_traces(jm)[0]
+    names = [a.name for a in comp.args if hasattr(a, "requires_grad") and a.requires_grad]
+    new = insert_grad_ready_hooks(bw, names, bucket_bytes=0, fw=fw)
+    alias = {}
+    for tr in (fw, new):
+        for b in tr.bound_symbols:
+            if may_alias_bsym(b):
+                srcs = [a.name for a in b.flat_proxy_args if hasattr(a, "shape")]
+                if srcs:
+                    for o in b.flat_proxy_outs:
+                        alias[o.name] = alias.get(srcs[0], srcs[0])
+    bs = new.bound_symbols
+    checked = 0
+    for i, b in enumerate(bs):
+        if not str(b.sym.name).startswith("optim_grad_ready"):
+            continue
+        for k in b.args[0]:
+            pname = names[k]
+            for j in range(i + 1, len(bs)):
+                bj = bs[j]
+                if str(bj.sym.name) in ("python_return", "python_del") or str(bj.sym.name).startswith("optim_"):
+                    continue
+                for a in bj.flat_proxy_args:
+                    assert alias.get(a.name, a.name) != pname, f"{pname} read through {a.name} after its hook"
+            checked += 1
+    assert checked >= 1
+
+
+def test_may_alias_bsym_identity_ops():
+    def f(x):
+        a = x.contiguous()
+        b = x.to(torch.float32)
+        c = x.to(torch.float64)
+        return a, b, c
+
+    jf = thunder.jit(f)
+    jf(torch.randn(4, 4))
+    tr = thunder.last_traces(jf)[0]
+    flags = {str(b.sym.name): may_alias_bsym(b) for b in tr.bound_symbols if b.flat_proxy_args}
+    assert flags.get("contiguous") is True
+    conv = [may_alias_bsym(b) for b in tr.bound_symbols if str(b.sym.name) in ("to", "convert_element_type")]
+    assert conv == [False], flags  # x.to(float32) of a float32 x is x itself in the trace; float64 allocates
 
 
 @pytest.mark.gpu
