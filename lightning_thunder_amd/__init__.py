@@ -263,8 +263,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
                 from .transforms.rematerialization import rematerialize_forward_and_backward
 
                 fb = rematerialize_forward_and_backward(fb)
-            fw_traces = [fb.forward_trace] + transform_for_execution(fb.forward_trace, executors)
-            bw_traces = [fb.backward_trace] + transform_for_execution(fb.backward_trace, executors)
+            from .distributed.utils import lower_tp_syncs
+
+            fw_traces = [fb.forward_trace] + transform_for_execution(lower_tp_syncs(fb.forward_trace), executors)
+            bw_traces = [fb.backward_trace] + transform_for_execution(lower_tp_syncs(fb.backward_trace), executors)
             fw = fw_traces[-1]
             bw = bw_traces[-1]
             fw = maybe_sort_waits(fw)
@@ -311,7 +313,9 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
                 if comp2 is not comp:
                     comp = comp2
                     computation_traces.append(comp)
-            ex_traces = transform_for_execution(comp, executors)
+            from .distributed.utils import lower_tp_syncs
+
+            ex_traces = transform_for_execution(lower_tp_syncs(comp), executors)
             c = ex_traces[-1]
             c = maybe_sort_waits(c)
             window = cd.compile_options.get("lta_fsdp_allgather_window")

@@ -281,17 +281,23 @@ vocab_parallel_cross_entropy_bwd = _make("vocab_parallel_cross_entropy_bwd", _vp
 # Runtime (torch executor) implementations: RCCL via torch.distributed
 # =========================================================================================
 class FutureHandle:
-    """(Work, tensor) pair produced by an async collective."""
+    """(Work, tensor) pair produced by an async collective; ``post`` (optional) turns the received
+    buffer into the result once the collective has completed (e.g. the rank-major -> last-dim
+    rearrangement of an all-gather along the last dim)."""
 
-    __slots__ = ("work", "tensor")
+    __slots__ = ("work", "tensor", "post")
 
-    def __init__(self, work, tensor):
+    def __init__(self, work, tensor, post=None):
         self.work = work
         self.tensor = tensor
+        self.post = post
 
     def wait(self):
         if self.work is not None:
             self.work.wait()
+            self.work = None
+        if self.post is not None:
+            self.tensor, self.post = self.post(self.tensor), None
         return self.tensor
 
 
@@ -311,6 +317,19 @@ def _all_reduce_impl(a, op, group, do_async=False, skip_clone=False):
 def _all_gather_impl(a, group, do_async=False, dim=0):
     w = _world(group)
     a = a.contiguous()
+    dim = dim % a.ndim if a.ndim else 0
+    if dim == a.ndim - 1 and dim != 0 and tdist.get_backend(group) != "gloo":
+        # last-dim gather (tensor-parallel column output): ONE rank-major all_gather_into_tensor of the
+        # [rows, n] view, rearranged to [rows, w * n] when the result is needed (after the wait)
+        rows, n = a.numel() // a.shape[-1], a.shape[-1]
+        buf = torch.empty((w * rows, n), dtype=a.dtype, device=a.device)
+        work = tdist.all_gather_into_tensor(buf, a.view(rows, n), group=group, async_op=do_async)
+        lead = tuple(a.shape[:-1])
+
+        def post(b):
+            return b.view(w, rows, n).permute(1, 0, 2).reshape(*lead, w * n)
+
+        return FutureHandle(work, buf, post) if do_async else post(buf)
     if dim != 0 or tdist.get_backend(group) == "gloo":
         parts = [torch.empty_like(a) for _ in range(w)]
         work = tdist.all_gather(parts, a, group=group, async_op=do_async)
@@ -577,7 +596,9 @@ def _register_vjps():
         out = all_reduce(a, op, group, do_async, skip_clone)
 
         def bwd(g):
-            return (all_reduce(g, op, group, False, False),)
+            # async (a wait that sort_waits can move past independent backward work); cloned: g may
+            # have other consumers
+            return (wait(all_reduce(g, op, group, True, False)),)
 
         return out, bwd
 
@@ -602,7 +623,9 @@ def _register_vjps():
 
         def bwd(g):
             if layer_type is TPLayerType.COLUMN_LINEAR:
-                return (all_reduce(g, DistributedReduceOps.SUM, group, False, False),)
+                # the input gradient summed over the column shards: the same all-reduce as a row
+                # linear's output, lowered to an async in-place all-reduce + wait (lower_tp_syncs)
+                return (synchronize_tensor_parallel_output(g, group, TPLayerType.ROW_LINEAR),)
             if layer_type is TPLayerType.ROW_LINEAR:
                 return (synchronize_tensor_parallel_output(g, group, TPLayerType.COLUMN_LINEAR),)
             return (g,)

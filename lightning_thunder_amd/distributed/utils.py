@@ -16,6 +16,67 @@ from ..core.symbol import BoundSymbol
 from ..core.trace import TraceCtx, from_trace, TraceProvenance
 
 
+def lower_tp_syncs(trace: TraceCtx) -> TraceCtx:
+    """Tensor-parallel syncs -> explicit async collectives + ``wait`` (reference: the TP prims issue
+    ``all_reduce(..., do_async=True, skip_clone=True).wait()`` / ``all_gather(..., True).wait()``,
+    thunder/distributed/prims.py:433-551), so that :func:`sort_waits` can move each wait past
+    independent work — e.g. a column-parallel linear's input-gradient all-reduce runs under the same
+    layer's weight-gradient GEMM.
+
+    * all-reduce syncs (row-parallel output, vocab-parallel embedding output, and the column-parallel
+      input gradient, which the VJP expresses as the same sync) -> ``all_reduce(a, SUM, group, True,
+      skip_clone)`` + ``wait``; the all-reduce runs in place (no clone) when ``a`` is a fresh tensor
+      nothing else reads: not a trace input or output, read only by this sync, and not made by an op
+      that may return (a view of) its input;
+    * last-dim all-gather syncs (column-parallel output) -> ``all_gather(a, group, True, -1)`` + ``wait``;
+    * the input-side syncs (identity / local slice) stay as they are.
+    Run on the traces right after autodiff, before the executors claim them."""
+    from .prims import (synchronize_tensor_parallel_output as tp_out, TPLayerType, all_reduce, all_gather, wait,
+                        DistributedReduceOps)
+    from ..transforms.optimizer_overlap import may_alias_bsym
+    from ..core.proxies import TensorProxy
+    from ..core.trace import tracectx
+
+    bsyms = list(trace.bound_symbols)
+    if not any(b.sym is tp_out for b in bsyms):
+        return trace
+    readers: dict[str, int] = {}
+    producer: dict[str, BoundSymbol] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            readers[a.name] = readers.get(a.name, 0) + 1
+        for o in b.flat_proxy_outs:
+            producer.setdefault(o.name, b)
+    from ..core.pytree import tree_flatten
+
+    inputs = {a.name for a in tree_flatten((trace.args, trace.kwargs))[0] if isinstance(a, Proxy)}
+    new = from_trace(trace)
+    out: list = []
+    n = 0
+    with tracectx(new):
+        for b in bsyms:
+            if b.sym is not tp_out:
+                out.append(b)
+                continue
+            a, group, kind = b.args[0], b.args[1], b.args[2]
+            if kind in (TPLayerType.ROW_LINEAR, TPLayerType.COLUMN_EMBED):
+                prod = producer.get(a.name)
+                fresh = (a.name not in inputs and readers.get(a.name, 0) == 1 and prod is not None
+                         and not may_alias_bsym(prod))
+                fut = all_reduce.bind(a, DistributedReduceOps.SUM, group, True, fresh,
+                                      output=all_reduce.meta(a, DistributedReduceOps.SUM, group, True, fresh))
+            else:
+                dim = len(a.shape) - 1
+                fut = all_gather.bind(a, group, True, dim, output=all_gather.meta(a, group, True, dim))
+            out.append(fut)
+            out.append(wait.bind(fut.output, output=b.output))
+            n += 1
+    new.bound_symbols = out
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"Lower tensor-parallel syncs ({n} -> async collective + wait)"))
+    return new
+
+
 def _is_collective(b: BoundSymbol) -> bool:
     n = b.sym.name
     return any(x in n for x in ("all_gather", "all_reduce", "reduce_scatter", "broadcast")) and "wait" not in n
@@ -23,6 +84,39 @@ def _is_collective(b: BoundSymbol) -> bool:
 
 def _is_wait(b: BoundSymbol) -> bool:
     return b.sym.name.endswith("wait")
+
+
+def hoist_collective_inputs(bsyms: list) -> list:
+    """Issue every collective as soon as its inputs CAN exist: in the stretch of program since the
+    previous collective, the ops the collective (transitively) depends on move before it, the
+    independent ops after it.  Autodiff emits a linear's dgrad and wgrad together, so a
+    tensor-parallel input-gradient all-reduce (fed by the dgrads of fc_1 and fc_2) would otherwise
+    be issued only after both wgrads, with nothing left to overlap; hoisted, the wgrad GEMMs run
+    while it is in flight (list scheduling alone keeps program order among ready ops)."""
+    coll = [i for i, b in enumerate(bsyms) if _is_collective(b)]
+    if not coll:
+        return bsyms
+    out: list = []
+    prev = 0
+    for c in coll:
+        window = bsyms[prev:c]
+        made = {}
+        for k, b in enumerate(window):
+            for o in b.flat_proxy_outs:
+                made.setdefault(o.name, k)
+        need = {a.name for a in bsyms[c].flat_proxy_args}
+        anc = set()
+        for k in range(len(window) - 1, -1, -1):
+            b = window[k]
+            if any(o.name in need for o in b.flat_proxy_outs):
+                anc.add(k)
+                need.update(a.name for a in b.flat_proxy_args)
+        out.extend(window[k] for k in range(len(window)) if k in anc)
+        out.append(bsyms[c])
+        out.extend(window[k] for k in range(len(window)) if k not in anc)
+        prev = c + 1
+    out.extend(bsyms[prev:])
+    return out
 
 
 def sort_waits(trace: TraceCtx) -> TraceCtx:
@@ -38,6 +132,7 @@ def sort_waits(trace: TraceCtx) -> TraceCtx:
         return trace
     ret = bsyms[-1] if bsyms and bsyms[-1].sym.id == PrimIDs.RETURN else None
     body = bsyms[:-1] if ret is not None else bsyms
+    body = hoist_collective_inputs(body)
     _, _, nodes = bsym_list_to_dag(body)
 
     def rank(n) -> tuple:

@@ -2,8 +2,12 @@
 // loop (csrc/gemm4.hip, variant 1) with parts removed, to price each part of a K-tile on random data.
 //   ABL bit 0: no LDS-DMA in the main loop      bit 1: no fragment ds_reads in the main loop
 //   ABL bit 2: no per-tile wait + barrier        bit 3: no epilogue (accumulators kept live, no stores)
-// Every workgroup's wave 0 stamps s_memtime / s_memrealtime around its whole life into `st`
-// (4 x u64 per workgroup), from which the in-kernel clock is read (MI355X_MICROARCH.md give-back 6).
+//   ABL bit 4: epilogue without the global stores (LDS image written and read back)
+//   ABL bit 5: epilogue without the LDS image (packed accumulators stored straight from registers;
+//              wrong layout, same bytes and store count)
+// Every workgroup's wave 0 stamps s_memtime at start / main-loop start / main-loop end / end and
+// s_memrealtime at start / end into `st` (6 x u64 per workgroup), from which the in-kernel clock and
+// the prologue / main loop / epilogue split are read (MI355X_MICROARCH.md give-back 6).
 #include "common.h"
 
 namespace {
@@ -88,6 +92,8 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
   for (int j = 0; j < NB2; ++j) glds(j, 1, smem + STAGE);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB2) : "memory");
   __builtin_amdgcn_s_barrier();
+  uint64_t tm0 = 0, tm1 = 0;
+  if (wave == 0) tm0 = __builtin_amdgcn_s_memtime();
 #pragma unroll
   for (int r = 0; r < 16; ++r) read_one(smem, 0, r, fa0, fb0);
   if constexpr (!R_ON) {
@@ -138,7 +144,22 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if constexpr (!(ABL & 8)) {
+  if (wave == 0) tm1 = __builtin_amdgcn_s_memtime();
+  if constexpr (ABL & 32) {
+    // same bytes and store count as the real epilogue, no LDS round trip
+#pragma unroll
+    for (int it = 0; it < 32; ++it) {
+      const int m = it >> 2, n0_ = (it & 3) * 2;
+      union { uint4 u; __hip_bfloat16 h[8]; } o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o.h[j] = __float2bfloat16(acc[m][n0_][j]);
+        o.h[4 + j] = __float2bfloat16(acc[m][n0_ + 1][j]);
+      }
+      const int row = it * 4 + (lane >> 4), ch = lane & 15;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * N + n0 + wn * 128 + ch * 8) = o.u;
+    }
+  } else if constexpr (!(ABL & 8)) {
     char* wbuf = smem + wave * (128 * 256);
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
@@ -158,7 +179,11 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
     for (int it = 0; it < 32; ++it) {
       const int id = it * 64 + lane, row = id >> 4, ch = id & 15;
       const uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
-      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * N + n0 + wn * 128 + ch * 8) = v;
+      if constexpr (ABL & 16) {
+        asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+      } else {
+        *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * N + n0 + wn * 128 + ch * 8) = v;
+      }
     }
   } else {
     // keep the accumulators live without storing them
@@ -171,10 +196,12 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
   }
   if (wave == 0 && lane == 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    st[blockIdx.x * 4 + 0] = t0;
-    st[blockIdx.x * 4 + 1] = t1;
-    st[blockIdx.x * 4 + 2] = r0;
-    st[blockIdx.x * 4 + 3] = r1;
+    st[blockIdx.x * 6 + 0] = t0;
+    st[blockIdx.x * 6 + 1] = t1;
+    st[blockIdx.x * 6 + 2] = r0;
+    st[blockIdx.x * 6 + 3] = r1;
+    st[blockIdx.x * 6 + 4] = tm0;
+    st[blockIdx.x * 6 + 5] = tm1;
   }
 }
 }  // namespace
@@ -184,7 +211,7 @@ LTA_EXPORT int anat_gemm(int abl, const void* A, const void* B, void* C, int M, 
   dim3 grid((M / BM) * (N / BN)), block(NTHR);
 #define L(X) case X: hipLaunchKernelGGL(anat_kernel<X>, grid, block, 0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, M, N, K, (uint64_t*)st); break;
   switch (abl) {
-    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(15)
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(15) L(16) L(32) L(17)
     default: return -1;
   }
 #undef L

@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 lib = ctypes.CDLL(os.path.join(HERE, "gemm_anatomy.so"))
 lib.anat_gemm.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
 NAMES = {0: "full", 1: "no_glds", 2: "no_dsread", 3: "no_glds_no_dsread", 4: "no_barrier", 7: "mfma_only",
-         8: "no_epilogue", 15: "mfma_only_no_epi"}
+         8: "no_epilogue", 15: "mfma_only_no_epi", 16: "epi_no_global_store", 32: "epi_regs_store_only",
+         17: "no_glds_epi_no_store"}
 
 
 def run(abl, a, b, c, st, M, N, K):
@@ -25,7 +26,7 @@ def run(abl, a, b, c, st, M, N, K):
 
 def main():
     shapes = [(4096, 12288, 4096), (4096, 4096, 4096)]
-    abls = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,1,2,3,4,7,8,15".split(","))]
+    abls = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,1,2,8,16,32,17".split(","))]
     rounds = int(os.environ.get("ROUNDS", "6"))
     out = {}
     for (M, N, K) in shapes:
@@ -33,7 +34,7 @@ def main():
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         nwg = (M // 256) * (N // 256)
-        st = torch.zeros(nwg * 4, dtype=torch.int64, device="cuda")
+        st = torch.zeros(nwg * 6, dtype=torch.int64, device="cuda")
         run(0, a, b, c, st, M, N, K)
         torch.cuda.synchronize()
         ref = (a.float() @ b.float().t())
@@ -44,7 +45,7 @@ def main():
             for _ in range(20):
                 run(0, a, b, c, st, M, N, K)
             torch.cuda.synchronize()
-        res = {x: {"us": [], "ghz": [], "cyc_per_ktile": []} for x in abls}
+        res = {x: {"us": [], "ghz": [], "cyc_per_ktile": [], "pro": [], "loop": [], "epi": []} for x in abls}
         for r in range(rounds):
             for x in abls:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,8 +58,11 @@ def main():
                 ev1.record()
                 torch.cuda.synchronize()
                 res[x]["us"].append(ev0.elapsed_time(ev1) * 1000 / n)
-                s = st.view(nwg, 4).cpu().double()
+                s = st.view(nwg, 6).cpu().double()
                 dt, dr = s[:, 1] - s[:, 0], s[:, 3] - s[:, 2]
+                res[x]["pro"].append((s[:, 4] - s[:, 0]).median().item())
+                res[x]["loop"].append(((s[:, 5] - s[:, 4]) / (K // 64)).median().item())
+                res[x]["epi"].append((s[:, 1] - s[:, 5]).median().item())
                 ghz = (dt / dr * 0.1).median().item()
                 res[x]["ghz"].append(ghz)
                 res[x]["cyc_per_ktile"].append((dt.median() / (K // 64)).item())
@@ -68,7 +72,10 @@ def main():
             us = statistics.median(res[x]["us"])
             row = {"us_median": round(us, 1), "us_min": round(min(res[x]["us"]), 1),
                    "tflops": round(fl / us / 1e6), "clock_ghz": round(statistics.median(res[x]["ghz"]), 3),
-                   "cycles_per_ktile_per_wg": round(statistics.median(res[x]["cyc_per_ktile"]))}
+                   "cycles_per_ktile_per_wg": round(statistics.median(res[x]["cyc_per_ktile"])),
+                   "prologue_cyc": round(statistics.median(res[x]["pro"])),
+                   "loop_cyc_per_ktile": round(statistics.median(res[x]["loop"])),
+                   "epilogue_cyc": round(statistics.median(res[x]["epi"]))}
             out[f"{M}x{N}x{K}"][NAMES[x]] = row
             print(f"{M}x{N}x{K} {NAMES[x]:>18}: {row}", flush=True)
     print("JSON", json.dumps(out))

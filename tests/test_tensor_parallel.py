@@ -75,8 +75,13 @@ def _worker(rank, port, mode, out_dir):
         res["grad"] = gmax
         tr = thunder.last_traces(tm)[-1]
         res["n_sync"] = sum(1 for b in tr.bound_symbols if "synchronize_tensor_parallel" in b.sym.name)
+        res["fw_ops"] = [b.sym.name for b in tr.bound_symbols]
+        res["fw_collectives"] = [(b.sym.name, b.args[3] if "all_reduce" in b.sym.name else None)
+                                 for b in tr.bound_symbols if b.sym.name in ("dist_all_reduce", "dist_all_gather")]
         bw = thunder.last_backward_traces(tm)[-1]
         res["n_sync_bw"] = sum(1 for b in bw.bound_symbols if "dist_" in b.sym.name)
+        res["bw_ops"] = [b.sym.name for b in bw.bound_symbols]
+        res["bw_trace"] = str(bw)
         torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     finally:
         torch.distributed.barrier()  # peers finish their collectives before gloo tears down
@@ -100,8 +105,33 @@ def test_tensor_parallel_matches_unsharded(mode):
 def test_megatron_mlp_has_single_allreduce_per_row_layer():
     res = _run("megatron")[0]
     # emb all-reduce, one identity sync for the shared fc input, proj all-reduce, head all-gather;
-    # the fc_1/fc_2 all-gathers and the proj slice are removed through the silu(.)*(.) chain
-    assert res["n_sync"] == 4, res
+    # the fc_1/fc_2 all-gathers and the proj slice are removed through the silu(.)*(.) chain.  The
+    # collectives are lowered to async all-reduce / all-gather + wait (lower_tp_syncs); only the
+    # identity input sync stays a sync prim
+    assert res["n_sync"] == 1, res
+    kinds = sorted(n for n, _ in res["fw_collectives"])
+    assert kinds == ["dist_all_gather", "dist_all_reduce", "dist_all_reduce"], res["fw_collectives"]
+    # the all-reduces of fresh GEMM / embedding outputs run in place (skip_clone)
+    assert all(sc for n, sc in res["fw_collectives"] if n == "dist_all_reduce"), res["fw_collectives"]
+    assert res["fw_ops"].count("dist_wait") == 3, res["fw_ops"]
+
+
+_GEMM_NAMES = ("matmul", "linear", "mm", "hip_matmul", "hip_linear")
+
+
+def test_tp_input_grad_allreduce_overlaps_weight_grad_gemms():
+    """Backward of the Megatron MLP: the all-reduce of the column-parallel input gradient is issued
+    right after the dgrad GEMMs that produce it and waited only after the weight-gradient GEMMs of
+    fc_1 / fc_2 (reference: async TP collectives + sort_waits, thunder/distributed/prims.py:433-551,
+    thunder/distributed/utils.py:120-194)."""
+    res = _run("megatron")[0]
+    ops = res["bw_ops"]
+    ars = [i for i, n in enumerate(ops) if n == "dist_all_reduce"]
+    assert ars, res["bw_trace"]
+    i = ars[0]
+    j = next(k for k in range(i + 1, len(ops)) if ops[k] == "dist_wait")
+    between = [n for n in ops[i + 1:j] if any(g == n or n.endswith(g) for g in _GEMM_NAMES)]
+    assert len(between) >= 2, (ops[i:j + 1], res["bw_trace"])  # both fc weight gradients
 
 
 def _litgpt_worker(rank, port, out_dir):
@@ -228,11 +258,10 @@ def _megatron_llama_worker(rank, port, out_dir):
         res["grad"] = gmax
         fw = thunder.last_traces(tm)[-1]
         # claimed by the torch executor as dist_<prim>: match by name
-        tp_out = [b for b in fw.bound_symbols if b.sym.name.endswith("synchronize_tensor_parallel_output")]
-        res["row_allreduce"] = sum(1 for b in tp_out if b.args[2] is dist_prims.TPLayerType.ROW_LINEAR)
-        res["gathers"] = sum(1 for b in tp_out if b.args[2] in (dist_prims.TPLayerType.COLUMN_LINEAR,
-                                                                dist_prims.TPLayerType.ROW_EMBED))
-        res["embed_allreduce"] = sum(1 for b in tp_out if b.args[2] is dist_prims.TPLayerType.COLUMN_EMBED)
+        # the TP output syncs are lowered to async collectives + waits (distributed/utils.py lower_tp_syncs)
+        res["tp_syncs_left"] = sum(1 for b in fw.bound_symbols if b.sym.name.endswith("synchronize_tensor_parallel_output"))
+        res["allreduce"] = sum(1 for b in fw.bound_symbols if b.sym.name == "dist_all_reduce")
+        res["gathers"] = sum(1 for b in fw.bound_symbols if b.sym.name == "dist_all_gather")
         res["vocab_ce"] = sum(1 for b in fw.bound_symbols if b.sym.name.endswith("vocab_parallel_cross_entropy_fwd"))
         res["sdpa_heads"] = [tuple(b.args[0].shape) for b in fw.bound_symbols
                              if "scaled_dot_product" in b.sym.name or "flash" in b.sym.name][:1]
@@ -253,9 +282,10 @@ def test_megatron_llama_head_parallel_vocab_parallel():
         for r in range(WORLD):
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             assert res["loss"] < 1e-10 and res["grad"] < 1e-8, res
-            assert res["row_allreduce"] == 2 * res["n_layer"], res
+            # one all-reduce per attention block and per MLP, plus the vocab-parallel embedding's
+            assert res["allreduce"] == 2 * res["n_layer"] + 1 and res["tp_syncs_left"] == 0, res
             assert res["gathers"] == 0, res
-            assert res["embed_allreduce"] == 1 and res["vocab_ce"] == 1, res
+            assert res["vocab_ce"] == 1, res
             if res["sdpa_heads"]:
                 assert res["sdpa_heads"][0][1] == 4 // WORLD, res  # local query heads
 
