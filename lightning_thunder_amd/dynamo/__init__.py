@@ -47,6 +47,7 @@ class SubgraphInfo:
     thunder_compiled_fns: list
     submodule_to_compiled_functions: dict
     split_reasons: list
+    original_split_modules: dict = None  # split module name -> the GraphModule before jit (graph benchmarking)
 
 
 _ALWAYS_EAGER = {
@@ -264,6 +265,7 @@ class ThunderCompiler:
             _convert_checkpoints(gm, part)
         compiled = []
         mapping = {}
+        originals = {}
         if all(ok for _, ok in part.values()):
             fn = jit(gm, **self._options(gm))
             compiled.append(fn)
@@ -277,12 +279,13 @@ class ThunderCompiler:
             sub = getattr(split_gm, n.target)
             supported = any(ok for (i, ok) in part.values() if i == idx)
             if supported:
+                originals[n.target] = sub
                 fn = jit(sub, **self._options(gm))
                 setattr(split_gm, n.target, fn)
                 compiled.append(fn)
                 mapping[n.target] = fn
         split_gm.recompile()
-        self.subgraph_infos.append(SubgraphInfo(gm, split_gm, compiled, mapping, reasons))
+        self.subgraph_infos.append(SubgraphInfo(gm, split_gm, compiled, mapping, reasons, originals))
         return split_gm
 
 

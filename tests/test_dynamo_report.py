@@ -112,3 +112,36 @@ def test_fusion_repro_runs_standalone_gpu(tmp_path):
     assert "GB/s" in r.stdout
     rows = thunderfx_benchmark_report(_fusing_fn, x, w, folder=str(tmp_path / "bench"))
     assert rows and all("fusion_ms" in row and row["fusion_gbps"] > 0 for row in rows), rows
+
+
+def test_compiler_graph_benchmarking_times_every_split_under_every_executor():
+    """Reference thunder/dynamo/compiler_graph_benchmark.py: each Thunder split module of each dynamo
+    graph is timed under every executor (built-in timer here: pytest-benchmark is not in the image)."""
+    import torch._dynamo
+
+    from lightning_thunder_amd import jit
+    from lightning_thunder_amd.dynamo.compiler_graph_benchmark import ThunderCompilerGraphBenchmarking
+
+    def func(x):
+        x = torch.sin(x)
+        if x.sum() > 0:  # graph break: two dynamo graphs
+            return torch.cos(x) + 1
+        return x - 1
+
+    torch._dynamo.reset()
+    backend = ThunderCompilerGraphBenchmarking(executors={"eager": None, "thunder": jit}, warmup=1, iters=3)
+    compiled = torch.compile(func, backend=backend, dynamic=False)
+    x = torch.ones(64, 32, requires_grad=True)
+    out = compiled(x)
+    torch.testing.assert_close(out, func(x))
+    assert backend.graph_idx >= 2
+    names = {(r["GraphID"], r["SplitModuleName"], r["executor"]) for r in backend.results}
+    for g in range(backend.graph_idx):
+        assert any(k[0] == g and k[2] == "eager" for k in names), names
+        assert any(k[0] == g and k[2] == "thunder" for k in names), names
+    assert all(r["median_ms"] > 0 for r in backend.results)
+    rep = backend.report()
+    assert "GraphID[0]" in rep and "thunder" in rep, rep
+    with pytest.raises(ValueError):
+        ThunderCompilerGraphBenchmarking(executors={"bad-name": None})
+    torch._dynamo.reset()
