@@ -48,9 +48,10 @@ SUPPORTED_HEAD_DIMS = (64, 96, 128, 256)  # the kernels' compile-time head dims
 # Q K^T unchanged, zero columns of V give zero columns of O (sliced off), the scale stays the
 # caller's (1 / sqrt(D) of the real D), and the padded gradient columns are exactly zero.
 # D = 256 (Gemma; cuDNN's limit, thunder/executors/cudnn_sdpa.py:339-363) runs 32-key tiles at one
-# workgroup per CU with the accumulators in the AGPR file, without masks or dropout.
+# workgroup per CU with the accumulators in the AGPR file; additive / boolean masks and dropout are
+# compiled into those kernels as for the smaller head dims (no spills: 248-256 VGPRs + AGPRs).
 MAX_PADDED_HEAD_DIM = 256
-PLAIN_ONLY_HEAD_DIM = 128  # above this head dim the kernels take no additive mask / dropout
+PLAIN_ONLY_HEAD_DIM = 256  # above this head dim the kernels would take no additive mask / dropout
 
 
 def padded_head_dim(D: int) -> int | None:

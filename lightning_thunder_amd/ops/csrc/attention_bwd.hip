@@ -1253,9 +1253,6 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   hipLaunchKernelGGL((attn_bwd_preprocess<T, D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
   if (exf) {  // masks / dropout: the plain-HIP kernels with the extra terms compiled in
-    if constexpr (D > 128) {
-      return -1;  // D = 256: plain (causal / full) attention only
-    } else {
     switch (exf) {
 #define LTA_M(F)                                                                                                  \
   case F:                                                                                                         \
@@ -1271,7 +1268,6 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
         return -1;
     }
     return (int)hipGetLastError();
-    }
   }
   dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM);
 #define LTA_V1(CA)                                                                                                   \

@@ -327,14 +327,12 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
     if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 96) return launch<__hip_bfloat16, 96>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
-    if (D == 256 && exf == 0)  // D = 256: plain (causal / full) attention only
-      return launch_ex<__hip_bfloat16, 256, 0>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, stream);
+    if (D == 256) return launch<__hip_bfloat16, 256>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
   } else if (dtype == kF16) {
     if (D == 128) return launch<__half, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 64) return launch<__half, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 96) return launch<__half, 96>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
-    if (D == 256 && exf == 0)
-      return launch_ex<__half, 256, 0>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, stream);
+    if (D == 256) return launch<__half, 256>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
   }
   return -1;
 }

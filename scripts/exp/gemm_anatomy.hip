@@ -5,6 +5,9 @@
 //   ABL bit 4: epilogue without the global stores (LDS image written and read back)
 //   ABL bit 5: epilogue without the LDS image (packed accumulators stored straight from registers;
 //              wrong layout, same bytes and store count)
+//   ABL bit 6: operands swapped in the MFMA (each lane accumulates 4 consecutive COLUMNS of a C row),
+//              epilogue in registers: cvt_pk + v_permlane16_swap give every lane 16 contiguous bytes
+//              of one row, one dwordx4 store per pair of 16x16 blocks, no LDS (correct layout)
 // Every workgroup's wave 0 stamps s_memtime at start / main-loop start / main-loop end / end and
 // s_memrealtime at start / end into `st` (6 x u64 per workgroup), from which the in-kernel clock and
 // the prologue / main loop / epilogue split are read (MI355X_MICROARCH.md give-back 6).
@@ -49,6 +52,16 @@ __device__ __forceinline__ bf16x8 read_frag(const char* img, int rc, int kk, int
 __device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
+template <bool SW>
+__device__ __forceinline__ void mma(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  if constexpr (SW) mfma16(acc, b, a); else mfma16(acc, a, b);
+}
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  union { __hip_bfloat16 h[2]; uint32_t u; } p;
+  p.h[0] = __float2bfloat16(lo);
+  p.h[1] = __float2bfloat16(hi);
+  return p.u;
+}
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
 template <int ABL>
@@ -84,7 +97,7 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
     else fa[r - 8] = read_frag(stage, wm * 128 + (r - 8) * 16, kk, fr, fq);
   };
   constexpr int NB2 = 8, NA = 8;
-  constexpr bool G_ON = !(ABL & 1), R_ON = !(ABL & 2), B_ON = !(ABL & 4);
+  constexpr bool G_ON = !(ABL & 1), R_ON = !(ABL & 2), B_ON = !(ABL & 4), SW = ABL & 64;
   const int nk = K / BK;
 #pragma unroll
   for (int j = 0; j < 16; ++j) glds(j, 0, smem);
@@ -107,14 +120,14 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
     const int t1 = min(t + 1, nk - 1), t2 = min(t + 2, nk - 1);
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
-      mfma16(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
+      mma<SW>(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
       if (R_ON && (i & 3) == 0) read_one(bc, 1, i >> 2, fa1, fb1);
       if (G_ON && (i & 3) == 2 && (i >> 2) < NA) glds(NB2 + (i >> 2), t1, bn);
       FENCE();
     }
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      mma<SW>(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
       FENCE();
     }
     if constexpr (B_ON) {
@@ -126,7 +139,7 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
     FENCE();
 #pragma unroll
     for (int i = 32; i < 64; ++i) {
-      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      mma<SW>(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
       const int s = i - 32;
       if (R_ON && (s & 1) == 0) read_one(bn, 0, s >> 1, fa0, fb0);
       else if (G_ON && (s & 3) == 1 && (s >> 2) < NB2) glds(s >> 2, t2, bc);
@@ -145,7 +158,25 @@ __global__ __launch_bounds__(NTHR, 1) void anat_kernel(const __hip_bfloat16* __r
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wave == 0) tm1 = __builtin_amdgcn_s_memtime();
-  if constexpr (ABL & 32) {
+  if constexpr (SW) {
+    // lane (fq, fr) holds C[m*16 + fr][n*16 + 4 fq + j]; blocks n, n+1 -> permlane16_swap -> 16 B per lane
+    const int rsel = fq & 1, csel = fq >> 1;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int np = 0; np < 4; ++np) {
+        const int n = 2 * np;
+        uint32_t x0 = pk2(acc[m][n][0], acc[m][n][1]), x1 = pk2(acc[m][n][2], acc[m][n][3]);
+        uint32_t y0 = pk2(acc[m][n + 1][0], acc[m][n + 1][1]), y1 = pk2(acc[m][n + 1][2], acc[m][n + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        const int row = m0 + wm * 128 + m * 16 + fr, col = n0 + wn * 128 + (n + rsel) * 16 + csel * 8;
+        *reinterpret_cast<uint4*>(C + (int64_t)row * N + col) = v;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else if constexpr (ABL & 32) {
     // same bytes and store count as the real epilogue, no LDS round trip
 #pragma unroll
     for (int it = 0; it < 32; ++it) {
@@ -211,7 +242,7 @@ LTA_EXPORT int anat_gemm(int abl, const void* A, const void* B, void* C, int M, 
   dim3 grid((M / BM) * (N / BN)), block(NTHR);
 #define L(X) case X: hipLaunchKernelGGL(anat_kernel<X>, grid, block, 0, s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, M, N, K, (uint64_t*)st); break;
   switch (abl) {
-    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(15) L(16) L(32) L(17)
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(15) L(16) L(32) L(17) L(64)
     default: return -1;
   }
 #undef L

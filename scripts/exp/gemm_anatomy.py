@@ -15,7 +15,7 @@ lib = ctypes.CDLL(os.path.join(HERE, "gemm_anatomy.so"))
 lib.anat_gemm.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
 NAMES = {0: "full", 1: "no_glds", 2: "no_dsread", 3: "no_glds_no_dsread", 4: "no_barrier", 7: "mfma_only",
          8: "no_epilogue", 15: "mfma_only_no_epi", 16: "epi_no_global_store", 32: "epi_regs_store_only",
-         17: "no_glds_epi_no_store"}
+         17: "no_glds_epi_no_store", 64: "swapped_regs_epilogue"}
 
 
 def run(abl, a, b, c, st, M, N, K):
@@ -26,7 +26,7 @@ def run(abl, a, b, c, st, M, N, K):
 
 def main():
     shapes = [(4096, 12288, 4096), (4096, 4096, 4096)]
-    abls = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,1,2,8,16,32,17".split(","))]
+    abls = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,64,8,16".split(","))]
     rounds = int(os.environ.get("ROUNDS", "6"))
     out = {}
     for (M, N, K) in shapes:
@@ -35,11 +35,16 @@ def main():
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         nwg = (M // 256) * (N // 256)
         st = torch.zeros(nwg * 6, dtype=torch.int64, device="cuda")
-        run(0, a, b, c, st, M, N, K)
-        torch.cuda.synchronize()
         ref = (a.float() @ b.float().t())
-        err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
-        print(f"{M}x{N}x{K} full-kernel rel err {err:.2e}", flush=True)
+        for x in (0, 64):
+            if x not in abls:
+                continue
+            c.zero_()
+            run(x, a, b, c, st, M, N, K)
+            torch.cuda.synchronize()
+            err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+            print(f"{M}x{N}x{K} {NAMES[x]} rel err {err:.2e}", flush=True)
+            assert err < 1e-2, (x, err)
         t_end = time.time() + 2.0
         while time.time() < t_end:
             for _ in range(20):

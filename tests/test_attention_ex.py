@@ -74,7 +74,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("kind", ["bool_padding", "float_bias", "bool_full"])
-@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("D", [64, 96, 128, 192, 256])  # 192 runs zero-padded to the D = 256 kernels
 def test_masked_attention_fwd_bwd(kind, D):
     from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
 
@@ -115,10 +115,11 @@ def test_mask_gradient():
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_dropout_matches_regenerated_mask(causal):
+@pytest.mark.parametrize("D", [128, 192, 256])
+def test_dropout_matches_regenerated_mask(causal, D):
     from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd
 
-    B, Hq, Hkv, T, S, D, p = 1, 4, 2, 256, 256, 128, 0.2
+    B, Hq, Hkv, T, S, p = 1, 4, 2, 256, 256, 0.2
     seed, offset = 1234567890123, 4096
     q, k, v = _qkv(B, Hq, Hkv, T, S, D)
     o, lse = attn_fwd(q, k, v, causal, dropout_p=p, seed=seed, offset=offset, out_layout="bhsd")
@@ -168,8 +169,9 @@ def test_sdpa_with_mask_and_dropout_claimed_by_hipex():
 
 
 def test_sdpa_head_dim_256_claimed_by_hipex():
-    """Gemma's head dim: plain causal SDPA at D=256 runs on the hand kernels (forward and backward),
-    matching fp32; with an additive mask it is declined (the D=256 kernels take no mask / dropout)."""
+    """Gemma's head dim: causal SDPA at D=256 runs on the hand kernels (forward and backward),
+    matching fp32, and so does SDPA with an additive mask (cuDNN takes masks up to D = 256,
+    thunder/executors/cudnn_sdpa.py:339-363)."""
     import lightning_thunder_amd as thunder
 
     B, Hq, Hkv, T, D = 1, 4, 2, 192, 256
@@ -191,11 +193,20 @@ def test_sdpa_head_dim_256_claimed_by_hipex():
     assert "hip_flash_attn_fwd" in str(thunder.last_traces(jf)[-1])
     assert "hip_flash_attn_bwd" in str(thunder.last_backward_traces(jf)[-1])
 
-    mask = torch.zeros(T, T, device="cuda", dtype=torch.bfloat16)
+    mask = (torch.randn(T, T, device="cuda") * 2.0).to(torch.bfloat16)
 
     def g(q, k, v):
         return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
 
+    qs, ks, vs = (t.detach().requires_grad_(True) for t in (q, k, v))
     jg = thunder.jit(g)
-    jg(q.detach(), k.detach(), v.detach())
-    assert "hip_flash_attn" not in str(thunder.last_traces(jg)[-1])
+    out = jg(qs, ks, vs)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = ref_attn(qr, kr, vr, mask=mask.float())
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    out.backward(do)
+    ref.backward(do.float())
+    for got, want in ((qs.grad, qr.grad), (ks.grad, kr.grad), (vs.grad, vr.grad)):
+        assert _rel(got, want) < 2e-2, _rel(got, want)
+    assert "hip_flash_attn_fwd_ex" in str(thunder.last_traces(jg)[-1])
+    assert "hip_flash_attn_bwd_ex" in str(thunder.last_backward_traces(jg)[-1])
