@@ -106,6 +106,14 @@ def make_optimizer(params, mode="eager"):
         return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, foreach=True)
 
 
+def _rccl_record(world):
+    if world == 1 and not _force_dist():
+        return None
+    from lightning_thunder_amd.distributed import rccl_policy
+
+    return {k: v for k, v in rccl_policy.describe().items() if v is not None}
+
+
 def _force_dist() -> bool:
     return os.environ.get("LTA_BENCH_FORCE_DIST") == "1"
 
@@ -261,9 +269,14 @@ def main():
         from datetime import timedelta
 
         # as the reference's benchmark_litgpt.py:64-69: no record_stream allocator thrash, async
-        # error handling, and a bounded rendezvous / collective timeout instead of an endless hang
-        os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+        # error handling, and a bounded rendezvous / collective timeout instead of an endless hang;
+        # the RCCL policy (distributed/rccl_policy.py) is applied before the communicator exists
+        from lightning_thunder_amd.distributed import rccl_policy
+
+        rccl_policy.apply()
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        if rank == 0:
+            print(f"[rccl] policy {rccl_policy.describe()}", file=sys.stderr, flush=True)
         timeout = timedelta(minutes=int(os.environ.get("LTA_DIST_TIMEOUT_MIN", "10")))
         if backend == "nccl":
             # a high-priority RCCL stream gets a hardware queue of its own: on the normal-priority
@@ -326,6 +339,7 @@ def main():
             "model_tflops_per_gpu": round(tflops, 1),
             "peak_mem_gb": round(mem, 2),
             "speedup_vs_eager": None if speedup is None else round(speedup, 3),
+            "rccl": _rccl_record(world),
             "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 3),
         }
         print(json.dumps(out), flush=True)

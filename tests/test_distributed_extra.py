@@ -228,3 +228,22 @@ def test_zero3_block_bucketing_window_order():
     torch.testing.assert_close(out1, out0)
     for n in g0:
         torch.testing.assert_close(g1[n], g0[n])
+
+
+def test_rccl_policy_defaults_and_presets():
+    from lightning_thunder_amd.distributed import rccl_policy
+
+    env = {}
+    assert rccl_policy.apply(env) == {"TORCH_NCCL_AVOID_RECORD_STREAMS": "1"}
+    assert "NCCL_MIN_NCHANNELS" not in env  # RCCL's own channel tuning by default (CUs stay with the GEMMs)
+    env = {"LTA_RCCL_POLICY": "wide", "NCCL_MIN_NCHANNELS": "8"}
+    rccl_policy.apply(env)
+    assert env["NCCL_MIN_NCHANNELS"] == "8"  # an explicit setting wins
+    env = {"LTA_RCCL_POLICY": "ring"}
+    rccl_policy.apply(env)
+    assert env["NCCL_ALGO"] == "Ring"
+    assert rccl_policy.apply({"LTA_RCCL_POLICY": "off"}) == {}
+    d = rccl_policy.describe({"LTA_RCCL_POLICY": "wide", "NCCL_MIN_NCHANNELS": "32"})
+    assert d["LTA_RCCL_POLICY"] == "wide" and d["NCCL_MIN_NCHANNELS"] == "32"
+    with pytest.raises(ValueError):
+        rccl_policy.apply({"LTA_RCCL_POLICY": "bogus"})
