@@ -81,6 +81,13 @@ __device__ __forceinline__ void mfma8(f32x4& acc, const v8i& a, const v8i& b) {
 
 #define LTA_FENCE() __builtin_amdgcn_sched_barrier(0)
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// two f32 -> one packed bf16 pair on ONE v_cvt_pk_bf16_f32 (round to nearest even, as __float2bfloat16)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
+}
+
 // RES: C = bf16(bf16(A.B^T / (sa sb) + bias) + R) — the residual add of the unfused pair, with the
 // same two rounding points (the FP8 transformer block's residual stream and the dgrad sum of the
 // gate / up projections never take a separate elementwise pass).
@@ -153,7 +160,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
       const int m = i >> 3, n = i & 7;
-      mfma8<FA, FB>(acc[m][n], fa[m], fb[n]);
+      // operands swapped (the B fragment and its format first): the accumulator holds the transposed
+      // 16 x 16 block, 4 consecutive C columns of one row per lane (register epilogue below)
+      mfma8<FB, FA>(acc[m][n], fb[n], fa[m]);
       if (i < 32 && (i & 1) == 0) glds(i >> 1, t2, bc);
       if (m >= 1 && n == 0) fa[m - 1] = read_frag8(bn, arow + (m - 1) * 16, fg);
       if (m == 7) fb[n] = read_frag8(bn + OP_BYTES, brow + n * 16, fg);
@@ -175,46 +184,54 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  // ---- epilogue: alpha = 1 / (sa * sb), + bias, -> swizzled bf16 image per wave -> 16-B stores ----
+  // ---- register epilogue (as csrc/gemm4.hip): alpha = 1 / (sa * sb), + bias, bf16; blocks n, n + 1
+  // through v_permlane16_swap -> 16 B of one row per lane -> (+ residual) -> store.  No LDS image.
   const float alpha = 1.f / (*sa * *sb);
-  char* wbuf = smem + wave * (128 * 256);
+  const int rsel = fg & 1, csel = fg >> 1;
+  float bv[8][4];
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
-    const int col = n * 16 + fr;
-    float bv = 0.f;
-    if constexpr (BIAS) bv = to_f32(bias[n0 + wn * 128 + col]);
-    const int ch = col >> 3, co = (col & 7) * 2;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    for (int j = 0; j < 4; ++j) bv[n][j] = 0.f;
+    if constexpr (BIAS) {
+      const uint2 u = *reinterpret_cast<const uint2*>(bias + n0 + wn * 128 + n * 16 + fg * 4);
+      const __hip_bfloat16* h = reinterpret_cast<const __hip_bfloat16*>(&u);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = m * 16 + fg * 4 + j;
-        *reinterpret_cast<__hip_bfloat16*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4) + co) =
-            __float2bfloat16(acc[m][n][j] * alpha + bv);
-      }
+      for (int j = 0; j < 4; ++j) bv[n][j] = to_f32(h[j]);
     }
-    __builtin_amdgcn_sched_barrier(0);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int it = 0; it < 32; ++it) {
-    const int id = it * 64 + lane;
-    const int row = id >> 4, ch = id & 15;
-    uint4 v = *reinterpret_cast<const uint4*>(wbuf + row * 256 + ((ch ^ (row & 15)) << 4));
-    if constexpr (RES) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(R + (int64_t)(m0 + wm * 128 + row) * ldr + n0 + wn * 128 + ch * 8);
-      const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&v);
-      const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
-      union {
-        uint4 u;
-        __hip_bfloat16 h[8];
-      } o;
+  for (int m = 0; m < 8; ++m) {
+    const int64_t grow = m0 + wm * 128 + m * 16 + fr;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
-      v = o.u;
+    for (int np = 0; np < 4; ++np) {
+      const int n = 2 * np;
+      float v[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[h][j] = acc[m][n + h][j] * alpha + bv[n + h][j];
+      const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[1][0], v[1][1]),
+                                                       false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v[0][2], v[0][3]), pack_bf16x2(v[1][2], v[1][3]),
+                                                       false, false);
+      uint4 val = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      const int gcol = n0 + wn * 128 + (n + rsel) * 16 + csel * 8;
+      if constexpr (RES) {
+        const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
+        const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&val);
+        const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
+        union {
+          uint4 u;
+          __hip_bfloat16 h[8];
+        } o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
+        val = o.u;
+      }
+      *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = val;
+      __builtin_amdgcn_sched_barrier(0);  // one block pair at a time: bounded VGPR use
     }
-    *reinterpret_cast<uint4*>(C + (int64_t)(m0 + wm * 128 + row) * ldc + n0 + wn * 128 + ch * 8) = v;
   }
 }
 

@@ -1,3 +1,4 @@
+// Reference copy of csrc/gemm4.hip before the swapped-operand register epilogue (A/B builds only).
 // K2 (v2): bf16 GEMM on CDNA4 MFMA, one 256x256 output tile per 4-wave workgroup.
 //
 //   C[M,N] = act(alpha * A . B + bias[col]) (+ R)        (reference: cuBLAS(Lt) behind ATen linear /
@@ -228,26 +229,6 @@ __device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& a, const bf16x8
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
 
-__device__ __forceinline__ float bf16_round(float x) { return __bfloat162float(__float2bfloat16(x)); }
-
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-// two f32 -> one packed bf16 pair on ONE v_cvt_pk_bf16_f32 (round to nearest even, as __float2bfloat16)
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
-}
-
-// Register epilogue of the swapped layout (see the kernel): lane (fq, fr) holds 4 consecutive columns
-// 4 fq .. 4 fq + 3 of row fr in every 16 x 16 block.  Blocks n and n + 1 of one row block, packed to
-// bf16 (x = block n, y = block n + 1, 2 dwords each), go through v_permlane16_swap: afterwards every
-// lane holds 8 consecutive columns (16 B) of ONE row - lanes with fq even block n, fq odd block
-// n + 1; fq < 2 columns 0..7, fq >= 2 columns 8..15 of their block (cdna_hip_programming.md T21).
-__device__ __forceinline__ uint4 swap_pair(uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1) {
-  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-  return make_uint4(s0[0], s1[0], s0[1], s1[1]);
-}
-
 // Extra operands of the fused epilogues.
 struct EpiArgs {
   const __hip_bfloat16* B2;  // EPI 1: W2
@@ -306,12 +287,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   static_assert(GRP == 0 || (EPI == 0 && !BIAS && !RES && ACT == 0), "grouped: plain products");
   static_assert(GRP != 1 || !AT, "grouped rows: A row-major");
   static_assert(GRP != 2 || (AT && BT), "grouped reduction: A and B stored [rows][.]");
-  // SW: MFMA operands swapped (D = B-fragment x A-fragment^T, the TRANSPOSED 16 x 16 block), so each
-  // lane accumulates 4 consecutive COLUMNS of one C row and the epilogue is register-only (cvt_pk +
-  // permlane16_swap -> 16-B row stores), no LDS image: the image's 256 ds_write_b16 per lane cost
-  // ~8.4k of a tile's ~12k epilogue cycles (profiles/gemm4_epilogue_anatomy.txt).  The gate-up / swiglu
-  // epilogues (EPI 1 / 2), which exchange data between waves through LDS, keep the direct layout.
-  constexpr bool SW = EPI == 0 || EPI == 3;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];  // the ONLY LDS object (rule 4a)
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -400,9 +375,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-  auto mma = [](f32x4& c, const bf16x8& a, const bf16x8& b) {
-    if constexpr (SW) mfma16(c, b, a); else mfma16(c, a, b);
-  };
   // fragment read r (0..15) of one k-step, in the order the MFMAs consume them: A0, B0..B7, A1..A7
   auto read_one = [&](const char* stage, int kk, int r, bf16x8* fa, bf16x8* fb) {
     if (r == 0)
@@ -443,7 +415,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     // phase A: k-step 0 of tile t from (fa0, fb0); read k-step 1; finish tile t+1's staging
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
-      mma(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
+      mfma16(acc[i >> 3][i & 7], fa0[i >> 3], fb0[i & 7]);
       if ((i & 3) == 0) read_one(bc, 1, i >> 2, fa1, fb1);
       if (NA > 0 && (i & 3) == 2 && (i >> 2) < NA) glds(NB2 + (i >> 2), t1, bn);
       LTA_FENCE();
@@ -451,7 +423,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     // phase B1: rows 0..3 of k-step 1
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-      mma(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
       LTA_FENCE();
     }
     // tile t+1 has landed for this wave and tile t is fully read by it; then for everyone
@@ -461,7 +433,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     // phase B2: rows 4..7 of k-step 1; read k-step 0 of tile t+1; stage tile t+2 into this buffer
 #pragma unroll
     for (int i = 32; i < 64; ++i) {
-      mma(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
+      mfma16(acc[i >> 3][i & 7], fa1[i >> 3], fb1[i & 7]);
       const int s = i - 32;
       if ((s & 1) == 0)
         read_one(bn, 0, s >> 1, fa0, fb0);
@@ -488,143 +460,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   __builtin_amdgcn_s_barrier();
 
   if constexpr (TAIL == 2) {  // tail split: the fp32 partial of this K half (summed by gemm4_tail_fixup)
-    static_assert(SW, "tail split: swapped layout");
     float* P = ep.partial + ((int64_t)((int)blockIdx.x & 1) * ep.tile_count + (wg_lin - ep.tile_base)) * (BM * BN);
 #pragma unroll
     for (int m = 0; m < 8; ++m)
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
-        // 4 consecutive fp32 columns of one row per lane: one 16-B store
-        *reinterpret_cast<f32x4*>(P + (wm * 128 + m * 16 + fr) * BN + wn * 128 + n * 16 + fq * 4) = acc[m][n];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) P[(wm * 128 + m * 16 + fq * 4 + j) * BN + wn * 128 + n * 16 + fr] = acc[m][n][j];
         __builtin_amdgcn_sched_barrier(0);  // one accumulator block at a time: bounded VGPR use
       }
     return;
   }
-  if constexpr (SW) {
-    const int rsel = fq & 1, csel = fq >> 1;
-    if constexpr (EPI == 3) {
-      // this wave's 128 columns are one head: q head cb, k head cb - nh or v head cb - nh - ng.  A
-      // dimension d < 64 (block n < 4) and its rotate-half partner d + 64 (block n + 4) sit in the same
-      // lane and register; both use cos / sin of d (rotate-half duplicates them), applied to the
-      // bf16-rounded projection as csrc/rope.hip does
-      const int cb = (n0 + wn * 128) >> 7;
-      const bool is_q = cb < ep.nh, is_k = !is_q && cb < ep.nh + ep.ng;
-      __hip_bfloat16* const dst = is_q ? C : (is_k ? C2 : C3);
-      const int hh = is_q ? cb : (is_k ? cb - ep.nh : cb - ep.nh - ep.ng);
-      const int nheads = is_q ? ep.nh : ep.ng;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int grow = m0 + wm * 128 + m * 16 + fr;
-        const int gr = min(grow, M - 1);
-        const int bi = gr / ep.T, t = gr - bi * ep.T;
-        __hip_bfloat16* const orow = dst + (((int64_t)bi * nheads + hh) * ep.T + t) * 128;
-        uint32_t lo[4][2], hi[4][2];  // blocks n (dims < 64) and n + 4 (partners), packed
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          float x1[4], x2[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            x1[j] = bf16_round(acc[m][n][j]);
-            x2[j] = bf16_round(acc[m][n + 4][j]);
-          }
-          if (is_q || is_k) {
-            const float4 c = *reinterpret_cast<const float4*>(ep.cos_ + (int64_t)t * 128 + n * 16 + fq * 4);
-            const float4 sn = *reinterpret_cast<const float4*>(ep.sin_ + (int64_t)t * 128 + n * 16 + fq * 4);
-            const float cs[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float a = x1[j], b = x2[j];
-              x1[j] = a * cs[j] - b * ss[j];
-              x2[j] = b * cs[j] + a * ss[j];
-            }
-          }
-          lo[n][0] = pack_bf16x2(x1[0], x1[1]);
-          lo[n][1] = pack_bf16x2(x1[2], x1[3]);
-          hi[n][0] = pack_bf16x2(x2[0], x2[1]);
-          hi[n][1] = pack_bf16x2(x2[2], x2[3]);
-        }
-#pragma unroll
-        for (int np = 0; np < 2; ++np) {
-          const int n = 2 * np;
-          const uint4 vlo = swap_pair(lo[n][0], lo[n][1], lo[n + 1][0], lo[n + 1][1]);
-          const uint4 vhi = swap_pair(hi[n][0], hi[n][1], hi[n + 1][0], hi[n + 1][1]);
-          if (grow < M) {
-            const int col = (n + rsel) * 16 + csel * 8;
-            *reinterpret_cast<uint4*>(orow + col) = vlo;
-            *reinterpret_cast<uint4*>(orow + col + 64) = vhi;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded VGPR use
-      }
-      return;
-    } else {
-      // plain / bias / activation / residual (GRP 0, 1, 2)
-      float bv[8][4];
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bv[n][j] = 0.f;
-      if constexpr (BIAS) {
-#pragma unroll
-        for (int n = 0; n < 8; ++n) {
-          const int c0 = n0 + wn * 128 + n * 16 + fq * 4;  // N % 8 == 0: the 4 columns are all in or all out
-          if (c0 < N) {
-            const uint2 u = *reinterpret_cast<const uint2*>(bias + c0);
-            const __hip_bfloat16* h = reinterpret_cast<const __hip_bfloat16*>(&u);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[n][j] = to_f32(h[j]);
-          }
-        }
-      }
-      auto store_all = [&](auto scaled_c) {
-        constexpr bool SCALED = decltype(scaled_c)::value;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int64_t grow = m0 + wm * 128 + m * 16 + fr;
-#pragma unroll
-        for (int np = 0; np < 4; ++np) {
-          const int n = 2 * np;
-          float v[2][4];
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float x = acc[m][n + h][j];
-              if constexpr (SCALED) x *= alpha;
-              if constexpr (BIAS) x += bv[n + h][j];
-              v[h][j] = act_fn<ACT>(x);
-            }
-          uint4 val = swap_pair(pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]),
-                                pack_bf16x2(v[1][0], v[1][1]), pack_bf16x2(v[1][2], v[1][3]));
-          const int gcol = n0 + wn * 128 + (n + rsel) * 16 + csel * 8;
-          if (grow < Mlim && gcol < N) {  // edge tile (or group end): N % 8 == 0, a chunk is all in or out
-            if constexpr (RES) {
-              // y (rounded to bf16, as ATen's linear stores it) + r, rounded once more
-              const uint4 rv = *reinterpret_cast<const uint4*>(R + grow * ldr + gcol);
-              const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&val);
-              const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&rv);
-              union {
-                uint4 u;
-                __hip_bfloat16 h[8];
-              } o;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(__bfloat162float(a[e]) + __bfloat162float(b[e]));
-              val = o.u;
-            }
-            *reinterpret_cast<uint4*>(Cg + grow * ldc + gcol) = val;
-          }
-          __builtin_amdgcn_sched_barrier(0);  // one block pair at a time: bounded VGPR use
-        }
-      }
-      };
-      // alpha == 1 (every training GEMM) skips the 256 multiplies per lane
-      if (alpha == 1.f)
-        store_all(std::false_type{});
-      else
-        store_all(std::true_type{});
-      return;
-    }
-  } else {
   // ---- epilogue: every wave has passed the last barrier after its final LDS read, so the stage
   // buffers are free: registers -> swizzled bf16 image (per wave 128 x 128, 256-B rows) -> stores
   char* wbuf = smem + wave * (128 * 256);
@@ -779,7 +625,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     }
     *reinterpret_cast<uint4*>(Cg + grow * ldc + gcol) = v;
   }
-  }  // !SW
 }
 
 #undef LTA_FENCE
