@@ -107,7 +107,8 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
 
 template <bool MN, bool DUAL = false, bool KEDGE = false>
 struct Stager {
-  i32x4 rsrc, rsrc2;     // DUAL (K-major only): rows 0..127 from rsrc, rows 128..255 from rsrc2
+  i32x4 rsrc, rsrc2;     // DUAL (K-major only): tile rows alternate in 64-row groups between rsrc and rsrc2
+                         // (rows 0-63: rsrc 0-63, 64-127: rsrc2 0-63, 128-191: rsrc 64-127, 192-255: rsrc2 64-127)
   // KEDGE (MN-major, grouped wgrad): the reduction length `kred` need not divide the K-tile.  Every
   // K-tile gets its own buffer resource ending at the last valid k-row, and the k-row offsets live
   // in the per-lane voffset (the range check covers voffset, not soffset), so k-rows past the end
@@ -179,9 +180,12 @@ struct Stager {
                    : "memory", "m0");
       return;
     }
-    const bool second = DUAL && i >= 4;
+    // DUAL: instruction i fills tile rows 32 i .. 32 i + 31 = source rows 64 (i >> 2) + 32 (i & 1) + .. of
+    // W1 (i & 2 == 0) or W2, so each wave's 128 columns are 64 of a = x W1^T and the same 64 of b = x W2^T
+    const bool second = DUAL && ((i >> 1) & 1);
     const int vo = DUAL ? voff[0] : (MN ? voff[i & 1] : voff[i]);
-    const int so = (DUAL || MN) ? (second ? i - 4 : i) * istride + kt * kstride : kt * kstride;
+    const int so = DUAL ? (2 * (i >> 2) + (i & 1)) * istride + kt * kstride
+                        : (MN ? i * istride + kt * kstride : kt * kstride);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :
                  : "s"(dst), "v"(vo), "s"(second ? rsrc2 : rsrc), "s"(so)
@@ -309,9 +313,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   // SW: MFMA operands swapped (D = B-fragment x A-fragment^T, the TRANSPOSED 16 x 16 block), so each
   // lane accumulates 4 consecutive COLUMNS of one C row and the epilogue is register-only (cvt_pk +
   // permlane16_swap -> 16-B row stores), no LDS image: the image's 256 ds_write_b16 per lane cost
-  // ~8.4k of a tile's ~12k epilogue cycles (profiles/gemm4_epilogue_anatomy.txt).  The gate-up / swiglu
-  // epilogues (EPI 1 / 2), which exchange data between waves through LDS, keep the direct layout.
-  constexpr bool SW = EPI == 0 || EPI == 3;
+  // ~8.4k of a tile's ~12k epilogue cycles (profiles/gemm4_epilogue_anatomy.txt).  Every epilogue runs in
+  // registers: for the gate-up GEMM (EPI 1) the B tile interleaves W1 / W2 rows in 64-row groups so a lane
+  // holds a (block n) and b (block n + 4) of the same output element.
+  constexpr bool SW = true;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];  // the ONLY LDS object (rule 4a)
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -502,6 +507,87 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   }
   if constexpr (SW) {
     const int rsel = fq & 1, csel = fq >> 1;
+    if constexpr (EPI == 1) {
+      // gate-up: blocks 0-3 of this wave are a = x W1^T and blocks 4-7 b = x W2^T for the SAME 64 output
+      // columns c0 .. c0 + 63 (c0 = n0 / 2 + 64 wn); y = silu(a) * b from the bf16-rounded a, b (the
+      // unfused path's rounding points)
+      const int c0 = n0 / 2 + wn * 64;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int64_t grow = m0 + wm * 128 + m * 16 + fr;
+        uint32_t pa[4][2], pb[4][2], py[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          float a[4], b[4], y[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[j] = bf16_round(acc[m][n][j]);
+            b[j] = bf16_round(acc[m][n + 4][j]);
+            y[j] = a[j] * sigmoid_f(a[j]) * b[j];
+          }
+          pa[n][0] = pack_bf16x2(a[0], a[1]);
+          pa[n][1] = pack_bf16x2(a[2], a[3]);
+          pb[n][0] = pack_bf16x2(b[0], b[1]);
+          pb[n][1] = pack_bf16x2(b[2], b[3]);
+          py[n][0] = pack_bf16x2(y[0], y[1]);
+          py[n][1] = pack_bf16x2(y[2], y[3]);
+        }
+#pragma unroll
+        for (int np = 0; np < 2; ++np) {
+          const int n = 2 * np;
+          const uint4 va = swap_pair(pa[n][0], pa[n][1], pa[n + 1][0], pa[n + 1][1]);
+          const uint4 vb = swap_pair(pb[n][0], pb[n][1], pb[n + 1][0], pb[n + 1][1]);
+          const uint4 vy = swap_pair(py[n][0], py[n][1], py[n + 1][0], py[n + 1][1]);
+          if (grow < M) {
+            const int64_t o = grow * ldc + c0 + (n + rsel) * 16 + csel * 8;
+            if (C != nullptr) *reinterpret_cast<uint4*>(C + o) = va;
+            if (C2 != nullptr) *reinterpret_cast<uint4*>(C2 + o) = vb;
+            *reinterpret_cast<uint4*>(C3 + o) = vy;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded VGPR use
+      }
+      return;
+    }
+    if constexpr (EPI == 2) {
+      // swiglu backward in the dgrad epilogue: g (rounded to bf16, as the unfused dgrad stores it) and
+      // a, b at the same 8 elements -> da = g b silu'(a), db = g silu(a); g never leaves the chip
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int64_t grow = m0 + wm * 128 + m * 16 + fr;
+#pragma unroll
+        for (int np = 0; np < 4; ++np) {
+          const int n = 2 * np;
+          const uint4 gv = swap_pair(pack_bf16x2(acc[m][n][0], acc[m][n][1]), pack_bf16x2(acc[m][n][2], acc[m][n][3]),
+                                     pack_bf16x2(acc[m][n + 1][0], acc[m][n + 1][1]),
+                                     pack_bf16x2(acc[m][n + 1][2], acc[m][n + 1][3]));
+          const int gcol = n0 + wn * 128 + (n + rsel) * 16 + csel * 8;
+          if (grow < M) {
+            const uint4 va = *reinterpret_cast<const uint4*>(R + grow * ldc + gcol);
+            const uint4 vb = *reinterpret_cast<const uint4*>(R2 + grow * ldc + gcol);
+            const __hip_bfloat16* g = reinterpret_cast<const __hip_bfloat16*>(&gv);
+            const __hip_bfloat16* a = reinterpret_cast<const __hip_bfloat16*>(&va);
+            const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&vb);
+            float da[8], db[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = __bfloat162float(a[e]), gg = __bfloat162float(g[e]), bb = __bfloat162float(b[e]);
+              const float sg = sigmoid_f(x);
+              da[e] = gg * bb * (sg * (1.f + x * (1.f - sg)));
+              db[e] = gg * (x * sg);
+            }
+            *reinterpret_cast<uint4*>(C + grow * ldc + gcol) =
+                make_uint4(pack_bf16x2(da[0], da[1]), pack_bf16x2(da[2], da[3]), pack_bf16x2(da[4], da[5]),
+                           pack_bf16x2(da[6], da[7]));
+            *reinterpret_cast<uint4*>(C2 + grow * ldc + gcol) =
+                make_uint4(pack_bf16x2(db[0], db[1]), pack_bf16x2(db[2], db[3]), pack_bf16x2(db[4], db[5]),
+                           pack_bf16x2(db[6], db[7]));
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one block pair at a time: bounded VGPR use
+        }
+      }
+      return;
+    }
     if constexpr (EPI == 3) {
       // this wave's 128 columns are one head: q head cb, k head cb - nh or v head cb - nh - ng.  A
       // dimension d < 64 (block n < 4) and its rotate-half partner d + 64 (block n + 4) sit in the same
@@ -576,8 +662,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
           }
         }
       }
-      auto store_all = [&](auto scaled_c) {
-        constexpr bool SCALED = decltype(scaled_c)::value;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const int64_t grow = m0 + wm * 128 + m * 16 + fr;
@@ -589,8 +673,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
           for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float x = acc[m][n + h][j];
-              if constexpr (SCALED) x *= alpha;
+              float x = acc[m][n + h][j] * alpha;
               if constexpr (BIAS) x += bv[n + h][j];
               v[h][j] = act_fn<ACT>(x);
             }
@@ -616,12 +699,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
           __builtin_amdgcn_sched_barrier(0);  // one block pair at a time: bounded VGPR use
         }
       }
-      };
-      // alpha == 1 (every training GEMM) skips the 256 multiplies per lane
-      if (alpha == 1.f)
-        store_all(std::false_type{});
-      else
-        store_all(std::true_type{});
       return;
     }
   } else {

@@ -89,3 +89,47 @@ def test_llama2_7b_shape_bf16_vs_fp32(gemm_mode, monkeypatch):
 
     # every GEMM of the step ran on the hand-written kernel (no library fallback)
     assert G.last_gemm_backend_counts().get("torch", 0) == 0, G.last_gemm_backend_counts()
+
+
+@pytest.mark.parametrize("tp", [2, 8])
+def test_llama3_8b_tensor_parallel_shard_shapes_on_hand_gemms(tp):
+    """BASELINE config 4 (Llama-3-8B, TP=8, seq 8192): one rank's GEMMs are the shard shapes — the
+    head-parallel qkv (4 query heads + 1 kv group at TP=8), the row-parallel proj (K = 512), the
+    column-parallel SwiGLU pair (N = 1792) and its down projection (K = 1792), the vocab-parallel LM head
+    (N = 16032).  One rank's block runs here as a plain model with those local sizes (the collectives
+    are identity at world 1); every forward and backward GEMM must take the hand-written kernel (no
+    library fallback), and the step must match fp32 eager."""
+    from lightning_thunder_amd.ops import gemm as G
+
+    seq = 8192
+    cfg = dict(n_layer=1, n_head=32 // tp, n_query_groups=8 // tp, intermediate_size=14336 // tp,
+               padded_vocab_size=128256 // tp, vocab_size=128256 // tp)
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = GPT.from_name("Llama-3-8B", **cfg).to(device=dev)
+    init_weights(m)
+    m = m.to(torch.bfloat16)
+    m.set_rope_cache(seq, device=dev)
+    idx = torch.randint(0, cfg["vocab_size"], (1, seq), device=dev)
+    tgt = torch.randint(0, cfg["vocab_size"], (1, seq), device=dev)
+
+    class TrainStep(torch.nn.Module):
+        def __init__(self, mm):
+            super().__init__()
+            self.m = mm
+
+        def forward(self, x, y):
+            logits = self.m(x)
+            return torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
+
+    tm = thunder.jit(TrainStep(m))
+    G.last_gemm_backend_counts(reset=True)
+    loss = tm(idx, tgt)
+    loss.backward()
+    torch.cuda.synchronize()
+    counts = G.last_gemm_backend_counts(reset=True)
+    assert counts.get("torch", 0) == 0 and counts.get("gemm4", 0) > 0, counts
+    with torch.no_grad():
+        ref = TrainStep(m)(idx, tgt).float()
+    assert abs(loss.item() - ref.item()) / abs(ref.item()) < 2e-2, (loss.item(), ref.item())
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
