@@ -512,7 +512,37 @@ def _tp_in_impl(a, group, layer_type):
     return a
 
 
+def _vp_ce_hand_kernels(logits) -> bool:
+    """The vocab-parallel CE runs its per-rank passes on the hand CE kernels (csrc/swiglu_ce.hip) for
+    GPU bf16 / fp16 / fp32 logits: one read of the local logits per pass instead of ATen's fp32 copy,
+    exp, reductions and the one-hot scatter over the whole [tokens, V / world] slice."""
+    if not logits.is_cuda or logits.dtype not in (torch.bfloat16, torch.float16, torch.float32) or logits.dim() != 2:
+        return False
+    try:
+        from ..ops._lib import require
+
+        require()
+        return True
+    except Exception:
+        return False
+
+
 def _vp_ce_fwd_impl(logits, target, group, vocab_start, ignore_index=-100):
+    if _vp_ce_hand_kernels(logits):
+        from ..ops.fused import ce_row_stats
+
+        V = logits.shape[-1]
+        t = target.long() - vocab_start
+        local = (t >= 0) & (t < V) & (target != ignore_index)
+        lse_r, loss_r = ce_row_stats(logits, torch.where(local, t, torch.full_like(t, ignore_index)), ignore_index)
+        xt = torch.where(local, lse_r - loss_r, torch.zeros((), device=logits.device))
+        m = lse_r.clone()
+        tdist.all_reduce(m, tdist.ReduceOp.MAX, group=group)
+        st = torch.stack(((lse_r - m).exp(), xt))
+        tdist.all_reduce(st, tdist.ReduceOp.SUM, group=group)
+        lse = m + st[0].log()
+        rows = torch.where(target != ignore_index, lse - st[1], torch.zeros((), device=logits.device))
+        return rows, lse
     x = logits if logits.dtype == torch.float64 else logits.float()
     V = x.shape[-1]
     m = x.amax(-1)
@@ -531,6 +561,17 @@ def _vp_ce_fwd_impl(logits, target, group, vocab_start, ignore_index=-100):
 
 
 def _vp_ce_bwd_impl(g_rows, logits, target, lse, vocab_start, ignore_index=-100):
+    if _vp_ce_hand_kernels(logits):
+        from ..ops.fused import cross_entropy_bwd
+
+        V = logits.shape[-1]
+        t = target.long() - vocab_start
+        inr = (t >= 0) & (t < V)
+        # V: "the target lives on another rank" (no one-hot term, the row's gradient is kept);
+        # ignore_index rows get a zero gradient from the kernel
+        tl = torch.where(target == ignore_index, torch.full_like(t, ignore_index),
+                         torch.where(inr, t, torch.full_like(t, V)))
+        return cross_entropy_bwd(g_rows, logits, tl, lse.float().contiguous(), None, ignore_index, reduction="none")
     x = logits if logits.dtype == torch.float64 else logits.float()
     V = x.shape[-1]
     p = (x - lse[:, None]).exp()

@@ -145,6 +145,21 @@ def cross_entropy_fwd(logits, target, ignore_index: int = -100, reduction: str =
     return loss, lse, stats
 
 
+def ce_row_stats(logits, target_local, ignore_index: int = -100):
+    """Per-row fp32 ``(lse, lse - x[target])`` of ``logits`` [rows, V] in ONE pass of the hand CE kernel
+    (rows whose ``target_local`` is ``ignore_index`` get 0 in the second output) — the local half of
+    a vocab-parallel cross-entropy."""
+    lib = require()
+    logits = _c(logits)
+    target = _c(target_local.to(torch.int64))
+    rows, V = logits.shape
+    loss_rows = torch.empty(rows, device=logits.device, dtype=torch.float32)
+    lse = torch.empty(rows, device=logits.device, dtype=torch.float32)
+    check(lib.lta_ce_fwd_w(dcode(logits), ptr(logits), ptr(target), None, ptr(loss_rows), ptr(lse), None, rows, V,
+                           int(ignore_index), 0, 0.0, stream_ptr(logits.device)), "lta_ce_fwd")
+    return lse, loss_rows
+
+
 def cross_entropy_bwd(g, logits, target, lse, stats, ignore_index: int = -100, reduction: str = "mean",
                       label_smoothing: float = 0.0, weight=None):
     lib = require()
