@@ -12,7 +12,9 @@ import threading
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lta_kernels.so")
+# LTA_KERNELS_SO: load another build of the library (e.g. the diagnostic build of
+# ``python -m lightning_thunder_amd.ops.build --diag``: phase-stamp / ablation kernels)
+LIB_PATH = os.environ.get("LTA_KERNELS_SO") or os.path.join(HERE, "_lta_kernels.so")
 
 _lib = None
 _lock = threading.Lock()

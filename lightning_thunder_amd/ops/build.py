@@ -48,8 +48,9 @@ FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
               "attention_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
-def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:
-    cmd = [_hipcc(), "-c", src, "-o", obj, "-fPIC", "-O3", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
+def _compile(src: str, obj: str, is_device: bool, verbose: bool, defines=()) -> str:
+    cmd = [_hipcc(), "-c", src, "-o", obj, "-fPIC", "-O3", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result",
+           *[f"-D{d}" for d in defines]]
     if is_device:
         cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + FILE_FLAGS.get(os.path.basename(src), [])
     else:
@@ -62,7 +63,14 @@ def _compile(src: str, obj: str, is_device: bool, verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None, defines=(), build_dir: str | None = None,
+          lib_path: str | None = None) -> str:
+    """Incremental hipcc build of every csrc source for gfx950 into one shared library.  ``defines``
+    / ``build_dir`` / ``lib_path`` make a separate variant (the diagnostic build: ``--diag OUT``
+    compiles the measurement-only kernels behind -DLTA_ATTN_DIAG into OUT, loaded with
+    LTA_KERNELS_SO=OUT; the production library is untouched)."""
+    BUILD = build_dir or globals()["BUILD"]
+    LIB = lib_path or globals()["LIB"]
     os.makedirs(BUILD, exist_ok=True)
     hip, cpp = _sources()
     hdr = _headers_mtime()
@@ -76,7 +84,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4) // 2))
     if todo:
         with cf.ThreadPoolExecutor(jobs) as pool:
-            futs = [pool.submit(_compile, s, o, d, verbose) for s, o, d in todo]
+            futs = [pool.submit(_compile, s, o, d, verbose, defines) for s, o, d in todo]
             for f in futs:
                 f.result()
     newest = max((os.path.getmtime(o) for o in objs), default=0.0)
@@ -92,5 +100,10 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
 
 
 if __name__ == "__main__":
-    path = build(force="--force" in sys.argv, verbose="-v" in sys.argv)
+    if "--diag" in sys.argv:
+        out = os.path.abspath(sys.argv[sys.argv.index("--diag") + 1])
+        path = build(force="--force" in sys.argv, verbose="-v" in sys.argv, defines=("LTA_ATTN_DIAG",),
+                     build_dir=os.path.join(os.path.dirname(out), "_build_diag"), lib_path=out)
+    else:
+        path = build(force="--force" in sys.argv, verbose="-v" in sys.argv)
     print(path)

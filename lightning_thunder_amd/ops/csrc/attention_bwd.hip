@@ -472,14 +472,16 @@ constexpr int kKB3 = 256;
 //   A: S = Q K^T (16 MFMA)      B: dP = dO V^T (16) | P = exp2(S c - LSE)
 //   C: dV^T += dO^T P (16) | dS = P (dP - delta), pack    D: dK^T += Q^T dS (16)
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool CAUSAL>
+// STAMP (diagnostic builds only, -DLTA_ATTN_DIAG): s_memtime at the phase boundaries of workgroup (0, 0)'s
+// first 64 query tiles, kept in LDS and copied to `dbg` at the end ([4 waves][64 tiles][8] u64)
+template <typename T, bool CAUSAL, int STAMP = 0>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                        const T* __restrict__ V, const T* __restrict__ dO,
                                                                        const float* __restrict__ LSE,
                                                                        const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
                                                                        float scale, float scale_log2, RowStrides sdo, QKVStrides sx,
-                                                                       int qrev = 0) {
+                                                                       int qrev = 0, uint64_t* dbg = nullptr) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -487,7 +489,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   constexpr int IMG = kQT * 256;
   constexpr int STAGE = 2 * IMG + 256;
   constexpr int VOFF = NST * STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[VOFF + kKB3 * C::RSTR * 2];
+  constexpr int SBASE = VOFF + kKB3 * C::RSTR * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[SBASE + (STAMP ? 4 * 64 * 8 * 8 : 0)];
   short* Vs = reinterpret_cast<short*>(smem + VOFF);
 
   const int kb = (int)blockIdx.y;
@@ -603,7 +606,18 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   }
   constexpr float kLog2e = 1.44269504088896340736f;
   int ti = 0, st = 0;
+  auto stamp = [&](int it, int k) {
+    if constexpr (STAMP != 0) {
+      if (blockIdx.x == 0 && blockIdx.y == 0 && it < 64) {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts = __builtin_amdgcn_s_memtime();
+        if (lane == 0) *reinterpret_cast<uint64_t*>(smem + SBASE + ((wave * 64 + it) * 8 + k) * 8) = ts;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   for (int it = 0; it < total; ++it) {
+    stamp(it, 0);
     const bool issue_next = it + 2 < total;
     const int st2 = st >= 1 ? st - 1 : 2;
     if (issue_next) issue(nhi, nti, st2);
@@ -639,6 +653,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           for (int j = 0; j < 2; ++j) sacc[j] = mfma(qa[s], kf[j][s], sacc[j]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      stamp(it, 1);
       // phase B: dP = dO V^T, with P = exp2(S c - LSE log2 e) in the MFMAs' shadow: slice s of the
       // exponentials (4 of the 32 per lane) follows the two MFMAs of k-step s, whose operands were
       // read one slice earlier
@@ -667,6 +682,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           va1 = vb1;
         }
       }
+      stamp(it, 2);
 #pragma unroll
       for (int a = 0; a < 4; ++a) Dl[a] = *reinterpret_cast<const f32x4v*>(sl + kQT + 4 * h + 8 * a);
       s16x4t xr[16];
@@ -689,6 +705,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
       }
       pack_frag(pf[1][0], sacc[1], 0);
       pack_frag(pf[1][1], sacc[1], 1);
+      stamp(it, 3);
       {
         F xt[8];
         tr_wait16(xt, xr);
@@ -714,6 +731,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+        stamp(it, 4);
         tr_wait16(xt, xr);  // Q^T
         // phase D: dK^T += Q^T dS
 #pragma unroll
@@ -725,6 +743,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           }
       }
     }
+    stamp(it, 5);
     if (issue_next) {
       advance();
       wait_all_but_newest();
@@ -732,11 +751,19 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    stamp(it, 6);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    stamp(it, 7);
     ti = ti + 1 == nq ? 0 : ti + 1;
     st = st == 2 ? 0 : st + 1;
+  }
+  if constexpr (STAMP != 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && dbg != nullptr) {
+      __syncthreads();
+      for (int i = tid; i < 4 * 64 * 8; i += kThreads) dbg[i] = *reinterpret_cast<const uint64_t*>(smem + SBASE + i * 8);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -1221,11 +1248,31 @@ void launch_masked(const void* dO, const void* Q, const void* K, const void* V, 
 #undef LTA_DQ
 }
 
+#ifdef LTA_ATTN_DIAG
+uint64_t* g_dkdv_stamps = nullptr;  // diagnostic builds: dK/dV phase stamps (lta_attn_bwd_set_stamps)
+#endif
 // dK/dV sweep order of the D = 128 kernel: query tiles last-to-first (A/B: LTA_DKDV_QREV=0)
 int g_dkdv_qrev = [] {
   const char* e = getenv("LTA_DKDV_QREV");
   return (e && e[0] == '0') ? 0 : 1;
 }();
+
+#ifdef LTA_ATTN_DIAG
+#define LTA_DKDV_LAUNCH(CA)                                                                                          \
+  if (g_dkdv_stamps)                                                                                                 \
+    hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 1>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,   \
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, \
+                       sl2, sdo, ex.sx, g_dkdv_qrev, g_dkdv_stamps);                                                  \
+  else                                                                                                               \
+    hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,       \
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, \
+                       sl2, sdo, ex.sx, g_dkdv_qrev, nullptr)
+#else
+#define LTA_DKDV_LAUNCH(CA)                                                                                          \
+  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,         \
+                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
+                     sdo, ex.sx, g_dkdv_qrev, nullptr)
+#endif
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -1242,9 +1289,7 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
   hipLaunchKernelGGL((attn_bwd_dq_v4_kernel<T, CA>), gq, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,            \
                      (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo,   \
                      ex.sx, (const T*)O, so);                                                                          \
-  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,          \
-                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
-                     sdo, ex.sx, g_dkdv_qrev)
+  LTA_DKDV_LAUNCH(CA)
     if (causal) { LTA_FAST(true); }
     else { LTA_FAST(false); }
 #undef LTA_FAST
@@ -1414,6 +1459,13 @@ LTA_EXPORT int lta_attn_bwd(int dtype, const void* dO, const void* Q, const void
                         nullptr, stream);
 }
 
+#ifdef LTA_ATTN_DIAG
+// diagnostic builds: route the dK/dV kernel to its phase-stamp build, stamps into `dbg` (null: off)
+LTA_EXPORT int lta_attn_bwd_set_stamps(void* dbg) {
+  g_dkdv_stamps = (uint64_t*)dbg;
+  return 0;
+}
+#endif
 // dK/dV query-tile order of the D = 128 kernel (A/B measurement hook): 1 = last tile first, 0 = first
 // tile first; returns the previous choice
 LTA_EXPORT int lta_attn_bwd_set_dkdv_qrev(int rev) {

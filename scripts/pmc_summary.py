@@ -16,8 +16,8 @@ def load(d):
     acc = defaultdict(lambda: defaultdict(list))
     for f in files:
         for r in csv.DictReader(open(f)):
-            k = r.get("Kernel_Name", "").split("(")[0].replace("void ", "")
-            k = k.replace("(anonymous namespace)::", "")
+            k = r.get("Kernel_Name", "").replace("(anonymous namespace)::", "").replace("void ", "")
+            k = k.split("(")[0]
             name = r.get("Counter_Name")
             val = float(r.get("Counter_Value", 0) or 0)
             disp = r.get("Dispatch_Id", r.get("Correlation_Id", "0"))
