@@ -205,10 +205,13 @@ def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: l
         buf[k] = _double_bits(x)
         k += 1
     ws = None
+    from ..ops._lib import stream_ptr
+
     if ks.ws_bytes:
         ws = torch.empty(ks.ws_bytes, dtype=torch.uint8, device=dev)  # stream-ordered by the allocator
         buf[k] = ws.data_ptr()
-    from ..ops._lib import stream_ptr
+        if ks.counters:
+            buf = _with_counters(buf, _counters(ks.counters, dev))
 
     launches = [(g, b) for _, g, b in ks.pre] + [(ks.grid, ks.block)] + [(g, b) for _, g, b in ks.extra]
     for fn, (grid, block) in zip(fns, launches):
@@ -217,6 +220,40 @@ def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: l
         if rc != 0:
             raise RuntimeError(f"{name}: hipModuleLaunchKernel failed with {rc}")
     del ws
+
+
+_COUNTERS: dict = {}
+_CNT_BUF_T: dict = {}
+
+
+def _counters(n: int, dev) -> torch.Tensor:
+    """Zeroed uint32 arrival counters of the column-mode kernels: one persistent buffer per (device,
+    stream), grown on demand.  Every launch leaves its counters at zero again (the last workgroup of
+    each column group resets its own), so kernels ordered on one stream can share it; a graph capture
+    keeps the capture stream's buffer."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _COUNTERS.get(key)
+    if buf is None or buf.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("hipFusion: column-reduction counters must be allocated before a graph capture "
+                               "(run the function once eagerly first)")
+        old = buf
+        buf = torch.zeros(max(n, 1024), dtype=torch.int32, device=dev)
+        if old is not None:
+            buf.record_stream(torch.cuda.current_stream(dev))
+        _COUNTERS[key] = buf
+    return buf
+
+
+def _with_counters(buf, cnt: torch.Tensor):
+    """``buf`` plus one trailing word: the counters pointer (Args ``cnt``)."""
+    n = len(buf)
+    t = _CNT_BUF_T.get(n)
+    if t is None:
+        t = _CNT_BUF_T[n] = ctypes.c_uint64 * (n + 1)
+    out = t(*buf)
+    out[n] = cnt.data_ptr()
+    return out
 
 
 def load_kernels(ks: cg.KernelSource) -> list:

@@ -35,6 +35,7 @@ from __future__ import annotations
 import hashlib
 import re
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -807,8 +808,19 @@ class TensorArg:
     align16: bool
 
 
+# column-mode partial hand-off between workgroups: "coherent" (sc1 vector memory ops + s_waitcnt) or
+# "fence" (__threadfence); LTA_HIPFUSE_COL_SYNC overrides (A/B hook, scripts/colred_bench.py)
+COL_SYNC = os.environ.get("LTA_HIPFUSE_COL_SYNC", "coherent")
+# column-mode grid (profiles/hipfuse_colred_sweep.txt: 8 waves x 8 rows in flight per wave, ~192
+# workgroups, at most 64 row splits was the fastest of the swept configurations on every shape)
+COL_NW = int(os.environ.get("LTA_HIPFUSE_COL_NW", "8"))  # waves per column-mode workgroup
+COL_WGS = int(os.environ.get("LTA_HIPFUSE_COL_WGS", "192"))  # target workgroups of a column-mode grid
+COL_UNROLL = int(os.environ.get("LTA_HIPFUSE_COL_UNROLL", "8"))  # rows in flight per wave
+COL_MAX_SPLITS = 64  # the last workgroup of a column group reads every split's partial
+
+
 class KernelSource:
-    def __init__(self, name, src, grid, block, vec, mode, extra=(), ws_bytes=0, pre=()):
+    def __init__(self, name, src, grid, block, vec, mode, extra=(), ws_bytes=0, pre=(), counters=0):
         self.name, self.src, self.grid, self.block, self.vec, self.mode = name, src, grid, block, vec, mode
         # further kernels launched after the main one with the same arguments: (name suffix, grid, block)
         self.extra = list(extra)
@@ -816,6 +828,9 @@ class KernelSource:
         self.pre = list(pre)
         # bytes of scratch the kernels share (passed as the last Args field), 0 = none
         self.ws_bytes = ws_bytes
+        # column mode: uint32 arrival counters the kernel reads and resets (a persistent zeroed buffer
+        # per (device, stream), passed after the workspace pointer), 0 = none
+        self.counters = counters
 
 
 def _contig_strides(shape):
@@ -895,7 +910,8 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
     name = f"{kernel_prefix}_{h}"
     src = src.replace("__KERNEL_NAME__", name)
-    return KernelSource(name, src, grid, block, vec, mode, extra=g.extra, ws_bytes=g.ws_bytes, pre=g.pre)
+    return KernelSource(name, src, grid, block, vec, mode, extra=g.extra, ws_bytes=g.ws_bytes, pre=g.pre,
+                        counters=g.counters)
 
 
 class _Gen:
@@ -914,6 +930,7 @@ class _Gen:
         self.extra: list = []
         self.pre: list = []
         self.ws_bytes = 0
+        self.counters = 0
         self.tensor_inputs = [a for a in inputs if isinstance(a, TensorProxy)]
         self.number_inputs = [a for a in inputs if not isinstance(a, TensorProxy)]
         self.in_index = {a.name: i for i, a in enumerate(self.tensor_inputs)}
@@ -1002,7 +1019,7 @@ class _Gen:
             sum((s - 1) * st for s, st in zip(t.shape, t.strides)) >= 2**31 for t in self.targs.values())
         self.IT = "unsigned long long" if big else "unsigned"
         if self.colred:
-            return self._build_col(numel)
+            return self._build_col_twopass(numel) if COL_SYNC == "twopass" else self._build_col(numel)
         if self.red:
             return self._build_row(numel)
         return self._build_pointwise(numel)
@@ -1017,6 +1034,8 @@ class _Gen:
             fields.append(f"double s[{ns}];")
         if self.colred:
             fields.append("void* ws;")
+            if self.counters:
+                fields.append("unsigned* cnt;")
         return "struct Args { " + " ".join(fields) + " };"
 
     def _ptr(self, t: TensorProxy, is_out: bool) -> str:
@@ -1806,6 +1825,223 @@ class _Gen:
         return act, ("0" if act == "long long" else _lit(0.0, act)), "+"
 
     def _build_col(self, numel):
+        """Column mode (leading dims reduced): ONE launch.  Workgroup (x, y) = NW waves over the rows of
+        split y for the 64 V columns of group x; each lane keeps V column accumulators (16-B loads),
+        the waves combine in LDS (fixed order).  With S > 1 row splits, every workgroup stores its
+        fp32 partial, and the LAST workgroup of a column group to finish (agent-scope counter, reset
+        by that workgroup) sums the S partials in a fixed order and runs the column epilogue: the
+        result does not depend on which workgroup finished last (deterministic), and no second
+        launch or host-visible state is needed.  Parity: the grid reduction of nvFuser's reduction
+        scheduler behind reference thunder/executors/nvfuserex_impl.py:836-939."""
+        V, IT = self.vec, self.IT
+        nd, k, D = self.nd, self.colred, self.D
+        C = math.prod(D[k:])
+        R = math.prod(D[:k])
+        NW = COL_NW  # waves per workgroup
+        ncs = (C // V + 63) // 64
+        # row splits: ~COL_WGS workgroups of NW waves (at most one per CU), >= 8 rows per wave, and at
+        # most COL_MAX_SPLITS (the serial tail reads them all)
+        S = max(1, min(-(-COL_WGS // ncs), -(-R // (8 * NW)), COL_MAX_SPLITS))
+        RPS = -(-R // S)
+        S = -(-R // RPS)
+        red_nodes = [i for i, b in enumerate(self.p.nodes) if b.sym.id in REDUCTIONS]
+        full_outs = [o for o in self.outputs if self.p.covers_reduced(self.p.maps.get(o.name))]
+        full_names = {o.name for o in full_outs}
+        col_outs = [o for o in self.outputs if o.name not in full_names]
+        self.load_names, self.loaded, self.idx_avail = {}, set(), set()
+        for kk, b in enumerate(self.p.nodes):
+            for i, a in tensor_args(b):
+                if a.name not in self.producer:
+                    self.ref(a, kk, i, "j")
+        accs = []
+        for n, kk in enumerate(red_nodes):
+            act, init, comb = self._red_acc(self.p.nodes[kk])
+            accs.append((n, kk, act, init, comb))
+
+        def cf(comb, act, u, v):
+            return f"({u} {comb} {v})" if comb in ("+", "*") else f"{comb}<{act}>({u}, {v})"
+
+        self._scope_id = "vec"
+        body: list[str] = []
+        body.append("  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;")
+        body.append(f"  const {IT} e = (({IT})blockIdx.x * 64u + lane) * {V}u;")
+        body.append(f"  const bool cvalid = e < {C}u;")
+        body.append(f"  const {IT} ec = cvalid ? e : 0u;")
+        self._decompose("ec", list(range(k, nd)), body, "  ")
+        self.flat_index = f"((unsigned long long)r * {C}ull + (unsigned long long)ec + (unsigned long long)j)"
+        for n, kk, act, init, comb in accs:
+            body.append(f"  {act} acc{n}[{V}];")
+            body.append(f"  #pragma unroll")
+            body.append(f"  for (int j = 0; j < {V}; ++j) acc{n}[j] = {init};")
+        body.append(f"  const {IT} r0 = ({IT})blockIdx.y * {RPS}u;")
+        body.append(f"  const {IT} r1 = r0 + {RPS}u < {R}u ? r0 + {RPS}u : {R}u;")
+        # unrolled: each wave keeps COL_UNROLL rows' loads in flight (the adds keep their serial order)
+        body.append(f"  #pragma unroll {COL_UNROLL}")
+        body.append(f"  for ({IT} r = r0 + wv; r < (cvalid ? r1 : 0u); r += {NW}u) {{")
+        ind = "    "
+        self._decompose("r", list(range(k)), body, ind)
+        need = {o.name for o in full_outs}
+        for n, kk, act, init, comb in accs:
+            a = self.p.nodes[kk].args[0]
+            if a.name in self.producer:
+                need.add(a.name)
+        emitted: set = set()
+        self._emit_nodes(need, "vec", emitted, body, ind)
+        for n, kk, act, init, comb in accs:
+            b = self.p.nodes[kk]
+            x = self.ref(b.args[0], kk, 0, "j")
+            self._materialize_loads(b, kk, True, body, ind)
+            body.append(f"{ind}#pragma unroll")
+            if comb in ("+", "*"):
+                body.append(f"{ind}for (int j = 0; j < {V}; ++j) acc{n}[j] {comb}= ({act})({x});")
+            else:
+                body.append(f"{ind}for (int j = 0; j < {V}; ++j) acc{n}[j] = {comb}<{act}>(acc{n}[j], ({act})({x}));")
+        for o in full_outs:
+            self._emit_store(o, True, body, ind)
+        body.append("  }")
+
+        def lds_combine():
+            """the NW waves' accumulators -> LDS (combined in a fixed order by ``wave_total``)"""
+            for n, kk, act, init, comb in accs:
+                body.append(f"  #pragma unroll")
+                body.append(f"  for (int j = 0; j < {V}; ++j) sm{n}[wv][lane * {V}u + j] = acc{n}[j];")
+            body.append("  __syncthreads();")
+
+        def wave_total(n, act, comb, q):
+            expr = f"sm{n}[0][{q}]"
+            for w in range(1, NW):
+                expr = cf(comb, act, expr, f"sm{n}[{w}][{q}]")
+            return expr
+
+        for n, kk, act, init, comb in accs:
+            body.append(f"  __shared__ {act} sm{n}[{NW}][{64 * V}];")
+        lds_combine()
+        ws_off = 0
+        offs = []
+        for n, kk, act, init, comb in accs:
+            offs.append(ws_off)
+            ws_off += S * C * 8
+        _SZ = {"float": 4, "double": 8, "int": 4, "long long": 8}
+
+        def vec_ok(act):
+            # whole 16-B vectors: every row of the partial and every lane's V columns 16-B aligned
+            sz = _SZ.get(act)
+            return sz is not None and (V * sz) % 16 == 0 and (C * sz) % 16 == 0
+
+        # cross-workgroup hand-off of the partials: "coherent" (default) writes and reads them with
+        # agent-coherent (sc1) vector memory operations and orders them with s_waitcnt before the
+        # arrival counter; "fence" uses __threadfence() (an agent-scope fence writes back / invalidates
+        # the whole L2 of the XCD: measured ~40 us per [8192, 1024] sum with 256 workgroups)
+        coherent = COL_SYNC == "coherent" and ws_off < 2**31
+        if S > 1:
+            if coherent:
+                self.typedefs["v4_u32"] = "typedef unsigned v4_u32 __attribute__((ext_vector_type(4)));"
+                body.append("  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(A.ws, (short)0, "
+                            "0x7fffffff, 0x00020000);")
+            # this split's partial (wave 0: the fixed-order wave combination)
+            body.append("  if (wv == 0u && cvalid) {")
+            for (n, kk, act, init, comb), off in zip(accs, offs):
+                body.append(f"    {act}* ws{n} = ({act}*)((char*)A.ws + {off}ull) + ({IT})blockIdx.y * {C}u;")
+                if vec_ok(act):
+                    vt = self._vtype(act, V)
+                    body.append(f"    {vt} pv{n};")
+                    body.append(f"    #pragma unroll")
+                    body.append(f"    for (int j = 0; j < {V}; ++j) pv{n}[j] = {wave_total(n, act, comb, f'lane * {V}u + j')};")
+                    if coherent:
+                        sz = _SZ[act]
+                        body.append(f"    const v4_u32* pu{n} = (const v4_u32*)&pv{n};")
+                        body.append(f"    const unsigned bo{n} = {off}u + ((unsigned)blockIdx.y * {C}u + (unsigned)e) * {sz}u;")
+                        for c in range(V * sz // 16):
+                            body.append(f"    __builtin_amdgcn_raw_buffer_store_b128(pu{n}[{c}], wsr, bo{n} + {16 * c}u, 0, 16);")
+                    else:
+                        body.append(f"    *({vt}*)(ws{n} + e) = pv{n};")
+                else:
+                    body.append(f"    #pragma unroll")
+                    if coherent:
+                        body.append(f"    for (int j = 0; j < {V}; ++j) __hip_atomic_store(ws{n} + e + j, "
+                                    f"({act})({wave_total(n, act, comb, f'lane * {V}u + j')}), __ATOMIC_RELAXED, "
+                                    "__HIP_MEMORY_SCOPE_AGENT);")
+                    else:
+                        body.append(f"    for (int j = 0; j < {V}; ++j) ws{n}[e + j] = {wave_total(n, act, comb, f'lane * {V}u + j')};")
+            body.append("  }")
+            # count this split in once its partial is at the coherence point; only the last workgroup of
+            # the column group goes on
+            if coherent:
+                body.append('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            else:
+                body.append("  __threadfence();")
+            body.append("  __shared__ unsigned last;")
+            body.append("  __syncthreads();")
+            body.append("  if (threadIdx.x == 0u) last = atomicAdd(A.cnt + blockIdx.x, 1u) == "
+                        f"{S - 1}u ? 1u : 0u;")
+            body.append("  __syncthreads();")
+            body.append("  if (last == 0u) return;")
+            if not coherent:
+                body.append("  __threadfence();  // acquire: the other splits' partials")
+            body.append("  if (threadIdx.x == 0u) __hip_atomic_store(A.cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, "
+                        "__HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch")
+            # wave w sums splits w, w + NW, ... (8 splits' loads in flight), then the waves combine in LDS
+            for (n, kk, act, init, comb), off in zip(accs, offs):
+                body.append(f"  const {act}* pw{n} = (const {act}*)((const char*)A.ws + {off}ull);")
+                body.append(f"  #pragma unroll")
+                body.append(f"  for (int j = 0; j < {V}; ++j) acc{n}[j] = {init};")
+                body.append("  #pragma unroll 8")
+                body.append(f"  for (unsigned sp = wv; sp < (cvalid ? {S}u : 0u); sp += {NW}u) {{")
+                if vec_ok(act) and coherent:
+                    sz = _SZ[act]
+                    nch = V * sz // 16
+                    body.append(f"    v4_u32 qr{n}[{nch}];")
+                    body.append(f"    const unsigned bq{n} = {off}u + (sp * {C}u + (unsigned)e) * {sz}u;")
+                    for c in range(nch):
+                        body.append(f"    qr{n}[{c}] = __builtin_amdgcn_raw_buffer_load_b128(wsr, bq{n} + {16 * c}u, 0, 16);")
+                    body.append(f"    const {act}* q{n} = (const {act}*)qr{n};")
+                elif vec_ok(act):
+                    vt = self._vtype(act, V)
+                    body.append(f"    const {vt} q{n} = *(const {vt}*)(pw{n} + ({IT})sp * {C}u + e);")
+                elif coherent:
+                    body.append(f"    {act} q{n}[{V}];")
+                    body.append(f"    #pragma unroll")
+                    body.append(f"    for (int j = 0; j < {V}; ++j) q{n}[j] = __hip_atomic_load(pw{n} + ({IT})sp * {C}u + e + j, "
+                                "__ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);")
+                else:
+                    body.append(f"    const {act}* q{n} = pw{n} + ({IT})sp * {C}u + e;")
+                body.append(f"    #pragma unroll")
+                body.append(f"    for (int j = 0; j < {V}; ++j) acc{n}[j] = {cf(comb, act, f'acc{n}[j]', f'q{n}[j]')};")
+                body.append("  }")
+            body.append("  __syncthreads();")
+            lds_combine()
+        # column epilogue: thread t takes columns t, t + 64 NW, ... of the group (one element each)
+        self.force_scalar = True
+        self._scope_id = "fin"
+        self.idx_avail = set()
+        body.append(f"  for (unsigned qc = threadIdx.x; qc < {64 * V}u; qc += {64 * NW}u) {{")
+        ind = "    "
+        body.append(f"{ind}const {IT} ecol = ({IT})blockIdx.x * {64 * V}u + qc;")
+        body.append(f"{ind}if (ecol >= {C}u) break;")
+        fin: list[str] = []
+        self._decompose("ecol", list(range(k, nd)), fin, ind)
+        done: set = set()
+        for n, kk, act, init, comb in accs:
+            o = self.p.nodes[kk].output
+            out_ct = _CTYPE[o.dtype]
+            fin.append(f"{ind}const {act} t{n} = {wave_total(n, act, comb, 'qc')};")
+            fin.append(f"{ind}const {out_ct} r_{o.name} = {_rnd(o.dtype, f'({out_ct})(t{n})')};")
+            done.add(o.name)
+        self._emit_nodes({o.name for o in col_outs}, "row", done, fin, ind)
+        for o in col_outs:
+            st, _ = self._out_strides(o)
+            off = " + ".join(f"(({IT})i{d} * {st[d]}u)" for d in range(nd) if st[d]) or "0"
+            fin.append(f"{ind}{self._ptr(o, True)}[{off}] = {_store_conv(o.dtype, f'r_{o.name}')};")
+        body += fin
+        body.append("  }")
+        self.force_scalar = False
+        self.extra = []
+        # the Args block always carries both pointers (S == 1 never touches them)
+        self.ws_bytes = ws_off
+        self.counters = ncs
+        return self._wrap(body, 64 * NW), (ncs, S, 1), (64 * NW, 1, 1), V, f"col(S={S})"
+
+    def _build_col_twopass(self, numel):
         V, IT = self.vec, self.IT
         nd, k, D = self.nd, self.colred, self.D
         C = math.prod(D[k:])

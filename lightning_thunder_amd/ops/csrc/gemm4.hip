@@ -264,9 +264,9 @@ struct EpiArgs {
   const int* offs;           // GRP 1 / 2: int32 cumulative group ends (device)
   int G;                     // GRP: number of groups
   int64_t bstride, cstride;  // GRP 1: elements between groups' B; GRP 2: between groups' C
-  // GRP 0 tail split (lta_gemm4_bf16_ws): this launch covers the linear tiles [tile_base, tile_base +
-  // tile_count) (kernel TAIL = 1 and 2); ksplit == 2: workgroup b computes K half b & 1 of tile
-  // tile_base + b / 2 and stores the fp32 partial [2][tile_count][256][256] (plain products)
+  // GRP 0 K splits (lta_gemm4_bf16_ws / _splitk): this launch covers the linear tiles [tile_base,
+  // tile_base + tile_count) (kernel TAIL = 1 and 2); TAIL 2: workgroup b computes K slice b % ksplit of
+  // tile tile_base + b / ksplit and stores the fp32 partial [ksplit][tile_count][256][256] (plain products)
   int tile_base, tile_count, ksplit;
   float* partial;
 };
@@ -329,15 +329,20 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   const __hip_bfloat16* Bg = B;
   __hip_bfloat16* Cg = C;
   int Mlim = M, Kr = K, m0, n0;
-  [[maybe_unused]] int wg_lin = 0;
+  [[maybe_unused]] int wg_lin = 0, kpart = 0;
   if constexpr (GRP == 0) {
     // TAIL 0: every tile (the production instantiations keep exactly this code: a run-time tile
     // range here changed hipcc's schedule of the GELU + bias epilogue into wrong results);
     // 1: tiles [tile_base, tile_base + tile_count); 2: the K-split tail (ksplit == 2, the host's only
     // split: shifts keep the index scalar)
     int wg;
-    if constexpr (TAIL == 2)
-      wg = ep.tile_base + ((int)blockIdx.x >> 1);
+    if constexpr (TAIL == 2) {
+      // workgroup b: K slice b % ksplit of tile tile_base + b / ksplit (readfirstlane: the division's
+      // VALU sequence must not turn the tile / slice indices into per-lane values)
+      const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x / ep.ksplit);
+      kpart = __builtin_amdgcn_readfirstlane((int)blockIdx.x - t * ep.ksplit);
+      wg = ep.tile_base + t;
+    }
     else if constexpr (TAIL == 1)
       wg = ep.tile_base + xcd_tile((int)blockIdx.x, ep.tile_count);
     else
@@ -347,11 +352,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
     tile_coords(wg, nTm, nTn, tm, tn);
     m0 = tm * BM;
     n0 = tn * BN;
-    if constexpr (TAIL == 2) {  // this workgroup's K half (K % (4 BK) == 0, checked by the host)
-      const int kp = (int)blockIdx.x & 1;
-      Kr = K >> 1;
-      Ag = A + (AT ? (int64_t)kp * Kr * lda : (int64_t)kp * Kr);
-      Bg = B + (BT ? (int64_t)kp * Kr * ldb : (int64_t)kp * Kr);
+    if constexpr (TAIL == 2) {
+      // this workgroup's K slice: the K / 2 BK tile pairs dealt as evenly as possible over the ksplit
+      // slices (the first P % ksplit slices take one pair more; K % 2 BK == 0, P >= ksplit: host)
+      const int P = K / (2 * BK), q = __builtin_amdgcn_readfirstlane(P / ep.ksplit), r = P - q * ep.ksplit;
+      const int k0 = (kpart * q + min(kpart, r)) * (2 * BK);
+      Kr = (q + (kpart < r ? 1 : 0)) * (2 * BK);
+      Ag = A + (AT ? (int64_t)k0 * lda : (int64_t)k0);
+      Bg = B + (BT ? (int64_t)k0 * ldb : (int64_t)k0);
     }
   } else if constexpr (GRP == 1) {
     const int bid = (int)blockIdx.x, tn = bid % nTn;
@@ -492,9 +500,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  if constexpr (TAIL == 2) {  // tail split: the fp32 partial of this K half (summed by gemm4_tail_fixup)
+  if constexpr (TAIL == 2) {  // K split: the fp32 partial of this K slice (summed by gemm4_tail_fixup)
     static_assert(SW, "tail split: swapped layout");
-    float* P = ep.partial + ((int64_t)((int)blockIdx.x & 1) * ep.tile_count + (wg_lin - ep.tile_base)) * (BM * BN);
+    float* P = ep.partial + ((int64_t)kpart * ep.tile_count + (wg_lin - ep.tile_base)) * (BM * BN);
 #pragma unroll
     for (int m = 0; m < 8; ++m)
 #pragma unroll
@@ -926,6 +934,30 @@ int launch4_tail(const void* A, const void* B, void* C, int M, int N, int K, int
   return (int)hipGetLastError();
 }
 
+// Plain product whose whole tile grid is at most half a wave (wgrad / dgrad of narrow layers: e.g. the
+// 16 - 128 tiles of GPT-2-medium's d = 1024 GEMMs): ksplit K slices per tile fill the CUs, a fixup
+// sums the fp32 partials in a fixed order (deterministic).  K % 2 BK == 0; the slices differ by at most
+// one 2 BK pair.
+template <bool AT, bool BT>
+int launch4_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                   int ksplit, void* ws, int64_t ws_bytes, hipStream_t s) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (ksplit < 2 || ksplit > 64 || K % (2 * BK) || K / (2 * BK) < ksplit || !ws ||
+      ws_bytes < (int64_t)ksplit * nwg * BM * BN * 4)
+    return -2;
+  EpiArgs ep{};
+  ep.tile_base = 0;
+  ep.tile_count = nwg;
+  ep.ksplit = ksplit;
+  ep.partial = (float*)ws;
+  hipLaunchKernelGGL((gemm4_bf16_kernel<kNone, false, false, AT, BT, 1, 0, 0, 2>), dim3(ksplit * nwg), dim3(NTHR), 0,
+                     s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N,
+                     K, lda, ldb, ldc, 0, 1.f, ep);
+  hipLaunchKernelGGL(gemm4_tail_fixup, dim3((unsigned)((int64_t)nwg * (BM * BN / 8) / 256)), dim3(256), 0, s,
+                     (const float*)ws, (__hip_bfloat16*)C, ksplit, 0, nwg, M, N, ldc, alpha);
+  return (int)hipGetLastError();
+}
+
 template <int ACT, bool AT, bool BT, int VAR>
 int launch4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int lda,
             int ldb, int ldc, int ldr, float alpha, hipStream_t s) {
@@ -1002,6 +1034,20 @@ LTA_EXPORT int lta_gemm4_bf16_ws(const void* A, const void* B, void* C, const vo
     }
   }
   return lta_gemm4_bf16(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, variant, s);
+}
+
+// Plain product C = alpha * opA . opB split over K into ksplit slices (launch4_splitk); ws: fp32, >=
+// ksplit * tiles * 256 * 256 elements.  Same layouts / limits as lta_gemm4_bf16; -2 on a bad split.
+LTA_EXPORT int lta_gemm4_bf16_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                     int ldc, float alpha, int at, int bt, int ksplit, void* ws, int64_t ws_bytes,
+                                     hipStream_t s) {
+  if (N % 8 || M <= 0 || N <= 0 || K <= 0 || (at && M % 8)) return -2;
+  const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
+  if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
+  if (!at && !bt) return launch4_splitk<false, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  if (!at && bt) return launch4_splitk<false, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  if (at && !bt) return launch4_splitk<true, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  return launch4_splitk<true, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
 }
 
 // Grouped GEMMs for mixture-of-experts training (K10; reference nvFuser _grouped_mm forward and

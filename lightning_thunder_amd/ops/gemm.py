@@ -76,6 +76,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
 # ---------------------------------------------------------------------------------------------
 register_signature("lta_gemm4_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p])
+register_signature("lta_gemm4_bf16_splitk", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                             c_float, c_int, c_int, c_int, c_void_p, c_int64, c_void_p])
 register_signature("lta_gemm4_bf16_ws", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p, c_int64,
                                          c_void_p])
@@ -106,12 +108,43 @@ def _tail_workspace(M: int, N: int, K: int, device):
     tail = nwg % cus
     if nwg <= cus or tail == 0 or 2 * tail > cus:
         return None
-    # one cached fp32 workspace per (device, stream), grown to the largest tail seen: the partials are
-    # consumed by the fixup launched right behind the split on the same stream, so reuse is ordered
-    need = 2 * tail * 256 * 256
+    return _workspace(2 * tail * 256 * 256, device)
+
+
+# under-filled grids of plain products (at most half a wave of 256 x 256 tiles: the wgrad / dgrad of
+# narrow layers, e.g. GPT-2-medium's d = 1024) split K over ksplit slices + an fp32 fixup
+# (csrc/gemm4.hip launch4_splitk); LTA_GEMM_SPLITK=0 turns it off
+_SPLITK = _os.environ.get("LTA_GEMM_SPLITK", "1") != "0"
+# static cost model of the split (MI355X, profiles/gemm_splitk_gpt2.txt): a K-tile of a 256 x 256 tile
+# takes ~1.3 us, prologue + epilogue ~4.5 us; every slice writes and the fixup reads a 256 KiB fp32
+# partial per tile at ~5 TB/s; the fixup launch ~3 us
+_KT_US, _FIXED_US, _PARTIAL_US, _LAUNCH_US = 1.3, 4.5, 2 * 262144 / 5e6, 3.0
+
+
+def splitk_factor(M: int, N: int, K: int, cus: int) -> int:
+    """K slices per tile for a plain product (0: no split) whose grid is at most half a wave of
+    ``cus`` workgroups: the slice count (grid <= one wave, >= one 128-deep K pair per slice) the
+    cost model above rates fastest, if it beats the unsplit grid."""
+    if not _SPLITK or K % 128:
+        return 0
+    nwg = -(-M // 256) * -(-N // 256)
+    if 2 * nwg > cus:
+        return 0
+    pairs = K // 128
+    best, best_t = 0, 2 * pairs * _KT_US + _FIXED_US
+    for s in range(2, min(64, cus // nwg, pairs) + 1):
+        t = 2 * -(-pairs // s) * _KT_US + _FIXED_US + nwg * s * _PARTIAL_US + _LAUNCH_US
+        if t < best_t:
+            best, best_t = s, t
+    return best
+
+
+def _workspace(need: int, device):
+    """fp32 scratch of >= ``need`` elements: one cached buffer per (device, stream), grown to the largest
+    request (its consumer, the fixup, runs right behind the producer on the same stream, so reuse is
+    ordered); inside a graph capture a fresh allocation from the graph's pool (the graph keeps the
+    pointer, which a later, larger request must never replace)."""
     if torch.cuda.is_current_stream_capturing():
-        # a captured graph keeps the pointer: give it its own allocation (from the graph's pool), never
-        # one a later, larger tail could replace
         return torch.empty(need, dtype=torch.float32, device=device)
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
@@ -166,7 +199,17 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
         assert residual.shape == (M, N) and residual.stride(1) == 1 and residual.dtype == torch.bfloat16
     if bias is not None:
         assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
-    ws = _tail_workspace(M, N, K, a.device) if (bias is None and residual is None and act is None and variant == 1) else None
+    plain = bias is None and residual is None and act is None and variant == 1
+    ks = splitk_factor(M, N, K, _device_cus(a.device)) if plain else 0
+    if ks:
+        nwg = -(-M // 256) * -(-N // 256)
+        ws = _workspace(ks * nwg * 256 * 256, a.device)
+        rc = require().lta_gemm4_bf16_splitk(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
+                                             out.stride(0), alpha, at, bt, ks, ws.data_ptr(), ws.numel() * 4,
+                                             stream_ptr(a.device))
+        check(rc, "lta_gemm4_bf16_splitk")
+        return out
+    ws = _tail_workspace(M, N, K, a.device) if plain else None
     if ws is not None:
         rc = require().lta_gemm4_bf16_ws(a.data_ptr(), b.data_ptr(), out.data_ptr(), None, None, M, N, K, lda, ldb,
                                          out.stride(0), 0, alpha, ACT[act], at, bt, variant, ws.data_ptr(),

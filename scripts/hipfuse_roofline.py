@@ -1,9 +1,13 @@
 """Bandwidth roofline of the hipfuse-generated kernels of a GPT-2-medium training step.
 
 Runs one jitted NanoGPT gpt2-medium step (B=8, T=1024, bf16, dropout 0.1) with every hipFusion call
-recorded, then re-launches each distinct generated kernel on the inputs of its first call and
-times it with HIP events (median of 50).  Bytes = the storage actually addressed by every input
-(broadcast operands counted once) + every output; TB/s against the MI355X's ~8 TB/s HBM3E.
+recorded, then re-launches each distinct generated kernel on copies of the inputs of its first call.
+Timing: HIP events around a batch of back-to-back launches that rotate over k copies of every
+input / output storage (k x bytes >= 1.5 GB, so no launch finds its operands in the 256 MB
+Infinity Cache left by the previous one); per-launch time = batch / k, median of 7 batches.  (One
+event pair per launch, the round-4 method, adds the event / launch gap to every kernel: ~6 us on a
+15 us kernel.)  Bytes = the storage actually addressed by every input (broadcast operands counted
+once) + every output; TB/s against the MI355X's ~8 TB/s HBM3E.
 
     python scripts/hipfuse_roofline.py [--json gpurun_out/hipfuse_roofline.json]
 """
@@ -28,6 +32,13 @@ def _addressed_bytes(t: torch.Tensor) -> int:
         return 0
     n = 1 + sum((s - 1) * st for s, st in zip(t.shape, t.stride()) if st != 0)
     return min(n, t.numel()) * t.element_size()
+
+
+def _copy(t: torch.Tensor) -> torch.Tensor:
+    """A tensor with the same size / strides / offset over a copy of ``t``'s storage (broadcast and
+    sliced views keep their layout, index operands their in-range values)."""
+    st = t.untyped_storage().clone()
+    return torch.empty(0, dtype=t.dtype, device=t.device).set_(st, t.storage_offset(), t.size(), t.stride())
 
 
 def main():
@@ -74,21 +85,27 @@ def main():
         ks = r["ks"]
         nbytes = sum(_addressed_bytes(t) for t in r["tensors"]) + sum(_addressed_bytes(o) for o in r["outs"])
 
-        def go():
-            hipfuse.launch(ks, r["fns"], r["tensors"], list(r["outs"]), r["numbers"])
+        store = sum(t.untyped_storage().nbytes() for t in r["tensors"]) + \
+            sum(o.untyped_storage().nbytes() for o in r["outs"])
+        k = max(2, min(64, -(-int(1.5e9) // max(store, 1))))
+        sets = [([_copy(t) for t in r["tensors"]], [_copy(o) for o in r["outs"]]) for _ in range(k)]
 
-        for _ in range(5):
-            go()
+        def batch():
+            for ins, outs in sets:
+                hipfuse.launch(ks, r["fns"], ins, outs, r["numbers"])
+
+        batch()
         ts = []
-        for _ in range(50):
+        for _ in range(7):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            go()
+            batch()
             e1.record()
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e3)
+            ts.append(e0.elapsed_time(e1) * 1e3 / k)
         ts.sort()
         us = ts[len(ts) // 2]
+        del sets
         tbs = nbytes / (us * 1e-6) / 1e12
         rows.append(dict(kernel=name, mode=ks.mode, calls_per_step=r["calls"], us=round(us, 2),
                          mbytes=round(nbytes / 1e6, 2), tb_s=round(tbs, 2), pct_hbm=round(100 * tbs / HBM_TBS, 1),
