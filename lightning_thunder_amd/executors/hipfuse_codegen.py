@@ -736,14 +736,17 @@ __device__ __forceinline__ float bf2f(unsigned short x) { return __builtin_bit_c
 // half the VALU of the bit-twiddling form, two values per instruction when paired)
 __device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
 __device__ __forceinline__ float bfr(float f) { return (float)(__bf16)f; }
-// tanh for regions whose every output is a 16-bit float: odd Taylor series to x^9 for |x| < 0.4
-// (truncation < 4e-7 absolute), 1 - 2 / (e^2|x| + 1) above (fast exp / divide, ~1e-7 absolute);
-// ~1e-6 relative worst case, far inside bf16 / fp16 rounding, at a third of ocml tanhf's instructions
+// Regions whose every output is a 16-bit float (rounded to ~4e-3 relative on the way out) use the
+// hardware approximations (v_exp_f32 / v_rcp_f32, ~1 ulp of fp32) instead of the correctly rounded
+// library sequences (an IEEE divide alone is ~10 VALU instructions: div_scale x2, div_fmas, div_fixup).
+// e^x: the rounding of x log2(e) costs ~|x| 6e-8 relative (5e-6 at |x| = 80).
+__device__ __forceinline__ float fast_expf(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// tanh: 1 - 2 / (e^2x + 1) (-> +-1 at overflow / underflow of e^2x, NaN propagates); ~1.2e-7 absolute,
+// so below |x| = 2^-4 x (1 - x^2 / 3) (truncation 2 x^5 / 15: < 2e-6 relative) keeps the relative error
+// of tiny arguments
 __device__ __forceinline__ float fast_tanhf(float x) {
-  const float ax = fabsf(x), x2 = x * x;
-  const float p = x + x * x2 * (-0.33333333f + x2 * (0.13333333f + x2 * (-0.053968254f + x2 * 0.021869488f)));
-  const float t = 1.f - __fdividef(2.f, __expf(2.f * ax) + 1.f);
-  return ax < 0.4f ? p : copysignf(t, x);
+  const float t = __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(fast_expf(2.f * x) + 1.f), 1.f);
+  return fabsf(x) < 0.0625f ? x * __builtin_fmaf(x * x, -0.33333333f, 1.f) : t;
 }
 __device__ __forceinline__ float hfr(float f) { return (float)(_Float16)f; }
 template <class T> __device__ __forceinline__ T nmax(T a, T b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
@@ -1111,8 +1114,9 @@ class _Gen:
         tin = [a for _, a in tensor_args(b)]
         ict = _CTYPE[tin[0].dtype] if tin else ct
         if sid in _UNARY_FLOAT:
-            if sid == PrimIDs.TANH and ict == "float" and self.half_outputs:
-                return [(out.name, _rnd(out.dtype, f"fast_tanhf({R(0)})"))]
+            if sid in (PrimIDs.TANH, PrimIDs.EXP) and ict == "float" and self.half_outputs:
+                fn = "fast_tanhf" if sid == PrimIDs.TANH else "fast_expf"
+                return [(out.name, _rnd(out.dtype, f"{fn}({R(0)})"))]
             return [(out.name, _rnd(out.dtype, f"{_f(_UNARY_FLOAT[sid], ict)}({R(0)})"))]
         if sid in _UNARY_ANY:
             x = R(0, ict)
