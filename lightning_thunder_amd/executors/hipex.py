@@ -181,6 +181,158 @@ hip_fp8_delayed_update = ex.register_operator("hip_fp8_delayed_update", meta=lam
 hip_fp8_delayed_update.not_capturable = True  # may all-reduce over the data-parallel group
 
 
+def _fp8_cast_meta(t, e5m2, key=None, slot=None):
+    C = t.shape[-1]
+    R = 1
+    for d in t.shape[:-1]:
+        R *= d
+    return (TensorProxy(like=t, shape=(R, C), dtype=torch.uint8, requires_grad=False),
+            TensorProxy(like=t, shape=(), dtype=torch.float32, requires_grad=False))
+
+
+def _fp8_cast_impl(t, e5m2):
+    from ..ops.fp8 import quantize_rows
+
+    return quantize_rows(t, e5m2)
+
+
+def _fp8_cast_delayed_impl(t, e5m2, key, slot):
+    from ..ops.fp8 import quantize_delayed_rows
+
+    return quantize_delayed_rows(t, e5m2, key, slot)
+
+
+def _fp8_gemm_layout_meta(qa, qb, sa, sb, fmt_a, at, out_shape, residual=None):
+    return TensorProxy(like=qa, shape=tuple(out_shape), dtype=torch.bfloat16)
+
+
+def _fp8_gemm_layout_impl(qa, qb, sa, sb, fmt_a, at, out_shape, residual=None):
+    from ..ops.fp8 import gemm_fp8_layout
+
+    return gemm_fp8_layout(qa, qb, sa, sb, fmt_a, at, residual).reshape(out_shape)
+
+
+# row-major fp8 copies only: the backward GEMMs read the saved e4m3 activation / weight and the e5m2
+# gradient in place (MN-major operands through ds_read_b64_tr_b8, csrc/gemm4_fp8.hip), so no
+# transposed copy is ever written (LTA_FP8_TRANSPOSED=1: the cast_transpose path, A/B)
+hip_fp8_cast = ex.register_operator("hip_fp8_cast", meta=_fp8_cast_meta, fn=_fp8_cast_impl)
+hip_fp8_cast_delayed = ex.register_operator("hip_fp8_cast_delayed", meta=_fp8_cast_meta, fn=_fp8_cast_delayed_impl)
+hip_fp8_gemm_layout = ex.register_operator("hip_fp8_gemm_layout", meta=_fp8_gemm_layout_meta,
+                                           fn=_fp8_gemm_layout_impl)
+
+
+def _rms_fp8_meta(x, w, eps, key, slot):
+    q, sc = _fp8_cast_meta(x, False)
+    return q, sc, TensorProxy(like=x, shape=(q.shape[0],), dtype=torch.float32, requires_grad=False)
+
+
+def _rms_fp8_impl(x, w, eps, key, slot):
+    from ..ops.fp8 import rms_norm_fwd_fp8_delayed
+
+    return rms_norm_fwd_fp8_delayed(x, w, eps, key, slot)
+
+
+def _swiglu_fp8_impl(a, b, key, slot):
+    from ..ops.fp8 import swiglu_fwd_fp8_delayed
+
+    return swiglu_fwd_fp8_delayed(a, b, key, slot)
+
+
+def _swiglu_bwd_fp8_meta(g, a, b, key, slot_a, slot_b):
+    qa, sa = _fp8_cast_meta(a, True)
+    qb, sb = _fp8_cast_meta(b, True)
+    return qa, sa, qb, sb
+
+
+def _swiglu_bwd_fp8_impl(g, a, b, key, slot_a, slot_b):
+    from ..ops.fp8 import swiglu_bwd_fp8_delayed
+
+    return swiglu_bwd_fp8_delayed(g, a, b, key, slot_a, slot_b)
+
+
+hip_swiglu_bwd_fp8 = ex.register_operator("hip_swiglu_bwd_fp8", meta=_swiglu_bwd_fp8_meta, fn=_swiglu_bwd_fp8_impl)
+
+# producer-fused input casts of the fp8 linears (delayed scaling; _fuse_fp8_cast_producers)
+hip_rms_norm_fwd_fp8 = ex.register_operator("hip_rms_norm_fwd_fp8", meta=_rms_fp8_meta, fn=_rms_fp8_impl)
+hip_swiglu_fp8 = ex.register_operator("hip_swiglu_fp8", meta=lambda a, b, key, slot: _fp8_cast_meta(a, False),
+                                      fn=_swiglu_fp8_impl)
+
+
+def _fuse_fp8_cast_producers(trace):
+    """``y, rstd = hip_rms_norm_fwd(x, w, eps); q, s = hip_fp8_cast_delayed(y, False, key, slot)`` ->
+    ``q, s, rstd = hip_rms_norm_fwd_fp8(x, w, eps, key, slot)``, and ``y = hip_swiglu(a, b)`` + its
+    cast -> ``q, s = hip_swiglu_fp8(a, b, key, slot)`` when the cast is y's only use: the activation
+    leaves the producing kernel as e4m3 (no bf16 round trip, no separate cast launch).  Parity: the
+    reference's TransformerEngine layers quantise inside their fused norm / activation kernels
+    (thunder/executors/transformer_engineex_impl.py)."""
+    import os
+
+    from ..core.trace import from_trace, TraceProvenance
+
+    if os.environ.get("LTA_FP8_FUSE_PRODUCERS", "1") == "0":  # A/B hook
+        return trace
+    bsyms = trace.bound_symbols
+    uses: dict[str, int] = {}
+    for b in bsyms:
+        for a in b.flat_proxy_args:
+            uses[a.name] = uses.get(a.name, 0) + 1
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_fp8_cast_delayed or len(b.args) != 4 or b.args[1]:
+            continue
+        y, _, key, slot = b.args
+        j = producer.get(y.name)
+        if j is None or j in replace or j in drop or uses.get(y.name, 0) != 1:
+            continue
+        pb = bsyms[j]
+        if pb.sym is hip_rms_norm_fwd and len(pb.args) >= 3 and pb.args[1] is not None and pb.output[0].name == y.name:
+            nb = hip_rms_norm_fwd_fp8.bind(pb.args[0], pb.args[1], pb.args[2], key, slot,
+                                           output=(b.output[0], b.output[1], pb.output[1]))
+        elif pb.sym is hip_swiglu and len(pb.args) == 2:
+            nb = hip_swiglu_fp8.bind(pb.args[0], pb.args[1], key, slot, output=b.output)
+        else:
+            continue
+        replace[j] = ex.bind_call_ctx(nb)
+        drop.add(i)
+    # backward: da, db = hip_swiglu_bwd(g, a, b) whose only uses are their e5m2 casts
+    casts: dict[str, int] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is hip_fp8_cast_delayed and len(b.args) == 4 and b.args[1] and i not in drop:
+            casts[b.args[0].name] = i
+    for j, pb in enumerate(bsyms):
+        if pb.sym is not hip_swiglu_bwd or j in replace or len(pb.args) != 3:
+            continue
+        da, db = pb.output
+        ia, ib = casts.get(da.name), casts.get(db.name)
+        if ia is None or ib is None or uses.get(da.name, 0) != 1 or uses.get(db.name, 0) != 1:
+            continue
+        ca, cb = bsyms[ia], bsyms[ib]
+        if ca.args[2] != cb.args[2]:
+            continue
+        nb = hip_swiglu_bwd_fp8.bind(*pb.args, ca.args[2], ca.args[3], cb.args[3],
+                                     output=(ca.output[0], ca.output[1], cb.output[0], cb.output[1]))
+        replace[j] = ex.bind_call_ctx(nb)
+        drop.update((ia, ib))
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} fp8 input cast(s) fused into their producers"))
+    return new
+
+
+def _fp8_transposed() -> bool:
+    import os
+
+    return os.environ.get("LTA_FP8_TRANSPOSED", "0") == "1"
+
+
 def _mx_quant_meta(t, e5m2):
     C = t.shape[-1]
     R = 1
@@ -293,6 +445,12 @@ def _quant(t, e5m2, key, slot):
     return hip_fp8_quantize_delayed(t, e5m2, key, slot)
 
 
+def _cast(t, e5m2, key, slot):
+    if key is None:
+        return hip_fp8_cast(t, e5m2)
+    return hip_fp8_cast_delayed(t, e5m2, key, slot)
+
+
 def _fp8_vjp(x, w, bias=None, key=None, slots=None):
     from .. import torch as ltorch
 
@@ -301,9 +459,23 @@ def _fp8_vjp(x, w, bias=None, key=None, slots=None):
     if key == "mxfp4":
         return _mx4_vjp(x, w, bias)
     sl = slots or (None, None, None)
+    out_shape = tuple(x.shape[:-1]) + (w.shape[0],)
+    if not _fp8_transposed():
+        qx, sx = _cast(x, False, key, sl[0])
+        qw, sw = _cast(w, False, key, sl[1])
+        y = hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, out_shape)
+
+        def bwd_rows(g):
+            qg, sg = _cast(g, True, key, sl[2])
+            dx = hip_fp8_gemm_layout(qg, qw, sg, sw, 1, False, tuple(x.shape))  # dY [M, out] . W [out][in]
+            dw = hip_fp8_gemm_layout(qg, qx, sg, sx, 1, True, tuple(w.shape))   # dY^T . X, both [tokens][.]
+            if bias is None:
+                return dx, dw
+            return dx, dw, ltorch.sum(g, tuple(range(g.ndim - 1)))
+
+        return y, bwd_rows
     qx, qxT, sx = _quant(x, False, key, sl[0])
     qw, qwT, sw = _quant(w, False, key, sl[1])
-    out_shape = tuple(x.shape[:-1]) + (w.shape[0],)
     y = hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, out_shape)
 
     def bwd(g):
@@ -326,8 +498,8 @@ def _fp8_exec(x, w, bias=None, key=None, slots=None):
     if key == "mxfp4":
         return _mx4_fwd(x, w, bias)
     sl = slots or (None, None, None)
-    qx, _, sx = _quant(x, False, key, sl[0])
-    qw, _, sw = _quant(w, False, key, sl[1])
+    qx, sx = _cast(x, False, key, sl[0])
+    qw, sw = _cast(w, False, key, sl[1])
     return hip_fp8_gemm(qx, qw, sx, sw, 0, 0, bias, tuple(x.shape[:-1]) + (w.shape[0],))
 
 
@@ -367,11 +539,20 @@ def _fuse_linear_epilogues(trace):
         for pos in (0, 1):
             y, r = b.args[pos], b.args[1 - pos]
             j = producer.get(y.name)
-            if j is None or j in drop or bsyms[j].sym not in (hip_linear, hip_matmul, hip_fp8_gemm) or uses.get(y.name, 0) != 1:
+            if (j is None or j in drop or bsyms[j].sym not in (hip_linear, hip_matmul, hip_fp8_gemm, hip_fp8_gemm_layout)
+                    or uses.get(y.name, 0) != 1):
                 continue
             lb = bsyms[j]
             if tuple(r.shape) != tuple(y.shape) or r.dtype != y.dtype or tuple(b.output.shape) != tuple(y.shape):
                 continue
+            if lb.sym is hip_fp8_gemm_layout:
+                if lb.args[5] or (len(lb.args) > 7 and lb.args[7] is not None) or "residual" in lb.kwargs:
+                    continue  # the residual epilogue exists for the dgrad layout (A [M][K]) only
+                if producer.get(r.name, -1) > i or j in replace:
+                    continue
+                replace[i] = ex.bind_call_ctx(hip_fp8_gemm_layout.bind(*lb.args[:7], r, output=b.output))
+                drop.add(j)
+                break
             if lb.sym is hip_fp8_gemm:
                 if len(lb.args) > 8 and lb.args[8] is not None or "residual" in lb.kwargs:
                     continue
@@ -1075,7 +1256,7 @@ def _fuse_attn_bwd_rope(trace):
 
 def _post_claim(trace):
     return _fuse_attn_bwd_rope(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
-        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(trace))))))))
+        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(_fuse_fp8_cast_producers(trace)))))))))
 
 
 ex.post_claim_pass = _post_claim

@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "fp8_cvt.h"
 
 using namespace lta;
 
@@ -25,28 +26,6 @@ __device__ __forceinline__ uint8_t to_e4m3(float v) {
 __device__ __forceinline__ uint8_t to_e5m2(float v) {
   v = fminf(fmaxf(v, -57344.f), 57344.f);
   return (uint8_t)(__builtin_amdgcn_cvt_pk_bf8_f32(v, 0.f, 0, false) & 0xff);
-}
-
-// four saturated values -> one word of four OCP fp8 (e4m3fn or e5m2), two per conversion instruction
-template <bool E5M2>
-__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
-  const float mx = E5M2 ? 57344.f : 448.f;
-  a = __builtin_amdgcn_fmed3f(a, -mx, mx);
-  b = __builtin_amdgcn_fmed3f(b, -mx, mx);
-  c = __builtin_amdgcn_fmed3f(c, -mx, mx);
-  d = __builtin_amdgcn_fmed3f(d, -mx, mx);
-  if constexpr (E5M2) {
-    const int w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
-  } else {
-    const int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  }
-}
-
-__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
-  // |x| >= 0: IEEE order == unsigned int order
-  atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
 }
 
 // scale = fmax / amax_in (device scalar written by lta_amax); block 0 publishes it to scale_out
@@ -97,19 +76,30 @@ __global__ __launch_bounds__(256) void cast_kernel(const T* __restrict__ x, uint
                                                    float* __restrict__ scale_out, float* __restrict__ amax) {
   const float s = dev_scale(amax_in, fmax, scale_out);
   float m = 0.f;
-  const int64_t nv = n / 8;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nv = n / 8, stride = (int64_t)gridDim.x * blockDim.x;
+  // two 8-element vectors per thread and iteration (both loads issued before the first conversion),
+  // two elements per hardware conversion (cvt4)
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < nv; i += 2 * stride) {
+    float v[2][8];
+    load8(x + i * 8, v[0]);
+    load8(x + (i + stride) * 8, v[1]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[u][j]));
+      const uint32_t lo = cvt4<E5M2>(v[u][0] * s, v[u][1] * s, v[u][2] * s, v[u][3] * s);
+      const uint32_t hi = cvt4<E5M2>(v[u][4] * s, v[u][5] * s, v[u][6] * s, v[u][7] * s);
+      *reinterpret_cast<uint2*>(y + (i + u * stride) * 8) = make_uint2(lo, hi);
+    }
+  }
+  if (i < nv) {
     float v[8];
     load8(x + i * 8, v);
-    uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = v[j];
-      m = fmaxf(m, fabsf(f));
-      const uint32_t q = E5M2 ? to_e5m2(f * s) : to_e4m3(f * s);
-      if (j < 4) lo |= q << (8 * j);
-      else hi |= q << (8 * (j - 4));
-    }
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    const uint32_t lo = cvt4<E5M2>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    const uint32_t hi = cvt4<E5M2>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
     *reinterpret_cast<uint2*>(y + i * 8) = make_uint2(lo, hi);
   }
   if (amax != nullptr) {  // one atomic per workgroup

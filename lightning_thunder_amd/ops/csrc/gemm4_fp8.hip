@@ -17,6 +17,8 @@
 // so the DMA of a tile has a whole tile (2048 MFMA cycles) to land and every LDS read overlaps
 // MFMAs.  A fragment of the 16x16x128 operand is 32 B per lane: 16-B chunks g and 4 + g of its
 // 128-B row (g = lane >> 4); A and B use the same k assignment, so the sum over k is exact.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace lta;
@@ -63,6 +65,55 @@ struct StagerB {
   }
 };
 
+// MN-major operand (stored [K][M or N], the backward's dY / X / W read in place, no transposed copy):
+// the K-tile's image is 128 k-rows of 256 B (the tile's 256 M or N bytes), 16-B chunk c of k-row R at
+// slot c ^ swz(R), swz(R) = (R & 7) | ((R >> 4) & 1) << 3, so the transposed fragment reads below are
+// bank-conflict free.  Instruction i (0..7) of wave w fills k-rows 16 i + 4 w .. +3 (LDS bytes
+// [(4i + w) KiB, +1 KiB), lane-linear); bit 4 of the row is i & 1, so even and odd instructions use
+// two lane offsets.
+struct StagerT {
+  i32x4 rsrc;
+  int voff[2], ld;
+  __device__ __forceinline__ void init(const char* X, int ld_, int c0, int K, int wave, int lane) {
+    ld = ld_;
+    rsrc = make_rsrc(X + c0, K * ld);
+    const int ro = lane >> 4, slot = lane & 15, r = 4 * wave + ro;
+    voff[0] = r * ld + ((slot ^ (r & 7)) << 4);
+    voff[1] = (16 + r) * ld + ((slot ^ ((r & 7) | 8)) << 4);
+  }
+  __device__ __forceinline__ void issue(int i, int kt, char* img, int wave) const {
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(img + (i * 4 + wave) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(dst), "v"(voff[i & 1]), "s"(rsrc), "s"((kt * BKB + 32 * (i >> 1)) * ld)
+                 : "memory", "m0");
+  }
+};
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2i lds_v2i;
+
+// Lane base of the transposed fragment reads of an MN-major image (LDS byte address; XOR-ed with the
+// fragment's (stage, 16-column block) constant, see read_frag_t).  ds_read_b64_tr_b8 (probed:
+// scripts/exp/tr8_probe.py): per 16-lane group a block of 8 k-rows x 16 bytes, lane 2q + p giving the
+// address of row q, bytes 8p .. 8p + 7, lane i receiving column i of the 8 rows.  Lane (column fr,
+// group g) reads k-rows 16g + q (+8, +64, +72): the k order of the K-major fragment (chunks g, 4 + g).
+__device__ __forceinline__ uint32_t tr_base(uint32_t img, int wblock, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
+  return img + (uint32_t)((16 * g + q) * 256 + 8 * p + ((((wblock ^ (g & 1)) << 3) | q) << 4));
+}
+// fragment of the 16-column block `blk` (0..7 within the wave's 128 columns) from the image whose
+// stage / operand offset `xo` is XOR-ed into the lane base (bits 4..6 select the chunk, 15..16 the
+// image); four 8-byte transposed reads at k-row offsets 0, 8, 64, 72
+__device__ __forceinline__ v8i read_frag_t(uint32_t base, uint32_t xo) {
+  const uint32_t a = base ^ xo;
+  auto rd = [&](uint32_t off) {
+    return __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(uintptr_t)(a + off));
+  };
+  const v2i r0 = rd(0), r1 = rd(8 * 256), r2 = rd(64 * 256), r3 = rd(72 * 256);
+  return v8i{r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y};
+}
+
 __device__ __forceinline__ v8i read_frag8(const char* img, int row, int g) {
   const uint4 lo = *reinterpret_cast<const uint4*>(img + row * 128 + ((g ^ (row & 7)) << 4));
   const uint4 hi = *reinterpret_cast<const uint4*>(img + row * 128 + (((4 + g) ^ (row & 7)) << 4));
@@ -91,7 +142,9 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 // RES: C = bf16(bf16(A.B^T / (sa sb) + bias) + R) — the residual add of the unfused pair, with the
 // same two rounding points (the FP8 transformer block's residual stream and the dgrad sum of the
 // gate / up projections never take a separate elementwise pass).
-template <int FA, int FB, bool BIAS, bool RES = false>
+// AT / BT: operand A / B stored MN-major ([K][M] / [K][N], pitches lda / ldb in bytes), read through
+// transposed LDS reads; else K-major ([M][K] / [N][K]).
+template <int FA, int FB, bool BIAS, bool RES = false, bool AT = false, bool BT = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                            __hip_bfloat16* __restrict__ C,
                                                            const __hip_bfloat16* __restrict__ bias, int M, int N,
@@ -118,16 +171,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
   const int tm = first_m + in_group % gm, tn = in_group / gm;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  StagerB st_a, st_b;
+  std::conditional_t<AT, StagerT, StagerB> st_a;
+  std::conditional_t<BT, StagerT, StagerB> st_b;
   st_a.init(A, lda, m0, K, wave, lane);
   st_b.init(B, ldb, n0, K, wave, lane);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  [[maybe_unused]] const uint32_t tra = tr_base(lds0, wm, lane), trb = tr_base(lds0 + OP_BYTES, wn, lane);
+  // fragment m of A / n of B from stage S (0 / 1)
+  auto frag_a = [&](int S, int m) -> v8i {
+    if constexpr (AT)
+      return read_frag_t(tra, (uint32_t)(S * STAGE) | (uint32_t)(m << 4));
+    else
+      return read_frag8(smem + S * STAGE, wm * 128 + fr + m * 16, fg);
+  };
+  auto frag_b = [&](int S, int n) -> v8i {
+    if constexpr (BT)
+      return read_frag_t(trb, (uint32_t)(S * STAGE) | (uint32_t)(n << 4));
+    else
+      return read_frag8(smem + S * STAGE + OP_BYTES, wn * 128 + fr + n * 16, fg);
+  };
   auto glds = [&](int j, int kt, char* stage) {
     if (j < 8)
       st_a.issue(j, kt, stage, wave);
     else
       st_b.issue(j - 8, kt, stage + OP_BYTES, wave);
   };
-  const int arow = wm * 128 + fr, brow = wn * 128 + fr;
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -145,14 +213,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int m = 0; m < 8; ++m) fa[m] = read_frag8(smem, arow + m * 16, fg);
+  for (int m = 0; m < 8; ++m) fa[m] = frag_a(0, m);
 #pragma unroll
-  for (int n = 0; n < 8; ++n) fb[n] = read_frag8(smem + OP_BYTES, brow + n * 16, fg);
+  for (int n = 0; n < 8; ++n) fb[n] = frag_b(0, n);
 
   auto body = [&](int t, auto cur_c) {
     constexpr int CUR = decltype(cur_c)::value;
     char* const bc = smem + CUR * STAGE;
-    char* const bn = smem + (CUR ^ 1) * STAGE;
     const int t2 = min(t + 2, nk - 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -164,9 +231,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
       // 16 x 16 block, 4 consecutive C columns of one row per lane (register epilogue below)
       mfma8<FB, FA>(acc[m][n], fb[n], fa[m]);
       if (i < 32 && (i & 1) == 0) glds(i >> 1, t2, bc);
-      if (m >= 1 && n == 0) fa[m - 1] = read_frag8(bn, arow + (m - 1) * 16, fg);
-      if (m == 7) fb[n] = read_frag8(bn + OP_BYTES, brow + n * 16, fg);
-      if (i == 63) fa[7] = read_frag8(bn, arow + 7 * 16, fg);
+      if (m >= 1 && n == 0) fa[m - 1] = frag_a(CUR ^ 1, m - 1);
+      if (m == 7) fb[n] = frag_b(CUR ^ 1, n);
+      if (i == 63) fa[7] = frag_a(CUR ^ 1, 7);
       LTA_FENCE();
     }
   };
@@ -258,6 +325,33 @@ LTA_EXPORT int lta_gemm4_fp8(const void* A, const void* B, void* C, const void* 
   else if (fmt_a == 0 && fmt_b == 1) { if (bi) LTA_G8(0, 1, true); else LTA_G8(0, 1, false); }
   else return -1;
 #undef LTA_G8
+  return (int)hipGetLastError();
+}
+
+// Backward layouts without transposed fp8 copies: at = 1 reads A stored [K][M] (e.g. dY for the wgrad
+// dW = dY^T X), bt = 1 reads B stored [K][N] (W for the dgrad dX = dY W, X for the wgrad), both through
+// ds_read_b64_tr_b8.  C = (opA . opB) / (sa sb) (+ R, bt-only layout); (at, bt) in {(0,1), (1,1)};
+// formats as lta_gemm4_fp8 (0 e4m3, 1 e5m2; e5m2 on A only).  Pitches in bytes, multiples of 16.
+LTA_EXPORT int lta_gemm4_fp8_layout(const void* A, const void* B, void* C, const void* R, int M, int N, int K, int lda,
+                                    int ldb, int ldc, int ldr, int fmt_a, int fmt_b, int at, int bt, const void* sa,
+                                    const void* sb, hipStream_t stream) {
+  if (M % BM || N % BN || K % (2 * BKB) || M <= 0 || N <= 0 || lda % 16 || ldb % 16 || ldc % 8 || ldr % 8) return -2;
+  if (!bt || (at && R) || fmt_b != 0 || (fmt_a != 0 && fmt_a != 1)) return -1;
+  const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = (int64_t)K * ldb;
+  if (ea >= (1ll << 31) || eb >= (1ll << 31) || (at && lda < M) || ldb < N) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+#define LTA_G8L(FA, RE, AT_)                                                                                       \
+  hipLaunchKernelGGL((gemm4_fp8_kernel<FA, 0, false, RE, AT_, true>), grid, block, 0, stream, (const char*)A,      \
+                     (const char*)B, (__hip_bfloat16*)C, nullptr, M, N, K, lda, ldb, ldc, (const float*)sa,         \
+                     (const float*)sb, (const __hip_bfloat16*)R, ldr)
+  if (at) {
+    if (fmt_a == 0) LTA_G8L(0, false, true); else LTA_G8L(1, false, true);
+  } else if (R) {
+    if (fmt_a == 0) LTA_G8L(0, true, false); else LTA_G8L(1, true, false);
+  } else {
+    if (fmt_a == 0) LTA_G8L(0, false, false); else LTA_G8L(1, false, false);
+  }
+#undef LTA_G8L
   return (int)hipGetLastError();
 }
 

@@ -7,8 +7,11 @@
 // row is read from HBM once.  The backward processes several rows per workgroup and keeps
 // the per-column dW partial sums in registers, writing one fp32 partial row per workgroup;
 // a second kernel reduces the partials (no float atomics: deterministic).
+#include <algorithm>
+
 #include "common.h"
 #include "colreduce.h"
+#include "fp8_cvt.h"
 
 using namespace lta;
 
@@ -59,6 +62,63 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(const T* __restri
       store16(yr + idx, o);
     }
   }
+}
+
+// FP8-linear producer (delayed scaling): the normalised row leaves as e4m3 (q = fp8(bf16(y) s),
+// s = fmax / amax_in) instead of bf16 -- the input cast of the following fp8 linears fused into the
+// norm (one pass less over the activation); max |bf16(y)| of the whole tensor into amax_out.  A
+// capped grid strides over the rows (one amax atomic per workgroup).
+template <typename T, int CHUNKS>
+__global__ __launch_bounds__(kThreads) void rmsnorm_fwd_fp8_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                                   uint8_t* __restrict__ q, float* __restrict__ rstd_out,
+                                                                   int64_t rows, int cols, float eps,
+                                                                   const float* __restrict__ amax_in, float fmax,
+                                                                   float* __restrict__ scale_out,
+                                                                   float* __restrict__ amax_out) {
+  constexpr int V = Vec16<T>::N;
+  static_assert(V == 8, "16-bit inputs");
+  __shared__ float smem[kWaves];
+  __shared__ float red[kWaves];
+  const float s = fp8_scale(amax_in, fmax, scale_out);
+  float m = 0.f;
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const T* xr = x + row * cols;
+    Vec16<T> xv[CHUNKS];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+      const int idx = (c * kThreads + threadIdx.x) * V;
+      if (idx < cols) {
+        xv[c] = load16(xr + idx);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float f = to_f32(xv[c].v[j]);
+          ss += f * f;
+        }
+      }
+    }
+    const float total = block_sum<kWaves>(ss, smem);
+    const float r = rsqrtf(total / (float)cols + eps);
+    if (threadIdx.x == 0 && rstd_out != nullptr) rstd_out[row] = r;
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+      const int idx = (c * kThreads + threadIdx.x) * V;
+      if (idx < cols) {
+        float yv[V];
+        const Vec16<T> wv = load16(w + idx);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          yv[j] = to_f32(from_f32<T>(to_f32(xv[c].v[j]) * r * to_f32(wv.v[j])));  // the unfused bf16 y
+          m = fmaxf(m, fabsf(yv[j]));
+        }
+        const uint32_t lo = cvt4<false>(yv[0] * s, yv[1] * s, yv[2] * s, yv[3] * s);
+        const uint32_t hi = cvt4<false>(yv[4] * s, yv[5] * s, yv[6] * s, yv[7] * s);
+        *reinterpret_cast<uint2*>(q + row * cols + idx) = make_uint2(lo, hi);
+      }
+    }
+    __syncthreads();  // smem is reused by the next row's block_sum
+  }
+  if (amax_out != nullptr) fp8_amax_out<kWaves>(m, amax_out, red);
 }
 
 // Generic (any cols) fallback: strided scalar loops, two passes over the row.
@@ -333,6 +393,35 @@ LTA_EXPORT int lta_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y,
     case kF32: return launch_fwd<float>(x, w, y, rstd, rows, (int)cols, eps, stream);
   }
   return -1;
+}
+
+// RMSNorm forward with an e4m3 output (rmsnorm_fwd_fp8_kernel): q [rows, cols] uint8, rstd fp32; the
+// delayed-scaling scale fmax / *amax_in goes to scale_out, max |y| into amax_out.  16-bit x / w,
+// cols % 8 == 0, cols <= 16384, 16-B aligned.  -1 when unsupported.
+LTA_EXPORT int lta_rmsnorm_fwd_fp8(int dtype, const void* x, const void* w, void* q, void* rstd, int64_t rows,
+                                   int64_t cols, float eps, const void* amax_in, float fmax, void* scale_out,
+                                   void* amax_out, hipStream_t stream) {
+  const int per_pass = kThreads * 8, chunks = (int)((cols + per_pass - 1) / per_pass);
+  if (!w || cols % 8 || chunks > 8 || ((uintptr_t)x % 16) || ((uintptr_t)w % 16) || ((uintptr_t)q % 8)) return -1;
+  dim3 grid((unsigned)std::min<int64_t>(rows, 1024)), block(kThreads);
+#define LTA_Q8(T, C)                                                                                              \
+  hipLaunchKernelGGL((rmsnorm_fwd_fp8_kernel<T, C>), grid, block, 0, stream, (const T*)x, (const T*)w, (uint8_t*)q, \
+                     (float*)rstd, rows, (int)cols, eps, (const float*)amax_in, fmax, (float*)scale_out,          \
+                     (float*)amax_out)
+#define LTA_Q8_T(T)                                                                                               \
+  switch (chunks) {                                                                                               \
+    case 1: LTA_Q8(T, 1); break;                                                                                  \
+    case 2: LTA_Q8(T, 2); break;                                                                                  \
+    case 3: LTA_Q8(T, 3); break;                                                                                  \
+    case 4: LTA_Q8(T, 4); break;                                                                                  \
+    default: LTA_Q8(T, 8); break;                                                                                 \
+  }
+  if (dtype == kBF16) { LTA_Q8_T(__hip_bfloat16) }
+  else if (dtype == kF16) { LTA_Q8_T(__half) }
+  else return -1;
+#undef LTA_Q8_T
+#undef LTA_Q8
+  return (int)hipGetLastError();
 }
 
 // res (optional, same shape as dx): added to dx in the same pass (the residual stream's gradient)

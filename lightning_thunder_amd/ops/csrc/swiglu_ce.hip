@@ -8,7 +8,10 @@
 // max/sum-exp pass per row (logits read once), saving the row's log-sum-exp; backward
 // writes (softmax - onehot) * dloss / n_valid in one pass.  Rows are [tokens, vocab]
 // with vocab = 32000 for Llama-2 (64 KB of bf16 per row).
+#include <algorithm>
+
 #include "common.h"
+#include "fp8_cvt.h"
 
 using namespace lta;
 
@@ -36,6 +39,75 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ a
     const float x = to_f32(a[i]);
     y[i] = from_f32<T>(x * sigmoidf_(x) * to_f32(b[i]));
   }
+}
+
+// FP8-linear producer (delayed scaling): y = silu(a) b leaves as e4m3 (q = fp8(bf16(y) s), s = fmax /
+// amax_in) -- the down projection's input cast fused into the SwiGLU pass; max |bf16(y)| into
+// amax_out, one atomic per workgroup of a capped grid.
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_fp8_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                             uint8_t* __restrict__ q, int64_t n,
+                                                             const float* __restrict__ amax_in, float fmax,
+                                                             float* __restrict__ scale_out,
+                                                             float* __restrict__ amax_out) {
+  static_assert(Vec16<T>::N == 8, "16-bit inputs");
+  __shared__ float red[4];
+  const float s = fp8_scale(amax_in, fmax, scale_out);
+  float m = 0.f;
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const Vec16<T> av = load16(a + i * 8), bv = load16(b + i * 8);
+    float y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = to_f32(av.v[j]);
+      y[j] = to_f32(from_f32<T>(x * sigmoidf_(x) * to_f32(bv.v[j])));  // the unfused bf16 y
+      m = fmaxf(m, fabsf(y[j]));
+    }
+    const uint32_t lo = cvt4<false>(y[0] * s, y[1] * s, y[2] * s, y[3] * s);
+    const uint32_t hi = cvt4<false>(y[4] * s, y[5] * s, y[6] * s, y[7] * s);
+    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(lo, hi);
+  }
+  if (amax_out != nullptr) fp8_amax_out<4>(m, amax_out, red);
+}
+
+// FP8-linear producer, backward (delayed scaling): da / db leave as e5m2 (the fc_1 / fc_2 output
+// gradients the fp8 dgrad / wgrad GEMMs read), each with its own scale (fmax / amax_in_x) and amax;
+// the values are the unfused kernel's bf16 da / db.
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_fp8_kernel(const T* __restrict__ g, const T* __restrict__ a,
+                                                             const T* __restrict__ b, uint8_t* __restrict__ qa,
+                                                             uint8_t* __restrict__ qb, int64_t n,
+                                                             const float* __restrict__ amax_in_a,
+                                                             const float* __restrict__ amax_in_b, float fmax,
+                                                             float* __restrict__ scale_a, float* __restrict__ scale_b,
+                                                             float* __restrict__ amax_a, float* __restrict__ amax_b) {
+  static_assert(Vec16<T>::N == 8, "16-bit inputs");
+  __shared__ float red[4];
+  const float sa = fp8_scale(amax_in_a, fmax, scale_a), sb = fp8_scale(amax_in_b, fmax, scale_b);
+  float ma = 0.f, mb = 0.f;
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const Vec16<T> gv = load16(g + i * 8), av = load16(a + i * 8), bv = load16(b + i * 8);
+    float ya[8], yb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = to_f32(av.v[j]), gg = to_f32(gv.v[j]), bb = to_f32(bv.v[j]);
+      const float s = sigmoidf_(x);
+      const float silu = x * s;
+      ya[j] = to_f32(from_f32<T>(gg * bb * (s * (1.f + x * (1.f - s)))));
+      yb[j] = to_f32(from_f32<T>(gg * silu));
+      ma = fmaxf(ma, fabsf(ya[j]));
+      mb = fmaxf(mb, fabsf(yb[j]));
+    }
+    *reinterpret_cast<uint2*>(qa + i * 8) = make_uint2(cvt4<true>(ya[0] * sa, ya[1] * sa, ya[2] * sa, ya[3] * sa),
+                                                       cvt4<true>(ya[4] * sa, ya[5] * sa, ya[6] * sa, ya[7] * sa));
+    *reinterpret_cast<uint2*>(qb + i * 8) = make_uint2(cvt4<true>(yb[0] * sb, yb[1] * sb, yb[2] * sb, yb[3] * sb),
+                                                       cvt4<true>(yb[4] * sb, yb[5] * sb, yb[6] * sb, yb[7] * sb));
+  }
+  if (amax_a != nullptr) fp8_amax_out<4>(ma, amax_a, red);
+  __syncthreads();
+  if (amax_b != nullptr) fp8_amax_out<4>(mb, amax_b, red);
 }
 
 template <typename T>
@@ -247,6 +319,42 @@ __global__ __launch_bounds__(kCeThreads) void ce_bwd_kernel(const T* __restrict_
 LTA_EXPORT int lta_swiglu_fwd(int dtype, const void* a, const void* b, void* y, int64_t n, hipStream_t stream) {
   LTA_DISPATCH_T(dtype, hipLaunchKernelGGL((swiglu_fwd_kernel<T>), dim3(ew_grid(n / Vec16<T>::N + 1)), dim3(256), 0,
                                            stream, (const T*)a, (const T*)b, (T*)y, n));
+  return (int)hipGetLastError();
+}
+
+// SwiGLU forward with an e4m3 output (swiglu_fwd_fp8_kernel); n % 8 == 0, 16-bit a / b.
+LTA_EXPORT int lta_swiglu_fwd_fp8(int dtype, const void* a, const void* b, void* q, int64_t n, const void* amax_in,
+                                  float fmax, void* scale_out, void* amax_out, hipStream_t stream) {
+  if (n % 8 || ((uintptr_t)a % 16) || ((uintptr_t)b % 16) || ((uintptr_t)q % 8)) return -1;
+  const dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 1024)), block(256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL((swiglu_fwd_fp8_kernel<__hip_bfloat16>), grid, block, 0, stream, (const __hip_bfloat16*)a,
+                       (const __hip_bfloat16*)b, (uint8_t*)q, n, (const float*)amax_in, fmax, (float*)scale_out,
+                       (float*)amax_out);
+  else if (dtype == kF16)
+    hipLaunchKernelGGL((swiglu_fwd_fp8_kernel<__half>), grid, block, 0, stream, (const __half*)a, (const __half*)b,
+                       (uint8_t*)q, n, (const float*)amax_in, fmax, (float*)scale_out, (float*)amax_out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// SwiGLU backward with e5m2 outputs (swiglu_bwd_fp8_kernel); n % 8 == 0, 16-bit g / a / b.
+LTA_EXPORT int lta_swiglu_bwd_fp8(int dtype, const void* g, const void* a, const void* b, void* qa, void* qb,
+                                  int64_t n, const void* amax_in_a, const void* amax_in_b, float fmax, void* scale_a,
+                                  void* scale_b, void* amax_a, void* amax_b, hipStream_t stream) {
+  if (n % 8 || ((uintptr_t)g % 16) || ((uintptr_t)a % 16) || ((uintptr_t)b % 16) || ((uintptr_t)qa % 8) ||
+      ((uintptr_t)qb % 8))
+    return -1;
+  const dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 1024)), block(256);
+#define LTA_SB8(T)                                                                                                 \
+  hipLaunchKernelGGL((swiglu_bwd_fp8_kernel<T>), grid, block, 0, stream, (const T*)g, (const T*)a, (const T*)b,     \
+                     (uint8_t*)qa, (uint8_t*)qb, n, (const float*)amax_in_a, (const float*)amax_in_b, fmax,         \
+                     (float*)scale_a, (float*)scale_b, (float*)amax_a, (float*)amax_b)
+  if (dtype == kBF16) LTA_SB8(__hip_bfloat16);
+  else if (dtype == kF16) LTA_SB8(__half);
+  else return -1;
+#undef LTA_SB8
   return (int)hipGetLastError();
 }
 

@@ -118,6 +118,41 @@ def grouped_mm_fp8(qa: torch.Tensor, qw: torch.Tensor, sa: torch.Tensor, sw: tor
     return out
 
 
+register_signature("lta_gemm4_fp8_layout", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                             c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p])
+
+
+def gemm_fp8_layout(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, fmt_a: int, at: bool,
+                    residual: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 C = (opA . opB) / (sa sb) (+ residual) reading the backward's operands where they are,
+    without transposed fp8 copies: B is stored [K][N] (the weight [out][in] for the dgrad, the saved
+    activation [tokens][in] for the wgrad); A is [M][K] (``at`` False: dY for the dgrad) or stored
+    [K][M] (``at`` True: dY [tokens][out] for the wgrad).  fp8 as uint8, scales device scalars."""
+    K, N = b.shape
+    M = a.shape[1] if at else a.shape[0]
+    assert (a.shape[0] if at else a.shape[1]) == K and a.stride(1) == 1 and b.stride(1) == 1
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    r2 = None
+    if residual is not None:
+        r2 = residual.reshape(M, N)
+        assert not at and r2.dtype == torch.bfloat16 and r2.stride(1) == 1
+    check(require().lta_gemm4_fp8_layout(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                         None if r2 is None else r2.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                         out.stride(0), 0 if r2 is None else r2.stride(0), fmt_a, 0, int(at), 1,
+                                         sa.data_ptr(), sb.data_ptr(), stream_ptr(a.device)), "lta_gemm4_fp8_layout")
+    return out
+
+
+def quantize_rows(t: torch.Tensor, e5m2: bool = False):
+    """t (any shape, last dim C) -> (q [R, C], scale): per-tensor current scaling, row-major copy only
+    (the backward GEMMs read it in place through transposed LDS reads)."""
+    t2 = t.reshape(-1, t.shape[-1])
+    st = torch.zeros(2, dtype=torch.float32, device=t.device)  # amax, scale
+    amax_into(t2, st[0])
+    q = cast(t2, st[0], E5M2_MAX if e5m2 else E4M3_MAX, st[1], e5m2=e5m2)
+    return q, st[1]
+
+
 def fp8_linear_supported(M: int, N: int, K: int) -> bool:
     return M % 256 == 0 and N % 256 == 0 and K % 256 == 0
 
@@ -295,6 +330,35 @@ def quantize_delayed(t: torch.Tensor, e5m2: bool, key: int, slot: int):
     return q, qT, scale
 
 
+def delayed_scaling_source(t2: torch.Tensor, e5m2: bool, key: int, slot: int):
+    """(amax source tensor, fmax, fresh scale scalar, amax sink) of a delayed-scaling quantisation of
+    the 2-D ``t2`` in ``slot`` -- the bookkeeping of :func:`quantize_delayed`, for kernels that cast
+    as a side output of their own pass (row casts, producer-fused casts)."""
+    st = _DELAYED[key]
+    st.ensure(t2.device)
+    fmax = (E5M2_MAX if e5m2 else E4M3_MAX) * 2.0 ** -st.recipe.margin
+    scale = torch.empty((), dtype=torch.float32, device=t2.device)
+    if st.step_seen[slot] != st.updates:
+        st.step_seen[slot] = st.updates
+        if st.seen[slot]:
+            st.step_src[slot] = st.hmax[slot]
+        else:
+            st.seen[slot] = True
+            amax_in = st.step_amax[slot]
+            amax_in.zero_()
+            amax_into(t2, amax_in)
+            st.step_src[slot] = amax_in
+    return st.step_src[slot], fmax, scale, st.cur[slot]
+
+
+def quantize_delayed_rows(t: torch.Tensor, e5m2: bool, key: int, slot: int):
+    """As :func:`quantize_delayed` without the transposed copy: (q [R, C], scale)."""
+    t2 = t.reshape(-1, t.shape[-1])
+    amax_in, fmax, scale, sink = delayed_scaling_source(t2, e5m2, key, slot)
+    q = cast(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=sink)
+    return q, scale
+
+
 # ---------------------------------------------------------------------------------------------
 # MXFP8 block scaling (reference: TE ``MXFP8BlockScaling``; CDNA4 runs it natively on
 # v_mfma_scale_f32_16x16x128_f8f6f4 with per-32-element E8M0 scales)
@@ -380,3 +444,91 @@ def mfma_scale_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: tor
     check(require().lta_fp8_mfma_scale_probe(a.data_ptr(), b.data_ptr(), sa.data_ptr(), sb.data_ptr(), c.data_ptr(),
                                              stream_ptr(a.device)), "lta_fp8_mfma_scale_probe")
     return c
+
+
+# ---------------------------------------------------------------------------------------------
+# Producer-fused input casts (delayed scaling): the RMSNorm / SwiGLU forward kernels emit the e4m3
+# copy the following fp8 linear reads, instead of a bf16 activation plus a separate cast pass
+# (csrc/rmsnorm.hip rmsnorm_fwd_fp8_kernel, csrc/swiglu_ce.hip swiglu_fwd_fp8_kernel).  A slot's first
+# quantisation (no amax history yet: current scaling of the tensor itself) takes the unfused path.
+# ---------------------------------------------------------------------------------------------
+register_signature("lta_rmsnorm_fwd_fp8", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_float,
+                                           c_void_p, c_float, c_void_p, c_void_p, c_void_p])
+register_signature("lta_swiglu_fwd_fp8", [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_void_p,
+                                          c_void_p, c_void_p])
+
+
+def _first_use(key: int, slot: int, device) -> bool:
+    st = _DELAYED[key]
+    st.ensure(device)
+    return not st.seen[slot]
+
+
+def rms_norm_fwd_fp8_delayed(x: torch.Tensor, w: torch.Tensor, eps: float, key: int, slot: int):
+    """(q [R, C] e4m3 as uint8, scale, rstd [R]) of rms_norm(x, w) quantised in ``slot``."""
+    from .rmsnorm import rms_norm_fwd
+
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    if not _first_use(key, slot, x.device):
+        amax_in, fmax, scale, sink = delayed_scaling_source(x2, False, key, slot)
+        q = torch.empty(x2.shape, dtype=torch.uint8, device=x.device)
+        rstd = torch.empty(x2.shape[0], dtype=torch.float32, device=x.device)
+        rc = require().lta_rmsnorm_fwd_fp8(DTYPE_CODE[x2.dtype], x2.data_ptr(), w.contiguous().data_ptr(), q.data_ptr(),
+                                           rstd.data_ptr(), x2.shape[0], C, float(eps), amax_in.data_ptr(), fmax,
+                                           scale.data_ptr(), sink.data_ptr(), stream_ptr(x.device))
+        if rc == 0:
+            return q, scale, rstd
+        if rc != -1:
+            check(rc, "lta_rmsnorm_fwd_fp8")
+    y, rstd = rms_norm_fwd(x2, w, eps)
+    q, scale = quantize_delayed_rows(y, False, key, slot)
+    return q, scale, rstd
+
+
+def swiglu_fwd_fp8_delayed(a: torch.Tensor, b: torch.Tensor, key: int, slot: int):
+    """(q [R, C] e4m3 as uint8, scale) of silu(a) * b quantised in ``slot``."""
+    from .fused import swiglu_fwd
+
+    C = a.shape[-1]
+    if not _first_use(key, slot, a.device) and a.is_contiguous() and b.is_contiguous():
+        amax_in, fmax, scale, sink = delayed_scaling_source(a.reshape(-1, C), False, key, slot)
+        q = torch.empty((a.numel() // C, C), dtype=torch.uint8, device=a.device)
+        rc = require().lta_swiglu_fwd_fp8(DTYPE_CODE[a.dtype], a.data_ptr(), b.data_ptr(), q.data_ptr(), a.numel(),
+                                          amax_in.data_ptr(), fmax, scale.data_ptr(), sink.data_ptr(),
+                                          stream_ptr(a.device))
+        if rc == 0:
+            return q, scale
+        if rc != -1:
+            check(rc, "lta_swiglu_fwd_fp8")
+    return quantize_delayed_rows(swiglu_fwd(a, b), False, key, slot)
+
+
+register_signature("lta_swiglu_bwd_fp8", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                          c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+
+
+def swiglu_bwd_fp8_delayed(g: torch.Tensor, a: torch.Tensor, b: torch.Tensor, key: int, slot_a: int, slot_b: int):
+    """(qa, sa, qb, sb): the SwiGLU input gradients da / db as e5m2 copies quantised in their slots."""
+    from .fused import swiglu_bwd
+
+    C = a.shape[-1]
+    if (not _first_use(key, slot_a, a.device) and not _first_use(key, slot_b, a.device) and g.is_contiguous()
+            and a.is_contiguous() and b.is_contiguous()):
+        ia, fmax, sa, ka = delayed_scaling_source(a.reshape(-1, C), True, key, slot_a)
+        ib, _, sb, kb = delayed_scaling_source(a.reshape(-1, C), True, key, slot_b)
+        qa = torch.empty((a.numel() // C, C), dtype=torch.uint8, device=a.device)
+        qb = torch.empty_like(qa)
+        rc = require().lta_swiglu_bwd_fp8(DTYPE_CODE[a.dtype], g.data_ptr(), a.data_ptr(), b.data_ptr(), qa.data_ptr(),
+                                          qb.data_ptr(), a.numel(), ia.data_ptr(), ib.data_ptr(), fmax, sa.data_ptr(),
+                                          sb.data_ptr(), ka.data_ptr(), kb.data_ptr(), stream_ptr(a.device))
+        if rc == 0:
+            return qa, sa, qb, sb
+        if rc != -1:
+            check(rc, "lta_swiglu_bwd_fp8")
+    da, db = swiglu_bwd(g, a, b)
+    qa, sa = quantize_delayed_rows(da, True, key, slot_a)
+    qb, sb = quantize_delayed_rows(db, True, key, slot_b)
+    return qa, sa, qb, sb

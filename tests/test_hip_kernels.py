@@ -529,6 +529,112 @@ def test_mxfp4_training_recipe():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(512, 768, 1024), (256, 256, 512), (1024, 512, 256)])
+@pytest.mark.parametrize("fmt_a", [0, 1])
+def test_fp8_gemm_mn_major_layouts(M, N, K, fmt_a):
+    """The backward fp8 GEMMs read MN-major operands in place (ds_read_b64_tr_b8 fragments):
+    dgrad C = A [M][K] . B stored [K][N] (+ residual), wgrad C = A stored [K][M] . B stored [K][N];
+    vs the fp32 product of the dequantised operands."""
+    from lightning_thunder_amd.ops.fp8 import gemm_fp8_layout
+
+    torch.manual_seed(0)
+    fa = torch.float8_e5m2 if fmt_a else torch.float8_e4m3fn
+
+    def q(shape, f):
+        return (torch.randn(shape, device="cuda") * 2).to(f).view(torch.uint8)
+
+    sa = torch.tensor(0.5, device="cuda")
+    sb = torch.tensor(2.0, device="cuda")
+    b = q((K, N), torch.float8_e4m3fn)
+    bd = b.view(torch.float8_e4m3fn).float()
+    for at in (False, True):
+        a = q((K, M) if at else (M, K), fa)
+        ad = a.view(fa).float()
+        ref = ((ad.t() if at else ad) @ bd) / (0.5 * 2.0)
+        out = gemm_fp8_layout(a, b, sa, sb, fmt_a, at)
+        err = ((out.float() - ref).norm() / ref.norm()).item()
+        assert err < 5e-3, (at, err)
+        if not at:
+            r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+            out_r = gemm_fp8_layout(a, b, sa, sb, fmt_a, at, residual=r)
+            torch.testing.assert_close(out_r.float(), (out.float() + r.float()), atol=0.06, rtol=0.02)
+
+
+@pytest.mark.gpu
+def test_fp8_rows_path_matches_transposed_path(monkeypatch):
+    """The default FP8 linear backward (row-major casts, MN-major GEMM reads) against the
+    cast_transpose path (LTA_FP8_TRANSPOSED=1): same fp8 values, same products up to fp32 summation
+    order."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 768), torch.nn.Linear(768, 256)).cuda().bfloat16()
+    x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(2, 256, 256, device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("LTA_FP8_TRANSPOSED", mode)
+        jm = thunder.jit(m, transforms=[FP8LinearTransform()])
+        out = jm(x)
+        res[mode] = (out,) + torch.autograd.grad(out, (x, m[0].weight, m[1].weight), g)
+        bw = str(thunder.last_backward_traces(jm)[-1])
+        assert ("hip_fp8_gemm_layout" in bw) == (mode == "0"), bw
+    for a, b in zip(res["0"], res["1"]):
+        err = ((a.float() - b.float()).norm() / b.float().norm()).item()
+        assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+def test_fp8_producer_fused_casts_match_unfused(monkeypatch):
+    """Delayed-scaling FP8 block (RMSNorm -> fc_1 / fc_2 -> SwiGLU -> proj): the RMSNorm and SwiGLU
+    forward kernels emit the e4m3 input of the next linears themselves (hip_rms_norm_fwd_fp8 /
+    hip_swiglu_fp8, no bf16 activation, no cast launch); losses and gradients over three steps (the
+    first on current scaling, then on the amax history) are bit-identical to the unfused program."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.litgpt import swiglu
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    class Block(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.norm = torch.nn.RMSNorm(512, eps=1e-5)
+            self.fc_1 = torch.nn.Linear(512, 768, bias=False)
+            self.fc_2 = torch.nn.Linear(512, 768, bias=False)
+            self.proj = torch.nn.Linear(768, 512, bias=False)
+
+        def forward(self, x):
+            h = self.norm(x)
+            return x + self.proj(swiglu(self.fc_1(h), self.fc_2(h)))
+
+    torch.manual_seed(0)
+    m = Block().cuda().bfloat16()
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("LTA_FP8_FUSE_PRODUCERS", fuse)
+        t = FP8LinearTransform(recipe=DelayedScaling(amax_history_len=4))
+        jm = thunder.jit(m, transforms=[t])
+        outs = []
+        for step in range(3):
+            x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16,
+                            generator=torch.Generator("cuda").manual_seed(step))
+            loss = (jm(x).float() ** 2).mean()
+            grads = torch.autograd.grad(loss, list(m.parameters()))
+            outs.append((loss.detach(),) + tuple(grads))
+        fw = str(thunder.last_traces(jm)[-1])
+        bw = str(thunder.last_backward_traces(jm)[-1])
+        if fuse == "1":
+            assert "hip_rms_norm_fwd_fp8" in fw and "hip_swiglu_fp8" in fw, fw
+            assert fw.count("hip_fp8_cast_delayed") == 3, fw  # only the three weights are cast separately
+            assert "hip_swiglu_bwd_fp8" in bw, bw  # fc_1 / fc_2 output gradients leave the kernel as e5m2
+        res[fuse] = outs
+    for a, b in zip(res["1"], res["0"]):
+        for u, v in zip(a, b):
+            torch.testing.assert_close(u, v, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
 def test_fp8_delayed_scaling_training():
     """DelayedScaling recipe: scales come from the amax history of earlier steps (recorded while
     casting); results stay close to bf16 over several steps, siblings share the x slot, and the
@@ -557,7 +663,8 @@ def test_fp8_delayed_scaling_training():
     assert t.n_converted == 2 and st.n == 6 and st.updates == 3 and all(st.seen)  # the first forward has no history yet
     torch.testing.assert_close(st.hmax[1], m[0].weight.detach().abs().max().float())
     fw = str(thunder.last_traces(jm)[-1])
-    assert "hip_fp8_quantize_delayed" in fw and "hip_fp8_delayed_update" in fw
+    assert "hip_fp8_cast_delayed" in fw and "hip_fp8_delayed_update" in fw
+    assert "cast_transpose" not in fw and "hip_fp8_quantize" not in fw  # no transposed copies
 
 
 @pytest.mark.gpu
