@@ -640,13 +640,14 @@ def linear_backward(a, w, bias, g):
     ga = gw = gb = None
     if _requires(a):
         ga = P.matmul(g, w)
-    if _requires(w) or (bias is not None and _requires(bias)):
+    if _requires(w):
         g2 = _clang().reshape(g, (-1, g.shape[-1]))
-        if _requires(w):
-            a2 = _clang().reshape(a, (-1, a.shape[-1]))
-            gw = P.matmul(ltorch.transpose(g2, 0, 1), a2)
-        if bias is not None and _requires(bias):
-            gb = ltorch.sum(g2, 0)
+        a2 = _clang().reshape(a, (-1, a.shape[-1]))
+        gw = P.matmul(ltorch.transpose(g2, 0, 1), a2)
+    if bias is not None and _requires(bias):
+        # summed over g's own leading dims (no flattening reshape): a fusion region producing g (an
+        # activation / dropout backward) then also emits the bias gradient as its column reduction
+        gb = ltorch.sum(g, tuple(range(g.ndim - 1))) if g.ndim > 1 else g
     return ga, gw, gb
 
 

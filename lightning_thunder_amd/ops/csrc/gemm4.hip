@@ -873,7 +873,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
 // One thread per 8 consecutive columns of a tile row.
 __global__ __launch_bounds__(256) void gemm4_tail_fixup(const float* __restrict__ partial, __hip_bfloat16* __restrict__ C,
                                                         int ksplit, int tile_base, int tile_count, int M, int N,
-                                                        int ldc, float alpha) {
+                                                        int ldc, float alpha,
+                                                        const __hip_bfloat16* __restrict__ bias = nullptr) {
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int t = (int)(id / (BM * BN / 8));
   if (t >= tile_count) return;
@@ -893,8 +894,15 @@ __global__ __launch_bounds__(256) void gemm4_tail_fixup(const float* __restrict_
     uint4 u;
     __hip_bfloat16 h[8];
   } o;
+  if (bias != nullptr) {  // the unsplit epilogue's alpha * acc + bias, one rounding
+    const uint4 bu = *reinterpret_cast<const uint4*>(bias + gcol);
+    const __hip_bfloat16* bh = reinterpret_cast<const __hip_bfloat16*>(&bu);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(a[e] * alpha);
+    for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(a[e] * alpha + __bfloat162float(bh[e]));
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.h[e] = __float2bfloat16(a[e] * alpha);
+  }
   *reinterpret_cast<uint4*>(C + grow * ldc + gcol) = o.u;
 }
 
@@ -939,8 +947,8 @@ int launch4_tail(const void* A, const void* B, void* C, int M, int N, int K, int
 // sums the fp32 partials in a fixed order (deterministic).  K % 2 BK == 0; the slices differ by at most
 // one 2 BK pair.
 template <bool AT, bool BT>
-int launch4_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-                   int ksplit, void* ws, int64_t ws_bytes, hipStream_t s) {
+int launch4_splitk(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
+                   int ldc, float alpha, int ksplit, void* ws, int64_t ws_bytes, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (ksplit < 2 || ksplit > 64 || K % (2 * BK) || K / (2 * BK) < ksplit || !ws ||
       ws_bytes < (int64_t)ksplit * nwg * BM * BN * 4)
@@ -954,7 +962,8 @@ int launch4_splitk(const void* A, const void* B, void* C, int M, int N, int K, i
                      s, (const __hip_bfloat16*)A, (const __hip_bfloat16*)B, (__hip_bfloat16*)C, nullptr, nullptr, M, N,
                      K, lda, ldb, ldc, 0, 1.f, ep);
   hipLaunchKernelGGL(gemm4_tail_fixup, dim3((unsigned)((int64_t)nwg * (BM * BN / 8) / 256)), dim3(256), 0, s,
-                     (const float*)ws, (__hip_bfloat16*)C, ksplit, 0, nwg, M, N, ldc, alpha);
+                     (const float*)ws, (__hip_bfloat16*)C, ksplit, 0, nwg, M, N, ldc, alpha,
+                     (const __hip_bfloat16*)bias);
   return (int)hipGetLastError();
 }
 
@@ -1036,18 +1045,18 @@ LTA_EXPORT int lta_gemm4_bf16_ws(const void* A, const void* B, void* C, const vo
   return lta_gemm4_bf16(A, B, C, bias, R, M, N, K, lda, ldb, ldc, ldr, alpha, act, at, bt, variant, s);
 }
 
-// Plain product C = alpha * opA . opB split over K into ksplit slices (launch4_splitk); ws: fp32, >=
-// ksplit * tiles * 256 * 256 elements.  Same layouts / limits as lta_gemm4_bf16; -2 on a bad split.
-LTA_EXPORT int lta_gemm4_bf16_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
-                                     int ldc, float alpha, int at, int bt, int ksplit, void* ws, int64_t ws_bytes,
-                                     hipStream_t s) {
-  if (N % 8 || M <= 0 || N <= 0 || K <= 0 || (at && M % 8)) return -2;
+// C = alpha * opA . opB (+ bias, forward layout) split over K into ksplit slices (launch4_splitk); ws:
+// fp32, >= ksplit * tiles * 256 * 256 elements.  Same layouts / limits as lta_gemm4_bf16; -2 on a bad split.
+LTA_EXPORT int lta_gemm4_bf16_splitk(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                                     int lda, int ldb, int ldc, float alpha, int at, int bt, int ksplit, void* ws,
+                                     int64_t ws_bytes, hipStream_t s) {
+  if (N % 8 || M <= 0 || N <= 0 || K <= 0 || (at && M % 8) || (bias && (at || bt))) return -2;
   const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;
   if (ea * 2 >= (1ll << 31) || eb * 2 >= (1ll << 31)) return -2;
-  if (!at && !bt) return launch4_splitk<false, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
-  if (!at && bt) return launch4_splitk<false, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
-  if (at && !bt) return launch4_splitk<true, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
-  return launch4_splitk<true, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  if (!at && !bt) return launch4_splitk<false, false>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  if (!at && bt) return launch4_splitk<false, true>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  if (at && !bt) return launch4_splitk<true, false>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
+  return launch4_splitk<true, true>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, ksplit, ws, ws_bytes, s);
 }
 
 // Grouped GEMMs for mixture-of-experts training (K10; reference nvFuser _grouped_mm forward and

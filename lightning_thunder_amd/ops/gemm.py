@@ -76,8 +76,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
 # ---------------------------------------------------------------------------------------------
 register_signature("lta_gemm4_bf16", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p])
-register_signature("lta_gemm4_bf16_splitk", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                                             c_float, c_int, c_int, c_int, c_void_p, c_int64, c_void_p])
+register_signature("lta_gemm4_bf16_splitk", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                             c_int, c_float, c_int, c_int, c_int, c_void_p, c_int64, c_void_p])
 register_signature("lta_gemm4_bf16_ws", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_void_p, c_int64,
                                          c_void_p])
@@ -200,11 +200,14 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
     if bias is not None:
         assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
     plain = bias is None and residual is None and act is None and variant == 1
-    ks = splitk_factor(M, N, K, _device_cus(a.device)) if plain else 0
+    # the K split also carries a bias (added in the fixup, forward layout)
+    splittable = residual is None and act is None and variant == 1 and (bias is None or (not at and not bt))
+    ks = splitk_factor(M, N, K, _device_cus(a.device)) if splittable else 0
     if ks:
         nwg = -(-M // 256) * -(-N // 256)
         ws = _workspace(ks * nwg * 256 * 256, a.device)
-        rc = require().lta_gemm4_bf16_splitk(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
+        rc = require().lta_gemm4_bf16_splitk(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                             None if bias is None else bias.data_ptr(), M, N, K, lda, ldb,
                                              out.stride(0), alpha, at, bt, ks, ws.data_ptr(), ws.numel() * 4,
                                              stream_ptr(a.device))
         check(rc, "lta_gemm4_bf16_splitk")

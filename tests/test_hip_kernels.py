@@ -1300,3 +1300,8 @@ def test_gemm4_splitk(M, N, K, layout):
     err = ((out.float() - ref).norm() / ref.norm()).item()
     assert err < 5e-3, err
     assert torch.equal(out, matmul4(a, b, alpha=0.5))
+    if layout == "nt":  # forward layout: the bias is added in the fixup
+        bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+        outb = matmul4(a, b, bias=bias)
+        refb = a.float() @ b.float() + bias.float()
+        assert ((outb.float() - refb).norm() / refb.norm()).item() < 5e-3
