@@ -820,6 +820,9 @@ COL_NW = int(os.environ.get("LTA_HIPFUSE_COL_NW", "8"))  # waves per column-mode
 COL_WGS = int(os.environ.get("LTA_HIPFUSE_COL_WGS", "192"))  # target workgroups of a column-mode grid
 COL_UNROLL = int(os.environ.get("LTA_HIPFUSE_COL_UNROLL", "8"))  # rows in flight per wave
 COL_MAX_SPLITS = 64  # the last workgroup of a column group reads every split's partial
+# regions with full-domain outputs besides the column reduction (GPT-2's GELU backward + bias gradient:
+# 80.7 -> 48 us at S = 24 -> 64, scripts/gpu_s5v.sh)
+COL_WGS_FULL = int(os.environ.get("LTA_HIPFUSE_COL_WGS_FULL", "768"))
 
 
 class KernelSource:
@@ -1843,13 +1846,16 @@ class _Gen:
         R = math.prod(D[:k])
         NW = COL_NW  # waves per workgroup
         ncs = (C // V + 63) // 64
-        # row splits: ~COL_WGS workgroups of NW waves (at most one per CU), >= 8 rows per wave, and at
-        # most COL_MAX_SPLITS (the serial tail reads them all)
-        S = max(1, min(-(-COL_WGS // ncs), -(-R // (8 * NW)), COL_MAX_SPLITS))
-        RPS = -(-R // S)
-        S = -(-R // RPS)
         red_nodes = [i for i, b in enumerate(self.p.nodes) if b.sym.id in REDUCTIONS]
         full_outs = [o for o in self.outputs if self.p.covers_reduced(self.p.maps.get(o.name))]
+        # row splits: ~COL_WGS workgroups of NW waves (at most one per CU; COL_WGS_FULL when the region
+        # also computes and stores full-domain outputs, e.g. an activation backward with its bias
+        # gradient: that work wants the occupancy of a pointwise grid), >= 8 rows per wave, and at most
+        # COL_MAX_SPLITS (the serial tail reads them all)
+        wgs = COL_WGS_FULL if full_outs else COL_WGS
+        S = max(1, min(-(-wgs // ncs), -(-R // (8 * NW)), COL_MAX_SPLITS))
+        RPS = -(-R // S)
+        S = -(-R // RPS)
         full_names = {o.name for o in full_outs}
         col_outs = [o for o in self.outputs if o.name not in full_names]
         self.load_names, self.loaded, self.idx_avail = {}, set(), set()

@@ -592,21 +592,18 @@ def test_fp8_producer_fused_casts_match_unfused(monkeypatch):
     hip_swiglu_fp8, no bf16 activation, no cast launch); losses and gradients over three steps (the
     first on current scaling, then on the amax history) are bit-identical to the unfused program."""
     import lightning_thunder_amd as thunder
-    from lightning_thunder_amd.models.litgpt import swiglu
+    from lightning_thunder_amd.models.litgpt import Config, LLaMAMLP, RMSNorm
     from lightning_thunder_amd.ops.fp8 import DelayedScaling
     from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
 
-    class Block(torch.nn.Module):
+    class Block(torch.nn.Module):  # the LitGPT pre-norm MLP half of a Llama block
         def __init__(self):
             super().__init__()
-            self.norm = torch.nn.RMSNorm(512, eps=1e-5)
-            self.fc_1 = torch.nn.Linear(512, 768, bias=False)
-            self.fc_2 = torch.nn.Linear(512, 768, bias=False)
-            self.proj = torch.nn.Linear(768, 512, bias=False)
+            self.norm = RMSNorm(512, eps=1e-5)
+            self.mlp = LLaMAMLP(Config(n_embd=512, intermediate_size=768, bias=False))
 
         def forward(self, x):
-            h = self.norm(x)
-            return x + self.proj(swiglu(self.fc_1(h), self.fc_2(h)))
+            return x + self.mlp(self.norm(x))
 
     torch.manual_seed(0)
     m = Block().cuda().bfloat16()
