@@ -15,7 +15,7 @@ from lightning_thunder_amd.models.nanogpt import NanoGPT
 from lightning_thunder_amd.optim import AdamW
 
 
-def main(steps=4, B=8, T=1024):
+def main(steps=6, B=8, T=1024):
     torch.manual_seed(0)
     m = NanoGPT.from_name("gpt2-medium", seq_len=T).to(device="cuda", dtype=torch.bfloat16)
     m.train()

@@ -6,7 +6,14 @@ from collections import defaultdict
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_bench/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
-seg = rows[idx[-2] + 1: idx[-1] + 1]
+# complete steps between consecutive AdamW kernels; report the median-span one (a host stall -- GC,
+# a page-in -- in a single step would otherwise set the printed span)
+segs = [rows[a + 1: b + 1] for a, b in zip(idx[:-1], idx[1:])]
+spans = [int(sg[-1]["End_Timestamp"]) - int(sg[0]["Start_Timestamp"]) for sg in segs]
+order = sorted(range(len(segs)), key=lambda k: spans[k])
+seg = segs[order[(len(order) - 1) // 2]]
+if len(segs) > 1:
+    print("step spans (ms): " + ", ".join(f"{x / 1e6:.2f}" for x in spans) + " -> median step below")
 
 
 def short(n):
