@@ -229,18 +229,19 @@ _CNT_BUF_T: dict = {}
 def _counters(n: int, dev) -> torch.Tensor:
     """Zeroed uint32 arrival counters of the column-mode kernels: one persistent buffer per (device,
     stream), grown on demand.  Every launch leaves its counters at zero again (the last workgroup of
-    each column group resets its own), so kernels ordered on one stream can share it; a graph capture
-    keeps the capture stream's buffer."""
+    each column group resets its own), so kernels ordered on one stream can share it.  Inside a graph
+    capture every launch gets a zero-filled buffer of the graph's own."""
+    if torch.cuda.is_current_stream_capturing():
+        # a buffer of the graph's own (its zero-fill is a node of the graph, replayed before the kernel):
+        # nothing the graph holds can be shared with or replaced by eager launches
+        return torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     buf = _COUNTERS.get(key)
     if buf is None or buf.numel() < n:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("hipFusion: column-reduction counters must be allocated before a graph capture "
-                               "(run the function once eagerly first)")
         old = buf
         buf = torch.zeros(max(n, 1024), dtype=torch.int32, device=dev)
-        if old is not None:
-            buf.record_stream(torch.cuda.current_stream(dev))
+        if old is not None:  # in-flight launches may still read it: free it behind the stream's work
+            old.record_stream(torch.cuda.current_stream(dev))
         _COUNTERS[key] = buf
     return buf
 
