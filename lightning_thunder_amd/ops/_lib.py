@@ -87,7 +87,22 @@ def ptr(t: torch.Tensor | None):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    """The current HIP stream of ``device`` as an integer handle.  Every kernel launch asks for it, so
+    it takes the raw-stream accessor (one C call) instead of building a torch.cuda.Stream object."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            if isinstance(device, str):
+                device = torch.device(device)
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

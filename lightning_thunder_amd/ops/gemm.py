@@ -6,6 +6,7 @@ import os as _os
 import torch
 
 import ctypes
+import functools
 
 from ._lib import require, stream_ptr, check, register_signature, dcode, c_int, c_void_p, c_float, c_int64
 
@@ -121,6 +122,7 @@ _SPLITK = _os.environ.get("LTA_GEMM_SPLITK", "1") != "0"
 _KT_US, _FIXED_US, _PARTIAL_US, _LAUNCH_US = 1.3, 4.5, 2 * 262144 / 5e6, 3.0
 
 
+@functools.lru_cache(maxsize=4096)
 def splitk_factor(M: int, N: int, K: int, cus: int) -> int:
     """K slices per tile for a plain product (0: no split) whose grid is at most half a wave of
     ``cus`` workgroups: the slice count (grid <= one wave, >= one 128-deep K pair per slice) the
