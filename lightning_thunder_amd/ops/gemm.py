@@ -157,6 +157,7 @@ def _workspace(need: int, device):
 
 
 GEMM4_MIN_M = 64
+_FWD_LIB = _os.environ.get("LTA_GEMM_FWD_LIB", "0") == "1"
 
 
 def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
@@ -422,6 +423,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
         if gemv_supported(x2, w, bias, r2):
             _count("gemv")
             return gemv_nt(x2, w, bias=bias, residual=r2, act=act).reshape(*x.shape[:-1], N)
+        if _FWD_LIB and act is None and bias is None and x2.shape[0] >= 1024 and x2.dtype == torch.bfloat16:
+            # A/B hook: forward products with no epilogue but the residual on the library GEMM
+            _count("torch")
+            return _torch_linear(x2, w, bias, r2, act).reshape(*x.shape[:-1], N)
         wt = w.t()
         lay = gemm4_layout(x2, wt)
         if lay is not None and nt_epilogue_ok(x2, w, bias, r2):

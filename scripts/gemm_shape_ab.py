@@ -19,6 +19,7 @@ MODELS = {
     # tokens, [(N, K)] of the linears (qkv, attn proj, fc, mlp proj, lm head)
     "gpt2-medium": (8192, [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096), (50304, 1024)]),
     "llama2-7b": (4096, [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (32000, 4096)]),
+    "llama2-7b-gateup": (4096, [(22016, 4096)]),
 }
 
 
