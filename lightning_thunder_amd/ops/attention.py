@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -37,6 +38,10 @@ register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_v
 register_signature("lta_attn_bwd_rope", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                          c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+register_signature("lta_attn_bwd_rope_ds", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                            c_int, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, ctypes.c_int64, c_void_p])
 register_signature("lta_attn_bwd_ex3", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
@@ -211,6 +216,12 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     return dq, dk, dv, g.to(mask.dtype)
 
 
+def _dq_from_ds() -> bool:
+    """LTA_ATTN_DQ_FROM_DS=1: the RoPE'd backward computes dQ from the dS the dK/dV kernel stores
+    (one B Hq T^2 bf16 workspace) instead of the dQ kernel's S / P / dP recompute."""
+    return os.environ.get("LTA_ATTN_DQ_FROM_DS", "0") == "1"
+
+
 def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):
     """The attention backward and the backward of the rotate-half RoPE + qkv split in one pass:
     returns d(qkv) [B, T, (n_head + 2 n_query_groups) * 128], with dQ / dK rotated back in the
@@ -233,6 +244,17 @@ def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: in
         delta = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
         st = (ctypes.c_int64 * 6)(*dd.stride()[:3], *oo.stride()[:3])
         esz = dqkv.element_size()
+        rc = -1
+        if _dq_from_ds() and T % 64 == 0:
+            ws = torch.empty(B * Hq * S * ((T + 255) // 256 * 256), device=q.device, dtype=q.dtype)
+            rc = lib.lta_attn_bwd_rope_ds(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
+                                          ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq,
+                                          Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p),
+                                          ctypes.cast(qkv_st, c_void_p), ctypes.cast(gst, c_void_p), ptr(cs), ptr(sn),
+                                          ptr(ws), ws.numel() * ws.element_size(), stream_ptr(q.device))
+            if rc != -1:
+                check(rc, "lta_attn_bwd_rope_ds")
+                return dqkv
         rc = lib.lta_attn_bwd_rope(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
                                    ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq, Hkv, T,
                                    S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ctypes.cast(qkv_st, c_void_p),

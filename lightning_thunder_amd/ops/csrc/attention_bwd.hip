@@ -474,14 +474,17 @@ constexpr int kKB3 = 256;
 // ---------------------------------------------------------------------------------------------
 // STAMP (diagnostic builds only, -DLTA_ATTN_DIAG): s_memtime at the phase boundaries of workgroup (0, 0)'s
 // first 64 query tiles, kept in LDS and copied to `dbg` at the end ([4 waves][64 tiles][8] u64)
-template <typename T, bool CAUSAL, int STAMP = 0>
+// WDS: also store dS^T to `dSt` (the dQ-from-dS path); a template flag so the default build keeps
+// its register allocation
+template <typename T, bool CAUSAL, int STAMP = 0, bool WDS = false>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                        const T* __restrict__ V, const T* __restrict__ dO,
                                                                        const float* __restrict__ LSE,
                                                                        const float* __restrict__ DELTA, T* __restrict__ dK,
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
                                                                        float scale, float scale_log2, RowStrides sdo, QKVStrides sx,
-                                                                       int qrev = 0, uint64_t* dbg = nullptr) {
+                                                                       int qrev = 0, uint64_t* dbg = nullptr,
+                                                                       T* __restrict__ dSt = nullptr) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -741,6 +744,24 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
             mfma_acc_agpr(dkacc[j][dt], xt[2 * dt], df[j][0]);
             mfma_acc_agpr(dkacc[j][dt], xt[2 * dt + 1], df[j][1]);
           }
+        if constexpr (WDS) {
+          // dS^T for the dQ pass (attn_bwd_dq_ds_kernel): [b, hq][query block of 256][key][256] bf16,
+          // so the reader's 64-key tiles are contiguous 32 KiB; this lane's 8 packed values of each
+          // fragment as one 16-B store at q offset 16 s + 8 h of the 32-query tile (the fragment's own
+          // order: query acc_row(8 s + e, h) at offset e; the reader un-permutes).  Streaming stores:
+          // the next kernel reads them, nothing in this one does
+          const int hq_cur = hk * group + it / nq;
+          const int nqb = (Tq + 255) >> 8;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            T* drow = dSt + (((int64_t)(b * Hq + hq_cur) * nqb + (qbase >> 8)) * Sk + (kw + 32 * j + r)) * 256 +
+                      (qbase & 255) + 8 * h;
+            if (kw + 32 * j + r < Sk) {
+              __builtin_nontemporal_store(df[j][0], reinterpret_cast<F*>(drow));
+              __builtin_nontemporal_store(df[j][1], reinterpret_cast<F*>(drow + 16));
+            }
+          }
+        }
       }
     }
     stamp(it, 5);
@@ -1224,6 +1245,174 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_v4_kernel(const T* __
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// dQ from the stored dS (LTA_ATTN_DQ_FROM_DS, D = 128): the dK/dV kernel already forms dS = P (dP -
+// delta) for every (key, query) pair and writes it (bf16, [b, hq][query block][key][256 queries],
+// 0.5 GB per causal Llama-2-7B layer); dQ = scale dS K is then one streaming product per head instead of a second pass that
+// recomputes S, P and dP (two of the dQ v4 kernel's three MFMA chains).  Workgroup: 256 queries x all
+// 128 d, 4 waves of 64 queries; 64-key tiles of K ([key][d], 16 KiB) and dS^T ([key][query], 32 KiB)
+// stream through a 3-stage LDS-DMA ring; dQ^T[d][q] = K^T dS^T on 32x32x16 MFMAs with both operands
+// read by ds_read_b64_tr_b16 (chunk c of row R at slot c ^ ((R & 3) << 2): conflict-free), so each
+// lane ends up owning one query row of dQ (the dK epilogue's store, RoPE transpose included).
+// Host: Tq == Sk, Sk % 64 == 0, Tq % 32 == 0.
+// one 16-key step of the dQ-from-dS product: the transposed fragments of 4 K^T blocks (256-B rows)
+// and 2 dS^T blocks (512-B rows), rows 16 S + {0..3} and + 8.  Inline asm: the compiler's LDS-DMA
+// alias tracking would put a vmcnt(0) in front of builtin LDS reads (a full memory round trip per
+// tile); the ring's own vmcnt + barrier order them
+template <int S>
+__device__ __forceinline__ void dqds_issue(s16x4t (&x)[12], const uint32_t (&ka)[4], const uint32_t (&sa)[2]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %12 offset:%18\n\tds_read_b64_tr_b16 %1, %12 offset:%19\n\t"
+      "ds_read_b64_tr_b16 %2, %13 offset:%18\n\tds_read_b64_tr_b16 %3, %13 offset:%19\n\t"
+      "ds_read_b64_tr_b16 %4, %14 offset:%18\n\tds_read_b64_tr_b16 %5, %14 offset:%19\n\t"
+      "ds_read_b64_tr_b16 %6, %15 offset:%18\n\tds_read_b64_tr_b16 %7, %15 offset:%19\n\t"
+      "ds_read_b64_tr_b16 %8, %16 offset:%20\n\tds_read_b64_tr_b16 %9, %16 offset:%21\n\t"
+      "ds_read_b64_tr_b16 %10, %17 offset:%20\n\tds_read_b64_tr_b16 %11, %17 offset:%21"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7]),
+        "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11])
+      : "v"(ka[0]), "v"(ka[1]), "v"(ka[2]), "v"(ka[3]), "v"(sa[0]), "v"(sa[1]), "i"(S * 4096), "i"(S * 4096 + 2048),
+        "i"(S * 8192), "i"(S * 8192 + 4096)
+      : "memory");
+}
+
+template <int S, int NSS, typename F>
+__device__ __forceinline__ void dqds_steps(f32x16 (&acc)[2][4], s16x4t (&cur)[12], s16x4t (&nxt)[12],
+                                           const uint32_t (&ka)[4], const uint32_t (&sa)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]), "+v"(cur[6]),
+                 "+v"(cur[7]), "+v"(cur[8]), "+v"(cur[9]), "+v"(cur[10]), "+v"(cur[11])
+               :
+               : "memory");
+  if constexpr (S + 1 < NSS) dqds_issue<S + 1>(nxt, ka, sa);
+  F f[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    union {
+      struct {
+        s16x4t a, b;
+      } s;
+      F f;
+    } u;
+    u.s.a = cur[2 * i];
+    u.s.b = cur[2 * i + 1];
+    f[i] = u.f;
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) mfma_acc_agpr(acc[x][dt], f[dt], f[4 + x]);
+  if constexpr (S + 1 < NSS) dqds_steps<S + 1, NSS, F>(acc, nxt, cur, ka, sa);
+}
+
+template <typename T, bool CAUSAL, int KT = 64, int NST = 3, int OCC = 1>
+__global__ __launch_bounds__(kThreads, OCC) void attn_bwd_dq_ds_kernel(const T* __restrict__ K, const T* __restrict__ dSt,
+                                                                     T* __restrict__ dQ, int Hq, int Hkv, int Tq, int Sk,
+                                                                     float scale, QKVStrides sx, int rotate) {
+  using F = typename Frag<T>::type;
+  // KT-key tiles, NST-stage ring, NST - 1 tiles in flight (the sweep: profiles/attn_dq_ds.txt)
+  constexpr int KIMG = KT * 256, SIMG = KT * 512, STG = KIMG + SIMG;
+  constexpr int NK = KT / 16, NS = KT / 8;  // LDS-DMA instructions per wave per tile: K, dS^T
+  static_assert(KT % 16 == 0 && NST >= 2 && NST <= 10 && NST * STG <= 160 * 1024, "dq_ds tiling");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
+  const int n_qb = (Tq + 255) / 256;
+  // causal: heavy blocks first; with OCC > 1 co-resident workgroups, the grid's second half walks
+  // light -> heavy again, so blocks y and y + n_qb / 2 (likely on one CU) carry complementary loads
+  const int y = (int)blockIdx.y, half = n_qb / 2;
+  const int qb = !CAUSAL ? y : (OCC == 1 || y < n_qb - half) ? n_qb - 1 - y : y - (n_qb - half);
+  const int bh = blockIdx.x, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
+  const int q0 = qb * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, g = lane >> 4, l16 = lane & 15, vq = l16 >> 2, vp = l16 & 3;
+  const T* Kb = K + b * sx.kb + hk * sx.kh;
+  const T* Sb = dSt + ((int64_t)bh * n_qb + qb) * Sk * 256;
+  const int kend = CAUSAL ? min(Sk, q0 + 256) : Sk;
+  const int nt = (kend + KT - 1) / KT;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // LDS-DMA of key tile t into stage st: wave w fills K rows KT/4 w .. (NK pieces of 4 rows) and
+  // dS^T rows KT/4 w .. (NS pieces of 2 rows of 512 B); the swizzle is applied to the source chunk
+  // every workgroup's stream starts at a 2 MiB-aligned block: rotating the tile order by a
+  // per-workgroup amount keeps the 256 streams off the same memory channels at the same time
+  const int rot = rotate ? (int)((blockIdx.x * 7u + blockIdx.y * 3u) % (unsigned)max(nt, 1)) : 0;
+  auto issue = [&](int t0, int st) {
+    const int t = t0 + rot < nt ? t0 + rot : t0 + rot - nt;
+    char* kimg = smem + st * STG;
+    char* simg = kimg + KIMG;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+      const int R = (KT / 4) * wave + 4 * i + (lane >> 4), slot = lane & 15, c = slot ^ ((R & 3) << 2);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)(t * KT + R) * sx.kt + c * 8),
+                                       (lds_void*)(kimg + (NK * wave + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int R = (KT / 4) * wave + 2 * i + (lane >> 5), slot = lane & 31, c = slot ^ ((R & 3) << 2);
+      // columns past Tq of a partial last block were never written: they only reach unstored dQ rows
+      __builtin_amdgcn_global_load_lds((const void*)(Sb + (int64_t)(t * KT + R) * 256 + c * 8),
+                                       (lds_void*)(simg + (NS * wave + i) * 1024), 16, 0, 0);
+    }
+  };
+  // transposed fragments (keys 16 s + 4 hh + {0..3, 8..11} of 32-column block `blk`) of the
+  // [key][column] images: this lane's byte offsets for s = 0
+  uint32_t koff[4], soff[2];
+#pragma unroll
+  for (int blk = 0; blk < 4; ++blk)
+    koff[blk] = (4 * hh + vq) * 256 + ((4 * (blk ^ vq) + 2 * (g & 1) + (vp >> 1)) << 4) + 8 * (vp & 1);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+    soff[x] = (4 * hh + vq) * 512 + ((4 * ((2 * wave + x) ^ vq) + 2 * (g & 1) + (vp >> 1)) << 4) + 8 * (vp & 1);
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[x][dt][i] = 0.f;
+
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nt) issue(p, p);
+  for (int t = 0; t < nt; ++t) {
+    // tile t landed: the tiles issued after it (min(nt - 1 - t, NST - 2) of them) may be in flight
+    const int later = min(nt - 1 - t, NST - 2);
+    switch (later) {
+#define LTA_W(n) \
+  case n: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n * (NK + NS)) : "memory"); break;
+      LTA_W(0) LTA_W(1) LTA_W(2) LTA_W(3) LTA_W(4) LTA_W(5) LTA_W(6) LTA_W(7) LTA_W(8)
+#undef LTA_W
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... for every wave; stage (t + NST - 1) % NST (tile t - 1) is free
+    if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
+    const uint32_t kimg = lds0 + (t % NST) * STG, simg = kimg + KIMG;
+    const uint32_t ka[4] = {kimg + koff[0], kimg + koff[1], kimg + koff[2], kimg + koff[3]};
+    const uint32_t sa[2] = {simg + soff[0], simg + soff[1]};
+    s16x4t xa[12], xb[12];
+    dqds_issue<0>(xa, ka, sa);
+    dqds_steps<0, KT / 16, F>(acc, xa, xb, ka, sa);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[x][dt]));
+  // lane column n of block 2 wave + x holds stored query offset n: query acc_row(8 s + e, h) of the
+  // 32-query tile for n = 16 s + 8 h + e (the dK/dV kernel's fragment order)
+  const bool rope = sx.rope_cos != nullptr;
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int n = lane & 31, e = n & 7;
+    const int q = q0 + 32 * (2 * wave + x) + (e & 3) + 8 * (e >> 2) + 4 * ((n >> 3) & 1) + 16 * (n >> 4);
+    if (q < Tq) {
+      T* qrow = dQ + (int64_t)b * sx.dqb + (int64_t)hq * sx.dqh + (int64_t)q * sx.dqt;
+      store_row_d128(qrow, acc[x], scale, hh, rope ? sx.rope_cos + (int64_t)q * 128 : nullptr,
+                     rope ? sx.rope_sin + (int64_t)q * 128 : nullptr);
+    }
+  }
+}
+
+
 template <typename T, int D, int EX>
 void launch_masked(const void* dO, const void* Q, const void* K, const void* V, const void* LSE, void* DELTA, void* dQ,
                    void* dK, void* dV, int B, int Hq, int Hkv, int Tq, int Sk, float scale, float sl2, int causal,
@@ -1273,6 +1462,54 @@ int g_dkdv_qrev = [] {
                      (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
                      sdo, ex.sx, g_dkdv_qrev, nullptr)
 #endif
+
+// dQ from the stored dS (attn_bwd_dq_ds_kernel): delta by the preprocess kernel, dK / dV (+ dS^T
+// into ds_ws), then the dQ product.  D = 128, Tq == Sk, Sk % 64 == 0, Tq % 32 == 0.
+// dQ-from-dS tiling (A/B knob LTA_ATTN_DQDS_CFG): 0 = 64 keys x 3 stages, 1 = 32 x 6, 2 = 16 x 10
+const int g_dqds_cfg = [] {
+  const char* e = getenv("LTA_ATTN_DQDS_CFG");
+  return e ? atoi(e) : 0;
+}();
+// LTA_ATTN_DQDS_ROT=0: every workgroup walks its key tiles from 0 (A/B of the rotated order)
+const int g_dqds_rot = [] {
+  const char* e = getenv("LTA_ATTN_DQDS_ROT");
+  return e ? atoi(e) : 1;
+}();
+
+template <typename T>
+int launch_bwd_ds(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE,
+                  void* DELTA, void* dQ, void* dK, void* dV, void* dS, int B, int Hq, int Hkv, int Tq, int Sk,
+                  float scale, int causal, RowStrides sdo, RowStrides so, const AttnExtra& ex, hipStream_t s) {
+  const float sl2 = scale * 1.44269504088896340736f;
+  const int64_t rows = (int64_t)B * Hq * Tq;
+  dim3 blk(kThreads);
+  hipLaunchKernelGGL((attn_bwd_preprocess<T, 128>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                     (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
+  dim3 gk(B * Hkv, (Sk + kKB3 - 1) / kKB3), gq(B * Hq, (Tq + 255) / 256);
+#define LTA_DS(CA)                                                                                                   \
+  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, true>), gk, blk, 0, s, (const T*)Q, (const T*)K,          \
+                     (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, \
+                     scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, (T*)dS);                                                        \
+  if (g_dqds_cfg == 1)                                                                                               \
+    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 32, 6>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq,  \
+                       Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                       \
+  else if (g_dqds_cfg == 2)                                                                                          \
+    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 16, 10>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, \
+                       Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                       \
+  else if (g_dqds_cfg == 3)                                                                                          \
+    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 32, 3, 2>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ,   \
+                       Hq, Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                   \
+  else if (g_dqds_cfg == 4)                                                                                          \
+    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 16, 6, 2>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ,   \
+                       Hq, Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                   \
+  else                                                                                                               \
+    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, Hkv,    \
+                       Tq, Sk, scale, ex.sx, g_dqds_rot)
+  if (causal) { LTA_DS(true); }
+  else { LTA_DS(false); }
+#undef LTA_DS
+  return (int)hipGetLastError();
+}
 
 template <typename T, int D>
 int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE, void* DELTA,
@@ -1374,6 +1611,34 @@ LTA_EXPORT int lta_attn_bwd_rope(int dtype, const void* dO, const void* Q, const
 // qkv_strides: optional int64[9] = (batch, head, token) strides of Q, K, V (as lta_attn_fwd_ex2)
 // grad_strides: optional int64[9] = dQ, dK, dV (batch, head, token) element strides (head dim
 // contiguous, rows 16-byte aligned); null = dense [B, H, T, D] gradients.
+// lta_attn_bwd_rope with dQ computed from the stored dS (launch_bwd_ds); ds_ws: >= B Hq Sk
+// ceil(Tq / 256) 256 elements of the input dtype.  -1 when the shape does not qualify (the caller then takes lta_attn_bwd_rope).
+LTA_EXPORT int lta_attn_bwd_rope_ds(int dtype, const void* dO, const void* Q, const void* K, const void* V,
+                                    const void* O, const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B,
+                                    int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
+                                    const int64_t* strides, const int64_t* qkv_strides, const int64_t* grad_strides,
+                                    const float* rope_cos, const float* rope_sin, void* ds_ws, int64_t ds_bytes,
+                                    hipStream_t stream) {
+  if (D != 128 || Tq != Sk || Tq <= 0 || Tq % 32 || Sk % 64 || Hq % Hkv != 0 || !rope_cos || !rope_sin || !ds_ws ||
+      ds_bytes < (int64_t)B * Hq * ((Tq + 255) / 256) * 256 * Sk * 2)
+    return -1;
+  const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
+  const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
+  const RowStrides so = strides ? RowStrides{strides[3], strides[4], strides[5]} : dflt;
+  AttnExtra ex{};
+  ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
+  ex.sx.set_grad(grad_strides);
+  ex.sx.rope_cos = rope_cos;
+  ex.sx.rope_sin = rope_sin;
+  if (dtype == kBF16)
+    return launch_bwd_ds<__hip_bfloat16>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, ds_ws, B, Hq, Hkv, Tq, Sk, scale,
+                                         causal, sdo, so, ex, stream);
+  if (dtype == kF16)
+    return launch_bwd_ds<__half>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, ds_ws, B, Hq, Hkv, Tq, Sk, scale, causal, sdo,
+                                 so, ex, stream);
+  return -1;
+}
+
 LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
                                 const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
                                 int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,

@@ -1220,6 +1220,47 @@ def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
     assert e_fused < 1e-2 and e_fused <= 1.5 * e_two + 1e-4, (e_fused, e_two)
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,T,causal", [(1, 4, 2, 512, True), (2, 4, 4, 256, False), (1, 8, 1, 320, True),
+                                                (1, 2, 2, 1088, False)])
+def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, monkeypatch):
+    """LTA_ATTN_DQ_FROM_DS=1: dQ = scale dS K from the dS^T the dK/dV kernel stores, against the
+    default (recompute) path and an fp32 reference."""
+    from lightning_thunder_amd.models.litgpt import build_rope_cache
+    from lightning_thunder_amd.ops import _lib
+    from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd_rope
+    from lightning_thunder_amd.ops.fused import qkv_rope_bwd
+
+    torch.manual_seed(0)
+    D = 128
+    cos, sin = build_rope_cache(T, D, device="cuda")
+    q = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    o, lse = attn_fwd(q, k, v, causal)
+    base = attn_bwd_rope(do, q, k, v, o, lse, causal, None, cos, sin, Hq, Hkv)
+    monkeypatch.setenv("LTA_ATTN_DQ_FROM_DS", "1")
+    calls = []
+    fn = _lib.require().lta_attn_bwd_rope_ds
+    monkeypatch.setattr(_lib.require(), "lta_attn_bwd_rope_ds", lambda *a: calls.append(1) or fn(*a))
+    ds = attn_bwd_rope(do, q, k, v, o, lse, causal, None, cos, sin, Hq, Hkv)
+    torch.cuda.synchronize()
+    assert calls, "dQ-from-dS path not taken"
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    rep = Hq // Hkv
+    s = qf @ kf.repeat_interleave(rep, 1).transpose(-1, -2) / D ** 0.5
+    if causal:
+        s = s.masked_fill(torch.ones(T, T, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
+    (torch.softmax(s, -1) @ vf.repeat_interleave(rep, 1)).backward(do.float())
+    ref = qkv_rope_bwd(qf.grad, kf.grad, vf.grad, cos, sin, Hq, Hkv, D, D)
+    nq = Hq * D
+    for name, sl in (("dq", slice(0, nq)), ("dkv", slice(nq, None))):
+        r = ref[..., sl]
+        e_ds = ((ds[..., sl].float() - r).norm() / r.norm()).item()
+        e_base = ((base[..., sl].float() - r).norm() / r.norm()).item()
+        assert e_ds < 1e-2 and e_ds <= 1.5 * e_base + 1e-4, (name, e_ds, e_base)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("cols", [1024, 1000, 3000])
 def test_layer_norm_backward_residual_fused(cols):
