@@ -216,10 +216,15 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     return dq, dk, dv, g.to(mask.dtype)
 
 
-def _dq_from_ds() -> bool:
-    """LTA_ATTN_DQ_FROM_DS=1: the RoPE'd backward computes dQ from the dS the dK/dV kernel stores
-    (one B Hq T^2 bf16 workspace) instead of the dQ kernel's S / P / dP recompute."""
-    return os.environ.get("LTA_ATTN_DQ_FROM_DS", "0") == "1"
+def _dq_from_ds(ws_bytes: int) -> bool:
+    """The RoPE'd backward computes dQ from the dS the dK/dV kernel stores (one B Hq T^2 bf16
+    workspace, 1 GiB for a Llama-2-7B layer at T = 4096) instead of the dQ kernel's S / P / dP
+    recompute: 59 us less per layer there (profiles/attn_dq_from_ds.txt).  On by default while the
+    workspace fits LTA_ATTN_DS_MAX_GB (default 4); LTA_ATTN_DQ_FROM_DS=0 / 1 forces it off / on."""
+    mode = os.environ.get("LTA_ATTN_DQ_FROM_DS", "auto")
+    if mode in ("0", "1"):
+        return mode == "1"
+    return ws_bytes <= float(os.environ.get("LTA_ATTN_DS_MAX_GB", "4")) * 2 ** 30
 
 
 def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):
@@ -245,8 +250,9 @@ def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: in
         st = (ctypes.c_int64 * 6)(*dd.stride()[:3], *oo.stride()[:3])
         esz = dqkv.element_size()
         rc = -1
-        if _dq_from_ds() and T % 64 == 0:
-            ws = torch.empty(B * Hq * S * ((T + 255) // 256 * 256), device=q.device, dtype=q.dtype)
+        n_ws = B * Hq * S * ((T + 255) // 256 * 256)
+        if T % 64 == 0 and _dq_from_ds(n_ws * esz):
+            ws = torch.empty(n_ws, device=q.device, dtype=q.dtype)
             rc = lib.lta_attn_bwd_rope_ds(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
                                           ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq,
                                           Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p),

@@ -1307,9 +1307,10 @@ __device__ __forceinline__ void dqds_steps(f32x16 (&acc)[2][4], s16x4t (&cur)[12
 template <typename T, bool CAUSAL, int KT = 64, int NST = 3, int OCC = 1>
 __global__ __launch_bounds__(kThreads, OCC) void attn_bwd_dq_ds_kernel(const T* __restrict__ K, const T* __restrict__ dSt,
                                                                      T* __restrict__ dQ, int Hq, int Hkv, int Tq, int Sk,
-                                                                     float scale, QKVStrides sx, int rotate) {
+                                                                     float scale, QKVStrides sx) {
   using F = typename Frag<T>::type;
-  // KT-key tiles, NST-stage ring, NST - 1 tiles in flight (the sweep: profiles/attn_dq_ds.txt)
+  // KT-key tiles, NST-stage ring, NST - 1 tiles in flight (64 x 3 measured best of 64 x 3, 32 x 6,
+  // 16 x 10 and two-workgroups-per-CU 32 x 3 / 16 x 6: profiles/attn_dq_from_ds.txt)
   constexpr int KIMG = KT * 256, SIMG = KT * 512, STG = KIMG + SIMG;
   constexpr int NK = KT / 16, NS = KT / 8;  // LDS-DMA instructions per wave per tile: K, dS^T
   static_assert(KT % 16 == 0 && NST >= 2 && NST <= 10 && NST * STG <= 160 * 1024, "dq_ds tiling");
@@ -1332,11 +1333,7 @@ __global__ __launch_bounds__(kThreads, OCC) void attn_bwd_dq_ds_kernel(const T* 
 
   // LDS-DMA of key tile t into stage st: wave w fills K rows KT/4 w .. (NK pieces of 4 rows) and
   // dS^T rows KT/4 w .. (NS pieces of 2 rows of 512 B); the swizzle is applied to the source chunk
-  // every workgroup's stream starts at a 2 MiB-aligned block: rotating the tile order by a
-  // per-workgroup amount keeps the 256 streams off the same memory channels at the same time
-  const int rot = rotate ? (int)((blockIdx.x * 7u + blockIdx.y * 3u) % (unsigned)max(nt, 1)) : 0;
-  auto issue = [&](int t0, int st) {
-    const int t = t0 + rot < nt ? t0 + rot : t0 + rot - nt;
+  auto issue = [&](int t, int st) {
     char* kimg = smem + st * STG;
     char* simg = kimg + KIMG;
 #pragma unroll
@@ -1465,17 +1462,6 @@ int g_dkdv_qrev = [] {
 
 // dQ from the stored dS (attn_bwd_dq_ds_kernel): delta by the preprocess kernel, dK / dV (+ dS^T
 // into ds_ws), then the dQ product.  D = 128, Tq == Sk, Sk % 64 == 0, Tq % 32 == 0.
-// dQ-from-dS tiling (A/B knob LTA_ATTN_DQDS_CFG): 0 = 64 keys x 3 stages, 1 = 32 x 6, 2 = 16 x 10
-const int g_dqds_cfg = [] {
-  const char* e = getenv("LTA_ATTN_DQDS_CFG");
-  return e ? atoi(e) : 0;
-}();
-// LTA_ATTN_DQDS_ROT=0: every workgroup walks its key tiles from 0 (A/B of the rotated order)
-const int g_dqds_rot = [] {
-  const char* e = getenv("LTA_ATTN_DQDS_ROT");
-  return e ? atoi(e) : 1;
-}();
-
 template <typename T>
 int launch_bwd_ds(const void* dO, const void* Q, const void* K, const void* V, const void* O, const void* LSE,
                   void* DELTA, void* dQ, void* dK, void* dV, void* dS, int B, int Hq, int Hkv, int Tq, int Sk,
@@ -1490,21 +1476,8 @@ int launch_bwd_ds(const void* dO, const void* Q, const void* K, const void* V, c
   hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, true>), gk, blk, 0, s, (const T*)Q, (const T*)K,          \
                      (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, \
                      scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, (T*)dS);                                                        \
-  if (g_dqds_cfg == 1)                                                                                               \
-    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 32, 6>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq,  \
-                       Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                       \
-  else if (g_dqds_cfg == 2)                                                                                          \
-    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 16, 10>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, \
-                       Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                       \
-  else if (g_dqds_cfg == 3)                                                                                          \
-    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 32, 3, 2>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ,   \
-                       Hq, Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                   \
-  else if (g_dqds_cfg == 4)                                                                                          \
-    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA, 16, 6, 2>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ,   \
-                       Hq, Hkv, Tq, Sk, scale, ex.sx, g_dqds_rot);                                                   \
-  else                                                                                                               \
-    hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, Hkv,    \
-                       Tq, Sk, scale, ex.sx, g_dqds_rot)
+  hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, Hkv, Tq,   \
+                     Sk, scale, ex.sx)
   if (causal) { LTA_DS(true); }
   else { LTA_DS(false); }
 #undef LTA_DS

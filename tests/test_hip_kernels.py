@@ -1223,8 +1223,8 @@ def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
 @pytest.mark.parametrize("B,Hq,Hkv,T,causal", [(1, 4, 2, 512, True), (2, 4, 4, 256, False), (1, 8, 1, 320, True),
                                                 (1, 2, 2, 1088, False)])
 def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, monkeypatch):
-    """LTA_ATTN_DQ_FROM_DS=1: dQ = scale dS K from the dS^T the dK/dV kernel stores, against the
-    default (recompute) path and an fp32 reference."""
+    """dQ = scale dS K from the dS^T the dK/dV kernel stores (the default while the workspace fits),
+    against the recompute path (LTA_ATTN_DQ_FROM_DS=0) and an fp32 reference."""
     from lightning_thunder_amd.models.litgpt import build_rope_cache
     from lightning_thunder_amd.ops import _lib
     from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd_rope
@@ -1238,8 +1238,9 @@ def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, monkeypatch):
     v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
     do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
     o, lse = attn_fwd(q, k, v, causal)
+    monkeypatch.setenv("LTA_ATTN_DQ_FROM_DS", "0")
     base = attn_bwd_rope(do, q, k, v, o, lse, causal, None, cos, sin, Hq, Hkv)
-    monkeypatch.setenv("LTA_ATTN_DQ_FROM_DS", "1")
+    monkeypatch.setenv("LTA_ATTN_DQ_FROM_DS", "auto")
     calls = []
     fn = _lib.require().lta_attn_bwd_rope_ds
     monkeypatch.setattr(_lib.require(), "lta_attn_bwd_rope_ds", lambda *a: calls.append(1) or fn(*a))
