@@ -454,6 +454,8 @@ __device__ __forceinline__ void tr_wait16(F (&f)[8], s16x4t (&x)[16]) {
   }
 }
 
+typedef int dsi32x4 __attribute__((ext_vector_type(4)));
+
 // ---------------------------------------------------------------------------------------------
 // dK / dV, D = 128: one workgroup per 256 keys, 64 per wave in two 32-key halves.  Every Q / dO
 // image read (row reads for S and dP, transposed reads for dV^T and dK^T) feeds both halves' MFMAs;
@@ -575,7 +577,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
                                        (lds_void*)(qimg + IMG + k * 1024), 16, 0, 0);
     }
   };
-  auto wait_all_but_newest = [&]() { asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory"); };
+  // everything but the newest tile's 4 DMA pieces (and, WDS, the 4 dS stores issued after them:
+  // vmcnt counts stores too, and the plain count would drain the prefetch of tile + 2 every tile)
+  auto wait_all_but_newest = [&](bool after_stores) {
+    if (WDS && after_stores)
+      asm volatile("s_waitcnt vmcnt(8)" : "+v"(plse), "+v"(pdel)::"memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(plse), "+v"(pdel)::"memory");
+  };
 
   int nhi = 0, nti = 0;
   auto advance = [&]() {
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   if (total > 1) {
     issue(nhi, nti, 1);
     advance();
-    wait_all_but_newest();
+    wait_all_but_newest(false);
     stash_stats(1);
   }
   __syncthreads();
@@ -749,17 +758,23 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           // so the reader's 64-key tiles are contiguous 32 KiB; this lane's 8 packed values of each
           // fragment as one 16-B store at q offset 16 s + 8 h of the 32-query tile (the fragment's own
           // order: query acc_row(8 s + e, h) at offset e; the reader un-permutes).  Streaming stores:
-          // the next kernel reads them, nothing in this one does
+          // the next kernel reads them, nothing in this one does.  Buffer stores: the wave's 64 key rows as one resource whose size drops the rows past Sk,
+          // the half j as a scalar offset, so the loop spends one VGPR on the address (every term is
+          // wave-uniform; readfirstlane says so, or the resource would be waterfalled)
           const int hq_cur = hk * group + it / nq;
           const int nqb = (Tq + 255) >> 8;
+          const uint64_t wa = (uint64_t)(uintptr_t)(dSt + ((((int64_t)(b * Hq + hq_cur) * nqb + (qbase >> 8)) * Sk + kw) * 256 +
+                                                           (qbase & 255)));
+          const uint64_t wu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(wa >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wa);
+          const int wbytes = __builtin_amdgcn_readfirstlane(max(0, min(64, Sk - kw)) * 512);
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)wu, (short)0, wbytes, 0x00020000);
+          const int loff = (r * 256 + 8 * h) * 2;
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            T* drow = dSt + (((int64_t)(b * Hq + hq_cur) * nqb + (qbase >> 8)) * Sk + (kw + 32 * j + r)) * 256 +
-                      (qbase & 255) + 8 * h;
-            if (kw + 32 * j + r < Sk) {
-              __builtin_nontemporal_store(df[j][0], reinterpret_cast<F*>(drow));
-              __builtin_nontemporal_store(df[j][1], reinterpret_cast<F*>(drow + 16));
-            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dsi32x4, df[j][0]), rs, loff, j * 16384, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dsi32x4, df[j][1]), rs, loff, j * 16384 + 32, 2);
           }
         }
       }
@@ -767,7 +782,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
     stamp(it, 5);
     if (issue_next) {
       advance();
-      wait_all_but_newest();
+      wait_all_but_newest(true);
       stash_stats(st2);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
