@@ -45,7 +45,8 @@ def _sources():
 # S / dP tiles stay where their softmax reads them while the dK / dV accumulators (inline-asm MFMAs)
 # own the AGPR file (without it hipcc swaps them through AGPRs every tile).
 FILE_FLAGS = {"attention_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-              "attention_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
+              "attention_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"],
+              "attention_fwd_d256.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _compile(src: str, obj: str, is_device: bool, verbose: bool, defines=()) -> str:

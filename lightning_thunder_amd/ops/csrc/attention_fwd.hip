@@ -252,6 +252,9 @@ __global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T
 // v2 / v3 kernels: profiles/attn_v2_ab.json, profiles/attn_fwd_pmc.json).  11..15 select the v4
 // measurement builds, compiled only with -DLTA_ATTN_DIAG.
 int g_fwd_impl = 10;
+// D = 256 without mask / dropout: 1 = the LDS-DMA ring kernel (attention_fwd_d256.hip), 0 = the
+// generic kernel below (A/B: lta_attn_fwd_set_d256)
+int g_fwd_d256 = 1;
 
 template <typename T, int D, int EX>
 int launch_ex(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
@@ -282,6 +285,10 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 }
 
 }  // namespace
+
+LTA_EXPORT int lta_attn_fwd_d256(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
+                                 int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
+                                 const int64_t* o_strides, const int64_t* qkv_strides, hipStream_t stream);
 
 LTA_EXPORT int lta_attn_fwd_v4(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B,
                                int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
@@ -323,6 +330,11 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
                                    stream);
     if (rc != -1) return rc;
   }
+  if (D == 256 && exf == 0 && g_fwd_d256) {  // LDS-DMA ring kernel (attention_fwd_d256.hip)
+    const int rc = lta_attn_fwd_d256(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides,
+                                     qkv_strides, stream);
+    if (rc != -1) return rc;
+  }
   if (dtype == kBF16) {
     if (D == 128) return launch<__hip_bfloat16, 128>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
     if (D == 64) return launch<__hip_bfloat16, 64>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, ex, exf, stream);
@@ -361,5 +373,12 @@ LTA_EXPORT int lta_attn_fwd(int dtype, const void* q, const void* k, const void*
 LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
   const int old = g_fwd_impl;
   if (impl >= 0 && impl <= 15) g_fwd_impl = impl;
+  return old;
+}
+
+// D = 256 forward kernel selection (A/B measurement hook): 1 = LDS-DMA ring kernel, 0 = generic
+LTA_EXPORT int lta_attn_fwd_set_d256(int on) {
+  const int old = g_fwd_d256;
+  if (on == 0 || on == 1) g_fwd_d256 = on;
   return old;
 }
