@@ -253,8 +253,9 @@ __global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T
 // measurement builds, compiled only with -DLTA_ATTN_DIAG.
 int g_fwd_impl = 10;
 // D = 256 without mask / dropout: 1 = the LDS-DMA ring kernel (attention_fwd_d256.hip), 0 = the
-// generic kernel below (A/B: lta_attn_fwd_set_d256)
-int g_fwd_d256 = 1;
+// generic kernel below (A/B: lta_attn_fwd_set_ring; a D = 64 port of the ring kernel measured no faster
+// than the generic kernel, profiles/attn_d256_bench.txt)
+int g_fwd_ring = 1;
 
 template <typename T, int D, int EX>
 int launch_ex(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
@@ -330,7 +331,7 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
                                    stream);
     if (rc != -1) return rc;
   }
-  if (D == 256 && exf == 0 && g_fwd_d256) {  // LDS-DMA ring kernel (attention_fwd_d256.hip)
+  if (D == 256 && exf == 0 && g_fwd_ring) {  // LDS-DMA ring kernel (attention_fwd_d256.hip)
     const int rc = lta_attn_fwd_d256(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides,
                                      qkv_strides, stream);
     if (rc != -1) return rc;
@@ -377,8 +378,8 @@ LTA_EXPORT int lta_attn_fwd_set_impl(int impl) {
 }
 
 // D = 256 forward kernel selection (A/B measurement hook): 1 = LDS-DMA ring kernel, 0 = generic
-LTA_EXPORT int lta_attn_fwd_set_d256(int on) {
-  const int old = g_fwd_d256;
-  if (on == 0 || on == 1) g_fwd_d256 = on;
+LTA_EXPORT int lta_attn_fwd_set_ring(int on) {
+  const int old = g_fwd_ring;
+  if (on == 0 || on == 1) g_fwd_ring = on;
   return old;
 }

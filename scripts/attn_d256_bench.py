@@ -32,10 +32,10 @@ from lightning_thunder_amd.ops._lib import require
 lib = require()
 for causal in (True, False):
     # generic kernel (the previous D = 256 path) for reference and A/B
-    lib.lta_attn_fwd_set_d256(0)
+    lib.lta_attn_fwd_set_ring(0)
     o0, lse0 = attn_fwd(q, k, v, causal)
     tf0 = timeit(lambda: attn_fwd(q, k, v, causal))
-    lib.lta_attn_fwd_set_d256(1)
+    lib.lta_attn_fwd_set_ring(1)
     o, lse = attn_fwd(q, k, v, causal)
     dmax = (o.float() - o0.float()).abs().max().item()
     dl = (lse - lse0).abs().max().item()
