@@ -136,6 +136,13 @@ __device__ __forceinline__ unsigned rng_k(int k) { return fmix32((unsigned)k * 0
 __device__ __forceinline__ bool rng_keep(const AttnExtra& e, unsigned qterm, unsigned kterm) {
   return fmix32(qterm ^ kterm) >= e.keep_thresh;
 }
+// A tile's key (or query) terms through a wave-private LDS row: lane l writes the term of index
+// base + l, and the 4 indices 8 a + 4 h + {0..3} a lane's accumulator elements 4 a .. 4 a + 3 carry
+// (acc_row) come back as one 16-B read, instead of one hash per element (a wave's LDS write -> read
+// needs no barrier: its LDS operations complete in order).
+__device__ __forceinline__ uint4 rng_tab4(const unsigned* row, int a, int h) {
+  return *reinterpret_cast<const uint4*>(row + 8 * a + 4 * h);
+}
 
 }  // namespace attn
 }  // namespace lta

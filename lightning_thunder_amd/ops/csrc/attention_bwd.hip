@@ -144,6 +144,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   constexpr int BUF = 2 * kQT * C::RSTR + 2 * kQT * C::TSTR;
   __shared__ __attribute__((aligned(16))) short smem[2 * BUF];
   __shared__ float s_lse[2][kQT], s_delta[2][kQT];
+  __shared__ __attribute__((aligned(16))) unsigned s_qterm[2][DROP ? kQT : 4];  // the tile's query terms (dropout)
 
   const int n_kb = (Sk + kKB - 1) / kKB;
   (void)n_kb;
@@ -233,6 +234,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       const bool ok = qbase + tid < Tq;
       s_lse[buf][tid] = ok ? plse * 1.44269504088896340736f : INFINITY;
       s_delta[buf][tid] = ok ? pdel : 0.f;
+      if constexpr (DROP) s_qterm[buf][tid] = rng_q(rng_head(ex, b * Hq + hk * group + it / nq), qbase + tid);
     }
   };
 
@@ -270,11 +272,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
     }
     // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
     [[maybe_unused]] const int hq_it = hk * group + it / nq;
-    [[maybe_unused]] unsigned head_rng = 0, kterm = 0;
-    if constexpr (DROP) {
-      head_rng = rng_head(ex, b * Hq + hq_it);
-      kterm = rng_k(key);
-    }
+    [[maybe_unused]] unsigned kterm = 0;
+    if constexpr (DROP) kterm = rng_k(key);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qr = acc_row(i, h);
@@ -288,7 +287,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       float dp = pacc[i];
       float pd = p;
       if constexpr (DROP) {  // dropped P feeds dV; dS = P (dP_dropped * keep / (1-p) - delta)
-        const bool keep = rng_keep(ex, rng_q(head_rng, qq), kterm);
+        const uint4 qv = rng_tab4(s_qterm[buf], i >> 2, h);  // query terms stashed with the tile
+        const unsigned qw4[4] = {qv.x, qv.y, qv.z, qv.w};
+        const bool keep = rng_keep(ex, qw4[i & 3], kterm);
         pd = keep ? p * ex.keep_scale : 0.f;
         dp = keep ? dp * ex.keep_scale : 0.f;
       }
@@ -837,6 +838,7 @@ __global__ __launch_bounds__(kThreads, (EX || D > 128) ? 1 : 2) void attn_bwd_dq
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[2 * C::BN * C::RSTR + C::BN * C::TSTR];
+  __shared__ __attribute__((aligned(16))) unsigned ktab[DROP ? 4 * C::BN : 4];  // per-wave key terms (dropout)
   short* Kr = smem;                    // [64][RSTR]  K rows (A operand of S^T)
   short* Vr = Kr + C::BN * C::RSTR;      // [64][RSTR]  V rows (A operand of dP^T)
   short* Kt = Vr + C::BN * C::RSTR;      // [64][TSTR]  K image for transposed reads (A of dQ^T)
@@ -933,6 +935,9 @@ __global__ __launch_bounds__(kThreads, (EX || D > 128) ? 1 : 2) void attn_bwd_dq
       }
     }
     const int kbase = t * C::BN;
+    [[maybe_unused]] unsigned* krow = ktab + wave * C::BN;
+    if constexpr (DROP)
+      if (lane < C::BN) krow[lane] = rng_k(kbase + lane);
     if constexpr (MASK) {
 #pragma unroll
       for (int kt = 0; kt < C::NKT; ++kt)
@@ -954,7 +959,9 @@ __global__ __launch_bounds__(kThreads, (EX || D > 128) ? 1 : 2) void attn_bwd_dq
         p = (kk >= Sk || (CAUSAL && kk > qi)) ? 0.f : p;
         float dp = pacc[kt][i];
         if constexpr (DROP) {
-          const bool keep = rng_keep(ex, qterm, rng_k(kk));
+          const uint4 kv = rng_tab4(krow + kt * 32, i >> 2, h);
+          const unsigned kw4[4] = {kv.x, kv.y, kv.z, kv.w};
+          const bool keep = rng_keep(ex, qterm, kw4[i & 3]);
           dp = keep ? dp * ex.keep_scale : 0.f;
         }
         pacc[kt][i] = p * (dp - dlt);  // dS^T

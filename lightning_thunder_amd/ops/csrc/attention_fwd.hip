@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T
   using C = Cfg<D>;
   using F = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) short smem[C::BN * C::KSTR + C::BN * C::VSTR];
+  __shared__ __attribute__((aligned(16))) unsigned ktab[DROP ? 4 * C::BN : 4];  // per-wave key terms (dropout)
   short* Ks = smem;
   short* Vs = smem + C::BN * C::KSTR;
   const __attribute__((address_space(3))) short* Vs3 = (const __attribute__((address_space(3))) short*)Vs;
@@ -188,12 +189,19 @@ __global__ __launch_bounds__(kThreads, Cfg<D>::OCC) void attn_fwd_kernel(const T
     l = l * alpha + rs;
     m = m_new;
     if constexpr (DROP) {  // the normalizer keeps every probability; only P.V sees the dropped ones
+      unsigned* krow = ktab + wave * C::BN;
+      if (lane < C::BN) krow[lane] = rng_k(kbase + lane);
 #pragma unroll
       for (int kt = 0; kt < C::NKT; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const bool keep = rng_keep(ex, qterm, rng_k(kbase + kt * 32 + acc_row(i, h)));
-          sacc[kt][i] = keep ? sacc[kt][i] * ex.keep_scale : 0.f;
+        for (int a = 0; a < 4; ++a) {
+          const uint4 kv = rng_tab4(krow + kt * 32, a, h);
+          const unsigned kk[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool keep = rng_keep(ex, qterm, kk[e]);
+            sacc[kt][4 * a + e] = keep ? sacc[kt][4 * a + e] * ex.keep_scale : 0.f;
+          }
         }
     }
 #pragma unroll
