@@ -1326,22 +1326,20 @@ __device__ __forceinline__ void dqds_steps(f32x16 (&acc)[2][4], s16x4t (&cur)[12
   if constexpr (S + 1 < NSS) dqds_steps<S + 1, NSS, F>(acc, nxt, cur, ka, sa);
 }
 
-template <typename T, bool CAUSAL, int KT = 64, int NST = 3, int OCC = 1>
-__global__ __launch_bounds__(kThreads, OCC) void attn_bwd_dq_ds_kernel(const T* __restrict__ K, const T* __restrict__ dSt,
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_ds_kernel(const T* __restrict__ K, const T* __restrict__ dSt,
                                                                      T* __restrict__ dQ, int Hq, int Hkv, int Tq, int Sk,
                                                                      float scale, QKVStrides sx) {
   using F = typename Frag<T>::type;
   // KT-key tiles, NST-stage ring, NST - 1 tiles in flight (64 x 3 measured best of 64 x 3, 32 x 6,
   // 16 x 10 and two-workgroups-per-CU 32 x 3 / 16 x 6: profiles/attn_dq_from_ds.txt)
+  constexpr int KT = 64, NST = 3;
   constexpr int KIMG = KT * 256, SIMG = KT * 512, STG = KIMG + SIMG;
   constexpr int NK = KT / 16, NS = KT / 8;  // LDS-DMA instructions per wave per tile: K, dS^T
-  static_assert(KT % 16 == 0 && NST >= 2 && NST <= 10 && NST * STG <= 160 * 1024, "dq_ds tiling");
+  static_assert(KT % 16 == 0 && NST * STG <= 160 * 1024, "dq_ds tiling");
   __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
   const int n_qb = (Tq + 255) / 256;
-  // causal: heavy blocks first; with OCC > 1 co-resident workgroups, the grid's second half walks
-  // light -> heavy again, so blocks y and y + n_qb / 2 (likely on one CU) carry complementary loads
-  const int y = (int)blockIdx.y, half = n_qb / 2;
-  const int qb = !CAUSAL ? y : (OCC == 1 || y < n_qb - half) ? n_qb - 1 - y : y - (n_qb - half);
+  const int qb = CAUSAL ? n_qb - 1 - (int)blockIdx.y : (int)blockIdx.y;  // causal: heavy blocks first
   const int bh = blockIdx.x, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
   const int q0 = qb * 256;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1394,15 +1392,12 @@ __global__ __launch_bounds__(kThreads, OCC) void attn_bwd_dq_ds_kernel(const T* 
   for (int p = 0; p < NST - 1; ++p)
     if (p < nt) issue(p, p);
   for (int t = 0; t < nt; ++t) {
-    // tile t landed: the tiles issued after it (min(nt - 1 - t, NST - 2) of them) may be in flight
-    const int later = min(nt - 1 - t, NST - 2);
-    switch (later) {
-#define LTA_W(n) \
-  case n: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n * (NK + NS)) : "memory"); break;
-      LTA_W(0) LTA_W(1) LTA_W(2) LTA_W(3) LTA_W(4) LTA_W(5) LTA_W(6) LTA_W(7) LTA_W(8)
-#undef LTA_W
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // tile t landed: tile t + 1 (NK + NS pieces per wave) may still be in flight
+    static_assert(NST == 3, "one tile in flight behind the one waited for");
+    if (t + 1 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NK + NS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // ... for every wave; stage (t + NST - 1) % NST (tile t - 1) is free
     if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
     const uint32_t kimg = lds0 + (t % NST) * STG, simg = kimg + KIMG;
