@@ -1366,8 +1366,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_ds_kernel(const T* __
     for (int i = 0; i < NS; ++i) {
       const int R = (KT / 4) * wave + 2 * i + (lane >> 5), slot = lane & 31, c = slot ^ ((R & 3) << 2);
       // columns past Tq of a partial last block were never written: they only reach unstored dQ rows
+      // dS is read exactly once: nontemporal (aux nt), so it streams past the L2 that keeps K
       __builtin_amdgcn_global_load_lds((const void*)(Sb + (int64_t)(t * KT + R) * 256 + c * 8),
-                                       (lds_void*)(simg + (NS * wave + i) * 1024), 16, 0, 0);
+                                       (lds_void*)(simg + (NS * wave + i) * 1024), 16, 0, 2);
     }
   };
   // transposed fragments (keys 16 s + 4 hh + {0..3, 8..11} of 32-column block `blk`) of the
