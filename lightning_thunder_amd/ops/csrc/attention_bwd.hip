@@ -47,8 +47,20 @@ __global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__
   const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 8;
   const int sub = threadIdx.x & 7;
   float acc = 0.f;
+  // row order: heads fastest when dO is stored token-major ([B, T, H, D], the output projection's
+  // layout), so a wave's 8 rows are 2 KiB of contiguous memory rather than 8 rows 8 KiB apart
+  const bool hfast = sdo.h < sdo.t;
+  int64_t t = 0, hh = 0, bb = 0;
+  if (hfast) {
+    hh = row % H;
+    t = (row / H) % Tq;
+    bb = row / ((int64_t)H * Tq);
+  } else {
+    t = row % Tq;
+    hh = (row / Tq) % H;
+    bb = row / ((int64_t)H * Tq);
+  }
   if (row < rows) {
-    const int64_t t = row % Tq, bh = row / Tq, hh = bh % H, bb = bh / H;
     const T* a = dO + bb * sdo.b + hh * sdo.h + t * sdo.t;
     const T* b = O + bb * so.b + hh * so.h + t * so.t;
 #pragma unroll
@@ -61,7 +73,7 @@ __global__ __launch_bounds__(256) void attn_bwd_preprocess(const T* __restrict__
   acc += __shfl_xor(acc, 1, 64);
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
-  if (row < rows && sub == 0) delta[row] = acc;
+  if (row < rows && sub == 0) delta[(bb * H + hh) * Tq + t] = acc;
 }
 
 // dK^T / dV^T accumulate in the accumulator (AGPR) file through inline-asm MFMAs: they are only
