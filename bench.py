@@ -65,10 +65,13 @@ def parse_args():
     p.add_argument("--n-layer", type=int, default=None, help="override layer count (debug only; invalid for the headline)")
     p.add_argument("--eager-baseline", default="auto", choices=["auto", "on", "off"],
                    help="also time PyTorch eager on the same config for speedup_vs_eager (auto: on for the 1-GPU "
-                        "thunder run; a short segment of --eager-steps after --eager-warmup, outside thunder's "
-                        "timed region)")
-    p.add_argument("--eager-steps", type=int, default=5)
-    p.add_argument("--eager-warmup", type=int, default=2)
+                        "thunder run; --eager-warmup + --eager-steps from the same init and data, outside "
+                        "thunder's timed region; both per-step loss curves go into the JSON line)")
+    p.add_argument("--eager-steps", type=int, default=None, help="default: --steps (same loss-curve length)")
+    p.add_argument("--eager-warmup", type=int, default=None, help="default: --warmup")
+    p.add_argument("--lr", type=float, default=3e-4)
+    p.add_argument("--lr-warmup", type=int, default=0,
+                   help="linear learning-rate warmup over this many optimizer steps (0: constant --lr)")
     p.add_argument("--profile-dir", default=None)
     return p.parse_args()
 
@@ -95,15 +98,15 @@ def build_model(args, device):
     return model, cfg
 
 
-def make_optimizer(params, mode="eager"):
+def make_optimizer(params, mode="eager", lr=3e-4):
     if mode == "thunder" and os.environ.get("LTA_TORCH_ADAMW") != "1":
         from lightning_thunder_amd.optim import AdamW
 
-        return AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)  # fused multi-tensor HIP kernel
+        return AdamW(params, lr=lr, betas=(0.9, 0.95), weight_decay=0.1)  # fused multi-tensor HIP kernel
     try:
-        return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
+        return torch.optim.AdamW(params, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
     except (RuntimeError, TypeError):
-        return torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, foreach=True)
+        return torch.optim.AdamW(params, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, foreach=True)
 
 
 def _rccl_record(world):
@@ -188,7 +191,7 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
 
             fwd = DistributedDataParallel(model, device_ids=[device.index])
         params = list(model.parameters())
-    opt = make_optimizer(params, mode)
+    opt = make_optimizer(params, mode, args.lr)
     overlap = args.optim_overlap == "on" or (args.optim_overlap == "auto" and world == 1 and not _force_dist())
     if mode == "thunder" and overlap and not args.hipgraph and hasattr(opt, "overlap_with_backward"):
         # the update still runs inside the timed step: in the backward's shadow, joined by opt.step()
@@ -204,7 +207,14 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
         x = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq + 1), device=device, generator=gen)
         return x[:, :-1].contiguous(), x[:, 1:].contiguous()
 
+    n_step = [0]
+
     def step(x, y):
+        if args.lr_warmup:
+            # host-side only (the fused AdamW kernels take lr as an argument): same schedule both modes
+            for g in opt.param_groups:
+                g["lr"] = args.lr * min(1.0, (n_step[0] + 1) / args.lr_warmup)
+            n_step[0] += 1
         if mode == "thunder":
             loss = fwd(x, y)
         else:
@@ -216,9 +226,12 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
         return loss
 
     data = [batch() for _ in range(4)]
+    # every step's loss stays on the device; .item() only after the timed region (no added syncs)
+    losses = []
     t_first = time.perf_counter()
     for i in range(warmup):
         loss = step(*data[i % 4])
+        losses.append(loss.detach())
         if i == 0:
             torch.cuda.synchronize()
             log(rank, f"[{mode}] first step (incl. compile) {time.perf_counter() - t_first:.1f}s loss={loss.item():.4f}")
@@ -228,7 +241,8 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        loss = step(*data[i % 4])
+        loss = step(*data[(warmup + i) % 4])
+        losses.append(loss.detach())
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -244,8 +258,9 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
 
         log(rank, f"[gemm] calls per backend since start (gemm4 = hand MFMA kernel, torch = library): "
                   f"{_g.last_gemm_backend_counts()}")
-    del model, opt, fwd, params
-    return dt, cfg, mem, parallel
+    curve = [round(v, 4) for v in torch.stack([l.float() for l in losses]).cpu().tolist()]
+    del model, opt, fwd, params, losses, loss
+    return dt, cfg, mem, parallel, curve
 
 
 def main():
@@ -289,7 +304,7 @@ def main():
         else:
             torch.distributed.init_process_group(backend, timeout=timeout)
 
-    dt, cfg, mem, parallel = run(args, rank, world, device, args.mode)
+    dt, cfg, mem, parallel, curve = run(args, rank, world, device, args.mode)
     data_parallel = parallel != "tp"
     tokens = args.steps * args.mbs * args.seq * (world if data_parallel else 1)
     value = tokens / dt
@@ -297,7 +312,7 @@ def main():
     from lightning_thunder_amd.models.litgpt import flops_per_token
 
     tflops = flops_per_token(cfg, args.seq) * per_gpu / 1e12
-    speedup = eager_ms = None
+    speedup = eager_ms = curve_eager = None
     want_eager = args.eager_baseline == "on" or (args.eager_baseline == "auto" and world == 1 and not _force_dist()
                                                  and not args.lora)
     if want_eager and args.mode == "thunder":
@@ -305,8 +320,10 @@ def main():
         # thunder's timed region; thunder's model and optimizer state are freed first
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
-        dte, _, _, _ = run(args, rank, world, device, "eager", steps=args.eager_steps, warmup=args.eager_warmup)
-        eager_ms = dte / args.eager_steps * 1000
+        esteps = args.steps if args.eager_steps is None else args.eager_steps
+        ewarm = args.warmup if args.eager_warmup is None else args.eager_warmup
+        dte, _, _, _, curve_eager = run(args, rank, world, device, "eager", steps=esteps, warmup=ewarm)
+        eager_ms = dte / esteps * 1000
         speedup = eager_ms / (dt / args.steps * 1000)
     base = BASELINE_TOKENS_PER_SEC_PER_GPU_1 if world == 1 else BASELINE_TOKENS_PER_SEC_PER_GPU_FSDP
     if rank == 0:
@@ -341,6 +358,11 @@ def main():
             "speedup_vs_eager": None if speedup is None else round(speedup, 3),
             "rccl": _rccl_record(world),
             "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 3),
+            "lr": args.lr,
+            "lr_warmup_steps": args.lr_warmup,
+            # per-step training loss (warmup steps first) from identical init and data
+            "loss_curve_" + args.mode: curve,
+            "loss_curve_eager": curve_eager if args.mode == "thunder" else curve,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

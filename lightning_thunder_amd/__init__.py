@@ -186,6 +186,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
 
     cs.last_trace_tracing_start = time.perf_counter_ns()
     tok = _compile_data_ctx.set(cd)
+    from .core.symbolic import ShapeEnv, current_env, _env as _shape_env_var
+
+    senv = ShapeEnv() if cd.cache_option is CACHE_OPTIONS.SYMBOLIC_VALUES else None
+    senv_tok = _shape_env_var.set(senv)
     try:
         lookasides = {}
         python_lookasides = []
@@ -261,8 +265,10 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
             fb = forward_and_backward_from_trace(comp, executors=executors)
             if cd.compile_options.get("rematerialize", True):
                 from .transforms.rematerialization import rematerialize_forward_and_backward
+                from .core.symbolic import no_guards
 
-                fb = rematerialize_forward_and_backward(fb)
+                with no_guards():  # a cut is valid for every size: its weights record no shape guards
+                    fb = rematerialize_forward_and_backward(fb)
             from .distributed.utils import lower_tp_syncs
 
             fw_traces = [fb.forward_trace] + transform_for_execution(lower_tp_syncs(fb.forward_trace), executors)
@@ -346,7 +352,24 @@ def _build_cache_entry(cd: CompileData, cs: CompileStats, module, args, kwargs) 
                 return _base(fa, *rest)
 
             entry.prologue_fn = prologue_with_late_checks
+        if senv is not None and senv.symbols:
+            # symbolic tensor dims: the prologue checked ranks and static dims; the guards recorded
+            # while tracing, transforming and claiming (core/symbolic.py) decide the rest
+            from .executors.pythonex import ThunderCacheMiss
+
+            guards = senv.guard_fn()
+            base2 = entry.prologue_fn
+
+            def prologue_with_shape_guards(fa, *rest, _base=base2, _g=guards):
+                out = _base(fa, *rest)
+                if not _g(fa):
+                    raise ThunderCacheMiss("symbolic shape guards")
+                return out
+
+            entry.prologue_fn = prologue_with_shape_guards
+            entry.shape_guards = guards
     finally:
+        _shape_env_var.reset(senv_tok)
         _compile_data_ctx.reset(tok)
         _torch.set_grad_enabled(entry.grad_enabled)
     return entry

@@ -16,6 +16,7 @@ import torch
 
 from ..core import dtypes, prims
 from ..core.baseutils import check
+from ..core.symbolic import unify
 from ..core.devices import to_device
 from ..core.proxies import TensorProxy, NumberProxy, pyval
 
@@ -151,7 +152,11 @@ def compute_broadcast_shape(*shapes):
             cur = out[off + i]
             if cur == 1:
                 out[off + i] = d
-            elif d != 1 and d != cur:
+            elif d == 1:
+                continue
+            elif d == cur:
+                out[off + i] = unify(cur, d)
+            else:
                 raise RuntimeError(f"Shapes {shapes} are not broadcastable")
     return tuple(out)
 
@@ -174,7 +179,7 @@ def expand(a, *shape):
                 final.append(cur)
             else:
                 check(cur == 1 or cur == s, lambda: f"expand: cannot expand {a.shape} to {shape}")
-                final.append(s)
+                final.append(s if cur == 1 else unify(s, cur))
     final = tuple(final)
     if final == tuple(a.shape):
         return a

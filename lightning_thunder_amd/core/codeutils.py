@@ -7,6 +7,8 @@ by name, so every trace stays executable Python.
 from __future__ import annotations
 
 import math
+from contextlib import contextmanager
+from contextvars import ContextVar
 from enum import Enum
 from numbers import Number
 from typing import Any
@@ -14,6 +16,37 @@ from typing import Any
 import torch
 
 from .proxies import Proxy, NumberProxy
+from .symbolic import SymInt
+
+# symbols the program being printed binds from its arguments (None: not printing a program — show
+# every expression); a SymInt over any other symbol is printed as its value and specialized
+_bindable: ContextVar = ContextVar("lta_bindable_syms", default=None)
+
+
+_used: ContextVar = ContextVar("lta_used_syms", default=None)
+
+
+@contextmanager
+def bindable_symbols(names, used: set | None = None):
+    """Prints SymInts over ``names`` as expressions (collecting the symbols printed into ``used``)."""
+    tok = _bindable.set(set(names))
+    tok2 = _used.set(used)
+    try:
+        yield
+    finally:
+        _used.reset(tok2)
+        _bindable.reset(tok)
+
+
+def _print_symint(x: SymInt) -> str:
+    ok = _bindable.get()
+    free = x.free_symbols()
+    if ok is None or free <= ok:
+        used = _used.get()
+        if used is not None:
+            used.update(free)
+        return x.expr
+    return repr(int(x))  # int() specializes the program on this value
 
 
 class ContextObject:
@@ -53,6 +86,8 @@ def prettyprint(x: Any, obj_ctx: dict[str, Any] | None = None, *, with_type: boo
         return "..."
     if isinstance(x, bool):
         return repr(x)
+    if isinstance(x, SymInt):
+        return _print_symint(x)
     if isinstance(x, int):
         return repr(x)
     if isinstance(x, float):

@@ -1284,6 +1284,8 @@ for _n, (_b, _i) in _BINOPS.items():
 def _binary_subscr(interp, f, arg, argval, target):
     k, pk = f.popp()
     c, pc = f.popp()
+    if isinstance(c, dict) and _is_number_proxy(k):
+        k = k.concrete()  # a symbolic number used as a dict key: the program is specialized on it
     v = c[k]
     p = None
     pc = interp.mprov(c, pc)
@@ -2142,3 +2144,9 @@ def interpret(fn: Callable, **interp_kwargs) -> Callable:
 
     wrapper.last_interpreter = None
     return wrapper
+
+
+def _is_number_proxy(x) -> bool:
+    from .proxies import NumberProxy
+
+    return isinstance(x, NumberProxy)

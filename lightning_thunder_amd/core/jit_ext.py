@@ -29,6 +29,7 @@ from .pytree import tree_flatten, tree_unflatten, tree_map
 from .trace import TraceCtx, tracectx, get_tracectx, TraceProvenance
 from .symbol import BoundSymbol
 from .functionalization import AliasTracker, storage_alias_pattern
+from .symbolic import current_env
 
 
 # -----------------------------------------------------------------------------------------
@@ -222,6 +223,7 @@ class AcquiredProgram:
         self.n_instructions = 0
         self.symbolic_args: dict[int, NumberProxy] = {}  # flat-arg index -> symbolic number input
         self.specialized_args: set[int] = set()  # symbolic inputs whose value the program read
+        self.symbolic_shapes: dict[int, tuple] = {}  # flat-arg index -> shape pattern (None = symbolic dim)
 
 
 def acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module | None = None,
@@ -355,6 +357,12 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
         for i, x in enumerate(flat_args):
             if isinstance(x, torch.Tensor):
                 p = tensorproxy(x)
+                env = current_env()
+                if symbolic_numbers and env is not None and not isinstance(x, torch.nn.Parameter) and x.ndim:
+                    # cache="symbolic values": every dim >= 2 of a non-parameter tensor argument is a
+                    # symbol (core/symbolic.py); 0 / 1 stay static (broadcasting depends on them)
+                    p._shape = tuple(env.new_symbol(n, i, d) if n >= 2 else n for d, n in enumerate(x.shape))
+                    prog.symbolic_shapes[i] = tuple(None if n >= 2 else n for n in x.shape)
                 arg_proxies.append((i, p))
                 proxied_flat.append(p)
                 prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
@@ -690,7 +698,9 @@ def build_prologue(prog: AcquiredProgram, flat_args: list, *, prune_param_checks
         unpacked = prims.unpack_sequence(fa, n)
         for i, (u, x) in enumerate(zip(unpacked, flat_args)):
             if isinstance(x, torch.Tensor):
-                prims.check_tensor_shape_and_metadata(u, tuple(x.shape), str(x.device), x.dtype, x.requires_grad)
+                # symbolic dims are checked by the guards of the cache entry (core/symbolic.py)
+                shape = prog.symbolic_shapes.get(i, tuple(x.shape))
+                prims.check_tensor_shape_and_metadata(u, shape, str(x.device), x.dtype, x.requires_grad)
             elif x is None:
                 prims.check_none(u)
             elif isinstance(x, str):

@@ -21,6 +21,7 @@ from . import dtypes
 from .baseutils import check
 from .codeutils import prettyprint
 from .devices import to_device
+from .symbolic import SymInt, unify_shapes
 from .proxies import Proxy, TensorProxy, NumberProxy, AnyProxy, FutureTensorProxy, pyval, contiguous_strides
 from .symbol import Symbol, register_symbol, NON_DIFFERENTIABLE_TAG
 from . import proxies as _proxies
@@ -291,6 +292,7 @@ def _check_same_shape(*args):
     shape = ts[0].shape
     for t in ts[1:]:
         check(t.shape == shape, lambda: f"Expected same shape, got {shape} and {t.shape}")
+        shape = unify_shapes(shape, t.shape)
     return shape
 
 
@@ -585,7 +587,7 @@ tensor_from_sequence = make_prim(PrimIDs.TENSOR_FROM_SEQUENCE, "tensor_from_sequ
 # Shape ops
 # -----------------------------------------------------------------------------------------
 def _broadcast_in_dim_meta(a, shape, broadcast_dimensions):
-    shape = tuple(int(s) for s in shape)
+    shape = tuple(s if isinstance(s, SymInt) else int(s) for s in shape)
     check(len(broadcast_dimensions) == a.ndim, lambda: f"broadcast_in_dim: {broadcast_dimensions} vs ndim {a.ndim}")
     for i, d in enumerate(broadcast_dimensions):
         check(a.shape[i] == shape[d] or a.shape[i] == 1, lambda: f"Cannot broadcast {a.shape} to {shape}")
@@ -632,7 +634,7 @@ pad = make_prim(PrimIDs.PAD, "pad", meta=_pad_meta)
 
 
 def _reshape_meta(a, shape):
-    shape = tuple(int(s) for s in shape)
+    shape = tuple(s if isinstance(s, SymInt) else int(s) for s in shape)
     check(math.prod(shape) == math.prod(a.shape), lambda: f"Cannot reshape {a.shape} to {shape}")
     return TensorProxy(like=a, shape=shape)
 
@@ -791,11 +793,25 @@ cumsum = make_prim(PrimIDs.CUMSUM, "cumsum", meta=_cumsum_meta)
 # Linear algebra / NN
 # -----------------------------------------------------------------------------------------
 def _matmul_meta(a, b):
-    ta = torch.empty(a.shape, dtype=a.dtype, device="meta")
-    tb = torch.empty(b.shape, dtype=b.dtype, device="meta")
-    out = torch.matmul(ta, tb)
+    # torch.matmul's shape rules written out (a meta-device call would turn symbolic dims into ints)
+    check(a.ndim >= 1 and b.ndim >= 1, "matmul: both arguments need at least one dimension")
+    check(a.dtype == b.dtype, lambda: f"matmul: dtype mismatch {a.dtype} vs {b.dtype}")
     device = _check_same_device(a, b)
-    return TensorProxy(shape=tuple(out.shape), device=device, dtype=out.dtype)
+    ka = a.shape[-1]
+    kb = b.shape[0] if b.ndim == 1 else b.shape[-2]
+    check(ka == kb, lambda: f"matmul: {tuple(a.shape)} @ {tuple(b.shape)} shape mismatch")
+    if a.ndim == 1 and b.ndim == 1:
+        shape = ()
+    elif b.ndim == 1:
+        shape = tuple(a.shape[:-1])
+    elif a.ndim == 1:
+        shape = tuple(b.shape[:-2]) + (b.shape[-1],)
+    else:
+        from ..clang import compute_broadcast_shape
+
+        batch = compute_broadcast_shape(tuple(a.shape[:-2]), tuple(b.shape[:-2])) or ()
+        shape = tuple(batch) + (a.shape[-2], b.shape[-1])
+    return TensorProxy(shape=shape, device=device, dtype=a.dtype)
 
 
 matmul = make_prim(PrimIDs.MATMUL, "matmul", meta=_matmul_meta, tags=(OpTags.MATMUL_OP,))

@@ -21,6 +21,8 @@ from . import dtypes
 from .devices import to_device, device_str
 
 
+from .symbolic import SymInt, make_shape
+
 class DistParallelType(Enum):
     NONE = auto()
     REPLICATED = auto()
@@ -299,7 +301,8 @@ class TensorProxy(Proxy):
                 distparallel_type = getattr(like, "distparallel_type", None)
             if thunder_fsdp_padding_size is None:
                 thunder_fsdp_padding_size = getattr(like, "thunder_fsdp_padding_size", None)
-        self._shape = tuple(int(s) for s in shape)
+        # symbolic dims (cache="symbolic values", core/symbolic.py) stay SymInts; everything else is a plain int
+        self._shape = tuple(s if isinstance(s, SymInt) else int(s) for s in shape)
         self._device = to_device(device)
         self._dtype = dtypes.to_torch_dtype(dtype)
         self.requires_grad = bool(requires_grad) if requires_grad is not None else False
@@ -310,7 +313,7 @@ class TensorProxy(Proxy):
     # --- metadata -----------------------------------------------------------------
     @property
     def shape(self):
-        return torch.Size(self._shape)
+        return make_shape(self._shape)
 
     @property
     def device(self) -> torch.device:
@@ -331,14 +334,15 @@ class TensorProxy(Proxy):
 
     @property
     def numel(self):  # reference exposes numel as a property; calls go through _NumelInt
-        return _CallableInt(math.prod(self._shape))
+        n = math.prod(self._shape)
+        return n if isinstance(n, SymInt) else _CallableInt(n)
 
     def nelement(self):
         return math.prod(self._shape)
 
     def size(self, dim: int | None = None):
         if dim is None:
-            return torch.Size(self._shape)
+            return make_shape(self._shape)
         return self._shape[dim]
 
     def stride(self, dim: int | None = None):
@@ -355,6 +359,10 @@ class TensorProxy(Proxy):
     @property
     def nbytes(self) -> int:
         return math.prod(self._shape) * dtypes.itemsize(self._dtype)
+
+    @property
+    def is_symbolic(self) -> bool:
+        return any(isinstance(s, SymInt) for s in self._shape)
 
     @property
     def is_cuda(self) -> bool:
@@ -426,11 +434,14 @@ class TensorProxy(Proxy):
         )
         return TensorProxy(changes.get("name"), **kw)
 
+    def _shape_str(self) -> str:
+        return "[" + ", ".join(s.expr if isinstance(s, SymInt) else repr(s) for s in self._shape) + "]"
+
     def type_string(self) -> str:
-        return f"{device_str(self._device)} {dtypes.short_name(self._dtype)}{list(self._shape)}"
+        return f"{device_str(self._device)} {dtypes.short_name(self._dtype)}{self._shape_str()}"
 
     def __repr__(self):
-        return f'<TensorProxy(name="{self.name}", dtype={self._dtype}, shape={self._shape}, device={self._device})>'
+        return f'<TensorProxy(name="{self.name}", dtype={self._dtype}, shape={self._shape_str()}, device={self._device})>'
 
     # --- torch interop ---------------------------------------------------------------
     @classmethod
@@ -555,14 +566,15 @@ class FutureTensorProxy(Proxy):
             shape = like.shape if shape is None else shape
             device = like.device if device is None else device
             dtype = like.dtype if dtype is None else dtype
-        self._shape = tuple(int(s) for s in shape)
+        # symbolic dims (cache="symbolic values", core/symbolic.py) stay SymInts; everything else is a plain int
+        self._shape = tuple(s if isinstance(s, SymInt) else int(s) for s in shape)
         self._device = to_device(device)
         self._dtype = dtype
         self.requires_grad = False
 
     @property
     def shape(self):
-        return torch.Size(self._shape)
+        return make_shape(self._shape)
 
     @property
     def dtype(self):
@@ -586,7 +598,7 @@ class FutureTensorProxy(Proxy):
         )
 
     def type_string(self):
-        return f"FUTURE {device_str(self._device)} {dtypes.short_name(self._dtype)}{list(self._shape)}"
+        return f"FUTURE {device_str(self._device)} {dtypes.short_name(self._dtype)}{TensorProxy._shape_str(self)}"
 
     def wait(self):
         from ..distributed import prims as dist_prims
@@ -599,7 +611,7 @@ def contiguous_strides(shape) -> tuple[int, ...]:
     acc = 1
     for s in reversed(tuple(shape)):
         strides.append(acc)
-        acc *= max(int(s), 1)
+        acc = acc * (s if isinstance(s, SymInt) else max(int(s), 1))  # symbolic dims are >= 2
     return tuple(reversed(strides))
 
 

@@ -16,7 +16,7 @@ from contextvars import ContextVar
 from typing import Any, Callable
 
 from .baseutils import build_callable
-from .codeutils import prettyprint, sanitize_name
+from .codeutils import prettyprint, sanitize_name, bindable_symbols
 from .proxies import Proxy, TensorProxy
 
 _tracectx: ContextVar = ContextVar("tracectx", default=None)
@@ -198,9 +198,16 @@ class TraceCtx:
         for a in self.args:
             if isinstance(a, Proxy):
                 lines.append(f'  # {a.name}: "{a.type_string()}"')
+        # symbolic dims (cache="symbolic values"): bound from this program's own tensor arguments
+        binds = _symbol_bindings(self.args)
         body = []
-        for bsym in self.bound_symbols:
-            body.extend(bsym.python(indent=1, print_depth=print_depth, obj_ctx=obj_ctx))
+        used: set = set()
+        with bindable_symbols(binds.keys(), used):
+            for bsym in self.bound_symbols:
+                body.extend(bsym.python(indent=1, print_depth=print_depth, obj_ctx=obj_ctx))
+        for sym, (arg, d) in binds.items():
+            if sym in used:
+                lines.append(f"  {sym} = {arg}.shape[{d}]")
         if not body:
             body = ["  pass"]
         lines.extend(body)
@@ -233,6 +240,19 @@ class TraceCtx:
 
     def __str__(self) -> str:
         return self.python()
+
+
+def _symbol_bindings(args) -> dict:
+    """symbol -> (argument name, dim) for every symbolic dim a tensor argument carries bare."""
+    from .symbolic import SymInt
+
+    out: dict = {}
+    for a in args:
+        if isinstance(a, TensorProxy):
+            for d, s in enumerate(a._shape):
+                if isinstance(s, SymInt) and s.expr.isidentifier() and s.expr not in out:
+                    out[s.expr] = (a.name, d)
+    return out
 
 
 def _iter_all_bsyms(bsyms):

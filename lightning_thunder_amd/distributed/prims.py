@@ -518,6 +518,8 @@ def _vp_ce_hand_kernels(logits) -> bool:
     exp, reductions and the one-hot scatter over the whole [tokens, V / world] slice."""
     if not logits.is_cuda or logits.dtype not in (torch.bfloat16, torch.float16, torch.float32) or logits.dim() != 2:
         return False
+    if logits.shape[0] == 0 or logits.shape[1] == 0:
+        return False  # an empty shard: a 0-workgroup launch is an invalid configuration; ATen handles it
     try:
         from ..ops._lib import require
 

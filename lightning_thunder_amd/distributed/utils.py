@@ -16,6 +16,24 @@ from ..core.symbol import BoundSymbol
 from ..core.trace import TraceCtx, from_trace, TraceProvenance
 
 
+# ops that always hand back a freshly allocated tensor (never their input or a view of it): the only
+# producers whose output a tensor-parallel all-reduce may reduce in place (skip_clone)
+_FRESH_PRODUCERS = frozenset({
+    "linear", "matmul", "mm", "bmm", "embedding", "add", "sub", "mul", "div", "true_divide", "neg", "silu", "gelu",
+    "relu", "tanh", "sigmoid", "exp", "sum", "where", "scaled_dot_product_attention", "cat", "rms_norm",
+    "layer_norm", "softmax", "baddbmm", "addmm",
+})
+
+
+def allocates_fresh(b: BoundSymbol) -> bool:
+    """True when ``b`` is known to allocate its outputs (allowlist, so an unknown op — a future
+    conversion or identity op that may return its input — is never reduced in place)."""
+    nm = str(getattr(b.sym, "name", ""))
+    base = nm[:-5] if nm.endswith("_prim") else nm
+    base = base.rsplit(".", 1)[-1]
+    return base in _FRESH_PRODUCERS
+
+
 def lower_tp_syncs(trace: TraceCtx) -> TraceCtx:
     """Tensor-parallel syncs -> explicit async collectives + ``wait`` (reference: the TP prims issue
     ``all_reduce(..., do_async=True, skip_clone=True).wait()`` / ``all_gather(..., True).wait()``,
@@ -26,15 +44,13 @@ def lower_tp_syncs(trace: TraceCtx) -> TraceCtx:
     * all-reduce syncs (row-parallel output, vocab-parallel embedding output, and the column-parallel
       input gradient, which the VJP expresses as the same sync) -> ``all_reduce(a, SUM, group, True,
       skip_clone)`` + ``wait``; the all-reduce runs in place (no clone) when ``a`` is a fresh tensor
-      nothing else reads: not a trace input or output, read only by this sync, and not made by an op
-      that may return (a view of) its input;
+      nothing else reads: not a trace input or output, read only by this sync, and made by an op on
+      the :func:`allocates_fresh` allowlist (GEMMs, embedding, elementwise math);
     * last-dim all-gather syncs (column-parallel output) -> ``all_gather(a, group, True, -1)`` + ``wait``;
     * the input-side syncs (identity / local slice) stay as they are.
     Run on the traces right after autodiff, before the executors claim them."""
     from .prims import (synchronize_tensor_parallel_output as tp_out, TPLayerType, all_reduce, all_gather, wait,
                         DistributedReduceOps)
-    from ..transforms.optimizer_overlap import may_alias_bsym
-    from ..core.proxies import TensorProxy
     from ..core.trace import tracectx
 
     bsyms = list(trace.bound_symbols)
@@ -62,7 +78,7 @@ def lower_tp_syncs(trace: TraceCtx) -> TraceCtx:
             if kind in (TPLayerType.ROW_LINEAR, TPLayerType.COLUMN_EMBED):
                 prod = producer.get(a.name)
                 fresh = (a.name not in inputs and readers.get(a.name, 0) == 1 and prod is not None
-                         and not may_alias_bsym(prod))
+                         and allocates_fresh(prod))
                 fut = all_reduce.bind(a, DistributedReduceOps.SUM, group, True, fresh,
                                       output=all_reduce.meta(a, DistributedReduceOps.SUM, group, True, fresh))
             else:

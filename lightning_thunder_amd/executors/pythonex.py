@@ -46,7 +46,11 @@ def _unpack_key(d, k):
 def _check_tensor(t, shape, device, dtype, requires_grad):
     if not isinstance(t, torch.Tensor):
         raise ThunderCacheMiss(f"expected a tensor, got {type(t)}")
-    if tuple(t.shape) != shape or t.dtype != dtype or str(t.device) != device or t.requires_grad != requires_grad:
+    if None in shape:  # symbolic dims (cache="symbolic values"): rank and static dims here
+        ok = t.ndim == len(shape) and all(n is None or n == m for n, m in zip(shape, t.shape))
+    else:
+        ok = tuple(t.shape) == shape
+    if not ok or t.dtype != dtype or str(t.device) != device or t.requires_grad != requires_grad:
         raise ThunderCacheMiss(
             f"tensor metadata mismatch: {tuple(t.shape)},{t.dtype},{t.device},{t.requires_grad} vs {shape},{dtype},{device},{requires_grad}"
         )

@@ -48,6 +48,9 @@ class Config:
     tie_embeddings: bool = False
     n_expert: int = 0
     n_expert_per_token: int = 0
+    # Gemma: token embeddings scaled by sqrt(n_embd), RMSNorm scale (1 + weight)
+    scale_embeddings: bool = False
+    norm_unit_offset: bool = False
 
     def __post_init__(self):
         if self.head_size is None:
@@ -88,6 +91,24 @@ configs = [
     # Mistral
     Config(name="Mistral-7B-v0.1", block_size=4096, vocab_size=32000, padded_vocab_size=32000, n_layer=32, n_head=32,
            n_embd=4096, n_query_groups=8, intermediate_size=14336),
+    Config(name="Mistral-7B-v0.2", block_size=32768, vocab_size=32000, padded_vocab_size=32000, n_layer=32, n_head=32,
+           n_embd=4096, n_query_groups=8, intermediate_size=14336, rope_base=1000000),
+    # Google Gemma (the reference's multi-model chart and GemmaMLP target, BASELINE.md:26):
+    # head_size 256 (n_head * head_size != n_embd), GeGLU (tanh) MLP, scaled embeddings, (1 + w) RMSNorm
+    Config(name="Gemma-2b", block_size=8192, vocab_size=256000, padding_multiple=64, n_layer=18, n_head=8,
+           n_query_groups=1, n_embd=2048, head_size=256, intermediate_size=16384, mlp_class_name="GemmaMLP",
+           gelu_approximate="tanh", scale_embeddings=True, norm_unit_offset=True, norm_eps=1e-6, tie_embeddings=True),
+    Config(name="Gemma-7b", block_size=8192, vocab_size=256000, padding_multiple=64, n_layer=28, n_head=16,
+           n_query_groups=16, n_embd=3072, head_size=256, intermediate_size=24576, mlp_class_name="GemmaMLP",
+           gelu_approximate="tanh", scale_embeddings=True, norm_unit_offset=True, norm_eps=1e-6, tie_embeddings=True),
+    # Microsoft Phi-3
+    Config(name="Phi-3-mini-4k-instruct", block_size=4096, vocab_size=32064, padded_vocab_size=32064, n_layer=32,
+           n_head=32, n_embd=3072, intermediate_size=8192, norm_eps=1e-5),
+    # Llama-1-architecture fine-tunes of the chart
+    Config(name="Nous-Hermes-13b", block_size=2048, vocab_size=32000, padded_vocab_size=32001, n_layer=40, n_head=40,
+           n_embd=5120, intermediate_size=13824, norm_eps=1e-6),
+    Config(name="Platypus-30B", block_size=2048, vocab_size=32000, padded_vocab_size=32000, n_layer=60, n_head=52,
+           n_embd=6656, intermediate_size=17920, norm_eps=1e-6),
     # CodeLlama
     Config(name="CodeLlama-34b-hf", block_size=16384, vocab_size=32000, padded_vocab_size=32000, n_layer=48, n_head=64,
            n_embd=8192, n_query_groups=8, intermediate_size=22016, rope_base=1000000),
@@ -107,6 +128,9 @@ configs = [
            intermediate_size=512, mlp_class_name="LLaMAMoE", n_expert=4, n_expert_per_token=2),
     Config(name="llama2-7b-shape-2l", vocab_size=32000, padding_multiple=64, n_layer=2, n_head=32, n_embd=4096,
            intermediate_size=11008),
+    Config(name="gemma-like", vocab_size=320, padding_multiple=64, n_layer=2, n_head=2, n_query_groups=1, n_embd=64,
+           head_size=256, intermediate_size=128, block_size=128, mlp_class_name="GemmaMLP", gelu_approximate="tanh",
+           scale_embeddings=True, norm_unit_offset=True, norm_eps=1e-6, tie_embeddings=True),
 ]
 name_to_config = {c.name: c for c in configs}
 
@@ -153,22 +177,27 @@ def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 class RMSNorm(nn.Module):
-    def __init__(self, size: int, dim: int = -1, eps: float = 1e-6):
+    """RMSNorm; ``add_unit_offset`` (Gemma) scales by ``1 + weight`` with the weight initialised to
+    zero, so the stored parameter is the deviation from identity."""
+
+    def __init__(self, size: int, dim: int = -1, eps: float = 1e-6, add_unit_offset: bool = False):
         super().__init__()
-        self.weight = nn.Parameter(torch.ones(size))
+        self.add_unit_offset = add_unit_offset
+        self.weight = nn.Parameter(torch.zeros(size) if add_unit_offset else torch.ones(size))
         self.eps = eps
         self.dim = dim
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return F.rms_norm(x, (x.shape[-1],), self.weight, self.eps)
+        w = self.weight + 1.0 if self.add_unit_offset else self.weight
+        return F.rms_norm(x, (x.shape[-1],), w, self.eps)
 
     def reset_parameters(self) -> None:
-        nn.init.ones_(self.weight)
+        (nn.init.zeros_ if self.add_unit_offset else nn.init.ones_)(self.weight)
 
 
 def _norm(config: Config, size: int) -> nn.Module:
     if config.norm_class_name == "RMSNorm":
-        return RMSNorm(size, eps=config.norm_eps)
+        return RMSNorm(size, eps=config.norm_eps, add_unit_offset=config.norm_unit_offset)
     return nn.LayerNorm(size, eps=config.norm_eps)
 
 
@@ -228,6 +257,26 @@ class LLaMAMLP(nn.Module):
         x_fc_1 = self.fc_1(x)
         x_fc_2 = self.fc_2(x)
         return self.proj(swiglu(x_fc_1, x_fc_2))
+
+
+def geglu(a: torch.Tensor, b: torch.Tensor, approximate: str = "tanh") -> torch.Tensor:
+    """Gemma MLP gate: gelu(a) * b."""
+    return F.gelu(a, approximate=approximate) * b
+
+
+class GemmaMLP(nn.Module):
+    """LitGPT ``GemmaMLP`` (the reference benchmarks it, thunder/benchmarks/targets.py:578): the
+    LLaMA MLP layout with a GeGLU gate."""
+
+    def __init__(self, config: Config):
+        super().__init__()
+        self.fc_1 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.fc_2 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
+        self.config = config
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.proj(geglu(self.fc_1(x), self.fc_2(x), self.config.gelu_approximate))
 
 
 class GptNeoxMLP(nn.Module):
@@ -294,6 +343,8 @@ class Block(nn.Module):
             self.mlp = LLaMAMLP(config)
         elif config.mlp_class_name == "LLaMAMoE":
             self.mlp = LLaMAMoE(config)
+        elif config.mlp_class_name == "GemmaMLP":
+            self.mlp = GemmaMLP(config)
         else:
             self.mlp = GptNeoxMLP(config)
         self.config = config
@@ -374,6 +425,8 @@ class GPT(nn.Module):
             sin = self.sin[:T]
             mask = None
         x = self.transformer.wte(idx)
+        if self.config.scale_embeddings:
+            x = x * math.sqrt(self.config.n_embd)
         for block in self.transformer.h:
             if self.activation_checkpointing and input_pos is None:
                 # recompute the block's intermediates in the backward (LitGPT / benchmark_litgpt

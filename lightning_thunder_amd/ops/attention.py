@@ -216,15 +216,23 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     return dq, dk, dv, g.to(mask.dtype)
 
 
-def _dq_from_ds(ws_bytes: int) -> bool:
+def _dq_from_ds(ws_bytes: int, device: torch.device | None = None) -> bool:
     """The RoPE'd backward computes dQ from the dS the dK/dV kernel stores (one B Hq T^2 bf16
     workspace, 1 GiB for a Llama-2-7B layer at T = 4096) instead of the dQ kernel's S / P / dP
     recompute: 59 us less per layer there (profiles/attn_dq_from_ds.txt).  On by default while the
-    workspace fits LTA_ATTN_DS_MAX_GB (default 4); LTA_ATTN_DQ_FROM_DS=0 / 1 forces it off / on."""
+    workspace fits LTA_ATTN_DS_MAX_GB (default 4) and at most half of what the device can still
+    hand out (driver-free plus the caching allocator's unused reserve), so a run near the memory
+    limit keeps the workspace-free recompute path; LTA_ATTN_DQ_FROM_DS=0 / 1 forces it off / on."""
     mode = os.environ.get("LTA_ATTN_DQ_FROM_DS", "auto")
     if mode in ("0", "1"):
         return mode == "1"
-    return ws_bytes <= float(os.environ.get("LTA_ATTN_DS_MAX_GB", "4")) * 2 ** 30
+    if ws_bytes > float(os.environ.get("LTA_ATTN_DS_MAX_GB", "4")) * 2 ** 30:
+        return False
+    if device is None or device.type != "cuda":
+        return True
+    free, _ = torch.cuda.mem_get_info(device)
+    spare = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    return 2 * ws_bytes <= free + spare
 
 
 def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):
@@ -251,7 +259,8 @@ def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: in
         esz = dqkv.element_size()
         rc = -1
         n_ws = B * Hq * S * ((T + 255) // 256 * 256)
-        if T % 64 == 0 and _dq_from_ds(n_ws * esz):
+        # the kernel's own shape rules (T == S checked above, T % 64) before the workspace is allocated
+        if T > 0 and T % 64 == 0 and Hq % Hkv == 0 and _dq_from_ds(n_ws * esz, q.device):
             ws = torch.empty(n_ws, device=q.device, dtype=q.dtype)
             rc = lib.lta_attn_bwd_rope_ds(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
                                           ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq,

@@ -42,7 +42,10 @@ def nt_epilogue_ok(a: torch.Tensor, b: torch.Tensor, bias=None, residual=None) -
     N = b.shape[0]
     if b.shape[1] != K:
         return False
-    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()):
+    # 16-byte vector bias loads in the epilogues and the split-K fixup: a bias view at an odd offset
+    # (a slice of a fused qkv bias) takes the library path
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()
+                             or bias.data_ptr() % 16):
         return False
     if residual is not None and (residual.dtype != torch.bfloat16 or tuple(residual.shape) != (M, N)
                                  or not _rowmajor_2d(residual)):
@@ -204,7 +207,8 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
         assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
     plain = bias is None and residual is None and act is None and variant == 1
     # the K split also carries a bias (added in the fixup, forward layout)
-    splittable = residual is None and act is None and variant == 1 and (bias is None or (not at and not bt))
+    splittable = residual is None and act is None and variant == 1 and (
+        bias is None or (not at and not bt and bias.data_ptr() % 16 == 0))
     ks = splitk_factor(M, N, K, _device_cus(a.device)) if splittable else 0
     if ks:
         nwg = -(-M // 256) * -(-N // 256)

@@ -101,18 +101,23 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._join()
-        handled, self._handled = self._handled, set()
+        handled = self._handled
+        # validate every parameter before any state changes, so a failed step() leaves the
+        # optimizer exactly as it was (no partial step counts, no second update on a retry)
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None and id(p) in handled:
+                    # p was already updated inside the backward; a gradient accumulated into p.grad by
+                    # another autograd path would otherwise get a second step this iteration
+                    raise RuntimeError(f"overlapped optimizer: parameter of shape {tuple(p.shape)} was updated "
+                                       "in the backward and also has p.grad set")
+        self._handled = set()
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             buckets: dict = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if id(p) in handled:
-                    # p was already updated inside the backward; a gradient accumulated into p.grad by
-                    # another autograd path would otherwise get a second step this iteration
-                    raise RuntimeError(f"overlapped optimizer: parameter of shape {tuple(p.shape)} was updated "
-                                       "in the backward and also has p.grad set")
                 st = self._state(p)
                 st["step"] += 1
                 if p.device.type != "cuda":

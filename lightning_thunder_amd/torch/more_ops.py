@@ -596,7 +596,9 @@ def dsplit(a, sections):
 @_export
 @torchsymbol(*_tfn("broadcast_tensors"), id="torch.broadcast_tensors")
 def broadcast_tensors(*tensors):
-    shape = torch.broadcast_shapes(*(tuple(t.shape) for t in tensors))
+    from ..clang import compute_broadcast_shape
+
+    shape = compute_broadcast_shape(*(tuple(t.shape) for t in tensors))
     return tuple(_f("expand")(t, shape) for t in tensors)
 
 

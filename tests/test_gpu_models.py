@@ -12,7 +12,7 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("name", ["llama2-like", "llama3-like", "gpt-neox-like"])
+@pytest.mark.parametrize("name", ["llama2-like", "llama3-like", "gpt-neox-like", "gemma-like"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_litgpt_fwd_bwd_gpu(name, dtype):
     """Compiled model vs an fp32 eager reference (bf16 runs must be as accurate as bf16 eager, up to 3x)."""
@@ -45,8 +45,10 @@ def test_litgpt_fwd_bwd_gpu(name, dtype):
         err = _rel(got[n], p.grad)
         assert err <= 3 * base + 1e-5, (n, err, base)
     src = str(thunder.last_traces(tm)[-1])
-    if name != "gpt-neox-like":
+    if name not in ("gpt-neox-like", "gemma-like"):
         assert "hip_rms_norm_fwd" in src and "hip_qkv_rope" in src and "hip_swiglu" in src
+    if name == "gemma-like":  # head_size 256: the D = 256 attention kernels in a model
+        assert "hip_rms_norm_fwd" in src and "hip_flash_attn" in src, src
 
 
 def test_train_step_with_fused_loss_gpu():

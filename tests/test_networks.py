@@ -85,7 +85,8 @@ def test_hf_bart_eval():
         torch.testing.assert_close(thunder.jit(model)(x, labels=x).logits, model(x, labels=x).logits)
 
 
-@pytest.mark.parametrize("name", ["llama2-like", "codellama2-like", "mistral-like", "falcon-7b-like", "gpt-neox-like"])
+@pytest.mark.parametrize("name", ["llama2-like", "codellama2-like", "mistral-like", "falcon-7b-like", "gpt-neox-like",
+                                  "gemma-like"])
 def test_litgpt_configs_training_parity(name):
     from lightning_thunder_amd.models.litgpt import GPT, Config, init_weights
 

@@ -232,3 +232,22 @@ def test_fused_adamw_overlapped_with_backward_gpu():
     for p, q in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p, q, rtol=0, atol=0)
     assert o2._side, "no update ran on the side stream"
+
+
+def test_failed_step_leaves_state_untouched():
+    """A step() that rejects a parameter updated in the backward AND carrying p.grad raises before
+    any state changes: no step counts move and the handled set survives for a consistent retry."""
+    from lightning_thunder_amd.optim import AdamW
+
+    a = torch.nn.Parameter(torch.randn(4))
+    b = torch.nn.Parameter(torch.randn(4))
+    opt = AdamW([a, b], lr=1e-2)
+    a.grad = torch.randn(4)
+    b.grad = torch.randn(4)
+    opt._handled.add(id(b))
+    a0 = a.detach().clone()
+    with pytest.raises(RuntimeError, match="updated in the backward"):
+        opt.step()
+    assert not opt.state[a] or opt.state[a]["step"] == 0
+    assert torch.equal(a.detach(), a0)
+    assert id(b) in opt._handled

@@ -335,3 +335,24 @@ def test_head_parallel_kv_cache_decode():
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             assert res["cache_groups"][1] == 2 // WORLD, res  # llama3-like: 2 kv groups
             assert res["err"] < 1e-9, res
+
+
+def test_tp_inplace_allreduce_only_for_allocating_producers():
+    """skip_clone (in-place TP all-reduce) is an allowlist decision: GEMM / elementwise producers
+    qualify, ``contiguous()`` / ``to()`` of an existing tensor (which may return the input itself at
+    run time) never do."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.distributed.utils import allocates_fresh
+
+    def f(x, w):
+        a = torch.nn.functional.linear(x, w)
+        b = a.contiguous()
+        c = x.to(torch.float64).to(torch.float32)
+        return a + c.sum(), b
+
+    jf = thunder.jit(f)
+    jf(torch.randn(4, 4), torch.randn(4, 4))
+    verdict = {b.sym.name: allocates_fresh(b) for b in thunder.last_traces(jf)[0].bound_symbols}
+    assert verdict["linear"] and verdict["add"] and verdict["sum"], verdict
+    assert not verdict["contiguous"], verdict
+    assert not any(v for k, v in verdict.items() if k in ("to", "convert_element_type")), verdict
