@@ -69,7 +69,10 @@ def parse_args():
                         "thunder's timed region; both per-step loss curves go into the JSON line)")
     p.add_argument("--eager-steps", type=int, default=None, help="default: --steps (same loss-curve length)")
     p.add_argument("--eager-warmup", type=int, default=None, help="default: --warmup")
-    p.add_argument("--lr", type=float, default=3e-4)
+    p.add_argument("--lr", type=float, default=1e-4,
+                   help="AdamW learning rate (1e-4: on the 4 cycling synthetic batches thunder and eager both descend "
+                        "smoothly and their per-step losses can be compared; a constant 3e-4 oscillates in bf16 for "
+                        "both, profiles/loss_curves_r6.txt)")
     p.add_argument("--lr-warmup", type=int, default=0,
                    help="linear learning-rate warmup over this many optimizer steps (0: constant --lr)")
     p.add_argument("--profile-dir", default=None)

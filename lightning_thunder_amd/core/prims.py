@@ -532,7 +532,8 @@ full = make_prim(PrimIDs.FULL, "full", meta=_full_meta)
 
 
 def _iota_meta(length, *, start, step, device, dtype):
-    return TensorProxy(shape=(int(length),), device=to_device(device), dtype=dtype, requires_grad=False)
+    n = length if isinstance(length, SymInt) else int(length)
+    return TensorProxy(shape=(n,), device=to_device(device), dtype=dtype, requires_grad=False)
 
 
 iota = make_prim(PrimIDs.IOTA, "iota", meta=_iota_meta)

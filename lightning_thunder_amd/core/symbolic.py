@@ -27,6 +27,7 @@ float on the LEFT goes through ``float.__mul__`` and never reaches this class.
 from __future__ import annotations
 
 import contextlib
+import operator
 from contextvars import ContextVar
 from typing import Any, Callable
 
@@ -134,8 +135,10 @@ def _plain(x) -> bool:
 class SymInt(int):
     """An int that remembers how it was computed from the call's symbolic dims (module docstring)."""
 
-    def __new__(cls, value: int, expr: str):
+    def __new__(cls, value: int, expr: str, poly: dict | None = None):
         self = int.__new__(cls, int(value))
+        # poly: {monomial (sorted tuple of atoms): coefficient}; a bare symbol is {("s0",): 1}
+        self.poly = poly if poly is not None else {(expr,): 1}
         self.expr = expr
         return self
 
@@ -180,51 +183,38 @@ class SymInt(int):
         return (int, (int.__int__(self),))
 
     # -- arithmetic stays symbolic ------------------------------------------------------------------
-    def _bin(self, other, op: str, fn, reflected: bool = False):
-        if isinstance(other, bool):
-            other = int(other)
-        if isinstance(other, float):
-            v = _specialize(self)
-            return fn(other, v) if reflected else fn(v, other)
-        if not isinstance(other, int):
-            return NotImplemented  # tensors / number proxies: their reflected operator handles it
-        if not isinstance(other, SymInt):
-            # identities keep the expressions short: s*1, 1*s, s+0, 0+s, s-0, s//1
-            if (op, other) in (("*", 1), ("+", 0)) or (not reflected and (op, other) in (("-", 0), ("//", 1))):
-                return self
-        a, b = (other, self) if reflected else (self, other)
-        val = fn(int.__int__(a) if isinstance(a, SymInt) else a, int.__int__(b) if isinstance(b, SymInt) else b)
-        return SymInt(val, f"({_expr(a)} {op} {_expr(b)})")
-
+    # Expressions are kept as integer polynomials over atoms (a symbol, or an opaque ``(p // c)`` /
+    # ``(p % c)`` term) in a canonical form, so ``(s0 - s0) + s0`` IS ``s0`` and a product written two
+    # ways compares identical: the guards stay short and identities record nothing.
     def __add__(self, o):
-        return self._bin(o, "+", lambda a, b: a + b)
+        return _arith(self, o, "+")
 
     def __radd__(self, o):
-        return self._bin(o, "+", lambda a, b: a + b, True)
+        return _arith(o, self, "+")
 
     def __sub__(self, o):
-        return self._bin(o, "-", lambda a, b: a - b)
+        return _arith(self, o, "-")
 
     def __rsub__(self, o):
-        return self._bin(o, "-", lambda a, b: a - b, True)
+        return _arith(o, self, "-")
 
     def __mul__(self, o):
-        return self._bin(o, "*", lambda a, b: a * b)
+        return _arith(self, o, "*")
 
     def __rmul__(self, o):
-        return self._bin(o, "*", lambda a, b: a * b, True)
+        return _arith(o, self, "*")
 
     def __floordiv__(self, o):
-        return self._bin(o, "//", lambda a, b: a // b)
+        return _arith(self, o, "//")
 
     def __rfloordiv__(self, o):
-        return self._bin(o, "//", lambda a, b: a // b, True)
+        return _arith(o, self, "//")
 
     def __mod__(self, o):
-        return self._bin(o, "%", lambda a, b: a % b)
+        return _arith(self, o, "%")
 
     def __rmod__(self, o):
-        return self._bin(o, "%", lambda a, b: a % b, True)
+        return _arith(o, self, "%")
 
     def __divmod__(self, o):
         return self // o, self % o
@@ -236,13 +226,18 @@ class SymInt(int):
         return (int(o) if isinstance(o, SymInt) else o) / _specialize(self)
 
     def __pow__(self, o, mod=None):
+        if mod is None and type(o) is int and 0 <= o <= 4:
+            r = 1
+            for _ in range(o):
+                r = r * self
+            return r
         return pow(_specialize(self), int(o) if isinstance(o, SymInt) else o, mod)
 
     def __rpow__(self, o):
         return pow(o, _specialize(self))
 
     def __neg__(self):
-        return SymInt(-int.__int__(self), f"(-{self.expr})")
+        return _arith(0, self, "-")
 
     def __pos__(self):
         return self
@@ -291,8 +286,9 @@ class SymInt(int):
         a = int.__int__(self)
         b = int.__int__(other) if isinstance(other, SymInt) else other
         out = fn(a, b)
-        if isinstance(other, SymInt) and other.expr == self.expr:
-            return out
+        diff = _padd(self.poly, _poly_of(other), -1)
+        if not diff or list(diff) == [()]:
+            return out  # the two sides differ by a constant: the outcome holds for every size
         return _record(f"{self.expr} {op} {_expr(other)}", out)
 
     def __eq__(self, o):
@@ -313,6 +309,96 @@ class SymInt(int):
     def __ge__(self, o):
         return self._cmp(o, ">=", lambda a, b: a >= b)
 
+
+
+# -- canonical integer polynomials over atoms -------------------------------------------------------------
+def _poly_of(x) -> dict:
+    if isinstance(x, SymInt):
+        return x.poly
+    return {(): int(x)} if x else {}
+
+
+def _padd(p: dict, q: dict, sign: int = 1) -> dict:
+    r = dict(p)
+    for m, c in q.items():
+        v = r.get(m, 0) + sign * c
+        if v:
+            r[m] = v
+        else:
+            r.pop(m, None)
+    return r
+
+
+def _pmul(p: dict, q: dict) -> dict:
+    r: dict = {}
+    for m1, c1 in p.items():
+        for m2, c2 in q.items():
+            m = tuple(sorted(m1 + m2))
+            v = r.get(m, 0) + c1 * c2
+            if v:
+                r[m] = v
+            else:
+                r.pop(m, None)
+    return r
+
+
+def _pstr(p: dict) -> str:
+    if not p:
+        return "0"
+    terms = []
+    for m in sorted(p, key=lambda m: (-len(m), m)):
+        c = p[m]
+        body = "*".join(m)
+        if not m:
+            t = repr(abs(c))
+        elif abs(c) == 1:
+            t = body
+        else:
+            t = f"{abs(c)}*{body}"
+        terms.append(("-" if c < 0 else "+", t))
+    out = ("-" if terms[0][0] == "-" else "") + terms[0][1]
+    for sg, t in terms[1:]:
+        out += f" {sg} {t}"
+    return out if len(terms) == 1 and not out.startswith("-") else f"({out})"
+
+
+def _make(value: int, poly: dict):
+    if not poly or list(poly) == [()]:
+        return int(value)  # the expression folded to a constant
+    if len(poly) == 1:
+        (m, c), = poly.items()
+        if c == 1 and len(m) == 1:
+            return SymInt(value, m[0], poly)
+    return SymInt(value, _pstr(poly), poly)
+
+
+def _arith(a, b, op: str):
+    """``a op b`` with at least one SymInt operand (the other an int, a float, or not a number)."""
+    for x in (a, b):
+        if isinstance(x, float):
+            av = _specialize(a) if isinstance(a, SymInt) else a
+            bv = _specialize(b) if isinstance(b, SymInt) else b
+            return {"+": operator.add, "-": operator.sub, "*": operator.mul, "//": operator.floordiv,
+                    "%": operator.mod}[op](av, bv)
+        if not isinstance(x, int):
+            return NotImplemented  # tensors / number proxies: their reflected operator handles it
+    av = int.__int__(a) if isinstance(a, SymInt) else int(a)
+    bv = int.__int__(b) if isinstance(b, SymInt) else int(b)
+    pa, pb = _poly_of(a), _poly_of(b)
+    if op == "+":
+        return _make(av + bv, _padd(pa, pb))
+    if op == "-":
+        return _make(av - bv, _padd(pa, pb, -1))
+    if op == "*":
+        return _make(av * bv, _pmul(pa, pb))
+    val = av // bv if op == "//" else av % bv
+    if not isinstance(b, SymInt) and bv > 0:
+        if all(c % bv == 0 for c in pa.values()):  # exact: every term is a multiple of the divisor
+            return _make(val, {m: c // bv for m, c in pa.items()} if op == "//" else {})
+        if bv == 1:
+            return a if op == "//" else 0
+    atom = f"({_pstr(pa) if isinstance(a, SymInt) else repr(av)} {op} {_pstr(pb) if isinstance(b, SymInt) else repr(bv)})"
+    return SymInt(val, atom, {(atom,): 1})
 
 def is_symbolic(x) -> bool:
     return isinstance(x, SymInt)

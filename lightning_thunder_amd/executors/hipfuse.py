@@ -26,6 +26,8 @@ import threading
 
 import torch
 
+from ..core.symbolic import SymInt
+
 from ..core import profile as _profile
 from ..core.prims import PrimIDs, OpTags
 from ..core.proxies import TensorProxy, Proxy
@@ -63,7 +65,9 @@ def _checker(*args, **kwargs):
                 return False
             if a.device.type != "cuda" and not ex.allow_cpu:
                 return False
-            if any(not isinstance(s, int) for s in a.shape):
+            if any(not isinstance(s, int) or isinstance(s, SymInt) for s in a.shape):
+                # symbolic dims (cache="symbolic values"): generated kernels bake their sizes in, so
+                # these ops stay on the per-op executors and one program serves every size
                 return False
     return True
 
@@ -154,6 +158,7 @@ class HipFusion:
             for p, t in zip((self.inputs[i] for i in self.tensor_pos), tensors):
                 targs[p.name] = cg.TensorArg(tuple(t.shape), tuple(t.stride()), t.dtype, t.data_ptr() % 16 == 0)
             ks = cg.generate(self.plan, self.inputs, self.outputs, targs)
+            RTC_STATS["generated"] += 1
             v = (load_kernels(ks), ks)
             self._variants[key] = v
             return v
@@ -307,6 +312,11 @@ def cache_dir() -> str:
 RTC_OPTIONS = "--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast"
 
 
+# kernel sources generated (one per fusion region and call signature) and hiprtc compiles run (disk
+# cache misses) in this process: a symbolic-shape program must not grow them per new size
+RTC_STATS = {"generated": 0, "compiled": 0}
+
+
 def compile_source(ks: cg.KernelSource) -> bytes:
     """HIP source -> gfx950 code object (hiprtc; works without a GPU).  Disk-cached."""
     h = hashlib.sha1((RTC_OPTIONS + ks.src).encode()).hexdigest()
@@ -315,6 +325,7 @@ def compile_source(ks: cg.KernelSource) -> bytes:
         with open(path, "rb") as f:
             return f.read()
     lib = _lib()
+    RTC_STATS["compiled"] += 1
     code = ctypes.c_void_p()
     size = ctypes.c_size_t()
     log = ctypes.create_string_buffer(1 << 16)

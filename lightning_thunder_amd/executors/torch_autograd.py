@@ -30,6 +30,10 @@ class ThunderFunction(torch.autograd.Function):
                 if not diff:
                     nondiff.append(o)
         ctx.out_is_tensor = [isinstance(o, torch.Tensor) for o in flat_out]
+        # this call's differentiable output shapes (a symbolic-shape program serves many sizes; the
+        # traced metadata holds only the first): zeros for missing cotangents take these
+        ctx.diff_shapes = [tuple(o.shape) if isinstance(o, torch.Tensor) else None
+                           for o, d in zip(flat_out, entry.diff_output_mask) if d]
         entry._last_out_spec = out_spec
         entry._last_flat_out = flat_out
         if nondiff:
@@ -66,6 +70,8 @@ class ThunderFunction(torch.autograd.Function):
         for i, g in enumerate(cts):
             if g is None:
                 shape, dtype, device = outs_meta[i]
+                if ctx.diff_shapes[i] is not None:
+                    shape = ctx.diff_shapes[i]
                 cts[i] = torch.zeros(shape, dtype=dtype, device=device)
         args.extend(cts)
         handled: set = set()

@@ -1126,7 +1126,7 @@ def _getitem_sym(a, key):
             strides.append(1)
             squeeze_dims.append(dim)
         elif isinstance(k, slice):
-            s, e, st = k.indices(size)
+            s, e, st = _slice_indices(k, size)
             st = pyval(st)
             check(st > 0, "step must be greater than zero")
             if e < s:
@@ -1146,6 +1146,31 @@ def _getitem_sym(a, key):
     if unsqueeze_positions:
         out = clang.unsqueeze(out, unsqueeze_positions)
     return out
+
+
+def _slice_indices(k: slice, size):
+    """``slice.indices`` that keeps symbolic dims / bounds symbolic (``slice.indices`` itself turns them
+    into plain ints through ``__index__``); the clamping comparisons record shape guards."""
+    from ..core.symbolic import SymInt
+
+    if not builtins.any(isinstance(v, SymInt) for v in (k.start, k.stop, k.step, size)):
+        return k.indices(pyval(size))
+    step = 1 if k.step is None else pyval(k.step)
+    check(step > 0, "step must be greater than zero")
+
+    def norm(v, default):
+        if v is None:
+            return default
+        v = pyval(v)
+        if v < 0:
+            v = v + size
+            if v < 0:
+                return 0
+        elif v > size:
+            return size
+        return v
+
+    return norm(k.start, 0), norm(k.stop, size), step
 
 
 def _advanced_getitem(a, key):

@@ -133,3 +133,70 @@ def test_llama3_8b_tensor_parallel_shard_shapes_on_hand_gemms(tp):
         ref = TrainStep(m)(idx, tgt).float()
     assert abs(loss.item() - ref.item()) / abs(ref.item()) < 2e-2, (loss.item(), ref.item())
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+def _loss_curve(step_module, params, opt, data, steps):
+    curve = []
+    for i in range(steps):
+        x, y = data[i % len(data)]
+        loss = step_module(x, y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        curve.append(loss.detach().float())
+    return [float(v) for v in torch.stack(curve).cpu()]
+
+
+def test_llama2_7b_shape_training_trajectory_vs_eager():
+    """10 optimizer steps of the 2-layer Llama-2-7B-shape model: thunder (HIP kernels + the fused HIP
+    AdamW, as bench.py runs it) vs bf16 eager (torch fused AdamW) vs an fp32 eager reference, from one
+    init and the same 4 cycling batches (reference: benchmark_litgpt.py:842-846 logs every iteration's
+    loss).  Thunder's distance from the fp32 curve must stay within the band bf16 eager itself keeps."""
+    from lightning_thunder_amd.optim import AdamW as HipAdamW
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m32 = GPT.from_name("llama2-7b-shape-2l").to(device=dev)
+    init_weights(m32)
+    m32.set_rope_cache(SEQ, device=dev)
+    V = m32.config.padded_vocab_size
+    state = {k: v.clone() for k, v in m32.state_dict().items()}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    data = []
+    for _ in range(4):
+        t = torch.randint(0, m32.config.vocab_size, (1, SEQ + 1), device=dev, generator=gen)
+        data.append((t[:, :-1].contiguous(), t[:, 1:].contiguous()))
+
+    class TrainStep(torch.nn.Module):
+        def __init__(self, mm):
+            super().__init__()
+            self.m = mm
+
+        def forward(self, x, y):
+            return torch.nn.functional.cross_entropy(self.m(x).reshape(-1, V).float(), y.reshape(-1))
+
+    kw = dict(lr=1e-4, betas=(0.9, 0.95), weight_decay=0.1)
+    steps = 10
+    c32 = _loss_curve(TrainStep(m32), None, torch.optim.AdamW(m32.parameters(), **kw), data, steps)
+
+    def bf16_model():
+        m = GPT.from_name("llama2-7b-shape-2l").to(device=dev)
+        m.load_state_dict(state)
+        m = m.to(torch.bfloat16)
+        m.set_rope_cache(SEQ, device=dev)
+        return m
+
+    me = bf16_model()
+    ce = _loss_curve(TrainStep(me), None, torch.optim.AdamW(me.parameters(), fused=True, **kw), data, steps)
+    del me
+    mt = bf16_model()
+    tm = thunder.jit(TrainStep(mt))
+    ct = _loss_curve(tm, None, HipAdamW([p for p in mt.parameters()], **kw), data, steps)
+
+    band = max(abs(a - b) for a, b in zip(ce, c32))
+    gap = max(abs(a - b) for a, b in zip(ct, c32))
+    assert c32[-1] < 0.5 * c32[0], c32  # the run trains (memorizes the 4 batches)
+    assert gap <= 2 * band + 0.05, {"fp32": c32, "eager_bf16": ce, "thunder": ct, "band": band, "gap": gap}
+    for k in range(steps):
+        assert abs(ct[k] - ce[k]) <= 2 * band + 0.05, (k, ct, ce, band)

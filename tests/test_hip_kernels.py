@@ -1220,11 +1220,15 @@ def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
     assert e_fused < 1e-2 and e_fused <= 1.5 * e_two + 1e-4, (e_fused, e_two)
 
 
-@pytest.mark.parametrize("B,Hq,Hkv,T,causal", [(1, 4, 2, 512, True), (2, 4, 4, 256, False), (1, 8, 1, 320, True),
-                                                (1, 2, 2, 1088, False)])
-def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, monkeypatch):
+@pytest.mark.parametrize("B,Hq,Hkv,T,causal,do_layout", [(1, 4, 2, 512, True, "bhtd"), (2, 4, 4, 256, False, "bhtd"),
+                                                          (1, 8, 1, 320, True, "bhtd"), (1, 2, 2, 1088, False, "bhtd"),
+                                                          (1, 4, 2, 512, True, "bthd"),
+                                                          (1, 32, 32, 4096, True, "bthd")])
+def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, do_layout, monkeypatch):
     """dQ = scale dS K from the dS^T the dK/dV kernel stores (the default while the workspace fits),
-    against the recompute path (LTA_ATTN_DQ_FROM_DS=0) and an fp32 reference."""
+    against the recompute path (LTA_ATTN_DQ_FROM_DS=0) and an fp32 reference.  ``bthd``: dO stored
+    token-major (the output projection's gradient layout, as in the Llama step) — the preprocess's
+    heads-fastest row order; the last case is the Llama-2-7B layer shape (T = 4096, 32 heads)."""
     from lightning_thunder_amd.models.litgpt import build_rope_cache
     from lightning_thunder_amd.ops import _lib
     from lightning_thunder_amd.ops.attention import attn_fwd, attn_bwd_rope
@@ -1236,7 +1240,10 @@ def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, monkeypatch):
     q = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
-    do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    if do_layout == "bthd":
+        do = torch.randn(B, T, Hq, D, device="cuda", dtype=torch.bfloat16).transpose(1, 2)
+    else:
+        do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
     o, lse = attn_fwd(q, k, v, causal)
     monkeypatch.setenv("LTA_ATTN_DQ_FROM_DS", "0")
     base = attn_bwd_rope(do, q, k, v, o, lse, causal, None, cos, sin, Hq, Hkv)

@@ -136,3 +136,41 @@ def test_symbolic_values_training_one_entry():
             assert_close(a, p.grad)
         m.zero_grad()
     assert thunder.cache_misses(jm) == 1 and thunder.cache_hits(jm) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["llama2-like", "llama3-like"])
+def test_symbolic_litgpt_three_lengths_one_entry_gpu(name):
+    """A small LitGPT (bf16, HIP executors) trains at three sequence lengths through ONE cache entry:
+    no re-trace and no new generated / hiprtc-compiled kernel after the first length; every length
+    matches eager."""
+    from lightning_thunder_amd.executors import hipfuse
+    from lightning_thunder_amd.models.litgpt import GPT, init_weights
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = GPT.from_name(name).to(device=dev)
+    init_weights(m)
+    m = m.to(torch.bfloat16)
+    m.set_rope_cache(256, device=dev)
+    jm = thunder.jit(m, cache="symbolic values")
+    counts = None
+    for T in (64, 128, 192):
+        x = torch.randint(0, 320, (2, T), device=dev)
+        out = jm(x)
+        ref = m(x)
+        assert_close(out.float(), ref.float(), atol=5e-2, rtol=5e-2)
+        g = torch.randn_like(ref)
+        out.backward(g)
+        got = [p.grad.float().clone() for p in m.parameters()]
+        m.zero_grad()
+        ref.backward(g)
+        for a, p in zip(got, m.parameters()):
+            assert_close(a, p.grad.float(), atol=5e-2, rtol=5e-2)
+        m.zero_grad()
+        if counts is None:
+            counts = dict(hipfuse.RTC_STATS)
+    assert thunder.cache_misses(jm) == 1 and thunder.cache_hits(jm) == 2
+    assert hipfuse.RTC_STATS == counts, (hipfuse.RTC_STATS, counts)
+    src = str(thunder.last_traces(jm)[-1])
+    assert "hip_" in src, src  # the HIP kernels (GEMM, attention, norms) serve every length
