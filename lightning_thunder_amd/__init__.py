@@ -132,11 +132,17 @@ def _autocast_key():
 
 
 def _has_device_autocast():
-    try:
-        _torch.is_autocast_enabled("cuda")
-        return True
-    except TypeError:
-        return False
+    global _HAS_DEVICE_AUTOCAST
+    if _HAS_DEVICE_AUTOCAST is None:
+        try:
+            _torch.is_autocast_enabled("cuda")
+            _HAS_DEVICE_AUTOCAST = True
+        except TypeError:
+            _HAS_DEVICE_AUTOCAST = False
+    return _HAS_DEVICE_AUTOCAST
+
+
+_HAS_DEVICE_AUTOCAST = None
 
 
 def _check_traces(traces, cd):
@@ -440,14 +446,13 @@ def jit(
     )
     cs = CompileStats()
     holder: dict[str, Any] = {"module": None}
+    from .executors.pythonex import ThunderCacheMiss
+    from .distributed import get_skip_data_parallel_grad_sync
 
     @_annotate_for_profile("get_computation_and_inputs")
     def get_computation_and_inputs(args, kwargs):
         cs.last_trace_cache_start = time.perf_counter_ns()
         flat_args, _ = tree_flatten((args, kwargs))
-        from .executors.pythonex import ThunderCacheMiss
-        from .distributed import get_skip_data_parallel_grad_sync
-
         grad_enabled = _torch.is_grad_enabled()
         ac = _autocast_key()
         nosync = get_skip_data_parallel_grad_sync()

@@ -16,7 +16,7 @@ import torch
 
 from ..core import dtypes, prims
 from ..core.baseutils import check
-from ..core.symbolic import unify
+from ..core.symbolic import SymInt, unify
 from ..core.devices import to_device
 from ..core.proxies import TensorProxy, NumberProxy, pyval
 
@@ -106,6 +106,8 @@ def elementwise_type_promotion(*args, type_promotion_kind: ELEMENTWISE_TYPE_PROM
             stubs.append(_meta_stub(a))
         elif isinstance(a, NumberProxy):
             stubs.append(a.value if a.value is not None else a.python_type(0))
+        elif isinstance(a, SymInt):
+            stubs.append(0)  # only the Python type takes part in promotion (an int)
         elif isinstance(a, (Number, torch.Tensor)):
             stubs.append(a)
     return elementwise_dtypes(*stubs, type_promotion_kind=_torch_kind(type_promotion_kind))
@@ -127,6 +129,8 @@ def maybe_convert_to_dtype(a, dtype, *, enforce_safe_casting: bool = False):
         if isinstance(a, NumberProxy) and (pt is a.python_type or (pt is float and a.python_type is int)
                                            or (pt is complex and a.python_type in (int, float))):
             return a  # a widening conversion the operation performs itself: the number stays symbolic
+        if isinstance(a, SymInt) and pt in (int, float, complex):
+            return a  # likewise for a symbolic int (a size argument used as a value)
         v = pyval(a)
         if pt is int and isinstance(v, float):
             return int(v)

@@ -41,12 +41,23 @@ def bindable_symbols(names, used: set | None = None):
 def _print_symint(x: SymInt) -> str:
     ok = _bindable.get()
     free = x.free_symbols()
-    if ok is None or free <= ok:
-        used = _used.get()
-        if used is not None:
-            used.update(free)
-        return x.expr
-    return repr(int(x))  # int() specializes the program on this value
+    expr = x.expr
+    if ok is not None and not free <= ok:
+        # a symbol the program cannot bind may equal (a recorded guard) one it can
+        from .symbolic import current_env
+        import re
+
+        env = current_env()
+        for s in free - ok:
+            alt = next((e for e in (env.equivalents(s) if env is not None else ()) if e in ok), None)
+            if alt is None:
+                return repr(int(x))  # int() specializes the program on this value
+            expr = re.sub(rf"\b{s}\b", alt, expr)
+        free = set(re.findall(r"\bs\d+\b", expr))
+    used = _used.get()
+    if used is not None:
+        used.update(free)
+    return expr
 
 
 class ContextObject:

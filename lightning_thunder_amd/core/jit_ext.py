@@ -395,7 +395,15 @@ def _acquire(fn: Callable, args: tuple, kwargs: dict, *, module: torch.nn.Module
 
                 p._on_value = _specialize
                 prog.symbolic_args[i] = p
-                proxied_flat.append(p)
+                env = current_env()
+                if env is not None and type(x) is int and x >= 2:
+                    # an int size argument is a dim symbol like a tensor's (core/symbolic.py): the program
+                    # sees a SymInt, the number input only carries the value the program binds it from
+                    si = env.new_symbol(x, i, None)
+                    p._sym = si.expr
+                    proxied_flat.append(si)
+                else:
+                    proxied_flat.append(p)
                 prog.input_specs.append(InputSpec("arg", path=i, proxy=p))
             else:
                 proxied_flat.append(x)

@@ -50,11 +50,26 @@ def _is_namedtuple(x) -> bool:
     return isinstance(x, tuple) and hasattr(type(x), "_fields") and type(x) is not tuple
 
 
+# exact types that are always leaves: checked first, so flattening a call's arguments (every
+# compiled call does it) costs one set lookup per tensor / number
+_FAST_LEAF = frozenset({torch.Tensor, torch.nn.Parameter, int, float, bool, str, type(None), torch.dtype,
+                        torch.device})
+
+
 def tree_flatten(tree, is_leaf: Callable | None = None) -> tuple[list, TreeSpec]:
     leaves: list = []
 
     def rec(x) -> TreeSpec:
-        if is_leaf is not None and is_leaf(x):
+        t = type(x)
+        if is_leaf is None:
+            if t in _FAST_LEAF:
+                leaves.append(x)
+                return LEAF
+            if t is tuple:
+                return TreeSpec("tuple", None, [rec(v) for v in x])
+            if t is list:
+                return TreeSpec("list", None, [rec(v) for v in x])
+        elif is_leaf(x):
             leaves.append(x)
             return LEAF
         if isinstance(x, torch.Size):
@@ -64,11 +79,13 @@ def tree_flatten(tree, is_leaf: Callable | None = None) -> tuple[list, TreeSpec]
             return TreeSpec("namedtuple", type(x), [rec(v) for v in x])
         if isinstance(x, tuple) and hasattr(type(x), "n_fields"):  # torch.return_types structseqs
             return TreeSpec("structseq", type(x), [rec(v) for v in x])
-        t = type(x)
         if t is tuple:
             return TreeSpec("tuple", None, [rec(v) for v in x])
         if t is list:
             return TreeSpec("list", None, [rec(v) for v in x])
+        if t is dict:
+            keys = list(x)
+            return TreeSpec("dict", (dict, tuple(keys)), [rec(x[k]) for k in keys])
         if isinstance(x, dict):
             keys = list(x.keys())
             # a dataclass that subclasses dict (diffusers / HF model outputs): fields that are not

@@ -41,12 +41,25 @@ class ShapeEnv:
         self.symbols: list[tuple[str, int, int, int]] = []  # (name, flat-arg index, dim, traced value)
         self.guards: dict[str, bool] = {}
         self._suspended = 0
+        self._parent: dict[str, str] = {}
 
     # -- symbols ---------------------------------------------------------------------------------
-    def new_symbol(self, value: int, arg_index: int, dim: int) -> "SymInt":
+    def new_symbol(self, value: int, arg_index: int, dim: int | None) -> "SymInt":
+        """A symbol for dim ``dim`` of tensor argument ``arg_index`` (``dim=None``: the int argument itself)."""
         name = f"s{len(self.symbols)}"
         self.symbols.append((name, arg_index, dim, int(value)))
+        self._parent[name] = name
         return SymInt(value, name)
+
+    # -- equal symbols (a recorded ``s3 == s1``): a program that cannot bind one binds the other --------
+    def _find(self, a: str) -> str:
+        while self._parent.get(a, a) != a:
+            a = self._parent[a]
+        return a
+
+    def equivalents(self, name: str) -> list[str]:
+        r = self._find(name)
+        return [n for n in self._parent if self._find(n) == r]
 
     @property
     def active(self) -> bool:
@@ -56,6 +69,9 @@ class ShapeEnv:
         if self._suspended:
             return
         self.guards[expr] = bool(outcome)
+        parts = expr.split(" == ")
+        if outcome and len(parts) == 2 and all(p in self._parent for p in parts):
+            self._parent[self._find(parts[0])] = self._find(parts[1])
 
     def specialize(self, s: "SymInt") -> None:
         self.record(f"({s.expr}) == {int.__int__(s)}", True)
@@ -76,7 +92,7 @@ class ShapeEnv:
         where = [(i, d) for _, i, d, _ in self.symbols]
 
         def check(flat_args):
-            return bool(g(*[flat_args[i].shape[d] for i, d in where]))
+            return bool(g(*[flat_args[i] if d is None else flat_args[i].shape[d] for i, d in where]))
 
         check.source = src
         return check
@@ -362,6 +378,13 @@ def _pstr(p: dict) -> str:
     return out if len(terms) == 1 and not out.startswith("-") else f"({out})"
 
 
+def _operand(p: dict) -> str:
+    """A polynomial as an operand of ``//`` / ``%``: parenthesized unless it is a single atom."""
+    t = _pstr(p)
+    return t if t.isidentifier() or (t.startswith("(") and len(p) == 1 and list(p.values()) == [1]
+                                     and len(next(iter(p))) == 1) else f"({t})" if not t.startswith("(") else t
+
+
 def _make(value: int, poly: dict):
     if not poly or list(poly) == [()]:
         return int(value)  # the expression folded to a constant
@@ -397,7 +420,7 @@ def _arith(a, b, op: str):
             return _make(val, {m: c // bv for m, c in pa.items()} if op == "//" else {})
         if bv == 1:
             return a if op == "//" else 0
-    atom = f"({_pstr(pa) if isinstance(a, SymInt) else repr(av)} {op} {_pstr(pb) if isinstance(b, SymInt) else repr(bv)})"
+    atom = f"({_operand(pa) if isinstance(a, SymInt) else repr(av)} {op} {_operand(pb) if isinstance(b, SymInt) else repr(bv)})"
     return SymInt(val, atom, {(atom,): 1})
 
 def is_symbolic(x) -> bool:

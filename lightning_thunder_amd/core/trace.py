@@ -207,7 +207,7 @@ class TraceCtx:
                 body.extend(bsym.python(indent=1, print_depth=print_depth, obj_ctx=obj_ctx))
         for sym, (arg, d) in binds.items():
             if sym in used:
-                lines.append(f"  {sym} = {arg}.shape[{d}]")
+                lines.append(f"  {sym} = {arg}" if d is None else f"  {sym} = {arg}.shape[{d}]")
         if not body:
             body = ["  pass"]
         lines.extend(body)
@@ -252,6 +252,8 @@ def _symbol_bindings(args) -> dict:
             for d, s in enumerate(a._shape):
                 if isinstance(s, SymInt) and s.expr.isidentifier() and s.expr not in out:
                     out[s.expr] = (a.name, d)
+        elif getattr(a, "_sym", None) is not None and a._sym not in out:  # an int size argument
+            out[a._sym] = (a.name, None)
     return out
 
 

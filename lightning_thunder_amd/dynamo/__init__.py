@@ -252,6 +252,9 @@ class ThunderCompiler:
             opts["transforms"] = ts
         else:
             opts.pop("extraction_only_prologue", None)
+            # dynamic graphs: symbolic tensor dims and size arguments (core/symbolic.py), so one
+            # compiled program serves every size dynamo's own graph serves
+            opts.setdefault("cache", "symbolic values")
         return opts
 
     def __call__(self, gm: torch.fx.GraphModule, sample_args):

@@ -34,3 +34,28 @@ LTA_EXPORT int lta_probe_lds_dma_oob(const void* src, void* out, int valid_bytes
   hipLaunchKernelGGL(probe_lds_dma_oob_kernel, dim3(1), dim3(64), 0, s, (const uint4*)src, (uint4*)out, valid_bytes);
   return (int)hipGetLastError();
 }
+
+// lta_cu_occupy: n_wg workgroups that each hold a CU slot for `ticks` of the 100 MHz real-time
+// counter, then exit (every wave reaches the exit: bounded by the counter, no flags).  Used to
+// emulate the workgroups an overlapped RCCL collective keeps resident (one per channel) while the
+// compute stream runs: `lds_bytes` of dynamic LDS and `threads` per workgroup set how much of a CU
+// each one takes (an RCCL channel workgroup's shape is read from a kernel trace), so the GEMMs'
+// one-tile-per-CU waves can be timed with 0 / 8 / 16 / 32 CUs taken (scripts/cu_contention.py).
+namespace {
+
+__global__ __launch_bounds__(1024) void cu_occupy_kernel(uint64_t ticks, int lds_bytes) {
+  extern __shared__ char lds_hold[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (ticks == 0 && (int)threadIdx.x < lds_bytes) lds_hold[threadIdx.x] = 0;  // keeps the LDS allocation referenced
+}
+
+}  // namespace
+
+LTA_EXPORT int lta_cu_occupy(int n_wg, int threads, int lds_bytes, uint64_t ticks, hipStream_t s) {
+  if (n_wg <= 0 || threads <= 0 || threads > 1024 || lds_bytes < 0 || lds_bytes > 160 * 1024) return -1;
+  if (lds_bytes > 64 * 1024)
+    hipFuncSetAttribute((const void*)cu_occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  hipLaunchKernelGGL(cu_occupy_kernel, dim3(n_wg), dim3(threads), lds_bytes, s, ticks, lds_bytes);
+  return (int)hipGetLastError();
+}

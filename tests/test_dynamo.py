@@ -75,7 +75,7 @@ def test_thunderfx_dynamic_shapes_no_eager_fallback():
     infos = f.subgraph_infos
     assert len(infos) == 1 and not infos[0].split_reasons and infos[0].split_graph_module is None
     (fn,) = infos[0].thunder_compiled_fns
-    assert thunder.cache_misses(fn) == 3
+    assert thunder.cache_misses(fn) == 1, thunder.cache_misses(fn)  # symbolic dims: one program
 
 
 def test_thunderfx_static_graph_extraction_only_prologue():

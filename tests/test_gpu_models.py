@@ -47,7 +47,7 @@ def test_litgpt_fwd_bwd_gpu(name, dtype):
     src = str(thunder.last_traces(tm)[-1])
     if name not in ("gpt-neox-like", "gemma-like"):
         assert "hip_rms_norm_fwd" in src and "hip_qkv_rope" in src and "hip_swiglu" in src
-    if name == "gemma-like":  # head_size 256: the D = 256 attention kernels in a model
+    if name == "gemma-like" and dtype == torch.bfloat16:  # head_size 256: the D = 256 attention kernels in a model
         assert "hip_rms_norm_fwd" in src and "hip_flash_attn" in src, src
 
 

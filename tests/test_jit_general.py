@@ -243,7 +243,7 @@ def test_symbolic_values_reuse_program_across_numbers():
 
 def test_symbolic_values_specialize_when_value_is_read():
     def g(x, n):
-        if n > 2:  # branching reads the value: this input is specialized and value-checked
+        if n > 2:  # branching on a size-like int records the guard n > 2 (core/symbolic.py)
             return x * n
         return x - n
 
@@ -251,8 +251,18 @@ def test_symbolic_values_specialize_when_value_is_read():
     x = torch.randn(6)
     for n in (3, 5, 1, 3):
         torch.testing.assert_close(jg(x, n), g(x, n))
-    assert thunder.cache_misses(jg) == 3 and thunder.cache_hits(jg) == 1
-    assert "check_number_type_and_value" in str(thunder.last_prologue_traces(jg)[-1])
+    # 3 and 5 take the same branch: one program (guard s0 > 2); 1 (< 2, a static value) is another
+    assert thunder.cache_misses(jg) == 2 and thunder.cache_hits(jg) == 2
+    guards = thunder.compile_stats(jg).interpreter_cache[0].shape_guards.source
+    assert "s1 > 2" in guards, guards  # s0 is x.shape[0], s1 the int argument n
+
+    def h(x, n):
+        return x * float(n)  # float() needs the bare value: this input is specialized
+
+    jh = thunder.jit(h, cache="symbolic values")
+    for n in (3, 5, 3):
+        torch.testing.assert_close(jh(x, n), h(x, n))
+    assert thunder.cache_misses(jh) == 2 and thunder.cache_hits(jh) == 1
 
     def h(x, n):  # used as a shape
         return x.reshape(n, -1).sum(0) * n
@@ -260,7 +270,9 @@ def test_symbolic_values_specialize_when_value_is_read():
     jh = thunder.jit(h, cache="symbolic values")
     for n in (2, 3, 2):
         torch.testing.assert_close(jh(x, n), h(x, n))
-    assert thunder.cache_misses(jh) == 2
+    # a size argument is a dim symbol: reshape(n, -1) prints as reshape(s1, s0 // s1), one program
+    # (guarded by s1 * (s0 // s1) == s0) serves n = 2 and n = 3
+    assert thunder.cache_misses(jh) == 1
 
 
 def test_symbolic_values_backward():

@@ -138,19 +138,27 @@ def test_symbolic_values_training_one_entry():
     assert thunder.cache_misses(jm) == 1 and thunder.cache_hits(jm) == 2
 
 
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["llama2-like", "llama3-like"])
 def test_symbolic_litgpt_three_lengths_one_entry_gpu(name):
     """A small LitGPT (bf16, HIP executors) trains at three sequence lengths through ONE cache entry:
-    no re-trace and no new generated / hiprtc-compiled kernel after the first length; every length
-    matches eager."""
+    no re-trace and no new generated / hiprtc-compiled kernel after the first length; at every length
+    the forward and every parameter gradient are as close to an fp32 eager reference as bf16 eager is
+    (3x band, as tests/test_gpu_models.py)."""
     from lightning_thunder_amd.executors import hipfuse
     from lightning_thunder_amd.models.litgpt import GPT, init_weights
 
     torch.manual_seed(0)
     dev = torch.device("cuda")
+    m32 = GPT.from_name(name).to(device=dev)
+    init_weights(m32)
+    m32.set_rope_cache(256, device=dev)
     m = GPT.from_name(name).to(device=dev)
-    init_weights(m)
+    m.load_state_dict(m32.state_dict())
     m = m.to(torch.bfloat16)
     m.set_rope_cache(256, device=dev)
     jm = thunder.jit(m, cache="symbolic values")
@@ -158,16 +166,23 @@ def test_symbolic_litgpt_three_lengths_one_entry_gpu(name):
     for T in (64, 128, 192):
         x = torch.randint(0, 320, (2, T), device=dev)
         out = jm(x)
-        ref = m(x)
-        assert_close(out.float(), ref.float(), atol=5e-2, rtol=5e-2)
+        eager = m(x)
+        ref = m32(x)
+        base = max(_rel(eager, ref), 1e-6)
+        assert _rel(out, ref) <= 3 * base + 1e-5, (T, _rel(out, ref), base)
         g = torch.randn_like(ref)
-        out.backward(g)
-        got = [p.grad.float().clone() for p in m.parameters()]
+        out.backward(g.to(torch.bfloat16))
+        got = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+        m.zero_grad()
+        eager.backward(g.to(torch.bfloat16))
+        eg = {n: p.grad.float().clone() for n, p in m.named_parameters()}
         m.zero_grad()
         ref.backward(g)
-        for a, p in zip(got, m.parameters()):
-            assert_close(a, p.grad.float(), atol=5e-2, rtol=5e-2)
-        m.zero_grad()
+        for n, p in m32.named_parameters():
+            b = max(_rel(eg[n], p.grad), 1e-6)
+            e = _rel(got[n], p.grad)
+            assert e <= 3 * b + 1e-5, (T, n, e, b)
+        m32.zero_grad()
         if counts is None:
             counts = dict(hipfuse.RTC_STATS)
     assert thunder.cache_misses(jm) == 1 and thunder.cache_hits(jm) == 2
