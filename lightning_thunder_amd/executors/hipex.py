@@ -1823,7 +1823,7 @@ hip_index_add = ex.register_operator("hip_index_add", meta=_index_add_meta, fn=_
 def _numel(shape) -> int:
     n = 1
     for d in shape:
-        n *= int(d)
+        n = n * d  # symbolic dims stay symbolic (core/symbolic.py)
     return n
 
 

@@ -76,9 +76,16 @@ for _sid in cg.SUPPORTED:
     ex.register_supported(_sid, _checker)
 
 
+def _symbolic(b: BoundSymbol) -> bool:
+    return any(isinstance(p, TensorProxy) and any(isinstance(d, SymInt) for d in p._shape)
+               for p in (*b.flat_proxy_args, *b.flat_proxy_outs))
+
+
 def _is_barrier(b: BoundSymbol) -> bool:
     if b.sym.id in (PrimIDs.RETURN, PrimIDs.DEL, PrimIDs.COMMENT):
         return True
+    if _symbolic(b):
+        return True  # symbolic dims: no region (kernels bake sizes in), not even a view inside one
     tags = set(b.sym.tags or ()) | set(getattr(b, "tags", ()) or ())
     if OpTags.DONT_DCE in tags or OpTags.IN_PLACE in tags or OpTags.RANDOM_OP in tags:
         return True
