@@ -143,7 +143,9 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
         if args.hipgraph:
             from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
 
-            transforms.append(HipGraphTransform())
+            # backward-graph gradients handed to autograd without a clone (the loop below zeroes them
+            # with set_to_none every step, which donation requires)
+            transforms.append(HipGraphTransform(donate_grads=True))
         if args.fp8:
             from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
 
@@ -234,7 +236,8 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
     t_first = time.perf_counter()
     for i in range(warmup):
         loss = step(*data[i % 4])
-        losses.append(loss.detach())
+        # a graphed forward's loss is a static tensor the next replay overwrites: keep a copy
+        losses.append(loss.detach().clone() if args.hipgraph else loss.detach())
         if i == 0:
             torch.cuda.synchronize()
             log(rank, f"[{mode}] first step (incl. compile) {time.perf_counter() - t_first:.1f}s loss={loss.item():.4f}")
@@ -245,7 +248,7 @@ def run(args, rank, world, device, mode, steps=None, warmup=None):
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(*data[(warmup + i) % 4])
-        losses.append(loss.detach())
+        losses.append(loss.detach().clone() if args.hipgraph else loss.detach())
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()

@@ -448,11 +448,15 @@ def jit(
     holder: dict[str, Any] = {"module": None}
     from .executors.pythonex import ThunderCacheMiss
     from .distributed import get_skip_data_parallel_grad_sync
+    from .core.pytree import _FAST_LEAF
 
     @_annotate_for_profile("get_computation_and_inputs")
     def get_computation_and_inputs(args, kwargs):
         cs.last_trace_cache_start = time.perf_counter_ns()
-        flat_args, _ = tree_flatten((args, kwargs))
+        if not kwargs and all(type(a) in _FAST_LEAF for a in args):
+            flat_args = list(args)  # the common call: tensors / numbers only, nothing to flatten
+        else:
+            flat_args, _ = tree_flatten((args, kwargs))
         grad_enabled = _torch.is_grad_enabled()
         ac = _autocast_key()
         nosync = get_skip_data_parallel_grad_sync()

@@ -43,14 +43,21 @@ def _unpack_key(d, k):
         raise ThunderCacheMiss(f"key {k!r}: {e}") from None
 
 
+_DEV_STR: dict = {}
+
+
 def _check_tensor(t, shape, device, dtype, requires_grad):
     if not isinstance(t, torch.Tensor):
         raise ThunderCacheMiss(f"expected a tensor, got {type(t)}")
     if None in shape:  # symbolic dims (cache="symbolic values"): rank and static dims here
         ok = t.ndim == len(shape) and all(n is None or n == m for n, m in zip(shape, t.shape))
     else:
-        ok = tuple(t.shape) == shape
-    if not ok or t.dtype != dtype or str(t.device) != device or t.requires_grad != requires_grad:
+        ok = t.shape == shape
+    dev = t.device
+    ds = _DEV_STR.get(dev)
+    if ds is None:
+        ds = _DEV_STR[dev] = str(dev)
+    if not ok or t.dtype != dtype or ds != device or t.requires_grad != requires_grad:
         raise ThunderCacheMiss(
             f"tensor metadata mismatch: {tuple(t.shape)},{t.dtype},{t.device},{t.requires_grad} vs {shape},{dtype},{device},{requires_grad}"
         )

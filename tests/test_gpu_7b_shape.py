@@ -143,7 +143,7 @@ def _loss_curve(step_module, params, opt, data, steps):
         loss.backward()
         opt.step()
         opt.zero_grad(set_to_none=True)
-        curve.append(loss.detach().float())
+        curve.append(loss.detach().float().clone())  # a graphed loss is overwritten by the next replay
     return [float(v) for v in torch.stack(curve).cpu()]
 
 
@@ -200,3 +200,53 @@ def test_llama2_7b_shape_training_trajectory_vs_eager():
     assert gap <= 2 * band + 0.05, {"fp32": c32, "eager_bf16": ce, "thunder": ct, "band": band, "gap": gap}
     for k in range(steps):
         assert abs(ct[k] - ce[k]) <= 2 * band + 0.05, (k, ct, ce, band)
+
+
+def test_llama2_7b_shape_training_under_hipgraph():
+    """The 2-layer 7B-shape model trains under HipGraphTransform(donate_grads=True) (forward and
+    backward replayed as hipGraphs, gradients adopted by autograd without a clone, the HIP AdamW
+    outside the graphs) with the same loss trajectory band as the uncaptured program, and the graphs
+    really replay (reference thunder/tests/test_networks.py:95-160)."""
+    from lightning_thunder_amd.optim import AdamW as HipAdamW
+    from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m32 = GPT.from_name("llama2-7b-shape-2l").to(device=dev)
+    init_weights(m32)
+    m32.set_rope_cache(SEQ, device=dev)
+    V = m32.config.padded_vocab_size
+    state = {k: v.clone() for k, v in m32.state_dict().items()}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    data = []
+    for _ in range(4):
+        t = torch.randint(0, m32.config.vocab_size, (1, SEQ + 1), device=dev, generator=gen)
+        data.append((t[:, :-1].contiguous(), t[:, 1:].contiguous()))
+
+    class TrainStep(torch.nn.Module):
+        def __init__(self, mm):
+            super().__init__()
+            self.m = mm
+
+        def forward(self, x, y):
+            return torch.nn.functional.cross_entropy(self.m(x).reshape(-1, V).float(), y.reshape(-1))
+
+    kw = dict(lr=1e-4, betas=(0.9, 0.95), weight_decay=0.1)
+    steps = 8
+    c32 = _loss_curve(TrainStep(m32), None, torch.optim.AdamW(m32.parameters(), **kw), data, steps)
+    curves = {}
+    for mode in ("plain", "hipgraph"):
+        m = GPT.from_name("llama2-7b-shape-2l").to(device=dev)
+        m.load_state_dict(state)
+        m = m.to(torch.bfloat16)
+        m.set_rope_cache(SEQ, device=dev)
+        t = HipGraphTransform(donate_grads=True) if mode == "hipgraph" else None
+        tm = thunder.jit(TrainStep(m), transforms=[t] if t else [])
+        curves[mode] = _loss_curve(tm, None, HipAdamW(list(m.parameters()), **kw), data, steps)
+        if t is not None:
+            assert sum(r.replays for r in t.runners) >= 2 * (steps - 2), [(r.name, r.replays) for r in t.runners]
+        del tm, m
+    band = max(abs(a - b) for a, b in zip(curves["plain"], c32))
+    gap = max(abs(a - b) for a, b in zip(curves["hipgraph"], c32))
+    assert gap <= 2 * band + 0.05, {"fp32": c32, **curves, "band": band}

@@ -202,7 +202,8 @@ class _FakeGraph:
         # .data aliases the storage with its own version counter: like a real replay, no version bump
         new = self.fn(*[a.data if isinstance(a, torch.Tensor) else a for a in self.ins])
         new = new if isinstance(new, tuple) else (new,)
-        for o, n in zip(self.outs, new):
+        outs = self.outs() if callable(self.outs) else self.outs
+        for o, n in zip(outs, new):
             o.copy_(n)
 
 
@@ -214,10 +215,13 @@ class _CpuRunner(HipGraphRunner):
         ins = tuple(a.clone() if i in clone and isinstance(a, torch.Tensor) else a for i, a in enumerate(args))
         outs = self.fn(*[a.clone() if isinstance(a, torch.Tensor) else a for a in ins])
         outs = tuple(outs) if isinstance(outs, (tuple, list)) else (outs,)
-        e = (ins, _FakeGraph(self.fn, ins, outs), outs)
-        self.entries[key] = e
-        self.captures += 1
-        return e
+        if self.donate_outputs:  # a real graph holds no tensor objects: write through the stored storage
+            from lightning_thunder_amd.transforms.hipgraph import _view_of
+
+            g = _FakeGraph(self.fn, ins, lambda: [_view_of(m) for m in self.entries[key][2]])
+        else:
+            g = _FakeGraph(self.fn, ins, outs)
+        return self._store(key, ins, g, outs)
 
 
 def _write_rows(cache, x, pos):
@@ -266,3 +270,24 @@ def test_runner_inference_mode_cpu():
             for step in range(4):
                 r(A, torch.full((1, D), float(gen * 10 + step)), torch.tensor([step]))
             torch.testing.assert_close(A[:4, 0], torch.tensor([gen * 10 + s for s in range(4)], dtype=A.dtype))
+
+
+def test_donated_outputs_are_adopted_and_guarded_cpu():
+    """donate_grads: a replay hands out fresh tensor objects over the graph's output storage (so
+    AccumulateGrad can adopt them without a clone) and refuses to overwrite an output that is still
+    referenced from the previous replay."""
+    owner = HipGraphTransform(donate_grads=True)
+    r = _CpuRunner(lambda x: (x * 2.0,), "HipGraphD", owner, private_inputs=(True,), donate_outputs=True)
+    x = torch.ones(4)
+    r(x)  # warm-up (eager)
+    a = r(x)[0]  # capture
+    torch.testing.assert_close(a, x * 2)
+    ptr = a.data_ptr()
+    del a
+    b = r(x + 1)[0]  # replay: same storage, fresh tensor object
+    assert b.data_ptr() == ptr
+    torch.testing.assert_close(b, (x + 1) * 2)
+    with pytest.raises(RuntimeError, match="still referenced"):
+        r(x)  # b is alive: the replay would overwrite it
+    del b
+    torch.testing.assert_close(r(x)[0], x * 2)
