@@ -21,6 +21,7 @@ import torch
 
 from ..core import dtypes, prims
 from ..core.baseutils import check
+from ..core.symbolic import SymInt
 from ..core.devices import to_device
 from ..core.proxies import TensorProxy, NumberProxy, Proxy, pyval, FutureTensorProxy
 from ..core.symbol import Symbol, register_symbol, NON_DIFFERENTIABLE_TAG
@@ -1256,7 +1257,8 @@ def mean(a, dim=None, keepdim: bool = False, *, dtype=None):
     x = clang.maybe_convert_to_dtype(a, compute)
     n = math.prod(a.shape[d] for d in dims) if a.ndim else 1
     out = prims.sum(x, dims) if a.ndim else x
-    out = prims.div(out, builtins.float(n))
+    # a symbolic element count stays symbolic (the division happens at run time on the bound dims)
+    out = prims.div(out, n if isinstance(n, SymInt) else builtins.float(n))
     return _restore_keepdim(clang.maybe_convert_to_dtype(out, result_dtype), a, dims, keepdim)
 
 

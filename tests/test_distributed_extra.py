@@ -234,8 +234,14 @@ def test_rccl_policy_defaults_and_presets():
     from lightning_thunder_amd.distributed import rccl_policy
 
     env = {}
+    # the measured decision (profiles/cu_contention_r6.txt): finish collectives fast, every CU a channel
+    # holds costs the one-tile-per-CU GEMMs a whole extra wave however many channels there are
+    assert rccl_policy.apply(env) == {"TORCH_NCCL_AVOID_RECORD_STREAMS": "1", "NCCL_MIN_NCHANNELS": "32"}
+    env = {"LTA_RCCL_POLICY": "narrow"}
+    rccl_policy.apply(env)
+    assert env["NCCL_MAX_NCHANNELS"] == "8" and "NCCL_MIN_NCHANNELS" not in env
+    env = {"LTA_RCCL_POLICY": "rccl"}
     assert rccl_policy.apply(env) == {"TORCH_NCCL_AVOID_RECORD_STREAMS": "1"}
-    assert "NCCL_MIN_NCHANNELS" not in env  # RCCL's own channel tuning by default (CUs stay with the GEMMs)
     env = {"LTA_RCCL_POLICY": "wide", "NCCL_MIN_NCHANNELS": "8"}
     rccl_policy.apply(env)
     assert env["NCCL_MIN_NCHANNELS"] == "8"  # an explicit setting wins
