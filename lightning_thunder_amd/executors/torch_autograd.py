@@ -11,10 +11,27 @@ import torch
 from torch.autograd.function import once_differentiable
 
 
+from ..core.pytree import LEAF as _LEAF
+
+_ONE_TENSOR = [True]
+
+
 class ThunderFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, entry, n_inputs, *flat_inputs):
         out, saved_tensors, saved_other = entry.forward_fn(*flat_inputs)
+        if type(out) is torch.Tensor and entry.diff_output_mask == [True]:
+            # the common case (a loss / one activation): no output tree to walk
+            ctx.entry = entry
+            ctx.overlap_params = getattr(entry, "_overlap_params", None)
+            ctx.saved = list(saved_tensors) + list(saved_other)
+            ctx.n_inputs = n_inputs
+            ctx.out_is_tensor = _ONE_TENSOR
+            ctx.diff_shapes = [tuple(out.shape)]
+            entry._last_out_spec = _LEAF
+            entry._last_flat_out = [out]
+            ctx.set_materialize_grads(False)
+            return (out,)
         from ..core.pytree import tree_flatten
 
         flat_out, out_spec = tree_flatten(out)
@@ -100,6 +117,9 @@ def connect_to_autograd(entry, flat_inputs):
     entry._overlap_params = None
     from ..core.pytree import tree_unflatten
 
+    if entry._last_out_spec is _LEAF:
+        entry._last_flat_out = None
+        return outs[0]
     flat_out = list(entry._last_flat_out)
     it = iter(outs)
     for i, o in enumerate(flat_out):
