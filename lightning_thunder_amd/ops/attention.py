@@ -37,11 +37,12 @@ register_signature("lta_attn_bwd_ex2", [c_int, c_void_p, c_void_p, c_void_p, c_v
                                         ctypes.c_uint64, c_void_p, c_void_p])
 register_signature("lta_attn_bwd_rope", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
-                                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+                                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         ctypes.c_int64, c_int, c_void_p])
 register_signature("lta_attn_bwd_rope_ds", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                             c_int, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                            c_void_p, ctypes.c_int64, c_void_p])
+                                            c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, c_int, c_void_p])
 register_signature("lta_attn_bwd_ex3", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                         c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_uint64,
@@ -235,6 +236,35 @@ def _dq_from_ds(ws_bytes: int, device: torch.device | None = None) -> bool:
     return 2 * ws_bytes <= free + spare
 
 
+def gqa_split(B: int, Hq: int, Hkv: int, S: int) -> int:
+    """How many workgroups share one kv group's query heads in the dK/dV pass.  The pass runs one
+    workgroup per (batch, kv head, 256 keys): for GQA models (Mistral / Llama-3: 8 kv heads) that is
+    128 workgroups at T = 4096, half of the 256 CUs, each sweeping 4 query heads.  Splitting the heads
+    over workgroups (fp32 partial dK / dV rows, summed by one reduce launch) targets >= 2 waves of
+    workgroups; LTA_ATTN_GQA_SPLIT caps it (1 = off)."""
+    group = Hq // Hkv
+    if group <= 1:
+        return 1
+    cap = int(os.environ.get("LTA_ATTN_GQA_SPLIT", "8"))
+    n_wg = B * Hkv * ((S + 255) // 256)
+    best = 1
+    for d in range(2, group + 1):
+        if group % d or d > cap:
+            continue
+        best = d
+        if n_wg * d >= 512:
+            break
+    return best if n_wg < 512 else 1
+
+
+def _gqa_workspace(B, Hq, Hkv, S, device):
+    hs = gqa_split(B, Hq, Hkv, S)
+    if hs <= 1:
+        return None, 0, 1
+    ws = torch.empty(hs * B * Hkv * S * 256, device=device, dtype=torch.float32)
+    return ws, ws.numel() * 4, hs
+
+
 def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):
     """The attention backward and the backward of the rotate-half RoPE + qkv split in one pass:
     returns d(qkv) [B, T, (n_head + 2 n_query_groups) * 128], with dQ / dK rotated back in the
@@ -259,6 +289,7 @@ def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: in
         esz = dqkv.element_size()
         rc = -1
         n_ws = B * Hq * S * ((T + 255) // 256 * 256)
+        part, part_bytes, hsplit = _gqa_workspace(B, Hq, Hkv, S, q.device)
         # the kernel's own shape rules (T == S checked above, T % 64) before the workspace is allocated
         if T > 0 and T % 64 == 0 and Hq % Hkv == 0 and _dq_from_ds(n_ws * esz, q.device):
             ws = torch.empty(n_ws, device=q.device, dtype=q.dtype)
@@ -266,14 +297,16 @@ def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: in
                                           ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq,
                                           Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p),
                                           ctypes.cast(qkv_st, c_void_p), ctypes.cast(gst, c_void_p), ptr(cs), ptr(sn),
-                                          ptr(ws), ws.numel() * ws.element_size(), stream_ptr(q.device))
+                                          ptr(ws), ws.numel() * ws.element_size(), ptr(part), part_bytes, hsplit,
+                                          stream_ptr(q.device))
             if rc != -1:
                 check(rc, "lta_attn_bwd_rope_ds")
                 return dqkv
         rc = lib.lta_attn_bwd_rope(dcode(qq), ptr(dd), ptr(qq), ptr(kk), ptr(vv), ptr(oo), ptr(lse), ptr(delta),
                                    ptr(dqkv), ptr(dqkv) + Hq * D * esz, ptr(dqkv) + (Hq + Hkv) * D * esz, B, Hq, Hkv, T,
                                    S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ctypes.cast(qkv_st, c_void_p),
-                                   ctypes.cast(gst, c_void_p), ptr(cs), ptr(sn), stream_ptr(q.device))
+                                   ctypes.cast(gst, c_void_p), ptr(cs), ptr(sn), ptr(part), part_bytes, hsplit,
+                                   stream_ptr(q.device))
         if rc != -1:
             check(rc, "lta_attn_bwd_rope")
             return dqkv

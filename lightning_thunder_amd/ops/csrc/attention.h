@@ -116,6 +116,8 @@ struct AttnExtra {
   float keep_scale;       // 1 / (1 - p)
   unsigned keep_thresh;   // keep iff hash >= p * 2^32
   unsigned seed_lo, seed_hi, offset;
+  float* part;            // GQA head split of the dK/dV pass: fp32 partial rows [hsplit][B Hkv Sk][2][128]
+  int hsplit;             // > 1: query heads of a kv group split over that many workgroups (attn_bwd_dkdv_reduce sums)
 };
 
 // Counter-based dropout mask: a pure function of (seed, offset, query head, query, key), so the

@@ -93,6 +93,41 @@ __device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const f16x8& a, const
 // values first — d and its partner d + 64 are tiles dt and dt + 2 of the same lane:
 //   o[d] = x[d] cos[d] + x[d+64] sin[d+64],  o[d+64] = x[d+64] cos[d+64] - x[d] sin[d]
 // (the rotation the forward applied to q / k, transposed: csrc/rope.hip's backward, one rounding).
+// fp32 variant (the GQA head split's partial rows, summed by attn_bwd_dkdv_reduce): same layout and
+// rotation, 4 consecutive d per 16-byte store
+template <typename ACC>
+__device__ __forceinline__ void store_row_d128_f32(float* row, const ACC& acc, float mul, int h, const float* cs,
+                                                   const float* sn) {
+  if (cs == nullptr) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<float4*>(row + dt * 32 + 8 * a + 4 * h) =
+            make_float4(acc[dt][4 * a] * mul, acc[dt][4 * a + 1] * mul, acc[dt][4 * a + 2] * mul, acc[dt][4 * a + 3] * mul);
+    return;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int d = dt * 32 + 8 * a + 4 * h;
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + d), s1 = *reinterpret_cast<const float4*>(sn + d);
+      const float4 c2 = *reinterpret_cast<const float4*>(cs + d + 64), s2 = *reinterpret_cast<const float4*>(sn + d + 64);
+      const float cl[4] = {c1.x, c1.y, c1.z, c1.w}, sl[4] = {s1.x, s1.y, s1.z, s1.w};
+      const float ch[4] = {c2.x, c2.y, c2.z, c2.w}, sh[4] = {s2.x, s2.y, s2.z, s2.w};
+      float lo[4], hi[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = acc[dt][4 * a + e] * mul, x2 = acc[dt + 2][4 * a + e] * mul;
+        lo[e] = x1 * cl[e] + x2 * sh[e];
+        hi[e] = x2 * ch[e] - x1 * sl[e];
+      }
+      *reinterpret_cast<float4*>(row + d) = make_float4(lo[0], lo[1], lo[2], lo[3]);
+      *reinterpret_cast<float4*>(row + d + 64) = make_float4(hi[0], hi[1], hi[2], hi[3]);
+    }
+}
+
 template <typename T, typename ACC>
 __device__ __forceinline__ void store_row_d128(T* row, const ACC& acc, float mul, int h, const float* cs,
                                                const float* sn) {
@@ -491,7 +526,7 @@ constexpr int kKB3 = 256;
 // first 64 query tiles, kept in LDS and copied to `dbg` at the end ([4 waves][64 tiles][8] u64)
 // WDS: also store dS^T to `dSt` (the dQ-from-dS path); a template flag so the default build keeps
 // its register allocation
-template <typename T, bool CAUSAL, int STAMP = 0, bool WDS = false>
+template <typename T, bool CAUSAL, int STAMP = 0, bool WDS = false, bool SPLIT = false>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                        const T* __restrict__ V, const T* __restrict__ dO,
                                                                        const float* __restrict__ LSE,
@@ -499,7 +534,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
                                                                        T* __restrict__ dV, int Hq, int Hkv, int Tq, int Sk,
                                                                        float scale, float scale_log2, RowStrides sdo, QKVStrides sx,
                                                                        int qrev = 0, uint64_t* dbg = nullptr,
-                                                                       T* __restrict__ dSt = nullptr) {
+                                                                       T* __restrict__ dSt = nullptr, int hsplit = 1,
+                                                                       float* __restrict__ part = nullptr) {
   constexpr int D = 128;
   using C = BCfg<D>;
   using F = typename Frag<T>::type;
@@ -512,9 +548,15 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   short* Vs = reinterpret_cast<short*>(smem + VOFF);
 
   const int kb = (int)blockIdx.y;
-  const int bh = blockIdx.x;
+  // GQA head split (hsplit > 1): workgroup x = (b, kv head, split) and the split owns group / hsplit of
+  // the kv group's query heads, storing fp32 partial dK / dV rows to `part` ([hsplit][B Hkv Sk][2][128],
+  // summed by attn_bwd_dkdv_reduce): B Hkv key blocks alone do not fill 256 CUs when Hkv is small
+  // SPLIT is a template flag so the unsplit build keeps its scalar-register allocation (no spills)
+  const int nsplit = SPLIT ? hsplit : 1;
+  const int bh = SPLIT ? (int)blockIdx.x / nsplit : (int)blockIdx.x, hs = SPLIT ? (int)blockIdx.x % nsplit : 0;
   const int b = bh / Hkv, hk = bh % Hkv;
   const int group = Hq / Hkv;
+  const int gsz = group / nsplit, hbase = hk * group + hs * gsz;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -552,7 +594,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
   const int n_qt = (Tq + kQT - 1) / kQT;
   const int qt_begin = CAUSAL ? min((kb * kKB3) / kQT, n_qt) : 0;
   const int nq = n_qt - qt_begin;
-  const int total = group * nq;
+  const int total = gsz * nq;
 
   float plse = 0.f, pdel = 0.f;
   auto stash_stats = [&](int st) {
@@ -563,7 +605,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
     }
   };
   auto issue = [&](int hi, int ti, int st) {
-    const int hq = hk * group + hi;
+    const int hq = hbase + hi;
     // qrev: every key block sweeps the query tiles from the last one down, so the workgroups of one
     // head (one XCD: grid x = head) read the same Q / dO tile at about the same time (L2 reuse)
     const int qbase = (qt_begin + (qrev ? nq - 1 - ti : ti)) * kQT;
@@ -774,7 +816,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
           // the next kernel reads them, nothing in this one does.  Buffer stores: the wave's 64 key rows as one resource whose size drops the rows past Sk,
           // the half j as a scalar offset, so the loop spends one VGPR on the address (every term is
           // wave-uniform; readfirstlane says so, or the resource would be waterfalled)
-          const int hq_cur = hk * group + it / nq;
+          const int hq_cur = hbase + it / nq;
           const int nqb = (Tq + 255) >> 8;
           const uint64_t wa = (uint64_t)(uintptr_t)(dSt + ((((int64_t)(b * Hq + hq_cur) * nqb + (qbase >> 8)) * Sk + kw) * 256 +
                                                            (qbase & 255)));
@@ -819,6 +861,21 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_v4_kernel(const T* 
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[j][dt]), "+a"(dvacc[j][dt]));
 
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int key = kw + 32 * j + r;
+      if (key < Sk) {
+        const int64_t nbh = gridDim.x / nsplit;
+        float* prow = part + (((int64_t)hs * nbh + bh) * Sk + key) * 256;
+        const bool rope = sx.rope_cos != nullptr;
+        store_row_d128_f32(prow, dkacc[j], scale, h, rope ? sx.rope_cos + (int64_t)key * 128 : nullptr,
+                           rope ? sx.rope_sin + (int64_t)key * 128 : nullptr);
+        store_row_d128_f32(prow + 128, dvacc[j], 1.f, h, nullptr, nullptr);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 32 * j + r;
@@ -1485,10 +1542,60 @@ int g_dkdv_qrev = [] {
                        sl2, sdo, ex.sx, g_dkdv_qrev, nullptr)
 #else
 #define LTA_DKDV_LAUNCH(CA)                                                                                          \
-  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,         \
-                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
-                     sdo, ex.sx, g_dkdv_qrev, nullptr)
+  {                                                                                                                  \
+    const int hsplit = (ex.part && ex.hsplit > 1) ? ex.hsplit : 1;                                                   \
+    dim3 gks(gk.x * hsplit, gk.y);                                                                                   \
+    if (hsplit > 1) {                                                                                                \
+      hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, false, true>), gks, blk, 0, s, (const T*)Q, (const T*)K, \
+                         (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv,   \
+                         Tq, Sk, scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, nullptr, hsplit, ex.part);            \
+      launch_dkdv_reduce<T>(dK, dV, B, Hkv, Sk, ex, s);                                                              \
+    } else {                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA>), gk, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,     \
+                         (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk,       \
+                         scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr);                                              \
+    }                                                                                                                \
+  }
 #endif
+
+// Sum of the GQA head split's fp32 partial dK / dV rows -> the gradients' dtype at their strides.
+// One thread per 8 consecutive d of one (kv head, key, dK|dV) row.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_reduce(const float* __restrict__ part, T* __restrict__ dK,
+                                                            T* __restrict__ dV, int nbh, int Hkv, int Sk, int hsplit,
+                                                            QKVStrides sx) {
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (int64_t)nbh * Sk * 32) return;
+  const int c = (int)(id & 15);
+  const int64_t row = id >> 4;  // (bh * Sk + key) * 2 + which
+  const int which = (int)(row & 1);
+  const int64_t bk = row >> 1;
+  const int key = (int)(bk % Sk), bh = (int)(bk / Sk);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < hsplit; ++s) {
+    const float4* src = reinterpret_cast<const float4*>(part + (((int64_t)s * nbh + bh) * Sk + key) * 256 + which * 128 + c * 8);
+    const float4 a = src[0], b = src[1];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  }
+  const int b = bh / Hkv, hk = bh % Hkv;
+  T* dst = which ? dV + (int64_t)b * sx.dvb + (int64_t)hk * sx.dvh + (int64_t)key * sx.dvt
+                 : dK + (int64_t)b * sx.dkb + (int64_t)hk * sx.dkh + (int64_t)key * sx.dkt;
+  union {
+    T v[8];
+    uint4 u;
+  } pk;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pk.v[e] = from_f32<T>(acc[e]);
+  *reinterpret_cast<uint4*>(dst + c * 8) = pk.u;
+}
+
+template <typename T>
+void launch_dkdv_reduce(void* dK, void* dV, int B, int Hkv, int Sk, const AttnExtra& ex, hipStream_t s) {
+  const int64_t n = (int64_t)B * Hkv * Sk * 32;
+  hipLaunchKernelGGL((attn_bwd_dkdv_reduce<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     (const float*)ex.part, (T*)dK, (T*)dV, B * Hkv, Hkv, Sk, ex.hsplit, ex.sx);
+}
 
 // dQ from the stored dS (attn_bwd_dq_ds_kernel): delta by the preprocess kernel, dK / dV (+ dS^T
 // into ds_ws), then the dQ product.  D = 128, Tq == Sk, Sk % 64 == 0, Tq % 32 == 0.
@@ -1501,11 +1608,19 @@ int launch_bwd_ds(const void* dO, const void* Q, const void* K, const void* V, c
   dim3 blk(kThreads);
   hipLaunchKernelGGL((attn_bwd_preprocess<T, 128>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                      (const T*)dO, (const T*)O, (float*)DELTA, rows, Hq, Tq, sdo, so);
-  dim3 gk(B * Hkv, (Sk + kKB3 - 1) / kKB3), gq(B * Hq, (Tq + 255) / 256);
+  const int hsplit = (ex.part && ex.hsplit > 1) ? ex.hsplit : 1;
+  dim3 gk(B * Hkv * hsplit, (Sk + kKB3 - 1) / kKB3), gq(B * Hq, (Tq + 255) / 256);
 #define LTA_DS(CA)                                                                                                   \
-  hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, true>), gk, blk, 0, s, (const T*)Q, (const T*)K,          \
-                     (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, \
-                     scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, (T*)dS);                                                        \
+  if (hsplit > 1) {                                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, true, true>), gk, blk, 0, s, (const T*)Q, (const T*)K,   \
+                       (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq,  \
+                       Sk, scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, (T*)dS, hsplit, ex.part);                   \
+    launch_dkdv_reduce<T>(dK, dV, B, Hkv, Sk, ex, s);                                                                \
+  } else {                                                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dkdv_v4_kernel<T, CA, 0, true>), gk, blk, 0, s, (const T*)Q, (const T*)K,          \
+                       (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq,  \
+                       Sk, scale, sl2, sdo, ex.sx, g_dkdv_qrev, nullptr, (T*)dS);                                    \
+  }                                                                                                                  \
   hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<T, CA>), gq, blk, 0, s, (const T*)K, (const T*)dS, (T*)dQ, Hq, Hkv, Tq,   \
                      Sk, scale, ex.sx)
   if (causal) { LTA_DS(true); }
@@ -1578,6 +1693,17 @@ static int fast_enabled() {
   return fast;
 }
 
+// GQA head split of the dK/dV pass (hsplit > 1 with an fp32 workspace of hsplit B Hkv Sk 256 floats):
+// validates it and records it in `ex`.  hsplit <= 1 or no workspace: no split.
+static bool gqa_split_ok(AttnExtra& ex, void* part_ws, int64_t part_bytes, int hsplit, int B, int Hq, int Hkv, int Sk) {
+  if (hsplit <= 1 || part_ws == nullptr) return true;
+  const int group = Hq / Hkv;
+  if (group % hsplit != 0 || part_bytes < (int64_t)hsplit * B * Hkv * Sk * 256 * 4 || (uintptr_t)part_ws % 16) return false;
+  ex.part = static_cast<float*>(part_ws);
+  ex.hsplit = hsplit;
+  return true;
+}
+
 // Attention backward with the RoPE backward fused into the dQ / dK epilogues (self-attention,
 // D = 128, no mask / dropout, dK/dV v4 + dQ v2..v4): rope_cos / rope_sin are fp32 [Tq][128] (the
 // forward rotated q and k with them), dQ / dK / dV may point into one [B, T, (Hq + 2 Hkv) * 128]
@@ -1587,7 +1713,8 @@ LTA_EXPORT int lta_attn_bwd_rope(int dtype, const void* dO, const void* Q, const
                                  const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
                                  int Tq, int Sk, int D, float scale, int causal, const int64_t* strides,
                                  const int64_t* qkv_strides, const int64_t* grad_strides, const float* rope_cos,
-                                 const float* rope_sin, hipStream_t stream) {
+                                 const float* rope_sin, void* part_ws, int64_t part_bytes, int hsplit,
+                                 hipStream_t stream) {
   if (D != 128 || Tq != Sk || Tq <= 0 || Hq % Hkv != 0 || !rope_cos || !rope_sin || !fast_enabled())
     return -1;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
@@ -1598,6 +1725,7 @@ LTA_EXPORT int lta_attn_bwd_rope(int dtype, const void* dO, const void* Q, const
   ex.sx.set_grad(grad_strides);
   ex.sx.rope_cos = rope_cos;
   ex.sx.rope_sin = rope_sin;
+  if (!gqa_split_ok(ex, part_ws, part_bytes, hsplit, B, Hq, Hkv, Sk)) return -2;
   if (dtype == kBF16)
     return launch_bwd<__hip_bfloat16, 128>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, B, Hq, Hkv, Tq, Sk, scale, causal, sdo,
                                            so, 1, ex, 0, stream);
@@ -1621,7 +1749,7 @@ LTA_EXPORT int lta_attn_bwd_rope_ds(int dtype, const void* dO, const void* Q, co
                                     int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
                                     const int64_t* strides, const int64_t* qkv_strides, const int64_t* grad_strides,
                                     const float* rope_cos, const float* rope_sin, void* ds_ws, int64_t ds_bytes,
-                                    hipStream_t stream) {
+                                    void* part_ws, int64_t part_bytes, int hsplit, hipStream_t stream) {
   if (D != 128 || Tq != Sk || Tq <= 0 || Tq % 32 || Sk % 64 || Hq % Hkv != 0 || !rope_cos || !rope_sin || !ds_ws ||
       ds_bytes < (int64_t)B * Hq * ((Tq + 255) / 256) * 256 * Sk * 2)
     return -1;
@@ -1633,6 +1761,7 @@ LTA_EXPORT int lta_attn_bwd_rope_ds(int dtype, const void* dO, const void* Q, co
   ex.sx.set_grad(grad_strides);
   ex.sx.rope_cos = rope_cos;
   ex.sx.rope_sin = rope_sin;
+  if (!gqa_split_ok(ex, part_ws, part_bytes, hsplit, B, Hq, Hkv, Sk)) return -2;
   if (dtype == kBF16)
     return launch_bwd_ds<__hip_bfloat16>(dO, Q, K, V, O, LSE, DELTA, dQ, dK, dV, ds_ws, B, Hq, Hkv, Tq, Sk, scale,
                                          causal, sdo, so, ex, stream);

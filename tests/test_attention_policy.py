@@ -26,3 +26,19 @@ def test_dq_from_ds_forced(monkeypatch, mode, expect):
 @pytest.mark.parametrize("D,Dp", [(64, 64), (128, 128), (256, 256), (80, 96), (192, 256), (8, 64), (264, None), (100, None)])
 def test_padded_head_dim(D, Dp):
     assert A.padded_head_dim(D) == Dp
+
+
+def test_gqa_head_split_rule(monkeypatch):
+    """dK/dV head split: only GQA, only while the (batch, kv head, 256-key block) grid is under two
+    waves of 256 CUs, by a divisor of the group size, capped by LTA_ATTN_GQA_SPLIT."""
+    from lightning_thunder_amd.ops import attention as A
+
+    assert A.gqa_split(1, 32, 32, 4096) == 1            # MHA: no split
+    assert A.gqa_split(1, 32, 8, 4096) == 4             # Mistral / Llama-3-8B: 128 workgroups -> 512
+    assert A.gqa_split(4, 32, 8, 4096) == 1             # 512 workgroups already
+    assert A.gqa_split(1, 64, 8, 4096) == 4             # Llama-2-70B: group 8, 128 -> 512
+    assert A.gqa_split(1, 8, 1, 320) == 8               # MQA, one key block: the largest divisor
+    monkeypatch.setenv("LTA_ATTN_GQA_SPLIT", "2")
+    assert A.gqa_split(1, 32, 8, 4096) == 2
+    monkeypatch.setenv("LTA_ATTN_GQA_SPLIT", "1")
+    assert A.gqa_split(1, 32, 8, 4096) == 1

@@ -1223,7 +1223,8 @@ def test_attention_backward_with_fused_rope(B, Hq, Hkv, T, causal):
 @pytest.mark.parametrize("B,Hq,Hkv,T,causal,do_layout", [(1, 4, 2, 512, True, "bhtd"), (2, 4, 4, 256, False, "bhtd"),
                                                           (1, 8, 1, 320, True, "bhtd"), (1, 2, 2, 1088, False, "bhtd"),
                                                           (1, 4, 2, 512, True, "bthd"),
-                                                          (1, 32, 32, 4096, True, "bthd")])
+                                                          (1, 32, 32, 4096, True, "bthd"),
+                                                          (1, 32, 8, 4096, True, "bthd")])
 def test_attention_backward_dq_from_ds(B, Hq, Hkv, T, causal, do_layout, monkeypatch):
     """dQ = scale dS K from the dS^T the dK/dV kernel stores (the default while the workspace fits),
     against the recompute path (LTA_ATTN_DQ_FROM_DS=0) and an fp32 reference.  ``bthd``: dO stored
