@@ -1118,6 +1118,30 @@ def test_lds_dma_out_of_range_lanes_write_zero():
     assert (out[valid:] == 0).all(), out[valid:valid + 32]
 
 
+@pytest.mark.gpu
+def test_cu_occupier_exits_and_gemm_stays_correct():
+    """The CU-contention probe (scripts/cu_contention.py): RCCL-shaped workgroups (37,664 B LDS) held
+    on a high-priority stream end on their own (bounded by the real-time counter), and a hand GEMM
+    issued meanwhile on the compute stream is still exact."""
+    from lightning_thunder_amd.ops.gemm import linear
+
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from cu_contention import occupier
+
+    occupy, hi = occupier()
+    x = torch.randn(1024, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(2048, 4096, device="cuda", dtype=torch.bfloat16)
+    occupy(16, 256, 37664, 0.02)
+    y = linear(x, w)
+    torch.cuda.current_stream().synchronize()
+    hi.synchronize()
+    ref = x.float() @ w.float().t()
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
 def _ragged_offsets(M, G, device):
     # uneven groups incl. an empty one and sizes that divide neither 64 nor 256
     sizes = torch.tensor([300, 0, 77, 513, 1, 129, 600, 0][:G])
