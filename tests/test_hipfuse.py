@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import lightning_thunder_amd as thunder
+from lightning_thunder_amd.core.prims import PrimIDs
 from lightning_thunder_amd.core.proxies import TensorProxy
 from lightning_thunder_amd.executors import hipfuse
 from lightning_thunder_amd.executors import hipfuse_codegen as cg
@@ -606,3 +607,24 @@ def test_generated_sources_compile_cpu(case, cpu_fusion):
     for o, r in zip(out if isinstance(out, tuple) else (out,), ref if isinstance(ref, tuple) else (ref,)):
         torch.testing.assert_close(o, r, rtol=1e-5, atol=1e-5)
     assert _compile_fusions_of(jf) >= 1
+
+
+def test_trailing_transpose_left_as_view_cpu(cpu_fusion):
+    """A region value consumed transposed by a GEMM (autodiff's wgrad operand dY^T) is stored once,
+    untransposed; the reshape/transpose chain runs after the region as zero-copy views instead of
+    the region storing a transposed copy (Gemma's GeGLU backward stored two [24576, 4096] copies)."""
+    def f(a, b, w):
+        d = torch.nn.functional.gelu(a, approximate="tanh") * b
+        g = d.reshape(-1, d.shape[-1])
+        return d, g.t() @ w
+
+    a, b, w = torch.randn(1, 8, 16), torch.randn(1, 8, 16), torch.randn(8, 4)
+    jf = thunder.jit(f, executors=["hipfuse", "torch"])
+    for o, r in zip(jf(a, b, w), f(a, b, w)):
+        torch.testing.assert_close(o, r, rtol=1e-5, atol=1e-5)
+    tr = thunder.last_traces(jf)[-1]
+    fus = hipfuse.fusions(tr)
+    assert fus
+    for fb in fus:
+        assert all(tuple(o.shape) != (16, 8) for o in fb.flat_proxy_outs), fb
+        assert all(s.sym.id != PrimIDs.TRANSPOSE for s in fb.subsymbols)
