@@ -6,6 +6,7 @@
 //                  the amax feeds the *next* step's scale, so one pass over x suffices)
 // cast_transpose:  the same, plus the transposed fp8 copy the backward GEMMs read (dgrad needs
 //                  W^T, wgrad needs X^T and dY^T; all three GEMMs then run on the one NT kernel)
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -70,22 +71,22 @@ __global__ __launch_bounds__(256) void amax_kernel(const T* __restrict__ x, int6
   if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
-template <typename T, bool E5M2>
+template <typename T, bool E5M2, int U = 2>
 __global__ __launch_bounds__(256) void cast_kernel(const T* __restrict__ x, uint8_t* __restrict__ y, int64_t n,
                                                    const float* __restrict__ amax_in, float fmax,
                                                    float* __restrict__ scale_out, float* __restrict__ amax) {
   const float s = dev_scale(amax_in, fmax, scale_out);
   float m = 0.f;
   const int64_t nv = n / 8, stride = (int64_t)gridDim.x * blockDim.x;
-  // two 8-element vectors per thread and iteration (both loads issued before the first conversion),
+  // U 8-element vectors per thread and iteration (all loads issued before the first conversion),
   // two elements per hardware conversion (cvt4)
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + stride < nv; i += 2 * stride) {
-    float v[2][8];
-    load8(x + i * 8, v[0]);
-    load8(x + (i + stride) * 8, v[1]);
+  for (; i + (U - 1) * stride < nv; i += U * stride) {
+    float v[U][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) load8(x + (i + u * stride) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[u][j]));
       const uint32_t lo = cvt4<E5M2>(v[u][0] * s, v[u][1] * s, v[u][2] * s, v[u][3] * s);
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void cast_kernel(const T* __restrict__ x, uint
       *reinterpret_cast<uint2*>(y + (i + u * stride) * 8) = make_uint2(lo, hi);
     }
   }
-  if (i < nv) {
+  for (; i < nv; i += stride) {
     float v[8];
     load8(x + i * 8, v);
 #pragma unroll
@@ -383,12 +384,29 @@ __global__ void mfma_probe_kernel(const v8i* __restrict__ a, const v8i* __restri
 
 }  // namespace
 
+// grid / unroll of the plain cast: LTA_CAST_CFG = "<max workgroups>,<vectors per thread>" (A/B hook,
+// scripts/fp8_cast_bench.py); the default is the measured fastest of that sweep
+static int g_cast_wgs = 512, g_cast_u = 4;
+static bool g_cast_cfg_read = false;
 template <typename T, bool E5>
 static void launch_cast(const void* x, void* y, int64_t n, const void* amax_in, float fmax, void* scale_out,
                         void* amax, hipStream_t s) {
-  dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 1024)), block(256);
-  hipLaunchKernelGGL((cast_kernel<T, E5>), grid, block, 0, s, (const T*)x, (uint8_t*)y, n, (const float*)amax_in, fmax,
-                     (float*)scale_out, (float*)amax);
+  if (!g_cast_cfg_read) {
+    g_cast_cfg_read = true;
+    if (const char* e = std::getenv("LTA_CAST_CFG")) {
+      int w = 0, u = 0;
+      if (sscanf(e, "%d,%d", &w, &u) == 2 && w > 0 && (u == 1 || u == 2 || u == 4 || u == 8)) g_cast_wgs = w, g_cast_u = u;
+    }
+  }
+  dim3 grid((unsigned)std::min<int64_t>((n / 8 + 255) / 256, g_cast_wgs)), block(256);
+#define LTA_CAST(UU)                                                                                               \
+  hipLaunchKernelGGL((cast_kernel<T, E5, UU>), grid, block, 0, s, (const T*)x, (uint8_t*)y, n, (const float*)amax_in, \
+                     fmax, (float*)scale_out, (float*)amax)
+  if (g_cast_u == 4) LTA_CAST(4);
+  else if (g_cast_u == 8) LTA_CAST(8);
+  else if (g_cast_u == 1) LTA_CAST(1);
+  else LTA_CAST(2);
+#undef LTA_CAST
 }
 
 template <typename T, bool E5>
@@ -406,6 +424,14 @@ static void launch_cast_t(const void* x, void* y, void* yt, int R, int C, const 
   dim3 grid((unsigned)std::min<int64_t>((int64_t)(C / 64) * (R / 64), 1024)), block(256);
   hipLaunchKernelGGL((cast_transpose_kernel<T, E5>), grid, block, 0, s, (const T*)x, (uint8_t*)y, (uint8_t*)yt, R, C,
                      (const float*)amax_in, fmax, (float*)scale_out, (float*)amax);
+}
+
+// A/B hook of the plain cast's grid cap / unroll (scripts/fp8_cast_bench.py); returns the previous cap
+LTA_EXPORT int lta_fp8_cast_set_cfg(int wgs, int u) {
+  g_cast_cfg_read = true;
+  const int old = g_cast_wgs;
+  if (wgs > 0 && (u == 1 || u == 2 || u == 4 || u == 8)) g_cast_wgs = wgs, g_cast_u = u;
+  return old;
 }
 
 // amax_out (zero-initialised by the caller) = max(amax_out, max |x|)
