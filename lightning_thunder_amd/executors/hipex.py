@@ -1192,6 +1192,69 @@ def _fuse_qkv_rope_gemm(trace):
     return new
 
 
+def _fp8_gemm_qkv_rope_impl(qa, qb, sa, sb, out_shape, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    from ..ops.fp8 import gemm_qkv_rope
+
+    return gemm_qkv_rope(qa, qb, sa, sb, out_shape, cos, sin, n_head, n_query_groups, head_size, rope_n)
+
+
+def _fp8_gemm_qkv_rope_meta(qa, qb, sa, sb, out_shape, cos, sin, n_head, n_query_groups, head_size, rope_n):
+    B, T = out_shape[0], out_shape[1]
+    mk = lambda h: TensorProxy(like=sa, shape=(B, h, T, head_size), dtype=torch.bfloat16)  # noqa: E731
+    return mk(n_head), mk(n_query_groups), mk(n_query_groups)
+
+
+hip_fp8_gemm_qkv_rope = ex.register_operator("hip_fp8_gemm_qkv_rope", meta=_fp8_gemm_qkv_rope_meta,
+                                             fn=_fp8_gemm_qkv_rope_impl)
+
+
+def _fuse_fp8_qkv_rope_gemm(trace):
+    """``qkv = hip_fp8_gemm(qx, qw, sx, sw, 0, 0, None, shape); q, k, v = hip_qkv_rope(qkv, ...)`` (qkv
+    read nowhere else) -> ``q, k, v = hip_fp8_gemm_qkv_rope(...)``: the FP8 path's counterpart of
+    :func:`_fuse_qkv_rope_gemm` (csrc/gemm4_fp8.hip QKV epilogue; reference: TransformerEngine's fused
+    attention input projection, thunder/executors/transformer_engineex_impl.py)."""
+    from ..core.trace import from_trace, TraceProvenance
+
+    bsyms = list(trace.bound_symbols)
+    uses: dict[str, list] = {}
+    for k, b in enumerate(bsyms):
+        for a in b.flat_proxy_args:
+            uses.setdefault(a.name, []).append(k)
+    outs = {o.name for o in tree_flatten(trace.output)[0] if isinstance(o, TensorProxy)} if trace.output is not None else set()
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_qkv_rope or len(b.args) != 7:
+            continue
+        qkv, cos, sin, nh, ng, hs, rn = b.args
+        j = producer.get(getattr(qkv, "name", None))
+        if j is None or j in drop or j in replace or bsyms[j].sym is not hip_fp8_gemm or uses.get(qkv.name, []) != [i] \
+                or qkv.name in outs:
+            continue
+        ga = bsyms[j].args
+        if len(ga) < 8 or (len(ga) > 8 and ga[8] is not None) or ga[4] != 0 or ga[5] != 0 or ga[6] is not None:
+            continue
+        out_shape = tuple(ga[7])
+        if len(out_shape) != 3 or not all(isinstance(v, int) for v in (nh, ng, hs, rn) + out_shape):
+            continue
+        if producer.get(getattr(cos, "name", None), -1) > j or producer.get(getattr(sin, "name", None), -1) > j:
+            continue
+        replace[j] = ex.bind_call_ctx(hip_fp8_gemm_qkv_rope.bind(ga[0], ga[1], ga[2], ga[3], out_shape, cos, sin, nh, ng,
+                                                                 hs, rn, output=b.output))
+        drop.add(i)
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} fp8 qkv projection(s) with the RoPE split in the GEMM epilogue"))
+    return new
+
+
 def _attn_bwd_rope_meta(g, q, k, v, o, lse, causal, scale, cos, sin, n_head, n_query_groups):
     B, _, T, D = q.shape
     return TensorProxy(like=g, shape=(B, T, (n_head + 2 * n_query_groups) * D))
@@ -1255,8 +1318,8 @@ def _fuse_attn_bwd_rope(trace):
 
 
 def _post_claim(trace):
-    return _fuse_attn_bwd_rope(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
-        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(_fuse_fp8_cast_producers(trace)))))))))
+    return _fuse_attn_bwd_rope(_fuse_fp8_qkv_rope_gemm(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
+        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(_fuse_fp8_cast_producers(trace))))))))))
 
 
 ex.post_claim_pass = _post_claim

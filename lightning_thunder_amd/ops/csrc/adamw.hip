@@ -6,6 +6,7 @@
 // described by a device table {tensor index, element offset}; every lane moves 16-byte
 // vectors.  Math in fp32.
 #include "common.h"
+#include "fp8_cvt.h"
 #include <cstdlib>
 
 using namespace lta;
@@ -18,6 +19,15 @@ struct TensorMeta {
   void* m;
   void* v;
   int64_t n;
+  // fp8 weight shadow (bf16 params of FP8 linears, ops/fp8.py weight shadows; q == nullptr: none): the
+  // updated weight leaves the kernel also as e4m3 q = sat(p * fmax / *amax_in) -- bitwise the forward's
+  // cast of it -- with the scale used in *scale_out and max |p| folded into *sink (the amax history)
+  uint8_t* q;
+  const float* amax_in;
+  float* scale_out;
+  float* sink;
+  float fmax;
+  int pad_;
 };
 
 constexpr int kChunk = 16384;  // elements per workgroup-chunk
@@ -39,7 +49,7 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 // rate on an idle GPU.  The lean variant (U = 1, <= 80 VGPRs, 6 waves/SIMD) is for the update
 // issued on a side stream during the backward: its waves fit next to a 4-wave gemm4 workgroup
 // (168 VGPR + 256 AGPR per wave), so the optimizer streams HBM while the GEMM keeps the MFMAs busy.
-template <typename TP, typename TS, int U, bool NT = false>
+template <typename TP, typename TS, int U, bool NT = false, bool SHADOW = false>
 __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
                                            float lr, float b1, float b2, float eps, float wd, float bc1,
                                            float bc2_sqrt, float grad_scale) {
@@ -52,8 +62,17 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
   TS* M = (TS*)mt.m;
   TS* V = (TS*)mt.v;
   constexpr int VP = Vec16<TP>::N;
+  [[maybe_unused]] uint8_t* const Q = SHADOW ? mt.q : nullptr;
+  [[maybe_unused]] float qs = 0.f, wmax = 0.f;
+  if constexpr (SHADOW) {
+    if (Q != nullptr) {
+      qs = mt.fmax / fmaxf(*mt.amax_in, 1e-12f);
+      if (ck.y == 0 && threadIdx.x == 0) *mt.scale_out = qs;
+    }
+  }
   const bool vec = ((end - start) % VP == 0) && ((uintptr_t)(P + start) % 16 == 0) && ((uintptr_t)(G + start) % 16 == 0) &&
-                   (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0);
+                   (sizeof(TS) == sizeof(TP)) && ((uintptr_t)(M + start) % 16 == 0) && ((uintptr_t)(V + start) % 16 == 0) &&
+                   (!SHADOW || Q == nullptr || (VP == 8 && (uintptr_t)(Q + start) % 8 == 0));
   if (vec) {
     // U vectors per lane per trip, all loads issued before any math: 4U 16-B loads in flight per lane
     for (int64_t i0 = start + (int64_t)threadIdx.x * VP; i0 < end; i0 += 256 * VP * U) {
@@ -88,6 +107,19 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
             mv[u].v[j] = from_f32<TS>(m);
             vv[u].v[j] = from_f32<TS>(v);
           }
+          if constexpr (SHADOW) {
+            if (Q != nullptr) {
+              float w[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                w[j] = to_f32(pv[u].v[j]);
+                wmax = fmaxf(wmax, fabsf(w[j]));
+              }
+              const uint32_t lo = cvt4<false>(w[0] * qs, w[1] * qs, w[2] * qs, w[3] * qs);
+              const uint32_t hi = cvt4<false>(w[4] * qs, w[5] * qs, w[6] * qs, w[7] * qs);
+              *reinterpret_cast<uint2*>(Q + i) = make_uint2(lo, hi);
+            }
+          }
           if constexpr (NT) {
             store16_nt(P + i, pv[u]);
             store16_nt(M + i, mv[u]);
@@ -107,15 +139,28 @@ __device__ __forceinline__ void adamw_body(const TensorMeta* __restrict__ metas,
       P[i] = from_f32<TP>(p);
       M[i] = from_f32<TS>(m);
       V[i] = from_f32<TS>(v);
+      if constexpr (SHADOW) {
+        if (Q != nullptr) {
+          const float w = to_f32(P[i]);
+          wmax = fmaxf(wmax, fabsf(w));
+          Q[i] = (uint8_t)(cvt4<false>(w * qs, 0.f, 0.f, 0.f) & 0xffu);
+        }
+      }
+    }
+  }
+  if constexpr (SHADOW) {
+    if (Q != nullptr) {  // uniform over the workgroup (one tensor per chunk)
+      __shared__ float red[4];
+      fp8_amax_out<4>(wmax, mt.sink, red);
     }
   }
 }
 
-template <typename TP, typename TS, bool NT = false>
+template <typename TP, typename TS, bool NT = false, bool SHADOW = false>
 __global__ __launch_bounds__(256) void adamw_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks,
                                                     float lr, float b1, float b2, float eps, float wd, float bc1,
                                                     float bc2_sqrt, float grad_scale) {
-  adamw_body<TP, TS, 4, NT>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+  adamw_body<TP, TS, 4, NT, SHADOW>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
 }
 
 // non-temporal loads / stores in the post-backward kernel (LTA_ADAMW_NT=0 turns them off): 5.99 vs
@@ -126,11 +171,11 @@ int g_adamw_nt = [] {
   return (e && e[0] == '0') ? 0 : 1;
 }();
 
-template <typename TP, typename TS>
+template <typename TP, typename TS, bool SHADOW = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void adamw_lean_kernel(
     const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks, float lr, float b1, float b2, float eps,
     float wd, float bc1, float bc2_sqrt, float grad_scale) {
-  adamw_body<TP, TS, 1>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+  adamw_body<TP, TS, 1, false, SHADOW>(metas, chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
 }
 
 }  // namespace
@@ -146,30 +191,42 @@ LTA_EXPORT int lta_adamw_set_nt(int nt) {
 
 // metas: device array of TensorMeta; chunks: device int2 array {tensor, chunk index}
 // lean = 1: the register-capped variant (see adamw_body) for updates overlapped with compute
-LTA_EXPORT int lta_adamw_ex(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr,
-                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, int lean,
-                            hipStream_t stream) {
+// shadow = 1: some tensors carry an fp8 weight shadow (TensorMeta.q; bf16 params only)
+LTA_EXPORT int lta_adamw_ex2(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr,
+                             float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale,
+                             int lean, int shadow, hipStream_t stream) {
   dim3 grid(n_chunks), block(256);
-#define LTA_L(TPt, TSt)                                                                                              \
+#define LTA_L(TPt, TSt, SH)                                                                                          \
   do {                                                                                                               \
     if (lean)                                                                                                        \
-      hipLaunchKernelGGL((adamw_lean_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,            \
+      hipLaunchKernelGGL((adamw_lean_kernel<TPt, TSt, SH>), grid, block, 0, stream, (const TensorMeta*)metas,        \
                          (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
     else if (g_adamw_nt)                                                                                             \
-      hipLaunchKernelGGL((adamw_kernel<TPt, TSt, true>), grid, block, 0, stream, (const TensorMeta*)metas,           \
+      hipLaunchKernelGGL((adamw_kernel<TPt, TSt, true, SH>), grid, block, 0, stream, (const TensorMeta*)metas,       \
                          (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
     else                                                                                                             \
-      hipLaunchKernelGGL((adamw_kernel<TPt, TSt>), grid, block, 0, stream, (const TensorMeta*)metas,                 \
+      hipLaunchKernelGGL((adamw_kernel<TPt, TSt, false, SH>), grid, block, 0, stream, (const TensorMeta*)metas,      \
                          (const int2*)chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);                       \
   } while (0)
-  if (pdtype == kBF16 && sdtype == kBF16) LTA_L(__hip_bfloat16, __hip_bfloat16);
-  else if (pdtype == kBF16 && sdtype == kF32) LTA_L(__hip_bfloat16, float);
-  else if (pdtype == kF16 && sdtype == kF16) LTA_L(__half, __half);
-  else if (pdtype == kF16 && sdtype == kF32) LTA_L(__half, float);
-  else if (pdtype == kF32 && sdtype == kF32) LTA_L(float, float);
+  if (shadow) {
+    if (pdtype == kBF16 && sdtype == kBF16) LTA_L(__hip_bfloat16, __hip_bfloat16, true);
+    else if (pdtype == kBF16 && sdtype == kF32) LTA_L(__hip_bfloat16, float, true);
+    else return -1;
+  } else if (pdtype == kBF16 && sdtype == kBF16) LTA_L(__hip_bfloat16, __hip_bfloat16, false);
+  else if (pdtype == kBF16 && sdtype == kF32) LTA_L(__hip_bfloat16, float, false);
+  else if (pdtype == kF16 && sdtype == kF16) LTA_L(__half, __half, false);
+  else if (pdtype == kF16 && sdtype == kF32) LTA_L(__half, float, false);
+  else if (pdtype == kF32 && sdtype == kF32) LTA_L(float, float, false);
   else return -1;
 #undef LTA_L
   return (int)hipGetLastError();
+}
+
+LTA_EXPORT int lta_adamw_ex(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr,
+                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float grad_scale, int lean,
+                            hipStream_t stream) {
+  return lta_adamw_ex2(pdtype, sdtype, metas, chunks, n_chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale, lean, 0,
+                       stream);
 }
 
 LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* chunks, int n_chunks, float lr, float b1,
@@ -177,3 +234,6 @@ LTA_EXPORT int lta_adamw(int pdtype, int sdtype, const void* metas, const void* 
   return lta_adamw_ex(pdtype, sdtype, metas, chunks, n_chunks, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale, 0,
                       stream);
 }
+
+// bytes of one TensorMeta (the host packs the table)
+LTA_EXPORT int lta_adamw_meta_bytes() { return (int)sizeof(TensorMeta); }

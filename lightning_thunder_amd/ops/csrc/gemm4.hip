@@ -606,8 +606,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
       __hip_bfloat16* const dst = is_q ? C : (is_k ? C2 : C3);
       const int hh = is_q ? cb : (is_k ? cb - ep.nh : cb - ep.nh - ep.ng);
       const int nheads = is_q ? ep.nh : ep.ng;
+      const bool rope = is_q || is_k;
+      // cos / sin of row block m + 1 are loaded while block m is rotated and stored (loading them inside
+      // its own sched region exposed an L2 round trip per row block)
+      float4 cc[4], sc[4];
+      auto load_cs = [&](int m, float4 (&c)[4], float4 (&sn)[4]) {
+        const int t = min(m0 + wm * 128 + m * 16 + fr, M - 1) % ep.T;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          c[n] = *reinterpret_cast<const float4*>(ep.cos_ + (int64_t)t * 128 + n * 16 + fq * 4);
+          sn[n] = *reinterpret_cast<const float4*>(ep.sin_ + (int64_t)t * 128 + n * 16 + fq * 4);
+        }
+      };
+      if (rope) load_cs(0, cc, sc);
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
+        float4 cn[4], snx[4];
+        if (rope && m < 7) load_cs(m + 1, cn, snx);
         const int grow = m0 + wm * 128 + m * 16 + fr;
         const int gr = min(grow, M - 1);
         const int bi = gr / ep.T, t = gr - bi * ep.T;
@@ -621,10 +636,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
             x1[j] = bf16_round(acc[m][n][j]);
             x2[j] = bf16_round(acc[m][n + 4][j]);
           }
-          if (is_q || is_k) {
-            const float4 c = *reinterpret_cast<const float4*>(ep.cos_ + (int64_t)t * 128 + n * 16 + fq * 4);
-            const float4 sn = *reinterpret_cast<const float4*>(ep.sin_ + (int64_t)t * 128 + n * 16 + fq * 4);
-            const float cs[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+          if (rope) {
+            const float cs[4] = {cc[n].x, cc[n].y, cc[n].z, cc[n].w}, ss[4] = {sc[n].x, sc[n].y, sc[n].z, sc[n].w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float a = x1[j], b = x2[j];
@@ -646,6 +659,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
             const int col = (n + rsel) * 16 + csel * 8;
             *reinterpret_cast<uint4*>(orow + col) = vlo;
             *reinterpret_cast<uint4*>(orow + col + 64) = vhi;
+          }
+        }
+        if (rope && m < 7) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            cc[n] = cn[n];
+            sc[n] = snx[n];
           }
         }
         __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded VGPR use

@@ -144,7 +144,19 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 // gate / up projections never take a separate elementwise pass).
 // AT / BT: operand A / B stored MN-major ([K][M] / [K][N], pitches lda / ldb in bytes), read through
 // transposed LDS reads; else K-major ([M][K] / [N][K]).
-template <int FA, int FB, bool BIAS, bool RES = false, bool AT = false, bool BT = false>
+// QKV: the attention input projection's epilogue of csrc/gemm4.hip (EPI 3) on the fp8 product: the
+// [q heads | k heads | v heads] x 128 columns go straight to q [B, nh, T, 128] (C), k / v
+// [B, ng, T, 128] (qk.k, qk.v) with the rotate-half RoPE on q and k, applied to the bf16-rounded
+// dequantised projection as csrc/rope.hip does (the qkv tensor is never written).
+struct QkvArgs {
+  __hip_bfloat16* k;
+  __hip_bfloat16* v;
+  const float* cos_;
+  const float* sin_;
+  int T, nh, ng;
+};
+
+template <int FA, int FB, bool BIAS, bool RES = false, bool AT = false, bool BT = false, bool QKV = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                            __hip_bfloat16* __restrict__ C,
                                                            const __hip_bfloat16* __restrict__ bias, int M, int N,
@@ -152,7 +164,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
                                                            const float* __restrict__ sa,
                                                            const float* __restrict__ sb,
                                                            const __hip_bfloat16* __restrict__ R = nullptr,
-                                                           int ldr = 0) {
+                                                           int ldr = 0, QkvArgs qk = {}) {
+  static_assert(!QKV || (!BIAS && !RES && !AT && !BT), "qkv rope: forward layout, no other epilogue");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -255,6 +268,79 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_fp8_kernel(const char* __restri
   // through v_permlane16_swap -> 16 B of one row per lane -> (+ residual) -> store.  No LDS image.
   const float alpha = 1.f / (*sa * *sb);
   const int rsel = fg & 1, csel = fg >> 1;
+  if constexpr (QKV) {
+    // this wave's 128 columns are one head (see csrc/gemm4.hip EPI 3); a dimension d < 64 (block n < 4)
+    // and its rotate-half partner d + 64 (block n + 4) sit in the same lane and register
+    const int cb = (n0 + wn * 128) >> 7;
+    const bool is_q = cb < qk.nh, is_k = !is_q && cb < qk.nh + qk.ng;
+    __hip_bfloat16* const dst = is_q ? C : (is_k ? qk.k : qk.v);
+    const int hh = is_q ? cb : (is_k ? cb - qk.nh : cb - qk.nh - qk.ng);
+    const int nheads = is_q ? qk.nh : qk.ng;
+    const bool rope = is_q || is_k;
+    // cos / sin of row block m + 1 are loaded while block m is rotated and stored (one row block per
+    // sched region: loading them inside it exposed an L2 round trip per block, +26 us per GEMM)
+    float4 cc[4], sc[4];
+    auto load_cs = [&](int m, float4 (&c)[4], float4 (&sn)[4]) {
+      const int t = (m0 + wm * 128 + m * 16 + fr) % qk.T;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        c[n] = *reinterpret_cast<const float4*>(qk.cos_ + (int64_t)t * 128 + n * 16 + fg * 4);
+        sn[n] = *reinterpret_cast<const float4*>(qk.sin_ + (int64_t)t * 128 + n * 16 + fg * 4);
+      }
+    };
+    if (rope) load_cs(0, cc, sc);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      float4 cn[4], snx[4];
+      if (rope && m < 7) load_cs(m + 1, cn, snx);
+      const int grow = m0 + wm * 128 + m * 16 + fr;  // M % 256 == 0: every row is in range
+      const int bi = grow / qk.T, t = grow - bi * qk.T;
+      __hip_bfloat16* const orow = dst + (((int64_t)bi * nheads + hh) * qk.T + t) * 128;
+      uint32_t lo[4][2], hi[4][2];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float x1[4], x2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x1[j] = __bfloat162float(__float2bfloat16(acc[m][n][j] * alpha));
+          x2[j] = __bfloat162float(__float2bfloat16(acc[m][n + 4][j] * alpha));
+        }
+        if (rope) {
+          const float cs[4] = {cc[n].x, cc[n].y, cc[n].z, cc[n].w}, ss[4] = {sc[n].x, sc[n].y, sc[n].z, sc[n].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float a = x1[j], b = x2[j];
+            x1[j] = a * cs[j] - b * ss[j];
+            x2[j] = b * cs[j] + a * ss[j];
+          }
+        }
+        lo[n][0] = pack_bf16x2(x1[0], x1[1]);
+        lo[n][1] = pack_bf16x2(x1[2], x1[3]);
+        hi[n][0] = pack_bf16x2(x2[0], x2[1]);
+        hi[n][1] = pack_bf16x2(x2[2], x2[3]);
+      }
+#pragma unroll
+      for (int np = 0; np < 2; ++np) {
+        const int n = 2 * np;
+        const auto a0 = __builtin_amdgcn_permlane16_swap(lo[n][0], lo[n + 1][0], false, false);
+        const auto a1 = __builtin_amdgcn_permlane16_swap(lo[n][1], lo[n + 1][1], false, false);
+        const auto b0 = __builtin_amdgcn_permlane16_swap(hi[n][0], hi[n + 1][0], false, false);
+        const auto b1 = __builtin_amdgcn_permlane16_swap(hi[n][1], hi[n + 1][1], false, false);
+        const int col = (n + rsel) * 16 + csel * 8;
+        *reinterpret_cast<uint4*>(orow + col) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
+        *reinterpret_cast<uint4*>(orow + col + 64) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
+      }
+      if (rope && m < 7) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          cc[n] = cn[n];
+          sc[n] = snx[n];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded VGPR use
+    }
+    return;
+  }
   float bv[8][4];
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
@@ -352,6 +438,28 @@ LTA_EXPORT int lta_gemm4_fp8_layout(const void* A, const void* B, void* C, const
     if (fmt_a == 0) LTA_G8L(0, false, false); else LTA_G8L(1, false, false);
   }
 #undef LTA_G8L
+  return (int)hipGetLastError();
+}
+
+// q, k, v = rope split of (A . B^T) / (sa sb) for a [q heads | k heads | v heads] x 128 projection
+// (the fp8 counterpart of lta_gemm4_qkv_rope): A [M, K] fp8 rows of M = B_ * T tokens, B [N, K] with
+// N = (nh + 2 ng) * 128; cos / sin [T][128] fp32 with equal halves (rotate-half caches).
+LTA_EXPORT int lta_gemm4_fp8_qkv_rope(const void* A, const void* B, const void* sa, const void* sb, const float* cos_,
+                                      const float* sin_, void* q, void* k, void* v, int M, int K, int lda, int ldb,
+                                      int T, int nh, int ng, int fmt_a, int fmt_b, hipStream_t stream) {
+  const int N = (nh + 2 * ng) * 128;
+  if (M % BM || N % BN || K % (2 * BKB) || M <= 0 || T <= 0 || M % T || nh <= 0 || ng <= 0 || lda % 16 || ldb % 16)
+    return -2;
+  if ((int64_t)M * lda >= (1ll << 31) || (int64_t)N * ldb >= (1ll << 31) || !q || !k || !v || !cos_ || !sin_) return -2;
+  dim3 grid((M / BM) * (N / BN)), block(NTHR);
+  const QkvArgs qa{(__hip_bfloat16*)k, (__hip_bfloat16*)v, cos_, sin_, T, nh, ng};
+#define LTA_G8Q(FA, FB)                                                                                             \
+  hipLaunchKernelGGL((gemm4_fp8_kernel<FA, FB, false, false, false, false, true>), grid, block, 0, stream,         \
+                     (const char*)A, (const char*)B, (__hip_bfloat16*)q, nullptr, M, N, K, lda, ldb, 0,             \
+                     (const float*)sa, (const float*)sb, nullptr, 0, qa)
+  if (fmt_a == 0 && fmt_b == 0) LTA_G8Q(0, 0);
+  else return -1;
+#undef LTA_G8Q
   return (int)hipGetLastError();
 }
 

@@ -100,6 +100,43 @@ def gemm_nt_fp8(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Te
     return out
 
 
+register_signature("lta_gemm4_fp8_qkv_rope", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                              c_int, c_int, c_void_p])
+
+
+def gemm_qkv_rope(qa: torch.Tensor, qb: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, out_shape, cos: torch.Tensor,
+                  sin: torch.Tensor, n_head: int, n_query_groups: int, head_size: int, rope_n: int):
+    """``q, k, v = qkv_split_rope(gemm(qa, qb) / (sa sb))`` for the e4m3 attention input projection:
+    the RoPE split runs in the fp8 GEMM's epilogue (csrc/gemm4_fp8.hip QKV) when supported, else
+    the GEMM then csrc/rope.hip.  ``out_shape`` = (B, T, N) of the unfused projection."""
+    import os
+
+    from .gemm import _rope_halves_equal
+    from .fused import qkv_rope_fwd
+
+    B, T, N = out_shape
+    M, K = qa.shape
+    ok = (os.environ.get("LTA_FUSED_QKV_ROPE", "1") != "0" and head_size == 128 and rope_n == 128
+          and N == (n_head + 2 * n_query_groups) * 128 and tuple(qb.shape) == (N, K) and M == B * T
+          and gemm4_fp8_supported(qa, qb) and cos.dtype == torch.float32 and sin.dtype == torch.float32
+          and cos.dim() == 2 and sin.dim() == 2 and cos.shape[-1] == 128 and sin.shape[-1] == 128
+          and cos.shape[0] >= T and sin.shape[0] >= T)
+    if ok and _rope_halves_equal(cos, sin, T):
+        c = cos[:T].contiguous()
+        s_ = sin[:T].contiguous()
+        q = torch.empty((B, n_head, T, 128), dtype=torch.bfloat16, device=qa.device)
+        k = torch.empty((B, n_query_groups, T, 128), dtype=torch.bfloat16, device=qa.device)
+        v = torch.empty_like(k)
+        check(require().lta_gemm4_fp8_qkv_rope(qa.data_ptr(), qb.data_ptr(), sa.data_ptr(), sb.data_ptr(), c.data_ptr(),
+                                               s_.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), M, K,
+                                               qa.stride(0), qb.stride(0), T, n_head, n_query_groups, 0, 0,
+                                               stream_ptr(qa.device)), "lta_gemm4_fp8_qkv_rope")
+        return q, k, v
+    return qkv_rope_fwd(gemm(qa, qb, sa, sb, 0, 0, None, out_shape), cos, sin, n_head, n_query_groups, head_size,
+                        rope_n)
+
+
 register_signature("lta_gemm_grouped_nt_fp8", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                                 c_int64, c_void_p, c_void_p, c_void_p])
 
@@ -246,6 +283,10 @@ class _DelayedState:
             z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=device)  # noqa: E731
             self.hist, self.cur, self.hmax = z(self.recipe.amax_history_len, self.n), z(self.n), z(self.n)
             self.step_amax = z(self.n)
+            # max |w| of each slot's fp8 weight shadow (written when the shadow is (re)cast), folded into the
+            # step's amaxes by delayed_update: a forward that reads a shadow launches no cast to record it
+            self.shadow_amax = z(self.n)
+            self.has_shadow = False
 
     def group(self):
         import torch.distributed as tdist
@@ -280,6 +321,8 @@ def delayed_update(key: int) -> None:
     st = _DELAYED[key]
     if st.hist is None:
         return
+    if st.has_shadow:
+        torch.maximum(st.cur, st.shadow_amax, out=st.cur)
     g = st.group()
     if g is not None and torch.distributed.get_world_size(g) > 1:
         torch.distributed.all_reduce(st.cur, op=torch.distributed.ReduceOp.MAX, group=g)
@@ -352,11 +395,94 @@ def delayed_scaling_source(t2: torch.Tensor, e5m2: bool, key: int, slot: int):
 
 
 def quantize_delayed_rows(t: torch.Tensor, e5m2: bool, key: int, slot: int):
-    """As :func:`quantize_delayed` without the transposed copy: (q [R, C], scale)."""
+    """As :func:`quantize_delayed` without the transposed copy: (q [R, C], scale).
+
+    A parameter's e4m3 copy is kept as a *weight shadow* that the fused AdamW rewrites while it
+    updates the weight (``optim.AdamW``, ``csrc/adamw.hip``): the next forward reads the shadow
+    instead of launching a cast of the whole weight (see :func:`weight_shadow`)."""
     t2 = t.reshape(-1, t.shape[-1])
+    sh = _shadow_lookup(t) if not e5m2 else None
+    if sh is not None and sh.key == key and sh.slot == slot:
+        st = _DELAYED[key]
+        st.ensure(t.device)
+        if st.step_seen[slot] != st.updates:
+            st.step_seen[slot] = st.updates
+            st.step_src[slot] = st.hmax[slot]
+        SHADOW_STATS["reused"] += 1
+        return sh.q, sh.scale
     amax_in, fmax, scale, sink = delayed_scaling_source(t2, e5m2, key, slot)
     q = cast(t2, amax_in, fmax, scale, e5m2=e5m2, amax_out=sink)
+    if not e5m2 and _shadow_candidate(t):
+        # a weight's slot is its own (FP8LinearTransform: one slot per linear operand), so the step's
+        # amax of the slot so far is max |w|
+        st = _DELAYED[key]
+        st.shadow_amax[slot].copy_(sink)
+        st.has_shadow = True
+        _SHADOWS[t.data_ptr()] = _WeightShadow(t, q, scale, key, slot, fmax)
+        SHADOW_STATS["registered"] += 1
     return q, scale
+
+
+# ---------------------------------------------------------------------------------------------
+# fp8 weight shadows: the e4m3 copy of a bf16 parameter, refreshed by the optimizer's update kernel
+# ---------------------------------------------------------------------------------------------
+class _WeightShadow:
+    """e4m3 copy ``q`` of parameter ``ref()`` cast with ``scale``, valid while the parameter's version
+    counter is ``version``.  The fused AdamW writes the updated weight's cast into ``q`` / ``scale``
+    (scaled from the slot's amax source of the step, max |w| folded into the slot's amax history);
+    any other in-place write to the parameter bumps its version and the next forward casts again."""
+    __slots__ = ("ref", "q", "scale", "key", "slot", "fmax", "version", "shape")
+
+    def __init__(self, t, q, scale, key, slot, fmax):
+        import weakref
+
+        self.ref = weakref.ref(t)
+        self.q, self.scale, self.key, self.slot, self.fmax = q, scale, key, slot, fmax
+        self.version = t._version
+        self.shape = tuple(t.shape)
+
+
+_SHADOWS: dict[int, _WeightShadow] = {}
+SHADOW_STATS = {"reused": 0, "registered": 0}  # forward casts skipped / shadows (re)created
+
+
+def _shadows_enabled() -> bool:
+    import os
+
+    return os.environ.get("LTA_FP8_WEIGHT_SHADOW", "1") != "0"
+
+
+def _shadow_candidate(t: torch.Tensor) -> bool:
+    return (_shadows_enabled() and t.is_cuda and t.dtype == torch.bfloat16 and t.is_leaf and t.requires_grad
+            and t.is_contiguous() and not torch.cuda.is_current_stream_capturing())
+
+
+def _shadow_lookup(t: torch.Tensor):
+    if not _SHADOWS or not _shadow_candidate(t):
+        return None
+    sh = _SHADOWS.get(t.data_ptr())
+    if sh is None or sh.ref() is not t or sh.version != t._version or sh.shape != tuple(t.shape):
+        return None
+    return sh
+
+
+def weight_shadow(p: torch.Tensor):
+    """The optimizer's view of ``p``'s shadow: (q, amax source, scale out, delayed state, slot, fmax)
+    for the update kernel to refresh (its max |w| goes to ``state.shadow_amax[slot]``, which the
+    optimizer zeroes first), or None (no shadow, or stale: the next forward re-casts)."""
+    sh = _shadow_lookup(p)
+    if sh is None:
+        return None
+    st = _DELAYED.get(sh.key)
+    if st is None or st.hist is None:
+        return None
+    src = st.step_src[sh.slot] if st.step_src[sh.slot] is not None else st.hmax[sh.slot]
+    return sh.q, src, sh.scale, st, sh.slot, sh.fmax
+
+
+def invalidate_weight_shadow(p: torch.Tensor) -> None:
+    """``p`` changed without its shadow being refreshed (e.g. an update overlapped with the backward)."""
+    _SHADOWS.pop(p.data_ptr(), None)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -14,6 +14,7 @@ stream and updates only what the backward did not.
 from __future__ import annotations
 
 import math
+import struct
 
 import torch
 
@@ -143,10 +144,14 @@ class AdamW(torch.optim.Optimizer):
         from .ops._lib import require, DTYPE_CODE, stream_ptr, check, register_signature, c_int, c_void_p, c_float
 
         lib = require()
-        register_signature("lta_adamw_ex", [c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
-                                            c_float, c_float, c_float, c_float, c_int, c_void_p])
+        register_signature("lta_adamw_ex2", [c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float,
+                                             c_float, c_float, c_float, c_float, c_float, c_int, c_int, c_void_p])
+        from .ops import fp8 as _fp8
+
         metas = []
         keep = []
+        shadow = False
+        zero: dict = {}
         for i, p in enumerate(ps):
             st = self.state[p]
             g = p.grad if grads is None else grads[i]
@@ -155,6 +160,22 @@ class AdamW(torch.optim.Optimizer):
                 g = g.to(p.dtype)
             keep.append(g)
             metas += [p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()]
+            # fp8 weight shadow (ops/fp8.py): refreshed by this launch; not beside a running backward,
+            # which may still read the old e4m3 copy (the overlapped update drops it instead)
+            sh = _fp8.weight_shadow(p) if _fp8._SHADOWS else None
+            if sh is not None and lean:
+                _fp8.invalidate_weight_shadow(p)
+                sh = None
+            if sh is not None:
+                q, src, scale, dst, slot, fmax = sh
+                shadow = True
+                zero.setdefault(id(dst), (dst, []))[1].append(slot)
+                metas += [q.data_ptr(), src.data_ptr(), scale.data_ptr(), dst.shadow_amax[slot].data_ptr(),
+                          int.from_bytes(struct.pack("<f", fmax), "little")]
+            else:
+                metas += [0, 0, 0, 0, 0]
+        for dst, slots in zero.values():  # the kernel max-folds each refreshed weight's max |w| into these
+            dst.shadow_amax.index_fill_(0, torch.tensor(slots, dtype=torch.int64).to(dev, non_blocking=True), 0.0)
         meta_t = torch.tensor(metas, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         key = (dev, tuple(p.numel() for p in ps))
         chunks = self._chunk_cache.get(key)
@@ -171,8 +192,8 @@ class AdamW(torch.optim.Optimizer):
             self._chunk_cache[key] = chunks
         bc1 = 1 - b1 ** step
         bc2_sqrt = math.sqrt(1 - b2 ** step)
-        rc = lib.lta_adamw_ex(DTYPE_CODE[pdt], DTYPE_CODE[sdt], meta_t.data_ptr(), chunks.data_ptr(), chunks.shape[0], lr,
-                              b1, b2, eps, wd, bc1, bc2_sqrt, 1.0, int(lean), stream_ptr(dev))
+        rc = lib.lta_adamw_ex2(DTYPE_CODE[pdt], DTYPE_CODE[sdt], meta_t.data_ptr(), chunks.data_ptr(), chunks.shape[0],
+                               lr, b1, b2, eps, wd, bc1, bc2_sqrt, 1.0, int(lean), int(shadow), stream_ptr(dev))
         check(rc, "lta_adamw")
         # keep the metadata (and converted gradients) alive until the kernel has consumed them
         self._last_meta = meta_t

@@ -250,3 +250,52 @@ def test_llama2_7b_shape_training_under_hipgraph():
     band = max(abs(a - b) for a, b in zip(curves["plain"], c32))
     gap = max(abs(a - b) for a, b in zip(curves["hipgraph"], c32))
     assert gap <= 2 * band + 0.05, {"fp32": c32, **curves, "band": band}
+
+
+def test_llama2_7b_shape_fp8_delayed_training_fusions():
+    """The FP8 (delayed scaling) path of BASELINE config 5 on the 7B block: the attention input
+    projection runs the fp8 GEMM with the RoPE split in its epilogue (no qkv tensor, no rope pass),
+    the fused AdamW refreshes the e4m3 weight shadows (later forwards launch no weight casts), and
+    three training steps track the bf16 compiled model's losses to fp8 accuracy."""
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.optim import AdamW
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    dev = torch.device("cuda")
+    losses = {}
+    for mode in ("fp8", "bf16"):
+        torch.manual_seed(0)
+        m = GPT.from_name("llama2-7b-shape-2l").to(device=dev, dtype=torch.bfloat16)
+        init_weights(m)
+        m.set_rope_cache(SEQ, device=dev)
+        V = m.config.padded_vocab_size
+
+        class TrainStep(torch.nn.Module):
+            def __init__(self, mm):
+                super().__init__()
+                self.m = mm
+
+            def forward(self, x, y):
+                return torch.nn.functional.cross_entropy(self.m(x).reshape(-1, V), y.reshape(-1))
+
+        tm = thunder.jit(TrainStep(m), transforms=[FP8LinearTransform("delayed")] if mode == "fp8" else [])
+        opt = AdamW(m.parameters(), lr=1e-4)
+        n0 = fp8.SHADOW_STATS["reused"]
+        out = []
+        for step in range(3):
+            g = torch.Generator(device=dev).manual_seed(step)
+            idx = torch.randint(0, V, (1, SEQ), device=dev, generator=g)
+            loss = tm(idx, torch.roll(idx, -1, 1))
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            out.append(loss.item())
+        losses[mode] = out
+        if mode == "fp8":
+            fw = str(thunder.last_traces(tm)[-1])
+            assert "hip_fp8_gemm_qkv_rope" in fw and "hip_qkv_rope(" not in fw, fw
+            # 2 layers x 5 linears (qkv, proj, fc_1, fc_2, mlp.proj) + lm head, forwards 2 and 3
+            assert fp8.SHADOW_STATS["reused"] - n0 >= 2 * 11, fp8.SHADOW_STATS
+        fp8._SHADOWS.clear()
+    for a, b in zip(losses["fp8"], losses["bf16"]):
+        assert abs(a - b) <= 0.02 * abs(b), losses

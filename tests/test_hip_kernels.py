@@ -1,4 +1,6 @@
 """Numerics of the hand-written HIP kernels vs plain PyTorch fp32 references (MI355X only)."""
+import os
+
 import pytest
 import torch
 
@@ -1376,3 +1378,131 @@ def test_gemm4_splitk(M, N, K, layout):
         outb = matmul4(a, b, bias=bias)
         refb = a.float() @ b.float() + bias.float()
         assert ((outb.float() - refb).norm() / refb.norm()).item() < 5e-3
+
+
+@pytest.mark.gpu
+def test_adamw_fp8_weight_shadow_kernel():
+    """The fused AdamW refreshes a parameter's fp8 weight shadow in the same pass: the e4m3 copy is
+    bitwise the cast of the updated weight (scaled from the slot's amax source of the step), the
+    scale and max |w| are published, the weight update itself is bitwise unchanged, the next forward
+    reads the shadow without a cast, and an in-place write outside the optimizer invalidates it."""
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.optim import AdamW
+
+    torch.manual_seed(0)
+    key = fp8.new_delayed_state(fp8.DelayedScaling(amax_history_len=4), 3)
+    try:
+        shapes = [(256, 512), (3, 9000), (48, 4096)]  # one chunk; a chunk tail; several chunks
+        ps = [torch.randn(s, device="cuda", dtype=torch.bfloat16, requires_grad=True) for s in shapes]
+        twins = [p.detach().clone().requires_grad_(True) for p in ps]
+        for i, p in enumerate(ps):
+            fp8.quantize_delayed_rows(p, False, key, i)  # the forward's cast registers the shadow
+        assert all(fp8._shadow_lookup(p) is not None for p in ps)
+        st = fp8.delayed_state(key)
+        src = [st.step_src[i].clone() for i in range(3)]
+        o1 = AdamW(ps, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+        o2 = AdamW(twins, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+        for p, t in zip(ps, twins):
+            g = torch.randn_like(p)
+            p.grad, t.grad = g, g.clone()
+        o1.step()
+        o2.step()
+        torch.cuda.synchronize()
+        for i, (p, t) in enumerate(zip(ps, twins)):
+            assert torch.equal(p, t)  # the shadow output changes nothing of the update
+            sh = fp8._SHADOWS[p.data_ptr()]
+            want_scale = torch.empty((), dtype=torch.float32, device="cuda")
+            want = fp8.cast(p.detach().reshape(-1, p.shape[-1]), src[i], fp8.E4M3_MAX, want_scale)
+            assert torch.equal(sh.q, want), i
+            torch.testing.assert_close(sh.scale, want_scale, rtol=0, atol=0)  # the cast kernel's own scale
+            torch.testing.assert_close(st.shadow_amax[i], p.detach().abs().max().float(), rtol=0, atol=0)
+        # the next forward reads the shadow, and its max |w| enters the amax history
+        cur = st.cur.clone()
+        fp8.delayed_update(key)
+        torch.testing.assert_close(st.hist[0], torch.maximum(cur, st.shadow_amax), rtol=0, atol=0)
+        n0 = fp8.SHADOW_STATS["reused"]
+        q, s = fp8.quantize_delayed_rows(ps[0], False, key, 0)
+        assert q is fp8._SHADOWS[ps[0].data_ptr()].q and fp8.SHADOW_STATS["reused"] == n0 + 1
+        with torch.no_grad():
+            ps[0].mul_(0.5)  # any other write bumps the version counter: the forward casts again
+        q2, _ = fp8.quantize_delayed_rows(ps[0], False, key, 0)
+        assert q2 is not q and torch.equal(q2, fp8.cast(ps[0].detach(), st.hmax[0], fp8.E4M3_MAX))
+    finally:
+        fp8.release_delayed_state(key)
+        fp8._SHADOWS.clear()
+
+
+@pytest.mark.gpu
+def test_fp8_weight_shadow_training_matches_casting():
+    """FP8 (delayed scaling) MLP block trained with the fused AdamW: with weight shadows the forwards
+    after the first launch no weight cast, and the loss curve stays with the always-casting run (the
+    shadow is scaled one history step earlier; every value is still saturated to e4m3's range)."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.litgpt import Config, LLaMAMLP
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling
+    from lightning_thunder_amd.optim import AdamW
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    curves = {}
+    for mode in ("1", "0"):
+        os.environ["LTA_FP8_WEIGHT_SHADOW"] = mode
+        try:
+            torch.manual_seed(0)
+            m = LLaMAMLP(Config(n_embd=512, intermediate_size=1024, bias=False)).cuda().bfloat16()
+            jm = thunder.jit(m, transforms=[FP8LinearTransform(recipe=DelayedScaling(amax_history_len=4))])
+            opt = AdamW(m.parameters(), lr=1e-3)
+            n0 = fp8.SHADOW_STATS["reused"]
+            losses = []
+            for step in range(5):
+                x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16,
+                                generator=torch.Generator("cuda").manual_seed(step))
+                loss = (jm(x).float() ** 2).mean()
+                loss.backward()
+                opt.step()
+                opt.zero_grad()
+                losses.append(loss.item())
+            curves[mode] = losses
+            reused = fp8.SHADOW_STATS["reused"] - n0
+            assert (reused >= 12) if mode == "1" else reused == 0, reused  # 3 weights x forwards 2..5
+        finally:
+            os.environ.pop("LTA_FP8_WEIGHT_SHADOW", None)
+            fp8._SHADOWS.clear()
+    for a, b in zip(curves["1"], curves["0"]):
+        assert abs(a - b) <= 0.03 * abs(b), curves
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,nh,ng,K", [(1, 512, 4, 4, 256), (2, 256, 4, 2, 512)])
+def test_fp8_gemm_qkv_rope_matches_unfused(B, T, nh, ng, K):
+    """The fp8 attention input projection with the RoPE split in its epilogue (gemm4_fp8 QKV) equals
+    the unfused fp8 GEMM + csrc/rope.hip pass (v bitwise, q / k to RoPE rounding) and the fp32
+    projection + rotate-half to fp8 accuracy."""
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.ops.fused import qkv_rope_fwd
+
+    torch.manual_seed(3)
+    D = 128
+    N = (nh + 2 * ng) * D
+    x = torch.randn(B * T, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    qx, sx = fp8.quantize_rows(x)
+    qw, sw = fp8.quantize_rows(w)
+    pos = torch.arange(T + 16, device="cuda", dtype=torch.float32)
+    inv = 1.0 / (10000 ** (torch.arange(0, D // 2, device="cuda", dtype=torch.float32) * 2 / D))
+    ang = torch.outer(pos, inv).repeat(1, 2)
+    cos, sin = ang.cos(), ang.sin()
+    q, k, v = fp8.gemm_qkv_rope(qx, qw, sx, sw, (B, T, N), cos, sin, nh, ng, D, D)
+    uq, uk, uv = qkv_rope_fwd(fp8.gemm(qx, qw, sx, sw, 0, 0, None, (B, T, N)), cos, sin, nh, ng, D, D)
+    assert q.shape == (B, nh, T, D) and k.shape == (B, ng, T, D) and v.shape == (B, ng, T, D)
+    assert torch.equal(v, uv)
+    for a, b in ((q, uq), (k, uk)):
+        assert ((a.float() - b.float()).norm() / b.float().norm()).item() < 1e-3
+    qkv = (x.float() @ w.float().t()).view(B, T, nh + 2 * ng, D).transpose(1, 2)
+
+    def rope(t):
+        x1, x2 = t[..., :D // 2], t[..., D // 2:]
+        return t * cos[:T] + torch.cat((-x2, x1), -1) * sin[:T]
+
+    for a, b in ((q, rope(qkv[:, :nh])), (k, rope(qkv[:, nh:nh + ng])), (v, qkv[:, nh + ng:])):
+        assert ((a.float() - b).norm() / b.norm()).item() < 0.08
