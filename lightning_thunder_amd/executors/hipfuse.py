@@ -129,6 +129,10 @@ class HipFusion:
         self._lock = threading.Lock()
         # + the workspace pointer (column mode) in the second type
         self._argbuf_t, self._argbuf_ws_t = arg_buffer_types(len(self.tensor_pos), len(outputs), len(self.number_pos))
+        # regions have static shapes (symbolic bound symbols are fusion barriers): the output
+        # allocations are fixed once here instead of re-deriving proxy shapes on every call
+        self._out_specs = [(tuple(int(d) for d in o.shape), o.dtype) for o in outputs]
+        self._out_empty = any(0 in shape for shape, _ in self._out_specs)
 
     def __repr__(self):
         return f"HipFusion({self.name}, {len(self.nodes)} prims)"
@@ -181,8 +185,8 @@ class HipFusion:
         dev = tensors[0].device if tensors else None
         if dev is None or dev.type != "cuda":
             return self._run_reference(args)
-        outs = [torch.empty(tuple(o.shape), dtype=o.dtype, device=dev) for o in self.outputs]
-        if any(o.numel() == 0 for o in outs) or any(t.numel() == 0 for t in tensors):
+        outs = [torch.empty(shape, dtype=dt, device=dev) for shape, dt in self._out_specs]
+        if self._out_empty or any(t.numel() == 0 for t in tensors):
             return tuple(outs)
         (fns, ks) = self._variant(tensors)
         launch(ks, fns, tensors, outs, [args[i] for i in self.number_pos], self._argbuf_t, self._argbuf_ws_t,

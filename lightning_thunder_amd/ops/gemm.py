@@ -165,7 +165,7 @@ _FWD_LIB = _os.environ.get("LTA_GEMM_FWD_LIB", "0") == "1"
 
 def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
     """(at, bt, lda, ldb) of ``a [M,K] @ b [K,N]`` for ``lta_gemm4_bf16``, or None when the operands
-    are not bf16 2-D GPU tensors with one unit-stride dim and 16-B aligned rows, or K % 128 != 0.
+    are not bf16 2-D GPU tensors with one unit-stride dim and 16-B aligned rows, or K % 64 != 0 (or K < 128).
     M and N need not divide the 256 x 256 tile (edge tiles clamp their operand rows and mask their
     stores; N % 8 == 0 for whole 16-B output chunks); M < GEMM4_MIN_M goes elsewhere (a 256-row
     tile would be mostly idle)."""
@@ -173,7 +173,7 @@ def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
         return None
     M, K = a.shape
     N = b.shape[1]
-    if b.shape[0] != K or M < GEMM4_MIN_M or N % 8 or K % 128 or N == 0 or K == 0:
+    if b.shape[0] != K or M < GEMM4_MIN_M or N % 8 or K % 64 or K < 128 or N == 0:
         return None
     la, lb = _operand_layout(a, M, K), _operand_layout(b, K, N)
     if la is None or lb is None:
@@ -413,11 +413,97 @@ def gemm4_variant(at: int, bt: int, M: int, N: int, K: int) -> int:
 _GEMM4_VARIANTS: dict = {}
 
 
+# ---------------------------------------------------------------------------------------------
+# launch plans: the dispatch decision of a GEMM call site depends only on its operands' shapes,
+# strides, dtypes, 16-B alignment and the LTA_GEMM mode, which a compiled program repeats on every
+# call; the plan caches that decision with the kernel's scalar arguments, so a repeated call costs the
+# output allocation and one native launch (the host path of launch-bound programs, benchmarks/targets.py)
+# ---------------------------------------------------------------------------------------------
+_PLANS: dict = {}
+_NO_PLAN = object()
+
+
+def _tkey(t):
+    return None if t is None else (t.shape, t.stride(), t.dtype, t.data_ptr() & 15)
+
+
+def _gemm4_plan(M: int, N: int, K: int, lda: int, ldb: int, at: int, bt: int, variant: int, act_code: int,
+                has_bias: bool, has_res: bool, ldr: int, out_shape, dev):
+    """A plain / bias / residual / activation gemm4 launch (no K split, no tail split) as a closure."""
+    fn = require().lta_gemm4_bf16
+    bf16 = torch.bfloat16
+
+    def run(a, b, bias, residual):
+        _backend_counts["gemm4"] = _backend_counts.get("gemm4", 0) + 1
+        out = torch.empty(out_shape, dtype=bf16, device=dev)
+        rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), bias.data_ptr() if has_bias else None,
+                residual.data_ptr() if has_res else None, M, N, K, lda, ldb, N, ldr, 1.0, act_code, at, bt, variant,
+                stream_ptr(dev))
+        if rc != 0:
+            check(rc, "lta_gemm4_bf16")
+        return out
+
+    return run
+
+
+def _gemm4_plain_plan(M, N, K, at, bt, lda, ldb, variant, bias, residual, act, out_shape, dev):
+    """The plan of a gemm4 product, or None when this call takes a K split / tail split (workspace per call)."""
+    plain = bias is None and residual is None and act is None and variant == 1
+    splittable = residual is None and act is None and variant == 1 and (
+        bias is None or (not at and not bt and bias.data_ptr() % 16 == 0))
+    if splittable and splitk_factor(M, N, K, _device_cus(dev)):
+        return None
+    if plain and _TAIL_SPLIT and K % 256 == 0:
+        cus = _device_cus(dev)
+        nwg = -(-M // 256) * -(-N // 256)
+        tail = nwg % cus
+        if not (nwg <= cus or tail == 0 or 2 * tail > cus):
+            return None
+    return _gemm4_plan(M, N, K, lda, ldb, at, bt, variant, ACT[act], bias is not None, residual is not None,
+                       0 if residual is None else residual.stride(0), out_shape, dev)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` on the hand-written kernels, chosen by a static rule:
     the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip, any M >= 64,
-    N % 8, K % 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
-    else torch (``LTA_GEMM=torch`` forces torch)."""
+    N % 8, K % 64 with K >= 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
+    else torch (``LTA_GEMM=torch`` forces torch).  Repeated call sites run a cached launch plan."""
+    key = ("lin", _tkey(x), _tkey(w), _tkey(bias), _tkey(residual), act, x.get_device(),
+           _os.environ.get("LTA_GEMM", "auto"))
+    plan = _PLANS.get(key)
+    if plan is not None and plan is not _NO_PLAN and x.is_cuda:
+        return plan(x, w, bias, residual)
+    out = _linear_dispatch(x, w, bias, residual, act)
+    if plan is None and x.is_cuda and not torch.cuda.is_current_stream_capturing():
+        _PLANS[key] = _linear_plan(x, w, bias, residual, act) or _NO_PLAN
+    return out
+
+
+def _linear_plan(x, w, bias, residual, act):
+    """The cached form of :func:`_linear_dispatch` for this call's operands (gemm4 launches only)."""
+    if _os.environ.get("LTA_GEMM", "auto") == "torch":
+        return None
+    K = x.shape[-1]
+    N = w.shape[0]
+    x2 = x.reshape(-1, K)
+    r2 = None if residual is None else residual.reshape(-1, N)
+    if gemv_supported(x2, w, bias, r2):
+        return None
+    if _FWD_LIB and act is None and bias is None and x2.shape[0] >= 1024 and x2.dtype == torch.bfloat16:
+        return None
+    wt = w.t()
+    lay = gemm4_layout(x2, wt)
+    if lay is None or not nt_epilogue_ok(x2, w, bias, r2):
+        return None
+    at, bt, lda, ldb = lay
+    M = x2.shape[0]
+    if x2.data_ptr() != x.data_ptr() or (r2 is not None and r2.data_ptr() != residual.data_ptr()):
+        return None  # a reshape that copied: the plan launches on the caller's tensors
+    return _gemm4_plain_plan(M, N, K, at, bt, lda, ldb, gemm4_variant(0, 0, M, N, K), bias, r2, act,
+                             tuple(x.shape[:-1]) + (N,), x.device)
+
+
+def _linear_dispatch(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     K = x.shape[-1]
     N = w.shape[0]
     x2 = x.reshape(-1, K)
@@ -508,12 +594,45 @@ def _torch_mm(a, b, residual=None):
 def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
     """``a @ b (+ residual)`` for the prim matmul (leading dims of ``a`` flattened) — the backward's
     dgrad / wgrad read their transposed operands in place.  Static rule as :func:`linear`: the
-    4-wave kernel, else the 8-wave kernel, else torch."""
+    4-wave kernel, else the 8-wave kernel, else torch.  Repeated call sites run a cached launch plan."""
+    key = ("mm", _tkey(a), _tkey(b), _tkey(residual), a.get_device(), _os.environ.get("LTA_GEMM", "auto"))
+    plan = _PLANS.get(key)
+    if plan is not None and plan is not _NO_PLAN and a.is_cuda:
+        return plan(a, b, None, residual)
+    out = _matmul_dispatch(a, b, residual)
+    if plan is None and a.is_cuda and not torch.cuda.is_current_stream_capturing():
+        _PLANS[key] = _matmul_plan(a, b, residual) or _NO_PLAN
+    return out
+
+
+def _matmul_plan(a, b, residual):
+    if _os.environ.get("LTA_GEMM", "auto") == "torch" or b.dim() != 2 or a.dim() < 2:
+        return None
+    a2 = a.reshape(-1, a.shape[-1]) if a.dim() > 2 else a
+    if a2.data_ptr() != a.data_ptr():
+        return None
+    N = b.shape[1]
+    r2 = None if residual is None else residual.reshape(-1, N)
+    if r2 is not None and r2.data_ptr() != residual.data_ptr():
+        return None
+    if r2 is not None and not (r2.dtype == torch.bfloat16 and r2.stride(1) == 1 and r2.stride(0) % 8 == 0
+                               and r2.data_ptr() % 16 == 0):
+        return None
+    lay = gemm4_layout(a2, b)
+    if lay is None:
+        return None
+    at, bt, lda, ldb = lay
+    M, K = a2.shape
+    return _gemm4_plain_plan(M, N, K, at, bt, lda, ldb, gemm4_variant(at, bt, M, N, K), None, r2, None,
+                             tuple(a.shape[:-1]) + (N,), a.device)
+
+
+def _matmul_dispatch(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
     if a.dim() > 2 and b.dim() == 2:
         lead = a.shape[:-1]
         a2 = a.reshape(-1, a.shape[-1])
         r2 = None if residual is None else residual.reshape(-1, b.shape[1])
-        return matmul(a2, b, r2).reshape(*lead, b.shape[1])
+        return _matmul_dispatch(a2, b, r2).reshape(*lead, b.shape[1])
     mode = _os.environ.get("LTA_GEMM", "auto")
     res_ok = residual is None or (residual.dtype == torch.bfloat16 and residual.stride(1) == 1
                                   and residual.stride(0) % 8 == 0 and residual.data_ptr() % 16 == 0)
@@ -712,7 +831,7 @@ def matmul_swiglu_bwd(dy: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: tor
     dy2 = dy.reshape(-1, dy.shape[-1])
     a2, b2 = a.reshape(-1, N), b.reshape(-1, N)
     lay = gemm4_layout(dy2, w) if _os.environ.get("LTA_GEMM", "auto") != "torch" else None
-    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _fused_swiglu_on() and N % 256 == 0
+    if (lay is not None and lay[0] == 0 and lay[1] == 1 and _fused_swiglu_on() and N % 256 == 0 and dy2.shape[1] % 128 == 0
             and a2.is_contiguous() and b2.is_contiguous() and a2.data_ptr() % 16 == 0 and b2.data_ptr() % 16 == 0
             and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.shape[0] == dy2.shape[0]):
         M, K = dy2.shape

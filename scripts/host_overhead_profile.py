@@ -23,9 +23,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--fwd-only", action="store_true", help="profile forward calls only")
     args = ap.parse_args()
     torch.manual_seed(0)
-    m = NanoGPT.from_name("gpt2").to(device="cuda", dtype=torch.bfloat16)
+    m = NanoGPT.from_name(args.model).to(device="cuda", dtype=torch.bfloat16)
     x = torch.randint(0, 255, (16, m.config.seq_len), device="cuda")
     y = torch.randint(0, 255, (16, m.config.seq_len), device="cuda")
     jm = thunder.jit(m)
@@ -45,7 +47,8 @@ def main():
     pr.enable()
     for _ in range(args.iters):
         out = jm(x, y)
-        out[1].backward()
+        if not args.fwd_only:
+            out[1].backward()
     pr.disable()
     torch.cuda.synchronize()
     s = io.StringIO()

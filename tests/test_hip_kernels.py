@@ -1005,7 +1005,8 @@ def test_flash_attention_strided_qkv_views(D, Hkv, masked):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-@pytest.mark.parametrize("shape", [(1000, 16032, 256), (300, 50304, 128), (777, 1000, 384), (4096, 264, 512)])
+@pytest.mark.parametrize("shape", [(1000, 16032, 256), (300, 50304, 128), (777, 1000, 384), (4096, 264, 512),
+                                   (777, 1000, 320), (2048, 4800, 1600)])  # odd K-tile counts (K % 128 == 64)
 @pytest.mark.parametrize("residual", [False, True])
 def test_gemm4_edge_tiles(layout, shape, residual):
     """gemm4 on shapes that do not divide its 256 x 256 tile (a T=1000 prefill, the GPT-2 LM head
@@ -1506,3 +1507,30 @@ def test_fp8_gemm_qkv_rope_matches_unfused(B, T, nh, ng, K):
 
     for a, b in ((q, rope(qkv[:, :nh])), (k, rope(qkv[:, nh:nh + ng])), (v, qkv[:, nh + ng:])):
         assert ((a.float() - b).norm() / b.norm()).item() < 0.08
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bias,act", [(False, None), (True, None), (True, "gelu_tanh")])
+def test_gemm4_linear_plan_gpt2xl_shapes(bias, act):
+    """GPT-2 XL's linears (d = 1600: K % 128 == 64, an odd K-tile count) run on gemm4 through the cached
+    launch plan: the first call dispatches and records the plan, repeated calls replay it with the same
+    result, and every call matches fp32."""
+    from lightning_thunder_amd.ops import gemm as G
+
+    torch.manual_seed(0)
+    for M, N, K in ((2048, 4800, 1600), (2048, 1600, 6400), (2048, 6400, 1600)):
+        x = torch.randn(16, M // 16, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+        bb = torch.randn(N, device="cuda", dtype=torch.bfloat16) if bias else None
+        G.last_gemm_backend_counts(reset=True)
+        outs = [G.linear(x, w, bb, act=act) for _ in range(3)]
+        counts = G.last_gemm_backend_counts(reset=True)
+        assert counts.get("gemm4", 0) == 3 and counts.get("torch", 0) == 0, counts
+        ref = x.float() @ w.float().t() + (bb.float() if bias else 0)
+        if act == "gelu_tanh":
+            ref = torch.nn.functional.gelu(ref, approximate="tanh")
+        for o in outs:
+            assert o.shape == (16, M // 16, N)
+            torch.testing.assert_close(o, outs[0], rtol=0, atol=0)
+        err = ((outs[0].float() - ref).norm() / ref.norm()).item()
+        assert err < 1e-2, (M, N, K, err)
