@@ -38,6 +38,92 @@ def next_seed_offset(numel: int) -> tuple[int, int]:
         return seed, off
 
 
+# ---------------------------------------------------------------------------------------------
+# Graph-safe RNG: inside a captured hipGraph the kernels' seed / offset arguments are baked into the
+# graph, so a replay would reuse the capture's dropout masks.  While a HipGraphRunner captures, every
+# ``get_rng_seed_offset`` returns ``GraphRngInt`` values instead of plain ints: the seed and an offset
+# RELATIVE to the region's Philox base, both carrying the region's device RNG state (int64 [seed, base]).
+# The consumers (hipfuse Philox kernels, attention dropout, the torch fallback) read seed and base from
+# that state, so the runner only rewrites the state (one small launch) before each replay, drawing
+# ``base = next_seed_offset(total)`` for the whole region: the same counter ranges, in the same order, as
+# an uncaptured run.  The backward receives the forward's GraphRngInt values and recomputes the masks from
+# the same state (requirement, as for delayed scaling: each forward's backward runs before the forward's
+# region replays again).  Reference counterpart: PyTorch's graph-safe Philox state (offset_extragraph).
+# ---------------------------------------------------------------------------------------------
+class GraphRngInt(int):
+    """An RNG seed / relative offset drawn inside a graph capture (see above)."""
+
+    def __new__(cls, value: int, state: torch.Tensor, kind: str):
+        o = int.__new__(cls, value)
+        o.state = state
+        o.kind = kind  # "seed" | "offset"
+        return o
+
+    def __repr__(self):
+        return f"GraphRngInt({int(self)}, {self.kind})"
+
+    def __reduce__(self):  # pickles / deep copies as the plain value it stands for
+        return (int, (int(self),))
+
+
+class GraphRngContext:
+    """The RNG draws of one region run under a hipGraph runner: ``state`` (int64 [2] on the device) and
+    the running total.  ``on_first_draw(state)`` (the runner's uncaptured warm-up call) writes the live
+    (seed, offset) into the state before the first consumer kernel is enqueued; the caller then
+    advances the counter by ``total`` (:func:`advance_offset`)."""
+
+    def __init__(self, state: torch.Tensor, on_first_draw=None):
+        self.state = state
+        self.total = 0
+        self.on_first_draw = on_first_draw
+
+    def draw(self, numel: int):
+        if self.total == 0 and self.on_first_draw is not None:
+            self.on_first_draw(self.state)
+        with _lock:
+            rel = self.total
+            self.total += int(numel)
+        return GraphRngInt(0, self.state, "seed"), GraphRngInt(rel, self.state, "offset")
+
+
+def peek_seed_offset() -> tuple[int, int]:
+    """(seed, offset) the next ``next_seed_offset`` call would return, without advancing."""
+    with _lock:
+        seed = torch.initial_seed() & _MASK32
+        if _state["seed"] != seed:
+            _state["seed"] = seed
+            _state["offset"] = 0
+        return seed, _state["offset"]
+
+
+def advance_offset(numel: int) -> None:
+    with _lock:
+        _state["offset"] += int(numel)
+
+
+_graph_ctx = threading.local()
+
+
+def graph_context():
+    return getattr(_graph_ctx, "ctx", None)
+
+
+def set_graph_context(ctx) -> None:
+    _graph_ctx.ctx = ctx
+
+
+def seed_offset_for(numel: int):
+    """``next_seed_offset`` outside a capture; GraphRngInt (seed, relative offset) inside one."""
+    ctx = graph_context()
+    if ctx is not None:
+        return ctx.draw(numel)
+    return next_seed_offset(numel)
+
+
+def is_graph_rng(*vals) -> bool:
+    return any(type(v) is GraphRngInt for v in vals)
+
+
 def _mulhilo(a: torch.Tensor, b: int):
     """(hi32, lo32) of a * b for a int64 tensor of uint32 values and a 32-bit constant b (exact)."""
     b_hi, b_lo = b >> 16, b & 0xFFFF
@@ -54,9 +140,18 @@ def philox_uniform_torch(shape, seed: int, offset: int, device, dtype=torch.floa
     blk = torch.arange((n + 3) // 4, device=device, dtype=torch.int64)
     c0 = blk & _MASK32
     c1 = (blk >> 32) & _MASK32
-    c2 = torch.full_like(blk, offset & _MASK32)
-    c3 = torch.full_like(blk, (offset >> 32) & _MASK32)
-    words = philox4x32(c0, c1, c2, c3, seed & _MASK32, 0)
+    if is_graph_rng(seed, offset):  # seed / base from the region's device state (graph-safe RNG)
+        st = (seed if type(seed) is GraphRngInt else offset).state
+        off = st[1] + int(offset)
+        c2 = (off & _MASK32).expand_as(blk)
+        c3 = ((off >> 32) & _MASK32).expand_as(blk)
+        k0 = st[0] & _MASK32
+    else:
+        seed, offset = int(seed), int(offset)
+        c2 = torch.full_like(blk, offset & _MASK32)
+        c3 = torch.full_like(blk, (offset >> 32) & _MASK32)
+        k0 = seed & _MASK32
+    words = philox4x32(c0, c1, c2, c3, k0, 0)
     w = torch.stack(words, dim=1).reshape(-1)[:n]
     u = (w >> 8).to(torch.float32) * (1.0 / 16777216.0)
     return u.reshape(tuple(shape)).to(dtype)

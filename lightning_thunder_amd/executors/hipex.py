@@ -66,12 +66,11 @@ def _linear_checker(a, w, bias=None):
 
 
 def _hand_gemm_shape(M: int, N: int, K: int) -> bool:
-    """A shape some hand GEMM tiles: gemm4 (any M >= 64 and N % 8 with edge tiles, K % 64 and K >= 128) or
-    the 8-wave kernel (M, N % 256, K % 64)."""
+    """A shape some hand GEMM tiles: gemm4 (any M >= 64 and N % 8 with edge tiles, K % 128) or the
+    8-wave kernel (M, N % 256, K % 64)."""
     from ..ops.gemm import GEMM4_MIN_M
 
-    return (M >= GEMM4_MIN_M and N % 8 == 0 and K % 64 == 0 and K >= 128) or (M % 256 == 0 and N % 256 == 0
-                                                                               and K % 64 == 0)
+    return (M >= GEMM4_MIN_M and N % 8 == 0 and K % 128 == 0) or (M % 256 == 0 and N % 256 == 0 and K % 64 == 0)
 
 
 def _linear_exec(a, w, bias=None):

@@ -24,6 +24,8 @@ import itertools
 import os
 import threading
 
+from ..core.rng import GraphRngInt
+
 import torch
 
 from ..core.symbolic import SymInt
@@ -156,8 +158,10 @@ class HipFusion:
         return tuple(env[o.name] for o in self.outputs)
 
     # -- native path ---------------------------------------------------------------------------
-    def _variant(self, tensors):
+    def _variant(self, tensors, rng_key=()):
         key = tuple((tuple(t.stride()), t.data_ptr() % 16 == 0) for t in tensors)
+        if rng_key:
+            key = (key, rng_key)
         v = self._variants.get(key)
         if v is not None:
             return v
@@ -168,7 +172,8 @@ class HipFusion:
             targs = {}
             for p, t in zip((self.inputs[i] for i in self.tensor_pos), tensors):
                 targs[p.name] = cg.TensorArg(tuple(t.shape), tuple(t.stride()), t.dtype, t.data_ptr() % 16 == 0)
-            ks = cg.generate(self.plan, self.inputs, self.outputs, targs)
+            rng = {self.inputs[self.number_pos[j]].name: (si, kind) for j, kind, si in rng_key} or None
+            ks = cg.generate(self.plan, self.inputs, self.outputs, targs, rng=rng)
             RTC_STATS["generated"] += 1
             v = (load_kernels(ks), ks)
             self._variants[key] = v
@@ -188,9 +193,25 @@ class HipFusion:
         outs = [torch.empty(shape, dtype=dt, device=dev) for shape, dt in self._out_specs]
         if self._out_empty or any(t.numel() == 0 for t in tensors):
             return tuple(outs)
-        (fns, ks) = self._variant(tensors)
-        launch(ks, fns, tensors, outs, [args[i] for i in self.number_pos], self._argbuf_t, self._argbuf_ws_t,
-               self.name)
+        numbers = [args[i] for i in self.number_pos]
+        rng_key, states = (), None
+        if numbers and any(type(x) is GraphRngInt for x in numbers):
+            # Philox arguments drawn inside a hipGraph capture: the kernel reads seed / base from the
+            # regions' device RNG states (one pointer per distinct state, after the numbers)
+            states, sidx, rk = [], {}, []
+            for j, x in enumerate(numbers):
+                if type(x) is GraphRngInt:
+                    si = sidx.get(id(x.state))
+                    if si is None:
+                        si = sidx[id(x.state)] = len(states)
+                        states.append(x.state)
+                    rk.append((j, x.kind, si))
+            rng_key = tuple(rk)
+        (fns, ks) = self._variant(tensors, rng_key)
+        if states:
+            launch(ks, fns, tensors, outs, numbers, name=self.name, rng_states=states)
+        else:
+            launch(ks, fns, tensors, outs, numbers, self._argbuf_t, self._argbuf_ws_t, self.name)
         return tuple(outs)
 
 
@@ -200,11 +221,14 @@ def arg_buffer_types(n_tensors: int, n_outputs: int, n_numbers: int):
 
 
 def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: list, argbuf_t=None, argbuf_ws_t=None,
-           name: str = "hipFusion") -> None:
+           name: str = "hipFusion", rng_states=None) -> None:
     """Launches a generated kernel source (and its extra kernels) with the fusion calling convention:
     one argument block of 64-bit words = input tensor pointers, output pointers (one dummy word when
-    there are none), numbers as double bits, then the workspace pointer when ``ks.ws_bytes``."""
-    if argbuf_t is None:
+    there are none), numbers as double bits, the device RNG state pointers of graph-safe Philox
+    arguments (``rng_states``), then the workspace pointer when ``ks.ws_bytes``."""
+    if rng_states:
+        argbuf_t, argbuf_ws_t = arg_buffer_types(len(tensors), len(outs), len(numbers) + len(rng_states))
+    elif argbuf_t is None:
         argbuf_t, argbuf_ws_t = arg_buffer_types(len(tensors), len(outs), len(numbers))
     dev = (tensors or outs)[0].device
     buf = argbuf_ws_t() if ks.ws_bytes else argbuf_t()
@@ -219,6 +243,9 @@ def launch(ks: cg.KernelSource, fns: list, tensors: list, outs: list, numbers: l
         k += 1
     for x in numbers:
         buf[k] = _double_bits(x)
+        k += 1
+    for st in rng_states or ():
+        buf[k] = st.data_ptr()
         k += 1
     ws = None
     from ..ops._lib import stream_ptr

@@ -904,10 +904,13 @@ def _canonical_names(body: str) -> str:
     return _VALUE_ID.sub(sub, body)
 
 
-def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix: str = "lta_fused") -> KernelSource:
+def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix: str = "lta_fused",
+             rng: dict | None = None) -> KernelSource:
     """``inputs``: region inputs (TensorProxy/NumberProxy), ``outputs``: TensorProxies,
-    ``targs``: input name -> TensorArg for the tensor inputs at this call signature."""
-    g = _Gen(plan, inputs, outputs, targs)
+    ``targs``: input name -> TensorArg for the tensor inputs at this call signature; ``rng``: number
+    input name -> (device RNG state index, "seed" | "offset") for Philox arguments drawn inside a
+    hipGraph capture (core/rng.py GraphRngInt: seed and base read from the state, offset relative)."""
+    g = _Gen(plan, inputs, outputs, targs, rng)
     body, grid, block, vec, mode = g.build()
     body = _canonical_names(body)
     from ..core.rng import PHILOX_HIP
@@ -921,8 +924,10 @@ def generate(plan: Plan, inputs: list, outputs: list, targs: dict, kernel_prefix
 
 
 class _Gen:
-    def __init__(self, plan: Plan, inputs, outputs, targs):
+    def __init__(self, plan: Plan, inputs, outputs, targs, rng=None):
         self.p = plan
+        self.rng_map = dict(rng or {})
+        self.n_rng = 1 + max((i for i, _ in self.rng_map.values()), default=-1)
         self.inputs = inputs
         self.outputs = outputs
         self.targs = targs
@@ -1038,6 +1043,8 @@ class _Gen:
         fields.append(f"void* out[{max(nout, 1)}];")
         if ns:
             fields.append(f"double s[{ns}];")
+        if self.n_rng:
+            fields.append(f"const long long* rng[{self.n_rng}];")
         if self.colred:
             fields.append("void* ws;")
             if self.counters:
@@ -1053,6 +1060,11 @@ class _Gen:
 
     def _scalar_ref(self, a, ct: str) -> str:
         if isinstance(a, Proxy) and not isinstance(a, TensorProxy):
+            if a.name in self.rng_map:  # graph-safe Philox argument: seed / base from the device state
+                ri, kind = self.rng_map[a.name]
+                if kind == "seed":
+                    return f"(({ct})A.rng[{ri}][0])"
+                return f"(({ct})(A.rng[{ri}][1] + (long long)A.s[{self.num_index[a.name]}]))"
             if a.name in self.num_index:
                 return f"(({ct})A.s[{self.num_index[a.name]}])"
             v = pyval(a)

@@ -116,9 +116,9 @@ for prim in (prims.python_return, prims.python_del, prims.comment, prims.unpack_
 
 
 def _get_rng_seed_offset(numel):
-    from ..core.rng import next_seed_offset
+    from ..core.rng import seed_offset_for
 
-    return next_seed_offset(int(numel))
+    return seed_offset_for(int(numel))  # GraphRngInt values while a hipGraph region captures
 
 
 _rng_op = ex.register_operator("get_rng_seed_offset", like=prims.get_rng_seed_offset, fn=_get_rng_seed_offset)

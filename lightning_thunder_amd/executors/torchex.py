@@ -82,7 +82,7 @@ def _uniform_philox(shape, minval, maxval, *, device, dtype, seed, offset):
     # the framework's Philox (core/rng.py): bit-identical to hipfuse's inline generator
     from ..core.rng import philox_uniform_torch
 
-    u = philox_uniform_torch(tuple(shape), int(seed), int(offset), device)
+    u = philox_uniform_torch(tuple(shape), seed, offset, device)  # GraphRngInt kept: graph-safe seed / base
     if minval != 0.0 or maxval != 1.0:
         u = u * (maxval - minval) + minval
     return u.to(dtype)

@@ -136,6 +136,21 @@ def _rows_ok(t) -> bool:
     return t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:-1]) and t.data_ptr() % 16 == 0
 
 
+register_signature("lta_attn_set_rng_state", [c_void_p])
+
+
+def _graph_rng(lib, dropout_p, seed, offset):
+    """Dropout seeds drawn inside a hipGraph capture (core/rng.py GraphRngInt): hand the kernel the
+    region's device RNG state; the offset stays relative to its base."""
+    from ..core.rng import GraphRngInt
+
+    if dropout_p > 0 and (type(seed) is GraphRngInt or type(offset) is GraphRngInt):
+        st = (seed if type(seed) is GraphRngInt else offset).state
+        lib.lta_attn_set_rng_state(st.data_ptr())
+        return 0, int(offset)
+    return seed, offset
+
+
 def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str = "bshd", mask=None,
              dropout_p: float = 0.0, seed: int = 0, offset: int = 0):
     """q [B, Hq, T, D], k/v [B, Hkv, S, D] -> (o [B, Hq, T, D], lse [B, Hq, T] fp32).
@@ -161,6 +176,7 @@ def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str 
         o = torch.empty((B, Hq, T, D), device=q.device, dtype=q.dtype)
     lse = torch.empty((B, Hq, T), device=q.device, dtype=torch.float32)
     mimg, mb, mh = (None, 0, 0) if mask is None else prepare_mask(mask, B, Hq, T, S)
+    seed, offset = _graph_rng(lib, dropout_p, seed, offset)
     rc = lib.lta_attn_fwd_ex2(dcode(q), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, Hq, Hkv, T, S, D, float(sc),
                               int(causal), ctypes.cast(_strides3(o), c_void_p), ptr(mimg), mb, mh, float(dropout_p),
                               int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), ctypes.cast(qkv_st, c_void_p),
@@ -198,6 +214,7 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
     if mask_grad:
         assert mask is not None and mask.dtype != torch.bool
         dmask = torch.empty((B, Hq, T, S), device=q.device, dtype=torch.float32)
+    seed, offset = _graph_rng(lib, dropout_p, seed, offset)
     rc = lib.lta_attn_bwd_ex3(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
                               ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
                               mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),

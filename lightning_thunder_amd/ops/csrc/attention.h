@@ -118,7 +118,18 @@ struct AttnExtra {
   unsigned seed_lo, seed_hi, offset;
   float* part;            // GQA head split of the dK/dV pass: fp32 partial rows [hsplit][B Hkv Sk][2][128]
   int hsplit;             // > 1: query heads of a kv group split over that many workgroups (attn_bwd_dkdv_reduce sums)
+  const long long* rng;   // graph-safe dropout (core/rng.py GraphRngInt): int64 [seed, base] on the device,
+                          // `offset` then relative to base; null: seed / offset are the values above
 };
+
+// the device RNG state for the NEXT attention launch of this host thread (lta_attn_set_rng_state): the
+// entry points take it (and clear it) when they build their AttnExtra
+inline thread_local const long long* g_attn_rng = nullptr;
+inline const long long* take_attn_rng() {
+  const long long* r = g_attn_rng;
+  g_attn_rng = nullptr;
+  return r;
+}
 
 // Counter-based dropout mask: a pure function of (seed, offset, query head, query, key), so the
 // forward and both backward kernels regenerate the same keep bit in any iteration order.
@@ -131,7 +142,14 @@ __device__ __forceinline__ unsigned fmix32(unsigned h) {
   return h;
 }
 __device__ __forceinline__ unsigned rng_head(const AttnExtra& e, int bh) {
-  return fmix32((unsigned)bh * 0x9e3779b9u ^ fmix32(e.seed_lo ^ (e.offset * 0x27d4eb2fu)) ^ e.seed_hi);
+  unsigned slo = e.seed_lo, shi = e.seed_hi, off = e.offset;
+  if (e.rng != nullptr) {  // graph-safe: seed and Philox base written before each graph replay
+    const unsigned long long sd = (unsigned long long)e.rng[0];
+    slo = (unsigned)sd;
+    shi = (unsigned)(sd >> 32);
+    off = (unsigned)((unsigned long long)e.rng[1] + (unsigned long long)e.offset);
+  }
+  return fmix32((unsigned)bh * 0x9e3779b9u ^ fmix32(slo ^ (off * 0x27d4eb2fu)) ^ shi);
 }
 __device__ __forceinline__ unsigned rng_q(unsigned head, int q) { return fmix32((unsigned)q * 0x61c88647u + head); }
 __device__ __forceinline__ unsigned rng_k(int k) { return fmix32((unsigned)k * 0x7feb352du + 0x3c6ef372u); }

@@ -1776,6 +1776,7 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
                                 int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
                                 int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
                                 const int64_t* qkv_strides, const int64_t* grad_strides, hipStream_t stream) {
+  const long long* rng = take_attn_rng();
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f || (dmask && !mask)) return -2;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
@@ -1803,6 +1804,7 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
     ex.seed_lo = (unsigned)seed;
     ex.seed_hi = (unsigned)(seed >> 32);
     ex.offset = (unsigned)offset;
+    ex.rng = rng;
     exf |= kExDrop;
   }
 #define LTA_B(TT, DD)                                                                                             \

@@ -313,6 +313,7 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
                                 int Hq, int Hkv, int Tq, int Sk, int D, float scale, int causal,
                                 const int64_t* o_strides, const void* mask, int mask_b, int mask_h, float dropout_p,
                                 uint64_t seed, uint64_t offset, const int64_t* qkv_strides, hipStream_t stream) {
+  const long long* rng = take_attn_rng();
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f) return -2;
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
@@ -331,6 +332,7 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
     ex.seed_lo = (unsigned)seed;
     ex.seed_hi = (unsigned)(seed >> 32);
     ex.offset = (unsigned)offset;
+    ex.rng = rng;
     exf |= kExDrop;
   }
   if (D == 128 && exf == 0 && g_fwd_impl >= 9 && Tq > 0 && Sk > 0) {  // v4 (attention_fwd4.hip)
@@ -357,6 +359,10 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
   }
   return -1;
 }
+
+// graph-safe dropout: the device RNG state (int64 [seed, base]) the next lta_attn_fwd_ex2 / lta_attn_bwd_ex3
+// call of this thread reads (its seed / offset arguments then relative to it)
+LTA_EXPORT void lta_attn_set_rng_state(const void* state) { g_attn_rng = (const long long*)state; }
 
 LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
                                int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,

@@ -483,13 +483,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm4_bf16_kernel(const __hip_bfloat1
       LTA_FENCE();
     }
   };
-  // K-tile pairs (stage buffers 0, 1), then an odd last K-tile (K % 128 == 64: e.g. GPT-2 XL's d = 1600) in
-  // buffer 0; nk >= 2 (host)
-  for (int t = 0; t + 1 < nk; t += 2) {
+  // nk is even (K % 128 == 0, checked by the host).  An odd-K-tile tail (K % 128 == 64) as a third body
+  // instance after this loop changed hipcc's schedule of the plain instantiation into wrong results
+  // (tests/test_hip_kernels.py::test_gemm4_edge_tiles, round 6): such K take the other GEMM paths.
+  for (int t = 0; t < nk; t += 2) {
     body(t, std::integral_constant<int, 0>{});
     body(t + 1, std::integral_constant<int, 1>{});
   }
-  if (nk & 1) body(nk - 1, std::integral_constant<int, 0>{});
 
   // the last asm MFMAs' results must be complete before the epilogue reads the accumulators
 #pragma unroll
@@ -1030,12 +1030,12 @@ int dispatch_layout(const void* A, const void* B, void* C, const void* bias, con
 //   at = 0: A [M][K] (lda = row pitch)        at = 1: A stored [K][M] (lda = its row pitch)
 //   bt = 0: B [N][K] (nn.Linear weight)       bt = 1: B stored [K][N]
 // act/bias only with at = bt = 0.  Any M, N with N % 8 == 0 (edge tiles: clamped operand sources,
-// masked stores), K % 64 == 0 and K >= 128, 16-B aligned rows, operands under 2 GiB (32-bit buffer offsets).
+// masked stores), K % 128 == 0, 16-B aligned rows, operands under 2 GiB (32-bit buffer offsets).
 // variant: glds split; 1 (half of a K-tile's LDS-DMA loads in the barrier phase) is the only one built.
 LTA_EXPORT int lta_gemm4_bf16(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N,
                               int K, int lda, int ldb, int ldc, int ldr, float alpha, int act, int at, int bt,
                               int variant, hipStream_t s) {
-  if (N % 8 || K % BK || K < 2 * BK || M <= 0 || N <= 0) return -2;
+  if (N % 8 || K % (2 * BK) || M <= 0 || N <= 0 || K <= 0) return -2;
   if (at && M % 8) return -2;  // MN-major A: 16-B rows
   // buffer-resource byte offsets are 32-bit
   const int64_t ea = at ? (int64_t)K * lda : (int64_t)M * lda, eb = bt ? (int64_t)K * ldb : (int64_t)N * ldb;

@@ -460,3 +460,20 @@ LTA_EXPORT int lta_index_rows_sum(int dtype, const void* src, int64_t lds, const
 #undef LTA_IRS
   return (int)hipGetLastError();
 }
+
+// Graph-safe RNG (core/rng.py): the two int64 words [seed, Philox base] a captured region's kernels read,
+// written stream-ordered right before the graph's replay (lane 0 stores from vector registers).
+namespace {
+__global__ __launch_bounds__(64) void store_i64x2_kernel(long long* __restrict__ p, long long a, long long b) {
+  if (threadIdx.x == 0) {
+    const longlong2 v = make_longlong2(a, b);
+    *reinterpret_cast<longlong2*>(p) = v;
+  }
+}
+}  // namespace
+
+LTA_EXPORT int lta_store_i64x2(void* p, long long a, long long b, hipStream_t s) {
+  if (!p || ((uintptr_t)p & 15)) return -2;
+  hipLaunchKernelGGL(store_i64x2_kernel, dim3(1), dim3(64), 0, s, (long long*)p, a, b);
+  return (int)hipGetLastError();
+}

@@ -165,7 +165,7 @@ _FWD_LIB = _os.environ.get("LTA_GEMM_FWD_LIB", "0") == "1"
 
 def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
     """(at, bt, lda, ldb) of ``a [M,K] @ b [K,N]`` for ``lta_gemm4_bf16``, or None when the operands
-    are not bf16 2-D GPU tensors with one unit-stride dim and 16-B aligned rows, or K % 64 != 0 (or K < 128).
+    are not bf16 2-D GPU tensors with one unit-stride dim and 16-B aligned rows, or K % 128 != 0.
     M and N need not divide the 256 x 256 tile (edge tiles clamp their operand rows and mask their
     stores; N % 8 == 0 for whole 16-B output chunks); M < GEMM4_MIN_M goes elsewhere (a 256-row
     tile would be mostly idle)."""
@@ -173,7 +173,7 @@ def gemm4_layout(a: torch.Tensor, b: torch.Tensor):
         return None
     M, K = a.shape
     N = b.shape[1]
-    if b.shape[0] != K or M < GEMM4_MIN_M or N % 8 or K % 64 or K < 128 or N == 0:
+    if b.shape[0] != K or M < GEMM4_MIN_M or N % 8 or K % 128 or N == 0 or K == 0:
         return None
     la, lb = _operand_layout(a, M, K), _operand_layout(b, K, N)
     if la is None or lb is None:
@@ -466,7 +466,7 @@ def _gemm4_plain_plan(M, N, K, at, bt, lda, ldb, variant, bias, residual, act, o
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` on the hand-written kernels, chosen by a static rule:
     the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip, any M >= 64,
-    N % 8, K % 64 with K >= 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
+    N % 8, K % 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
     else torch (``LTA_GEMM=torch`` forces torch).  Repeated call sites run a cached launch plan."""
     key = ("lin", _tkey(x), _tkey(w), _tkey(bias), _tkey(residual), act, x.get_device(),
            _os.environ.get("LTA_GEMM", "auto"))

@@ -35,10 +35,14 @@ import weakref
 import torch
 
 from ..core.prims import PrimIDs
+from ..core.rng import GraphRngInt
+from ..ops._lib import register_signature, c_void_p, c_int64
 from ..core.proxies import TensorProxy, Proxy
 from ..core.symbol import Symbol, BoundSymbol
 from ..core.trace import TraceCtx, from_trace, TraceProvenance, tracectx
 from ..core.transform_common import Transform
+
+register_signature("lta_store_i64x2", [c_void_p, c_int64, c_int64, c_void_p])
 
 _NOT_CAPTURABLE_IDS = {PrimIDs.RETURN, PrimIDs.DEL, PrimIDs.COMMENT, PrimIDs.ITEM}
 
@@ -47,9 +51,17 @@ def _is_unpack(b) -> bool:
     return isinstance(b.sym.name, str) and b.sym.name.startswith("unpack")
 
 
+def _is_rng_draw(bsym: BoundSymbol) -> bool:
+    return bsym.sym.id == PrimIDs.GET_RNG_SEED_OFFSET or bsym.sym.name == "get_rng_seed_offset"
+
+
 def default_capturable(bsym: BoundSymbol, *, capture_collectives: bool = False) -> bool:
     if bsym.sym.id in _NOT_CAPTURABLE_IDS or _is_unpack(bsym) or getattr(bsym.sym, "not_capturable", False):
         return False
+    if _is_rng_draw(bsym):
+        # host numbers, but no sync: inside a capture it draws graph-safe values (core/rng.py GraphRngInt)
+        # whose Philox base the runner rewrites on the device before every replay
+        return True
     if not capture_collectives and (getattr(bsym.sym, "module", None) == "dist_prims"
                                     or (isinstance(bsym.sym.id, str) and bsym.sym.id.startswith("dist."))):
         return False
@@ -115,6 +127,10 @@ class HipGraphRunner:
         self._lock = threading.Lock()
         self.replays = 0
         self.captures = 0
+        # graph-safe RNG (core/rng.py): per captured signature, the device state [seed, base] its kernels
+        # read and the Philox counter range one replay consumes
+        self._rng: dict = {}
+        self._rng_states: dict = {}
 
     @staticmethod
     def _key(args):
@@ -122,15 +138,52 @@ class HipGraphRunner:
         for a in args:
             if isinstance(a, torch.Tensor):
                 k.append((tuple(a.shape), tuple(a.stride()), a.dtype, a.device))
+            elif type(a) is GraphRngInt:  # a region's graph-safe RNG draw: its state is part of the graph
+                k.append(("rng", int(a), a.kind, id(a.state)))
             else:
                 k.append(("py", a))
         return tuple(k)
+
+    def _rng_state(self, sig, args):
+        """The device RNG state [seed, base] of one signature (shared by its warm-up call and capture)."""
+        st = self._rng_states.get(sig)
+        if st is None:
+            dev = next((a.device for a in args if isinstance(a, torch.Tensor) and a.is_cuda), None)
+            if dev is None:
+                return None
+            st = self._rng_states[sig] = torch.zeros(2, dtype=torch.int64, device=dev)
+        return st
+
+    def _warm_call(self, sig, args):
+        """The uncaptured first call.  RNG draws already take the graph-safe form (so the kernel variants
+        the capture needs are built and loaded here, outside the capture), with the state holding the
+        live (seed, offset): the same counter ranges as a run without graphs."""
+        from ..core import rng as _rng
+
+        st = self._rng_state(sig, args)
+        if st is None:
+            return self.fn(*args)
+
+        def first_draw(state):
+            seed, base = _rng.peek_seed_offset()
+            self._store_rng(state, seed, base)
+
+        ctx = _rng.GraphRngContext(st, on_first_draw=first_draw)
+        prev = _rng.graph_context()
+        _rng.set_graph_context(ctx)
+        try:
+            out = self.fn(*args)
+        finally:
+            _rng.set_graph_context(prev)
+        if ctx.total:
+            _rng.advance_offset(ctx.total)
+        return out
 
     def __call__(self, *args):
         sig = self._key(args)
         if sig not in self._warm:
             self._warm.add(sig)
-            return self.fn(*args)
+            return self._warm_call(sig, args)
         private = False
         if self._bound:
             storage = tuple(args[i].data_ptr() for i in self._bound)
@@ -149,6 +202,9 @@ class HipGraphRunner:
         for i, (s, a) in enumerate(zip(ins, args)):
             if isinstance(a, torch.Tensor) and i not in skip and a.data_ptr() != s.data_ptr():
                 s.copy_(a)
+        rng = self._rng.get(key)
+        if rng is not None:
+            self._set_rng(*rng)
         graph.replay()
         if self._bound:
             dst = [args[i] for i in self._bound]
@@ -196,9 +252,26 @@ class HipGraphRunner:
                 return
         torch._foreach_copy_([ins[i] for i in self._bound], src)
 
+    @staticmethod
+    def _store_rng(state, seed, base):
+        from ..ops._lib import require, stream_ptr, check
+
+        check(require().lta_store_i64x2(state.data_ptr(), seed, base, stream_ptr(state.device)), "lta_store_i64x2")
+
+    def _set_rng(self, state, total):
+        """This replay's Philox counter range (drawn as an uncaptured run would draw it) into the state."""
+        from ..core.rng import next_seed_offset
+
+        seed, base = next_seed_offset(total)
+        self._store_rng(state, seed, base)
+
     def _capture(self, key, args, private: bool):
+        from ..core import rng as _rng
+
         clone = set(self._clone) | (set(self._bound) if private else set())
         ins = tuple(a.clone() if i in clone and isinstance(a, torch.Tensor) else a for i, a in enumerate(args))
+        st = self._rng_state(key[0], args)
+        ctx = _rng.GraphRngContext(st) if st is not None else None
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         # TunableOp's GEMM path creates a BLAS handle per stream on first use, which a capture
@@ -207,12 +280,17 @@ class HipGraphRunner:
         tuned = tun is not None and tun.is_enabled()
         if tuned:
             tun.enable(False)
+        prev = _rng.graph_context()
+        _rng.set_graph_context(ctx)
         try:
             with torch.cuda.graph(g, pool=self.owner.pool()):
                 outs = self.fn(*ins)
         finally:
+            _rng.set_graph_context(prev)
             if tuned:
                 tun.enable(True)
+        if ctx is not None and ctx.total:
+            self._rng[key] = (ctx.state, ctx.total)
         return self._store(key, ins, g, outs)
 
     def _store(self, key, ins, graph, outs):

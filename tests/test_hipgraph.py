@@ -291,3 +291,118 @@ def test_donated_outputs_are_adopted_and_guarded_cpu():
         r(x)  # b is alive: the replay would overwrite it
     del b
     torch.testing.assert_close(r(x)[0], x * 2)
+
+
+def test_graph_rng_draws_and_torch_philox_cpu():
+    """Graph-safe RNG (core/rng.py): inside a runner's context the draws are GraphRngInt seeds / offsets
+    relative to the region's base; the torch Philox reads seed and base from the device state and gives
+    exactly the uncaptured values; a warm-up context draws the same counter ranges as plain draws."""
+    from lightning_thunder_amd.core import rng
+
+    rng._state["seed"] = None
+    torch.manual_seed(7)
+    plain = [rng.next_seed_offset(n) for n in (100, 40, 12)]
+    rng._state["seed"] = None
+    state = torch.zeros(2, dtype=torch.int64)
+    written = []
+
+    def first_draw(st):
+        seed, base = rng.peek_seed_offset()
+        st[0], st[1] = seed, base
+        written.append((seed, base))
+
+    ctx = rng.GraphRngContext(state, on_first_draw=first_draw)
+    rng.set_graph_context(ctx)
+    try:
+        draws = [rng.seed_offset_for(n) for n in (100, 40, 12)]
+    finally:
+        rng.set_graph_context(None)
+    rng.advance_offset(ctx.total)
+    assert rng.peek_seed_offset()[1] == plain[-1][1] + 12  # the counter ends where plain draws end
+    assert len(written) == 1 and ctx.total == 152
+    for (s_ref, o_ref), (s, o) in zip(plain, draws):
+        assert type(s) is rng.GraphRngInt and type(o) is rng.GraphRngInt and o.state is state
+        assert int(state[1]) + int(o) == o_ref and int(state[0]) == s_ref
+        got = rng.philox_uniform_torch((5, 7), s, o, "cpu")
+        want = rng.philox_uniform_torch((5, 7), s_ref, o_ref, "cpu")
+        assert torch.equal(got, want)
+    # runner keys tell graph draws of different regions apart
+    other = torch.zeros(2, dtype=torch.int64)
+    k1 = HipGraphRunner._key((rng.GraphRngInt(0, state, "offset"),))
+    k2 = HipGraphRunner._key((rng.GraphRngInt(0, other, "offset"),))
+    assert k1 != k2
+
+
+def test_graph_rng_codegen_reads_device_state_cpu():
+    """A hipfuse region whose Philox seed / offset are graph draws reads them from the state pointers
+    appended after the numbers (seed and base from the state, offset relative)."""
+    from lightning_thunder_amd.executors import hipfuse
+    from lightning_thunder_amd.executors import hipfuse_codegen as cg
+    from lightning_thunder_amd.core.proxies import TensorProxy
+
+    old = hipfuse.ex.allow_cpu
+    hipfuse.ex.allow_cpu = True
+    try:
+        def f(x):
+            return torch.nn.functional.dropout(x * 2.0, p=0.3, training=True)
+
+        jf = thunder.jit(f, executors=["hipfuse", "torch"])
+        jf(torch.randn(64, 128, requires_grad=True))
+        fus = [fb for fb in hipfuse.fusions(thunder.last_traces(jf)[-1])
+               if "uniform_philox" in str(fb.subsymbols)]
+        assert fus
+        h = fus[0]._call_ctx[fus[0].sym.name]
+        nums = [h.inputs[i] for i in h.number_pos]
+        assert len(nums) >= 2
+        targs = {p.name: cg.TensorArg(tuple(p.shape), tuple(torch.empty(tuple(p.shape)).stride()), p.dtype, True)
+                 for p in h.inputs if isinstance(p, TensorProxy)}
+        plain = cg.generate(h.plan, h.inputs, h.outputs, targs)
+        rngmap = {nums[0].name: (0, "seed"), nums[1].name: (0, "offset")}
+        g = cg.generate(h.plan, h.inputs, h.outputs, targs, rng=rngmap)
+        assert "A.rng[" not in plain.src and "const long long* rng[1];" in g.src
+        assert "A.rng[0][0]" in g.src and "A.rng[0][1]" in g.src
+        hipfuse.compile_source(g)  # hiprtc compiles it (no GPU needed)
+    finally:
+        hipfuse.ex.allow_cpu = old
+
+
+@pytest.mark.gpu
+def test_hipgraph_dropout_training_matches_uncaptured_gpu():
+    """A dropout model (NanoGPT blocks, dropout 0.1: hipfuse Philox regions and attention dropout) under
+    HipGraphTransform: the RNG draws no longer split the trace into per-dropout regions, replays draw
+    fresh masks, and every step's loss and gradients equal the uncaptured compiled run's (same counter
+    ranges in the same order)."""
+    from lightning_thunder_amd.core import rng
+    from lightning_thunder_amd.models.nanogpt import NanoGPT, NanoGPTConfig
+
+    cfg = NanoGPTConfig(n_layer=2, n_head=4, n_embd=256, seq_len=128, block_size=128, vocab_size=512, dropout=0.1)
+
+    def run(graphs):
+        torch.manual_seed(0)
+        m = NanoGPT(cfg).to(device="cuda", dtype=torch.bfloat16)
+        t = HipGraphTransform()
+        jm = thunder.jit(m, transforms=[t] if graphs else [])
+        rng._state["seed"] = None
+        torch.manual_seed(11)
+        out = []
+        for step in range(5):
+            g = torch.Generator(device="cuda").manual_seed(step)
+            x = torch.randint(0, 512, (4, 128), device="cuda", generator=g)
+            y = torch.randint(0, 512, (4, 128), device="cuda", generator=g)
+            _, loss = jm(x, y)
+            loss.backward()
+            out.append((loss.detach().clone(), [p.grad.clone() for p in m.parameters()]))
+            for p in m.parameters():
+                p.grad = None
+        return out, t, jm
+
+    ref, _, _ = run(False)
+    got, t, jm = run(True)
+    for (lr, gr), (lg, gg) in zip(ref, got):
+        torch.testing.assert_close(lg, lr, rtol=0, atol=0)
+        for a, b in zip(gg, gr):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+    fw = thunder.last_traces(jm)[-1]
+    assert sum(b.sym.name.startswith("HipGraph") for b in fw.bound_symbols) <= 2, \
+        [b.sym.name for b in fw.bound_symbols]
+    assert sum(r.replays for r in t.runners) >= 3 and any(r._rng for r in t.runners)
