@@ -115,7 +115,8 @@ def run_one(bench: Bench, executor: str, iters: int, warmup: int, device="cuda")
     elif executor == "thunder+hipgraph":
         from ..transforms.hipgraph import HipGraphTransform
 
-        fn = thunder.jit(fn, transforms=[HipGraphTransform()])
+        # gradients donated to autograd (the timed backward drops p.grad after every call)
+        fn = thunder.jit(fn, transforms=[HipGraphTransform(donate_grads=True)])
     elif executor != "eager":
         raise ValueError(executor)
     params = [p for p in (fn.parameters() if hasattr(fn, "parameters") else [])]
