@@ -269,14 +269,45 @@ _COUNTERS: dict = {}
 _CNT_BUF_T: dict = {}
 
 
+class CaptureCounters:
+    """Arrival counters of the column-mode launches captured into one hipGraph: consecutive slices of
+    buffers of the graph's own, each zero-filled once by one graph node (every launch leaves its counters
+    at zero again, so replays need no re-zeroing) instead of one zero-fill node per launch."""
+
+    CHUNK = 1 << 16
+
+    def __init__(self):
+        self.buf = None
+        self.used = 0
+
+    def take(self, n: int, dev) -> torch.Tensor:
+        n = max(n, 1)
+        if self.buf is None or self.buf.device != dev or self.used + n > self.buf.numel():
+            self.buf = torch.zeros(max(n, self.CHUNK), dtype=torch.int32, device=dev)
+            self.used = 0
+        out = self.buf[self.used:self.used + n]
+        self.used += (n + 63) // 64 * 64
+        return out
+
+
+_capture_ctx = threading.local()
+
+
+def set_capture_counters(c) -> None:
+    """Installed by HipGraphRunner around a capture (None afterwards)."""
+    _capture_ctx.counters = c
+
+
 def _counters(n: int, dev) -> torch.Tensor:
     """Zeroed uint32 arrival counters of the column-mode kernels: one persistent buffer per (device,
     stream), grown on demand.  Every launch leaves its counters at zero again (the last workgroup of
     each column group resets its own), so kernels ordered on one stream can share it.  Inside a graph
-    capture every launch gets a zero-filled buffer of the graph's own."""
+    capture the counters are the graph's own (nothing the graph holds can be shared with or replaced by
+    eager launches): slices of the runner's CaptureCounters, else a zero-filled buffer per launch."""
     if torch.cuda.is_current_stream_capturing():
-        # a buffer of the graph's own (its zero-fill is a node of the graph, replayed before the kernel):
-        # nothing the graph holds can be shared with or replaced by eager launches
+        cc = getattr(_capture_ctx, "counters", None)
+        if cc is not None:
+            return cc.take(n, dev)
         return torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     buf = _COUNTERS.get(key)

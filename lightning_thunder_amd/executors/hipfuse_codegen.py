@@ -1063,8 +1063,8 @@ class _Gen:
             if a.name in self.rng_map:  # graph-safe Philox argument: seed / base from the device state
                 ri, kind = self.rng_map[a.name]
                 if kind == "seed":
-                    return f"(({ct})A.rng[{ri}][0])"
-                return f"(({ct})(A.rng[{ri}][1] + (long long)A.s[{self.num_index[a.name]}]))"
+                    return f"(({ct})rng_seed{ri})"
+                return f"(({ct})(rng_base{ri} + (long long)A.s[{self.num_index[a.name]}]))"
             if a.name in self.num_index:
                 return f"(({ct})A.s[{self.num_index[a.name]}])"
             v = pyval(a)
@@ -2228,4 +2228,7 @@ class _Gen:
     def _wrap(self, body, block):
         head = [self._decl_args(), *self.typedefs.values(),
                 f'extern "C" __global__ void __launch_bounds__({block}) __KERNEL_NAME__(Args A) {{']
+        # graph-safe Philox state: read once per thread (the outputs' stores could alias it for the compiler)
+        for ri in range(self.n_rng):
+            head.append(f"  const long long rng_seed{ri} = A.rng[{ri}][0], rng_base{ri} = A.rng[{ri}][1];")
         return "\n".join(head + body + ["}"]) + "\n"

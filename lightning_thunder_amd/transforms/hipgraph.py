@@ -280,13 +280,17 @@ class HipGraphRunner:
         tuned = tun is not None and tun.is_enabled()
         if tuned:
             tun.enable(False)
+        from ..executors import hipfuse as _hf
+
         prev = _rng.graph_context()
         _rng.set_graph_context(ctx)
+        _hf.set_capture_counters(_hf.CaptureCounters())
         try:
             with torch.cuda.graph(g, pool=self.owner.pool()):
                 outs = self.fn(*ins)
         finally:
             _rng.set_graph_context(prev)
+            _hf.set_capture_counters(None)
             if tuned:
                 tun.enable(True)
         if ctx is not None and ctx.total:

@@ -14,14 +14,23 @@ phase = sys.argv[3] if len(sys.argv) > 3 else "forward"
 fn, args, to_loss = BENCHMARKS[name].make("cuda")
 if executor == "thunder":
     fn = thunder.jit(fn)
+elif executor == "thunder+hipgraph":
+    from lightning_thunder_amd.transforms.hipgraph import HipGraphTransform
+
+    fn = thunder.jit(fn, transforms=[HipGraphTransform(donate_grads=True)])
+params = list(fn.parameters()) if hasattr(fn, "parameters") else []
 for _ in range(5):
     out = fn(*args)
     if phase == "backward":
         to_loss(out).backward()
+        for p in params:
+            p.grad = None
 torch.cuda.synchronize()
 for _ in range(10):
     out = fn(*args)
     if phase == "backward":
         to_loss(out).backward()
+        for p in params:
+            p.grad = None
 torch.cuda.synchronize()
 print("done", flush=True)

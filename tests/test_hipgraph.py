@@ -360,7 +360,7 @@ def test_graph_rng_codegen_reads_device_state_cpu():
         rngmap = {nums[0].name: (0, "seed"), nums[1].name: (0, "offset")}
         g = cg.generate(h.plan, h.inputs, h.outputs, targs, rng=rngmap)
         assert "A.rng[" not in plain.src and "const long long* rng[1];" in g.src
-        assert "A.rng[0][0]" in g.src and "A.rng[0][1]" in g.src
+        assert "rng_seed0 = A.rng[0][0], rng_base0 = A.rng[0][1]" in g.src and "rng_base0 +" in g.src
         hipfuse.compile_source(g)  # hiprtc compiles it (no GPU needed)
     finally:
         hipfuse.ex.allow_cpu = old
