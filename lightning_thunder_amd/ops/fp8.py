@@ -436,7 +436,9 @@ class _WeightShadow:
     def __init__(self, t, q, scale, key, slot, fmax):
         import weakref
 
-        self.ref = weakref.ref(t)
+        ptr = t.data_ptr()
+        # drop the registry entry (and its e4m3 copy) with the parameter
+        self.ref = weakref.ref(t, lambda _r, ptr=ptr: _SHADOWS.pop(ptr, None) if _SHADOWS.get(ptr) is self else None)
         self.q, self.scale, self.key, self.slot, self.fmax = q, scale, key, slot, fmax
         self.version = t._version
         self.shape = tuple(t.shape)
@@ -461,7 +463,12 @@ def _shadow_lookup(t: torch.Tensor):
     if not _SHADOWS or not _shadow_candidate(t):
         return None
     sh = _SHADOWS.get(t.data_ptr())
-    if sh is None or sh.ref() is not t or sh.version != t._version or sh.shape != tuple(t.shape):
+    if sh is None:
+        return None
+    if sh.ref() is None:  # the parameter is gone: free its e4m3 copy
+        del _SHADOWS[t.data_ptr()]
+        return None
+    if sh.ref() is not t or sh.version != t._version or sh.shape != tuple(t.shape):
         return None
     return sh
 
