@@ -703,7 +703,7 @@ def _fusion_pass(trace):
         # dY^T of an elementwise producer): the region stores the base value and the views run
         # standalone after it (zero-copy; the GEMMs read transposed operands in place) instead of the
         # region storing a transposed copy with strided 2-byte stores (Gemma's GeGLU backward: 2.4 ms)
-        post = _trailing_views(keep, internal_names)
+        post = _trailing_views(keep, internal_names, lazy_names | set(remat_names.get(idx, ())))
         if post:
             post_ids = {id(b) for b in post}
             keep = [b for b in keep if id(b) not in post_ids]
@@ -757,9 +757,11 @@ def _fusion_pass(trace):
     return new
 
 
-def _trailing_views(group: list, internal_names: set) -> list:
+def _trailing_views(group: list, internal_names: set, unstorable: set = frozenset()) -> list:
     """View ops at the end of a region's dataflow (outputs read by no other op of the region) that
-    form chains ending in a transpose of a region value; [] when there is no transpose among them."""
+    form chains ending in a transpose of a region value; [] when there is no transpose among them, or
+    when a chain starts from a value the region cannot hand out (``unstorable``: lazily re-materialised
+    casts, values recomputed from other regions)."""
     moved: list = []
     mids: set = set()
     remaining = list(group)
@@ -775,6 +777,9 @@ def _trailing_views(group: list, internal_names: set) -> list:
         mids |= ids
         remaining = [b for b in remaining if id(b) not in ids]
     if not any(b.sym.id == PrimIDs.TRANSPOSE for b in moved):
+        return []
+    moved_outs = {o.name for b in moved for o in b.flat_proxy_outs}
+    if any(a.name in unstorable for b in moved for a in b.flat_proxy_args if a.name not in moved_outs):
         return []
     if not any(cg.is_compute(b) for b in remaining):
         return []

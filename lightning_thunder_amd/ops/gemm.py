@@ -423,6 +423,12 @@ _PLANS: dict = {}
 _NO_PLAN = object()
 
 
+def _remember(key, plan) -> None:
+    if len(_PLANS) >= 8192:  # bounded: a program seeing ever new sizes re-dispatches instead of growing
+        _PLANS.clear()
+    _PLANS[key] = plan or _NO_PLAN
+
+
 def _tkey(t):
     return None if t is None else (t.shape, t.stride(), t.dtype, t.data_ptr() & 15)
 
@@ -475,7 +481,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
         return plan(x, w, bias, residual)
     out = _linear_dispatch(x, w, bias, residual, act)
     if plan is None and x.is_cuda and not torch.cuda.is_current_stream_capturing():
-        _PLANS[key] = _linear_plan(x, w, bias, residual, act) or _NO_PLAN
+        _remember(key, _linear_plan(x, w, bias, residual, act))
     return out
 
 
@@ -601,7 +607,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = Non
         return plan(a, b, None, residual)
     out = _matmul_dispatch(a, b, residual)
     if plan is None and a.is_cuda and not torch.cuda.is_current_stream_capturing():
-        _PLANS[key] = _matmul_plan(a, b, residual) or _NO_PLAN
+        _remember(key, _matmul_plan(a, b, residual))
     return out
 
 
