@@ -7,7 +7,7 @@ import os
 
 import torch
 
-from ._lib import require, dcode, ptr, stream_ptr, check, register_signature, c_int, c_void_p, c_float
+from ._lib import require, dcode, ptr, stream_ptr, check, register_signature, c_int, c_int64, c_void_p, c_float
 
 register_signature("lta_attn_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_float, c_int, c_void_p])
@@ -215,6 +215,13 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float | None = None, mask
         assert mask is not None and mask.dtype != torch.bool
         dmask = torch.empty((B, Hq, T, S), device=q.device, dtype=torch.float32)
     seed, offset = _graph_rng(lib, dropout_p, seed, offset)
+    part = None
+    if Hq > Hkv and mask is None and dropout_p == 0:
+        # GQA / MQA: the dK/dV pass splits each kv group's query heads over workgroups (D = 128 runs the
+        # v4 kernel's 256-key blocks, other head dims the v1 kernel's 128-key blocks)
+        part, nbytes, hs = _gqa_workspace(B, Hq, Hkv, S, q.device, D, 256 if D == 128 else 128)
+        if part is not None:
+            lib.lta_attn_set_gqa_workspace(part.data_ptr(), nbytes, hs)
     rc = lib.lta_attn_bwd_ex3(dcode(q), ptr(do), ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(delta), ptr(dq), ptr(dk),
                               ptr(dv), B, Hq, Hkv, T, S, D, float(sc), int(causal), ctypes.cast(st, c_void_p), ptr(mimg),
                               mb, mh, ptr(dmask), float(dropout_p), int(seed) & (2 ** 64 - 1),
@@ -253,7 +260,7 @@ def _dq_from_ds(ws_bytes: int, device: torch.device | None = None) -> bool:
     return 2 * ws_bytes <= free + spare
 
 
-def gqa_split(B: int, Hq: int, Hkv: int, S: int) -> int:
+def gqa_split(B: int, Hq: int, Hkv: int, S: int, keys_per_wg: int = 256) -> int:
     """How many workgroups share one kv group's query heads in the dK/dV pass.  The pass runs one
     workgroup per (batch, kv head, 256 keys): for GQA models (Mistral / Llama-3: 8 kv heads) that is
     128 workgroups at T = 4096, half of the 256 CUs, each sweeping 4 query heads.  Splitting the heads
@@ -263,7 +270,7 @@ def gqa_split(B: int, Hq: int, Hkv: int, S: int) -> int:
     if group <= 1:
         return 1
     cap = int(os.environ.get("LTA_ATTN_GQA_SPLIT", "8"))
-    n_wg = B * Hkv * ((S + 255) // 256)
+    n_wg = B * Hkv * ((S + keys_per_wg - 1) // keys_per_wg)
     best = 1
     for d in range(2, group + 1):
         if group % d or d > cap:
@@ -274,12 +281,15 @@ def gqa_split(B: int, Hq: int, Hkv: int, S: int) -> int:
     return best if n_wg < 512 else 1
 
 
-def _gqa_workspace(B, Hq, Hkv, S, device):
-    hs = gqa_split(B, Hq, Hkv, S)
+def _gqa_workspace(B, Hq, Hkv, S, device, D: int = 128, keys_per_wg: int = 256):
+    hs = gqa_split(B, Hq, Hkv, S, keys_per_wg)
     if hs <= 1:
         return None, 0, 1
-    ws = torch.empty(hs * B * Hkv * S * 256, device=device, dtype=torch.float32)
+    ws = torch.empty(hs * B * Hkv * S * 2 * D, device=device, dtype=torch.float32)
     return ws, ws.numel() * 4, hs
+
+
+register_signature("lta_attn_set_gqa_workspace", [c_void_p, c_int64, c_int])
 
 
 def attn_bwd_rope(do, q, k, v, o, lse, causal: bool, scale, cos, sin, n_head: int, n_query_groups: int):

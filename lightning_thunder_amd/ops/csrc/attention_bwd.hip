@@ -174,7 +174,11 @@ __device__ __forceinline__ void store_row_d128(T* row, const ACC& acc, float mul
 constexpr int kKB = 128;  // keys per workgroup
 constexpr int kQT = 32;   // queries per inner tile
 
-template <typename T, int D, bool CAUSAL, int EX = 0>
+// SPLIT (GQA / MQA head split, as the v4 kernel's): the grid's x holds B Hkv hsplit workgroups, workgroup
+// (bh, hs) sweeps query heads hs gsz .. hs gsz + gsz - 1 of its kv group (gsz = group / hsplit) and stores
+// fp32 partial dK / dV rows part[hs][bh][key][dK | dV][D] that attn_bwd_dkdv_reduce sums: Gemma-2b's one kv
+// head at T = 4096 is 32 workgroups of 128 keys without it (8 query heads each), 256 with it.
+template <typename T, int D, bool CAUSAL, int EX = 0, bool SPLIT = false>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                     const T* __restrict__ V, const T* __restrict__ dO,
                                                                     const float* __restrict__ LSE,
@@ -197,9 +201,13 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   (void)n_kb;
   // grid = (B*Hkv, key blocks): heaviest (causal) key blocks of every head first, balanced over XCDs
   const int kb = (int)blockIdx.y;
-  const int bh = blockIdx.x;
+  const int nsplit = SPLIT ? ex.hsplit : 1;
+  const int bh = SPLIT ? (int)blockIdx.x / nsplit : (int)blockIdx.x;
+  const int hs = SPLIT ? (int)blockIdx.x - bh * nsplit : 0;
   const int b = bh / Hkv, hk = bh % Hkv;
   const int group = Hq / Hkv;
+  const int gsz = group / nsplit;              // query heads this workgroup sweeps
+  const int hbase = hk * group + hs * gsz;     // the first of them
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   const int n_qt = (Tq + kQT - 1) / kQT;
   const int qt_begin = CAUSAL ? min((kb * kKB) / kQT, n_qt) : 0;
   const int nq = n_qt - qt_begin;
-  const int total = group * nq;
+  const int total = gsz * nq;
   // 16-B chunks per thread per tile, rounded up (D = 96: 384 chunks over 256 threads); the tail is
   // guarded by NCH
   constexpr int NCH = kQT * C::CH, LOADS = (NCH + kThreads - 1) / kThreads;
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
   uint4 pq[LOADS], po[LOADS];
   float plse = 0.f, pdel = 0.f;
   auto issue = [&](int it) {
-    const int hq = hk * group + it / nq;
+    const int hq = hbase + it / nq;
     const int qbase = (qt_begin + it % nq) * kQT;
     const T* Qb = Q + b * ex.sx.qb + hq * ex.sx.qh;
     const T* dOb = dO + b * sdo.b + hq * sdo.h;
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       const bool ok = qbase + tid < Tq;
       s_lse[buf][tid] = ok ? plse * 1.44269504088896340736f : INFINITY;
       s_delta[buf][tid] = ok ? pdel : 0.f;
-      if constexpr (DROP) s_qterm[buf][tid] = rng_q(rng_head(ex, b * Hq + hk * group + it / nq), qbase + tid);
+      if constexpr (DROP) s_qterm[buf][tid] = rng_q(rng_head(ex, b * Hq + hbase + it / nq), qbase + tid);
     }
   };
 
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
       pacc = mfma(oa, vf[s], pacc);  // dP = dO V^T
     }
     // P and dS (element i: query qbase + acc_row(i,h), key = this lane's key)
-    [[maybe_unused]] const int hq_it = hk * group + it / nq;
+    [[maybe_unused]] const int hq_it = hbase + it / nq;
     [[maybe_unused]] unsigned kterm = 0;
     if constexpr (DROP) kterm = rng_k(key);
 #pragma unroll
@@ -379,7 +387,20 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const T* __r
     for (int dt = 0; dt < C::DT; ++dt) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(dkacc[dt]), "+a"(dvacc[dt]));
   }
   // dK^T / dV^T: element i of tile dt is d = dt*32 + acc_row(i,h), key = this lane's key
-  if (key < Sk) {
+  if (SPLIT && key < Sk) {  // fp32 partial rows of this head split (summed by attn_bwd_dkdv_reduce)
+    const int nbh = (int)gridDim.x / nsplit;
+    float* prow = ex.part + (((int64_t)hs * nbh + bh) * Sk + key) * (2 * D);
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int d = dt * 32 + 8 * a + 4 * h;
+        *reinterpret_cast<float4*>(prow + d) = make_float4(dkacc[dt][4 * a] * scale, dkacc[dt][4 * a + 1] * scale,
+                                                           dkacc[dt][4 * a + 2] * scale, dkacc[dt][4 * a + 3] * scale);
+        *reinterpret_cast<float4*>(prow + D + d) =
+            make_float4(dvacc[dt][4 * a], dvacc[dt][4 * a + 1], dvacc[dt][4 * a + 2], dvacc[dt][4 * a + 3]);
+      }
+  } else if (key < Sk) {
     T* dkrow = dK + (int64_t)b * ex.sx.dkb + (int64_t)hk * ex.sx.dkh + (int64_t)key * ex.sx.dkt;
     T* dvrow = dV + (int64_t)b * ex.sx.dvb + (int64_t)hk * ex.sx.dvh + (int64_t)key * ex.sx.dvt;
 #pragma unroll
@@ -1560,20 +1581,21 @@ int g_dkdv_qrev = [] {
 
 // Sum of the GQA head split's fp32 partial dK / dV rows -> the gradients' dtype at their strides.
 // One thread per 8 consecutive d of one (kv head, key, dK|dV) row.
-template <typename T>
+template <typename T, int D = 128>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_reduce(const float* __restrict__ part, T* __restrict__ dK,
                                                             T* __restrict__ dV, int nbh, int Hkv, int Sk, int hsplit,
                                                             QKVStrides sx) {
+  constexpr int CH = D / 8;  // 8-float chunks per row
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (int64_t)nbh * Sk * 32) return;
-  const int c = (int)(id & 15);
-  const int64_t row = id >> 4;  // (bh * Sk + key) * 2 + which
+  if (id >= (int64_t)nbh * Sk * 2 * CH) return;
+  const int c = (int)(id % CH);
+  const int64_t row = id / CH;  // (bh * Sk + key) * 2 + which
   const int which = (int)(row & 1);
   const int64_t bk = row >> 1;
   const int key = (int)(bk % Sk), bh = (int)(bk / Sk);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < hsplit; ++s) {
-    const float4* src = reinterpret_cast<const float4*>(part + (((int64_t)s * nbh + bh) * Sk + key) * 256 + which * 128 + c * 8);
+    const float4* src = reinterpret_cast<const float4*>(part + (((int64_t)s * nbh + bh) * Sk + key) * (2 * D) + which * D + c * 8);
     const float4 a = src[0], b = src[1];
     acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
     acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
@@ -1590,10 +1612,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_reduce(const float* __restr
   *reinterpret_cast<uint4*>(dst + c * 8) = pk.u;
 }
 
-template <typename T>
+template <typename T, int D = 128>
 void launch_dkdv_reduce(void* dK, void* dV, int B, int Hkv, int Sk, const AttnExtra& ex, hipStream_t s) {
-  const int64_t n = (int64_t)B * Hkv * Sk * 32;
-  hipLaunchKernelGGL((attn_bwd_dkdv_reduce<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+  const int64_t n = (int64_t)B * Hkv * Sk * 2 * (D / 8);
+  hipLaunchKernelGGL((attn_bwd_dkdv_reduce<T, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      (const float*)ex.part, (T*)dK, (T*)dV, B * Hkv, Hkv, Sk, ex.hsplit, ex.sx);
 }
 
@@ -1669,11 +1691,19 @@ int launch_bwd(const void* dO, const void* Q, const void* K, const void* V, cons
     }
     return (int)hipGetLastError();
   }
-  dim3 g1(B * Hkv, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM);
+  const int hsplit = (ex.part && ex.hsplit > 1) ? ex.hsplit : 1;
+  dim3 g1(B * Hkv * hsplit, (Sk + kKB - 1) / kKB), g2(B * Hq, (Tq + kBM - 1) / kBM);
 #define LTA_V1(CA)                                                                                                   \
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, CA>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,          \
-                     (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale, sl2, \
-                     sdo, ex);                                                                                         \
+  if (hsplit > 1) {                                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, CA, 0, true>), g1, blk, 0, s, (const T*)Q, (const T*)K,           \
+                       (const T*)V, (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, \
+                       Sk, scale, sl2, sdo, ex);                                                                       \
+    launch_dkdv_reduce<T, D>(dK, dV, B, Hkv, Sk, ex, s);                                                               \
+  } else {                                                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D, CA>), g1, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,        \
+                       (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dK, (T*)dV, Hq, Hkv, Tq, Sk, scale,   \
+                       sl2, sdo, ex);                                                                                  \
+  }                                                                                                                  \
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, CA>), g2, blk, 0, s, (const T*)Q, (const T*)K, (const T*)V,            \
                      (const T*)dO, (const float*)LSE, (const float*)DELTA, (T*)dQ, Hq, Hkv, Tq, Sk, scale, sl2, sdo, ex)
   if (causal) { LTA_V1(true); }
@@ -1695,10 +1725,11 @@ static int fast_enabled() {
 
 // GQA head split of the dK/dV pass (hsplit > 1 with an fp32 workspace of hsplit B Hkv Sk 256 floats):
 // validates it and records it in `ex`.  hsplit <= 1 or no workspace: no split.
-static bool gqa_split_ok(AttnExtra& ex, void* part_ws, int64_t part_bytes, int hsplit, int B, int Hq, int Hkv, int Sk) {
+static bool gqa_split_ok(AttnExtra& ex, void* part_ws, int64_t part_bytes, int hsplit, int B, int Hq, int Hkv, int Sk,
+                         int D = 128) {
   if (hsplit <= 1 || part_ws == nullptr) return true;
   const int group = Hq / Hkv;
-  if (group % hsplit != 0 || part_bytes < (int64_t)hsplit * B * Hkv * Sk * 256 * 4 || (uintptr_t)part_ws % 16) return false;
+  if (group % hsplit != 0 || part_bytes < (int64_t)hsplit * B * Hkv * Sk * 2 * D * 4 || (uintptr_t)part_ws % 16) return false;
   ex.part = static_cast<float*>(part_ws);
   ex.hsplit = hsplit;
   return true;
@@ -1771,12 +1802,24 @@ LTA_EXPORT int lta_attn_bwd_rope_ds(int dtype, const void* dO, const void* Q, co
   return -1;
 }
 
+// GQA / MQA head split of the next lta_attn_bwd_ex3 call of this host thread (fp32 workspace of hsplit B Hkv
+// Sk 2 D floats; taken and cleared by that call)
+struct GqaWs {
+  void* part = nullptr;
+  int64_t bytes = 0;
+  int hsplit = 1;
+};
+inline thread_local GqaWs g_gqa_ws;
+LTA_EXPORT void lta_attn_set_gqa_workspace(void* part, int64_t bytes, int hsplit) { g_gqa_ws = GqaWs{part, bytes, hsplit}; }
+
 LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const void* K, const void* V, const void* O,
                                 const void* LSE, void* DELTA, void* dQ, void* dK, void* dV, int B, int Hq, int Hkv,
                                 int Tq, int Sk, int D, float scale, int causal, const int64_t* strides, const void* mask,
                                 int mask_b, int mask_h, void* dmask, float dropout_p, uint64_t seed, uint64_t offset,
                                 const int64_t* qkv_strides, const int64_t* grad_strides, hipStream_t stream) {
   const long long* rng = take_attn_rng();
+  const GqaWs gws = g_gqa_ws;
+  g_gqa_ws = GqaWs{};
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f || (dmask && !mask)) return -2;
   const RowStrides dflt{(int64_t)Hq * Tq * D, (int64_t)Tq * D, D};
   const RowStrides sdo = strides ? RowStrides{strides[0], strides[1], strides[2]} : dflt;
@@ -1785,6 +1828,7 @@ LTA_EXPORT int lta_attn_bwd_ex3(int dtype, const void* dO, const void* Q, const 
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
   ex.sx.set_grad(grad_strides);
+  if (!mask && dropout_p == 0.f && !gqa_split_ok(ex, gws.part, gws.bytes, gws.hsplit, B, Hq, Hkv, Sk, D)) return -2;
   int exf = 0;
   if (mask) {
     const int64_t skp = (int64_t)(Sk + 63) / 64 * 64;

@@ -1532,3 +1532,30 @@ def test_gemm4_linear_plan_repeats(bias, act):
             torch.testing.assert_close(o, outs[0], rtol=0, atol=0)
         err = ((outs[0].float() - ref).norm() / ref.norm()).item()
         assert err < 1e-2, (M, N, K, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [256, 128])
+def test_attention_backward_mqa_head_split(D, monkeypatch):
+    """Gemma-2b's multi-query attention (8 query heads on one kv head): the dK/dV pass splits the group's
+    query heads over workgroups (fp32 partial rows + one reduce launch) instead of running 8 heads in
+    each of T / 128 workgroups; dQ / dK / dV match fp32 and the unsplit kernel."""
+    from lightning_thunder_amd.ops.attention import attn_bwd, attn_fwd, gqa_split
+
+    B, Hq, Hkv, T = 1, 8, 1, 1024
+    assert gqa_split(B, Hq, Hkv, T, 128 if D != 128 else 256) == 8
+    torch.manual_seed(0)
+    q = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, Hq, T, D, device="cuda", dtype=torch.bfloat16)
+    o, lse = attn_fwd(q, k, v, True)
+    split = attn_bwd(do, q, k, v, o, lse, True)
+    monkeypatch.setenv("LTA_ATTN_GQA_SPLIT", "1")
+    plain = attn_bwd(do, q, k, v, o, lse, True)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    _sdpa_ref(qf, kf, vf, True).backward(do.float())
+    for got, base, ref in zip(split, plain, (qf.grad, kf.grad, vf.grad)):
+        err = ((got.float() - ref).norm() / ref.norm()).item()
+        base_err = ((base.float() - ref).norm() / ref.norm()).item()
+        assert err < 2e-2 and err <= 1.5 * base_err + 1e-3, (err, base_err)
