@@ -1317,9 +1317,68 @@ def _fuse_attn_bwd_rope(trace):
     return new
 
 
+def _rms_bwd_fp8_meta(dy, x, weight, rstd, residual, key, slot):
+    q, sc = _fp8_cast_meta(x, True)
+    return TensorProxy(like=x), (None if weight is None else TensorProxy(like=weight)), q, sc
+
+
+def _rms_bwd_fp8_impl(dy, x, weight, rstd, residual, key, slot):
+    from ..ops.fp8 import rms_norm_bwd_fp8_delayed
+
+    return rms_norm_bwd_fp8_delayed(dy, x, weight, rstd, residual, key, slot)
+
+
+hip_rms_norm_bwd_fp8 = ex.register_operator("hip_rms_norm_bwd_fp8", meta=_rms_bwd_fp8_meta, fn=_rms_bwd_fp8_impl)
+
+
+def _fuse_fp8_rms_bwd_casts(trace):
+    """``dx, dw = hip_rms_norm_bwd(g, x, w, rstd[, r]); q, s = hip_fp8_cast_delayed(dx, True, key, slot)``
+    -> ``dx, dw, q, s = hip_rms_norm_bwd_fp8(g, x, w, rstd, r, key, slot)``: a LLaMA block's residual-
+    stream gradient is the output gradient of the preceding fp8 linear (the attention projection after
+    norm_2's backward, the previous block's MLP projection after norm_1's), so its e5m2 copy leaves the
+    norm backward's store pass (dx keeps its other uses; the cast launch re-reading dx disappears).
+    Runs after :func:`_fuse_rms_bwd_residual`, so the residual add is already in the norm backward."""
+    import os
+
+    from ..core.trace import from_trace, TraceProvenance
+
+    if os.environ.get("LTA_FP8_FUSE_PRODUCERS", "1") == "0":  # A/B hook (with the forward producers)
+        return trace
+    bsyms = trace.bound_symbols
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_fp8_cast_delayed or len(b.args) != 4 or not b.args[1]:
+            continue
+        y, _, key, slot = b.args
+        j = producer.get(y.name)
+        if j is None or j in replace:
+            continue
+        pb = bsyms[j]
+        if pb.sym is not hip_rms_norm_bwd or pb.output[0].name != y.name:
+            continue
+        res = pb.args[4] if len(pb.args) > 4 else None
+        nb = hip_rms_norm_bwd_fp8.bind(*pb.args[:4], res, key, slot,
+                                       output=(pb.output[0], pb.output[1], b.output[0], b.output[1]))
+        replace[j] = ex.bind_call_ctx(nb)
+        drop.add(i)
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} e5m2 gradient cast(s) fused into RMSNorm backwards"))
+    return new
+
+
 def _post_claim(trace):
     return _fuse_attn_bwd_rope(_fuse_fp8_qkv_rope_gemm(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
-        _fuse_decode_gemv(_fuse_rms_bwd_residual(_fuse_linear_epilogues(_fuse_fp8_cast_producers(trace))))))))))
+        _fuse_decode_gemv(_fuse_fp8_rms_bwd_casts(_fuse_rms_bwd_residual(_fuse_linear_epilogues(
+            _fuse_fp8_cast_producers(trace)))))))))))
 
 
 ex.post_claim_pass = _post_claim

@@ -142,14 +142,28 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_generic(const T* __restr
   }
 }
 
-template <typename T, int CHUNKS>
+// FP8-linear consumer of the backward (delayed scaling, Q8): dx also leaves as e5m2 (q = fp8(bf16(dx) s),
+// s = fmax / amax_in) for the preceding linear's dgrad / wgrad GEMMs -- the gradient cast fused into the
+// norm backward; max |bf16(dx)| of the whole tensor into amax_out.
+struct Q8Args {
+  uint8_t* q;
+  const float* amax_in;
+  float fmax;
+  float* scale_out;
+  float* amax_out;
+};
+
+template <typename T, int CHUNKS, bool Q8 = false>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                const T* __restrict__ w, const float* __restrict__ rstd,
                                                                T* __restrict__ dx, float* __restrict__ dw_partial,
                                                                int64_t rows, int cols, int rows_per_block,
-                                                               const T* __restrict__ res) {
+                                                               const T* __restrict__ res, Q8Args q8 = {}) {
   constexpr int V = Vec16<T>::N;
+  static_assert(!Q8 || V == 8, "fp8 output: 16-bit gradients");
   __shared__ float smem[2 * kWaves];
+  [[maybe_unused]] float qs = 0.f, qm = 0.f;
+  if constexpr (Q8) qs = fp8_scale(q8.amax_in, q8.fmax, q8.scale_out);
   float dw_acc[CHUNKS][V];
 #pragma unroll
   for (int c = 0; c < CHUNKS; ++c)
@@ -248,9 +262,22 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
             const float xh = to_f32(xv[h][c].v[j]) * r;
             const float gw = to_f32(gv[h][c].v[j]) * to_f32(wv[c].v[j]);
             const float add = res != nullptr ? to_f32(rv[h][c].v[j]) : 0.f;  // gradient through the residual
-            o.v[j] = from_f32<T>(r * (gw - xh * dot) + add);
+            // explicit fmas: the same rounding in every instantiation (the Q8 variant's e5m2 copy is
+            // of exactly the dx the plain kernel stores)
+            o.v[j] = from_f32<T>(__builtin_fmaf(r, __builtin_fmaf(-xh, dot, gw), add));
           }
           store16(dx + rr * cols + idx, o);
+          if constexpr (Q8) {
+            float ov[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+              ov[j] = to_f32(o.v[j]);  // the unfused bf16 dx
+              qm = fmaxf(qm, fabsf(ov[j]));
+            }
+            const uint32_t lo = cvt4<true>(ov[0] * qs, ov[1] * qs, ov[2] * qs, ov[3] * qs);
+            const uint32_t hi = cvt4<true>(ov[4] * qs, ov[5] * qs, ov[6] * qs, ov[7] * qs);
+            *reinterpret_cast<uint2*>(q8.q + rr * cols + idx) = make_uint2(lo, hi);
+          }
         }
       }
     }
@@ -265,6 +292,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(const T* __restri
         for (int j = 0; j < V; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(dw_acc[c][j], dw_acc[c][j + 1], dw_acc[c][j + 2], dw_acc[c][j + 3]);
       }
     }
+  }
+  if constexpr (Q8) {
+    __shared__ float red[kWaves];  // not smem: a slower wave may still be reading the last row's dot products
+    if (q8.amax_out != nullptr) fp8_amax_out<kWaves>(qm, q8.amax_out, red);
   }
 }
 
@@ -346,7 +377,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* rstd, int64_t rows, 
 
 template <typename T>
 int launch_bwd(const void* dy, const void* x, const void* w, const void* rstd, void* dx, void* dw, void* workspace,
-               int64_t rows, int cols, int nblocks, const void* res, hipStream_t s) {
+               int64_t rows, int cols, int nblocks, const void* res, hipStream_t s, const Q8Args* q8 = nullptr) {
   constexpr int V = Vec16<T>::N;
   const int per_pass = kThreads * V;
   const int chunks = (cols + per_pass - 1) / per_pass;
@@ -360,8 +391,24 @@ int launch_bwd(const void* dy, const void* x, const void* w, const void* rstd, v
   T* DX = (T*)dx;
   float* Pp = dw ? P : nullptr;
   const T* RES = (const T*)res;
-  if (cols % V != 0 || chunks > 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) || ((uintptr_t)dx % 16) || (w && ((uintptr_t)w % 16)) ||
-      ((uintptr_t)res % 16)) {
+  const bool vec_ok = !(cols % V != 0 || chunks > 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) ||
+                        ((uintptr_t)dx % 16) || (w && ((uintptr_t)w % 16)) || ((uintptr_t)res % 16));
+  if (q8 != nullptr) {  // fp8 output: the vectorised kernel only (-1: the caller casts separately)
+    if constexpr (Vec16<T>::N != 8) {
+      return -1;
+    } else {
+      if (!vec_ok || ((uintptr_t)q8->q % 8)) return -1;
+      switch (chunks) {
+#define LTA_CASE(C)                                                                                          \
+  case C:                                                                                                    \
+    hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, C, true>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, \
+                       rpb, RES, *q8);                                                                       \
+    break;
+        LTA_CASE(1) LTA_CASE(2) LTA_CASE(3) LTA_CASE(4)
+#undef LTA_CASE
+      }
+    }
+  } else if (!vec_ok) {
     hipLaunchKernelGGL((rmsnorm_bwd_generic<T>), grid, block, 0, s, DY, X, W, R, DX, Pp, rows, cols, rpb, RES);
   } else {
     switch (chunks) {
@@ -432,6 +479,21 @@ LTA_EXPORT int lta_rmsnorm_bwd_res(int dtype, const void* dy, const void* x, con
     case kBF16: return launch_bwd<__hip_bfloat16>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
     case kF16: return launch_bwd<__half>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
     case kF32: return launch_bwd<float>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream);
+  }
+  return -1;
+}
+
+// lta_rmsnorm_bwd_res plus an e5m2 copy of dx (Q8Args semantics above): q [rows, cols] uint8, the delayed
+// scale fmax / *amax_in to scale_out, max |dx| into amax_out.  16-bit dtypes, the vectorised shapes
+// (cols % 8 == 0, cols <= 8192, 16-B aligned rows); -1 when unsupported (nothing launched).
+LTA_EXPORT int lta_rmsnorm_bwd_fp8(int dtype, const void* dy, const void* x, const void* w, const void* rstd, void* dx,
+                                   void* dw, void* workspace, int64_t rows, int64_t cols, int nblocks, const void* res,
+                                   void* q, const void* amax_in, float fmax, void* scale_out, void* amax_out,
+                                   hipStream_t stream) {
+  const Q8Args q8{(uint8_t*)q, (const float*)amax_in, fmax, (float*)scale_out, (float*)amax_out};
+  switch (dtype) {
+    case kBF16: return launch_bwd<__hip_bfloat16>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream, &q8);
+    case kF16: return launch_bwd<__half>(dy, x, w, rstd, dx, dw, workspace, rows, (int)cols, nblocks, res, stream, &q8);
   }
   return -1;
 }

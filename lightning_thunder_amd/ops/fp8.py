@@ -665,3 +665,40 @@ def swiglu_bwd_fp8_delayed(g: torch.Tensor, a: torch.Tensor, b: torch.Tensor, ke
     qa, sa = quantize_delayed_rows(da, True, key, slot_a)
     qb, sb = quantize_delayed_rows(db, True, key, slot_b)
     return qa, sa, qb, sb
+
+
+register_signature("lta_rmsnorm_bwd_fp8", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                                           c_void_p, c_void_p])
+
+
+def rms_norm_bwd_fp8_delayed(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor | None, rstd: torch.Tensor,
+                             residual: torch.Tensor | None, key: int, slot: int):
+    """(dx, dw, q, scale): the RMSNorm backward (+ the residual stream's gradient) whose dx is also the
+    output gradient of an fp8 linear, so it leaves the kernel a second time as an e5m2 copy quantised
+    in ``slot`` (csrc/rmsnorm.hip Q8: no separate cast launch re-reading dx)."""
+    from .rmsnorm import rms_norm_bwd, _as_2d, _bwd_blocks
+    from ._lib import ptr
+
+    C = x.shape[-1]
+    if not _first_use(key, slot, x.device) and x.dtype in (torch.bfloat16, torch.float16):
+        x2, rows, _ = _as_2d(x)
+        dy2 = _as_2d(dy)[0]
+        r2 = None if residual is None else _as_2d(residual)[0]
+        wc = None if w is None else w.contiguous()
+        amax_in, fmax, scale, sink = delayed_scaling_source(x2, True, key, slot)
+        dx = torch.empty_like(x2)
+        q = torch.empty(x2.shape, dtype=torch.uint8, device=x.device)
+        nblocks = _bwd_blocks(rows)
+        dw = None if wc is None else torch.empty_like(wc)
+        ws = None if wc is None else torch.empty((nblocks, C), device=x.device, dtype=torch.float32)
+        rc = require().lta_rmsnorm_bwd_fp8(DTYPE_CODE[x2.dtype], ptr(dy2), ptr(x2), ptr(wc), ptr(rstd), ptr(dx), ptr(dw),
+                                           ptr(ws), rows, C, nblocks, ptr(r2), q.data_ptr(), amax_in.data_ptr(), fmax,
+                                           scale.data_ptr(), sink.data_ptr(), stream_ptr(x.device))
+        if rc == 0:
+            return dx.view(x.shape), dw, q, scale
+        if rc != -1:
+            check(rc, "lta_rmsnorm_bwd_fp8")
+    dx, dw = rms_norm_bwd(dy, x, w, rstd, residual)
+    q, scale = quantize_delayed_rows(dx, True, key, slot)
+    return dx, dw, q, scale

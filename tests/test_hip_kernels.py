@@ -634,6 +634,87 @@ def test_fp8_producer_fused_casts_match_unfused(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_fp8_rms_bwd_fused_gradient_cast_matches_unfused(monkeypatch):
+    """h = inp(x); out = h + proj(norm(h)) under delayed FP8: the residual-stream gradient of h leaves
+    the RMSNorm backward (residual add fused) a second time as the e5m2 output gradient of ``inp``
+    (hip_rms_norm_bwd_fp8, no cast launch); losses and gradients over three steps match the unfused
+    program bit for bit."""
+    import lightning_thunder_amd as thunder
+    from lightning_thunder_amd.models.litgpt import RMSNorm
+    from lightning_thunder_amd.ops.fp8 import DelayedScaling
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    class Block(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.inp = torch.nn.Linear(256, 512, bias=False)
+            self.norm = RMSNorm(512, eps=1e-5)
+            self.proj = torch.nn.Linear(512, 512, bias=False)
+
+        def forward(self, x):
+            h = self.inp(x)
+            return h + self.proj(self.norm(h))
+
+    torch.manual_seed(0)
+    m = Block().cuda().bfloat16()
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("LTA_FP8_FUSE_PRODUCERS", fuse)
+        t = FP8LinearTransform(recipe=DelayedScaling(amax_history_len=4))
+        jm = thunder.jit(m, transforms=[t])
+        outs = []
+        for step in range(3):
+            x = torch.randn(2, 256, 256, device="cuda", dtype=torch.bfloat16,
+                            generator=torch.Generator("cuda").manual_seed(step))
+            loss = (jm(x).float() ** 2).mean()
+            grads = torch.autograd.grad(loss, list(m.parameters()))
+            outs.append((loss.detach(),) + tuple(grads))
+        bw = str(thunder.last_backward_traces(jm)[-1])
+        if fuse == "1":
+            assert "hip_rms_norm_bwd_fp8" in bw, bw
+        else:
+            assert "hip_rms_norm_bwd_fp8" not in bw, bw
+        res[fuse] = outs
+    for a, b in zip(res["1"], res["0"]):
+        for u, v in zip(a, b):
+            torch.testing.assert_close(u, v, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_rms_norm_bwd_fp8_kernel_matches_cast():
+    """lta_rmsnorm_bwd_fp8 (vectorised backward + e5m2 side output) against the plain backward followed
+    by the delayed-scaling row cast: dx, dw, the e5m2 bytes and the recorded amax are identical."""
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.ops.rmsnorm import rms_norm_bwd, rms_norm_fwd
+
+    torch.manual_seed(0)
+    for rows, cols, with_res in ((1000, 4096, True), (333, 1024, False), (64, 2048, True)):
+        x = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
+        w = (1 + 0.1 * torch.randn(cols, device="cuda")).bfloat16()
+        g = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
+        r = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16) if with_res else None
+        _, rstd = rms_norm_fwd(x, w, 1e-5)
+        key = fp8.new_delayed_state(fp8.DelayedScaling(amax_history_len=2), 1)
+        dx_ref, dw_ref = rms_norm_bwd(g, x, w, rstd, r)
+        # first use: the unfused fallback records the slot's amax; the second call runs the kernel
+        fp8.rms_norm_bwd_fp8_delayed(g, x, w, rstd, r, key, 0)
+        st = fp8._DELAYED[key]
+        st.cur[0].zero_()
+        dx, dw, q, s = fp8.rms_norm_bwd_fp8_delayed(g, x, w, rstd, r, key, 0)
+        torch.testing.assert_close(dx, dx_ref, rtol=0, atol=0)
+        torch.testing.assert_close(dw, dw_ref, rtol=0, atol=0)
+        amax_in = st.step_src[0]
+        fmax = fp8.E5M2_MAX * 2.0 ** -st.recipe.margin
+        s_ref = torch.tensor(fmax, device="cuda") / amax_in.clamp_min(1e-12)
+        torch.testing.assert_close(s, s_ref.reshape(()), rtol=1e-6, atol=0)
+        q_ref = (dx_ref.float() * s).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+        mism = (q.view(-1) != q_ref.view(-1)).float().mean().item()
+        assert mism < 1e-3, mism  # rounding-mode ties only
+        assert st.cur[0].item() == dx_ref.float().abs().max().item()
+        fp8.release_delayed_state(key)
+
+
+@pytest.mark.gpu
 def test_fp8_delayed_scaling_training():
     """DelayedScaling recipe: scales come from the amax history of earlier steps (recorded while
     casting); results stay close to bf16 over several steps, siblings share the x slot, and the
