@@ -814,12 +814,14 @@ class TensorArg:
 # column-mode partial hand-off between workgroups: "coherent" (sc1 vector memory ops + s_waitcnt) or
 # "fence" (__threadfence); LTA_HIPFUSE_COL_SYNC overrides (A/B hook, scripts/colred_bench.py)
 COL_SYNC = os.environ.get("LTA_HIPFUSE_COL_SYNC", "coherent")
-# column-mode grid (profiles/hipfuse_colred_sweep.txt: 8 waves x 8 rows in flight per wave, ~192
-# workgroups, at most 64 row splits was the fastest of the swept configurations on every shape)
+# column-mode grid: 8 waves per workgroup, ~192 workgroups (profiles/hipfuse_colred_sweep.txt), at most
+# 128 row splits and 4 rows in flight per wave (round 6, device-side kernel durations of the GPT-2-medium
+# step's column kernels: profiles/hipfuse_roofline_gpt2_r6.txt -- 4.78 -> 4.52 ms of generated kernels per
+# step; the earlier sweeps timed batches of Python launches, which bound the short kernels)
 COL_NW = int(os.environ.get("LTA_HIPFUSE_COL_NW", "8"))  # waves per column-mode workgroup
 COL_WGS = int(os.environ.get("LTA_HIPFUSE_COL_WGS", "192"))  # target workgroups of a column-mode grid
-COL_UNROLL = int(os.environ.get("LTA_HIPFUSE_COL_UNROLL", "8"))  # rows in flight per wave
-COL_MAX_SPLITS = 64  # the last workgroup of a column group reads every split's partial
+COL_UNROLL = int(os.environ.get("LTA_HIPFUSE_COL_UNROLL", "4"))  # rows in flight per wave
+COL_MAX_SPLITS = int(os.environ.get("LTA_HIPFUSE_COL_MAX_SPLITS", "128"))  # the last workgroup of a column group reads every split's partial
 # regions with full-domain outputs besides the column reduction (GPT-2's GELU backward + bias gradient:
 # 80.7 -> 48 us at S = 24 -> 64, scripts/gpu_s5v.sh)
 COL_WGS_FULL = int(os.environ.get("LTA_HIPFUSE_COL_WGS_FULL", "768"))
@@ -1891,6 +1893,9 @@ class _Gen:
         body.append(f"  const {IT} ec = cvalid ? e : 0u;")
         self._decompose("ec", list(range(k, nd)), body, "  ")
         self.flat_index = f"((unsigned long long)r * {C}ull + (unsigned long long)ec + (unsigned long long)j)"
+        # a lane's V columns start at a multiple of 4 of the flat index when V and C are: Philox draws
+        # then take whole 4-word blocks (one philox4 per 4 elements, as in pointwise mode)
+        self.flat_base4 = f"((unsigned long long)r * {C}ull + (unsigned long long)ec)" if V % 4 == 0 and C % 4 == 0 else None
         for n, kk, act, init, comb in accs:
             body.append(f"  {act} acc{n}[{V}];")
             body.append(f"  #pragma unroll")
@@ -2033,6 +2038,7 @@ class _Gen:
             body.append("  __syncthreads();")
             lds_combine()
         # column epilogue: thread t takes columns t, t + 64 NW, ... of the group (one element each)
+        self.flat_base4 = None
         self.force_scalar = True
         self._scope_id = "fin"
         self.idx_avail = set()
@@ -2100,6 +2106,9 @@ class _Gen:
         body.append(f"  const {IT} ec = cvalid ? e : 0u;")
         self._decompose("ec", list(range(k, nd)), body, "  ")
         self.flat_index = f"((unsigned long long)r * {C}ull + (unsigned long long)ec + (unsigned long long)j)"
+        # a lane's V columns start at a multiple of 4 of the flat index when V and C are: Philox draws
+        # then take whole 4-word blocks (one philox4 per 4 elements, as in pointwise mode)
+        self.flat_base4 = f"((unsigned long long)r * {C}ull + (unsigned long long)ec)" if V % 4 == 0 and C % 4 == 0 else None
         for n, kk, act, init, comb in accs:
             body.append(f"  {act} acc{n}[{V}];")
             body.append(f"  #pragma unroll")

@@ -533,6 +533,35 @@ def test_philox_dropout_gpu_matches_torch_philox(shape):
     torch.testing.assert_close(gx, ref, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 512, 1024), (64, 36), (33, 7)])  # 4-word vector draws / scalar draws
+def test_philox_dropout_column_region_gpu(shape):
+    """Dropout on a biased activation: the backward's mask regeneration and the bias-gradient column
+    sum share one column-mode kernel (Philox words drawn whole blocks at a time where the columns
+    allow); mask and both gradients match the torch Philox reference."""
+    from lightning_thunder_amd.core import rng
+    from lightning_thunder_amd.core.rng import philox_uniform_torch
+
+    def f(x, b):
+        return torch.nn.functional.dropout(x + b, p=0.25, training=True)
+
+    x = torch.randn(*shape, device="cuda", requires_grad=True)
+    b = torch.randn(shape[-1], device="cuda", requires_grad=True)
+    jf = thunder.jit(f, executors=["hipfuse", "torch"])
+    torch.manual_seed(321)
+    rng._state["seed"] = None
+    y = jf(x, b)
+    keep = philox_uniform_torch(x.shape, 321, 0, "cuda") < 0.75
+    assert torch.equal(y != 0, keep)
+    g = torch.randn_like(y)
+    gx, gb = torch.autograd.grad(y, (x, b), g)
+    bw = thunder.last_backward_traces(jf)[-1]
+    assert any("uniform_philox" in s and "sum" in s for s in (str(fb.subsymbols) for fb in hipfuse.fusions(bw))), bw
+    ref = torch.where(keep, g / 0.75, torch.zeros_like(g))
+    torch.testing.assert_close(gx, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gb, ref.reshape(-1, shape[-1]).sum(0), rtol=1e-4, atol=1e-4)
+
+
 def test_moe_model_cpu():
     """Mixtral-style MoE (top-k routing, sorted tokens, grouped GEMMs) fwd+bwd vs eager."""
     from lightning_thunder_amd.models.litgpt import GPT, Config
