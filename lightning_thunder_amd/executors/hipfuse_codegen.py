@@ -814,14 +814,17 @@ class TensorArg:
 # column-mode partial hand-off between workgroups: "coherent" (sc1 vector memory ops + s_waitcnt) or
 # "fence" (__threadfence); LTA_HIPFUSE_COL_SYNC overrides (A/B hook, scripts/colred_bench.py)
 COL_SYNC = os.environ.get("LTA_HIPFUSE_COL_SYNC", "coherent")
-# column-mode grid: 8 waves per workgroup, ~192 workgroups (profiles/hipfuse_colred_sweep.txt), at most
-# 128 row splits and 4 rows in flight per wave (round 6, device-side kernel durations of the GPT-2-medium
-# step's column kernels: profiles/hipfuse_roofline_gpt2_r6.txt -- 4.78 -> 4.52 ms of generated kernels per
-# step; the earlier sweeps timed batches of Python launches, which bound the short kernels)
+# column-mode grid: 8 waves per workgroup, ~192 workgroups (profiles/hipfuse_colred_sweep.txt), 4 rows in
+# flight per wave, at most 64 row splits for a bare column reduction (the last workgroup of a column group
+# reads every split's partial: more splits measured slower) and 128 when the region also stores
+# full-domain outputs (its per-element work wants the occupancy).  Round 6, device-side kernel durations
+# (profiles/hipfuse_roofline_gpt2_r6.txt, profiles/hipfuse_colred_sweep_r6.txt); the earlier sweeps timed
+# batches of Python launches, which bound the short kernels.
 COL_NW = int(os.environ.get("LTA_HIPFUSE_COL_NW", "8"))  # waves per column-mode workgroup
 COL_WGS = int(os.environ.get("LTA_HIPFUSE_COL_WGS", "192"))  # target workgroups of a column-mode grid
 COL_UNROLL = int(os.environ.get("LTA_HIPFUSE_COL_UNROLL", "4"))  # rows in flight per wave
-COL_MAX_SPLITS = int(os.environ.get("LTA_HIPFUSE_COL_MAX_SPLITS", "128"))  # the last workgroup of a column group reads every split's partial
+COL_MAX_SPLITS = int(os.environ.get("LTA_HIPFUSE_COL_MAX_SPLITS", "64"))
+COL_MAX_SPLITS_FULL = int(os.environ.get("LTA_HIPFUSE_COL_MAX_SPLITS_FULL", "128"))
 # regions with full-domain outputs besides the column reduction (GPT-2's GELU backward + bias gradient:
 # 80.7 -> 48 us at S = 24 -> 64, scripts/gpu_s5v.sh)
 COL_WGS_FULL = int(os.environ.get("LTA_HIPFUSE_COL_WGS_FULL", "768"))
@@ -1867,7 +1870,7 @@ class _Gen:
         # gradient: that work wants the occupancy of a pointwise grid), >= 8 rows per wave, and at most
         # COL_MAX_SPLITS (the serial tail reads them all)
         wgs = COL_WGS_FULL if full_outs else COL_WGS
-        S = max(1, min(-(-wgs // ncs), -(-R // (8 * NW)), COL_MAX_SPLITS))
+        S = max(1, min(-(-wgs // ncs), -(-R // (8 * NW)), COL_MAX_SPLITS_FULL if full_outs else COL_MAX_SPLITS))
         RPS = -(-R // S)
         S = -(-R // RPS)
         full_names = {o.name for o in full_outs}
