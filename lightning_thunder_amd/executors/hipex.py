@@ -1375,10 +1375,110 @@ def _fuse_fp8_rms_bwd_casts(trace):
     return new
 
 
+def _attn_fwd_fp8_meta(q, k, v, causal, scale, key, slot):
+    B, H, L, E = q.shape
+    return (TensorProxy(like=q), TensorProxy(like=q, shape=(B, H, L), dtype=torch.float32, requires_grad=False),
+            TensorProxy(like=q, shape=(B * L, H * E), dtype=torch.uint8, requires_grad=False),
+            TensorProxy(like=q, shape=(), dtype=torch.float32, requires_grad=False))
+
+
+def _attn_fwd_fp8_impl(q, k, v, causal, scale, key, slot):
+    from ..ops.fp8 import attn_fwd_fp8_delayed
+
+    return attn_fwd_fp8_delayed(q, k, v, causal, scale, key, slot)
+
+
+hip_attn_fwd_fp8 = ex.register_operator("hip_flash_attn_fwd_fp8", meta=_attn_fwd_fp8_meta, fn=_attn_fwd_fp8_impl)
+
+# the view ops of o.transpose(1, 2).reshape(B, T, H D) at every level a trace can hold them (ltorch symbols
+# before flattening, their torch-executor operators, the prims)
+_HEAD_MERGE_VIEWS = {"transpose", "permute", "reshape", "view", "torch_transpose", "torch_permute", "torch_reshape",
+                     "torch_view", "transpose_prim", "reshape_prim"}
+
+
+def _merges_heads(chain, out) -> bool:
+    """``chain`` (producer order) turns the attention output [B, H, T, D] into its [B, T, H D] (or
+    [B T, H D]) rows: one (1, 2) transpose / permute, then reshapes only."""
+    B, H, T, D = out.shape
+    swapped = False
+    for b in chain:
+        n = b.sym.name
+        if n in ("transpose", "torch_transpose"):
+            dims = {int(pyval(d)) % 4 for d in b.args[1:3]}
+            if swapped or dims != {1, 2}:
+                return False
+            swapped = True
+        elif n in ("permute", "torch_permute", "transpose_prim"):
+            perm = (b.args[1] if len(b.args) == 2 else b.args[1:]) if len(b.args) > 1 else \
+                b.kwargs.get("permutation", b.kwargs.get("dims"))
+            try:
+                perm = tuple(int(pyval(d)) % 4 for d in perm)
+            except TypeError:
+                return False
+            if swapped or perm != (0, 2, 1, 3):
+                return False
+            swapped = True
+        elif not swapped:
+            return False
+    y = chain[-1].output
+    return swapped and tuple(y.shape) in ((B, T, H * D), (B * T, H * D))
+
+
+def _fuse_fp8_attn_out_casts(trace):
+    """``o, lse = hip_flash_attn_fwd(q, k, v, ...); y = o.transpose(1, 2).reshape(B, T, H D);
+    qy, sy = hip_fp8_cast_delayed(y, False, key, slot)`` -> ``o, lse, qy, sy = hip_flash_attn_fwd_fp8(q, k,
+    v, ..., key, slot)``: the e4m3 input of the FP8 output projection leaves the attention epilogue
+    (O is stored [B, T, H, D], so its rows are the projection's rows); O itself is still written for the
+    backward.  The view chain stays for its other readers."""
+    import os
+
+    from ..core.trace import from_trace, TraceProvenance
+
+    if os.environ.get("LTA_FP8_FUSE_PRODUCERS", "1") == "0":
+        return trace
+    bsyms = trace.bound_symbols
+    producer = {}
+    for i, b in enumerate(bsyms):
+        for o in b.flat_proxy_outs:
+            producer[o.name] = i
+    drop: set[int] = set()
+    replace: dict[int, object] = {}
+    for i, b in enumerate(bsyms):
+        if b.sym is not hip_fp8_cast_delayed or len(b.args) != 4 or b.args[1]:
+            continue
+        y, _, key, slot = b.args
+        chain, cur = [], y
+        j = producer.get(cur.name)
+        while j is not None and bsyms[j].sym.name in _HEAD_MERGE_VIEWS and len(chain) < 4:
+            chain.append(bsyms[j])
+            cur = bsyms[j].args[0]
+            if not isinstance(cur, TensorProxy):
+                break
+            j = producer.get(cur.name)
+        if j is None or j in replace or not chain or bsyms[j].sym is not hip_attn_fwd:
+            continue
+        ab = bsyms[j]
+        out = ab.output[0]
+        if cur.name != out.name or out.dtype != torch.bfloat16 or out.shape[-1] != 128:
+            continue
+        if not _merges_heads(chain[::-1], out):
+            continue
+        nb = hip_attn_fwd_fp8.bind(*ab.args[:5], key, slot, output=(ab.output[0], ab.output[1], b.output[0], b.output[1]))
+        replace[j] = ex.bind_call_ctx(nb)
+        drop.add(i)
+    if not replace:
+        return trace
+    new = from_trace(trace)
+    new.bound_symbols = [replace.get(i, b) for i, b in enumerate(bsyms) if i not in drop]
+    new.scopes = [new.bound_symbols]
+    new.set_provenance(TraceProvenance(f"hipex: {len(replace)} e4m3 attention-output cast(s) fused into the attention epilogue"))
+    return new
+
+
 def _post_claim(trace):
     return _fuse_attn_bwd_rope(_fuse_fp8_qkv_rope_gemm(_fuse_qkv_rope_gemm(_group_decode_projections(_fuse_kv_cache_writes(_fuse_swiglu_gemms(
         _fuse_decode_gemv(_fuse_fp8_rms_bwd_casts(_fuse_rms_bwd_residual(_fuse_linear_epilogues(
-            _fuse_fp8_cast_producers(trace)))))))))))
+            _fuse_fp8_attn_out_casts(_fuse_fp8_cast_producers(trace))))))))))))
 
 
 ex.post_claim_pass = _post_claim

@@ -137,6 +137,8 @@ def _rows_ok(t) -> bool:
 
 
 register_signature("lta_attn_set_rng_state", [c_void_p])
+register_signature("lta_attn_set_fp8_out", [c_void_p, c_void_p, c_float, c_void_p, c_void_p])
+register_signature("lta_attn_fp8_out_used", [])
 
 
 def _graph_rng(lib, dropout_p, seed, offset):
@@ -152,12 +154,30 @@ def _graph_rng(lib, dropout_p, seed, offset):
 
 
 def attn_fwd(q, k, v, causal: bool, scale: float | None = None, out_layout: str = "bshd", mask=None,
-             dropout_p: float = 0.0, seed: int = 0, offset: int = 0):
+             dropout_p: float = 0.0, seed: int = 0, offset: int = 0, fp8_out=None):
     """q [B, Hq, T, D], k/v [B, Hkv, S, D] -> (o [B, Hq, T, D], lse [B, Hq, T] fp32).
 
     ``out_layout="bshd"`` (default) stores O as [B, T, Hq, D] and returns its [B, Hq, T, D]
     transposed view: the usual ``o.transpose(1, 2).reshape(B, T, Hq * D)`` before the output
-    projection is then a view instead of a copy, and the backward reads it (and dO) in place."""
+    projection is then a view instead of a copy, and the backward reads it (and dO) in place.
+
+    ``fp8_out`` = (q8 uint8 [B, T, Hq, D], amax_in, fmax, scale_out, amax_out): ask the kernel for an
+    e4m3 copy of O as well (the FP8 output projection's input, delayed scaling; csrc AttnQ8).  Returns
+    (o, lse, written) then; ``written`` is False when the launched kernel has no such output (the caller
+    casts separately)."""
+    if fp8_out is not None:
+        lib = require()
+        if out_layout != "bshd" or q.shape[-1] != 128 or mask is not None or dropout_p:
+            return attn_fwd(q, k, v, causal, scale, out_layout, mask, dropout_p, seed, offset) + (False,)
+        q8, amax_in, fmax, scale_out, amax_out = fp8_out
+        lib.lta_attn_set_fp8_out(q8.data_ptr(), amax_in.data_ptr(), float(fmax), scale_out.data_ptr(),
+                                 amax_out.data_ptr())
+        try:
+            o, lse = attn_fwd(q, k, v, causal, scale, out_layout)
+        finally:
+            used = bool(lib.lta_attn_fp8_out_used())
+            lib.lta_attn_set_fp8_out(None, None, 0.0, None, None)  # never left armed for another call
+        return o, lse, used
     lib = require()
     D0 = q.shape[-1]
     Dp = padded_head_dim(D0)

@@ -131,6 +131,29 @@ inline const long long* take_attn_rng() {
   return r;
 }
 
+// e4m3 side output of the D = 128 v4 forward (the FP8 output projection's input, delayed scaling):
+// q8 holds fp8(bf16(O) s) in O's element layout (1 byte per element), s = fmax / *amax_in goes to
+// scale_out, max |bf16(O)| into amax_out.  Requested for the NEXT lta_attn_fwd_ex2 call of this host
+// thread (lta_attn_set_fp8_out); lta_attn_fp8_out_used() says whether the launched kernel wrote it.
+struct AttnQ8 {
+  uint8_t* q;
+  const float* amax_in;
+  float fmax;
+  float* scale_out;
+  float* amax_out;
+};
+inline thread_local AttnQ8 g_attn_q8{};
+inline thread_local int g_attn_q8_used = 0;
+inline AttnQ8 take_attn_q8() {
+  const AttnQ8 r = g_attn_q8;
+  g_attn_q8 = AttnQ8{};
+  return r;
+}
+// v4 forward with an optional e4m3 side output (attention_fwd4.hip); -1 when unsupported
+int attn_fwd_v4_q8(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv,
+                   int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
+                   const int64_t* qkv_strides, int defer, const AttnQ8* q8, hipStream_t stream);
+
 // Counter-based dropout mask: a pure function of (seed, offset, query head, query, key), so the
 // forward and both backward kernels regenerate the same keep bit in any iteration order.
 __device__ __forceinline__ unsigned fmix32(unsigned h) {

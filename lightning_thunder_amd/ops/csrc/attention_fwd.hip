@@ -314,6 +314,7 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
                                 const int64_t* o_strides, const void* mask, int mask_b, int mask_h, float dropout_p,
                                 uint64_t seed, uint64_t offset, const int64_t* qkv_strides, hipStream_t stream) {
   const long long* rng = take_attn_rng();
+  const AttnQ8 q8 = take_attn_q8();
   if (Hq % Hkv != 0 || dropout_p < 0.f || dropout_p >= 1.f) return -2;
   AttnExtra ex{};
   ex.sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
@@ -336,9 +337,17 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
     exf |= kExDrop;
   }
   if (D == 128 && exf == 0 && g_fwd_impl >= 9 && Tq > 0 && Sk > 0) {  // v4 (attention_fwd4.hip)
+    const int defer = g_fwd_impl == 9 ? 0 : (g_fwd_impl == 10 ? 1 : 1 | ((g_fwd_impl - 10) << 1));
+    if (q8.q != nullptr) {
+      const int rc = attn_fwd_v4_q8(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides,
+                                    qkv_strides, defer, &q8, stream);
+      if (rc != -1) {
+        g_attn_q8_used = rc == 0;
+        return rc;
+      }
+    }
     const int rc = lta_attn_fwd_v4(dtype, q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, D, scale, causal, o_strides,
-                                   qkv_strides, g_fwd_impl == 9 ? 0 : (g_fwd_impl == 10 ? 1 : 1 | ((g_fwd_impl - 10) << 1)),
-                                   stream);
+                                   qkv_strides, defer, stream);
     if (rc != -1) return rc;
   }
   if (D == 256 && exf == 0 && g_fwd_ring) {  // LDS-DMA ring kernel (attention_fwd_d256.hip)
@@ -363,6 +372,18 @@ LTA_EXPORT int lta_attn_fwd_ex2(int dtype, const void* q, const void* k, const v
 // graph-safe dropout: the device RNG state (int64 [seed, base]) the next lta_attn_fwd_ex2 / lta_attn_bwd_ex3
 // call of this thread reads (its seed / offset arguments then relative to it)
 LTA_EXPORT void lta_attn_set_rng_state(const void* state) { g_attn_rng = (const long long*)state; }
+
+// FP8 side output (AttnQ8, attention.h) for the next lta_attn_fwd_ex2 call of this thread
+LTA_EXPORT void lta_attn_set_fp8_out(void* q, const void* amax_in, float fmax, void* scale_out, void* amax_out) {
+  g_attn_q8 = AttnQ8{(uint8_t*)q, (const float*)amax_in, fmax, (float*)scale_out, (float*)amax_out};
+  g_attn_q8_used = 0;
+}
+// 1 when the last lta_attn_fwd_ex2 call of this thread wrote the requested FP8 side output (then cleared)
+LTA_EXPORT int lta_attn_fp8_out_used() {
+  const int u = g_attn_q8_used;
+  g_attn_q8_used = 0;
+  return u;
+}
 
 LTA_EXPORT int lta_attn_fwd_ex(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
                                int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,

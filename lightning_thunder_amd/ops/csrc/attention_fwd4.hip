@@ -30,7 +30,10 @@
 //    (T13; THR = 0 is the exact online softmax), row sums kept per lane and paired once at the end;
 //  * causal: a wave's tiles end at its diagonal tile (64-row waves on 64-key tiles), so only that
 //    tile is masked; the workgroup keeps staging for its later waves.
+#include <type_traits>
+
 #include "attention.h"
+#include "fp8_cvt.h"
 
 using namespace lta;
 using namespace lta::attn;
@@ -41,6 +44,9 @@ constexpr int kD = 128, kBN = 64, kNW = 4, kRows = 64, kBM = kNW * kRows, kThrea
 constexpr int kTileB = kBN * kD * 2;  // bytes of one K or V tile image (16 KiB)
 constexpr int kNBuf = 4;  // slots: t-1 (V still read), t, and the two tiles in flight
 constexpr int kVBase = kNBuf * kTileB;  // V images follow the K images
+// epilogue staging per wave: 64 bf16 rows of O (256 B) + their e4m3 copies (128 B)
+constexpr int kStageB = 64 * 256 + 64 * 128;
+static_assert(kNW * kStageB <= 2 * kNBuf * kTileB, "epilogue staging fits in the K / V ring");
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -146,12 +152,13 @@ using IC = std::integral_constant<int, N>;
 // ABL (measurement builds only, impl 11..15): 1 no LDS-DMA in the loop, 2 no softmax-finish VALU,
 // 3 no per-tile barrier, 4 no softmax start (results are wrong; timing only), 5 s_memtime stamps of
 // workgroup (0, 0) at every phase boundary of its first 64 tiles, written over LSE (diagnostic)
-template <typename T, bool CAUSAL, int THR, int ABL = 0>
+// Q8: O also leaves as e4m3 into q8.q (same element layout as O; AttnQ8 in attention.h)
+template <typename T, bool CAUSAL, int THR, int ABL = 0, bool Q8 = false>
 __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                                   const T* __restrict__ V, T* __restrict__ O,
                                                                   float* __restrict__ LSE, int Hq, int Hkv, int Tq,
                                                                   int Sk, float c, int64_t so_b, int64_t so_h,
-                                                                  int64_t so_t, QKVStrides sx) {
+                                                                  int64_t so_t, QKVStrides sx, AttnQ8 q8 = {}) {
   using F = typename Frag<T>::type;
   constexpr int kStampBase = 2 * kNBuf * kTileB;
   __shared__ __attribute__((aligned(1024))) char smem[2 * kNBuf * kTileB + (ABL == 5 ? 4 * 64 * 6 * 8 : 0)];  // the only LDS object
@@ -173,6 +180,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5, g = lane >> 4, l16 = lane & 15;
+  [[maybe_unused]] float q8m = 0.f;  // Q8: this lane's max |bf16(O)|
   for (int pass = 0; pass < npass; ++pass) {
   const int qt = pass == 0 ? qt_heavy : qt_light;
   const int q0 = qt * kBM + wave * kRows;  // block X: queries q0 + 32 X + r
@@ -501,6 +509,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
   // ---- epilogue: O = O^T / l ; LSE -----------------------------------------------------------------
+  if constexpr (!Q8) {
 #pragma unroll
   for (int x = 0; x < 2; ++x) {
     const float l = pair_sum(lp[x][0] + lp[x][1]);
@@ -525,8 +534,78 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
     if (h == 0 && LSE != nullptr)
       LSE[((int64_t)b * Hq + hq) * Tq + qi] = (l > 0.f) ? (m[x] + log2f(l)) * 0.69314718055994530942f : -INFINITY;
   }
+  } else {
+  // Q8 (O also as e4m3): a lane holds 4-element pieces of one query row, so direct stores would be 8 B
+  // and 4 B at a row stride (32-64 lines per store instruction, issue-bound: cdna_hip_programming.md
+  // T21; measured +0.6 ms per 7B step for the e4m3 copy).  Each wave stages its 64 rows in LDS instead
+  // (the K / V ring is free now; 16-B chunks XOR-swizzled by row) and stores whole rows with
+  // row-contiguous 16-B stores.  (The same staging for the plain bf16 output measured 1 % slower than
+  // the direct stores above: scripts/attn_epi_ab.py.)
+  [[maybe_unused]] float qs = 0.f;
+  if constexpr (Q8) qs = q8.fmax / fmaxf(*q8.amax_in, 1e-12f);
+  __syncthreads();  // every wave's last K / V reads are done before the ring is overwritten
+  char* const ob = smem + wave * kStageB;
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const float l = pair_sum(lp[x][0] + lp[x][1]);
+    const int row = 32 * x + r, qi = q0 + row;
+    const float inv = (l > 0.f) ? 1.f / l : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        union {
+          T v[4];
+          uint2 u;
+        } pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f32<T>(oacc[x][dt][4 * a + e] * inv);
+        // bytes 64 dt + 16 a + 8 h of the 256-B row: chunk 4 dt + a, half h
+        *reinterpret_cast<uint2*>(ob + row * 256 + (((4 * dt + a) ^ (row & 15)) << 4) + 8 * h) = pk.u;
+        if constexpr (Q8) {
+          float f[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[e] = to_f32(pk.v[e]);  // the bf16 O the unfused cast would read
+            if (qi < Tq) q8m = fmaxf(q8m, fabsf(f[e]));
+          }
+          // bytes 32 dt + 8 a + 4 h of the 128-B e4m3 row: chunk 2 dt + a / 2
+          *reinterpret_cast<uint32_t*>(ob + 64 * 256 + row * 128 + (((2 * dt + (a >> 1)) ^ (row & 7)) << 4) +
+                                       8 * (a & 1) + 4 * h) = cvt4<false>(f[0] * qs, f[1] * qs, f[2] * qs, f[3] * qs);
+        }
+      }
+    }
+    if (h == 0 && LSE != nullptr && qi < Tq)
+      LSE[((int64_t)b * Hq + hq) * Tq + qi] = (l > 0.f) ? (m[x] + log2f(l)) * 0.69314718055994530942f : -INFINITY;
+  }
+  __syncthreads();  // the wave's image is complete (other lanes' writes) before its rows are read back
+  {
+    T* const obase = O + b * so_b + hq * so_h;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {  // 64 rows x 16 chunks of 16 B: 4 rows per instruction
+      const int row = 4 * it + (lane >> 4), c = lane & 15, qi = q0 + row;
+      const uint4 v = *reinterpret_cast<const uint4*>(ob + row * 256 + ((c ^ (row & 15)) << 4));
+      if (qi < Tq) *reinterpret_cast<uint4*>(obase + qi * so_t + 8 * c) = v;
+    }
+    if constexpr (Q8) {
+      uint8_t* const qbase = q8.q + b * so_b + hq * so_h;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {  // 64 rows x 8 chunks: 8 rows per instruction
+        const int row = 8 * it + (lane >> 3), c = lane & 7, qi = q0 + row;
+        const uint4 v = *reinterpret_cast<const uint4*>(ob + 64 * 256 + row * 128 + ((c ^ (row & 7)) << 4));
+        if (qi < Tq) *reinterpret_cast<uint4*>(qbase + qi * so_t + 16 * c) = v;
+      }
+    }
+  }
+  }  // Q8
   __builtin_amdgcn_s_barrier();  // every wave's LDS reads of this pass precede the next pass's DMA
   }  // pass
+  if constexpr (Q8) {
+    // after the last pass's barrier the LDS image is free: its first words take the per-wave maxima
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && q8.scale_out != nullptr)
+      *q8.scale_out = q8.fmax / fmaxf(*q8.amax_in, 1e-12f);
+    if (q8.amax_out != nullptr) fp8_amax_out<kNW>(q8m, q8.amax_out, reinterpret_cast<float*>(smem));
+  }
   if constexpr (ABL == 5) {
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       uint64_t* dst = reinterpret_cast<uint64_t*>(LSE) + wave * 64 * 6;
@@ -538,11 +617,28 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_v4_kernel(const T* __res
 
 template <typename T>
 int launch(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq, int Hkv, int Tq, int Sk,
-           float scale, int causal, const int64_t* so, const QKVStrides& sx, int thr, int abl, hipStream_t s) {
+           float scale, int causal, const int64_t* so, const QKVStrides& sx, int thr, int abl, hipStream_t s,
+           const AttnQ8* q8 = nullptr) {
   const float c = scale * 1.44269504088896340736f;
   const int n_qt = (Tq + kBM - 1) / kBM;
   dim3 grid(B * Hq, causal ? (n_qt + 1) / 2 : n_qt), block(kThreads);
   const int64_t sb = so ? so[0] : (int64_t)Hq * Tq * kD, sh = so ? so[1] : (int64_t)Tq * kD, st = so ? so[2] : kD;
+  if (q8 != nullptr) {
+    // the Q8 epilogue stores whole rows in 16-B pieces (the e4m3 copy: same element offsets)
+    if ((uintptr_t)o % 16 || sb % 16 || sh % 16 || st % 16) return -1;  // e4m3 side output: bf16, deferred rescale (the production configuration) only
+    if constexpr (!std::is_same<T, __hip_bfloat16>::value) {
+      return -1;
+    } else {
+      if (!thr || abl || ((uintptr_t)q8->q % 16)) return -1;
+      if (causal)
+        hipLaunchKernelGGL((attn_fwd_v4_kernel<T, true, 8, 0, true>), grid, block, 0, s, (const T*)q, (const T*)k,
+                           (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st, sx, *q8);
+      else
+        hipLaunchKernelGGL((attn_fwd_v4_kernel<T, false, 8, 0, true>), grid, block, 0, s, (const T*)q, (const T*)k,
+                           (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st, sx, *q8);
+      return (int)hipGetLastError();
+    }
+  }
 #ifdef LTA_V4_ONE
 #define LTA_V4(CA, TH) if (CA && TH) hipLaunchKernelGGL((attn_fwd_v4_kernel<T, true, 8>), grid, block, 0, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, (float*)lse, Hq, Hkv, Tq, Sk, c, sb, sh, st, sx)
 #else
@@ -580,6 +676,16 @@ int launch(const void* q, const void* k, const void* v, void* o, void* lse, int 
 }
 
 }  // namespace
+
+int lta::attn::attn_fwd_v4_q8(int dtype, const void* q, const void* k, const void* v, void* o, void* lse, int B, int Hq,
+                              int Hkv, int Tq, int Sk, int D, float scale, int causal, const int64_t* o_strides,
+                              const int64_t* qkv_strides, int defer, const AttnQ8* q8, hipStream_t stream) {
+  if (D != kD || Hq % Hkv != 0 || Tq <= 0 || Sk <= 0 || dtype != kBF16) return -1;
+  const QKVStrides sx = QKVStrides::from(qkv_strides, Hq, Hkv, Tq, Sk, D);
+  if ((double)Sk * (double)(sx.kt > sx.vt ? sx.kt : sx.vt) * 2.0 >= 4294967295.0) return -1;
+  return launch<__hip_bfloat16>(q, k, v, o, lse, B, Hq, Hkv, Tq, Sk, scale, causal, o_strides, sx, defer & 1, defer >> 1,
+                                stream, q8);
+}
 
 // v4 forward entry: D = 128, no mask / dropout.  qkv_strides as lta_attn_fwd_ex2 (null = dense);
 // rows must be 16-byte aligned and every key-row offset of a head must fit 32 bits.  defer: rescale

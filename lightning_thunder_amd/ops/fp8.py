@@ -667,7 +667,29 @@ def swiglu_bwd_fp8_delayed(g: torch.Tensor, a: torch.Tensor, b: torch.Tensor, ke
     return qa, sa, qb, sb
 
 
-register_signature("lta_rmsnorm_bwd_fp8", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+def attn_fwd_fp8_delayed(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool, scale: float, key: int,
+                         slot: int):
+    """(o, lse, q8 [B*T, Hq*D], scale): the flash-attention forward whose output is also the input of an
+    fp8 output projection: O leaves the kernel a second time as e4m3 quantised in ``slot`` (csrc
+    AttnQ8 epilogue of the v4 kernel; no separate cast re-reading O).  O keeps its [B, T, Hq, D] storage,
+    so the e4m3 rows are the projection input's [B*T, Hq*D] rows."""
+    from .attention import attn_fwd
+
+    B, Hq, T, D = q.shape
+    if not _first_use(key, slot, q.device) and q.dtype == torch.bfloat16:
+        amax_in, fmax, sc, sink = delayed_scaling_source(q, False, key, slot)  # not the first use: q unread
+        q8 = torch.empty((B * T, Hq * D), dtype=torch.uint8, device=q.device)
+        o, lse, used = attn_fwd(q, k, v, causal, scale, fp8_out=(q8, amax_in, fmax, sc, sink))
+        if used:
+            return o, lse, q8, sc
+        qq, s2 = quantize_delayed_rows(o.transpose(1, 2).reshape(B * T, Hq * D), False, key, slot)
+        return o, lse, qq, s2
+    o, lse = attn_fwd(q, k, v, causal, scale)
+    qq, s2 = quantize_delayed_rows(o.transpose(1, 2).reshape(B * T, Hq * D), False, key, slot)
+    return o, lse, qq, s2
+
+
+register_signature("lta_rmsnorm_bwd_fp8",[c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                                            c_void_p, c_void_p])
 

@@ -294,8 +294,43 @@ def test_llama2_7b_shape_fp8_delayed_training_fusions():
         if mode == "fp8":
             fw = str(thunder.last_traces(tm)[-1])
             assert "hip_fp8_gemm_qkv_rope" in fw and "hip_qkv_rope(" not in fw, fw
+            assert "hip_flash_attn_fwd_fp8" in fw, fw  # the o-projection's e4m3 input from the attention epilogue
+            bw = str(thunder.last_backward_traces(tm)[-1])
+            assert "hip_rms_norm_bwd_fp8" in bw, bw  # residual-stream e5m2 gradients from the norm backward
             # 2 layers x 5 linears (qkv, proj, fc_1, fc_2, mlp.proj) + lm head, forwards 2 and 3
             assert fp8.SHADOW_STATS["reused"] - n0 >= 2 * 11, fp8.SHADOW_STATS
         fp8._SHADOWS.clear()
     for a, b in zip(losses["fp8"], losses["bf16"]):
         assert abs(a - b) <= 0.02 * abs(b), losses
+
+
+def test_llama2_7b_shape_fp8_producer_fusions_bit_identical(monkeypatch):
+    """Every FP8 producer fusion of the 7B block (RMSNorm / SwiGLU forwards, the attention epilogue's e4m3
+    output, the SwiGLU and RMSNorm backwards' e5m2 gradients) against the same program with the casts as
+    separate launches: losses and all parameter gradients of two delayed-scaling steps are bit-identical."""
+    from lightning_thunder_amd.transforms.fp8 import FP8LinearTransform
+
+    dev = torch.device("cuda")
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("LTA_FP8_FUSE_PRODUCERS", fuse)
+        torch.manual_seed(0)
+        m = GPT.from_name("llama2-7b-shape-2l").to(device=dev, dtype=torch.bfloat16)
+        init_weights(m)
+        m.set_rope_cache(SEQ, device=dev)
+        V = m.config.padded_vocab_size
+        tm = thunder.jit(m, transforms=[FP8LinearTransform("delayed")])
+        outs = []
+        for step in range(2):
+            g = torch.Generator(device=dev).manual_seed(step)
+            idx = torch.randint(0, V, (1, SEQ), device=dev, generator=g)
+            loss = torch.nn.functional.cross_entropy(tm(idx).reshape(-1, V).float(), torch.roll(idx, -1, 1).reshape(-1))
+            grads = torch.autograd.grad(loss, [p for p in m.parameters() if p.requires_grad])
+            outs.append((loss.detach(),) + tuple(grads))
+        fw = str(thunder.last_traces(tm)[-1])
+        assert ("hip_flash_attn_fwd_fp8" in fw) == (fuse == "1"), fw
+        res[fuse] = outs
+        del tm, m
+    for a, b in zip(res["1"], res["0"]):
+        for u, v in zip(a, b):
+            torch.testing.assert_close(u, v, rtol=0, atol=0)

@@ -681,6 +681,40 @@ def test_fp8_rms_bwd_fused_gradient_cast_matches_unfused(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("causal", [True, False])
+def test_attn_fwd_fp8_side_output_matches_cast(causal):
+    """v4 attention forward with the AttnQ8 epilogue: O is unchanged, and its e4m3 copy (token-major
+    [B*T, H*D] rows), scale and recorded amax equal the separate delayed-scaling row cast of O."""
+    from lightning_thunder_amd.ops import fp8
+    from lightning_thunder_amd.ops.attention import attn_fwd
+
+    torch.manual_seed(0)
+    B, H, Hkv, T, D = 2, 8, 2, 640, 128
+    q = torch.randn(B, H, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    key = fp8.new_delayed_state(fp8.DelayedScaling(amax_history_len=2), 1)
+    try:
+        o_ref, lse_ref = attn_fwd(q, k, v, causal, None)
+        rows = o_ref.transpose(1, 2).reshape(B * T, H * D)
+        fp8.quantize_delayed_rows(rows, False, key, 0)  # first use: records the slot's amax source
+        st = fp8._DELAYED[key]
+        st.cur[0].zero_()
+        q_ref, s_ref = fp8.quantize_delayed_rows(rows, False, key, 0)
+        amax_ref = st.cur[0].clone()
+        st.cur[0].zero_()
+        o, lse, q8, s = fp8.attn_fwd_fp8_delayed(q, k, v, causal, 1.0 / D ** 0.5, key, 0)
+        torch.testing.assert_close(o, o_ref, rtol=0, atol=0)
+        torch.testing.assert_close(lse, lse_ref, rtol=0, atol=0)
+        assert tuple(q8.shape) == (B * T, H * D)
+        torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
+        assert torch.equal(q8, q_ref)
+        assert st.cur[0].item() == amax_ref.item() == rows.float().abs().max().item()
+    finally:
+        fp8.release_delayed_state(key)
+
+
+@pytest.mark.gpu
 def test_rms_norm_bwd_fp8_kernel_matches_cast():
     """lta_rmsnorm_bwd_fp8 (vectorised backward + e5m2 side output) against the plain backward followed
     by the delayed-scaling row cast: dx, dw, the e5m2 bytes and the recorded amax are identical."""
