@@ -47,8 +47,8 @@ def main():
         torch.cuda.synchronize()
         same = torch.equal(outs["new"][1], outs["old"][1]) and torch.equal(outs["new"][2], outs["old"][2])
         ts = {"new": [], "old": []}
-        for _ in range(6):
-            for name in ("new", "old"):
+        for rnd in range(8):
+            for name in (("new", "old") if rnd % 2 == 0 else ("old", "new")):  # alternate the order (clock bias)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(20):
