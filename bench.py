@@ -371,7 +371,7 @@ def main():
             "loss_curve_eager": curve_eager if args.mode == "thunder" else curve,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 
