@@ -205,6 +205,7 @@ def matmul4(a: torch.Tensor, b: torch.Tensor, *, bias=None, residual=None, act=N
         assert residual.shape == (M, N) and residual.stride(1) == 1 and residual.dtype == torch.bfloat16
     if bias is not None:
         assert bias.dtype == torch.bfloat16 and bias.numel() == N and bias.is_contiguous()
+        bias = _aligned_bias(bias)
     plain = bias is None and residual is None and act is None and variant == 1
     # the K split also carries a bias (added in the fixup, forward layout)
     splittable = residual is None and act is None and variant == 1 and (
@@ -429,6 +430,15 @@ def _remember(key, plan) -> None:
     _PLANS[key] = plan or _NO_PLAN
 
 
+def _aligned_bias(bias):
+    """The kernels read the bias with 8- / 16-byte vector loads (gemm4 epilogue, split-K fixup): a
+    bias view at an element offset that is not a multiple of 8 (a slice of a fused qkv bias) is
+    copied to a fresh, aligned buffer (N elements) instead of being read misaligned."""
+    if bias is not None and bias.is_cuda and bias.data_ptr() % 16:
+        return bias.contiguous().clone()
+    return bias
+
+
 def _tkey(t):
     return None if t is None else (t.shape, t.stride(), t.dtype, t.data_ptr() & 15)
 
@@ -474,6 +484,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None)
     the weight-streaming GEMV for <= 8 rows, the 4-wave MFMA GEMM (csrc/gemm4.hip, any M >= 64,
     N % 8, K % 128: edge tiles), the 8-wave kernel (csrc/gemm.hip) when tile-divisible with K % 64,
     else torch (``LTA_GEMM=torch`` forces torch).  Repeated call sites run a cached launch plan."""
+    bias = _aligned_bias(bias)
     key = ("lin", _tkey(x), _tkey(w), _tkey(bias), _tkey(residual), act, x.get_device(),
            _os.environ.get("LTA_GEMM", "auto"))
     plan = _PLANS.get(key)

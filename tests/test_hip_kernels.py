@@ -1493,6 +1493,14 @@ def test_gemm4_splitk(M, N, K, layout):
         outb = matmul4(a, b, bias=bias)
         refb = a.float() @ b.float() + bias.float()
         assert ((outb.float() - refb).norm() / refb.norm()).item() < 5e-3
+        # a bias that is a view at an element offset not a multiple of 8 (a slice of a fused qkv
+        # bias): the fixup's 16-byte bias loads would be misaligned, so it must not take them
+        fused = torch.randn(N + 3, device="cuda", dtype=torch.bfloat16)
+        bview = fused[3:]
+        assert bview.data_ptr() % 16 != 0
+        outv = matmul4(a, b, bias=bview)
+        refv = a.float() @ b.float() + bview.float()
+        assert ((outv.float() - refv).norm() / refv.norm()).item() < 5e-3
 
 
 @pytest.mark.gpu
