@@ -38,6 +38,30 @@ def next_seed_offset(numel: int) -> tuple[int, int]:
         return seed, off
 
 
+def _restart_on_manual_seed():
+    """``torch.manual_seed(s)`` restarts the counter even when ``s`` equals the current seed, so that
+    re-seeding with the same value replays the same dropout masks (as ATen's generators do); the seed
+    comparison in :func:`next_seed_offset` alone only catches a changed seed."""
+    import functools
+
+    orig = torch.manual_seed
+    if getattr(orig, "_lta_restarts_philox", False):
+        return
+
+    @functools.wraps(orig)
+    def manual_seed(seed):
+        with _lock:
+            _state["seed"] = None
+        return orig(seed)
+
+    manual_seed._lta_restarts_philox = True
+    torch.manual_seed = manual_seed
+    torch.random.manual_seed = manual_seed
+
+
+_restart_on_manual_seed()
+
+
 # ---------------------------------------------------------------------------------------------
 # Graph-safe RNG: inside a captured hipGraph the kernels' seed / offset arguments are baked into the
 # graph, so a replay would reuse the capture's dropout masks.  While a HipGraphRunner captures, every
