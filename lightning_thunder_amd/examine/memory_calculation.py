@@ -36,7 +36,7 @@ def _nbytes(p: TensorProxy) -> int:
 def get_alloc_memory(trace, *, timeline: bool = False):
     """Peak bytes of live tensor storage while executing ``trace``.
 
-    Returns ``(peak, live)`` where ``live`` maps the names alive at the end to their storage bytes;
+    Returns ``(peak, live)`` where ``live`` maps one name per storage alive at the end to its bytes;
     with ``timeline=True`` a third element lists ``(bound symbol name, live bytes after it)``.
     """
     storage_of: dict[str, int] = {}   # tensor name -> storage id
@@ -93,7 +93,14 @@ def get_alloc_memory(trace, *, timeline: bool = False):
         peak = max(peak, cur)
         if timeline:
             tl.append((str(b.sym.name), cur))
-    live = {n: size[s] for n, s in storage_of.items()}
+    # one entry per live storage (its first live name): views / aliases of a storage are not counted
+    # again, so ``sum(live.values())`` is the live byte count at the end
+    live, seen = {}, set()
+    for n, s in storage_of.items():
+        if s not in seen:
+            seen.add(s)
+            live[n] = size[s]
+    assert sum(live.values()) == cur
     return (peak, live, tl) if timeline else (peak, live)
 
 
